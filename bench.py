@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Benchmark: sketch updates/sec on MI355X (BASELINE.json metric, config 2).
+
+A step = one pass of the sketch-update hot path over one batch resident in
+HBM: the rank's unordered Zipf (item, user) stream -> the finished
+[n_items][d][w] u32 sketch table (partition by owner, LDS row build with the
+zero fill and sum-of-squares fused, hot-row reduce), followed by
+cms_finalize (RCCL all-reduce of the counters when N > 1, norms).  Weak
+scaling: every rank ingests its own 50M-pair shard of the user-hash-sharded
+stream into the shared 100K-item table.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before libmahout_cms: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "sketch updates/sec + item-pair cosines/sec @1M items, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-items", type=int, default=100_000)
+    ap.add_argument("--n-users", type=int, default=1_000_000)
+    ap.add_argument("--pairs", type=int, default=50_000_000, help="pairs per rank")
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the CSR and cosine side measurements")
+    return ap.parse_args()
+
+
+def rank_stream(args, rank, world, device):
+    """This rank's shard of the user-hash-sharded Zipf stream, on the GPU."""
+    from mahout_amd.sketch import shard_of_keys
+    from mahout_amd.synth import zipf_stream_torch
+    if world == 1:
+        return zipf_stream_torch(args.n_users, args.n_items, args.pairs, seed=20261015, device=device)
+    shard_tbl = torch.from_numpy(shard_of_keys(np.arange(args.n_users, dtype=np.int64), world)).to(device)
+    items_out = torch.empty(args.pairs, dtype=torch.int64, device=device)
+    users_out = torch.empty(args.pairs, dtype=torch.int64, device=device)
+    got, chunk, it = 0, 1 << 25, 0
+    while got < args.pairs:
+        it_, us = zipf_stream_torch(args.n_users, args.n_items, chunk, seed=20261015 + 7919 * it, device=device)
+        keep = shard_tbl[us] == rank
+        it_, us = it_[keep], us[keep]
+        m = min(int(it_.numel()), args.pairs - got)
+        items_out[got:got + m] = it_[:m]
+        users_out[got:got + m] = us[:m]
+        got += m
+        it += 1
+    return items_out, users_out
+
+
+def cpu_baseline(items_d, users_d, args):
+    """Reference cost model timed on the host: per owner, a fresh fp64
+    DoubleCountMinSketch (w*d zero fill) plus d BigInteger-equivalent hashes
+    per update (oracle/cms_oracle.c, 1 core).  Sample: every owner whose
+    item ID is divisible by 5 (with all of its pairs) -- 20% of the owners."""
+    from mahout_amd.synth import to_csr
+    from oracle import oracle as O
+    items = items_d.cpu().numpy()
+    users = users_d.cpu().numpy()
+    sel = items % 5 == 0
+    rows = items[sel] // 5
+    n_rows = (args.n_items + 4) // 5
+    off, keys, _ = to_csr(rows, users[sel], n_rows)
+    a, b = O.hash_params(42, args.depth)
+    t0 = time.perf_counter()
+    upd, _ = O.build_rows_reuse(off, keys, None, 0, n_rows, args.depth, args.width, a, b)
+    dt = time.perf_counter() - t0
+    return {"value": upd / dt, "unit": "updates/s", "cores": 1, "kind": "port",
+            "sample": f"{n_rows} owners (item ID % 5 == 0) = {upd} updates of the rank-0 stream, "
+                      f"{dt:.1f} s, fp64 DoubleCountMinSketch rebuild per owner + 128-bit BigInteger-equivalent hash"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = f"cuda:{local}"
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://")  # control plane only; data path is RCCL in the lib
+
+    from mahout_amd import SketchTable, comm_unique_id
+
+    table = SketchTable(args.n_items, depth=args.depth, width=args.width, seed=42, device=local)
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        table.comm_init(uid[0], rank, world)
+
+    items, users = rank_stream(args, rank, world, device)
+    npairs = int(items.numel())
+    torch.cuda.synchronize()
+
+    def step():
+        table.reset()
+        table.ingest_device_rows(items, users, None, npairs)
+        table.finalize()
+
+    for _ in range(args.warmup):
+        step()
+    table.set_timing(True)
+    table.reset_timing()
+
+    def barrier():
+        table.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_updates = npairs * world * args.steps
+    value = total_updates / elapsed
+
+    breakdown = {}
+    for name in ["partition", "build_plan", "build_rows", "reduce_hot", "norms", "allreduce"]:
+        ms, n = table.timing(name)
+        if n:
+            breakdown[name] = round(ms / args.steps, 4)
+    build_ms, build_n = table.timing("build_rows")
+    n, d, w = args.n_items, args.depth, args.width
+    table_bytes = n * d * w * 4
+    build_alg_bytes = npairs * 8 + (n + 1) * 8 + table_bytes  # CSR keys + offsets read, table written once
+    achieved = build_alg_bytes / (build_ms / build_n * 1e-3) / 1e9 if build_n else None
+    table.set_timing(False)
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "updates/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic Zipf stream (items ~ rank^-1.1, users ~ rank^-0.9), generated on the GPU, resident in HBM",
+        "config": {
+            "workload": f"config 2: Zipf {args.n_users} users x {n} items, {npairs} pairs per rank, d={d} w={w}; "
+                        "unordered COO (item, user) stream -> finished u32 sketch table + norms",
+            "n_items": n, "n_users": args.n_users, "pairs_per_rank": npairs, "depth": d, "width": w,
+            "sharding": "user-hash (splitmix64) across ranks, RCCL all-reduce of u32 counters",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_build_rows",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
+            "traffic": None,
+            "algorithmic_bytes_per_launch": build_alg_bytes,
+            "avg_launch_ms": build_ms / build_n if build_n else None,
+        },
+        "step_roofline": {
+            "algorithmic_bytes": npairs * 16 + table_bytes,
+            "achieved_GBps": (npairs * 16 + table_bytes) / (ms_per_step * 1e-3) / 1e9,
+            "frac": (npairs * 16 + table_bytes) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+        },
+        "breakdown_ms_per_step": breakdown,
+    }
+
+    if rank == 0 and not args.no_extras:
+        extras = {}
+        # CSR (DataModel layout) ingest of the same stream: no partition pass
+        order = torch.argsort(items, stable=True)
+        ckeys = users[order].contiguous()
+        counts = torch.bincount(items, minlength=n)
+        off = torch.zeros(n + 1, dtype=torch.int64, device=device)
+        off[1:] = torch.cumsum(counts, 0)
+        del order
+        table.reset()
+        table.ingest_csr_device(off, ckeys)
+        table.finalize()
+        table.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            table.reset()
+            table.ingest_csr_device(off, ckeys)
+            table.finalize()
+        table.synchronize()
+        dt = time.perf_counter() - t0
+        extras["csr_updates_per_s"] = npairs * args.steps / dt
+        extras["csr_ms_per_step"] = dt * 1e3 / args.steps
+        del ckeys, off
+        # sketch-cosine (v1 pair kernel, exact fp64 epilogue): 8 owners vs all owners
+        q = 8
+        ids = np.arange(n, dtype=np.int64)
+        table.similarities(0, ids)
+        t0 = time.perf_counter()
+        for r in range(q):
+            table.similarities(r, ids)
+        dt = time.perf_counter() - t0
+        extras["pair_kernel_cosines_per_s"] = q * n / dt
+        result["extras"] = extras
+
+    if rank == 0 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(items, users, args)
+    if rank == 0:
+        print(json.dumps(result))
+    table.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

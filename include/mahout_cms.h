@@ -1,0 +1,189 @@
+/*
+ * mahout_cms.h -- C ABI of the MI355X-native count-min-sketch ingest and
+ * sketch-cosine similarity path (libmahout_cms.so, gfx950).
+ *
+ * This is the drop-in boundary for Mahout Taste's CosineCM path.  Every entry
+ * point below names the reference interface it replaces; "T/" abbreviates
+ * mr/src/main/java/org/apache/mahout/cf/taste/ in jalhajj/mahout.
+ *
+ * Vocabulary (reference domain terms):
+ *   owner  -- the entity a sketch belongs to.  CosineCM sketches a Taste
+ *             "user" (T/impl/similarity/CosineCM.java:41-58); over a
+ *             transposed DataModel (FileDataModel transpose=true,
+ *             T/impl/model/file/FileDataModel.java:166,414-418) the owner is an
+ *             item and this path is the sketch-cosine ItemSimilarity.
+ *   key    -- the ID hashed into the sketch (the owner's preference IDs).
+ *   row    -- dense index of an owner in the sorted owner-ID universe.
+ *   depth d / width w -- sketch shape; counters are [d][w] row-major per
+ *             owner (T/impl/common/DoubleCountMinSketch.java:62-64).
+ *
+ * Conventions:
+ *   - every function is extern "C", noexcept, and returns int status
+ *     (CMS_OK = 0) unless stated; the message of the last failure on the
+ *     calling thread is cms_last_error().
+ *   - pointers named h_* / plain are HOST memory, copied during the call and
+ *     never retained; pointers named d_* are DEVICE memory on the handle's GPU.
+ *   - similarity values are the reference's: in [-1, 1] or NaN ("unknown").
+ *     NaN is a value, never an error.
+ *   - the handle serialises ingest/finalize with an internal mutex; queries
+ *     after cms_finalize are reentrant.
+ */
+#ifndef MAHOUT_CMS_H
+#define MAHOUT_CMS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMS_ABI_VERSION 1
+
+/* ---- status codes (mapped to Java exceptions by the JNI shim) ---------- */
+#define CMS_OK 0
+#define CMS_E_PARAM 1      /* IllegalArgumentException / CMException (AbstractCountMinSketch.java:170-175) */
+#define CMS_E_SHAPE 2      /* checkArgument w/d mismatch (DoubleCountMinSketch.java:117-118) */
+#define CMS_E_NO_SUCH_ID 3 /* NoSuchUserException / NoSuchItemException (GenericDataModel.java:210-215) */
+#define CMS_E_STATE 4      /* call-order violation (query before finalize, ...) */
+#define CMS_E_VALUE 5      /* increment not representable in the counter type */
+#define CMS_E_OVERFLOW 6   /* a counter could exceed the counter type */
+#define CMS_E_HIP 7        /* HIP runtime error */
+#define CMS_E_RCCL 8       /* RCCL error */
+#define CMS_E_OOM 9        /* device or host allocation failed */
+
+/* ---- parameters ----------------------------------------------------------- */
+#define CMS_COUNTER_U32 0 /* exact integer counters (non-negative integer increments) */
+
+#define CMS_UNWEIGHTED 0 /* org.apache.mahout.cf.taste.common.Weighting */
+#define CMS_WEIGHTED 1
+
+typedef struct cms_params {
+  uint32_t struct_size; /* = sizeof(cms_params); filled by cms_params_init */
+  int32_t depth;        /* d, 1..32 (AbstractCountMinSketch.java:155-157) */
+  int32_t width;        /* w, 1..2^20 */
+  int32_t counter_type; /* CMS_COUNTER_* */
+  int64_t seed;         /* HashFunctionBuilder(long seed) (HashFunctionBuilder.java:59) */
+  int64_t num_owners;   /* n: rows of the sketch table */
+  int32_t weighting;    /* CMS_UNWEIGHTED | CMS_WEIGHTED (CosineCM.java:33) */
+  int32_t device;       /* HIP device ordinal; -1 = current device */
+} cms_params;
+
+typedef struct cms_handle cms_handle;
+
+/* Defaults: d=5, w=4096, u32, seed=42, n=0, unweighted, device -1. */
+int cms_params_init(cms_params* p);
+
+/* AbstractCountMinSketch(double delta, double epsilon, ...) shape rule
+ * (T/impl/common/AbstractCountMinSketch.java:168-182): w = ceil(e/eps),
+ * d = ceil(ln(1/delta)); CMS_E_PARAM for the CMException ranges. */
+int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, int32_t* depth);
+
+/* new DoubleCountMinSketch(width, depth, hfBuilder) for every owner at once
+ * (T/impl/common/DoubleCountMinSketch.java:32-42) plus the CosineCM instance
+ * state (CosineCM.java:26-39).  Counters start at zero. */
+int cms_create(const cms_params* p, cms_handle** out);
+void cms_destroy(cms_handle* h);
+const char* cms_last_error(void);
+int cms_abi_version(void);
+
+/* Owner-ID universe: strictly ascending IDs, row i <-> ids[i] (the order of
+ * DataModel.getUserIDs(), GenericDataModel.java:128-134).  Without this call
+ * owner IDs are the row indices 0..n-1. */
+int cms_set_owner_ids(cms_handle* h, const int64_t* ids, int64_t n);
+
+/* The d hash parameters (a_i, b_i) of HashFunctionBuilder(seed)
+ * (HashFunctionBuilder.java:76-97). */
+int cms_hash_params(cms_handle* h, int64_t* a, int64_t* b);
+
+/* HashFunction.hash(key) for every row i < d, computed on the GPU
+ * (HashFunction.java:31-34): out[k*d + i] = h_i(keys[k]). */
+int cms_hash_keys(cms_handle* h, const int64_t* keys, int64_t n, int32_t* out);
+
+/* ---- ingest: DoubleCountMinSketch.update(key, inc) for many owners --------
+ * (DoubleCountMinSketch.java:72-80; CosineCM.exportProfile :41-58 feeds it the
+ * owner's PreferenceArray).  val may be NULL (every increment 1.0, the
+ * implicit-feedback stream).  With CMS_COUNTER_U32 every val must be a
+ * non-negative integer (CMS_E_VALUE otherwise).  Duplicate (owner, key) pairs
+ * ADD, as repeated update() calls do. */
+
+/* COO pairs from host memory, owners by ID. */
+int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t n);
+/* COO pairs already resident on the device, owners by row index. Asynchronous
+ * on the handle's stream (use cms_synchronize). */
+int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val,
+                           int64_t n);
+/* CSR from host memory: the owner at row r has keys[offsets[r] .. offsets[r+1])
+ * -- the DataModel layout (one PreferenceArray per owner,
+ * GenericUserPreferenceArray.java:52-54).  offsets has num_owners+1 entries. */
+int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, const float* vals);
+/* CSR resident on the device. Asynchronous. */
+int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t* d_keys, const float* d_vals);
+
+/* Forget all counters (next ingest rebuilds the table from zero). */
+int cms_reset(cms_handle* h);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------
+ * The interaction stream is sharded by key (user) hash; each rank ingests its
+ * shard into a full-shape partial table and cms_finalize sums the tables with
+ * RCCL.  Counters are integers, so the merged table is bit-identical for any
+ * rank count. */
+int cms_comm_unique_id(void* out /* 128 bytes, ncclUniqueId */);
+int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t world);
+/* The sharding function: rank that owns `key` among `world` ranks. */
+int32_t cms_shard_of_key(int64_t key, int32_t world);
+
+/* Merge (RCCL all-reduce when a communicator is attached), then derive the
+ * per-(owner,row) norms the cosine needs.  Queries require it. */
+int cms_finalize(cms_handle* h);
+int cms_synchronize(cms_handle* h);
+
+/* ---- queries (after cms_finalize) ---------------------------------------- */
+
+/* CosineCM.userSimilarity(id1, id2) (CosineCM.java:83-96): min over the d rows
+ * of the per-row cosine (DoubleCountMinSketch.cosine :114-149), then
+ * normalizeWeightResult(r, 1, 0) (AbstractSimilarity.java:313-330).
+ * CMS_E_NO_SUCH_ID for unknown owners. */
+int cms_similarity(cms_handle* h, int64_t id1, int64_t id2, double* out);
+/* ItemSimilarity.itemSimilarities(id1, ids2[]) (ItemSimilarity.java:58) as
+ * one batched GPU call. */
+int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n, double* out);
+/* DoubleCountMinSketch.get(key) of owner `id` (DoubleCountMinSketch.java:94-103),
+ * the point query GenericUserBasedRecommender uses (:153-158). */
+int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out);
+/* GenericUserBasedRecommender.mostSimilarUserIDs(id, k) with the CosineCM
+ * estimator (:119-127, :231-247) and TopItems.getTopUsers (TopItems.java:91-136):
+ * the first k other owners under (similarity desc, ID asc), NaN excluded.
+ * Writes *count <= k entries; scores are the fp64 similarities. */
+int cms_most_similar(cms_handle* h, int64_t id, int32_t k, int64_t* out_ids, double* out_scores, int32_t* count);
+/* mostSimilar for every owner in rows [row_begin, row_begin+row_count): the
+ * all-pairs top-k pass (config 4).  ids/scores are [row_count][k]; counts[row_count]. */
+int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* ids,
+                   double* scores, int32_t* counts);
+
+/* Counters of rows [row_begin, row_begin+row_count) as fp64 (the reference's
+ * counter type), [row_count][d][w]. */
+int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out);
+
+/* ---- instrumentation ------------------------------------------------------- */
+typedef struct cms_stats {
+  int64_t pairs_ingested;   /* update() calls applied on this rank */
+  int64_t num_owners;
+  int32_t depth, width;
+  int32_t exact_norms;      /* 1 if every (owner,row) norm is < 2^53 (bit-exact fast path) */
+  int32_t world, rank;
+  int64_t table_bytes;
+} cms_stats;
+int cms_get_stats(cms_handle* h, cms_stats* out);
+
+/* Per-kernel HIP-event timing on the handle's stream (off by default). */
+int cms_set_timing(cms_handle* h, int32_t enabled);
+/* Accumulated (total ms, launches) for a kernel family name, e.g.
+ * "build_rows", "partition", "norms", "allreduce", "cosine". */
+int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* launches);
+int cms_reset_timing(cms_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAHOUT_CMS_H */

@@ -1,0 +1,142 @@
+"""ctypes binding of libmahout_cms.so (include/mahout_cms.h).
+
+The product path has exactly one implementation: the gfx950 HIP library.  If
+the in-tree shared object is missing this module raises -- there is no CPU
+fallback.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(HERE, "libmahout_cms.so")
+
+# status codes (include/mahout_cms.h)
+CMS_OK = 0
+CMS_E_PARAM = 1
+CMS_E_SHAPE = 2
+CMS_E_NO_SUCH_ID = 3
+CMS_E_STATE = 4
+CMS_E_VALUE = 5
+CMS_E_OVERFLOW = 6
+CMS_E_HIP = 7
+CMS_E_RCCL = 8
+CMS_E_OOM = 9
+
+CMS_COUNTER_U32 = 0
+CMS_UNWEIGHTED = 0
+CMS_WEIGHTED = 1
+
+# Every symbol the header declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "cms_params_init", "cms_shape_from_delta_epsilon", "cms_create", "cms_destroy", "cms_last_error",
+    "cms_abi_version", "cms_set_owner_ids", "cms_hash_params", "cms_hash_keys", "cms_ingest",
+    "cms_ingest_device_rows", "cms_ingest_csr", "cms_ingest_csr_device", "cms_reset", "cms_comm_unique_id",
+    "cms_comm_init", "cms_shard_of_key", "cms_finalize", "cms_synchronize", "cms_similarity", "cms_similarities",
+    "cms_point_query", "cms_most_similar", "cms_top_k_rows", "cms_read_counters", "cms_get_stats",
+    "cms_set_timing", "cms_get_timing", "cms_reset_timing",
+]
+
+
+class CmsParams(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_uint32),
+        ("depth", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("counter_type", ctypes.c_int32),
+        ("seed", ctypes.c_int64),
+        ("num_owners", ctypes.c_int64),
+        ("weighting", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+    ]
+
+
+class CmsStats(ctypes.Structure):
+    _fields_ = [
+        ("pairs_ingested", ctypes.c_int64),
+        ("num_owners", ctypes.c_int64),
+        ("depth", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("exact_norms", ctypes.c_int32),
+        ("world", ctypes.c_int32),
+        ("rank", ctypes.c_int32),
+        ("table_bytes", ctypes.c_int64),
+    ]
+
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_int = ctypes.c_int
+_dbl = ctypes.c_double
+
+_SIGS = {
+    "cms_params_init": (_int, [ctypes.POINTER(CmsParams)]),
+    "cms_shape_from_delta_epsilon": (_int, [_dbl, _dbl, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "cms_create": (_int, [ctypes.POINTER(CmsParams), ctypes.POINTER(_vp)]),
+    "cms_destroy": (None, [_vp]),
+    "cms_last_error": (ctypes.c_char_p, []),
+    "cms_abi_version": (_int, []),
+    "cms_set_owner_ids": (_int, [_vp, _vp, _i64]),
+    "cms_hash_params": (_int, [_vp, _vp, _vp]),
+    "cms_hash_keys": (_int, [_vp, _vp, _i64, _vp]),
+    "cms_ingest": (_int, [_vp, _vp, _vp, _vp, _i64]),
+    "cms_ingest_device_rows": (_int, [_vp, _vp, _vp, _vp, _i64]),
+    "cms_ingest_csr": (_int, [_vp, _vp, _vp, _vp]),
+    "cms_ingest_csr_device": (_int, [_vp, _vp, _vp, _vp]),
+    "cms_reset": (_int, [_vp]),
+    "cms_comm_unique_id": (_int, [_vp]),
+    "cms_comm_init": (_int, [_vp, _vp, _i32, _i32]),
+    "cms_shard_of_key": (_i32, [_i64, _i32]),
+    "cms_finalize": (_int, [_vp]),
+    "cms_synchronize": (_int, [_vp]),
+    "cms_similarity": (_int, [_vp, _i64, _i64, ctypes.POINTER(_dbl)]),
+    "cms_similarities": (_int, [_vp, _i64, _vp, _i64, _vp]),
+    "cms_point_query": (_int, [_vp, _i64, _i64, ctypes.POINTER(_dbl)]),
+    "cms_most_similar": (_int, [_vp, _i64, _i32, _vp, _vp, ctypes.POINTER(_i32)]),
+    "cms_top_k_rows": (_int, [_vp, _i64, _i64, _i32, _vp, _vp, _vp]),
+    "cms_read_counters": (_int, [_vp, _i64, _i64, _vp]),
+    "cms_get_stats": (_int, [_vp, ctypes.POINTER(CmsStats)]),
+    "cms_set_timing": (_int, [_vp, _i32]),
+    "cms_get_timing": (_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_dbl), ctypes.POINTER(_i64)]),
+    "cms_reset_timing": (_int, [_vp]),
+}
+
+_lib = None
+
+
+def load():
+    """Load the in-tree gfx950 library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(SO_PATH):
+        raise RuntimeError(
+            f"{SO_PATH} is missing: build it with `python -m mahout_amd.build_lib` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    # torch (device-memory/stream plumbing for callers) ships its own
+    # libamdhip64/librccl with the same SONAMEs; loading it first makes this
+    # library bind to that one runtime instead of a second copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(SO_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class CmsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def check(rc):
+    if rc != CMS_OK:
+        msg = load().cms_last_error()
+        raise CmsError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,30 @@
+"""Builds libmahout_cms.so in-tree with hipcc for gfx950 (no JIT cache: the
+.so travels with the repo snapshot to the GPU box)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libmahout_cms.so")
+SOURCES = ["cms_api.hip", "cms_ingest.hip", "cms_query.hip", "cms_cosine_mfma.hip"]
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
+         "-mcode-object-version=5", "-Wall", "-Wno-unused-function", "-I/opt/rocm/include"]
+
+
+def build(verbose=False, force=False):
+    srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(HERE, "..", "include", "mahout_cms.h"))
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+        return OUT
+    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + srcs + ["-o", OUT, "-L/opt/rocm/lib", "-lrccl",
+                                                   "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

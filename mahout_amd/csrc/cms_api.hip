@@ -1,0 +1,587 @@
+// cms_api.hip -- extern "C" entry points of libmahout_cms.so (see
+// include/mahout_cms.h for the reference interface each one replaces).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "cms_internal.h"
+
+namespace cms {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  if (e == hipErrorOutOfMemory) return set_error(CMS_E_OOM, "out of device memory in %s", what);
+  return set_error(CMS_E_HIP, "%s failed: %s", what, hipGetErrorString(e));
+}
+
+hipError_t DevBuf::ensure(size_t need) {
+  if (need <= bytes && ptr) return hipSuccess;
+  if (ptr) {
+    hipError_t e = hipFree(ptr);
+    if (e != hipSuccess) return e;
+    ptr = nullptr;
+    bytes = 0;
+  }
+  size_t alloc = std::max<size_t>(need, 256);
+  hipError_t e = hipMalloc(&ptr, alloc);
+  if (e == hipSuccess) bytes = alloc;
+  return e;
+}
+
+void DevBuf::release() {
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  bytes = 0;
+}
+
+TimedScope::TimedScope(cms_handle* hh, const char* nm) : h(hh), name(nm) {
+  if (h->timing) {
+    if (hipEventCreate(&start) == hipSuccess) (void)hipEventRecord(start, h->stream);
+    else start = nullptr;
+  }
+}
+
+TimedScope::~TimedScope() {
+  if (!h->timing || !start) return;
+  hipEvent_t stop;
+  if (hipEventCreate(&stop) != hipSuccess) return;
+  (void)hipEventRecord(stop, h->stream);
+  h->pending.push_back(PendingEvent{name, start, stop});
+}
+
+// java.util.Random restated for HashFunctionBuilder (HashFunctionBuilder.java:59-97):
+// (a_i, b_i) = (Math.abs(nextLong()), Math.abs(nextLong())) for i = 0..d-1.
+static void java_hash_params(int64_t seed, int depth, int64_t* a, int64_t* b) {
+  const uint64_t mult = 0x5DEECE66DULL, add = 0xBULL, mask = (1ULL << 48) - 1;
+  uint64_t s = ((uint64_t)seed ^ mult) & mask;
+  auto next32 = [&]() -> int64_t {
+    s = (s * mult + add) & mask;
+    return (int64_t)(int32_t)(uint32_t)(s >> 16);
+  };
+  auto next_long = [&]() -> int64_t {
+    int64_t hi = next32();
+    int64_t lo = next32();
+    return (int64_t)((uint64_t)hi << 32) + lo;
+  };
+  auto jabs = [](int64_t v) -> int64_t { return v < 0 ? (int64_t)(0 - (uint64_t)v) : v; };
+  for (int i = 0; i < depth; ++i) {
+    a[i] = jabs(next_long());
+    b[i] = jabs(next_long());
+  }
+}
+
+static int check_flags(cms_handle* h, bool by_id) {
+  uint32_t f = 0;
+  CMS_HIP(hipMemcpy(&f, h->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (f == 0) return CMS_OK;
+  CMS_HIP(hipMemset(h->d_flags, 0, sizeof(uint32_t)));
+  if (f & kFlagBadRow)
+    return by_id ? set_error(CMS_E_NO_SUCH_ID, "owner ID not in the owner universe")
+                 : set_error(CMS_E_PARAM, "owner row outside [0, num_owners)");
+  if (f & kFlagBadValue) return set_error(CMS_E_VALUE, "u32 counters need non-negative integer increments");
+  return set_error(CMS_E_OVERFLOW, "a row's total increment reached 2^32 (u32 counters)");
+}
+
+static int resolve_timing(cms_handle* h) {
+  for (auto& pe : h->pending) {
+    float ms = 0.f;
+    CMS_HIP(hipEventSynchronize(pe.stop));
+    CMS_HIP(hipEventElapsedTime(&ms, pe.start, pe.stop));
+    auto& acc = h->timing_acc[pe.name];
+    acc.total_ms += ms;
+    acc.launches += 1;
+    (void)hipEventDestroy(pe.start);
+    (void)hipEventDestroy(pe.stop);
+  }
+  h->pending.clear();
+  return CMS_OK;
+}
+
+static int row_of(cms_handle* h, int64_t id, int64_t* row) {
+  if (h->h_owner_ids.empty()) {
+    if (id < 0 || id >= h->n) return set_error(CMS_E_NO_SUCH_ID, "no such owner ID %lld", (long long)id);
+    *row = id;
+    return CMS_OK;
+  }
+  auto it = std::lower_bound(h->h_owner_ids.begin(), h->h_owner_ids.end(), id);
+  if (it == h->h_owner_ids.end() || *it != id) return set_error(CMS_E_NO_SUCH_ID, "no such owner ID %lld", (long long)id);
+  *row = it - h->h_owner_ids.begin();
+  return CMS_OK;
+}
+
+struct Guard {
+  cms_handle* h;
+  explicit Guard(cms_handle* hh) : h(hh) {
+    h->mu.lock();
+    (void)hipSetDevice(h->device);
+  }
+  ~Guard() { h->mu.unlock(); }
+};
+
+static int require_finalized(cms_handle* h) {
+  if (!h->finalized) return set_error(CMS_E_STATE, "call cms_finalize before queries");
+  return CMS_OK;
+}
+
+}  // namespace cms
+
+using namespace cms;
+
+extern "C" {
+
+int cms_abi_version(void) { return CMS_ABI_VERSION; }
+
+const char* cms_last_error(void) { return g_err; }
+
+int cms_params_init(cms_params* p) {
+  if (!p) return set_error(CMS_E_PARAM, "null params");
+  std::memset(p, 0, sizeof(*p));
+  p->struct_size = sizeof(cms_params);
+  p->depth = 5;
+  p->width = 4096;
+  p->counter_type = CMS_COUNTER_U32;
+  p->seed = 42;
+  p->num_owners = 0;
+  p->weighting = CMS_UNWEIGHTED;
+  p->device = -1;
+  return CMS_OK;
+}
+
+int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, int32_t* depth) {
+  if (!width || !depth) return set_error(CMS_E_PARAM, "null output");
+  if (delta <= 0 || delta > std::exp(-1.0))
+    return set_error(CMS_E_PARAM, "CountMinSketch: delta must be between 0 and 1, exclusive");
+  if (epsilon <= 0 || epsilon > std::exp(1.0))
+    return set_error(CMS_E_PARAM, "CountMinSketch: epsilon must be between 0 and 1, exclusive");
+  *width = (int32_t)std::ceil(std::exp(1.0) / epsilon);
+  *depth = (int32_t)std::ceil(std::log(1.0 / delta));
+  return CMS_OK;
+}
+
+int cms_create(const cms_params* p, cms_handle** out) {
+  if (!p || !out) return set_error(CMS_E_PARAM, "null argument");
+  if (p->struct_size != sizeof(cms_params)) return set_error(CMS_E_PARAM, "cms_params ABI mismatch");
+  if (p->depth < 1 || p->depth > CMS_MAX_DEPTH) return set_error(CMS_E_PARAM, "depth must be in [1, %d]", CMS_MAX_DEPTH);
+  if (p->width < 1 || p->width > (1 << 15))
+    return set_error(CMS_E_PARAM, "width must be in [1, 32768] (LDS-staged sketch rows)");
+  if (p->num_owners < 1 || p->num_owners > (int64_t(1) << 24))
+    return set_error(CMS_E_PARAM, "num_owners must be in [1, 2^24]");
+  if (p->counter_type != CMS_COUNTER_U32) return set_error(CMS_E_PARAM, "unsupported counter type");
+  cms_handle* h = new (std::nothrow) cms_handle();
+  if (!h) return set_error(CMS_E_OOM, "host allocation failed");
+  h->p = *p;
+  int dev = p->device;
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  h->device = dev;
+  hipError_t e = hipSetDevice(dev);
+  if (e != hipSuccess) {
+    delete h;
+    return hip_fail(e, "hipSetDevice");
+  }
+  h->n = p->num_owners;
+  h->dw = (int64_t)p->depth * p->width;
+  java_hash_params(p->seed, p->depth, h->a, h->b);
+  HashParams& hp = h->hp;
+  std::memset(&hp, 0, sizeof(hp));
+  for (int i = 0; i < p->depth; ++i) {
+    hp.ap[i] = reduce_key(h->a[i]);
+    hp.bp[i] = reduce_key(h->b[i]);
+  }
+  hp.width = (uint32_t)p->width;
+  hp.depth = p->depth;
+  hp.pow2 = (p->width & (p->width - 1)) == 0;
+  hp.wmask = hp.pow2 ? (uint32_t)(p->width - 1) : 0u;
+  hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)p->width;
+
+  size_t tbytes = sizeof(uint32_t) * (size_t)h->n * (size_t)h->dw;
+  if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipMalloc(&h->d_table, tbytes)) != hipSuccess ||
+      (e = hipMalloc(&h->d_row_mass, sizeof(uint64_t) * h->n)) != hipSuccess ||
+      (e = hipMalloc(&h->d_norm, sizeof(uint64_t) * h->n * p->depth)) != hipSuccess ||
+      (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess ||
+      (e = hipMalloc(&h->d_flags, 64 * sizeof(uint32_t))) != hipSuccess ||
+      (e = hipMemset(h->d_flags, 0, 64 * sizeof(uint32_t))) != hipSuccess ||
+      (e = hipMemset(h->d_row_mass, 0, sizeof(uint64_t) * h->n)) != hipSuccess) {
+    int rc = hip_fail(e, "cms_create allocation");
+    cms_destroy(h);
+    return rc;
+  }
+  h->empty = true;
+  h->norms_valid = false;
+  *out = h;
+  return CMS_OK;
+}
+
+void cms_destroy(cms_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (auto& pe : h->pending) {
+    (void)hipEventDestroy(pe.start);
+    (void)hipEventDestroy(pe.stop);
+  }
+  if (h->comm) (void)ncclCommDestroy(h->comm);
+  void* bufs[] = {h->d_table, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_flags, h->d_owner_ids};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
+                  &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
+                  &h->ws_hot, &h->ws_query, &h->ws_out};
+  for (DevBuf* b : ws) b->release();
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int cms_set_owner_ids(cms_handle* h, const int64_t* ids, int64_t n) {
+  if (!h || !ids) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  if (n != h->n) return set_error(CMS_E_PARAM, "expected %lld owner IDs, got %lld", (long long)h->n, (long long)n);
+  for (int64_t i = 1; i < n; ++i)
+    if (ids[i] <= ids[i - 1]) return set_error(CMS_E_PARAM, "owner IDs must be strictly ascending");
+  h->h_owner_ids.assign(ids, ids + n);
+  if (!h->d_owner_ids) CMS_HIP(hipMalloc(&h->d_owner_ids, sizeof(int64_t) * n));
+  CMS_HIP(hipMemcpy(h->d_owner_ids, ids, sizeof(int64_t) * n, hipMemcpyHostToDevice));
+  return CMS_OK;
+}
+
+int cms_hash_params(cms_handle* h, int64_t* a, int64_t* b) {
+  if (!h || !a || !b) return set_error(CMS_E_PARAM, "null argument");
+  for (int i = 0; i < h->p.depth; ++i) {
+    a[i] = h->a[i];
+    b[i] = h->b[i];
+  }
+  return CMS_OK;
+}
+
+int cms_hash_keys(cms_handle* h, const int64_t* keys, int64_t n, int32_t* out) {
+  if (!h || (n > 0 && (!keys || !out))) return set_error(CMS_E_PARAM, "null argument");
+  if (n <= 0) return CMS_OK;
+  Guard g(h);
+  CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * n));
+  CMS_HIP(h->ws_out.ensure(sizeof(int32_t) * n * h->p.depth));
+  CMS_HIP(hipMemcpyAsync(h->ws_in_key.ptr, keys, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+  int rc = hash_keys_device(h, h->ws_in_key.as<int64_t>(), n, h->ws_out.as<int32_t>());
+  if (rc) return rc;
+  CMS_HIP(hipMemcpyAsync(out, h->ws_out.ptr, sizeof(int32_t) * n * h->p.depth, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
+int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t n) {
+  if (!h || (n > 0 && (!owner || !key))) return set_error(CMS_E_PARAM, "null argument");
+  if (n <= 0) return CMS_OK;
+  Guard g(h);
+  CMS_HIP(h->ws_in_row.ensure(sizeof(int64_t) * n));
+  CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * n));
+  if (val) CMS_HIP(h->ws_in_val.ensure(sizeof(float) * n));
+  int64_t* d_row = h->ws_in_row.as<int64_t>();
+  CMS_HIP(hipMemcpyAsync(d_row, owner, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipMemcpyAsync(h->ws_in_key.ptr, key, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+  if (val) CMS_HIP(hipMemcpyAsync(h->ws_in_val.ptr, val, sizeof(float) * n, hipMemcpyHostToDevice, h->stream));
+  const bool by_id = !h->h_owner_ids.empty();
+  if (by_id) {
+    int rc = map_owner_ids(h, d_row, n, d_row);  // in place: each thread reads then writes its own slot
+    if (rc) return rc;
+  }
+  int rc = ingest_coo_device(h, d_row, h->ws_in_key.as<int64_t>(), val ? h->ws_in_val.as<float>() : nullptr, n);
+  if (rc) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  h->finalized = false;
+  rc = check_flags(h, by_id);
+  if (rc == CMS_OK) h->pairs_ingested += n;
+  return rc;
+}
+
+int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n) {
+  if (!h || (n > 0 && (!d_row || !d_key))) return set_error(CMS_E_PARAM, "null argument");
+  if (n <= 0) return CMS_OK;
+  Guard g(h);
+  int rc = ingest_coo_device(h, d_row, d_key, d_val, n);
+  if (rc == CMS_OK) {
+    h->pairs_ingested += n;
+    h->finalized = false;
+  }
+  return rc;
+}
+
+int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, const float* vals) {
+  if (!h || !offsets) return set_error(CMS_E_PARAM, "null argument");
+  const int64_t n = h->n;
+  if (offsets[0] != 0) return set_error(CMS_E_PARAM, "offsets[0] must be 0");
+  for (int64_t r = 0; r < n; ++r)
+    if (offsets[r + 1] < offsets[r]) return set_error(CMS_E_PARAM, "offsets must be non-decreasing");
+  const int64_t np = offsets[n];
+  if (np > 0 && !keys) return set_error(CMS_E_PARAM, "null keys");
+  Guard g(h);
+  CMS_HIP(h->ws_in_row.ensure(sizeof(int64_t) * (n + 1)));
+  CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * std::max<int64_t>(np, 1)));
+  if (vals) CMS_HIP(h->ws_in_val.ensure(sizeof(float) * std::max<int64_t>(np, 1)));
+  CMS_HIP(hipMemcpyAsync(h->ws_in_row.ptr, offsets, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+  if (np > 0)
+    CMS_HIP(hipMemcpyAsync(h->ws_in_key.ptr, keys, sizeof(int64_t) * np, hipMemcpyHostToDevice, h->stream));
+  if (vals && np > 0)
+    CMS_HIP(hipMemcpyAsync(h->ws_in_val.ptr, vals, sizeof(float) * np, hipMemcpyHostToDevice, h->stream));
+  int rc = ingest_csr_device(h, h->ws_in_row.as<int64_t>(), h->ws_in_key.as<int64_t>(),
+                             vals ? h->ws_in_val.as<float>() : nullptr, np);
+  if (rc) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  h->finalized = false;
+  rc = check_flags(h, false);
+  if (rc == CMS_OK) h->pairs_ingested += np;
+  return rc;
+}
+
+int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t* d_keys, const float* d_vals) {
+  if (!h || !d_offsets) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int64_t np = 0;
+  CMS_HIP(hipMemcpyAsync(&np, d_offsets + h->n, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  int rc = ingest_csr_device(h, d_offsets, d_keys, d_vals, np);
+  if (rc == CMS_OK) {
+    h->pairs_ingested += np;
+    h->finalized = false;
+  }
+  return rc;
+}
+
+int cms_reset(cms_handle* h) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  Guard g(h);
+  CMS_HIP(hipMemsetAsync(h->d_row_mass, 0, sizeof(uint64_t) * h->n, h->stream));
+  h->empty = true;
+  h->norms_valid = false;
+  h->finalized = false;
+  h->pairs_ingested = 0;
+  return CMS_OK;
+}
+
+int cms_comm_unique_id(void* out) {
+  if (!out) return set_error(CMS_E_PARAM, "null argument");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(out, &id, sizeof(id));
+  return CMS_OK;
+}
+
+int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t world) {
+  if (!h || !unique_id) return set_error(CMS_E_PARAM, "null argument");
+  if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
+  Guard g(h);
+  if (h->comm) {
+    (void)ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+  }
+  h->rank = rank;
+  h->world = world;
+  if (world == 1) return CMS_OK;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof(id));
+  ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
+  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  return CMS_OK;
+}
+
+// splitmix64 finalizer of the key, modulo world.
+int32_t cms_shard_of_key(int64_t key, int32_t world) {
+  if (world <= 1) return 0;
+  uint64_t z = (uint64_t)key + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return (int32_t)(z % (uint64_t)world);
+}
+
+int cms_finalize(cms_handle* h) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  Guard g(h);
+  if (h->empty) {
+    CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * h->n * h->dw, h->stream));
+    h->empty = false;
+    h->norms_valid = false;
+  }
+  if (h->comm && h->world > 1) {
+    TimedScope ts(h, "allreduce");
+    ncclResult_t r = ncclAllReduce(h->d_table, h->d_table, (size_t)(h->n * h->dw), ncclUint32, ncclSum, h->comm,
+                                   h->stream);
+    if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce(table): %s", ncclGetErrorString(r));
+    r = ncclAllReduce(h->d_row_mass, h->d_row_mass, (size_t)h->n, ncclUint64, ncclSum, h->comm, h->stream);
+    if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce(mass): %s", ncclGetErrorString(r));
+    h->norms_valid = false;
+  }
+  int rc = compute_norms(h);
+  if (rc) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  rc = check_flags(h, false);
+  if (rc) return rc;
+  uint32_t inexact = 0;
+  CMS_HIP(hipMemcpy(&inexact, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  h->exact_norms = inexact == 0;
+  h->finalized = true;
+  return CMS_OK;
+}
+
+int cms_synchronize(cms_handle* h) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  Guard g(h);
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return check_flags(h, false);
+}
+
+int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n, double* out) {
+  if (!h || (n > 0 && (!ids2 || !out))) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  int64_t q;
+  if ((rc = row_of(h, id1, &q))) return rc;
+  if (n <= 0) return CMS_OK;
+  std::vector<int64_t> rows(n);
+  for (int64_t i = 0; i < n; ++i)
+    if ((rc = row_of(h, ids2[i], &rows[i]))) return rc;
+  CMS_HIP(h->ws_query.ensure(sizeof(int64_t) * n));
+  CMS_HIP(h->ws_small.ensure(sizeof(double) * n));
+  CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, rows.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+  if ((rc = pair_cosines(h, q, h->ws_query.as<int64_t>(), n, h->ws_small.as<double>()))) return rc;
+  CMS_HIP(hipMemcpyAsync(out, h->ws_small.ptr, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
+int cms_similarity(cms_handle* h, int64_t id1, int64_t id2, double* out) {
+  return cms_similarities(h, id1, &id2, 1, out);
+}
+
+int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out) {
+  if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  int64_t row;
+  if ((rc = row_of(h, id, &row))) return rc;
+  CMS_HIP(h->ws_query.ensure(sizeof(int64_t)));
+  CMS_HIP(h->ws_small.ensure(sizeof(double)));
+  CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, &key, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+  if ((rc = point_queries(h, row, h->ws_query.as<int64_t>(), 1, h->ws_small.as<double>()))) return rc;
+  CMS_HIP(hipMemcpyAsync(out, h->ws_small.ptr, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
+static int top_k_host(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* ids, double* scores,
+                      int32_t* counts) {
+  DevBuf o_ids, o_sc, o_cnt;
+  CMS_HIP(o_ids.ensure(sizeof(int64_t) * row_count * k));
+  CMS_HIP(o_sc.ensure(sizeof(double) * row_count * k));
+  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * row_count));
+  int rc = top_k_rows(h, row_begin, row_count, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
+  if (rc == CMS_OK) {
+    hipError_t e = hipMemcpyAsync(ids, o_ids.ptr, sizeof(int64_t) * row_count * k, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && scores)
+      e = hipMemcpyAsync(scores, o_sc.ptr, sizeof(double) * row_count * k, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(counts, o_cnt.ptr, sizeof(int32_t) * row_count, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) rc = hip_fail(e, "top-k copy-out");
+  }
+  o_ids.release();
+  o_sc.release();
+  o_cnt.release();
+  return rc;
+}
+
+int cms_most_similar(cms_handle* h, int64_t id, int32_t k, int64_t* out_ids, double* out_scores, int32_t* count) {
+  if (!h || !out_ids || !count) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  int64_t row;
+  if ((rc = row_of(h, id, &row))) return rc;
+  return top_k_host(h, row, 1, k, out_ids, out_scores, count);
+}
+
+int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* ids, double* scores,
+                   int32_t* counts) {
+  if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
+  if (row_count == 0) return CMS_OK;
+  return top_k_host(h, row_begin, row_count, k, ids, scores, counts);
+}
+
+int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out) {
+  if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
+  size_t cnt = (size_t)(row_count * h->dw);
+  std::vector<uint32_t> tmp(cnt);
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (h->empty) {
+    std::fill(out, out + cnt, 0.0);
+    return CMS_OK;
+  }
+  CMS_HIP(hipMemcpy(tmp.data(), h->d_table + row_begin * h->dw, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < cnt; ++i) out[i] = (double)tmp[i];
+  return CMS_OK;
+}
+
+int cms_get_stats(cms_handle* h, cms_stats* out) {
+  if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
+  out->pairs_ingested = h->pairs_ingested;
+  out->num_owners = h->n;
+  out->depth = h->p.depth;
+  out->width = h->p.width;
+  out->exact_norms = h->exact_norms;
+  out->world = h->world;
+  out->rank = h->rank;
+  out->table_bytes = (int64_t)sizeof(uint32_t) * h->n * h->dw;
+  return CMS_OK;
+}
+
+int cms_set_timing(cms_handle* h, int32_t enabled) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  h->timing = enabled != 0;
+  return CMS_OK;
+}
+
+int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* launches) {
+  if (!h || !name || !total_ms || !launches) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int rc = resolve_timing(h);
+  if (rc) return rc;
+  auto it = h->timing_acc.find(name);
+  *total_ms = it == h->timing_acc.end() ? 0.0 : it->second.total_ms;
+  *launches = it == h->timing_acc.end() ? 0 : it->second.launches;
+  return CMS_OK;
+}
+
+int cms_reset_timing(cms_handle* h) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  Guard g(h);
+  int rc = resolve_timing(h);
+  h->timing_acc.clear();
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+// cms_internal.h -- handle state and kernel launchers shared by the
+// libmahout_cms.so translation units.  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mahout_cms.h"
+#include "cms_hash.h"
+
+namespace cms {
+
+// Device error flags (one u32 word per handle).
+enum : uint32_t {
+  kFlagBadRow = 1u << 0,    // owner row outside [0, n)
+  kFlagBadValue = 1u << 1,  // increment not a non-negative integer (u32 counters)
+  kFlagOverflow = 1u << 2,  // a row's total mass reached 2^32
+};
+
+// Growable device scratch buffer (grown outside any capture region).
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t need);
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(ptr); }
+  void release();
+};
+
+struct TimingAcc {
+  double total_ms = 0.0;
+  int64_t launches = 0;
+};
+
+struct PendingEvent {
+  std::string name;
+  hipEvent_t start, stop;
+};
+
+// Row-build tuning: pairs per build work item.
+constexpr int64_t kSlice = 16384;
+constexpr int kBuildThreads = 256;
+
+}  // namespace cms
+
+struct cms_handle {
+  cms_params p{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+
+  int64_t a[CMS_MAX_DEPTH] = {};  // HashFunctionBuilder parameters as drawn
+  int64_t b[CMS_MAX_DEPTH] = {};
+  cms::HashParams hp{};
+
+  int64_t n = 0;       // rows
+  int64_t dw = 0;      // d*w counters per row
+  uint32_t* d_table = nullptr;      // [n][d][w]
+  uint64_t* d_row_mass = nullptr;   // [n] total increment mass per row
+  uint64_t* d_norm = nullptr;       // [n][d] exact sum of squares (saturating)
+  double* d_norm_sqrt = nullptr;    // [n][d] Math.sqrt((double) norm)
+  uint32_t* d_flags = nullptr;      // error flags word + counters
+  int64_t* d_owner_ids = nullptr;   // [n] sorted IDs (null => identity)
+  std::vector<int64_t> h_owner_ids;
+
+  bool empty = true;         // every counter is zero (next large batch builds rows)
+  bool norms_valid = false;  // d_norm matches d_table
+  bool finalized = false;
+  int64_t pairs_ingested = 0;
+  int32_t exact_norms = 1;
+
+  // scratch
+  cms::DevBuf ws_in_row, ws_in_key, ws_in_val;   // host-ingest staging
+  cms::DevBuf ws_p1_row, ws_p1_key, ws_p1_val;   // pass-1 partition output
+  cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
+  cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
+  cms::DevBuf ws_query, ws_out;
+
+  // communicator
+  ncclComm_t comm = nullptr;
+  int32_t rank = 0, world = 1;
+
+  // instrumentation
+  bool timing = false;
+  std::map<std::string, cms::TimingAcc> timing_acc;
+  std::vector<cms::PendingEvent> pending;
+};
+
+namespace cms {
+
+// error plumbing (cms_api.hip)
+int set_error(int code, const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+#define CMS_HIP(call)                                  \
+  do {                                                 \
+    hipError_t _e = (call);                            \
+    if (_e != hipSuccess) return cms::hip_fail(_e, #call); \
+  } while (0)
+
+// timing scopes on the handle stream
+struct TimedScope {
+  cms_handle* h;
+  hipEvent_t start = nullptr;
+  const char* name;
+  TimedScope(cms_handle* hh, const char* nm);
+  ~TimedScope();
+};
+
+// ---- launchers (cms_ingest.hip) ----
+// COO -> table. rows are dense row indices (validated on device).
+int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n);
+// CSR (offsets int64 [n+1]) -> table.
+int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs);
+// owner IDs -> rows by binary search over h->d_owner_ids.
+int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_rows);
+int compute_norms(cms_handle* h);
+int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d_out);
+
+// ---- launchers (cms_query.hip) ----
+int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);
+int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
+               int32_t* d_counts);
+
+}  // namespace cms

@@ -1,0 +1,210 @@
+"""SketchTable: a handle to the device-resident count-min-sketch table.
+
+Thin, typed wrapper over the C ABI (include/mahout_cms.h).  One table holds
+the [num_owners][depth][width] u32 sketches of every owner; the reference
+builds the same sketches one DoubleCountMinSketch at a time
+(T/impl/common/DoubleCountMinSketch.java, T/impl/similarity/CosineCM.java:41-67).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _dev_ptr(x):
+    """Device pointer from an int or a torch tensor (None passes through)."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return ctypes.c_void_p(x)
+    return ctypes.c_void_p(x.data_ptr())
+
+
+def shape_from_delta_epsilon(delta, epsilon):
+    """AbstractCountMinSketch(delta, epsilon) shape rule -> (width, depth)."""
+    lib = _lib.load()
+    w = ctypes.c_int32()
+    d = ctypes.c_int32()
+    check(lib.cms_shape_from_delta_epsilon(delta, epsilon, ctypes.byref(w), ctypes.byref(d)))
+    return w.value, d.value
+
+
+def shard_of_key(key, world):
+    return _lib.load().cms_shard_of_key(int(key), int(world))
+
+
+def comm_unique_id():
+    buf = (ctypes.c_uint8 * 128)()
+    check(_lib.load().cms_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class SketchTable:
+    def __init__(self, num_owners, depth=5, width=4096, seed=42, weighted=False, device=-1, owner_ids=None):
+        lib = _lib.load()
+        p = _lib.CmsParams()
+        check(lib.cms_params_init(ctypes.byref(p)))
+        p.depth = depth
+        p.width = width
+        p.seed = seed
+        p.num_owners = num_owners
+        p.weighting = _lib.CMS_WEIGHTED if weighted else _lib.CMS_UNWEIGHTED
+        p.device = device
+        h = ctypes.c_void_p()
+        check(lib.cms_create(ctypes.byref(p), ctypes.byref(h)))
+        self._lib = lib
+        self._h = h
+        self.num_owners = num_owners
+        self.depth = depth
+        self.width = width
+        self.seed = seed
+        if owner_ids is not None:
+            self.set_owner_ids(owner_ids)
+
+    # -- lifecycle --
+    def close(self):
+        if self._h:
+            self._lib.cms_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- setup --
+    def set_owner_ids(self, ids):
+        ids = np.ascontiguousarray(ids, np.int64)
+        check(self._lib.cms_set_owner_ids(self._h, _ptr(ids), ids.size))
+
+    def hash_params(self):
+        a = np.zeros(self.depth, np.int64)
+        b = np.zeros(self.depth, np.int64)
+        check(self._lib.cms_hash_params(self._h, _ptr(a), _ptr(b)))
+        return a, b
+
+    def hash_keys(self, keys):
+        keys = np.ascontiguousarray(keys, np.int64)
+        out = np.zeros((keys.size, self.depth), np.int32)
+        check(self._lib.cms_hash_keys(self._h, _ptr(keys), keys.size, _ptr(out)))
+        return out
+
+    # -- ingest --
+    def ingest(self, owner, key, val=None):
+        owner = np.ascontiguousarray(owner, np.int64)
+        key = np.ascontiguousarray(key, np.int64)
+        v = None if val is None else np.ascontiguousarray(val, np.float32)
+        if owner.size != key.size or (v is not None and v.size != key.size):
+            raise ValueError("owner/key/val length mismatch")
+        check(self._lib.cms_ingest(self._h, _ptr(owner), _ptr(key), _ptr(v), owner.size))
+
+    def ingest_device_rows(self, d_row, d_key, d_val, n):
+        check(self._lib.cms_ingest_device_rows(self._h, _dev_ptr(d_row), _dev_ptr(d_key), _dev_ptr(d_val), int(n)))
+
+    def ingest_csr(self, offsets, keys, vals=None):
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        keys = np.ascontiguousarray(keys, np.int64)
+        v = None if vals is None else np.ascontiguousarray(vals, np.float32)
+        if offsets.size != self.num_owners + 1:
+            raise ValueError("offsets must have num_owners + 1 entries")
+        check(self._lib.cms_ingest_csr(self._h, _ptr(offsets), _ptr(keys), _ptr(v)))
+
+    def ingest_csr_device(self, d_offsets, d_keys, d_vals=None):
+        check(self._lib.cms_ingest_csr_device(self._h, _dev_ptr(d_offsets), _dev_ptr(d_keys), _dev_ptr(d_vals)))
+
+    def reset(self):
+        check(self._lib.cms_reset(self._h))
+
+    def comm_init(self, unique_id, rank, world):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        check(self._lib.cms_comm_init(self._h, buf, rank, world))
+
+    def finalize(self):
+        check(self._lib.cms_finalize(self._h))
+
+    def synchronize(self):
+        check(self._lib.cms_synchronize(self._h))
+
+    # -- queries --
+    def similarity(self, id1, id2):
+        out = ctypes.c_double()
+        check(self._lib.cms_similarity(self._h, int(id1), int(id2), ctypes.byref(out)))
+        return out.value
+
+    def similarities(self, id1, ids2):
+        ids2 = np.ascontiguousarray(ids2, np.int64)
+        out = np.zeros(ids2.size, np.float64)
+        check(self._lib.cms_similarities(self._h, int(id1), _ptr(ids2), ids2.size, _ptr(out)))
+        return out
+
+    def point_query(self, owner_id, key):
+        out = ctypes.c_double()
+        check(self._lib.cms_point_query(self._h, int(owner_id), int(key), ctypes.byref(out)))
+        return out.value
+
+    def most_similar(self, owner_id, k):
+        ids = np.zeros(k, np.int64)
+        sc = np.zeros(k, np.float64)
+        cnt = ctypes.c_int32()
+        check(self._lib.cms_most_similar(self._h, int(owner_id), int(k), _ptr(ids), _ptr(sc), ctypes.byref(cnt)))
+        return ids[:cnt.value], sc[:cnt.value]
+
+    def top_k_rows(self, row_begin, row_count, k):
+        ids = np.zeros((row_count, k), np.int64)
+        sc = np.zeros((row_count, k), np.float64)
+        cnt = np.zeros(row_count, np.int32)
+        check(self._lib.cms_top_k_rows(self._h, int(row_begin), int(row_count), int(k), _ptr(ids), _ptr(sc),
+                                       _ptr(cnt)))
+        return ids, sc, cnt
+
+    def read_counters(self, row_begin=0, row_count=None):
+        if row_count is None:
+            row_count = self.num_owners - row_begin
+        out = np.zeros((row_count, self.depth, self.width), np.float64)
+        check(self._lib.cms_read_counters(self._h, int(row_begin), int(row_count), _ptr(out)))
+        return out
+
+    # -- instrumentation --
+    def stats(self):
+        s = _lib.CmsStats()
+        check(self._lib.cms_get_stats(self._h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f, _ in s._fields_}
+
+    def set_timing(self, enabled=True):
+        check(self._lib.cms_set_timing(self._h, 1 if enabled else 0))
+
+    def timing(self, name):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self._lib.cms_get_timing(self._h, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def reset_timing(self):
+        check(self._lib.cms_reset_timing(self._h))
+
+
+def shard_of_keys(keys, world):
+    """Vectorised cms_shard_of_key (splitmix64 finalizer mod world) for host
+    arrays -- used to route a stream's pairs to their rank before ingest."""
+    z = np.asarray(keys, np.int64).astype(np.uint64)
+    if world <= 1:
+        return np.zeros(z.shape, np.int32)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z % np.uint64(world)).astype(np.int32)

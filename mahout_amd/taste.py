@@ -1,0 +1,166 @@
+"""Host-side mirror of the reference's plugin surface for the sketch path.
+
+``CosineCM`` keeps the names, argument meaning and error behaviour of
+org.apache.mahout.cf.taste.impl.similarity.CosineCM
+(T/impl/similarity/CosineCM.java) and of the two plugin interfaces it
+serves, UserSimilarity (T/similarity/UserSimilarity.java:31-58) and
+ItemSimilarity (T/similarity/ItemSimilarity.java:31-64); every similarity
+is computed by libmahout_cms.so on the GPU.
+
+Shape: the reference sizes each owner's sketch from CountMinSketchConfig's
+(delta, epsilon) (CosineCM.java:63,86).  The fixed-shape configs of this
+path (d, w for every owner) are expressed by ``FixedShapeConfig``, whose
+getDelta/getEpsilon return exp(-d) and e/w -- the subclass override the
+reference allows (CountMinSketchConfig.getDelta/getEpsilon are public,
+non-final) -- and the shape actually used is the one
+AbstractCountMinSketch(delta, epsilon) derives from them.
+"""
+import math
+
+import numpy as np
+
+from . import _lib
+from .datamodel import NoSuchUserException
+from .sketch import SketchTable, shape_from_delta_epsilon
+
+
+class TasteException(Exception):
+    """org.apache.mahout.cf.taste.common.TasteException"""
+
+
+class NoSuchItemException(TasteException, KeyError):
+    """org.apache.mahout.cf.taste.common.NoSuchItemException"""
+
+
+class Weighting:
+    UNWEIGHTED = "UNWEIGHTED"
+    WEIGHTED = "WEIGHTED"
+
+
+class HashFunctionBuilder:
+    """HashFunctionBuilder(long seed) (T/impl/common/HashFunctionBuilder.java:59-65)."""
+
+    def __init__(self, seed):
+        self.seed = int(seed)
+
+
+class FixedShapeConfig:
+    """Every owner gets the same (depth, width)."""
+
+    def __init__(self, depth, width):
+        self.depth = int(depth)
+        self.width = int(width)
+
+    def getDelta(self, owner_id=None):
+        return math.exp(-float(self.depth))
+
+    def getEpsilon(self, owner_id=None):
+        return math.e / float(self.width)
+
+    def shape(self):
+        """(width, depth) that new DoubleCountMinSketch(delta, epsilon, ...) builds."""
+        return shape_from_delta_epsilon(self.getDelta(), self.getEpsilon())
+
+
+def _map_error(e, owner_kind="user"):
+    if e.code == _lib.CMS_E_NO_SUCH_ID:
+        return NoSuchUserException(str(e)) if owner_kind == "user" else NoSuchItemException(str(e))
+    if e.code in (_lib.CMS_E_PARAM, _lib.CMS_E_SHAPE):
+        return ValueError(str(e))  # IllegalArgumentException
+    return TasteException(str(e))
+
+
+class CosineCM:
+    """CosineCM(DataModel, [Weighting,] CountMinSketchConfig, HashFunctionBuilder).
+
+    Owners are the DataModel's users (sketches keyed by item ID).  Over a
+    transposed DataModel the owners are items and userSimilarity /
+    itemSimilarity are the sketch-cosine ItemSimilarity.
+    """
+
+    def __init__(self, dataModel, conf, hfBuilder, weighting=Weighting.UNWEIGHTED, device=-1):
+        if not dataModel.hasPreferenceValues():  # CosineCM.java:38
+            raise ValueError("DataModel doesn't have preference values")
+        width, depth = conf.shape() if hasattr(conf, "shape") else (conf.width, conf.depth)
+        self._model = dataModel
+        self._conf = conf
+        self._hfb = hfBuilder
+        self._weighted = weighting == Weighting.WEIGHTED
+        self._device = device
+        self.depth, self.width = depth, width
+        self._inferrer = None
+        self._build()
+
+    def _build(self):
+        m = self._model
+        self._table = SketchTable(m.getNumUsers(), depth=self.depth, width=self.width, seed=self._hfb.seed,
+                                  weighted=self._weighted, device=self._device, owner_ids=m.getUserIDs())
+        try:
+            self._table.ingest_csr(m.offsets, m.keys, m.values)
+            self._table.finalize()
+        except _lib.CmsError as e:
+            raise _map_error(e)
+
+    @property
+    def table(self):
+        return self._table
+
+    # ---- UserSimilarity ----
+    def userSimilarity(self, userID1, userID2):
+        try:
+            return self._table.similarity(userID1, userID2)
+        except _lib.CmsError as e:
+            raise _map_error(e, "user")
+
+    def setPreferenceInferrer(self, inferrer):
+        if inferrer is None:
+            raise ValueError("inferrer is null")
+        self._inferrer = inferrer  # unused by the sketch cosine, as in CosineCM
+
+    # ---- ItemSimilarity (owners are items in the transposed orientation) ----
+    def itemSimilarity(self, itemID1, itemID2):
+        try:
+            return self._table.similarity(itemID1, itemID2)
+        except _lib.CmsError as e:
+            raise _map_error(e, "item")
+
+    def itemSimilarities(self, itemID1, itemID2s):
+        try:
+            return self._table.similarities(itemID1, itemID2s)
+        except _lib.CmsError as e:
+            raise _map_error(e, "item")
+
+    def allSimilarItemIDs(self, itemID):
+        """AbstractItemSimilarity.allSimilarItemIDs: every owner whose
+        similarity is not NaN (T/impl/similarity/AbstractItemSimilarity.java:48-58)."""
+        ids = self._model.getUserIDs()
+        sims = self.itemSimilarities(itemID, ids)
+        return ids[~np.isnan(sims)]
+
+    # ---- recommender-side consumers ----
+    def mostSimilarUserIDs(self, userID, howMany):
+        """GenericUserBasedRecommender.mostSimilarUserIDs (:119-127) with
+        TopItems.getTopUsers (TopItems.java:91-136)."""
+        if howMany < 1:
+            raise ValueError("howMany must be at least 1")
+        try:
+            ids, _ = self._table.most_similar(userID, howMany)
+        except _lib.CmsError as e:
+            raise _map_error(e, "user")
+        return ids
+
+    def getExportedCMProfileEstimate(self, userID, itemID):
+        """DoubleCountMinSketch.get(itemID) on userID's sketch, the point query
+        GenericUserBasedRecommender.doEstimatePreference uses (:153-158)."""
+        try:
+            return self._table.point_query(userID, itemID)
+        except _lib.CmsError as e:
+            raise _map_error(e, "user")
+
+    def refresh(self, alreadyRefreshed=None):
+        """Refreshable.refresh: rebuild every sketch from the data model."""
+        self._table.close()
+        self._build()
+
+    def close(self):
+        self._table.close()

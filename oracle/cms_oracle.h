@@ -1,0 +1,106 @@
+/*
+ * cms_oracle.h -- CPU restatement of the reference count-min-sketch +
+ * sketch-cosine path (Mahout Taste CosineCM), used ONLY as test
+ * infrastructure: the parity checker for tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg.  Nothing in mahout_amd/ links or loads it.
+ *
+ * Every function cites the reference file:line it restates.  Paths are
+ * relative to mr/src/main/java/org/apache/mahout/cf/taste/ ("T/").
+ *
+ * Parity pinning (see DESIGN.md "Oracle"): the reference is Java and cannot
+ * run in this image (no JDK), and no reference test exercises this path.
+ * The restatement is pinned by (1) published java.util.Random known-answer
+ * values, (2) an independent pure-Python big-integer restatement of the
+ * BigInteger hash (tests/test_oracle_kats.py), and (3) the reference's own
+ * adjacent exact-cosine known answers (VectorSimilarityMeasuresTest 0.769846046,
+ * ItemSimilarityJobTest 0.45 / 0.89) reproduced through collision-free sketches.
+ */
+#ifndef MAHOUT_CMS_ORACLE_H
+#define MAHOUT_CMS_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- java.util.Random (JDK; third-party semantics, see header) ---- */
+typedef struct { uint64_t seed; } orc_jrandom;
+void    orc_jrandom_init(orc_jrandom* r, int64_t seed);
+int32_t orc_jrandom_next_int(orc_jrandom* r);
+int64_t orc_jrandom_next_long(orc_jrandom* r);
+
+/* T/impl/common/HashFunctionBuilder.java:59-97 */
+void orc_hash_params(int64_t seed, int32_t depth, int64_t* a, int64_t* b);
+
+/* T/impl/common/HashFunction.java:31-34 */
+int32_t orc_hash(int64_t a, int64_t b, int32_t width, int64_t key);
+void orc_hash_many(const int64_t* a, const int64_t* b, int32_t depth, int32_t width,
+                   const int64_t* keys, int64_t n, int32_t* out /* [n][depth] */);
+
+/* T/impl/common/AbstractCountMinSketch.java:168-182: (delta, epsilon) -> (w, d).
+ * Returns 0 on success, -1 for the CMException cases. */
+int orc_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, int32_t* depth);
+
+/* ---- DoubleCountMinSketch: row-major [d][w] fp64, T/impl/common/DoubleCountMinSketch.java ---- */
+/* update :72-80 (order = call order), applied to a table of `rows` sketches.
+ * owner_row[i] selects the sketch, key[i] the key, val (nullable => 1.0). */
+void orc_sketch_build(double* table /* [rows][d][w], caller-zeroed */,
+                      int64_t rows, int32_t depth, int32_t width,
+                      const int64_t* a, const int64_t* b,
+                      const int64_t* owner_row, const int64_t* key, const float* val, int64_t n);
+/* point query get(key) :94-103 */
+double orc_sketch_get(const double* sketch, int32_t depth, int32_t width,
+                      const int64_t* a, const int64_t* b, int64_t key);
+/* static cosine(a,b) :114-149 (sequential fp64 sums, min over rows, NaN if none) */
+double orc_sketch_cosine(const double* sa, const double* sb, int32_t depth, int32_t width);
+
+/* T/impl/similarity/AbstractSimilarity.java:313-330, called as
+ * normalizeWeightResult(r, 1, 0) from CosineCM.java:91-93 */
+double orc_normalize_weight_result(double result, int count, int num, int weighted);
+
+/* CosineCM.userSimilarity (T/impl/similarity/CosineCM.java:83-96) in the
+ * fixed-shape orientation: cosine of two prebuilt sketches, then the
+ * NaN-guarded normalizeWeightResult. */
+double orc_cosine_cm(const double* sa, const double* sb, int32_t depth, int32_t width, int weighted);
+
+/* All similarities of row `q` against rows [0,rows): out[j] (NaN for j==q,
+ * as MostSimilarEstimator, GenericUserBasedRecommender.java:231-247). */
+void orc_similarities_row(const double* table, int64_t rows, int32_t depth, int32_t width,
+                          int64_t q, int weighted, double* out);
+
+/* TopItems.getTopUsers (T/impl/recommender/TopItems.java:91-136) + SimilarUser.compareTo
+ * (T/impl/recommender/SimilarUser.java:62-78), over candidates in ascending ID order.
+ * Returns the count written to out_ids (<= k).  scores[i] belongs to ids[i]. */
+int32_t orc_top_users(const int64_t* ids, const double* scores, int64_t n, int32_t k,
+                      int64_t* out_ids, double* out_scores);
+
+/* CountMinSketchConfig (T/impl/common/CountMinSketchConfig.java:268-317, 218-256) */
+double orc_proba_inserted(int32_t w, int32_t d, int32_t n, int32_t u);
+double orc_proba_not_exact_retrieve(int32_t w, int32_t d, int32_t n);
+double orc_fmeasure(int32_t w, int32_t d, int32_t n, int32_t u, double q);
+/* per-owner grid search; returns -1 if no solution (TasteException) */
+int orc_compute_config(int32_t n_prefs, int32_t u_items, double q, int32_t* best_w, int32_t* best_d,
+                       double* delta, double* epsilon);
+
+/* Faithful CosineCM cost model used by bench.py's cpu_baseline (port):
+ * rebuild the first owner's sketch per call from its CSR preferences, the
+ * second from a cache, then cosine.  Returns the number of similarities computed. */
+int64_t orc_faithful_pairs(const int64_t* offsets, const int64_t* keys, const float* vals,
+                           int64_t rows, int32_t depth, int32_t width,
+                           const int64_t* a, const int64_t* b,
+                           const int64_t* pair_i, const int64_t* pair_j, int64_t npairs,
+                           double* out);
+
+/* CPU ingest baseline in the reference's own cost model: for each owner in
+ * [row_lo,row_hi) rebuild its sketch into ONE reusable fp64 buffer (w*d zero
+ * fill + n_u updates, DoubleCountMinSketch ctor :253-257 + update :72-80) and
+ * fold a checksum of the counters so nothing is dead.  Returns #updates. */
+int64_t orc_build_rows_reuse(const int64_t* offsets, const int64_t* keys, const float* vals,
+                             int64_t row_lo, int64_t row_hi, int32_t depth, int32_t width,
+                             const int64_t* a, const int64_t* b, double* checksum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

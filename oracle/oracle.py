@@ -1,0 +1,175 @@
+"""ctypes wrapper over oracle/_build/liboracle_cms.so (the C restatement).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never by mahout_amd/ (the product).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle_cms.so")
+
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def _load():
+    if not os.path.exists(_SO):
+        build()
+    lib = ctypes.CDLL(_SO)
+    c = ctypes
+    sig = {
+        "orc_hash_params": (None, [c.c_int64, c.c_int32, _i64p, _i64p]),
+        "orc_hash": (c.c_int32, [c.c_int64, c.c_int64, c.c_int32, c.c_int64]),
+        "orc_hash_many": (None, [_i64p, _i64p, c.c_int32, c.c_int32, _i64p, c.c_int64, _i32p]),
+        "orc_shape_from_delta_epsilon": (c.c_int, [c.c_double, c.c_double, c.POINTER(c.c_int32), c.POINTER(c.c_int32)]),
+        "orc_sketch_build": (None, [_f64p, c.c_int64, c.c_int32, c.c_int32, _i64p, _i64p, _i64p, _i64p, c.c_void_p, c.c_int64]),
+        "orc_sketch_get": (c.c_double, [c.c_void_p, c.c_int32, c.c_int32, _i64p, _i64p, c.c_int64]),
+        "orc_sketch_cosine": (c.c_double, [c.c_void_p, c.c_void_p, c.c_int32, c.c_int32]),
+        "orc_normalize_weight_result": (c.c_double, [c.c_double, c.c_int, c.c_int, c.c_int]),
+        "orc_cosine_cm": (c.c_double, [c.c_void_p, c.c_void_p, c.c_int32, c.c_int32, c.c_int]),
+        "orc_similarities_row": (None, [_f64p, c.c_int64, c.c_int32, c.c_int32, c.c_int64, c.c_int, _f64p]),
+        "orc_top_users": (c.c_int32, [_i64p, _f64p, c.c_int64, c.c_int32, _i64p, _f64p]),
+        "orc_fmeasure": (c.c_double, [c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.c_double]),
+        "orc_compute_config": (c.c_int, [c.c_int32, c.c_int32, c.c_double, c.POINTER(c.c_int32), c.POINTER(c.c_int32),
+                                         c.POINTER(c.c_double), c.POINTER(c.c_double)]),
+        "orc_faithful_pairs": (c.c_int64, [_i64p, _i64p, c.c_void_p, c.c_int64, c.c_int32, c.c_int32, _i64p, _i64p,
+                                           _i64p, _i64p, c.c_int64, _f64p]),
+        "orc_build_rows_reuse": (c.c_int64, [_i64p, _i64p, c.c_void_p, c.c_int64, c.c_int64, c.c_int32, c.c_int32,
+                                             _i64p, _i64p, c.POINTER(c.c_double)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def _vp(arr):
+    return None if arr is None else arr.ctypes.data_as(ctypes.c_void_p)
+
+
+def hash_params(seed, depth):
+    a = np.zeros(depth, np.int64)
+    b = np.zeros(depth, np.int64)
+    lib().orc_hash_params(seed, depth, a, b)
+    return a, b
+
+
+def hash_keys(a, b, width, keys):
+    keys = np.ascontiguousarray(keys, np.int64)
+    out = np.zeros((keys.size, len(a)), np.int32)
+    lib().orc_hash_many(np.ascontiguousarray(a, np.int64), np.ascontiguousarray(b, np.int64), len(a), width,
+                        keys, keys.size, out)
+    return out
+
+
+def shape_from_delta_epsilon(delta, epsilon):
+    w = ctypes.c_int32()
+    d = ctypes.c_int32()
+    rc = lib().orc_shape_from_delta_epsilon(delta, epsilon, ctypes.byref(w), ctypes.byref(d))
+    if rc != 0:
+        raise ValueError("CMException: delta/epsilon out of range")
+    return w.value, d.value
+
+
+def build_table(rows, depth, width, a, b, owner_row, key, val=None):
+    """fp64 [rows][depth][width] table, updates applied in stream order."""
+    table = np.zeros((rows, depth, width), np.float64)
+    owner_row = np.ascontiguousarray(owner_row, np.int64)
+    key = np.ascontiguousarray(key, np.int64)
+    v = None if val is None else np.ascontiguousarray(val, np.float32)
+    lib().orc_sketch_build(table, rows, depth, width, a, b, owner_row, key, _vp(v), owner_row.size)
+    return table
+
+
+def sketch_get(sketch, a, b, key):
+    sk = np.ascontiguousarray(sketch, np.float64)
+    d, w = sk.shape
+    return lib().orc_sketch_get(_vp(sk), d, w, a, b, int(key))
+
+
+def cosine(sa, sb):
+    sa = np.ascontiguousarray(sa, np.float64)
+    sb = np.ascontiguousarray(sb, np.float64)
+    d, w = sa.shape
+    return lib().orc_sketch_cosine(_vp(sa), _vp(sb), d, w)
+
+
+def cosine_cm(sa, sb, weighted=False):
+    sa = np.ascontiguousarray(sa, np.float64)
+    sb = np.ascontiguousarray(sb, np.float64)
+    d, w = sa.shape
+    return lib().orc_cosine_cm(_vp(sa), _vp(sb), d, w, int(weighted))
+
+
+def normalize_weight_result(r, count=1, num=0, weighted=False):
+    return lib().orc_normalize_weight_result(r, count, num, int(weighted))
+
+
+def similarities_row(table, q, weighted=False):
+    rows, d, w = table.shape
+    out = np.zeros(rows, np.float64)
+    lib().orc_similarities_row(np.ascontiguousarray(table), rows, d, w, q, int(weighted), out)
+    return out
+
+
+def top_users(ids, scores, k):
+    ids = np.ascontiguousarray(ids, np.int64)
+    scores = np.ascontiguousarray(scores, np.float64)
+    oi = np.zeros(k, np.int64)
+    os_ = np.zeros(k, np.float64)
+    n = lib().orc_top_users(ids, scores, ids.size, k, oi, os_)
+    return oi[:n], os_[:n]
+
+
+def fmeasure(w, d, n, u, q):
+    return lib().orc_fmeasure(w, d, n, u, q)
+
+
+def compute_config(n_prefs, u_items, q):
+    w = ctypes.c_int32()
+    d = ctypes.c_int32()
+    de = ctypes.c_double()
+    ep = ctypes.c_double()
+    rc = lib().orc_compute_config(n_prefs, u_items, q, ctypes.byref(w), ctypes.byref(d), ctypes.byref(de),
+                                  ctypes.byref(ep))
+    if rc != 0:
+        raise RuntimeError("No solution found")
+    return w.value, d.value, de.value, ep.value
+
+
+def faithful_pairs(offsets, keys, vals, rows, depth, width, a, b, pi, pj):
+    out = np.zeros(len(pi), np.float64)
+    v = None if vals is None else np.ascontiguousarray(vals, np.float32)
+    lib().orc_faithful_pairs(np.ascontiguousarray(offsets, np.int64), np.ascontiguousarray(keys, np.int64), _vp(v),
+                             rows, depth, width, a, b, np.ascontiguousarray(pi, np.int64),
+                             np.ascontiguousarray(pj, np.int64), len(pi), out)
+    return out
+
+
+def build_rows_reuse(offsets, keys, vals, lo, hi, depth, width, a, b):
+    cs = ctypes.c_double()
+    v = None if vals is None else np.ascontiguousarray(vals, np.float32)
+    n = lib().orc_build_rows_reuse(np.ascontiguousarray(offsets, np.int64), np.ascontiguousarray(keys, np.int64),
+                                   _vp(v), lo, hi, depth, width, a, b, ctypes.byref(cs))
+    return n, cs.value

@@ -1,0 +1,92 @@
+"""CPU: libmahout_cms.so loads, exports every symbol include/mahout_cms.h
+declares, and its pure-host entry points behave (no device calls here)."""
+import ctypes
+import math
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mahout_cms.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|int32_t)\s+(cms_\w+)\s*\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from mahout_amd import build_lib, _lib
+    build_lib.build()
+    return _lib.load()
+
+
+def test_header_symbols_match_binding():
+    from mahout_amd import _lib
+    assert header_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(lib):
+    raw = ctypes.CDLL(os.path.join(ROOT, "mahout_amd", "libmahout_cms.so"))
+    for sym in header_symbols():
+        assert hasattr(raw, sym), sym
+
+
+def test_abi_version(lib):
+    assert lib.cms_abi_version() == 1
+
+
+def test_params_init_defaults(lib):
+    from mahout_amd._lib import CmsParams
+    p = CmsParams()
+    assert lib.cms_params_init(ctypes.byref(p)) == 0
+    assert p.struct_size == ctypes.sizeof(CmsParams) == 40
+    assert (p.depth, p.width, p.seed, p.device) == (5, 4096, 42, -1)
+
+
+def test_shape_from_delta_epsilon_matches_oracle(lib, oracle):
+    from mahout_amd import shape_from_delta_epsilon
+    for w in [39, 40, 43, 78, 1024, 4096, 8192]:
+        for d in [1, 4, 5, 25]:
+            assert shape_from_delta_epsilon(math.exp(-d), math.e / w) == oracle.shape_from_delta_epsilon(
+                math.exp(-d), math.e / w)
+    from mahout_amd._lib import CmsError, CMS_E_PARAM
+    with pytest.raises(CmsError) as ei:
+        shape_from_delta_epsilon(0.0, 0.5)
+    assert ei.value.code == CMS_E_PARAM
+
+
+def test_shard_function_balanced_and_stable(lib):
+    from mahout_amd import shard_of_key
+    for world in [1, 2, 4, 8]:
+        counts = [0] * world
+        for k in range(20000):
+            counts[shard_of_key(k, world)] += 1
+        assert min(counts) > 0.9 * 20000 / world
+    assert shard_of_key(12345, 8) == shard_of_key(12345, 8)
+    assert shard_of_key(-1, 8) in range(8)
+
+
+def test_create_rejects_bad_params_without_device(lib):
+    from mahout_amd._lib import CmsParams
+    p = CmsParams()
+    lib.cms_params_init(ctypes.byref(p))
+    h = ctypes.c_void_p()
+    p.num_owners = 0
+    assert lib.cms_create(ctypes.byref(p), ctypes.byref(h)) == 1
+    p.num_owners = 10
+    p.depth = 0
+    assert lib.cms_create(ctypes.byref(p), ctypes.byref(h)) == 1
+    assert b"depth" in lib.cms_last_error()
+
+
+def test_vectorised_shard_matches_library(lib):
+    import numpy as np
+    from mahout_amd import shard_of_key
+    from mahout_amd.sketch import shard_of_keys
+    keys = np.concatenate([np.arange(-1000, 1000), np.array([2 ** 63 - 1, -2 ** 63, 123456789012345])]).astype(np.int64)
+    for world in [1, 2, 3, 8]:
+        got = shard_of_keys(keys, world)
+        assert got.tolist() == [shard_of_key(int(k), world) for k in keys]

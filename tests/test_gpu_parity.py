@@ -1,0 +1,260 @@
+"""GPU parity: libmahout_cms.so (gfx950) against the CPU restatement oracle.
+
+Bar: bit-exact hash indices and counters; cosine/similarity values compared
+bit for bit (the exact-integer + IEEE fp64 epilogue reproduces the
+reference's arithmetic; the north-star tolerance of 1e-5 relative is the
+ceiling, asserted separately as a floor check).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from mahout_amd import SketchTable
+from mahout_amd._lib import CmsError, CMS_E_NO_SUCH_ID, CMS_E_VALUE, CMS_E_STATE, CMS_E_PARAM
+from mahout_amd.synth import zipf_stream, to_csr
+
+pytestmark = pytest.mark.gpu
+
+EDGE = np.array([0, 1, -1, 2 ** 63 - 1, -2 ** 63, 9223372036854775783, 9223372036854775782, -9223372036854775783,
+                 -9223372036854775784, 2 ** 62, -2 ** 62, 943, 1682], np.int64)
+
+
+def same(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return a.shape == b.shape and bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+def oracle_table(oracle, n, d, w, seed, rows, keys, vals=None):
+    a, b = oracle.hash_params(seed, d)
+    return oracle.build_table(n, d, w, a, b, rows, keys, vals)
+
+
+@pytest.mark.parametrize("width", [1024, 4096, 8192, 1000, 39, 1])
+def test_hash_keys_bit_exact(oracle, width):
+    rng = np.random.Generator(np.random.PCG64(width))
+    keys = np.concatenate([EDGE, rng.integers(-2 ** 63, 2 ** 63 - 1, size=100000, dtype=np.int64)])
+    with SketchTable(4, depth=5, width=width, seed=42) as t:
+        a, b = t.hash_params()
+        oa, ob = oracle.hash_params(42, 5)
+        assert a.tolist() == oa.tolist() and b.tolist() == ob.tolist()
+        np.testing.assert_array_equal(t.hash_keys(keys), oracle.hash_keys(oa, ob, width, keys))
+
+
+def test_ingest_small_atomic_path(oracle):
+    rows = np.array([0, 1, 1, 2, 3, 3, 3, 0], np.int64)
+    keys = np.array([5, -7, 5, 2 ** 62, 1, 1, 99, -2 ** 63], np.int64)
+    with SketchTable(4, depth=4, width=64, seed=42) as t:
+        t.ingest(rows, keys)
+        t.finalize()
+        assert same(t.read_counters(), oracle_table(oracle, 4, 4, 64, 42, rows, keys))
+
+
+@pytest.mark.parametrize("n,d,w,npairs", [(3000, 4, 256, 400_000), (700, 5, 1024, 300_000), (50, 3, 100, 270_000)])
+def test_ingest_partition_path_with_hot_rows(oracle, n, d, w, npairs):
+    items, users = zipf_stream(20000, n, npairs, seed=n)
+    with SketchTable(n, depth=d, width=w, seed=7) as t:
+        t.ingest(items, users)
+        t.finalize()
+        got = t.read_counters()
+    exp = oracle_table(oracle, n, d, w, 7, items, users)
+    assert same(got, exp)
+    assert np.bincount(items, minlength=n).max() > 16384  # a hot row was split into slices
+
+
+def test_ingest_csr_matches_coo(oracle):
+    n, d, w = 2000, 5, 512
+    items, users = zipf_stream(50000, n, 500_000, seed=3)
+    off, keys, _ = to_csr(items, users, n)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest_csr(off, keys)
+        t.finalize()
+        got = t.read_counters()
+    assert same(got, oracle_table(oracle, n, d, w, 42, items, users))
+
+
+def test_integer_values_and_bad_value(oracle):
+    n = 300
+    items, users = zipf_stream(5000, n, 300_000, seed=9)
+    vals = np.random.Generator(np.random.PCG64(1)).integers(1, 6, size=items.size).astype(np.float32)
+    with SketchTable(n, depth=4, width=1024, seed=42) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        assert same(t.read_counters(), oracle_table(oracle, n, 4, 1024, 42, items, users, vals))
+    with SketchTable(n, depth=4, width=1024, seed=42) as t:
+        bad = vals.copy()
+        bad[12345] = 0.5
+        with pytest.raises(CmsError) as ei:
+            t.ingest(items, users, bad)
+        assert ei.value.code == CMS_E_VALUE
+
+
+def test_owner_ids_and_errors(oracle):
+    ids = np.array([-50, 3, 10, 11, 1000], np.int64)
+    with SketchTable(5, depth=4, width=128, seed=42, owner_ids=ids) as t:
+        with pytest.raises(CmsError) as ei:
+            t.similarity(3, 10)
+        assert ei.value.code == CMS_E_STATE
+        t.ingest(np.array([3, 3, 1000, -50, 10], np.int64), np.array([1, 2, 1, 1, 2], np.int64))
+        t.finalize()
+        with pytest.raises(CmsError) as ei:
+            t.similarity(3, 4)
+        assert ei.value.code == CMS_E_NO_SUCH_ID
+        with pytest.raises(CmsError) as ei:
+            t.ingest(np.array([7], np.int64), np.array([1], np.int64))
+        assert ei.value.code == CMS_E_NO_SUCH_ID
+        # owner 11 never ingested: zero sketch -> every row denominator 0 -> NaN
+        assert math.isnan(t.similarity(3, 11))
+        assert abs(t.similarity(3, 3) - 1.0) < 1e-15
+
+
+def test_accumulate_equals_single_batch(oracle):
+    n, d, w = 1500, 4, 512
+    items, users = zipf_stream(30000, n, 800_000, seed=21)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items[:400_000], users[:400_000])       # partition build into an empty table
+        t.ingest(items[400_000:700_000], users[400_000:700_000])  # partition build, accumulate mode
+        t.ingest(items[700_000:], users[700_000:])       # atomic path (small batch)
+        t.finalize()
+        got = t.read_counters()
+    assert same(got, oracle_table(oracle, n, d, w, 42, items, users))
+
+
+def _oracle_row_sims(oracle, table, q, weighted=False):
+    return oracle.similarities_row(table, q, weighted)
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_similarities_bit_exact(oracle, weighted):
+    n, d, w = 400, 5, 1024
+    items, users = zipf_stream(8000, n, 300_000, seed=5)
+    vals = np.random.Generator(np.random.PCG64(2)).integers(1, 6, size=items.size).astype(np.float32)
+    ot = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42, weighted=weighted) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        assert t.stats()["exact_norms"] == 1
+        for q in [0, 1, 17, 399]:
+            got = t.similarities(q, np.arange(n))
+            exp = _oracle_row_sims(oracle, ot, q, weighted)
+            exp[q] = oracle.cosine_cm(ot[q], ot[q], weighted)
+            assert same(got, exp), q
+            assert t.similarity(q, (q + 1) % n) == exp[(q + 1) % n] or (
+                math.isnan(exp[(q + 1) % n]) and math.isnan(t.similarity(q, (q + 1) % n)))
+
+
+def test_inexact_norm_regime_matches_sequential_reference(oracle):
+    """Counters large enough that sum(c^2) >= 2^53: the reference's fp64 sums
+    round; the GPU switches to the reference's sequential order."""
+    n, d, w = 6, 3, 64
+    rng = np.random.Generator(np.random.PCG64(4))
+    rows = np.repeat(np.arange(n), 40)
+    keys = rng.integers(0, 1000, size=rows.size).astype(np.int64)
+    vals = rng.integers(2 ** 22, 2 ** 24, size=rows.size).astype(np.float32)
+    ot = oracle_table(oracle, n, d, w, 42, rows, keys, vals)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(rows, keys, vals)
+        t.finalize()
+        assert t.stats()["exact_norms"] == 0
+        assert same(t.read_counters(), ot)
+        for q in range(n):
+            exp = _oracle_row_sims(oracle, ot, q)
+            exp[q] = oracle.cosine_cm(ot[q], ot[q])
+            assert same(t.similarities(q, np.arange(n)), exp)
+
+
+def _collision_free_seed(oracle, keys, depth, width):
+    for seed in range(1, 10000):
+        a, b = oracle.hash_params(seed, depth)
+        h = oracle.hash_keys(a, b, width, np.array(keys, np.int64))
+        if all(len(set(h[:, r].tolist())) == len(keys) for r in range(depth)):
+            return seed
+    raise AssertionError
+
+
+def test_reference_kats_on_gpu(oracle):
+    """VectorSimilarityMeasuresTest (0.769846046 +- 1e-6) and ItemSimilarityJobTest
+    (0.45, 0.89 +- 0.01) through collision-free sketches on the GPU."""
+    va = [0, 2, 0, 0, 8, 3, 0, 6, 0, 1, 2, 2, 0]
+    vb = [3, 0, 0, 0, 7, 0, 2, 2, 1, 3, 2, 1, 1]
+    seed = _collision_free_seed(oracle, list(range(13)), 4, 1024)
+    with SketchTable(2, depth=4, width=1024, seed=seed) as t:
+        t.ingest(np.array([0] * 13 + [1] * 13), np.array(list(range(13)) * 2), np.array(va + vb, np.float32))
+        t.finalize()
+        assert abs(t.similarity(0, 1) - 0.769846046) < 1e-6
+    lines = ["2,1,1", "1,2,1", "3,4,1", "1,3,2", "2,3,1"]
+    users, items, prefs = zip(*[map(int, ln.split(",")) for ln in lines])
+    seed = _collision_free_seed(oracle, sorted(set(users)), 4, 1024)
+    with SketchTable(4, depth=4, width=1024, seed=seed, owner_ids=[1, 2, 3, 4]) as t:
+        t.ingest(np.array(items), np.array(users), np.array(prefs, np.float32))
+        t.finalize()
+        assert abs(t.similarity(1, 3) - 0.45) < 0.01
+        assert abs(t.similarity(2, 3) - 0.89) < 0.01
+        assert t.similarity(1, 3) == 1 / math.sqrt(5) or abs(t.similarity(1, 3) - 1 / math.sqrt(5)) < 1e-16
+
+
+def test_point_query(oracle):
+    n, d, w = 200, 4, 256
+    items, users = zipf_stream(3000, n, 50_000, seed=8)
+    ot = oracle_table(oracle, n, d, w, 42, items, users)
+    a, b = oracle.hash_params(42, d)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        for owner in [0, 5, 199]:
+            for key in [0, 1, int(users[0]), 2999, -4]:
+                assert t.point_query(owner, key) == oracle.sketch_get(ot[owner], a, b, key)
+
+
+def test_most_similar_top_users_semantics(oracle):
+    n, d, w = 600, 4, 128
+    items, users = zipf_stream(400, n, 60_000, seed=13)  # few users -> many ties / duplicates
+    ids = np.arange(n, dtype=np.int64) * 7 + 3
+    ot = oracle_table(oracle, n, d, w, 42, items, users)
+    with SketchTable(n, depth=d, width=w, seed=42, owner_ids=ids) as t:
+        t.ingest(ids[items], users)
+        t.finalize()
+        for q in [0, 1, 300, 599]:
+            for k in [1, 10, 100]:
+                sims = _oracle_row_sims(oracle, ot, q)
+                eids, esc = oracle.top_users(ids, sims, k)
+                gids, gsc = t.most_similar(int(ids[q]), k)
+                assert gids.tolist() == eids.tolist(), (q, k)
+                assert same(gsc, esc)
+        rows, sc, cnt = t.top_k_rows(0, 8, 20)
+        for q in range(8):
+            eids, _ = oracle.top_users(ids, _oracle_row_sims(oracle, ot, q), 20)
+            assert rows[q, :cnt[q]].tolist() == eids.tolist()
+
+
+def test_movielens_shape_config1(oracle):
+    """Config 1 shape: ML-100K stand-in, transposed (item sketches keyed by user),
+    d=4, w=1024, integer ratings; all pairs of 64 items + top-10 for 5 items."""
+    from mahout_amd.synth import movielens_like
+    users, items, ratings = movielens_like()
+    item_ids = np.unique(items)
+    rows = np.searchsorted(item_ids, items)
+    ot = oracle_table(oracle, item_ids.size, 4, 1024, 42, rows, users, ratings)
+    with SketchTable(item_ids.size, depth=4, width=1024, seed=42, owner_ids=item_ids) as t:
+        t.ingest(items, users, ratings)
+        t.finalize()
+        assert same(t.read_counters(), ot)
+        for q in range(0, 64):
+            exp = _oracle_row_sims(oracle, ot, q)
+            exp[q] = oracle.cosine_cm(ot[q], ot[q])
+            assert same(t.similarities(int(item_ids[q]), item_ids), exp)
+        for q in [0, 10, 500, 1000, item_ids.size - 1]:
+            eids, _ = oracle.top_users(item_ids, _oracle_row_sims(oracle, ot, q), 10)
+            assert t.most_similar(int(item_ids[q]), 10)[0].tolist() == eids.tolist()
+
+
+def test_bad_row_index_device_path():
+    import torch
+    with SketchTable(10, depth=2, width=64) as t:
+        rows = torch.tensor([0, 1, 10], dtype=torch.int64, device="cuda")
+        keys = torch.tensor([1, 2, 3], dtype=torch.int64, device="cuda")
+        t.ingest_device_rows(rows, keys, None, 3)
+        with pytest.raises(CmsError) as ei:
+            t.synchronize()
+        assert ei.value.code == CMS_E_PARAM
