@@ -296,11 +296,16 @@ int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const fl
   CMS_HIP(hipMemcpyAsync(h->ws_in_key.ptr, key, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
   if (val) CMS_HIP(hipMemcpyAsync(h->ws_in_val.ptr, val, sizeof(float) * n, hipMemcpyHostToDevice, h->stream));
   const bool by_id = !h->h_owner_ids.empty();
+  int rc;
   if (by_id) {
-    int rc = map_owner_ids(h, d_row, n, d_row);  // in place: each thread reads then writes its own slot
+    rc = map_owner_ids(h, d_row, n, d_row);  // in place: each thread reads then writes its own slot
     if (rc) return rc;
   }
-  int rc = ingest_coo_device(h, d_row, h->ws_in_key.as<int64_t>(), val ? h->ws_in_val.as<float>() : nullptr, n);
+  // all-or-nothing: reject unknown owners / bad increments before touching the table
+  if ((rc = validate_batch(h, by_id ? nullptr : d_row, val ? h->ws_in_val.as<float>() : nullptr, n))) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if ((rc = check_flags(h, by_id))) return rc;
+  rc = ingest_coo_device(h, d_row, h->ws_in_key.as<int64_t>(), val ? h->ws_in_val.as<float>() : nullptr, n);
   if (rc) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
   h->finalized = false;
@@ -338,8 +343,12 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
     CMS_HIP(hipMemcpyAsync(h->ws_in_key.ptr, keys, sizeof(int64_t) * np, hipMemcpyHostToDevice, h->stream));
   if (vals && np > 0)
     CMS_HIP(hipMemcpyAsync(h->ws_in_val.ptr, vals, sizeof(float) * np, hipMemcpyHostToDevice, h->stream));
-  int rc = ingest_csr_device(h, h->ws_in_row.as<int64_t>(), h->ws_in_key.as<int64_t>(),
-                             vals ? h->ws_in_val.as<float>() : nullptr, np);
+  int rc;
+  if (vals && (rc = validate_batch(h, nullptr, h->ws_in_val.as<float>(), np))) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if ((rc = check_flags(h, false))) return rc;
+  rc = ingest_csr_device(h, h->ws_in_row.as<int64_t>(), h->ws_in_key.as<int64_t>(),
+                         vals ? h->ws_in_val.as<float>() : nullptr, np);
   if (rc) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
   h->finalized = false;

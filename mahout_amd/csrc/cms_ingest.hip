@@ -173,7 +173,8 @@ int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d
 
 // ----------------------------------------------------- owner ID -> row --
 
-__global__ void k_map_ids(const int64_t* ids, int64_t n, const int64_t* sorted, int64_t nrows, int64_t* rows) {
+__global__ void k_map_ids(const int64_t* ids, int64_t n, const int64_t* sorted, int64_t nrows, int64_t* rows,
+                          uint32_t* flags) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t id = ids[i];
     int64_t lo = 0, hi = nrows;
@@ -182,14 +183,39 @@ __global__ void k_map_ids(const int64_t* ids, int64_t n, const int64_t* sorted, 
       if (sorted[mid] < id) lo = mid + 1;
       else hi = mid;
     }
-    rows[i] = (lo < nrows && sorted[lo] == id) ? lo : -1;
+    bool found = lo < nrows && sorted[lo] == id;
+    rows[i] = found ? lo : -1;
+    if (!found) atomicOr(flags, kFlagBadRow);
   }
+}
+
+// Pre-ingest validation of host-supplied batches (all-or-nothing ingest).
+__global__ void k_validate(const int64_t* rows, const float* val, int64_t n, int64_t nrows, uint32_t* flags) {
+  uint32_t f = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (rows) {
+      int64_t r = rows[i];
+      if (r < 0 || r >= nrows) f |= kFlagBadRow;
+    }
+    uint32_t inc;
+    if (val && !load_inc(val, i, inc)) f |= kFlagBadValue;
+  }
+  if (f) atomicOr(flags, f);
+}
+
+int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n) {
+  if (n <= 0 || (!d_rows && !d_val)) return CMS_OK;
+  unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_validate, dim3(grid), dim3(256), 0, h->stream, d_rows, d_val, n, h->n, h->d_flags);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
 }
 
 int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_rows) {
   if (n <= 0) return CMS_OK;
   unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_map_ids, dim3(grid), dim3(256), 0, h->stream, d_ids, n, h->d_owner_ids, h->n, d_rows);
+  hipLaunchKernelGGL(k_map_ids, dim3(grid), dim3(256), 0, h->stream, d_ids, n, h->d_owner_ids, h->n, d_rows,
+                     h->d_flags);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

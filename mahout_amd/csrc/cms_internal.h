@@ -118,6 +118,8 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
 // owner IDs -> rows by binary search over h->d_owner_ids.
 int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_rows);
 int compute_norms(cms_handle* h);
+// flags rows outside [0,n) and increments the counter type cannot hold.
+int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n);
 int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d_out);
 
 // ---- launchers (cms_query.hip) ----
