@@ -1,0 +1,283 @@
+// cms_build.hip -- LDS-staged sketch-row build (the sketch-update hot kernel).
+//
+// Input: CSR keys grouped by owner row (the DataModel layout, or the output of
+// the COO partition in cms_ingest.hip).  One workgroup builds one owner's
+// d x w sketch one sketch row at a time in LDS:
+//   - the owner's keys are read once (cached in registers across the d sketch
+//     rows when the owner has <= 1024 keys, otherwise streamed in batches of
+//     four loads per thread) and reduced mod p once;
+//   - every update of sketch row r is an LDS atomic add at h_r(key)
+//     (DoubleCountMinSketch.update, T/impl/common/DoubleCountMinSketch.java:72-80);
+//   - the finished row leaves LDS as 16-byte coalesced stores, the same pass
+//     zeroes the LDS slot for row r+1 and accumulates sum(c^2) (the valueA of
+//     DoubleCountMinSketch.cosine :131-138) -- so the table is written exactly
+//     once, zero fill included, and the norms cost no extra HBM pass.
+// Hot owners (more than kSlice keys) are split into slices built by separate
+// workgroups; a slice adds its LDS row into the (pre-zeroed) table row with
+// 256-byte coalesced atomics and a small pass derives the hot rows' norms.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "cms_device.h"
+#include "cms_internal.h"
+
+namespace cms {
+
+struct HotInfo {
+  int64_t row;
+  int32_t nslices;
+  int32_t pad;
+};
+
+constexpr int kKeyRegs = 4;  // keys cached per thread: owners up to 1024 keys are read once
+
+__global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
+                             int2* extra_map, uint32_t* counters /* [0]=hot rows [2]=extra slices */,
+                             uint64_t* norm, int depth) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t c = off[r + 1] - off[r];
+    if (c <= slice) {
+      row_hot[r] = -1;
+      continue;
+    }
+    int32_t ns = (int32_t)((c + slice - 1) / slice);
+    uint32_t hidx = atomicAdd(&counters[0], 1u);
+    uint32_t e0 = atomicAdd(&counters[2], (uint32_t)(ns - 1));
+    hot[hidx] = HotInfo{r, ns, 0};
+    row_hot[r] = (int32_t)hidx;
+    for (int32_t s = 1; s < ns; ++s) extra_map[e0 + s - 1] = make_int2((int)hidx, s);
+    for (int d = 0; d < depth; ++d) norm[r * depth + d] = 0;
+  }
+}
+
+// Zero the table rows of hot owners (bulk build only); grid (max_hot, depth).
+__global__ __launch_bounds__(256) void k_zero_hot(const HotInfo* hot, const uint32_t* counters, HashParams hp,
+                                                  uint32_t* table) {
+  if (blockIdx.x >= counters[0]) return;
+  const int64_t dw = (int64_t)hp.depth * hp.width;
+  uint32_t* p = table + hot[blockIdx.x].row * dw + (int64_t)blockIdx.y * hp.width;
+  for (int j = threadIdx.x; j < (int)hp.width; j += blockDim.x) p[j] = 0u;
+}
+
+// grid = emax + nrows: blocks [0, emax) build extra slices of hot owners (heavy
+// work first), blocks [emax, emax + nrows) one owner each (slice 0 if hot).
+__global__ __launch_bounds__(kBuildThreads) void k_build_rows(
+    const int64_t* off, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp, int64_t slice,
+    const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
+    uint32_t* table, uint64_t* row_mass, uint64_t* norm, uint32_t* flags, int accumulate) {
+  extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w]
+  __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
+  __shared__ unsigned long long s_mass;
+  const int w = (int)hp.width;
+  const int64_t dw = (int64_t)hp.depth * w;
+  const int tid = threadIdx.x;
+
+  int64_t row, lo, hi;
+  bool atomic_mode;
+  if (blockIdx.x < emax) {
+    if (blockIdx.x >= counters[2]) return;
+    int2 m = extra_map[blockIdx.x];
+    row = hot[m.x].row;
+    lo = off[row] + (int64_t)m.y * slice;
+    hi = min(off[row + 1], lo + slice);
+    atomic_mode = true;
+  } else {
+    row = (int64_t)blockIdx.x - emax;
+    lo = off[row];
+    atomic_mode = row_hot[row] >= 0;
+    hi = atomic_mode ? lo + slice : off[row + 1];
+  }
+  uint32_t* dst = table + row * dw;
+  const bool load_old = accumulate && !atomic_mode;
+  if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+  if (tid == 0) s_mass = 0ULL;
+
+  // keys of small owners: read and reduced once for all d sketch rows
+  const bool cached = (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs;
+  uint64_t kp[kKeyRegs];
+  uint32_t ik[kKeyRegs];
+  uint64_t mass = 0;
+  bool badv = false;
+  if (cached) {
+#pragma unroll
+    for (int k = 0; k < kKeyRegs; ++k) {
+      int64_t i = lo + tid + (int64_t)k * kBuildThreads;
+      kp[k] = 0;
+      ik[k] = 0;
+      if (i < hi) {
+        int64_t key = keys[i];
+        uint32_t inc;
+        if (!load_inc(vals, i, inc)) {
+          badv = true;
+          inc = 0;
+        }
+        kp[k] = reduce_key(key);
+        ik[k] = inc;
+        mass += inc;
+      }
+    }
+  }
+  // LDS slot for sketch row 0
+  if ((w & 3) == 0) {
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    const uint4* s4 = reinterpret_cast<const uint4*>(dst);
+    for (int j = tid; j < (w >> 2); j += kBuildThreads) l4[j] = load_old ? s4[j] : make_uint4(0, 0, 0, 0);
+  } else {
+    for (int j = tid; j < w; j += kBuildThreads) lds[j] = load_old ? dst[j] : 0u;
+  }
+  __syncthreads();
+
+  for (int d = 0; d < hp.depth; ++d) {
+    // ---- updates of sketch row d ----
+    if (cached) {
+#pragma unroll
+      for (int k = 0; k < kKeyRegs; ++k)
+        if (ik[k]) atomicAdd(&lds[bucket(hp, d, kp[k])], ik[k]);
+    } else {
+      for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
+        int64_t kk[4];
+        uint32_t inc4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int64_t i = base + tid + (int64_t)u * kBuildThreads;
+          kk[u] = i < hi ? keys[i] : 0;
+          inc4[u] = 0;
+          if (i < hi) {
+            uint32_t inc;
+            if (!load_inc(vals, i, inc)) {
+              badv = true;
+              inc = 0;
+            }
+            inc4[u] = inc;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (inc4[u]) atomicAdd(&lds[bucket(hp, d, reduce_key(kk[u]))], inc4[u]);
+          if (d == 0) mass += inc4[u];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- write-out of row d, zero/load the slot for row d+1, sum of squares ----
+    uint32_t* dst_d = dst + (int64_t)d * w;
+    const uint32_t* nxt = (load_old && d + 1 < hp.depth) ? dst + (int64_t)(d + 1) * w : nullptr;
+    if (atomic_mode) {
+      for (int j = tid; j < w; j += kBuildThreads) {
+        uint32_t v = lds[j];
+        lds[j] = 0u;
+        if (v) atomicAdd(dst_d + j, v);
+      }
+    } else {
+      uint64_t sq = 0;
+      if ((w & 3) == 0) {
+        uint4* l4 = reinterpret_cast<uint4*>(lds);
+        uint4* d4 = reinterpret_cast<uint4*>(dst_d);
+        const uint4* n4 = reinterpret_cast<const uint4*>(nxt);
+        for (int j = tid; j < (w >> 2); j += kBuildThreads) {
+          uint4 v = l4[j];
+          l4[j] = nxt ? n4[j] : make_uint4(0, 0, 0, 0);
+          d4[j] = v;
+          sq = sat_add(sq, (uint64_t)v.x * v.x);
+          sq = sat_add(sq, (uint64_t)v.y * v.y);
+          sq = sat_add(sq, (uint64_t)v.z * v.z);
+          sq = sat_add(sq, (uint64_t)v.w * v.w);
+        }
+      } else {
+        for (int j = tid; j < w; j += kBuildThreads) {
+          uint32_t v = lds[j];
+          lds[j] = nxt ? nxt[j] : 0u;
+          dst_d[j] = v;
+          sq = sat_add(sq, (uint64_t)v * v);
+        }
+      }
+      // per-thread sums stay far below 2^64 for counters < 2^26; anything at or
+      // above 2^53 only has to stay >= 2^53 (inexact regime), so clamp.
+      sq = wave_sum_u64_sat(sq);
+      if (sq > (1ULL << 60)) sq = 1ULL << 60;
+      if ((tid & 63) == 0) atomicAdd(&s_norm[d], (unsigned long long)sq);
+    }
+    __syncthreads();
+  }
+
+  if (badv) atomicOr(flags, kFlagBadValue);
+  mass = wave_sum_u64_sat(mass);
+  if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, (unsigned long long)mass);
+  __syncthreads();
+  if (!atomic_mode && tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+  if (tid == 0) {
+    uint64_t tm = s_mass;
+    if (!atomic_mode) {
+      uint64_t m = accumulate ? row_mass[row] + tm : tm;
+      row_mass[row] = m;
+      if (m >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+    } else if (tm) {
+      unsigned long long old = atomicAdd((unsigned long long*)&row_mass[row], (unsigned long long)tm);
+      if (old + tm >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+    }
+  }
+}
+
+// Sum of squares of the hot rows after every slice landed; grid (max_hot, depth, chunks of 1024).
+__global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uint32_t* counters, HashParams hp,
+                                                   const uint32_t* table, uint64_t* norm) {
+  __shared__ uint64_t red[4];
+  if (blockIdx.x >= counters[0]) return;
+  const int64_t row = hot[blockIdx.x].row;
+  const int d = blockIdx.y;
+  const int w = (int)hp.width;
+  const uint32_t* p = table + row * (int64_t)hp.depth * w + (int64_t)d * w;
+  uint64_t sq = 0;
+  for (int j = blockIdx.z * 1024 + threadIdx.x; j < min(w, (int)(blockIdx.z + 1) * 1024); j += 256)
+    sq = sat_add(sq, (uint64_t)p[j] * p[j]);
+  uint64_t tot = block_sum_u64_sat(sq, red);
+  if (tot > (1ULL << 60)) tot = 1ULL << 60;
+  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
+}
+
+int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs) {
+  const int64_t n = h->n;
+  const int accumulate = h->empty ? 0 : 1;
+  const int64_t max_hot = std::min<int64_t>(n, npairs / kSlice + 1);
+  const int64_t emax = npairs / kSlice + 1;
+  const size_t sz_rowhot = (sizeof(int32_t) * (size_t)n + 15) & ~size_t(15);
+  const size_t sz_hot = (sizeof(HotInfo) * (size_t)max_hot + 15) & ~size_t(15);
+  const size_t sz_extra = sizeof(int2) * (size_t)emax;
+  CMS_HIP(h->ws_hot.ensure(sz_rowhot + sz_hot + sz_extra + 64));
+  char* base = h->ws_hot.as<char>();
+  int32_t* row_hot = reinterpret_cast<int32_t*>(base);
+  HotInfo* hot = reinterpret_cast<HotInfo*>(base + sz_rowhot);
+  int2* extra_map = reinterpret_cast<int2*>(base + sz_rowhot + sz_hot);
+  uint32_t* counters = h->d_flags + 4;  // [4..7]
+  CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
+  {
+    TimedScope ts(h, "build_plan");
+    unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_off, n, kSlice, row_hot, hot, extra_map,
+                       counters, h->d_norm, h->p.depth);
+    if (!accumulate)
+      hipLaunchKernelGGL(k_zero_hot, dim3((unsigned)max_hot, (unsigned)h->p.depth), dim3(256), 0, h->stream, hot,
+                         counters, h->hp, h->d_table);
+    CMS_HIP(hipGetLastError());
+  }
+  const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
+  {
+    TimedScope ts(h, "build_rows");
+    hipLaunchKernelGGL(k_build_rows, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_off, d_key,
+                       d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->d_table, h->d_row_mass,
+                       h->d_norm, h->d_flags, accumulate);
+    CMS_HIP(hipGetLastError());
+  }
+  {
+    TimedScope ts(h, "hot_norms");
+    dim3 grid((unsigned)max_hot, (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
+    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->d_table, h->d_norm);
+    CMS_HIP(hipGetLastError());
+  }
+  h->empty = false;
+  h->norms_valid = true;  // build_rows + hot_norms wrote the norm of every row
+  return CMS_OK;
+}
+
+}  // namespace cms

@@ -1,0 +1,85 @@
+// cms_device.h -- wave64 / workgroup helpers shared by the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cms {
+
+// Increment of pair i: 1 for implicit streams, else the float preference,
+// which u32 counters accept only as a non-negative integer < 2^32.
+__device__ __forceinline__ bool load_inc(const float* val, int64_t i, uint32_t& inc) {
+  if (val == nullptr) {
+    inc = 1u;
+    return true;
+  }
+  float v = val[i];
+  if (!(v >= 0.0f) || v != floorf(v) || v >= 4294967296.0f) {
+    inc = 0u;
+    return false;
+  }
+  inc = (uint32_t)v;
+  return true;
+}
+
+__device__ __forceinline__ uint64_t sat_add(uint64_t a, uint64_t b) {
+  uint64_t s = a + b;
+  return s < a ? ~0ULL : s;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64_sat(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = sat_add(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Exclusive scan across the block; scratch needs (blockDim/64 + 1) words.
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* scratch, uint32_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t inc = wave_incl_scan_u32(v);
+  if (lane == 63) scratch[wid] = inc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int i = 0; i < nw; ++i) {
+      uint32_t t = scratch[i];
+      scratch[i] = s;
+      s += t;
+    }
+    scratch[nw] = s;
+  }
+  __syncthreads();
+  uint32_t res = inc - v + scratch[wid];
+  if (total) *total = scratch[nw];
+  __syncthreads();
+  return res;
+}
+
+// Block-wide saturating u64 sum; returns the sum in every thread.
+__device__ __forceinline__ uint64_t block_sum_u64_sat(uint64_t v, uint64_t* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum_u64_sat(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  uint64_t s = 0;
+  for (int i = 0; i < nw; ++i) s = sat_add(s, scratch[i]);
+  __syncthreads();
+  return s;
+}
+
+}  // namespace cms

@@ -42,7 +42,7 @@ struct PendingEvent {
 };
 
 // Row-build tuning: pairs per build work item.
-constexpr int64_t kSlice = 16384;
+constexpr int64_t kSlice = 32768;
 constexpr int kBuildThreads = 256;
 
 }  // namespace cms
@@ -121,6 +121,11 @@ int compute_norms(cms_handle* h);
 // flags rows outside [0,n) and increments the counter type cannot hold.
 int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n);
 int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d_out);
+int scan_exclusive_u32(cms_handle* h, const uint32_t* in, uint32_t* out, int64_t L, uint32_t* bsum);
+// ---- cms_partition.hip ----
+// COO -> CSR grouped by row; outputs live in handle scratch.
+int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
+                     int64_t** out_off, int64_t** out_key, float** out_val);
 
 // ---- launchers (cms_query.hip) ----
 int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);
