@@ -243,7 +243,8 @@ void cms_destroy(cms_handle* h) {
     if (b) (void)hipFree(b);
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
-                  &h->ws_hot, &h->ws_query, &h->ws_out};
+                  &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
+                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -445,6 +446,7 @@ int cms_finalize(cms_handle* h) {
   uint32_t inexact = 0;
   CMS_HIP(hipMemcpy(&inexact, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
   h->exact_norms = inexact == 0;
+  h->mfma_ready = false;
   h->finalized = true;
   return CMS_OK;
 }

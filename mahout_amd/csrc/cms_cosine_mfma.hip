@@ -1,0 +1,473 @@
+// cms_cosine_mfma.hip -- all-pairs sketch cosine on the gfx950 matrix cores.
+//
+// The table is a dense [n][d*w] matrix; DoubleCountMinSketch.cosine
+// (T/impl/common/DoubleCountMinSketch.java:114-149) needs, per sketch row r,
+// the dot product of two owners' w counters.  Those are d GEMMs with K = w,
+// run here as ONE MFMA pipeline whose K loop walks the d segments and runs an
+// fp64 epilogue at every segment boundary (den = sqrt(A)*sqrt(B), AB/den,
+// Math.min over rows, NaN when no row qualifies, normalizeWeightResult).
+//
+// Exactness: counters are split into 7-bit limbs (c = sum_k c_k 128^k), so
+// every product is an int8 x int8 MFMA with exact i32 accumulation
+// (127^2 * 32768 < 2^31).  Owners whose counters all fit one limb (almost
+// every owner of a Zipf stream) need one v_mfma_i32_32x32x32_i8 pass; tiles
+// touching multi-limb owners run the MULTI variant, which folds each limb
+// pair into an exact int64 dot.  The integer dot converted to double equals
+// the reference's fp64 valueAB whenever the norms are < 2^53, and the
+// epilogue performs the same correctly rounded IEEE operations as Java, so
+// the similarities are bit-identical.
+//
+// Tile: 128 x 128 outputs per 256-thread workgroup (2 x 2 waves, each 64 x 64
+// = 2 x 2 MFMA 32x32 tiles), K staged 128 bytes per row per stage through a
+// double-buffered, XOR-swizzled LDS image (conflict-free ds_read_b128).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <vector>
+
+#include "cms_device.h"
+#include "cms_internal.h"
+
+namespace cms {
+
+typedef int8_t i8x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTile = 128;      // output rows/cols per workgroup
+constexpr int kBK = 128;        // K bytes per stage
+constexpr int kMaxLimbs = 5;    // 35 bits >= any u32 counter
+
+// ------------------------------------------------------------ preparation --
+
+// Per owner: limb count, int8 limb 0, inexact flag, tile limb maxima.
+__global__ __launch_bounds__(256) void k_limb_prep(const uint32_t* table, int64_t nrows, int64_t dw,
+                                                   const uint64_t* norm, int depth, int8_t* limb0, uint8_t* rowL,
+                                                   int32_t* hot_list, uint32_t* hot_count,
+                                                   uint32_t* inexact_rows) {
+  __shared__ uint32_t smax[4];
+  const int64_t row = blockIdx.x;
+  const uint32_t* src = table + row * dw;
+  int8_t* dst = limb0 + row * dw;
+  uint32_t mx = 0;
+  for (int64_t j = threadIdx.x * 4; j < dw; j += 256 * 4) {
+    uint4 v = *reinterpret_cast<const uint4*>(src + j);
+    mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
+    char4 o = make_char4((signed char)(v.x & 127u), (signed char)(v.y & 127u), (signed char)(v.z & 127u),
+                         (signed char)(v.w & 127u));
+    *reinterpret_cast<char4*>(dst + j) = o;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+    int L = 1;
+    while (L < kMaxLimbs && (mx >> (7 * L)) != 0) ++L;
+    rowL[row] = (uint8_t)L;
+    if (L > 1) {
+      uint32_t h = atomicAdd(hot_count, 1u);
+      hot_list[h] = (int32_t)row;
+    }
+    bool inexact = false;
+    for (int d = 0; d < depth; ++d) inexact |= norm[row * depth + d] >= (1ULL << 53);
+    if (inexact) atomicAdd(inexact_rows, 1u);
+  }
+}
+
+// Higher limbs of multi-limb owners: hl[h][k-1][dw] = (c >> 7k) & 127.
+__global__ __launch_bounds__(256) void k_limb_hot(const uint32_t* table, int64_t dw, const int32_t* hot_list,
+                                                  int32_t* row_hot, int8_t* hl) {
+  const int h = blockIdx.x;
+  const int k = blockIdx.y + 1;
+  const int64_t row = hot_list[h];
+  if (threadIdx.x == 0 && k == 1) row_hot[row] = h;
+  const uint32_t* src = table + row * dw;
+  int8_t* dst = hl + ((int64_t)h * (kMaxLimbs - 1) + (k - 1)) * dw;
+  for (int64_t j = threadIdx.x; j < dw; j += 256) dst[j] = (int8_t)((src[j] >> (7 * k)) & 127u);
+}
+
+__global__ void k_tile_limbs(const uint8_t* rowL, int64_t nrows, uint8_t* tileL) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t r0 = t * kTile;
+  if (r0 >= nrows) return;
+  uint8_t m = 1;
+  for (int64_t r = r0; r < min(nrows, r0 + kTile); ++r) m = max(m, rowL[r]);
+  tileL[t] = m;
+}
+
+// ------------------------------------------------------------- the kernel --
+
+__device__ __forceinline__ double java_min_d(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+  return (a <= b) ? a : b;
+}
+
+// LDS image of one 128 x 128-byte operand tile: row-major rows of 128 B, the
+// 16-B chunk index XOR-swizzled with (row >> 1) & 7 so that every
+// ds_read_b128 lane group of the fragment reads hits 16 distinct slots.
+__device__ __forceinline__ int lds_off(int row, int ch) { return row * kBK + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+struct CosArgs {
+  const int8_t* limb0;      // [n][dw]
+  const int8_t* hl;         // [hot][kMaxLimbs-1][dw]
+  const int32_t* row_hot;   // [n] -> hot index or -1
+  const uint8_t* rowL;      // [n]
+  const uint8_t* tileL;     // [ceil(n/128)]
+  const double* nsqrt;      // [n][d]
+  int64_t n;
+  int64_t dw;
+  int32_t w;
+  int32_t depth;
+  int64_t q0;               // first query row of the slab
+  int64_t qcount;           // slab rows
+  int64_t ldo;              // slab row stride (= n)
+  double* out;              // [qcount][ldo]
+  int32_t weighted;
+  int32_t tiles_x;          // column tiles
+};
+
+__device__ int8_t g_zero16[16];  // source of the zero rows (past n, missing limbs)
+
+// One stage of one operand (128 rows x 128 B = 16 KiB) by direct global->LDS
+// loads: wave v, instruction u fills the 1 KiB (8 rows) at block 4v+u; lane i
+// lands at byte 16 i of it, i.e. row 8(4v+u) + i/8, slot i%8, so it fetches
+// chunk (i%8) ^ swz(row) -- the XOR swizzle lives on the source address and
+// the LDS image stays lane-linear (glds writes base + 16 * lane).
+__device__ __forceinline__ void stage_glds(const CosArgs& a, int64_t row0, int limb, int64_t koff,
+                                           unsigned char* buf) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int blk = wv * 4 + u;
+    const int row = blk * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    const int64_t grow = row0 + row;
+    const int8_t* src = g_zero16;
+    if (grow < a.n) {
+      if (limb == 0) src = a.limb0 + grow * a.dw + koff + ch * 16;
+      else if (a.rowL[grow] > limb)
+        src = a.hl + ((int64_t)a.row_hot[grow] * (kMaxLimbs - 1) + (limb - 1)) * a.dw + koff + ch * 16;
+    }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(buf + blk * 1024), 16, 0, 0);
+  }
+}
+
+// Single-limb operand stage through a per-tile buffer descriptor: SGPR base
+// (the tile's first row), 32-bit lane offsets, K offset in soffset; rows past
+// n fall outside num_records and land as zeros.
+struct TileSrc {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int32_t voff[4];
+};
+
+__device__ __forceinline__ TileSrc tile_src(const CosArgs& a, int64_t row0) {
+  TileSrc t;
+  const int64_t rows = max<int64_t>(0, min<int64_t>(kTile, a.n - row0));
+  const int8_t* base = a.limb0 + row0 * a.dw;
+  t.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rows * a.dw), 0x00020000);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int row = (wv * 4 + u) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    t.voff[u] = (int32_t)(row * a.dw) + ch * 16;
+  }
+  return t;
+}
+
+__device__ __forceinline__ void stage_buf(const TileSrc& t, int32_t koff, unsigned char* buf) {
+  const int wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(t.rsrc, (__attribute__((address_space(3))) void*)(buf + (wv * 4 + u) * 1024),
+                                             16, t.voff[u], koff, 0, 0);
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(256, MULTI ? 1 : 2) void k_cosine_tile(CosArgs a, const int2* tile_list,
+                                                                   int32_t tile_count) {
+  extern __shared__ __align__(16) unsigned char lds[];  // [2 buffers][A 16K | B 16K] + sqrt norms
+  double* s_sa = reinterpret_cast<double*>(lds + 4 * kTile * kBK);
+  double* s_sb = s_sa + kTile;
+  int64_t trow, tcol;
+  if (tile_list) {
+    if ((int)blockIdx.x >= tile_count) return;
+    int2 t = tile_list[blockIdx.x];
+    trow = t.y;
+    tcol = t.x;
+  } else {
+    tcol = blockIdx.x;
+    trow = blockIdx.y;
+  }
+  const int64_t row0 = a.q0 + trow * kTile;  // A rows (queries)
+  const int64_t col0 = tcol * kTile;         // B rows (candidates)
+  const int LA = MULTI ? a.tileL[row0 / kTile] : 1;
+  const int LB = MULTI ? a.tileL[col0 / kTile] : 1;
+  if (!MULTI && !tile_list && (a.tileL[row0 / kTile] > 1 || a.tileL[col0 / kTile] > 1)) return;  // MULTI's job
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int w = a.w;
+  const int cstages = w / kBK;
+  const int npairs = LA * LB;
+  const int total = a.depth * npairs * cstages;
+
+  i32x16 acc[2][2];
+  int64_t dot[MULTI ? 2 : 1][MULTI ? 2 : 1][MULTI ? 16 : 1];
+  double mn[2][2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        acc[i][j][e] = 0;
+        mn[i][j][e] = DBL_MAX;
+      }
+    }
+  if constexpr (MULTI) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dot[i][j][e] = 0;
+  }
+
+  auto decode = [&](int s, int& r, int& la, int& lb, int& cs) {
+    cs = s % cstages;
+    int t = s / cstages;
+    int p = t % npairs;
+    r = t / npairs;
+    la = p / LB;
+    lb = p % LB;
+  };
+
+  TileSrc srcA, srcB;
+  if constexpr (!MULTI) {
+    srcA = tile_src(a, row0);
+    srcB = tile_src(a, col0);
+  }
+  auto stage = [&](int s_, unsigned char* dstbuf) {
+    int r_, la_, lb_, cs_;
+    decode(s_, r_, la_, lb_, cs_);
+    const int32_t koff = r_ * w + cs_ * kBK;
+    if constexpr (MULTI) {
+      stage_glds(a, row0, la_, koff, dstbuf);
+      stage_glds(a, col0, lb_, koff, dstbuf + kTile * kBK);
+    } else {
+      stage_buf(srcA, koff, dstbuf);
+      stage_buf(srcB, koff, dstbuf + kTile * kBK);
+    }
+  };
+  stage(0, lds);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int s = 0; s < total; ++s) {
+    const int buf = s & 1;
+    unsigned char* A = lds + buf * (2 * kTile * kBK);
+    unsigned char* B = A + kTile * kBK;
+    int r, la, lb, cs;
+    decode(s, r, la, lb, cs);
+    if (s + 1 < total) stage(s + 1, lds + (buf ^ 1) * (2 * kTile * kBK));  // prefetch into the free buffer
+    // ---- 4 K-steps of 32 bytes, 2 x 2 MFMA tiles per wave ----
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int ch = 2 * ks + (lane >> 5);
+      i8x16 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wr * 64 + i * 32 + (lane & 31);
+        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off(row, ch));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wc * 64 + j * 32 + (lane & 31);
+        fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off(col, ch));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    const bool epilogue = cs == cstages - 1 && la == LA - 1 && lb == LB - 1;
+    if (epilogue) {  // sqrt norms of this tile's rows/cols for sketch row r
+      const int t = threadIdx.x & (kTile - 1);
+      const int64_t g = (threadIdx.x < kTile ? row0 : col0) + t;
+      const double v = g < a.n ? a.nsqrt[g * a.depth + r] : 0.0;
+      (threadIdx.x < kTile ? s_sa : s_sb)[t] = v;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage s+1 landed (LDS-DMA counts on vmcnt)
+    __syncthreads();
+
+    if (cs == cstages - 1) {
+      if constexpr (MULTI) {
+        const int sh = 7 * (la + lb);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              dot[i][j][e] += (int64_t)acc[i][j][e] << sh;
+              acc[i][j][e] = 0;
+            }
+      }
+      if (la == LA - 1 && lb == LB - 1) {
+        // ---- fp64 epilogue of sketch row r (DoubleCountMinSketch.java:143-147) ----
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const double sb = s_sb[wc * 64 + j * 32 + (lane & 31)];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const double sa = s_sa[wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)];
+              double valueAB;
+              if constexpr (MULTI) {
+                valueAB = (double)dot[i][j][e];
+                dot[i][j][e] = 0;
+              } else {
+                valueAB = (double)acc[i][j][e];
+                acc[i][j][e] = 0;
+              }
+              const double den = __dmul_rn(sa, sb);
+              if (den != 0.0) mn[i][j][e] = java_min_d(mn[i][j][e], __ddiv_rn(valueAB, den));
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ---- write the slab: NaN when no row qualified, then normalizeWeightResult ----
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t gcol = col0 + wc * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t grow = row0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (grow >= a.q0 + a.qcount || gcol >= a.n) continue;
+        double rr = mn[i][j][e] == DBL_MAX ? __builtin_nan("") : mn[i][j][e];
+        if (rr == rr) {
+          if (a.weighted) rr = rr < 0.0 ? -1.0 : 1.0;  // scaleFactor 1 - 1/(0+1) = 0
+          if (rr < -1.0) rr = -1.0;
+          else if (rr > 1.0) rr = 1.0;
+        }
+        a.out[(grow - a.q0) * a.ldo + gcol] = rr;
+      }
+    }
+}
+
+// ---------------------------------------------------------------- driver --
+
+int cosine_prepare(cms_handle* h) {
+  if (h->mfma_ready) return CMS_OK;
+  const int64_t n = h->n, dw = h->dw;
+  const int64_t ntiles = (n + kTile - 1) / kTile;
+  CMS_HIP(h->ws_limb0.ensure((size_t)n * (size_t)dw));
+  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (1 + 4) + (size_t)ntiles + 4 * sizeof(uint32_t) + 64));
+  char* meta = h->ws_limbmeta.as<char>();
+  uint8_t* rowL = reinterpret_cast<uint8_t*>(meta);
+  int32_t* row_hot = reinterpret_cast<int32_t*>(meta + ((n + 15) & ~int64_t(15)));
+  uint8_t* tileL = reinterpret_cast<uint8_t*>(row_hot + n);
+  uint32_t* cnt = h->d_flags + 8;  // [8]=hot rows [9]=inexact rows
+  int32_t* hot_list = row_hot;     // reuse: filled by k_limb_prep, consumed by k_limb_hot
+  CMS_HIP(h->ws_hotlist.ensure(sizeof(int32_t) * (size_t)n));
+  hot_list = h->ws_hotlist.as<int32_t>();
+  CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
+  CMS_HIP(hipMemsetAsync(row_hot, 0xFF, sizeof(int32_t) * (size_t)n, h->stream));
+  {
+    TimedScope ts(h, "limb_prep");
+    hipLaunchKernelGGL(k_limb_prep, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, n, dw, h->d_norm,
+                       h->p.depth, h->ws_limb0.as<int8_t>(), rowL, hot_list, cnt, cnt + 1);
+    hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowL, n, tileL);
+    CMS_HIP(hipGetLastError());
+  }
+  uint32_t counts[2];
+  CMS_HIP(hipMemcpyAsync(counts, cnt, sizeof(counts), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  h->n_hot_limb = counts[0];
+  h->n_inexact_rows = counts[1];
+  if (counts[0] > 0) {
+    CMS_HIP(h->ws_limbhot.ensure((size_t)counts[0] * (kMaxLimbs - 1) * (size_t)dw));
+    hipLaunchKernelGGL(k_limb_hot, dim3(counts[0], kMaxLimbs - 1), dim3(256), 0, h->stream, h->d_table, dw, hot_list,
+                       row_hot, h->ws_limbhot.as<int8_t>());
+    CMS_HIP(hipGetLastError());
+  }
+  h->tile_limbs.resize(ntiles);
+  CMS_HIP(hipMemcpyAsync(h->tile_limbs.data(), tileL, ntiles, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  h->mfma_ready = true;
+  return CMS_OK;
+}
+
+bool mfma_eligible(cms_handle* h) { return (h->p.width % kBK) == 0; }
+
+// Similarities of query rows [q0, q0+qc) against every owner into slab
+// [qc][n] (fp64, column = row index).  q0 must be a multiple of kTile.
+int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
+  int rc = cosine_prepare(h);
+  if (rc) return rc;
+  const int64_t n = h->n, dw = h->dw;
+  char* meta = h->ws_limbmeta.as<char>();
+  CosArgs a;
+  a.limb0 = h->ws_limb0.as<int8_t>();
+  a.hl = h->n_hot_limb ? h->ws_limbhot.as<int8_t>() : nullptr;
+  a.rowL = reinterpret_cast<uint8_t*>(meta);
+  a.row_hot = reinterpret_cast<int32_t*>(meta + ((n + 15) & ~int64_t(15)));
+  a.tileL = reinterpret_cast<uint8_t*>(const_cast<int32_t*>(a.row_hot) + n);
+  a.nsqrt = h->d_norm_sqrt;
+  a.n = n;
+  a.dw = dw;
+  a.w = h->p.width;
+  a.depth = h->p.depth;
+  a.q0 = q0;
+  a.qcount = qc;
+  a.ldo = n;
+  a.out = d_out;
+  a.weighted = h->p.weighting == CMS_WEIGHTED;
+  const int64_t ntiles = (n + kTile - 1) / kTile;
+  const int64_t trows = (qc + kTile - 1) / kTile;
+  a.tiles_x = (int)ntiles;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_cosine_tile<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_cosine_tile<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  const size_t lds = 4 * kTile * kBK + 2 * kTile * sizeof(double);  // 2 buffers x (A + B) + norms
+  {
+    TimedScope ts(h, "cosine_mfma");
+    hipLaunchKernelGGL(k_cosine_tile<false>, dim3((unsigned)ntiles, (unsigned)trows), dim3(256), lds, h->stream, a,
+                       (const int2*)nullptr, 0);
+    CMS_HIP(hipGetLastError());
+  }
+  // tiles touching a multi-limb owner
+  std::vector<int2> multi;
+  for (int64_t tr = 0; tr < trows; ++tr)
+    for (int64_t tc = 0; tc < ntiles; ++tc)
+      if (h->tile_limbs[(q0 / kTile) + tr] > 1 || h->tile_limbs[tc] > 1) multi.push_back(make_int2((int)tc, (int)tr));
+  if (!multi.empty()) {
+    CMS_HIP(h->ws_tiles.ensure(sizeof(int2) * multi.size()));
+    CMS_HIP(hipMemcpyAsync(h->ws_tiles.ptr, multi.data(), sizeof(int2) * multi.size(), hipMemcpyHostToDevice,
+                           h->stream));
+    TimedScope ts(h, "cosine_mfma_multi");
+    hipLaunchKernelGGL(k_cosine_tile<true>, dim3((unsigned)multi.size()), dim3(256), lds, h->stream, a,
+                       h->ws_tiles.as<int2>(), (int32_t)multi.size());
+    CMS_HIP(hipGetLastError());
+    CMS_HIP(hipStreamSynchronize(h->stream));  // the host tile list must outlive the copy
+  }
+  return CMS_OK;
+}
+
+}  // namespace cms

@@ -303,10 +303,37 @@ __global__ __launch_bounds__(kTopThreads) void k_top_k(const double* scores, int
   if (threadIdx.x == 0) counts[q] = (int32_t)kk;
 }
 
+int top_k_slab(cms_handle* h, const double* slab, int64_t ld, int64_t first_row, int64_t count, int32_t k,
+               int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  TimedScope ts(h, "top_k");
+  hipLaunchKernelGGL(k_top_k, dim3((unsigned)count), dim3(kTopThreads), 0, h->stream, slab, ld, h->n, k, first_row,
+                     h->d_owner_ids, d_ids, d_scores, d_counts);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts) {
   if (k < 1 || k > kTopMax) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kTopMax);
   const int64_t n = h->n;
+  int rc = CMS_OK;
+  if (mfma_eligible(h) && (rc = cosine_prepare(h))) return rc;
+  if (mfma_eligible(h) && h->n_inexact_rows == 0) {
+    // all-pairs MFMA slab for 128-aligned query blocks, then top-k per row
+    const int64_t a0 = row_begin / 128 * 128, a1 = row_begin + row_count;
+    const int64_t qb = std::max<int64_t>(128, ((int64_t(1) << 28) / std::max<int64_t>(1, n)) / 128 * 128);
+    CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(std::min(qb, a1 - a0) * n)));
+    for (int64_t q0 = a0; q0 < a1; q0 += qb) {
+      const int64_t qc = std::min(qb, a1 - q0);
+      rc = cosine_slab(h, q0, qc, h->ws_slab.as<double>());
+      if (rc) return rc;
+      const int64_t f0 = std::max(q0, row_begin), f1 = std::min(q0 + qc, a1);
+      rc = top_k_slab(h, h->ws_slab.as<double>() + (f0 - q0) * n, n, f0, f1 - f0, k, d_ids + (f0 - row_begin) * k,
+                      d_scores + (f0 - row_begin) * k, d_counts + (f0 - row_begin));
+      if (rc) return rc;
+    }
+    return CMS_OK;
+  }
   // rows of the score slab per batch, bounded to ~1 GiB of fp64 scores
   int64_t qb = std::max<int64_t>(1, std::min<int64_t>(row_count, (int64_t(1) << 27) / std::max<int64_t>(1, n)));
   CMS_HIP(h->ws_out.ensure(sizeof(double) * (size_t)(qb * n)));

@@ -258,3 +258,29 @@ def test_bad_row_index_device_path():
         with pytest.raises(CmsError) as ei:
             t.synchronize()
         assert ei.value.code == CMS_E_PARAM
+
+
+@pytest.mark.parametrize("n,d,w,vmax,seed", [(700, 5, 256, 5, 31), (260, 4, 128, 50, 32), (129, 3, 512, 1, 33)])
+def test_all_pairs_mfma_every_similarity(oracle, n, d, w, vmax, seed):
+    """cms_top_k_rows with k = n-1 returns every other owner sorted by
+    (similarity desc, ID asc): the whole similarity matrix through the
+    int8-limb MFMA kernels (single- and multi-limb tiles), bit for bit."""
+    items, users = zipf_stream(3000, n, 300_000, seed=seed)
+    vals = np.random.Generator(np.random.PCG64(seed)).integers(1, vmax + 1, size=items.size).astype(np.float32)
+    ot = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        k = min(n - 1, 1024)
+        rows = list(range(0, n, max(1, n // 37))) + [n - 1]
+        ids, sc, cnt = t.top_k_rows(5, n - 5, k)  # unaligned query start
+        for q in rows:
+            if q < 5:
+                continue
+            sims = _oracle_row_sims(oracle, ot, q)
+            eids, esc = oracle.top_users(np.arange(n), sims, k)
+            got_ids = ids[q - 5, :cnt[q - 5]]
+            assert got_ids.tolist() == eids.tolist(), q
+            assert same(sc[q - 5, :cnt[q - 5]], esc), q
+    if vmax > 1:
+        assert ot.max() > 127  # multi-limb owners were exercised
