@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--width", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the CSR and cosine side measurements")
+    ap.add_argument("--no-cosine-1m", action="store_true", help="skip the 1M-item all-pairs measurement")
     return ap.parse_args()
 
 
@@ -98,6 +99,61 @@ def cpu_baseline(off_d, keys_d, args, budget_s=12.0):
     return {"value": upd / dt, "unit": "updates/s", "cores": 1, "kind": "port",
             "sample": f"{rows_done} owner sketches ({upd} updates) of the rank-0 config-2 stream in owner-ID order, "
                       f"{dt:.1f} s; fp64 DoubleCountMinSketch rebuilt per owner + 128-bit BigInteger-equivalent hash"}
+
+
+INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense peak), MI355X_MICROARCH.md
+
+
+def allpairs_measure(table, row_begin, row_count, k, n, d, w):
+    """cms_top_k_rows over [row_begin, row_begin+row_count): every query row
+    against all n owners (n^2-shaped slab, no symmetry), HIP-event kernel times."""
+    table.set_timing(True)
+    table.top_k_rows(row_begin, min(row_count, 128), k)  # operands prepared, kernels warm
+    table.reset_timing()
+    t0 = time.perf_counter()
+    _, _, cnt = table.top_k_rows(row_begin, row_count, k)
+    wall = time.perf_counter() - t0
+    mf, nf = table.timing("cosine_mfma")
+    mm, nm = table.timing("cosine_mfma_multi")
+    tk, _ = table.timing("top_k")
+    table.set_timing(False)
+    pairs = row_count * n
+    ops = pairs * 2 * d * w
+    kern_s = (mf + mm) * 1e-3
+    return {
+        "query_rows": row_count, "candidates": n, "k": k, "wall_s": wall,
+        "ordered_pairs_per_s": pairs / wall,
+        "unique_item_pair_cosines_per_s": pairs / 2 / wall,
+        "mfma_ms": mf, "mfma_multi_limb_ms": mm, "multi_limb_launches": nm, "top_k_ms": tk,
+        "mfma_TOPS": ops / kern_s / 1e12 if kern_s else None,
+        "mfma_frac_int8_peak": ops / kern_s / 1e12 / INT8_MFMA_PEAK_TOPS if kern_s else None,
+        "returned_full_lists": int((cnt == k).sum()),
+    }
+
+
+def cosine_1m(args, local, device, q=2048):
+    """Config 4 shape: 1M item sketches, d=5 w=8192 (the config-3 table built
+    on one GPU from a 500M-pair Zipf stream), top-100 for q query items
+    against all 1M items through the MFMA all-pairs kernels."""
+    from mahout_amd import SketchTable
+    from mahout_amd.synth import zipf_stream_torch
+    n, d, w, npairs = 1_000_000, 5, 8192, 500_000_000
+    t = SketchTable(n, depth=d, width=w, seed=42, device=local)
+    items, users = zipf_stream_torch(10_000_000, n, npairs, seed=20261016, device=device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    t.ingest_device_rows(items, users, None, npairs)
+    t.finalize()
+    ingest_s = time.perf_counter() - t0
+    del items, users
+    torch.cuda.empty_cache()
+    t.release_scratch()
+    res = allpairs_measure(t, n // 2, q, 100, n, d, w)
+    res["workload"] = (f"config 4: top-100 of {q} query items vs all {n} items, d={d} w={w} "
+                       f"(table from a {npairs}-pair config-3 Zipf stream on 1 GPU)")
+    res["config3_ingest_1gpu_s"] = ingest_s
+    t.close()
+    return res
 
 
 def main():
@@ -224,19 +280,17 @@ def main():
         dt = time.perf_counter() - t0
         extras["csr_updates_per_s"] = npairs * args.steps / dt
         extras["csr_ms_per_step"] = dt * 1e3 / args.steps
-        # sketch-cosine (v1 pair kernel, exact fp64 epilogue): 8 owners vs all owners
-        q = 8
-        ids = np.arange(n, dtype=np.int64)
-        table.similarities(0, ids)
-        t0 = time.perf_counter()
-        for r in range(q):
-            table.similarities(r, ids)
-        dt = time.perf_counter() - t0
-        extras["pair_kernel_cosines_per_s"] = q * n / dt
+        # all-pairs top-100 over the config-2 table (int8-limb MFMA + exact fp64 epilogue)
+        extras["allpairs_top100_cfg2"] = allpairs_measure(table, 0, n, 100, n, d, w)
         result["extras"] = extras
-
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(off, ckeys, args)
+    if rank == 0 and not args.no_cosine_1m:
+        del off, ckeys
+        table.close()
+        del items, users
+        torch.cuda.empty_cache()
+        result["cosine"] = cosine_1m(args, local, device)
     if rank == 0:
         print(json.dumps(result))
     table.close()

@@ -123,6 +123,11 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
 /* Forget all counters (next ingest rebuilds the table from zero). */
 int cms_reset(cms_handle* h);
 
+/* Return the handle's ingest/query scratch to the device allocator (the
+ * table, norms and the all-pairs operands stay).  For 288 GB budgets: a
+ * 1M-owner d=5 w=8192 table is 164 GB on its own. */
+int cms_release_scratch(cms_handle* h);
+
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ----------------------
  * The interaction stream is sharded by key (user) hash; each rank ingests its
  * shard into a full-shape partial table and cms_finalize sums the tables with

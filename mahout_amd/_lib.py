@@ -30,7 +30,8 @@ CMS_WEIGHTED = 1
 EXPORTS = [
     "cms_params_init", "cms_shape_from_delta_epsilon", "cms_create", "cms_destroy", "cms_last_error",
     "cms_abi_version", "cms_set_owner_ids", "cms_hash_params", "cms_hash_keys", "cms_ingest",
-    "cms_ingest_device_rows", "cms_ingest_csr", "cms_ingest_csr_device", "cms_reset", "cms_comm_unique_id",
+    "cms_ingest_device_rows", "cms_ingest_csr", "cms_ingest_csr_device", "cms_reset", "cms_release_scratch",
+    "cms_comm_unique_id",
     "cms_comm_init", "cms_shard_of_key", "cms_finalize", "cms_synchronize", "cms_similarity", "cms_similarities",
     "cms_point_query", "cms_most_similar", "cms_top_k_rows", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
@@ -84,6 +85,7 @@ _SIGS = {
     "cms_ingest_csr": (_int, [_vp, _vp, _vp, _vp]),
     "cms_ingest_csr_device": (_int, [_vp, _vp, _vp, _vp]),
     "cms_reset": (_int, [_vp]),
+    "cms_release_scratch": (_int, [_vp]),
     "cms_comm_unique_id": (_int, [_vp]),
     "cms_comm_init": (_int, [_vp, _vp, _i32, _i32]),
     "cms_shard_of_key": (_i32, [_i64, _i32]),

@@ -40,22 +40,17 @@ constexpr int kMaxLimbs = 5;    // 35 bits >= any u32 counter
 
 // ------------------------------------------------------------ preparation --
 
-// Per owner: limb count, int8 limb 0, inexact flag, tile limb maxima.
-__global__ __launch_bounds__(256) void k_limb_prep(const uint32_t* table, int64_t nrows, int64_t dw,
-                                                   const uint64_t* norm, int depth, int8_t* limb0, uint8_t* rowL,
-                                                   int32_t* hot_list, uint32_t* hot_count,
-                                                   uint32_t* inexact_rows) {
+// Per owner row: limb count (max counter), multi-limb flag, inexact-norm count.
+__global__ __launch_bounds__(256) void k_limb_count(const uint32_t* table, int64_t dw, const uint64_t* norm,
+                                                    int depth, uint8_t* rowL, uint32_t* multi_flag,
+                                                    uint32_t* inexact_rows) {
   __shared__ uint32_t smax[4];
   const int64_t row = blockIdx.x;
   const uint32_t* src = table + row * dw;
-  int8_t* dst = limb0 + row * dw;
   uint32_t mx = 0;
   for (int64_t j = threadIdx.x * 4; j < dw; j += 256 * 4) {
     uint4 v = *reinterpret_cast<const uint4*>(src + j);
     mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
-    char4 o = make_char4((signed char)(v.x & 127u), (signed char)(v.y & 127u), (signed char)(v.z & 127u),
-                         (signed char)(v.w & 127u));
-    *reinterpret_cast<char4*>(dst + j) = o;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
@@ -66,26 +61,43 @@ __global__ __launch_bounds__(256) void k_limb_prep(const uint32_t* table, int64_
     int L = 1;
     while (L < kMaxLimbs && (mx >> (7 * L)) != 0) ++L;
     rowL[row] = (uint8_t)L;
-    if (L > 1) {
-      uint32_t h = atomicAdd(hot_count, 1u);
-      hot_list[h] = (int32_t)row;
-    }
+    multi_flag[row] = L > 1 ? 1u : 0u;
     bool inexact = false;
     for (int d = 0; d < depth; ++d) inexact |= norm[row * depth + d] >= (1ULL << 53);
     if (inexact) atomicAdd(inexact_rows, 1u);
   }
 }
 
-// Higher limbs of multi-limb owners: hl[h][k-1][dw] = (c >> 7k) & 127.
-__global__ __launch_bounds__(256) void k_limb_hot(const uint32_t* table, int64_t dw, const int32_t* hot_list,
-                                                  int32_t* row_hot, int8_t* hl) {
-  const int h = blockIdx.x;
-  const int k = blockIdx.y + 1;
-  const int64_t row = hot_list[h];
-  if (threadIdx.x == 0 && k == 1) row_hot[row] = h;
-  const uint32_t* src = table + row * dw;
-  int8_t* dst = hl + ((int64_t)h * (kMaxLimbs - 1) + (k - 1)) * dw;
-  for (int64_t j = threadIdx.x; j < dw; j += 256) dst[j] = (int8_t)((src[j] >> (7 * k)) & 127u);
+// Stable multi-first permutation from the exclusive scan of the multi flags.
+__global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, const uint8_t* rowL, int64_t nrows,
+                            int64_t n_multi, int64_t* perm, int64_t* inv, uint8_t* rowLp) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = multi_flag[r] ? (int64_t)mpos[r] : n_multi + (r - (int64_t)mpos[r]);
+    perm[p] = r;
+    inv[r] = p;
+    rowLp[p] = rowL[r];
+  }
+}
+
+// Limb images in permuted order: limb0[p] = c & 127 for every owner;
+// hl[p][k-1] = (c >> 7k) & 127 for the multi-limb prefix p < n_multi.
+__global__ __launch_bounds__(256) void k_limb_write(const uint32_t* table, int64_t dw, const int64_t* perm,
+                                                    const uint8_t* rowLp, int64_t n_multi, int8_t* limb0, int8_t* hl) {
+  const int64_t p = blockIdx.x;
+  const uint32_t* src = table + perm[p] * dw;
+  int8_t* dst = limb0 + p * dw;
+  const int L = p < n_multi ? rowLp[p] : 1;
+  for (int64_t j = threadIdx.x * 4; j < dw; j += 256 * 4) {
+    uint4 v = *reinterpret_cast<const uint4*>(src + j);
+    *reinterpret_cast<char4*>(dst + j) = make_char4((signed char)(v.x & 127u), (signed char)(v.y & 127u),
+                                                    (signed char)(v.z & 127u), (signed char)(v.w & 127u));
+    for (int k = 1; k < L; ++k) {
+      const int sh = 7 * k;
+      *reinterpret_cast<char4*>(hl + (p * (kMaxLimbs - 1) + (k - 1)) * dw + j) =
+          make_char4((signed char)((v.x >> sh) & 127u), (signed char)((v.y >> sh) & 127u),
+                     (signed char)((v.z >> sh) & 127u), (signed char)((v.w >> sh) & 127u));
+    }
+  }
 }
 
 __global__ void k_tile_limbs(const uint8_t* rowL, int64_t nrows, uint8_t* tileL) {
@@ -110,13 +122,17 @@ __device__ __forceinline__ double java_min_d(double a, double b) {
 // ds_read_b128 lane group of the fragment reads hits 16 distinct slots.
 __device__ __forceinline__ int lds_off(int row, int ch) { return row * kBK + ((ch ^ ((row >> 1) & 7)) << 4); }
 
+// Operands live in PERMUTED order: multi-limb owners first (positions
+// [0, n_multi)), then the single-limb ones, each group in row order, so the
+// multi-limb tiles are the first ceil(n_multi/128) row/column tiles only.
 struct CosArgs {
-  const int8_t* limb0;      // [n][dw]
-  const int8_t* hl;         // [hot][kMaxLimbs-1][dw]
-  const int32_t* row_hot;   // [n] -> hot index or -1
-  const uint8_t* rowL;      // [n]
-  const uint8_t* tileL;     // [ceil(n/128)]
-  const double* nsqrt;      // [n][d]
+  const int8_t* limb0;      // [n][dw]   limb 0 of perm[p]
+  const int8_t* hl;         // [n_multi][kMaxLimbs-1][dw]  limbs 1.. of perm[p]
+  const int64_t* perm;      // [n] permuted position -> owner row
+  const uint8_t* rowL;      // [n] limb count of perm[p]
+  const uint8_t* tileL;     // [ceil(n/128)] max limb count of a permuted tile
+  const double* nsqrt;      // [n][d] by owner row
+  int64_t n_multi;
   int64_t n;
   int64_t dw;
   int32_t w;
@@ -148,8 +164,8 @@ __device__ __forceinline__ void stage_glds(const CosArgs& a, int64_t row0, int l
     const int8_t* src = g_zero16;
     if (grow < a.n) {
       if (limb == 0) src = a.limb0 + grow * a.dw + koff + ch * 16;
-      else if (a.rowL[grow] > limb)
-        src = a.hl + ((int64_t)a.row_hot[grow] * (kMaxLimbs - 1) + (limb - 1)) * a.dw + koff + ch * 16;
+      else if (grow < a.n_multi && a.rowL[grow] > limb)
+        src = a.hl + (grow * (kMaxLimbs - 1) + (limb - 1)) * a.dw + koff + ch * 16;
     }
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(buf + blk * 1024), 16, 0, 0);
@@ -299,7 +315,7 @@ __global__ __launch_bounds__(256, MULTI ? 1 : 2) void k_cosine_tile(CosArgs a, c
     if (epilogue) {  // sqrt norms of this tile's rows/cols for sketch row r
       const int t = threadIdx.x & (kTile - 1);
       const int64_t g = (threadIdx.x < kTile ? row0 : col0) + t;
-      const double v = g < a.n ? a.nsqrt[g * a.depth + r] : 0.0;
+      const double v = g < a.n ? a.nsqrt[a.perm[g] * a.depth + r] : 0.0;
       (threadIdx.x < kTile ? s_sa : s_sb)[t] = v;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage s+1 landed (LDS-DMA counts on vmcnt)
@@ -373,57 +389,77 @@ int cosine_prepare(cms_handle* h) {
   const int64_t n = h->n, dw = h->dw;
   const int64_t ntiles = (n + kTile - 1) / kTile;
   CMS_HIP(h->ws_limb0.ensure((size_t)n * (size_t)dw));
-  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (1 + 4) + (size_t)ntiles + 4 * sizeof(uint32_t) + 64));
-  char* meta = h->ws_limbmeta.as<char>();
-  uint8_t* rowL = reinterpret_cast<uint8_t*>(meta);
-  int32_t* row_hot = reinterpret_cast<int32_t*>(meta + ((n + 15) & ~int64_t(15)));
-  uint8_t* tileL = reinterpret_cast<uint8_t*>(row_hot + n);
-  uint32_t* cnt = h->d_flags + 8;  // [8]=hot rows [9]=inexact rows
-  int32_t* hot_list = row_hot;     // reuse: filled by k_limb_prep, consumed by k_limb_hot
-  CMS_HIP(h->ws_hotlist.ensure(sizeof(int32_t) * (size_t)n));
-  hot_list = h->ws_hotlist.as<int32_t>();
-  CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
-  CMS_HIP(hipMemsetAsync(row_hot, 0xFF, sizeof(int32_t) * (size_t)n, h->stream));
+  // meta: perm[n] i64 | inv[n] i64 | multi_flag[n] u32 | mpos[n] u32 | bsum | rowL[n] | rowLp[n] | tileL[ntiles]
+  const int64_t nbs = (n + 4095) / 4096 + 1;
+  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (8 + 8 + 4 + 4 + 1 + 1) + 4 * (size_t)nbs + (size_t)ntiles + 64));
+  int64_t* perm = h->ws_limbmeta.as<int64_t>();
+  int64_t* inv = perm + n;
+  uint32_t* mflag = reinterpret_cast<uint32_t*>(inv + n);
+  uint32_t* mpos = mflag + n;
+  uint32_t* bsum = mpos + n;
+  uint8_t* rowL = reinterpret_cast<uint8_t*>(bsum + nbs);
+  uint8_t* rowLp = rowL + n;
+  uint8_t* tileL = rowLp + n;
+  uint32_t* cnt = h->d_flags + 8;  // [8] inexact owners
+  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+  uint32_t host[3];
   {
     TimedScope ts(h, "limb_prep");
-    hipLaunchKernelGGL(k_limb_prep, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, n, dw, h->d_norm,
-                       h->p.depth, h->ws_limb0.as<int8_t>(), rowL, hot_list, cnt, cnt + 1);
-    hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowL, n, tileL);
+    hipLaunchKernelGGL(k_limb_count, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, dw, h->d_norm,
+                       h->p.depth, rowL, mflag, cnt);
+    int rc = scan_exclusive_u32(h, mflag, mpos, n, bsum);
+    if (rc) return rc;
     CMS_HIP(hipGetLastError());
+    CMS_HIP(hipMemcpyAsync(&host[0], mpos + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[1], mflag + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[2], cnt, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
   }
-  uint32_t counts[2];
-  CMS_HIP(hipMemcpyAsync(counts, cnt, sizeof(counts), hipMemcpyDeviceToHost, h->stream));
-  CMS_HIP(hipStreamSynchronize(h->stream));
-  h->n_hot_limb = counts[0];
-  h->n_inexact_rows = counts[1];
-  if (counts[0] > 0) {
-    CMS_HIP(h->ws_limbhot.ensure((size_t)counts[0] * (kMaxLimbs - 1) * (size_t)dw));
-    hipLaunchKernelGGL(k_limb_hot, dim3(counts[0], kMaxLimbs - 1), dim3(256), 0, h->stream, h->d_table, dw, hot_list,
-                       row_hot, h->ws_limbhot.as<int8_t>());
+  const int64_t n_multi = (int64_t)host[0] + host[1];
+  h->n_hot_limb = (uint32_t)n_multi;
+  h->n_inexact_rows = host[2];
+  CMS_HIP(h->ws_limbhot.ensure((size_t)std::max<int64_t>(1, n_multi) * (kMaxLimbs - 1) * (size_t)dw));
+  {
+    TimedScope ts(h, "limb_prep");
+    unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, rowL, n, n_multi, perm, inv,
+                       rowLp);
+    hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, dw, perm, rowLp, n_multi,
+                       h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
+    hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
+                       tileL);
     CMS_HIP(hipGetLastError());
   }
   h->tile_limbs.resize(ntiles);
+  h->h_perm.resize(n);
+  h->h_inv.resize(n);
   CMS_HIP(hipMemcpyAsync(h->tile_limbs.data(), tileL, ntiles, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(h->h_perm.data(), perm, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(h->h_inv.data(), inv, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
   h->mfma_ready = true;
   return CMS_OK;
 }
 
+const int64_t* cosine_perm_device(cms_handle* h) { return h->ws_limbmeta.as<int64_t>(); }
+
 bool mfma_eligible(cms_handle* h) { return (h->p.width % kBK) == 0; }
 
-// Similarities of query rows [q0, q0+qc) against every owner into slab
-// [qc][n] (fp64, column = row index).  q0 must be a multiple of kTile.
+// Similarities of the owners at PERMUTED positions [q0, q0+qc) against every
+// owner into slab [qc][n] (fp64, column = permuted position; owner row =
+// perm[column]).  q0 must be a multiple of kTile.
 int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   int rc = cosine_prepare(h);
   if (rc) return rc;
   const int64_t n = h->n, dw = h->dw;
-  char* meta = h->ws_limbmeta.as<char>();
+  const int64_t nbs = (n + 4095) / 4096 + 1;
   CosArgs a;
   a.limb0 = h->ws_limb0.as<int8_t>();
-  a.hl = h->n_hot_limb ? h->ws_limbhot.as<int8_t>() : nullptr;
-  a.rowL = reinterpret_cast<uint8_t*>(meta);
-  a.row_hot = reinterpret_cast<int32_t*>(meta + ((n + 15) & ~int64_t(15)));
-  a.tileL = reinterpret_cast<uint8_t*>(const_cast<int32_t*>(a.row_hot) + n);
+  a.hl = h->ws_limbhot.as<int8_t>();
+  a.perm = h->ws_limbmeta.as<int64_t>();
+  a.rowL = reinterpret_cast<const uint8_t*>(reinterpret_cast<const uint32_t*>(a.perm + 2 * n) + 2 * n + nbs) + n;
+  a.tileL = a.rowL + n;
+  a.n_multi = h->n_hot_limb;
   a.nsqrt = h->d_norm_sqrt;
   a.n = n;
   a.dw = dw;

@@ -74,7 +74,8 @@ struct cms_handle {
   bool mfma_ready = false;
   uint32_t n_hot_limb = 0;      // owners with counters >= 128 (multi-limb)
   uint32_t n_inexact_rows = 0;  // owners with a norm >= 2^53
-  std::vector<uint8_t> tile_limbs;
+  std::vector<uint8_t> tile_limbs;   // per permuted 128-row tile: max limb count
+  std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
   int64_t pairs_ingested = 0;
   int32_t exact_norms = 1;
 
@@ -84,7 +85,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out;
-  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab;
+  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq;
 
   // communicator
   ncclComm_t comm = nullptr;
@@ -138,8 +139,8 @@ int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m,
 int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts);
-int top_k_slab(cms_handle* h, const double* slab, int64_t ld, int64_t first_row, int64_t count, int32_t k,
-               int64_t* d_ids, double* d_scores, int32_t* d_counts);
+// ---- cms_cosine_mfma.hip ----
+const int64_t* cosine_perm_device(cms_handle* h);
 // ---- cms_cosine_mfma.hip ----
 int cosine_prepare(cms_handle* h);
 bool mfma_eligible(cms_handle* h);

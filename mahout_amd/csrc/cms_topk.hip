@@ -1,0 +1,271 @@
+// cms_topk.hip -- per-owner top-k over a similarity slab on gfx950.
+//
+// TopItems.getTopUsers (T/impl/recommender/TopItems.java:91-136) iterates the
+// candidate owners in ascending ID order, skips NaN (self included, via
+// MostSimilarEstimator, GenericUserBasedRecommender.java:231-247) and keeps
+// the first k of the total order SimilarUser.compareTo defines
+// (T/impl/recommender/SimilarUser.java:62-78): similarity descending, ID
+// ascending.  One workgroup per query row:
+//   1. radix select (8 x 8-bit digits) of the k-th largest similarity key;
+//   2. when more candidates tie at that key than are needed, a second radix
+//      select over the OWNER ROW of the tied candidates (the slab columns may
+//      be permuted, so column order is not ID order);
+//   3. gather the survivors into LDS and bitonic-sort them by (key desc, row asc).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "cms_internal.h"
+
+namespace cms {
+
+constexpr int kTopThreads = 1024;
+constexpr int kTopMax = 1024;
+
+__device__ __forceinline__ uint64_t score_key(double s) {
+  if (s == 0.0) s = 0.0;  // -0.0 == +0.0 under SimilarUser.compareTo
+  uint64_t u = (uint64_t)__double_as_longlong(s);
+  return (u >> 63) ? ~u : (u | (1ULL << 63));
+}
+
+struct TopQuery {
+  int64_t slab_row;  // row of the slab holding this query's similarities
+  int64_t self_col;  // slab column of the query itself (excluded)
+  int64_t out_pos;   // output slot
+};
+
+__device__ __forceinline__ uint32_t block_count(uint32_t v, uint32_t* wsum) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int i = 0; i < kTopThreads / 64; ++i) t += wsum[i];
+  return t;
+}
+
+__global__ __launch_bounds__(kTopThreads) void k_top_k(const double* slab, int64_t ld, int64_t n, int32_t k,
+                                                        const TopQuery* queries, const int64_t* perm,
+                                                        const int64_t* owner_ids, int64_t* out_ids,
+                                                        double* out_scores, int32_t* counts) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_need, s_tied;
+  __shared__ uint64_t ckey[kTopMax];
+  __shared__ int64_t crow[kTopMax];
+  __shared__ int64_t ccol[kTopMax];
+  __shared__ uint32_t s_cnt;
+  __shared__ uint32_t wsum[kTopThreads / 64];
+
+  const TopQuery Q = queries[blockIdx.x];
+  const double* sc = slab + Q.slab_row * ld;
+  const int tid = threadIdx.x;
+  auto row_of = [&](int64_t j) -> int64_t { return perm ? perm[j] : j; };
+
+  uint32_t valid = 0;
+  for (int64_t j = tid; j < n; j += kTopThreads) {
+    const double s = sc[j];
+    valid += (j != Q.self_col && s == s);
+  }
+  const uint32_t nvalid = block_count(valid, wsum);
+  const uint32_t kk = (uint32_t)min<int64_t>(k, nvalid);
+  if (kk == 0) {
+    if (tid == 0) counts[Q.out_pos] = 0;
+    return;
+  }
+  if (tid == 0) {
+    s_prefix = 0;
+    s_need = kk;
+    s_cnt = 0;
+  }
+  __syncthreads();
+  // ---- 1. k-th largest key T; s_need = how many keys == T to take ----
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kTopThreads) hist[i] = 0;
+    __syncthreads();
+    const uint64_t pre = s_prefix;
+    const uint64_t hmask = shift == 56 ? 0ULL : (~0ULL << (shift + 8));
+    for (int64_t j = tid; j < n; j += kTopThreads) {
+      const double s = sc[j];
+      if (j == Q.self_col || s != s) continue;
+      const uint64_t key = score_key(s);
+      if ((key & hmask) == pre) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t need = s_need;
+      int digit = 255;
+      for (; digit > 0; --digit) {
+        if (hist[digit] >= need) break;
+        need -= hist[digit];
+      }
+      s_need = need;
+      s_prefix = pre | ((uint64_t)digit << shift);
+      if (shift == 0) s_tied = hist[digit];
+    }
+    __syncthreads();
+  }
+  const uint64_t T = s_prefix;
+  const uint32_t ties_needed = s_need;
+  const uint32_t ties_total = s_tied;
+  // ---- 2. among keys == T, the ties_needed-th smallest owner row R ----
+  uint64_t R = ~0ULL;
+  if (ties_needed < ties_total) {
+    if (tid == 0) s_prefix = 0;
+    __syncthreads();
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      for (int i = tid; i < 256; i += kTopThreads) hist[i] = 0;
+      __syncthreads();
+      const uint64_t pre = s_prefix;
+      const uint64_t hmask = shift == 56 ? 0ULL : (~0ULL << (shift + 8));
+      for (int64_t j = tid; j < n; j += kTopThreads) {
+        const double s = sc[j];
+        if (j == Q.self_col || s != s || score_key(s) != T) continue;
+        const uint64_t rk = (uint64_t)row_of(j);
+        if ((rk & hmask) == pre) atomicAdd(&hist[(rk >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t need = s_need;  // smallest-first: walk digits upward
+        int digit = 0;
+        for (; digit < 255; ++digit) {
+          if (hist[digit] >= need) break;
+          need -= hist[digit];
+        }
+        s_need = need;
+        s_prefix = pre | ((uint64_t)digit << shift);
+      }
+      __syncthreads();
+    }
+    R = s_prefix;
+  }
+  // ---- 3. gather: keys > T, and ties with owner row <= R ----
+  for (int64_t j = tid; j < n; j += kTopThreads) {
+    const double s = sc[j];
+    if (j == Q.self_col || s != s) continue;
+    const uint64_t key = score_key(s);
+    if (key < T) continue;
+    const int64_t rw = row_of(j);
+    if (key == T && (uint64_t)rw > R) continue;
+    const uint32_t pos = atomicAdd(&s_cnt, 1u);
+    if (pos < kTopMax) {
+      ckey[pos] = key;
+      crow[pos] = rw;
+      ccol[pos] = j;
+    }
+  }
+  __syncthreads();
+  uint32_t P = 1;
+  while (P < kk) P <<= 1;
+  for (uint32_t i = kk + tid; i < P; i += kTopThreads) {
+    ckey[i] = 0;
+    crow[i] = INT64_MAX;
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = tid; i < P; i += kTopThreads) {
+        const uint32_t jx = i ^ stride;
+        if (jx > i) {
+          const bool up = (i & size) == 0;
+          const bool i_first = ckey[i] > ckey[jx] || (ckey[i] == ckey[jx] && crow[i] < crow[jx]);
+          if (up != i_first) {
+            uint64_t tk = ckey[i];
+            ckey[i] = ckey[jx];
+            ckey[jx] = tk;
+            int64_t tr = crow[i];
+            crow[i] = crow[jx];
+            crow[jx] = tr;
+            int64_t tc = ccol[i];
+            ccol[i] = ccol[jx];
+            ccol[jx] = tc;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = tid; i < kk; i += kTopThreads) {
+    out_ids[Q.out_pos * k + i] = owner_ids ? owner_ids[crow[i]] : crow[i];
+    out_scores[Q.out_pos * k + i] = sc[ccol[i]];
+  }
+  if (tid == 0) counts[Q.out_pos] = (int32_t)kk;
+}
+
+static int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k,
+                        const int64_t* d_perm, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  if (qs.empty()) return CMS_OK;
+  CMS_HIP(h->ws_topq.ensure(sizeof(TopQuery) * qs.size()));
+  CMS_HIP(hipMemcpyAsync(h->ws_topq.ptr, qs.data(), sizeof(TopQuery) * qs.size(), hipMemcpyHostToDevice, h->stream));
+  {
+    TimedScope ts(h, "top_k");
+    hipLaunchKernelGGL(k_top_k, dim3((unsigned)qs.size()), dim3(kTopThreads), 0, h->stream, slab, h->n, h->n, k,
+                       h->ws_topq.as<TopQuery>(), d_perm, h->d_owner_ids, d_ids, d_scores, d_counts);
+    CMS_HIP(hipGetLastError());
+  }
+  CMS_HIP(hipStreamSynchronize(h->stream));  // host query list and ws reuse
+  return CMS_OK;
+}
+
+int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
+               int32_t* d_counts) {
+  if (k < 1 || k > kTopMax) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kTopMax);
+  const int64_t n = h->n;
+  int rc = CMS_OK;
+  if (mfma_eligible(h) && (rc = cosine_prepare(h))) return rc;
+  const int64_t slab_rows = std::max<int64_t>(128, ((int64_t(1) << 28) / std::max<int64_t>(1, n)) / 128 * 128);
+  if (mfma_eligible(h) && h->n_inexact_rows == 0) {
+    // MFMA slabs over PERMUTED 128-row query tiles that hold a requested owner
+    std::vector<int64_t> tiles;
+    for (int64_t r = row_begin; r < row_begin + row_count; ++r) tiles.push_back(h->h_inv[r] / 128);
+    std::sort(tiles.begin(), tiles.end());
+    tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
+    // a run of consecutive tiles below never exceeds slab_rows rows (nor the tiles present)
+    const int64_t max_run = std::min<int64_t>(slab_rows, (int64_t)tiles.size() * 128);
+    CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(max_run * n)));
+    size_t ti = 0;
+    while (ti < tiles.size()) {
+      // a run of consecutive tiles, at most slab_rows rows
+      size_t tj = ti + 1;
+      while (tj < tiles.size() && tiles[tj] == tiles[tj - 1] + 1 && (int64_t)(tj - ti + 1) * 128 <= slab_rows) ++tj;
+      const int64_t q0 = tiles[ti] * 128;
+      const int64_t qc = std::min<int64_t>(n - q0, (int64_t)(tj - ti) * 128);
+      if ((rc = cosine_slab(h, q0, qc, h->ws_slab.as<double>()))) return rc;
+      std::vector<TopQuery> qs;
+      for (int64_t p = q0; p < q0 + qc; ++p) {
+        const int64_t r = h->h_perm[p];
+        if (r >= row_begin && r < row_begin + row_count) qs.push_back(TopQuery{p - q0, p, r - row_begin});
+      }
+      if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, cosine_perm_device(h), d_ids, d_scores, d_counts)))
+        return rc;
+      ti = tj;
+    }
+    return CMS_OK;
+  }
+  // exact pair kernel per query row (widths not a multiple of 128, or owners
+  // whose norms left the exact fp64 regime)
+  const int64_t qb = std::min<int64_t>(row_count, slab_rows);
+  CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(qb * n)));
+  CMS_HIP(h->ws_query.ensure(sizeof(int64_t) * (size_t)n));
+  {
+    std::vector<int64_t> all(n);
+    for (int64_t i = 0; i < n; ++i) all[i] = i;
+    CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, all.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+  }
+  for (int64_t r0 = 0; r0 < row_count; r0 += qb) {
+    const int64_t rcnt = std::min(qb, row_count - r0);
+    std::vector<TopQuery> qs;
+    for (int64_t q = 0; q < rcnt; ++q) {
+      const int64_t row = row_begin + r0 + q;
+      if ((rc = pair_cosines(h, row, h->ws_query.as<int64_t>(), n, h->ws_slab.as<double>() + q * n))) return rc;
+      qs.push_back(TopQuery{q, row, r0 + q});
+    }
+    if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, nullptr, d_ids, d_scores, d_counts))) return rc;
+  }
+  return CMS_OK;
+}
+
+}  // namespace cms

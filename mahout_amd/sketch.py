@@ -208,3 +208,10 @@ def shard_of_keys(keys, world):
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
     return (z % np.uint64(world)).astype(np.int32)
+
+
+def _release_scratch(self):
+    check(self._lib.cms_release_scratch(self._h))
+
+
+SketchTable.release_scratch = _release_scratch
