@@ -101,6 +101,19 @@ def cpu_baseline(off_d, keys_d, args, budget_s=12.0):
                       f"{dt:.1f} s; fp64 DoubleCountMinSketch rebuilt per owner + 128-bit BigInteger-equivalent hash"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>/pmc_summary.json, scripts/profile.sh on this bench command:
+    2 * FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    rec = data.get(kernel)
+    return (rec.get("hbm_bytes_per_launch") if rec else None), os.path.relpath(files[-1], ROOT)
+
+
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense peak), MI355X_MICROARCH.md
 
 
@@ -221,6 +234,7 @@ def main():
     build_alg_bytes = npairs * 8 + (n + 1) * 8 + table_bytes  # CSR keys + offsets read, table written once
     achieved = build_alg_bytes / (build_ms / build_n * 1e-3) / 1e9 if build_n else None
     table.set_timing(False)
+    traffic, traffic_src = pmc_traffic("cms::k_build_rows")
 
     result = {
         "metric": METRIC,
@@ -248,7 +262,8 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": build_alg_bytes,
             "avg_launch_ms": build_ms / build_n if build_n else None,
         },

@@ -1,0 +1,181 @@
+/*
+ * Drop-in for the CosineCM sketch-cosine path (reference:
+ * mr/src/main/java/org/apache/mahout/cf/taste/impl/similarity/CosineCM.java)
+ * backed by libmahout_cms.so (include/mahout_cms.h) through the JNI shim in
+ * integration/jni/mahout_cms_jni.c.
+ *
+ * NOTE: written against the reference's Taste interfaces; no JDK exists in
+ * the build image, so this file is not compiled here (see INTEGRATION.md).
+ *
+ * Shape: every owner gets the same (depth, width) -- the fixed-shape configs
+ * of this path.  The reference's per-owner (delta, epsilon) sizing
+ * (CountMinSketchConfig) is not carried over yet.
+ */
+package org.apache.mahout.cf.taste.impl.similarity;
+
+import java.util.Collection;
+
+import org.apache.mahout.cf.taste.common.NoSuchItemException;
+import org.apache.mahout.cf.taste.common.NoSuchUserException;
+import org.apache.mahout.cf.taste.common.Refreshable;
+import org.apache.mahout.cf.taste.common.TasteException;
+import org.apache.mahout.cf.taste.common.Weighting;
+import org.apache.mahout.cf.taste.impl.common.LongPrimitiveIterator;
+import org.apache.mahout.cf.taste.model.DataModel;
+import org.apache.mahout.cf.taste.model.PreferenceArray;
+import org.apache.mahout.cf.taste.similarity.PreferenceInferrer;
+import org.apache.mahout.cf.taste.similarity.UserSimilarity;
+
+public final class CosineCMGpu extends AbstractItemSimilarity implements UserSimilarity {
+
+  static {
+    System.loadLibrary("mahout_cms_jni");  // links libmahout_cms.so
+  }
+
+  // status codes of include/mahout_cms.h
+  static final int CMS_E_PARAM = 1;
+  static final int CMS_E_SHAPE = 2;
+  static final int CMS_E_NO_SUCH_ID = 3;
+
+  private final int depth;
+  private final int width;
+  private final long seed;
+  private final boolean weighted;
+  private final int device;
+  private long handle;  // cms_handle*
+
+  /**
+   * @param hfBuilderSeed the seed a HashFunctionBuilder(seed) would be built with
+   *        (HashFunctionBuilder.java:59); the same seed gives the same buckets
+   */
+  public CosineCMGpu(DataModel dataModel, int depth, int width, long hfBuilderSeed, Weighting weighting, int device)
+      throws TasteException {
+    super(dataModel);
+    if (!dataModel.hasPreferenceValues()) {  // CosineCM.java:38
+      throw new IllegalArgumentException("DataModel doesn't have preference values");
+    }
+    this.depth = depth;
+    this.width = width;
+    this.seed = hfBuilderSeed;
+    this.weighted = weighting == Weighting.WEIGHTED;
+    this.device = device;
+    build();
+  }
+
+  public CosineCMGpu(DataModel dataModel, int depth, int width, long hfBuilderSeed) throws TasteException {
+    this(dataModel, depth, width, hfBuilderSeed, Weighting.UNWEIGHTED, -1);
+  }
+
+  /** DataModel -> CSR (sorted owner IDs, per-owner PreferenceArray order) -> GPU table. */
+  private void build() throws TasteException {
+    DataModel model = getDataModel();
+    int n = model.getNumUsers();
+    long[] ids = new long[n];
+    long[] offsets = new long[n + 1];
+    int r = 0;
+    long total = 0;
+    LongPrimitiveIterator it = model.getUserIDs();
+    while (it.hasNext()) {
+      long id = it.nextLong();
+      ids[r] = id;
+      total += model.getPreferencesFromUser(id).length();
+      offsets[++r] = total;
+    }
+    long[] keys = new long[(int) total];
+    float[] vals = new float[(int) total];
+    for (int i = 0; i < n; i++) {
+      PreferenceArray prefs = model.getPreferencesFromUser(ids[i]);
+      int base = (int) offsets[i];
+      for (int j = 0; j < prefs.length(); j++) {
+        keys[base + j] = prefs.getItemID(j);
+        vals[base + j] = prefs.getValue(j);
+      }
+    }
+    long h = nativeCreate(depth, width, seed, n, weighted, device);
+    try {
+      nativeSetOwnerIds(h, ids);
+      nativeIngestCsr(h, offsets, keys, vals);
+      nativeFinalize(h);
+    } catch (TasteException | RuntimeException e) {
+      nativeDestroy(h);
+      throw e;
+    }
+    long old = handle;
+    handle = h;
+    if (old != 0) {
+      nativeDestroy(old);
+    }
+  }
+
+  /** CosineCM.userSimilarity (CosineCM.java:83-96). */
+  @Override
+  public double userSimilarity(long userID1, long userID2) throws TasteException {
+    return nativeSimilarity(handle, userID1, userID2, false);
+  }
+
+  @Override
+  public void setPreferenceInferrer(PreferenceInferrer inferrer) {
+    if (inferrer == null) {
+      throw new IllegalArgumentException("inferrer is null");
+    }
+    // the sketch cosine does not infer preferences (as CosineCM)
+  }
+
+  /** Sketch cosine between owners; owners are items over a transposed DataModel. */
+  @Override
+  public double itemSimilarity(long itemID1, long itemID2) throws TasteException {
+    return nativeSimilarity(handle, itemID1, itemID2, true);
+  }
+
+  @Override
+  public double[] itemSimilarities(long itemID1, long[] itemID2s) throws TasteException {
+    return nativeSimilarities(handle, itemID1, itemID2s);
+  }
+
+  /** GenericUserBasedRecommender.mostSimilarUserIDs + TopItems.getTopUsers semantics. */
+  public long[] mostSimilarIDs(long ownerID, int howMany) throws TasteException {
+    if (howMany < 1) {
+      throw new IllegalArgumentException("howMany must be at least 1");
+    }
+    return nativeMostSimilar(handle, ownerID, howMany);
+  }
+
+  /** DoubleCountMinSketch.get(key) on the owner's sketch (point query). */
+  public double pointQuery(long ownerID, long key) throws TasteException {
+    return nativePointQuery(handle, ownerID, key);
+  }
+
+  @Override
+  public void refresh(Collection<Refreshable> alreadyRefreshed) {
+    super.refresh(alreadyRefreshed);
+    try {
+      build();
+    } catch (TasteException te) {
+      throw new IllegalStateException(te);
+    }
+  }
+
+  public void close() {
+    if (handle != 0) {
+      nativeDestroy(handle);
+      handle = 0;
+    }
+  }
+
+  @Override
+  public String toString() {
+    return "CosineCMGpu[dataModel:" + getDataModel() + ",d:" + depth + ",w:" + width + ']';
+  }
+
+  // --- JNI (integration/jni/mahout_cms_jni.c) --------------------------------
+  private static native long nativeCreate(int depth, int width, long seed, long numOwners, boolean weighted,
+                                          int device) throws TasteException;
+  private static native void nativeSetOwnerIds(long h, long[] ids) throws TasteException;
+  private static native void nativeIngestCsr(long h, long[] offsets, long[] keys, float[] vals) throws TasteException;
+  private static native void nativeFinalize(long h) throws TasteException;
+  private static native double nativeSimilarity(long h, long id1, long id2, boolean itemIds) throws TasteException;
+  private static native double[] nativeSimilarities(long h, long id1, long[] ids2) throws TasteException;
+  private static native long[] nativeMostSimilar(long h, long id, int k) throws TasteException;
+  private static native double nativePointQuery(long h, long id, long key) throws TasteException;
+  private static native void nativeDestroy(long h);
+}

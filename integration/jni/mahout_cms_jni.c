@@ -1,0 +1,131 @@
+/*
+ * JNI shim: org.apache.mahout.cf.taste.impl.similarity.CosineCMGpu -> the C
+ * ABI of libmahout_cms.so (include/mahout_cms.h).
+ *
+ * Built only where a JDK provides jni.h (not in this image):
+ *   cc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux \
+ *      -I../../include mahout_cms_jni.c -L../../mahout_amd -lmahout_cms \
+ *      -Wl,-rpath,'$ORIGIN' -o libmahout_cms_jni.so
+ *
+ * Status codes map to the reference's exceptions: CMS_E_NO_SUCH_ID ->
+ * NoSuchUserException / NoSuchItemException (GenericDataModel.java:210-215),
+ * CMS_E_PARAM / CMS_E_SHAPE -> IllegalArgumentException
+ * (AbstractCountMinSketch CMException / DoubleCountMinSketch checkArgument),
+ * anything else -> TasteException.  NaN similarities are values, not errors.
+ * Java arrays are pinned only for the duration of the copy into the library
+ * (GetPrimitiveArrayCritical); the library never retains host pointers.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "mahout_cms.h"
+
+#define CLS "org/apache/mahout/cf/taste/"
+
+static int fail(JNIEnv* env, int rc, int item_ids) {
+  if (rc == CMS_OK) return 0;
+  const char* cls = CLS "common/TasteException";
+  if (rc == CMS_E_NO_SUCH_ID) cls = item_ids ? CLS "common/NoSuchItemException" : CLS "common/NoSuchUserException";
+  else if (rc == CMS_E_PARAM || rc == CMS_E_SHAPE) cls = "java/lang/IllegalArgumentException";
+  jclass ex = (*env)->FindClass(env, cls);
+  if (ex) (*env)->ThrowNew(env, ex, cms_last_error());
+  return 1;
+}
+
+#define H(x) ((cms_handle*)(intptr_t)(x))
+#define JFN(name) Java_org_apache_mahout_cf_taste_impl_similarity_CosineCMGpu_##name
+
+JNIEXPORT jlong JNICALL JFN(nativeCreate)(JNIEnv* env, jclass c, jint depth, jint width, jlong seed, jlong n,
+                                          jboolean weighted, jint device) {
+  (void)c;
+  cms_params p;
+  cms_params_init(&p);
+  p.depth = depth;
+  p.width = width;
+  p.seed = seed;
+  p.num_owners = n;
+  p.weighting = weighted ? CMS_WEIGHTED : CMS_UNWEIGHTED;
+  p.device = device;
+  cms_handle* h = NULL;
+  if (fail(env, cms_create(&p, &h), 0)) return 0;
+  return (jlong)(intptr_t)h;
+}
+
+JNIEXPORT void JNICALL JFN(nativeSetOwnerIds)(JNIEnv* env, jclass c, jlong h, jlongArray ids) {
+  (void)c;
+  jsize n = (*env)->GetArrayLength(env, ids);
+  jlong* p = (*env)->GetPrimitiveArrayCritical(env, ids, NULL);
+  int rc = cms_set_owner_ids(H(h), (const int64_t*)p, n);
+  (*env)->ReleasePrimitiveArrayCritical(env, ids, p, JNI_ABORT);
+  fail(env, rc, 0);
+}
+
+JNIEXPORT void JNICALL JFN(nativeIngestCsr)(JNIEnv* env, jclass c, jlong h, jlongArray off, jlongArray keys,
+                                            jfloatArray vals) {
+  (void)c;
+  jlong* po = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
+  jlong* pk = (*env)->GetPrimitiveArrayCritical(env, keys, NULL);
+  jfloat* pv = vals ? (*env)->GetPrimitiveArrayCritical(env, vals, NULL) : NULL;
+  int rc = cms_ingest_csr(H(h), (const int64_t*)po, (const int64_t*)pk, (const float*)pv);
+  if (pv) (*env)->ReleasePrimitiveArrayCritical(env, vals, pv, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, keys, pk, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, off, po, JNI_ABORT);
+  fail(env, rc, 0);
+}
+
+JNIEXPORT void JNICALL JFN(nativeFinalize)(JNIEnv* env, jclass c, jlong h) {
+  (void)c;
+  fail(env, cms_finalize(H(h)), 0);
+}
+
+JNIEXPORT jdouble JNICALL JFN(nativeSimilarity)(JNIEnv* env, jclass c, jlong h, jlong a, jlong b, jboolean items) {
+  (void)c;
+  double out = 0.0;
+  fail(env, cms_similarity(H(h), a, b, &out), items);
+  return out;
+}
+
+JNIEXPORT jdoubleArray JNICALL JFN(nativeSimilarities)(JNIEnv* env, jclass c, jlong h, jlong a, jlongArray ids) {
+  (void)c;
+  jsize n = (*env)->GetArrayLength(env, ids);
+  jdoubleArray res = (*env)->NewDoubleArray(env, n);
+  if (!res) return NULL;
+  int64_t* tmp_ids = (int64_t*)malloc(sizeof(int64_t) * (n ? n : 1));
+  double* tmp_out = (double*)malloc(sizeof(double) * (n ? n : 1));
+  (*env)->GetLongArrayRegion(env, ids, 0, n, (jlong*)tmp_ids);
+  int rc = cms_similarities(H(h), a, tmp_ids, n, tmp_out);
+  if (rc == CMS_OK) (*env)->SetDoubleArrayRegion(env, res, 0, n, tmp_out);
+  free(tmp_ids);
+  free(tmp_out);
+  return fail(env, rc, 1) ? NULL : res;
+}
+
+JNIEXPORT jlongArray JNICALL JFN(nativeMostSimilar)(JNIEnv* env, jclass c, jlong h, jlong id, jint k) {
+  (void)c;
+  int64_t* ids = (int64_t*)malloc(sizeof(int64_t) * (k > 0 ? k : 1));
+  double* sc = (double*)malloc(sizeof(double) * (k > 0 ? k : 1));
+  int32_t cnt = 0;
+  int rc = cms_most_similar(H(h), id, k, ids, sc, &cnt);
+  jlongArray res = NULL;
+  if (rc == CMS_OK) {
+    res = (*env)->NewLongArray(env, cnt);
+    if (res) (*env)->SetLongArrayRegion(env, res, 0, cnt, (const jlong*)ids);
+  }
+  free(ids);
+  free(sc);
+  return fail(env, rc, 0) ? NULL : res;
+}
+
+JNIEXPORT jdouble JNICALL JFN(nativePointQuery)(JNIEnv* env, jclass c, jlong h, jlong id, jlong key) {
+  (void)c;
+  double out = 0.0;
+  fail(env, cms_point_query(H(h), id, key, &out), 0);
+  return out;
+}
+
+JNIEXPORT void JNICALL JFN(nativeDestroy)(JNIEnv* env, jclass c, jlong h) {
+  (void)env;
+  (void)c;
+  cms_destroy(H(h));
+}
