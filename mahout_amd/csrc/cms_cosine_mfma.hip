@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 #include <vector>
 
 #include "cms_device.h"
@@ -221,7 +222,9 @@ __global__ __launch_bounds__(256, MULTI ? 1 : 2) void k_cosine_tile(CosArgs a, c
   }
   const int64_t row0 = a.q0 + trow * kTile;  // A rows (queries)
   const int64_t col0 = tcol * kTile;         // B rows (candidates)
-  const int LA = MULTI ? a.tileL[row0 / kTile] : 1;
+  // an unaligned query start makes the row tile straddle two permuted tiles
+  const int64_t tlast = min<int64_t>((row0 + kTile - 1) / kTile, a.tiles_x - 1);
+  const int LA = MULTI ? max(a.tileL[row0 / kTile], a.tileL[tlast]) : 1;
   const int LB = MULTI ? a.tileL[col0 / kTile] : 1;
   if (!MULTI && !tile_list && (a.tileL[row0 / kTile] > 1 || a.tileL[col0 / kTile] > 1)) return;  // MULTI's job
 
@@ -382,6 +385,230 @@ __global__ __launch_bounds__(256, MULTI ? 1 : 2) void k_cosine_tile(CosArgs a, c
     }
 }
 
+// --------------------------------------------------------- 256 x 128 tile --
+// 8 waves (4 x 2), each 64 x 64 MFMA outputs.  A = 256 operand rows, B = 128.
+// NSTAGE-deep LDS ring of 48 KiB stages filled by buffer LDS-DMA; a raw
+// s_barrier behind a counted vmcnt keeps the next stage in flight across it.
+// The workgroups an XCD runs at once share one A panel (XCD-aware map).
+//
+// LS = limb slots per A owner.  LS = 1: A rows are owners (single-limb
+// limb0 image).  LS = 2 / 4: A rows are the "virtual limb rows" of the
+// multi-limb owners (ws_vl): within each 32-row MFMA block, row 8g + i holds
+// limb g % LS of owner (g / LS) * 8 + i, so the LS limbs of an owner land in
+// accumulator elements e, e+4, ... of ONE lane and fold exactly in registers
+// (dot = sum_l acc_l << 7l) -- multi-limb x single-limb costs LS passes of
+// A rows instead of a separate int64 kernel.  TRANS writes the transposed
+// slab entries (query = B row), which is how single-limb queries meet
+// multi-limb candidates: cosine(a, b) == cosine(b, a) bit for bit.
+constexpr int kTA = 256, kTB = 128;
+constexpr int kStageA = kTA * kBK, kStageB = kTB * kBK, kStage = kStageA + kStageB;
+
+struct BigArgs {
+  const int8_t* A;      // operand rows (limb0 image or ws_vl), first row of this launch
+  int64_t a_vrows;      // operand rows available from A
+  int64_t a_pos0;       // permuted position of A's first owner
+  int64_t a_owners;     // owners covered from a_pos0
+  const int8_t* B;      // candidate rows (limb0 image)
+  int64_t b_pos0;       // permuted position of B's first row
+  int64_t b_rows;       // candidates covered
+  const int64_t* perm;  // permuted position -> owner row
+  const double* nsqrt;  // [n][d] by owner row
+  double* out;          // slab [qcount][ldo]
+  int64_t ldo;
+  int64_t q0, qcount;   // slab rows = permuted positions [q0, q0 + qcount)
+  int64_t dw;
+  int32_t w, depth;
+  int32_t weighted, trans;
+  int32_t tilesB, nblk;
+  int32_t mode;  // EXPERIMENT: bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
+};
+
+template <int NSTAGE, int LS>
+__global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
+  constexpr int OA = kTA / LS;  // owners per A panel
+  constexpr int OG = 4 / LS;    // owner groups per 32-row block in one lane
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int depth = g.depth;
+  double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][OA]
+  double* s_sb = s_sa + depth * OA;                                  // [depth][128]
+  const int nblk = g.nblk;
+  const int bx = blockIdx.x, xcd = bx & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
+  const int ta = lin / g.tilesB, tb = lin % g.tilesB;
+  const int64_t vrow0 = (int64_t)ta * kTA;  // first operand row of the A panel
+  const int64_t own0 = (int64_t)ta * OA;    // first owner (relative to a_pos0)
+  const int64_t bcol0 = (int64_t)tb * kTB;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int w = g.w;
+  const int cstages = w / kBK;
+  const int total = depth * cstages;
+
+  for (int i = tid; i < depth * OA; i += 512) {
+    const int r = i / OA, t = i % OA;
+    const int64_t o = own0 + t;
+    s_sa[i] = o < g.a_owners ? g.nsqrt[g.perm[g.a_pos0 + o] * depth + r] : 0.0;
+  }
+  for (int i = tid; i < depth * kTB; i += 512) {
+    const int r = i / kTB, t = i % kTB;
+    const int64_t c = bcol0 + t;
+    s_sb[i] = c < g.b_rows ? g.nsqrt[g.perm[g.b_pos0 + c] * depth + r] : 0.0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // buffer descriptors bound the panel: rows past the end land as zeros
+  const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, g.a_vrows - vrow0));
+  const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, g.b_rows - bcol0));
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + vrow0 * g.dw), (short)0, (int)(rowsA * g.dw), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.B + bcol0 * g.dw), (short)0, (int)(rowsB * g.dw), 0x00020000);
+  // staging row of lane for op u: wid*8 + (lane>>3) + 64u.  The 64-row step
+  // leaves the swizzle unchanged, so one voffset per lane serves every op and
+  // the row step rides in the voffset as a constant add.
+  const int srow = wid * 8 + (lane >> 3);
+  const int32_t vo = (int32_t)(srow * g.dw) + (((lane & 7) ^ ((srow >> 1) & 7)) << 4);
+  const int32_t rstep = 64 * (int32_t)g.dw;
+  auto issue = [&](int s) {
+    if (g.mode & 1) return;
+    const int r = s / cstages, cs = s - r * cstages;
+    const int32_t koff = r * w + cs * kBK;
+    unsigned char* st = lds + (s % NSTAGE) * kStage;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + 8 * u) * 1024),
+                                               16, vo + u * rstep, koff, 0, 0);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + 8 * u) * 1024), 16, vo + u * rstep,
+          koff, 0, 0);
+  };
+
+  i32x16 acc[2][2];
+  double mn[2][2][4 * OG];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+#pragma unroll
+      for (int e = 0; e < 4 * OG; ++e) mn[i][j][e] = DBL_MAX;
+    }
+
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < total) issue(s);
+
+  for (int s = 0; s < total; ++s) {
+    // stage s landed: at most the (NSTAGE-2) younger stages (6 ops each) stay in flight
+    if (s + NSTAGE - 2 < total) {
+      if constexpr (NSTAGE == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);  // refill the slot read in iteration s-1
+    const unsigned char* A = lds + (s % NSTAGE) * kStage;
+    const unsigned char* B = A + kStageA;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (g.mode & 2) break;
+      const int ch = 2 * ks + (lane >> 5);
+      i8x16 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off(wr * 64 + i * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off(wc * 64 + j * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    const int r = s / cstages;
+    if (s - r * cstages == cstages - 1 && !(g.mode & 4)) {
+      // ---- fp64 epilogue of sketch row r (DoubleCountMinSketch.java:143-147) ----
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const double sb = s_sb[r * kTB + wc * 64 + j * 32 + (lane & 31)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int og = 0; og < OG; ++og)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int ol = (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
+              const double sa = s_sa[r * OA + ol];
+              double valueAB;
+              if constexpr (LS == 1) {
+                valueAB = (double)acc[i][j][q + 4 * og];
+              } else {
+                int64_t dot = 0;
+#pragma unroll
+                for (int l = 0; l < LS; ++l) dot += (int64_t)acc[i][j][q + 4 * (og * LS + l)] << (7 * l);
+                valueAB = (double)dot;
+              }
+              const double den = __dmul_rn(sa, sb);
+              if (den != 0.0) mn[i][j][og * 4 + q] = java_min_d(mn[i][j][og * 4 + q], __ddiv_rn(valueAB, den));
+            }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+        }
+      }
+    }
+  }
+
+  // ---- write the slab: NaN when no row qualified, then normalizeWeightResult ----
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t bi = bcol0 + wc * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int og = 0; og < OG; ++og)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t ai = own0 + (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
+          if (ai >= g.a_owners || bi >= g.b_rows) continue;
+          const int64_t ap = g.a_pos0 + ai, bp = g.b_pos0 + bi;
+          const int64_t orow = g.trans ? bp : ap, ocol = g.trans ? ap : bp;
+          if (orow < g.q0 || orow >= g.q0 + g.qcount) continue;
+          double rr = mn[i][j][og * 4 + q];
+          rr = rr == DBL_MAX ? __builtin_nan("") : rr;
+          if (rr == rr) {
+            if (g.weighted) rr = rr < 0.0 ? -1.0 : 1.0;  // scaleFactor 1 - 1/(0+1) = 0
+            if (rr < -1.0) rr = -1.0;
+            else if (rr > 1.0) rr = 1.0;
+          }
+          g.out[(orow - g.q0) * g.ldo + ocol] = rr;
+        }
+    }
+}
+
+// Virtual limb rows of the multi-limb owners (positions [0, n_multi)) for
+// the LS-slot layout above; missing limbs and the tail are zero rows.
+__global__ __launch_bounds__(256) void k_vl_build(const int8_t* limb0, const int8_t* hl, const uint8_t* rowLp,
+                                                  int64_t n_multi, int64_t dw, int LS, int8_t* vl) {
+  const int64_t v = blockIdx.x;
+  const int rr = (int)(v & 31), grp = rr >> 3;
+  const int limb = grp % LS;
+  const int64_t o = (v >> 5) * (32 / LS) + (grp / LS) * 8 + (rr & 7);
+  const int8_t* src = nullptr;
+  if (o < n_multi) {
+    if (limb == 0) src = limb0 + o * dw;
+    else if (limb < rowLp[o]) src = hl + (o * (kMaxLimbs - 1) + (limb - 1)) * dw;
+  }
+  int4* dst = reinterpret_cast<int4*>(vl + v * dw);
+  for (int64_t j = threadIdx.x; j < dw / 16; j += 256)
+    dst[j] = src ? reinterpret_cast<const int4*>(src)[j] : make_int4(0, 0, 0, 0);
+}
+
 // ---------------------------------------------------------------- driver --
 
 int cosine_prepare(cms_handle* h) {
@@ -437,6 +664,20 @@ int cosine_prepare(cms_handle* h) {
   CMS_HIP(hipMemcpyAsync(h->h_perm.data(), perm, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipMemcpyAsync(h->h_inv.data(), inv, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
+  // virtual limb rows for the multi-limb x single-limb blocks (k_cosine_big<., LS>)
+  int maxL = 1;
+  for (int64_t t = 0; t * kTile < n_multi; ++t) maxL = std::max<int>(maxL, h->tile_limbs[t]);
+  h->vl_slots = n_multi == 0 ? 0 : maxL <= 2 ? 2 : maxL <= 4 ? 4 : 0;
+  h->vl_rows = 0;
+  if (h->vl_slots) {
+    const int per = 32 / h->vl_slots;  // owners per 32-row block
+    h->vl_rows = (n_multi + per - 1) / per * 32;
+    CMS_HIP(h->ws_vl.ensure((size_t)h->vl_rows * (size_t)dw));
+    TimedScope ts(h, "limb_prep");
+    hipLaunchKernelGGL(k_vl_build, dim3((unsigned)h->vl_rows), dim3(256), 0, h->stream, h->ws_limb0.as<int8_t>(),
+                       h->ws_limbhot.as<int8_t>(), rowLp, n_multi, dw, h->vl_slots, h->ws_vl.as<int8_t>());
+    CMS_HIP(hipGetLastError());
+  }
   h->mfma_ready = true;
   return CMS_OK;
 }
@@ -474,21 +715,125 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   const int64_t trows = (qc + kTile - 1) / kTile;
   a.tiles_x = (int)ntiles;
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_cosine_tile<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_cosine_tile<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    const void* fns[] = {(const void*)k_cosine_tile<false>, (const void*)k_cosine_tile<true>,
+                         (const void*)k_cosine_big<2, 1>,   (const void*)k_cosine_big<3, 1>,
+                         (const void*)k_cosine_big<2, 2>,   (const void*)k_cosine_big<3, 2>,
+                         (const void*)k_cosine_big<2, 4>,   (const void*)k_cosine_big<3, 4>};
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
   const size_t lds = 4 * kTile * kBK + 2 * kTile * sizeof(double);  // 2 buffers x (A + B) + norms
+  const int depth = h->p.depth;
+  const int64_t nm = a.n_multi;
+  const size_t norms = (size_t)depth * (kTA + kTB) * sizeof(double);
+  const int nstage = 3 * (size_t)kStage + norms <= 160 * 1024 ? 3 : 2 * (size_t)kStage + norms <= 160 * 1024 ? 2 : 0;
+  const int64_t qend = q0 + qc;
+
+  if (nstage && (nm == 0 || h->vl_slots)) {
+    // Four blocks of the slab in permuted coordinates (M = multi-limb owners
+    // [0, nm), S = the rest):  S x S and M x S / S x M on k_cosine_big,
+    // M x M on the int64-folding MULTI tile kernel.
+    auto launch = [&](BigArgs g, int ls) -> int {
+      const int oa = kTA / ls;
+      const int64_t tilesA = (g.a_owners + oa - 1) / oa;
+      g.tilesB = (int)((g.b_rows + kTB - 1) / kTB);
+      g.nblk = (int)(tilesA * g.tilesB);
+      if (g.nblk <= 0) return CMS_OK;
+      const size_t bytes = (size_t)nstage * kStage + norms;
+      const dim3 grid((unsigned)g.nblk), blk(512);
+#define CMS_BIG(NS, L) hipLaunchKernelGGL((k_cosine_big<NS, L>), grid, blk, bytes, h->stream, g)
+      if (nstage == 3) {
+        if (ls == 1) CMS_BIG(3, 1);
+        else if (ls == 2) CMS_BIG(3, 2);
+        else CMS_BIG(3, 4);
+      } else {
+        if (ls == 1) CMS_BIG(2, 1);
+        else if (ls == 2) CMS_BIG(2, 2);
+        else CMS_BIG(2, 4);
+      }
+#undef CMS_BIG
+      CMS_HIP(hipGetLastError());
+      return CMS_OK;
+    };
+    BigArgs base{};
+    if (const char* m = getenv("CMS_COS_MODE")) base.mode = atoi(m);  // EXPERIMENT
+    base.perm = a.perm;
+    base.nsqrt = a.nsqrt;
+    base.out = d_out;
+    base.ldo = n;
+    base.q0 = q0;
+    base.qcount = qc;
+    base.dw = dw;
+    base.w = a.w;
+    base.depth = depth;
+    base.weighted = a.weighted;
+    const int64_t slo = std::max(q0, nm);  // single-limb query rows [slo, qend)
+    if (slo < qend && nm < n) {  // S x S
+      BigArgs g = base;
+      g.A = a.limb0 + slo * dw;
+      g.a_vrows = g.a_owners = qend - slo;
+      g.a_pos0 = slo;
+      g.B = a.limb0 + nm * dw;
+      g.b_pos0 = nm;
+      g.b_rows = n - nm;
+      TimedScope ts(h, "cosine_mfma");
+      if ((rc = launch(g, 1))) return rc;
+    }
+    if (nm > 0) {
+      const int ls = h->vl_slots, per = 32 / ls;
+      const int8_t* vl = h->ws_vl.as<int8_t>();
+      TimedScope ts(h, "cosine_mfma_limbs");
+      if (q0 < nm && nm < n) {  // M x S: multi-limb queries against single-limb candidates
+        const int64_t oa0 = q0 / per * per;
+        BigArgs g = base;
+        g.A = vl + (oa0 / per) * 32 * dw;
+        g.a_vrows = h->vl_rows - (oa0 / per) * 32;
+        g.a_pos0 = oa0;
+        g.a_owners = std::min(qend, nm) - oa0;
+        g.B = a.limb0 + nm * dw;
+        g.b_pos0 = nm;
+        g.b_rows = n - nm;
+        if ((rc = launch(g, ls))) return rc;
+      }
+      if (slo < qend) {  // S x M, computed as M x S and written transposed
+        BigArgs g = base;
+        g.A = vl;
+        g.a_vrows = h->vl_rows;
+        g.a_pos0 = 0;
+        g.a_owners = nm;
+        g.B = a.limb0 + slo * dw;
+        g.b_pos0 = slo;
+        g.b_rows = qend - slo;
+        g.trans = 1;
+        if ((rc = launch(g, ls))) return rc;
+      }
+    }
+    // M x M: the 128-tiles holding multi-limb queries and multi-limb candidates
+    std::vector<int2> multi;
+    for (int64_t tr = 0; q0 + tr * kTile < std::min(qend, nm); ++tr)
+      for (int64_t tc = 0; tc * kTile < nm; ++tc) multi.push_back(make_int2((int)tc, (int)tr));
+    if (!multi.empty()) {
+      CMS_HIP(h->ws_tiles.ensure(sizeof(int2) * multi.size()));
+      CMS_HIP(hipMemcpyAsync(h->ws_tiles.ptr, multi.data(), sizeof(int2) * multi.size(), hipMemcpyHostToDevice,
+                             h->stream));
+      TimedScope ts(h, "cosine_mfma_multi");
+      hipLaunchKernelGGL(k_cosine_tile<true>, dim3((unsigned)multi.size()), dim3(256), lds, h->stream, a,
+                         h->ws_tiles.as<int2>(), (int32_t)multi.size());
+      CMS_HIP(hipGetLastError());
+      CMS_HIP(hipStreamSynchronize(h->stream));  // the host tile list must outlive the copy
+    }
+    return CMS_OK;
+  }
+
+  // Legacy 128 x 128 path (depth > 21, or owners needing 5 limbs): the fast
+  // kernel skips tiles touching a multi-limb owner, MULTI takes them.
   {
     TimedScope ts(h, "cosine_mfma");
     hipLaunchKernelGGL(k_cosine_tile<false>, dim3((unsigned)ntiles, (unsigned)trows), dim3(256), lds, h->stream, a,
                        (const int2*)nullptr, 0);
     CMS_HIP(hipGetLastError());
   }
-  // tiles touching a multi-limb owner
   std::vector<int2> multi;
   for (int64_t tr = 0; tr < trows; ++tr)
     for (int64_t tc = 0; tc < ntiles; ++tc)

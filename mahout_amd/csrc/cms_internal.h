@@ -75,6 +75,8 @@ struct cms_handle {
   uint32_t n_hot_limb = 0;      // owners with counters >= 128 (multi-limb)
   uint32_t n_inexact_rows = 0;  // owners with a norm >= 2^53
   std::vector<uint8_t> tile_limbs;   // per permuted 128-row tile: max limb count
+  int32_t vl_slots = 0;         // limb slots per multi-limb owner in ws_vl (2 or 4; 0 = not built)
+  int64_t vl_rows = 0;          // rows of ws_vl
   std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
   int64_t pairs_ingested = 0;
   int32_t exact_norms = 1;
@@ -85,7 +87,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out;
-  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq;
+  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_vl;
 
   // communicator
   ncclComm_t comm = nullptr;

@@ -110,6 +110,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_k(const double* slab, int64
   const uint64_t T = s_prefix;
   const uint32_t ties_needed = s_need;
   const uint32_t ties_total = s_tied;
+  __syncthreads();  // every thread holds T before step 2 reuses s_prefix / s_need
   // ---- 2. among keys == T, the ties_needed-th smallest owner row R ----
   uint64_t R = ~0ULL;
   if (ties_needed < ties_total) {

@@ -260,7 +260,8 @@ def test_bad_row_index_device_path():
         assert ei.value.code == CMS_E_PARAM
 
 
-@pytest.mark.parametrize("n,d,w,vmax,seed", [(700, 5, 256, 5, 31), (260, 4, 128, 50, 32), (129, 3, 512, 1, 33)])
+@pytest.mark.parametrize("n,d,w,vmax,seed", [(700, 5, 256, 5, 31), (260, 4, 128, 50, 32), (129, 3, 512, 1, 33), (3000, 5, 256, 1, 34),
+     (1500, 8, 128, 3, 35), (600, 25, 128, 2, 36)])
 def test_all_pairs_mfma_every_similarity(oracle, n, d, w, vmax, seed):
     """cms_top_k_rows with k = n-1 returns every other owner sorted by
     (similarity desc, ID asc): the whole similarity matrix through the
