@@ -110,7 +110,11 @@ int cms_hash_keys(cms_handle* h, const int64_t* keys, int64_t n, int32_t* out);
 /* COO pairs from host memory, owners by ID. */
 int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t n);
 /* COO pairs already resident on the device, owners by row index. Asynchronous
- * on the handle's stream (use cms_synchronize). */
+ * on the handle's stream (use cms_synchronize).  The handle's stream is a
+ * BLOCKING stream: it is ordered after work already queued on the device's
+ * legacy default stream and before work queued there later.  Buffers written
+ * on any other stream must be complete before the call, and every device
+ * input must stay allocated until cms_synchronize (or a blocking call) returns. */
 int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val,
                            int64_t n);
 /* CSR from host memory: the owner at row r has keys[offsets[r] .. offsets[r+1])
@@ -178,6 +182,8 @@ typedef struct cms_stats {
   int32_t exact_norms;      /* 1 if every (owner,row) norm is < 2^53 (bit-exact fast path) */
   int32_t world, rank;
   int64_t table_bytes;
+  int64_t multi_limb_owners; /* owners with a counter >= 128 (all-pairs limb split; -1 before the first all-pairs call) */
+  int64_t topk_redo;         /* top-k rows that needed the radix-select fallback */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

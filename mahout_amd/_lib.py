@@ -61,6 +61,8 @@ class CmsStats(ctypes.Structure):
         ("world", ctypes.c_int32),
         ("rank", ctypes.c_int32),
         ("table_bytes", ctypes.c_int64),
+        ("multi_limb_owners", ctypes.c_int64),
+        ("topk_redo", ctypes.c_int64),
     ]
 
 

@@ -211,11 +211,12 @@ int cms_create(const cms_params* p, cms_handle** out) {
   hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)p->width;
 
   size_t tbytes = sizeof(uint32_t) * (size_t)h->n * (size_t)h->dw;
-  if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess ||
+  if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
       (e = hipMalloc(&h->d_table, tbytes)) != hipSuccess ||
       (e = hipMalloc(&h->d_row_mass, sizeof(uint64_t) * h->n)) != hipSuccess ||
       (e = hipMalloc(&h->d_norm, sizeof(uint64_t) * h->n * p->depth)) != hipSuccess ||
       (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess ||
+      (e = hipMalloc(&h->d_rowmax, sizeof(uint32_t) * h->n)) != hipSuccess ||
       (e = hipMalloc(&h->d_flags, 64 * sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_flags, 0, 64 * sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_row_mass, 0, sizeof(uint64_t) * h->n)) != hipSuccess) {
@@ -238,7 +239,7 @@ void cms_destroy(cms_handle* h) {
     (void)hipEventDestroy(pe.stop);
   }
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  void* bufs[] = {h->d_table, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_flags, h->d_owner_ids};
+  void* bufs[] = {h->d_table, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
@@ -578,6 +579,8 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->world = h->world;
   out->rank = h->rank;
   out->table_bytes = (int64_t)sizeof(uint32_t) * h->n * h->dw;
+  out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
+  out->topk_redo = h->topk_redo;
   return CMS_OK;
 }
 

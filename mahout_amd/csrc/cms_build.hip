@@ -34,7 +34,7 @@ constexpr int kKeyRegs = 4;  // keys cached per thread: owners up to 1024 keys a
 
 __global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
                              int2* extra_map, uint32_t* counters /* [0]=hot rows [2]=extra slices */,
-                             uint64_t* norm, int depth) {
+                             uint64_t* norm, uint32_t* rowmax, int depth) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
     int64_t c = off[r + 1] - off[r];
     if (c <= slice) {
@@ -48,6 +48,7 @@ __global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, i
     row_hot[r] = (int32_t)hidx;
     for (int32_t s = 1; s < ns; ++s) extra_map[e0 + s - 1] = make_int2((int)hidx, s);
     for (int d = 0; d < depth; ++d) norm[r * depth + d] = 0;
+    rowmax[r] = 0;
   }
 }
 
@@ -65,10 +66,11 @@ __global__ __launch_bounds__(256) void k_zero_hot(const HotInfo* hot, const uint
 __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
     const int64_t* off, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp, int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
-    uint32_t* table, uint64_t* row_mass, uint64_t* norm, uint32_t* flags, int accumulate) {
+    uint32_t* table, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w]
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
+  __shared__ uint32_t s_max;  // largest counter of the row (limb count of the all-pairs operands)
   const int w = (int)hp.width;
   const int64_t dw = (int64_t)hp.depth * w;
   const int tid = threadIdx.x;
@@ -91,7 +93,11 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
   uint32_t* dst = table + row * dw;
   const bool load_old = accumulate && !atomic_mode;
   if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
-  if (tid == 0) s_mass = 0ULL;
+  if (tid == 0) {
+    s_mass = 0ULL;
+    s_max = 0u;
+  }
+  uint32_t vmax = 0;
 
   // keys of small owners: read and reduced once for all d sketch rows
   const bool cached = (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs;
@@ -179,6 +185,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
           uint4 v = l4[j];
           l4[j] = nxt ? n4[j] : make_uint4(0, 0, 0, 0);
           d4[j] = v;
+          vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
           sq = sat_add(sq, (uint64_t)v.x * v.x);
           sq = sat_add(sq, (uint64_t)v.y * v.y);
           sq = sat_add(sq, (uint64_t)v.z * v.z);
@@ -189,6 +196,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
           uint32_t v = lds[j];
           lds[j] = nxt ? nxt[j] : 0u;
           dst_d[j] = v;
+          vmax = max(vmax, v);
           sq = sat_add(sq, (uint64_t)v * v);
         }
       }
@@ -204,8 +212,12 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
   if (badv) atomicOr(flags, kFlagBadValue);
   mass = wave_sum_u64_sat(mass);
   if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, (unsigned long long)mass);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+  if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
   __syncthreads();
   if (!atomic_mode && tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+  if (!atomic_mode && tid == 0) rowmax[row] = s_max;
   if (tid == 0) {
     uint64_t tm = s_mass;
     if (!atomic_mode) {
@@ -221,7 +233,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
 
 // Sum of squares of the hot rows after every slice landed; grid (max_hot, depth, chunks of 1024).
 __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uint32_t* counters, HashParams hp,
-                                                   const uint32_t* table, uint64_t* norm) {
+                                                   const uint32_t* table, uint64_t* norm, uint32_t* rowmax) {
   __shared__ uint64_t red[4];
   if (blockIdx.x >= counters[0]) return;
   const int64_t row = hot[blockIdx.x].row;
@@ -229,8 +241,14 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
   const int w = (int)hp.width;
   const uint32_t* p = table + row * (int64_t)hp.depth * w + (int64_t)d * w;
   uint64_t sq = 0;
-  for (int j = blockIdx.z * 1024 + threadIdx.x; j < min(w, (int)(blockIdx.z + 1) * 1024); j += 256)
+  uint32_t vmax = 0;
+  for (int j = blockIdx.z * 1024 + threadIdx.x; j < min(w, (int)(blockIdx.z + 1) * 1024); j += 256) {
     sq = sat_add(sq, (uint64_t)p[j] * p[j]);
+    vmax = max(vmax, p[j]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+  if ((threadIdx.x & 63) == 0 && vmax) atomicMax(&rowmax[row], vmax);
   uint64_t tot = block_sum_u64_sat(sq, red);
   if (tot > (1ULL << 60)) tot = 1ULL << 60;
   if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
@@ -255,7 +273,7 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
     TimedScope ts(h, "build_plan");
     unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
     hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_off, n, kSlice, row_hot, hot, extra_map,
-                       counters, h->d_norm, h->p.depth);
+                       counters, h->d_norm, h->d_rowmax, h->p.depth);
     if (!accumulate)
       hipLaunchKernelGGL(k_zero_hot, dim3((unsigned)max_hot, (unsigned)h->p.depth), dim3(256), 0, h->stream, hot,
                          counters, h->hp, h->d_table);
@@ -266,13 +284,14 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
     TimedScope ts(h, "build_rows");
     hipLaunchKernelGGL(k_build_rows, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_off, d_key,
                        d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->d_table, h->d_row_mass,
-                       h->d_norm, h->d_flags, accumulate);
+                       h->d_norm, h->d_rowmax, h->d_flags, accumulate);
     CMS_HIP(hipGetLastError());
   }
   {
     TimedScope ts(h, "hot_norms");
     dim3 grid((unsigned)max_hot, (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
-    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->d_table, h->d_norm);
+    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->d_table, h->d_norm,
+                       h->d_rowmax);
     CMS_HIP(hipGetLastError());
   }
   h->empty = false;

@@ -41,32 +41,21 @@ constexpr int kMaxLimbs = 5;    // 35 bits >= any u32 counter
 
 // ------------------------------------------------------------ preparation --
 
-// Per owner row: limb count (max counter), multi-limb flag, inexact-norm count.
-__global__ __launch_bounds__(256) void k_limb_count(const uint32_t* table, int64_t dw, const uint64_t* norm,
+// Per owner row: limb count (from the largest counter, which the norm
+// passes record), multi-limb flag, inexact-norm count.
+__global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int64_t nrows, const uint64_t* norm,
                                                     int depth, uint8_t* rowL, uint32_t* multi_flag,
                                                     uint32_t* inexact_rows) {
-  __shared__ uint32_t smax[4];
-  const int64_t row = blockIdx.x;
-  const uint32_t* src = table + row * dw;
-  uint32_t mx = 0;
-  for (int64_t j = threadIdx.x * 4; j < dw; j += 256 * 4) {
-    uint4 v = *reinterpret_cast<const uint4*>(src + j);
-    mx = max(mx, max(max(v.x, v.y), max(v.z, v.w)));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-  if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    mx = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
-    int L = 1;
-    while (L < kMaxLimbs && (mx >> (7 * L)) != 0) ++L;
-    rowL[row] = (uint8_t)L;
-    multi_flag[row] = L > 1 ? 1u : 0u;
-    bool inexact = false;
-    for (int d = 0; d < depth; ++d) inexact |= norm[row * depth + d] >= (1ULL << 53);
-    if (inexact) atomicAdd(inexact_rows, 1u);
-  }
+  const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (row >= nrows) return;
+  const uint32_t mx = rowmax[row];
+  int L = 1;
+  while (L < kMaxLimbs && (mx >> (7 * L)) != 0) ++L;
+  rowL[row] = (uint8_t)L;
+  multi_flag[row] = L > 1 ? 1u : 0u;
+  bool inexact = false;
+  for (int d = 0; d < depth; ++d) inexact |= norm[row * depth + d] >= (1ULL << 53);
+  if (inexact) atomicAdd(inexact_rows, 1u);
 }
 
 // Stable multi-first permutation from the exclusive scan of the multi flags.
@@ -632,8 +621,8 @@ int cosine_prepare(cms_handle* h) {
   uint32_t host[3];
   {
     TimedScope ts(h, "limb_prep");
-    hipLaunchKernelGGL(k_limb_count, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, dw, h->d_norm,
-                       h->p.depth, rowL, mflag, cnt);
+    hipLaunchKernelGGL(k_limb_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->d_rowmax, n,
+                       h->d_norm, h->p.depth, rowL, mflag, cnt);
     int rc = scan_exclusive_u32(h, mflag, mpos, n, bsum);
     if (rc) return rc;
     CMS_HIP(hipGetLastError());

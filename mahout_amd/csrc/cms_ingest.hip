@@ -177,11 +177,14 @@ __global__ void k_ingest_atomic(const int64_t* row, const int64_t* key, const fl
 
 // --------------------------------------------------------- norms pass ----
 
-__global__ __launch_bounds__(256) void k_norms(const uint32_t* table, int64_t nrows, HashParams hp, uint64_t* norm) {
+__global__ __launch_bounds__(256) void k_norms(const uint32_t* table, int64_t nrows, HashParams hp, uint64_t* norm,
+                                               uint32_t* rowmax) {
   __shared__ uint64_t red[4];
+  __shared__ uint32_t smax[4];
   const int64_t dw = (int64_t)hp.depth * hp.width;
   const int w = (int)hp.width;
   for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+    uint32_t vmax = 0;
     for (int d = 0; d < hp.depth; ++d) {
       const uint32_t* p = table + row * dw + (int64_t)d * w;
       uint64_t sq = 0;
@@ -189,17 +192,27 @@ __global__ __launch_bounds__(256) void k_norms(const uint32_t* table, int64_t nr
         const uint4* p4 = reinterpret_cast<const uint4*>(p);
         for (int j = threadIdx.x; j < (w >> 2); j += blockDim.x) {
           uint4 v = p4[j];
+          vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
           sq = sat_add(sq, (uint64_t)v.x * v.x);
           sq = sat_add(sq, (uint64_t)v.y * v.y);
           sq = sat_add(sq, (uint64_t)v.z * v.z);
           sq = sat_add(sq, (uint64_t)v.w * v.w);
         }
       } else {
-        for (int j = threadIdx.x; j < w; j += blockDim.x) sq = sat_add(sq, (uint64_t)p[j] * p[j]);
+        for (int j = threadIdx.x; j < w; j += blockDim.x) {
+          sq = sat_add(sq, (uint64_t)p[j] * p[j]);
+          vmax = max(vmax, p[j]);
+        }
       }
       uint64_t tot = block_sum_u64_sat(sq, red);
       if (threadIdx.x == 0) norm[row * hp.depth + d] = tot;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) rowmax[row] = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+    __syncthreads();
   }
 }
 
@@ -217,7 +230,8 @@ int compute_norms(cms_handle* h) {
   TimedScope ts(h, "norms");
   if (!h->norms_valid) {
     unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
-    if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->n, h->hp, h->d_norm);
+    if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->n, h->hp, h->d_norm,
+                                     h->d_rowmax);
     CMS_HIP(hipGetLastError());
     h->norms_valid = true;
   }

@@ -63,6 +63,7 @@ struct cms_handle {
   uint64_t* d_row_mass = nullptr;   // [n] total increment mass per row
   uint64_t* d_norm = nullptr;       // [n][d] exact sum of squares (saturating)
   double* d_norm_sqrt = nullptr;    // [n][d] Math.sqrt((double) norm)
+  uint32_t* d_rowmax = nullptr;     // [n] largest counter of the owner (valid with the norms)
   uint32_t* d_flags = nullptr;      // error flags word + counters
   int64_t* d_owner_ids = nullptr;   // [n] sorted IDs (null => identity)
   std::vector<int64_t> h_owner_ids;
@@ -77,6 +78,7 @@ struct cms_handle {
   std::vector<uint8_t> tile_limbs;   // per permuted 128-row tile: max limb count
   int32_t vl_slots = 0;         // limb slots per multi-limb owner in ws_vl (2 or 4; 0 = not built)
   int64_t vl_rows = 0;          // rows of ws_vl
+  int64_t topk_redo = 0;        // top-k rows the sampled threshold missed (radix-select redo)
   std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
   int64_t pairs_ingested = 0;
   int32_t exact_norms = 1;

@@ -195,16 +195,219 @@ __global__ __launch_bounds__(kTopThreads) void k_top_k(const double* slab, int64
   if (tid == 0) counts[Q.out_pos] = (int32_t)kk;
 }
 
+// ---- one-pass top-k: sampled threshold, candidate gather, LDS sort ----
+// bucket(s) is monotone in s, so every score in a bucket >= t outranks every
+// score below it: the first k of the candidates with bucket >= t (sorted by
+// the same total order) are the first k of the row whenever at least k
+// candidates exist.  t comes from a 1/32 sample of the row, aiming at ~2k+64
+// candidates; rows where the guess misses (fewer than k, or more than
+// kCand) are flagged with count -1 and redone by k_top_k.
+constexpr int kBins = 4096;
+constexpr int kCand = 2048;
+constexpr int kSampleSeg = 256;  // sample = one 256-column segment in every 32
+
+__device__ __forceinline__ int score_bucket(double s) {
+  const int b = (int)((s + 1.0) * (kBins / 2));
+  return b < 0 ? 0 : (b >= kBins ? kBins - 1 : b);
+}
+
+__global__ __launch_bounds__(kTopThreads) void k_top_k_fast(const double* slab, int64_t ld, int64_t n, int32_t k,
+                                                             const TopQuery* queries, const int64_t* perm,
+                                                             const int64_t* owner_ids, int64_t* out_ids,
+                                                             double* out_scores, int32_t* counts) {
+  __shared__ uint32_t hist[kBins];
+  __shared__ uint64_t ckey[kCand];
+  __shared__ uint32_t crow[kCand];
+  __shared__ uint32_t ccol[kCand];
+  __shared__ uint32_t wsum[kTopThreads / 64];
+  __shared__ uint32_t s_cnt;
+  __shared__ int s_t;
+
+  const TopQuery Q = queries[blockIdx.x];
+  const double* sc = slab + Q.slab_row * ld;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kBins; i += kTopThreads) hist[i] = 0;
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  // 1. sample histogram
+  const int64_t nseg = (n + kSampleSeg - 1) / kSampleSeg;
+  uint32_t sampled = 0;
+  for (int64_t base = 0; base < nseg; base += 32 * (kTopThreads / kSampleSeg)) {
+    const int64_t sg = base + 32 * (tid / kSampleSeg);  // every 32nd segment, 4 per pass
+    const int64_t j = sg * kSampleSeg + (tid & (kSampleSeg - 1));
+    if (sg >= nseg || j >= n) continue;
+    const double s = sc[j];
+    if (j == Q.self_col || s != s) continue;
+    atomicAdd(&hist[score_bucket(s)], 1u);
+    ++sampled;
+  }
+  const uint32_t nsample = block_count(sampled, wsum);
+  // 2. threshold bucket: highest t whose sampled tail, scaled up, reaches 2k + 64
+  if (tid == 0) {
+    const double scale = (double)n / (double)max<int64_t>(1, min<int64_t>(n, ((nseg + 31) / 32) * kSampleSeg));
+    const double want = 2.0 * k + 64.0;
+    uint32_t tail = 0;
+    int t = kBins - 1;
+    for (; t > 0; --t) {
+      tail += hist[t];
+      if ((double)tail * scale >= want) break;
+    }
+    s_t = nsample == 0 ? 0 : t;
+  }
+  __syncthreads();
+  const int t = s_t;
+  // 3. one pass over the row: count valid, gather candidates with bucket >= t
+  uint32_t valid = 0;
+  for (int64_t j0 = 0; j0 < n; j0 += 4 * kTopThreads) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = j0 + u * kTopThreads + tid;
+      v[u] = j < n ? sc[j] : __builtin_nan("");
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = j0 + u * kTopThreads + tid;
+      const double s = v[u];
+      if (j == Q.self_col || s != s) continue;
+      ++valid;
+      if (score_bucket(s) < t) continue;
+      const uint32_t pos = atomicAdd(&s_cnt, 1u);
+      if (pos < kCand) {
+        ckey[pos] = score_key(s);
+        crow[pos] = (uint32_t)(perm ? perm[j] : j);
+        ccol[pos] = (uint32_t)j;
+      }
+    }
+  }
+  const uint32_t nvalid = block_count(valid, wsum);
+  uint32_t cnt = s_cnt;
+  const uint32_t kk = (uint32_t)min<int64_t>(k, nvalid);
+  if (kk == 0) {
+    if (tid == 0) counts[Q.out_pos] = 0;
+    return;
+  }
+  if (cnt < kk || cnt > (uint32_t)kCand) {
+    // The sampled guess missed.  Histogram the side of t that holds the k-th
+    // score (below t when too few candidates, at/above t when too many),
+    // place the exact threshold bucket, and gather again.
+    const bool below = cnt < kk;
+    for (int i = tid; i < kBins; i += kTopThreads) hist[i] = 0;
+    __syncthreads();
+    for (int64_t j = tid; j < n; j += kTopThreads) {
+      const double s = sc[j];
+      if (j == Q.self_col || s != s) continue;
+      const int b = score_bucket(s);
+      if ((b < t) == below) atomicAdd(&hist[b], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t tail = below ? cnt : 0;
+      int b = below ? t - 1 : kBins - 1;
+      for (; b > 0; --b) {
+        tail += hist[b];
+        if (tail >= kk) break;
+      }
+      if (b == 0 && tail < kk) tail += hist[0];
+      s_t = b;
+      s_cnt = 0;
+      wsum[0] = tail;  // candidates at bucket >= b
+    }
+    __syncthreads();
+    const int t2 = s_t;
+    const uint32_t need = wsum[0];
+    __syncthreads();
+    if (need > (uint32_t)kCand) {  // one bucket too dense to hold: radix select redo
+      if (tid == 0) counts[Q.out_pos] = -1;
+      return;
+    }
+    for (int64_t j = tid; j < n; j += kTopThreads) {
+      const double s = sc[j];
+      if (j == Q.self_col || s != s || score_bucket(s) < t2) continue;
+      const uint32_t pos = atomicAdd(&s_cnt, 1u);
+      if (pos < kCand) {
+        ckey[pos] = score_key(s);
+        crow[pos] = (uint32_t)(perm ? perm[j] : j);
+        ccol[pos] = (uint32_t)j;
+      }
+    }
+    __syncthreads();
+    cnt = s_cnt;
+  }
+  // 4. bitonic sort of the candidates by (key desc, row asc)
+  uint32_t P = 1;
+  while (P < cnt) P <<= 1;
+  for (uint32_t i = cnt + tid; i < P; i += kTopThreads) {
+    ckey[i] = 0;
+    crow[i] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = tid; i < P; i += kTopThreads) {
+        const uint32_t jx = i ^ stride;
+        if (jx > i) {
+          const bool up = (i & size) == 0;
+          const bool i_first = ckey[i] > ckey[jx] || (ckey[i] == ckey[jx] && crow[i] < crow[jx]);
+          if (up != i_first) {
+            const uint64_t tk = ckey[i];
+            ckey[i] = ckey[jx];
+            ckey[jx] = tk;
+            const uint32_t tr = crow[i];
+            crow[i] = crow[jx];
+            crow[jx] = tr;
+            const uint32_t tc = ccol[i];
+            ccol[i] = ccol[jx];
+            ccol[jx] = tc;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = tid; i < kk; i += kTopThreads) {
+    out_ids[Q.out_pos * k + i] = owner_ids ? owner_ids[crow[i]] : (int64_t)crow[i];
+    out_scores[Q.out_pos * k + i] = sc[ccol[i]];
+  }
+  if (tid == 0) counts[Q.out_pos] = (int32_t)kk;
+}
+
 static int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k,
                         const int64_t* d_perm, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
   if (qs.empty()) return CMS_OK;
   CMS_HIP(h->ws_topq.ensure(sizeof(TopQuery) * qs.size()));
   CMS_HIP(hipMemcpyAsync(h->ws_topq.ptr, qs.data(), sizeof(TopQuery) * qs.size(), hipMemcpyHostToDevice, h->stream));
+  const bool fast = h->n < (int64_t(1) << 32);  // candidate rows/columns held as u32
   {
     TimedScope ts(h, "top_k");
-    hipLaunchKernelGGL(k_top_k, dim3((unsigned)qs.size()), dim3(kTopThreads), 0, h->stream, slab, h->n, h->n, k,
-                       h->ws_topq.as<TopQuery>(), d_perm, h->d_owner_ids, d_ids, d_scores, d_counts);
+    if (fast)
+      hipLaunchKernelGGL(k_top_k_fast, dim3((unsigned)qs.size()), dim3(kTopThreads), 0, h->stream, slab, h->n, h->n,
+                         k, h->ws_topq.as<TopQuery>(), d_perm, h->d_owner_ids, d_ids, d_scores, d_counts);
+    else
+      hipLaunchKernelGGL(k_top_k, dim3((unsigned)qs.size()), dim3(kTopThreads), 0, h->stream, slab, h->n, h->n, k,
+                         h->ws_topq.as<TopQuery>(), d_perm, h->d_owner_ids, d_ids, d_scores, d_counts);
     CMS_HIP(hipGetLastError());
+  }
+  if (fast) {  // rows the sampled threshold missed go through the radix select
+    std::vector<TopQuery> redo;
+    // counts are indexed by out_pos; gather them per query
+    std::vector<int32_t> all;
+    int64_t maxpos = 0;
+    for (const TopQuery& q : qs) maxpos = std::max(maxpos, q.out_pos);
+    all.resize(maxpos + 1);
+    CMS_HIP(hipMemcpyAsync(all.data(), d_counts, sizeof(int32_t) * (maxpos + 1), hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    for (const TopQuery& q : qs)
+      if (all[q.out_pos] < 0) redo.push_back(q);
+    h->topk_redo += (int64_t)redo.size();
+    if (!redo.empty()) {
+      CMS_HIP(hipMemcpyAsync(h->ws_topq.ptr, redo.data(), sizeof(TopQuery) * redo.size(), hipMemcpyHostToDevice,
+                             h->stream));
+      TimedScope ts(h, "top_k");
+      hipLaunchKernelGGL(k_top_k, dim3((unsigned)redo.size()), dim3(kTopThreads), 0, h->stream, slab, h->n, h->n, k,
+                         h->ws_topq.as<TopQuery>(), d_perm, h->d_owner_ids, d_ids, d_scores, d_counts);
+      CMS_HIP(hipGetLastError());
+    }
   }
   CMS_HIP(hipStreamSynchronize(h->stream));  // host query list and ws reuse
   return CMS_OK;
@@ -216,7 +419,8 @@ int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, i
   const int64_t n = h->n;
   int rc = CMS_OK;
   if (mfma_eligible(h) && (rc = cosine_prepare(h))) return rc;
-  const int64_t slab_rows = std::max<int64_t>(128, ((int64_t(1) << 28) / std::max<int64_t>(1, n)) / 128 * 128);
+  // slab budget: 2^30 fp64 similarities (8 GiB) -- 1,024 query rows at 1M owners
+  const int64_t slab_rows = std::max<int64_t>(128, ((int64_t(1) << 30) / std::max<int64_t>(1, n)) / 128 * 128);
   if (mfma_eligible(h) && h->n_inexact_rows == 0) {
     // MFMA slabs over PERMUTED 128-row query tiles that hold a requested owner
     std::vector<int64_t> tiles;

@@ -26,6 +26,17 @@ def _dev_ptr(x):
     return ctypes.c_void_p(x.data_ptr())
 
 
+def _producers_done(*xs):
+    """The library's stream does not order against torch's (possibly
+    non-default) current stream: wait for the kernels that wrote the inputs."""
+    import torch
+
+    for x in xs:
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            torch.cuda.current_stream(x.device).synchronize()
+            return
+
+
 def shape_from_delta_epsilon(delta, epsilon):
     """AbstractCountMinSketch(delta, epsilon) shape rule -> (width, depth)."""
     lib = _lib.load()
@@ -112,7 +123,9 @@ class SketchTable:
         check(self._lib.cms_ingest(self._h, _ptr(owner), _ptr(key), _ptr(v), owner.size))
 
     def ingest_device_rows(self, d_row, d_key, d_val, n):
+        _producers_done(d_row, d_key, d_val)
         check(self._lib.cms_ingest_device_rows(self._h, _dev_ptr(d_row), _dev_ptr(d_key), _dev_ptr(d_val), int(n)))
+        self.synchronize()  # the inputs may be freed once this returns
 
     def ingest_csr(self, offsets, keys, vals=None):
         offsets = np.ascontiguousarray(offsets, np.int64)
@@ -123,7 +136,9 @@ class SketchTable:
         check(self._lib.cms_ingest_csr(self._h, _ptr(offsets), _ptr(keys), _ptr(v)))
 
     def ingest_csr_device(self, d_offsets, d_keys, d_vals=None):
+        _producers_done(d_offsets, d_keys, d_vals)
         check(self._lib.cms_ingest_csr_device(self._h, _dev_ptr(d_offsets), _dev_ptr(d_keys), _dev_ptr(d_vals)))
+        self.synchronize()  # the inputs may be freed once this returns
 
     def reset(self):
         check(self._lib.cms_reset(self._h))

@@ -254,9 +254,11 @@ def test_bad_row_index_device_path():
     with SketchTable(10, depth=2, width=64) as t:
         rows = torch.tensor([0, 1, 10], dtype=torch.int64, device="cuda")
         keys = torch.tensor([1, 2, 3], dtype=torch.int64, device="cuda")
-        t.ingest_device_rows(rows, keys, None, 3)
+        # device ingest is asynchronous in the C ABI; the Python wrapper
+        # synchronizes (the inputs may be freed after it returns), so the
+        # bad row surfaces from the ingest call itself
         with pytest.raises(CmsError) as ei:
-            t.synchronize()
+            t.ingest_device_rows(rows, keys, None, 3)
         assert ei.value.code == CMS_E_PARAM
 
 
@@ -285,3 +287,49 @@ def test_all_pairs_mfma_every_similarity(oracle, n, d, w, vmax, seed):
             assert same(sc[q - 5, :cnt[q - 5]], esc), q
     if vmax > 1:
         assert ot.max() > 127  # multi-limb owners were exercised
+
+
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_top_k_small_k_sampled_threshold(oracle, k):
+    """k << n: the one-pass sampled-threshold top-k against TopItems.getTopUsers."""
+    n, d, w = 3000, 4, 256
+    items, users = zipf_stream(5000, n, 400_000, seed=40 + k)
+    ot = oracle_table(oracle, n, d, w, 42, items, users)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        ids, sc, cnt = t.top_k_rows(0, n, k)
+        for q in list(range(0, n, 97)) + [n - 1]:
+            sims = _oracle_row_sims(oracle, ot, q)
+            eids, esc = oracle.top_users(np.arange(n), sims, k)
+            assert ids[q, :cnt[q]].tolist() == eids.tolist(), q
+            assert same(sc[q, :cnt[q]], esc), q
+
+
+def test_top_k_heavy_ties(oracle):
+    """Many owners with identical sketches: long runs of equal scores, broken
+    by owner ID (SimilarUser.compareTo)."""
+    n, d, w = 1500, 3, 128
+    rng = np.random.Generator(np.random.PCG64(77))
+    # owners in groups of 50 share one user profile
+    rows, keys = [], []
+    for o in range(n):
+        g = o // 50
+        prof = np.random.Generator(np.random.PCG64(g)).integers(0, 400, size=6)
+        rows.append(np.full(prof.size, o))
+        keys.append(prof)
+    rows = np.concatenate(rows).astype(np.int64)
+    keys = np.concatenate(keys).astype(np.int64)
+    perm = rng.permutation(rows.size)
+    rows, keys = rows[perm], keys[perm]
+    ot = oracle_table(oracle, n, d, w, 42, rows, keys)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(rows, keys)
+        t.finalize()
+        for k in (5, 60, 300):
+            ids, sc, cnt = t.top_k_rows(0, n, k)
+            for q in range(0, n, 71):
+                sims = _oracle_row_sims(oracle, ot, q)
+                eids, esc = oracle.top_users(np.arange(n), sims, k)
+                assert ids[q, :cnt[q]].tolist() == eids.tolist(), (k, q)
+                assert same(sc[q, :cnt[q]], esc), (k, q)
