@@ -119,7 +119,10 @@ INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense peak),
 
 def allpairs_measure(table, row_begin, row_count, k, n, d, w):
     """cms_top_k_rows over [row_begin, row_begin+row_count): every query row
-    against all n owners (n^2-shaped slab, no symmetry), HIP-event kernel times."""
+    against all n owners (n^2-shaped slab, no symmetry), HIP-event kernel times.
+    Kernels: cosine_mfma = single-limb x single-limb 256x128 tiles (the bulk),
+    cosine_mfma_limbs = multi-limb owners as virtual limb rows (M x S, S x M),
+    cosine_mfma_multi = multi x multi 128-tiles (int64 folding), top_k."""
     table.set_timing(True)
     table.top_k_rows(row_begin, min(row_count, 128), k)  # operands prepared, kernels warm
     table.reset_timing()
@@ -127,19 +130,26 @@ def allpairs_measure(table, row_begin, row_count, k, n, d, w):
     _, _, cnt = table.top_k_rows(row_begin, row_count, k)
     wall = time.perf_counter() - t0
     mf, nf = table.timing("cosine_mfma")
+    ml, _ = table.timing("cosine_mfma_limbs")
     mm, nm = table.timing("cosine_mfma_multi")
     tk, _ = table.timing("top_k")
     table.set_timing(False)
+    st = table.stats()
+    n_multi = max(0, int(st["multi_limb_owners"]))
     pairs = row_count * n
     ops = pairs * 2 * d * w
-    kern_s = (mf + mm) * 1e-3
+    ops_ss = row_count * (n - n_multi) * 2 * d * w  # query rows here are single-limb owners
+    kern_s = (mf + ml + mm) * 1e-3
     return {
         "query_rows": row_count, "candidates": n, "k": k, "wall_s": wall,
         "ordered_pairs_per_s": pairs / wall,
         "unique_item_pair_cosines_per_s": pairs / 2 / wall,
-        "mfma_ms": mf, "mfma_multi_limb_ms": mm, "multi_limb_launches": nm, "top_k_ms": tk,
-        "mfma_TOPS": ops / kern_s / 1e12 if kern_s else None,
-        "mfma_frac_int8_peak": ops / kern_s / 1e12 / INT8_MFMA_PEAK_TOPS if kern_s else None,
+        "multi_limb_owners": n_multi, "top_k_redo_rows": int(st["topk_redo"]),
+        "mfma_ms": mf, "mfma_limb_rows_ms": ml, "mfma_multi_multi_ms": mm, "top_k_ms": tk,
+        "single_limb_kernel_TOPS": ops_ss / (mf * 1e-3) / 1e12 if mf else None,
+        "single_limb_kernel_frac_int8_peak": ops_ss / (mf * 1e-3) / 1e12 / INT8_MFMA_PEAK_TOPS if mf else None,
+        "all_cosine_kernels_TOPS": ops / kern_s / 1e12 if kern_s else None,
+        "all_cosine_kernels_frac_int8_peak": ops / kern_s / 1e12 / INT8_MFMA_PEAK_TOPS if kern_s else None,
         "returned_full_lists": int((cnt == k).sum()),
     }
 

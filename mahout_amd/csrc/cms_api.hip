@@ -245,7 +245,7 @@ void cms_destroy(cms_handle* h) {
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
-                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->ws_vl};
+                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->ws_vl, &h->ws_nsq};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;

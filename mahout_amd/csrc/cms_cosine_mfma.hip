@@ -90,6 +90,15 @@ __global__ __launch_bounds__(256) void k_limb_write(const uint32_t* table, int64
   }
 }
 
+// sqrt norms in PERMUTED order, row-major by sketch row: nsq_t[r][p] =
+// nsqrt[perm[p]][r], so a panel's norms are one contiguous run per row.
+__global__ void k_perm_norms(const double* nsqrt, const int64_t* perm, int64_t n, int depth, double* nsq_t) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t o = perm[p];
+    for (int r = 0; r < depth; ++r) nsq_t[(int64_t)r * n + p] = nsqrt[o * depth + r];
+  }
+}
+
 __global__ void k_tile_limbs(const uint8_t* rowL, int64_t nrows, uint8_t* tileL) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t r0 = t * kTile;
@@ -390,7 +399,22 @@ __global__ __launch_bounds__(256, MULTI ? 1 : 2) void k_cosine_tile(CosArgs a, c
 // slab entries (query = B row), which is how single-limb queries meet
 // multi-limb candidates: cosine(a, b) == cosine(b, a) bit for bit.
 constexpr int kTA = 256, kTB = 128;
-constexpr int kStageA = kTA * kBK, kStageB = kTB * kBK, kStage = kStageA + kStageB;
+
+// LDS image of a BK-byte K slice of R rows: row-major, the 16-B chunk index
+// XOR-swizzled so that each 16-lane ds_read_b128 group (16 consecutive rows,
+// one chunk) hits 16 distinct 16-B slots of a 256-B bank line.
+template <int BK>
+__device__ __forceinline__ int lds_off_bk(int row, int ch) {
+  if constexpr (BK == 128) return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
+  else return row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);  // BK == 64
+}
+
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt fields at their maxima), gfx9 encoding.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
 
 struct BigArgs {
   const int8_t* A;      // operand rows (limb0 image or ws_vl), first row of this launch
@@ -401,7 +425,8 @@ struct BigArgs {
   int64_t b_pos0;       // permuted position of B's first row
   int64_t b_rows;       // candidates covered
   const int64_t* perm;  // permuted position -> owner row
-  const double* nsqrt;  // [n][d] by owner row
+  const double* nsq_t;  // [d][n] sqrt norms by PERMUTED position (row stride n)
+  int64_t n;
   double* out;          // slab [qcount][ldo]
   int64_t ldo;
   int64_t q0, qcount;   // slab rows = permuted positions [q0, q0 + qcount)
@@ -412,39 +437,63 @@ struct BigArgs {
   int32_t mode;  // EXPERIMENT: bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
 };
 
-template <int NSTAGE, int LS>
+template <int NSTAGE, int LS, int BK>
 __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
+  static_assert(BK == 128 || BK == 64, "stage depth");
   constexpr int OA = kTA / LS;  // owners per A panel
   constexpr int OG = 4 / LS;    // owner groups per 32-row block in one lane
+  constexpr int kStageA = kTA * BK, kStageB = kTB * BK, kStage = kStageA + kStageB;
+  constexpr int RPI = 1024 / BK;            // rows per 1-KiB LDS-DMA instruction
+  constexpr int OPA = kTA / RPI / 8;        // A instructions per wave per stage
+  constexpr int OPB = kTB / RPI / 8;        // B instructions per wave per stage
+  constexpr int OPS = OPA + OPB;
   extern __shared__ __align__(16) unsigned char lds[];
   const int depth = g.depth;
-  double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][OA]
-  double* s_sb = s_sa + depth * OA;                                  // [depth][128]
+  double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][256] (OA used)
+  double* s_sb = s_sa + depth * kTA;                                 // [depth][128]
   const int nblk = g.nblk;
   const int bx = blockIdx.x, xcd = bx & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
-  const int ta = lin / g.tilesB, tb = lin % g.tilesB;
+  // A panel fastest: an XCD's co-resident workgroups cover a few candidate
+  // tiles x every query panel, so both operands mostly hit the XCD's L2 and
+  // each candidate tile leaves HBM once per launch.
+  const int tilesA = g.nblk / g.tilesB;
+  const int ta = lin % tilesA, tb = lin / tilesA;
   const int64_t vrow0 = (int64_t)ta * kTA;  // first operand row of the A panel
   const int64_t own0 = (int64_t)ta * OA;    // first owner (relative to a_pos0)
   const int64_t bcol0 = (int64_t)tb * kTB;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
   const int w = g.w;
-  const int cstages = w / kBK;
+  const int cstages = w / BK;
   const int total = depth * cstages;
 
-  for (int i = tid; i < depth * OA; i += 512) {
-    const int r = i / OA, t = i % OA;
-    const int64_t o = own0 + t;
-    s_sa[i] = o < g.a_owners ? g.nsqrt[g.perm[g.a_pos0 + o] * depth + r] : 0.0;
+  if (g.mode & 32) return;  // EXPERIMENT: launch cost only
+  if (g.mode & 64) {        // EXPERIMENT: skeleton loop only
+    for (int s = 0; s < total; ++s) __builtin_amdgcn_s_barrier();
+    return;
   }
-  for (int i = tid; i < depth * kTB; i += 512) {
-    const int r = i / kTB, t = i % kTB;
-    const int64_t c = bcol0 + t;
-    s_sb[i] = c < g.b_rows ? g.nsqrt[g.perm[g.b_pos0 + c] * depth + r] : 0.0;
+  // sqrt norms of the panel's owners, straight into LDS by LDS-DMA (256 B
+  // per instruction, past-the-end owners land as zeros).  Issued before the
+  // first stages, so the stage-0 vmcnt wait covers them, and the first
+  // epilogue runs behind at least one barrier.
+  for (int k = wid; k < 12 * depth; k += 8) {
+    const int r = k / 12, part = k % 12;  // parts 0..7: A (8 x 32 owners), 8..11: B (4 x 32)
+    const bool isA = part < 8;
+    const int64_t first = isA ? own0 + part * 32 : bcol0 + (part - 8) * 32;
+    const int64_t lim = isA ? min<int64_t>(g.a_owners, own0 + OA) : g.b_rows;
+    const int64_t cnt = max<int64_t>(0, min<int64_t>(32, lim - first));
+    const double* src = g.nsq_t + (int64_t)r * g.n + (isA ? g.a_pos0 : g.b_pos0) + first;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * 8), 0x00020000);
+    double* dst = isA ? s_sa + r * kTA + part * 32 : s_sb + r * kTB + (part - 8) * 32;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (g.mode & 128) {  // EXPERIMENT: norms only
+    wait_vmcnt<0>();
+    return;
+  }
 
   // buffer descriptors bound the panel: rows past the end land as zeros
   const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, g.a_vrows - vrow0));
@@ -453,23 +502,28 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + vrow0 * g.dw), (short)0, (int)(rowsA * g.dw), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.B + bcol0 * g.dw), (short)0, (int)(rowsB * g.dw), 0x00020000);
-  // staging row of lane for op u: wid*8 + (lane>>3) + 64u.  The 64-row step
-  // leaves the swizzle unchanged, so one voffset per lane serves every op and
-  // the row step rides in the voffset as a constant add.
-  const int srow = wid * 8 + (lane >> 3);
-  const int32_t vo = (int32_t)(srow * g.dw) + (((lane & 7) ^ ((srow >> 1) & 7)) << 4);
-  const int32_t rstep = 64 * (int32_t)g.dw;
+  // Instruction u of wave wid fills LDS rows [(wid + 8u) * RPI, +RPI); lane
+  // i lands at byte 16 i, i.e. row (wid + 8u) * RPI + i / (BK/16), slot
+  // i % (BK/16), and fetches the chunk the swizzle puts there.  The 8*RPI-row
+  // step leaves the swizzle unchanged, so one voffset per lane serves every
+  // instruction and the row step is a constant add.
+  constexpr int CPR = BK / 16;  // 16-B chunks per row
+  const int srow = wid * RPI + lane / CPR;
+  const int slot = lane % CPR;
+  const int32_t vo = (int32_t)(srow * g.dw) +
+                     ((BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4);
+  const int32_t rstep = 8 * RPI * (int32_t)g.dw;
   auto issue = [&](int s) {
     if (g.mode & 1) return;
     const int r = s / cstages, cs = s - r * cstages;
-    const int32_t koff = r * w + cs * kBK;
+    const int32_t koff = r * w + cs * BK;
     unsigned char* st = lds + (s % NSTAGE) * kStage;
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < OPA; ++u)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + 8 * u) * 1024),
                                                16, vo + u * rstep, koff, 0, 0);
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < OPB; ++u)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + 8 * u) * 1024), 16, vo + u * rstep,
           koff, 0, 0);
@@ -492,29 +546,27 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     if (s < total) issue(s);
 
   for (int s = 0; s < total; ++s) {
-    // stage s landed: at most the (NSTAGE-2) younger stages (6 ops each) stay in flight
-    if (s + NSTAGE - 2 < total) {
-      if constexpr (NSTAGE == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // stage s landed: at most the (NSTAGE-2) younger stages (OPS ops each) stay in flight
+    asm volatile("" ::: "memory");
+    if (s + NSTAGE - 2 < total) wait_vmcnt<OPS * (NSTAGE - 2)>();
+    else wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if (!(g.mode & 8)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);  // refill the slot read in iteration s-1
     const unsigned char* A = lds + (s % NSTAGE) * kStage;
     const unsigned char* B = A + kStageA;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int ks = 0; ks < BK / 32; ++ks) {
       if (g.mode & 2) break;
       const int ch = 2 * ks + (lane >> 5);
       i8x16 fa[2], fb[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off(wr * 64 + i * 32 + (lane & 31), ch));
+        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off(wc * 64 + j * 32 + (lane & 31), ch));
+        fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 64 + j * 32 + (lane & 31), ch));
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -523,17 +575,23 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     const int r = s / cstages;
     if (s - r * cstages == cstages - 1 && !(g.mode & 4)) {
       // ---- fp64 epilogue of sketch row r (DoubleCountMinSketch.java:143-147) ----
+      // Branch-free: every term is AB / (sqrtA * sqrtB) with AB >= 0 and a
+      // finite den, so no NaN or -0.0 reaches Math.min and it is a plain
+      // "smaller wins"; den == 0 rows are masked out.  Each sqrtA serves
+      // both column fragments.
+      double sb[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const double sb = s_sb[r * kTB + wc * 64 + j * 32 + (lane & 31)];
+      for (int j = 0; j < 2; ++j) sb[j] = s_sb[r * kTB + wc * 64 + j * 32 + (lane & 31)];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 2; ++i) {
 #pragma unroll
-          for (int og = 0; og < OG; ++og)
+        for (int og = 0; og < OG; ++og)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int ol = (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
-              const double sa = s_sa[r * OA + ol];
+          for (int q = 0; q < 4; ++q) {
+            const int ol = (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
+            const double sa = s_sa[r * kTA + ol];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
               double valueAB;
               if constexpr (LS == 1) {
                 valueAB = (double)acc[i][j][q + 4 * og];
@@ -543,16 +601,21 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
                 for (int l = 0; l < LS; ++l) dot += (int64_t)acc[i][j][q + 4 * (og * LS + l)] << (7 * l);
                 valueAB = (double)dot;
               }
-              const double den = __dmul_rn(sa, sb);
-              if (den != 0.0) mn[i][j][og * 4 + q] = java_min_d(mn[i][j][og * 4 + q], __ddiv_rn(valueAB, den));
+              const double den = __dmul_rn(sa, sb[j]);
+              const double v = __ddiv_rn(valueAB, den);
+              double& m = mn[i][j][og * 4 + q];
+              m = (den != 0.0 && v < m) ? v : m;
             }
+          }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
-        }
       }
     }
   }
 
+  if (g.mode & 16) return;  // EXPERIMENT
   // ---- write the slab: NaN when no row qualified, then normalizeWeightResult ----
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -644,6 +707,9 @@ int cosine_prepare(cms_handle* h) {
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
                        tileL);
+    CMS_HIP(h->ws_nsq.ensure(sizeof(double) * (size_t)n * (size_t)h->p.depth));
+    hipLaunchKernelGGL(k_perm_norms, dim3(grid), dim3(256), 0, h->stream, h->d_norm_sqrt, perm, n, h->p.depth,
+                       h->ws_nsq.as<double>());
     CMS_HIP(hipGetLastError());
   }
   h->tile_limbs.resize(ntiles);
@@ -703,20 +769,33 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   const int64_t ntiles = (n + kTile - 1) / kTile;
   const int64_t trows = (qc + kTile - 1) / kTile;
   a.tiles_x = (int)ntiles;
+  const int depth = h->p.depth;
+  const int64_t nm = a.n_multi;
+  const size_t norms = (size_t)depth * (kTA + kTB) * sizeof(double);
+  constexpr size_t kLdsMax = 160 * 1024;
+  // stage depth: 128-B K slices (one cache line per row) in a 3- or 2-deep
+  // ring; 64-B slices in a 6-deep ring measured slower (twice the line
+  // requests per byte, twice the barriers)
+  int bk = 128, nstage = 0;
+  if (const char* e = getenv("CMS_COS_BK")) bk = atoi(e) == 64 ? 64 : 128;  // EXPERIMENT
+  if (bk == 64) {
+    nstage = 6 * 384 * 64 + norms <= kLdsMax ? 6 : 4 * 384 * 64 + norms <= kLdsMax ? 4 : 0;
+    if (!nstage) bk = 128;
+  }
+  if (bk == 128) nstage = 3 * 384 * 128 + norms <= kLdsMax ? 3 : 2 * 384 * 128 + norms <= kLdsMax ? 2 : 0;
   static bool attr = [] {
-    const void* fns[] = {(const void*)k_cosine_tile<false>, (const void*)k_cosine_tile<true>,
-                         (const void*)k_cosine_big<2, 1>,   (const void*)k_cosine_big<3, 1>,
-                         (const void*)k_cosine_big<2, 2>,   (const void*)k_cosine_big<3, 2>,
-                         (const void*)k_cosine_big<2, 4>,   (const void*)k_cosine_big<3, 4>};
+    const void* fns[] = {(const void*)k_cosine_tile<false>,      (const void*)k_cosine_tile<true>,
+                         (const void*)k_cosine_big<2, 1, 128>,   (const void*)k_cosine_big<3, 1, 128>,
+                         (const void*)k_cosine_big<2, 2, 128>,   (const void*)k_cosine_big<3, 2, 128>,
+                         (const void*)k_cosine_big<2, 4, 128>,   (const void*)k_cosine_big<3, 4, 128>,
+                         (const void*)k_cosine_big<4, 1, 64>,    (const void*)k_cosine_big<6, 1, 64>,
+                         (const void*)k_cosine_big<4, 2, 64>,    (const void*)k_cosine_big<6, 2, 64>,
+                         (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
   const size_t lds = 4 * kTile * kBK + 2 * kTile * sizeof(double);  // 2 buffers x (A + B) + norms
-  const int depth = h->p.depth;
-  const int64_t nm = a.n_multi;
-  const size_t norms = (size_t)depth * (kTA + kTB) * sizeof(double);
-  const int nstage = 3 * (size_t)kStage + norms <= 160 * 1024 ? 3 : 2 * (size_t)kStage + norms <= 160 * 1024 ? 2 : 0;
   const int64_t qend = q0 + qc;
 
   if (nstage && (nm == 0 || h->vl_slots)) {
@@ -729,18 +808,23 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
       g.tilesB = (int)((g.b_rows + kTB - 1) / kTB);
       g.nblk = (int)(tilesA * g.tilesB);
       if (g.nblk <= 0) return CMS_OK;
-      const size_t bytes = (size_t)nstage * kStage + norms;
+      const size_t bytes = (size_t)nstage * 384 * bk + norms;
       const dim3 grid((unsigned)g.nblk), blk(512);
-#define CMS_BIG(NS, L) hipLaunchKernelGGL((k_cosine_big<NS, L>), grid, blk, bytes, h->stream, g)
-      if (nstage == 3) {
-        if (ls == 1) CMS_BIG(3, 1);
-        else if (ls == 2) CMS_BIG(3, 2);
-        else CMS_BIG(3, 4);
+#define CMS_BIG(NS, L, K) hipLaunchKernelGGL((k_cosine_big<NS, L, K>), grid, blk, bytes, h->stream, g)
+#define CMS_BIG_LS(NS, K)       \
+  do {                          \
+    if (ls == 1) CMS_BIG(NS, 1, K); \
+    else if (ls == 2) CMS_BIG(NS, 2, K); \
+    else CMS_BIG(NS, 4, K);     \
+  } while (0)
+      if (bk == 64) {
+        if (nstage == 6) CMS_BIG_LS(6, 64);
+        else CMS_BIG_LS(4, 64);
       } else {
-        if (ls == 1) CMS_BIG(2, 1);
-        else if (ls == 2) CMS_BIG(2, 2);
-        else CMS_BIG(2, 4);
+        if (nstage == 3) CMS_BIG_LS(3, 128);
+        else CMS_BIG_LS(2, 128);
       }
+#undef CMS_BIG_LS
 #undef CMS_BIG
       CMS_HIP(hipGetLastError());
       return CMS_OK;
@@ -748,7 +832,8 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
     BigArgs base{};
     if (const char* m = getenv("CMS_COS_MODE")) base.mode = atoi(m);  // EXPERIMENT
     base.perm = a.perm;
-    base.nsqrt = a.nsqrt;
+    base.nsq_t = h->ws_nsq.as<double>();
+    base.n = n;
     base.out = d_out;
     base.ldo = n;
     base.q0 = q0;

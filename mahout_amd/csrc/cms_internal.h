@@ -89,7 +89,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out;
-  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_vl;
+  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_vl, ws_nsq;
 
   // communicator
   ncclComm_t comm = nullptr;

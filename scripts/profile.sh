@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras ${BENCH_ARGS}"
+BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras --no-cosine-1m ${BENCH_ARGS}"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $BENCH \
     > $OUT/trace.log 2>&1 && echo "trace ok" \
   && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $BENCH \
