@@ -169,6 +169,12 @@ int cms_most_similar(cms_handle* h, int64_t id, int32_t k, int64_t* out_ids, dou
  * all-pairs top-k pass (config 4).  ids/scores are [row_count][k]; counts[row_count]. */
 int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* ids,
                    double* scores, int32_t* counts);
+/* mostSimilar for EVERY owner (config 4, the suggested cms_topk_all of the
+ * scope table): the same lists as cms_top_k_rows(h, 0, num_owners, ...), but
+ * each unordered pair's similarity is computed once and streamed into both
+ * owners' lists (no n x n slab).  ids/scores are [num_owners][k] by owner
+ * row, counts[num_owners]; k <= 512. */
+int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts);
 
 /* Counters of rows [row_begin, row_begin+row_count) as fp64 (the reference's
  * counter type), [row_count][d][w]. */

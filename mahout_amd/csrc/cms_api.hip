@@ -245,7 +245,7 @@ void cms_destroy(cms_handle* h) {
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
-                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->ws_vl, &h->ws_nsq};
+                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->ws_vl, &h->ws_nsq, &h->ws_cand};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -390,7 +390,7 @@ int cms_release_scratch(cms_handle* h) {
   CMS_HIP(hipStreamSynchronize(h->stream));
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_hot, &h->ws_query,
-                  &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles};
+                  &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand};
   for (DevBuf* b : ws) b->release();
   return CMS_OK;
 }
@@ -551,6 +551,29 @@ int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t 
   if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
   if (row_count == 0) return CMS_OK;
   return top_k_host(h, row_begin, row_count, k, ids, scores, counts);
+}
+
+int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts) {
+  if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  const int64_t n = h->n;
+  DevBuf o_ids, o_sc, o_cnt;
+  CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
+  CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
+  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
+  rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
+  if (rc == CMS_OK) {
+    hipError_t e = hipMemcpyAsync(ids, o_ids.ptr, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && scores)
+      e = hipMemcpyAsync(scores, o_sc.ptr, sizeof(double) * n * k, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(counts, o_cnt.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) rc = hip_fail(e, "top-k copy-out");
+  }
+  return rc;
 }
 
 int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out) {

@@ -435,6 +435,18 @@ struct BigArgs {
   int32_t weighted, trans;
   int32_t tilesB, nblk;
   int32_t mode;  // EXPERIMENT: bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
+  // ---- candidate (streaming top-k) mode: cval != nullptr ----
+  // Instead of the slab, every similarity v of a pair (a, b) is offered to
+  // row a's candidate list when append_a and v >= thr[a], and to row b's when
+  // append_b and v >= thr[b] (NaN never).  Lists hold (position, v).
+  const double* thr;    // [n] per-position admission threshold (-inf: admit all)
+  uint32_t* ccnt;       // [n] list lengths
+  uint32_t* cidx;       // [n][cap] partner positions
+  double* cval;         // [n][cap] similarities
+  int32_t cap, append_a, append_b;
+  // ---- symmetric wave: unordered 256-row block pairs {I, (I + wave) % nb} ----
+  int32_t sym, wave, nb;  // sym: block I = positions [s0 + 256 I, ...) of the s_rows region
+  int64_t s0, s_rows;
 };
 
 template <int NSTAGE, int LS, int BK>
@@ -454,14 +466,34 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   const int nblk = g.nblk;
   const int bx = blockIdx.x, xcd = bx & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
-  // A panel fastest: an XCD's co-resident workgroups cover a few candidate
-  // tiles x every query panel, so both operands mostly hit the XCD's L2 and
-  // each candidate tile leaves HBM once per launch.
-  const int tilesA = g.nblk / g.tilesB;
-  const int ta = lin % tilesA, tb = lin / tilesA;
-  const int64_t vrow0 = (int64_t)ta * kTA;  // first operand row of the A panel
-  const int64_t own0 = (int64_t)ta * OA;    // first owner (relative to a_pos0)
-  const int64_t bcol0 = (int64_t)tb * kTB;
+  const int8_t* gA = g.A;
+  const int8_t* gB = g.B;
+  int64_t a_pos0 = g.a_pos0, a_owners = g.a_owners, a_vrows = g.a_vrows, b_pos0 = g.b_pos0, b_rows = g.b_rows;
+  int64_t vrow0, own0, bcol0;
+  bool diag = false;  // symmetric diagonal block: only pairs a < b
+  if (g.sym) {
+    // consecutive workgroups = the two 128-column halves of one block pair
+    const int I = lin >> 1, half = lin & 1;
+    const int J = (I + g.wave) % g.nb;
+    diag = I == J;
+    a_pos0 = g.s0 + (int64_t)I * kTA;
+    a_owners = a_vrows = min<int64_t>(kTA, g.s_rows - (int64_t)I * kTA);
+    b_pos0 = g.s0 + (int64_t)J * kTA + half * kTB;
+    b_rows = min<int64_t>(kTB, g.s_rows - (int64_t)J * kTA - half * kTB);
+    if (b_rows <= 0) return;  // the whole workgroup leaves before any barrier
+    gA = g.A + a_pos0 * g.dw;
+    gB = g.B + b_pos0 * g.dw;
+    vrow0 = own0 = bcol0 = 0;
+  } else {
+    // A panel fastest: an XCD's co-resident workgroups cover a few candidate
+    // tiles x every query panel, so both operands mostly hit the XCD's L2 and
+    // each candidate tile leaves HBM once per launch.
+    const int tilesA = g.nblk / g.tilesB;
+    const int ta = lin % tilesA, tb = lin / tilesA;
+    vrow0 = (int64_t)ta * kTA;  // first operand row of the A panel
+    own0 = (int64_t)ta * OA;    // first owner (relative to a_pos0)
+    bcol0 = (int64_t)tb * kTB;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
@@ -482,9 +514,9 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     const int r = k / 12, part = k % 12;  // parts 0..7: A (8 x 32 owners), 8..11: B (4 x 32)
     const bool isA = part < 8;
     const int64_t first = isA ? own0 + part * 32 : bcol0 + (part - 8) * 32;
-    const int64_t lim = isA ? min<int64_t>(g.a_owners, own0 + OA) : g.b_rows;
+    const int64_t lim = isA ? min<int64_t>(a_owners, own0 + OA) : b_rows;
     const int64_t cnt = max<int64_t>(0, min<int64_t>(32, lim - first));
-    const double* src = g.nsq_t + (int64_t)r * g.n + (isA ? g.a_pos0 : g.b_pos0) + first;
+    const double* src = g.nsq_t + (int64_t)r * g.n + (isA ? a_pos0 : b_pos0) + first;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * 8), 0x00020000);
     double* dst = isA ? s_sa + r * kTA + part * 32 : s_sb + r * kTB + (part - 8) * 32;
@@ -496,12 +528,12 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   }
 
   // buffer descriptors bound the panel: rows past the end land as zeros
-  const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, g.a_vrows - vrow0));
-  const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, g.b_rows - bcol0));
+  const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, a_vrows - vrow0));
+  const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, b_rows - bcol0));
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A + vrow0 * g.dw), (short)0, (int)(rowsA * g.dw), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(gA + vrow0 * g.dw), (short)0, (int)(rowsA * g.dw), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g.B + bcol0 * g.dw), (short)0, (int)(rowsB * g.dw), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(gB + bcol0 * g.dw), (short)0, (int)(rowsB * g.dw), 0x00020000);
   // Instruction u of wave wid fills LDS rows [(wid + 8u) * RPI, +RPI); lane
   // i lands at byte 16 i, i.e. row (wid + 8u) * RPI + i / (BK/16), slot
   // i % (BK/16), and fetches the chunk the swizzle puts there.  The 8*RPI-row
@@ -616,21 +648,21 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   }
 
   if (g.mode & 16) return;  // EXPERIMENT
-  // ---- write the slab: NaN when no row qualified, then normalizeWeightResult ----
+  // ---- NaN when no row qualified, then normalizeWeightResult; slab or lists ----
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int64_t bi = bcol0 + wc * 64 + j * 32 + (lane & 31);
+      const int64_t bp = b_pos0 + bi;
+      const double tb_ = (g.cval && g.append_b && bi < b_rows) ? g.thr[bp] : 0.0;
 #pragma unroll
       for (int og = 0; og < OG; ++og)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int64_t ai = own0 + (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
-          if (ai >= g.a_owners || bi >= g.b_rows) continue;
-          const int64_t ap = g.a_pos0 + ai, bp = g.b_pos0 + bi;
-          const int64_t orow = g.trans ? bp : ap, ocol = g.trans ? ap : bp;
-          if (orow < g.q0 || orow >= g.q0 + g.qcount) continue;
+          if (ai >= a_owners || bi >= b_rows) continue;
+          const int64_t ap = a_pos0 + ai;
           double rr = mn[i][j][og * 4 + q];
           rr = rr == DBL_MAX ? __builtin_nan("") : rr;
           if (rr == rr) {
@@ -638,6 +670,26 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
             if (rr < -1.0) rr = -1.0;
             else if (rr > 1.0) rr = 1.0;
           }
+          if (g.cval) {
+            if (rr != rr || ap == bp || (diag && ap > bp)) continue;
+            if (g.append_a && rr >= g.thr[ap]) {
+              const uint32_t slot = atomicAdd(&g.ccnt[ap], 1u);
+              if (slot < (uint32_t)g.cap) {
+                g.cidx[ap * g.cap + slot] = (uint32_t)bp;
+                g.cval[ap * g.cap + slot] = rr;
+              }
+            }
+            if (g.append_b && rr >= tb_) {
+              const uint32_t slot = atomicAdd(&g.ccnt[bp], 1u);
+              if (slot < (uint32_t)g.cap) {
+                g.cidx[bp * g.cap + slot] = (uint32_t)ap;
+                g.cval[bp * g.cap + slot] = rr;
+              }
+            }
+            continue;
+          }
+          const int64_t orow = g.trans ? bp : ap, ocol = g.trans ? ap : bp;
+          if (orow < g.q0 || orow >= g.q0 + g.qcount) continue;
           g.out[(orow - g.q0) * g.ldo + ocol] = rr;
         }
     }
@@ -744,6 +796,90 @@ bool mfma_eligible(cms_handle* h) { return (h->p.width % kBK) == 0; }
 // Similarities of the owners at PERMUTED positions [q0, q0+qc) against every
 // owner into slab [qc][n] (fp64, column = permuted position; owner row =
 // perm[column]).  q0 must be a multiple of kTile.
+// Launch shape of k_cosine_big for this table: stage depth and ring size
+// that fit 160 KiB of LDS beside the panel norms.
+struct BigCfg {
+  int bk = 128, nstage = 0;
+  size_t norms = 0;
+};
+
+static BigCfg big_config(cms_handle* h) {
+  BigCfg c;
+  c.norms = (size_t)h->p.depth * (kTA + kTB) * sizeof(double);
+  constexpr size_t kLdsMax = 160 * 1024;
+  // 128-B K slices (one cache line per row) in a 3- or 2-deep ring; 64-B
+  // slices in a 6-deep ring measured slower (twice the line requests per
+  // byte, twice the barriers)
+  if (const char* e = getenv("CMS_COS_BK")) c.bk = atoi(e) == 64 ? 64 : 128;  // EXPERIMENT
+  if (c.bk == 64) {
+    c.nstage = 6 * 384 * 64 + c.norms <= kLdsMax ? 6 : 4 * 384 * 64 + c.norms <= kLdsMax ? 4 : 0;
+    if (!c.nstage) c.bk = 128;
+  }
+  if (c.bk == 128) c.nstage = 3 * 384 * 128 + c.norms <= kLdsMax ? 3 : 2 * 384 * 128 + c.norms <= kLdsMax ? 2 : 0;
+  static bool attr = [] {
+    const void* fns[] = {(const void*)k_cosine_tile<false>,      (const void*)k_cosine_tile<true>,
+                         (const void*)k_cosine_big<2, 1, 128>,   (const void*)k_cosine_big<3, 1, 128>,
+                         (const void*)k_cosine_big<2, 2, 128>,   (const void*)k_cosine_big<3, 2, 128>,
+                         (const void*)k_cosine_big<2, 4, 128>,   (const void*)k_cosine_big<3, 4, 128>,
+                         (const void*)k_cosine_big<4, 1, 64>,    (const void*)k_cosine_big<6, 1, 64>,
+                         (const void*)k_cosine_big<4, 2, 64>,    (const void*)k_cosine_big<6, 2, 64>,
+                         (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>};
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  return c;
+}
+
+// One k_cosine_big launch.  Rectangular mode: A owners x B rows; symmetric
+// mode (g.sym): sym_pairs block pairs of the wave, two workgroups each.
+static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t sym_pairs = 0) {
+  if (g.sym) {
+    g.tilesB = 2;
+    g.nblk = (int)(2 * sym_pairs);
+  } else {
+    const int oa = kTA / ls;
+    const int64_t tilesA = (g.a_owners + oa - 1) / oa;
+    g.tilesB = (int)((g.b_rows + kTB - 1) / kTB);
+    g.nblk = (int)(tilesA * g.tilesB);
+  }
+  if (g.nblk <= 0) return CMS_OK;
+  const size_t bytes = (size_t)c.nstage * 384 * c.bk + c.norms;
+  const dim3 grid((unsigned)g.nblk), blk(512);
+#define CMS_BIG(NS, L, K) hipLaunchKernelGGL((k_cosine_big<NS, L, K>), grid, blk, bytes, h->stream, g)
+#define CMS_BIG_LS(NS, K)              \
+  do {                                 \
+    if (ls == 1) CMS_BIG(NS, 1, K);      \
+    else if (ls == 2) CMS_BIG(NS, 2, K); \
+    else CMS_BIG(NS, 4, K);            \
+  } while (0)
+  if (c.bk == 64) {
+    if (c.nstage == 6) CMS_BIG_LS(6, 64);
+    else CMS_BIG_LS(4, 64);
+  } else {
+    if (c.nstage == 3) CMS_BIG_LS(3, 128);
+    else CMS_BIG_LS(2, 128);
+  }
+#undef CMS_BIG_LS
+#undef CMS_BIG
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+static BigArgs big_base(cms_handle* h) {
+  BigArgs b{};
+  if (const char* m = getenv("CMS_COS_MODE")) b.mode = atoi(m);  // EXPERIMENT
+  b.perm = h->ws_limbmeta.as<int64_t>();
+  b.nsq_t = h->ws_nsq.as<double>();
+  b.n = h->n;
+  b.ldo = h->n;
+  b.dw = h->dw;
+  b.w = h->p.width;
+  b.depth = h->p.depth;
+  b.weighted = h->p.weighting == CMS_WEIGHTED;
+  return b;
+}
+
 int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   int rc = cosine_prepare(h);
   if (rc) return rc;
@@ -769,79 +905,20 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   const int64_t ntiles = (n + kTile - 1) / kTile;
   const int64_t trows = (qc + kTile - 1) / kTile;
   a.tiles_x = (int)ntiles;
-  const int depth = h->p.depth;
   const int64_t nm = a.n_multi;
-  const size_t norms = (size_t)depth * (kTA + kTB) * sizeof(double);
-  constexpr size_t kLdsMax = 160 * 1024;
-  // stage depth: 128-B K slices (one cache line per row) in a 3- or 2-deep
-  // ring; 64-B slices in a 6-deep ring measured slower (twice the line
-  // requests per byte, twice the barriers)
-  int bk = 128, nstage = 0;
-  if (const char* e = getenv("CMS_COS_BK")) bk = atoi(e) == 64 ? 64 : 128;  // EXPERIMENT
-  if (bk == 64) {
-    nstage = 6 * 384 * 64 + norms <= kLdsMax ? 6 : 4 * 384 * 64 + norms <= kLdsMax ? 4 : 0;
-    if (!nstage) bk = 128;
-  }
-  if (bk == 128) nstage = 3 * 384 * 128 + norms <= kLdsMax ? 3 : 2 * 384 * 128 + norms <= kLdsMax ? 2 : 0;
-  static bool attr = [] {
-    const void* fns[] = {(const void*)k_cosine_tile<false>,      (const void*)k_cosine_tile<true>,
-                         (const void*)k_cosine_big<2, 1, 128>,   (const void*)k_cosine_big<3, 1, 128>,
-                         (const void*)k_cosine_big<2, 2, 128>,   (const void*)k_cosine_big<3, 2, 128>,
-                         (const void*)k_cosine_big<2, 4, 128>,   (const void*)k_cosine_big<3, 4, 128>,
-                         (const void*)k_cosine_big<4, 1, 64>,    (const void*)k_cosine_big<6, 1, 64>,
-                         (const void*)k_cosine_big<4, 2, 64>,    (const void*)k_cosine_big<6, 2, 64>,
-                         (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>};
-    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    return true;
-  }();
-  (void)attr;
+  const BigCfg cfg = big_config(h);
   const size_t lds = 4 * kTile * kBK + 2 * kTile * sizeof(double);  // 2 buffers x (A + B) + norms
   const int64_t qend = q0 + qc;
 
-  if (nstage && (nm == 0 || h->vl_slots)) {
+  if (cfg.nstage && (nm == 0 || h->vl_slots)) {
     // Four blocks of the slab in permuted coordinates (M = multi-limb owners
     // [0, nm), S = the rest):  S x S and M x S / S x M on k_cosine_big,
     // M x M on the int64-folding MULTI tile kernel.
-    auto launch = [&](BigArgs g, int ls) -> int {
-      const int oa = kTA / ls;
-      const int64_t tilesA = (g.a_owners + oa - 1) / oa;
-      g.tilesB = (int)((g.b_rows + kTB - 1) / kTB);
-      g.nblk = (int)(tilesA * g.tilesB);
-      if (g.nblk <= 0) return CMS_OK;
-      const size_t bytes = (size_t)nstage * 384 * bk + norms;
-      const dim3 grid((unsigned)g.nblk), blk(512);
-#define CMS_BIG(NS, L, K) hipLaunchKernelGGL((k_cosine_big<NS, L, K>), grid, blk, bytes, h->stream, g)
-#define CMS_BIG_LS(NS, K)       \
-  do {                          \
-    if (ls == 1) CMS_BIG(NS, 1, K); \
-    else if (ls == 2) CMS_BIG(NS, 2, K); \
-    else CMS_BIG(NS, 4, K);     \
-  } while (0)
-      if (bk == 64) {
-        if (nstage == 6) CMS_BIG_LS(6, 64);
-        else CMS_BIG_LS(4, 64);
-      } else {
-        if (nstage == 3) CMS_BIG_LS(3, 128);
-        else CMS_BIG_LS(2, 128);
-      }
-#undef CMS_BIG_LS
-#undef CMS_BIG
-      CMS_HIP(hipGetLastError());
-      return CMS_OK;
-    };
-    BigArgs base{};
-    if (const char* m = getenv("CMS_COS_MODE")) base.mode = atoi(m);  // EXPERIMENT
-    base.perm = a.perm;
-    base.nsq_t = h->ws_nsq.as<double>();
-    base.n = n;
+    auto launch = [&](const BigArgs& g, int ls) { return launch_big(h, cfg, g, ls); };
+    BigArgs base = big_base(h);
     base.out = d_out;
-    base.ldo = n;
     base.q0 = q0;
     base.qcount = qc;
-    base.dw = dw;
-    base.w = a.w;
-    base.depth = depth;
-    base.weighted = a.weighted;
     const int64_t slo = std::max(q0, nm);  // single-limb query rows [slo, qend)
     if (slo < qend && nm < n) {  // S x S
       BigArgs g = base;
@@ -922,6 +999,133 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
     CMS_HIP(hipGetLastError());
     CMS_HIP(hipStreamSynchronize(h->stream));  // the host tile list must outlive the copy
   }
+  return CMS_OK;
+}
+
+// ---------------------------------------------- all-pairs top-k, streaming --
+// TopItems.getTopUsers for EVERY owner (T/impl/recommender/TopItems.java:91-136,
+// one GenericUserBasedRecommender.mostSimilarUserIDs per owner) without an
+// n x n slab and with each unordered single-limb pair computed ONCE:
+//   1. multi-limb rows (M): exact slab top-k (slab_top_k_positions);
+//   2. single-limb rows (S) x M candidates: k_cosine_big in candidate mode,
+//      M owners as virtual limb rows, offered to the S rows' lists;
+//   3. S x S: symmetric waves -- wave w computes block pairs {I, I+w mod nb}
+//      of 256 rows, each similarity offered to BOTH rows' lists;
+//   4. lists compacted to the first k of (score desc, owner row asc) --
+//      SimilarUser.compareTo -- whenever a pass could overflow them; the
+//      k-th score becomes the row's admission threshold (score >= thr,
+//      ties admitted, so the order among equal scores stays exact).
+// A row receives at most 512 offers per wave (its block as A, and as B), and
+// a list is compacted before a pass whenever it holds more than cap - 512, so
+// lists cannot overflow; should one ever do, the row is recomputed exactly.
+int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  int rc = cosine_prepare(h);
+  if (rc) return rc;
+  const int64_t n = h->n, dw = h->dw;
+  const BigCfg cfg = big_config(h);
+  const int64_t nm = h->n_hot_limb, ns = n - nm;
+  if (!cfg.nstage || (nm > 0 && !h->vl_slots) || h->n_inexact_rows != 0 || k > kCandCap / 2) {
+    return top_k_rows(h, 0, n, k, d_ids, d_scores, d_counts);  // per-row slab path
+  }
+  const int32_t cap = kCandCap;
+  constexpr uint32_t kPerPass = 512;  // most offers one row takes in one pass
+  DevBuf& ws = h->ws_cand;
+  const size_t off_cidx = (sizeof(uint32_t) * (size_t)n + 255) & ~size_t(255);
+  const size_t off_cval = off_cidx + ((sizeof(uint32_t) * (size_t)n * cap + 255) & ~size_t(255));
+  const size_t off_thr = off_cval + sizeof(double) * (size_t)n * cap;
+  const size_t off_ovf = off_thr + sizeof(double) * (size_t)n;
+  const size_t off_list = off_ovf + sizeof(uint32_t) * (size_t)n;
+  const size_t off_ln = off_list + sizeof(uint32_t) * (size_t)n;
+  CMS_HIP(ws.ensure(off_ln + 256));
+  char* wsb = ws.as<char>();
+  CandBufs cb;
+  cb.ccnt = reinterpret_cast<uint32_t*>(wsb);
+  cb.cidx = reinterpret_cast<uint32_t*>(wsb + off_cidx);
+  cb.cval = reinterpret_cast<double*>(wsb + off_cval);
+  cb.thr = reinterpret_cast<double*>(wsb + off_thr);
+  cb.ovf = reinterpret_cast<uint32_t*>(wsb + off_ovf);
+  cb.list = reinterpret_cast<uint32_t*>(wsb + off_list);
+  cb.list_n = reinterpret_cast<uint32_t*>(wsb + off_ln);
+  cb.cap = cap;
+  CMS_HIP(hipMemsetAsync(cb.ccnt, 0, sizeof(uint32_t) * n, h->stream));
+  CMS_HIP(hipMemsetAsync(cb.ovf, 0, sizeof(uint32_t) * n, h->stream));
+  {
+    std::vector<double> ninf(1 << 16, -__builtin_inf());
+    for (int64_t o = 0; o < n; o += (int64_t)ninf.size())
+      CMS_HIP(hipMemcpyAsync(cb.thr + o, ninf.data(), sizeof(double) * std::min<int64_t>(ninf.size(), n - o),
+                             hipMemcpyHostToDevice, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+  }
+  // 1. multi-limb rows: exact slab top-k
+  if (nm > 0) {
+    TimedScope ts(h, "topk_all_multi_rows");
+    std::vector<int64_t> pos(nm), outp(nm);
+    for (int64_t p = 0; p < nm; ++p) {
+      pos[p] = p;
+      outp[p] = h->h_perm[p];
+    }
+    if ((rc = slab_top_k_positions(h, pos, outp, k, d_ids, d_scores, d_counts))) return rc;
+  }
+  BigArgs base = big_base(h);
+  base.thr = cb.thr;
+  base.ccnt = cb.ccnt;
+  base.cidx = cb.cidx;
+  base.cval = cb.cval;
+  base.cap = cap;
+  const int8_t* limb0 = h->ws_limb0.as<int8_t>();
+  // 2. S rows x M candidates, kPerPass multi-limb owners per pass
+  if (nm > 0 && ns > 0) {
+    const int ls = h->vl_slots, per = 32 / ls;
+    const int8_t* vl = h->ws_vl.as<int8_t>();
+    for (int64_t m0 = 0; m0 < nm; m0 += kPerPass) {
+      if ((rc = cand_compact(h, cb, nm, ns, (uint32_t)cap - kPerPass, k))) return rc;
+      BigArgs g = base;
+      g.A = vl + (m0 / per) * 32 * dw;
+      g.a_vrows = h->vl_rows - (m0 / per) * 32;
+      g.a_pos0 = m0;
+      g.a_owners = std::min<int64_t>(kPerPass, nm - m0);
+      g.B = limb0 + nm * dw;
+      g.b_pos0 = nm;
+      g.b_rows = ns;
+      g.append_b = 1;
+      TimedScope ts(h, "topk_all_limbs");
+      if ((rc = launch_big(h, cfg, g, ls))) return rc;
+    }
+  }
+  // 3. S x S symmetric waves
+  if (ns > 0) {
+    const int64_t nb = (ns + kTA - 1) / kTA;
+    for (int64_t wv = 0; wv <= nb / 2; ++wv) {
+      int64_t pairs = nb;
+      if (wv > 0 && 2 * wv == nb) pairs = nb / 2;  // {I, I + nb/2}: each pair once
+      if ((rc = cand_compact(h, cb, nm, ns, (uint32_t)cap - kPerPass, k))) return rc;
+      BigArgs g = base;
+      g.A = g.B = limb0;
+      g.sym = 1;
+      g.wave = (int32_t)wv;
+      g.nb = (int32_t)nb;
+      g.s0 = nm;
+      g.s_rows = ns;
+      g.append_a = g.append_b = 1;
+      TimedScope ts(h, "topk_all_waves");
+      if ((rc = launch_big(h, cfg, g, 1, pairs))) return rc;
+    }
+    // 4. final lists -> outputs
+    if ((rc = cand_compact(h, cb, nm, ns, 0, k))) return rc;
+    if ((rc = cand_emit(h, cb, nm, ns, k, d_ids, d_scores, d_counts))) return rc;
+  }
+  // rows whose list overflowed (not expected): exact per-row recompute
+  std::vector<uint32_t> ovf(ns > 0 ? ns : 1);
+  if (ns > 0) CMS_HIP(hipMemcpyAsync(ovf.data(), cb.ovf + nm, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  std::vector<int64_t> pos, outp;
+  for (int64_t i = 0; i < ns; ++i)
+    if (ovf[i]) {
+      pos.push_back(nm + i);
+      outp.push_back(h->h_perm[nm + i]);
+    }
+  h->topk_redo += (int64_t)pos.size();
+  if (!pos.empty() && (rc = slab_top_k_positions(h, pos, outp, k, d_ids, d_scores, d_counts))) return rc;
   return CMS_OK;
 }
 

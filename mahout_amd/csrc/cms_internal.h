@@ -89,7 +89,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out;
-  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_vl, ws_nsq;
+  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_vl, ws_nsq, ws_cand;
 
   // communicator
   ncclComm_t comm = nullptr;
@@ -143,6 +143,25 @@ int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m,
 int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts);
+// exact top-k (slab path) of the owners at PERMUTED positions pos, written at out_pos
+int slab_top_k_positions(cms_handle* h, const std::vector<int64_t>& pos, const std::vector<int64_t>& out_pos,
+                         int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
+// candidate lists of the streaming all-pairs top-k
+constexpr int kCandCap = 1024;  // entries per row
+struct CandBufs {
+  uint32_t* ccnt;  // [n]
+  uint32_t* cidx;  // [n][cap]
+  double* cval;    // [n][cap]
+  double* thr;     // [n]
+  uint32_t* ovf;   // [n]
+  uint32_t* list;  // [n]
+  uint32_t* list_n;
+  int32_t cap;
+};
+int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint32_t limit, int32_t k);
+int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t k, int64_t* d_ids, double* d_scores,
+              int32_t* d_counts);
+int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
 // ---- cms_cosine_mfma.hip ----
 const int64_t* cosine_perm_device(cms_handle* h);
 // ---- cms_cosine_mfma.hip ----

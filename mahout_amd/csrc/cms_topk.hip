@@ -413,41 +413,181 @@ static int launch_top_k(cms_handle* h, const double* slab, const std::vector<Top
   return CMS_OK;
 }
 
+// ---- candidate lists of the streaming all-pairs top-k (cosine_mfma: top_k_all) ----
+// Rows whose list holds more than `limit` entries, appended to `list`.
+__global__ void k_cand_select(const uint32_t* ccnt, int64_t p0, int64_t np, uint32_t limit, uint32_t* list,
+                              uint32_t* list_n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x)
+    if (ccnt[p0 + i] > limit) list[atomicAdd(list_n, 1u)] = (uint32_t)(p0 + i);
+}
+
+constexpr int kCandThreads = 256;
+
+// Shrink each listed row to its first k candidates under (score desc, owner
+// row asc) -- the SimilarUser order -- and raise its admission threshold to
+// the k-th score.  A list that overflowed its capacity is flagged (its row is
+// recomputed exactly afterwards); the threshold stays a valid lower bound.
+__global__ __launch_bounds__(kCandThreads) void k_cand_compact(const uint32_t* list, const uint32_t* list_n,
+                                                               uint32_t* ccnt, uint32_t* cidx, double* cval,
+                                                               int32_t cap, int32_t k, const int64_t* perm,
+                                                               double* thr, uint32_t* ovf) {
+  __shared__ uint64_t key[kCandCap];
+  __shared__ uint32_t row[kCandCap];
+  __shared__ uint32_t pid[kCandCap];
+  __shared__ double val[kCandCap];
+  const uint32_t nl = *list_n;
+  const int tid = threadIdx.x;
+  for (uint32_t e = blockIdx.x; e < nl; e += gridDim.x) {
+    const int64_t p = list[e];
+    const uint32_t c = ccnt[p];
+    const uint32_t m = min(c, (uint32_t)cap);
+    if (tid == 0 && c > (uint32_t)cap) ovf[p] = 1u;
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t i = tid; i < P; i += kCandThreads) {
+      if (i < m) {
+        const uint32_t o = cidx[p * cap + i];
+        const double v = cval[p * cap + i];
+        key[i] = score_key(v);
+        row[i] = (uint32_t)perm[o];
+        pid[i] = o;
+        val[i] = v;
+      } else {
+        key[i] = 0;
+        row[i] = 0xFFFFFFFFu;
+      }
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1) {
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = tid; i < P; i += kCandThreads) {
+          const uint32_t jx = i ^ stride;
+          if (jx > i) {
+            const bool up = (i & size) == 0;
+            const bool i_first = key[i] > key[jx] || (key[i] == key[jx] && row[i] < row[jx]);
+            if (up != i_first) {
+              const uint64_t tk = key[i];
+              key[i] = key[jx];
+              key[jx] = tk;
+              const uint32_t tr = row[i];
+              row[i] = row[jx];
+              row[jx] = tr;
+              const uint32_t tp = pid[i];
+              pid[i] = pid[jx];
+              pid[jx] = tp;
+              const double tv = val[i];
+              val[i] = val[jx];
+              val[jx] = tv;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    const uint32_t kk = min(m, (uint32_t)k);
+    for (uint32_t i = tid; i < kk; i += kCandThreads) {
+      cidx[p * cap + i] = pid[i];
+      cval[p * cap + i] = val[i];
+    }
+    if (tid == 0) {
+      ccnt[p] = kk;
+      if (kk == (uint32_t)k) thr[p] = val[k - 1];
+    }
+    __syncthreads();
+  }
+}
+
+// Final lists -> outputs indexed by owner row (IDs through owner_ids).
+__global__ void k_cand_emit(const uint32_t* ccnt, const uint32_t* cidx, const double* cval, int32_t cap, int32_t k,
+                            int64_t p0, int64_t np, const int64_t* perm, const int64_t* owner_ids, int64_t* ids,
+                            double* scores, int32_t* counts) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = p0 + i;
+    const int64_t orow = perm[p];
+    const uint32_t c = min(ccnt[p], (uint32_t)k);
+    counts[orow] = (int32_t)c;
+    for (uint32_t t = 0; t < c; ++t) {
+      const int64_t r = perm[cidx[p * cap + t]];
+      ids[orow * k + t] = owner_ids ? owner_ids[r] : r;
+      scores[orow * k + t] = cval[p * cap + t];
+    }
+  }
+}
+
+int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint32_t limit, int32_t k) {
+  if (np <= 0) return CMS_OK;
+  CMS_HIP(hipMemsetAsync(cb.list_n, 0, sizeof(uint32_t), h->stream));
+  const unsigned g1 = (unsigned)std::min<int64_t>((np + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_cand_select, dim3(g1), dim3(256), 0, h->stream, cb.ccnt, p0, np, limit, cb.list, cb.list_n);
+  hipLaunchKernelGGL(k_cand_compact, dim3(4096), dim3(kCandThreads), 0, h->stream, cb.list, cb.list_n, cb.ccnt,
+                     cb.cidx, cb.cval, cb.cap, k, cosine_perm_device(h), cb.thr, cb.ovf);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t k, int64_t* d_ids, double* d_scores,
+              int32_t* d_counts) {
+  if (np <= 0) return CMS_OK;
+  const unsigned g1 = (unsigned)std::min<int64_t>((np + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_cand_emit, dim3(g1), dim3(256), 0, h->stream, cb.ccnt, cb.cidx, cb.cval, cb.cap, k, p0, np,
+                     cosine_perm_device(h), h->d_owner_ids, d_ids, d_scores, d_counts);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+// slab budget: 2^30 fp64 similarities (8 GiB) -- 1,024 query rows at 1M owners
+static int64_t slab_rows_for(int64_t n) {
+  return std::max<int64_t>(128, ((int64_t(1) << 30) / std::max<int64_t>(1, n)) / 128 * 128);
+}
+
+int slab_top_k_positions(cms_handle* h, const std::vector<int64_t>& pos, const std::vector<int64_t>& out_pos,
+                         int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  // MFMA slabs over the PERMUTED 128-row query tiles that hold a requested position
+  const int64_t n = h->n;
+  int rc = CMS_OK;
+  if (pos.empty()) return CMS_OK;
+  const int64_t slab_rows = slab_rows_for(n);
+  std::vector<int64_t> tiles;
+  for (int64_t p : pos) tiles.push_back(p / 128);
+  std::sort(tiles.begin(), tiles.end());
+  tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
+  // a run of consecutive tiles below never exceeds slab_rows rows (nor the tiles present)
+  const int64_t max_run = std::min<int64_t>(slab_rows, (int64_t)tiles.size() * 128);
+  CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(max_run * n)));
+  std::vector<std::pair<int64_t, int64_t>> q(pos.size());
+  for (size_t i = 0; i < pos.size(); ++i) q[i] = {pos[i], out_pos[i]};
+  std::sort(q.begin(), q.end());
+  size_t ti = 0, qi = 0;
+  while (ti < tiles.size()) {
+    // a run of consecutive tiles, at most slab_rows rows
+    size_t tj = ti + 1;
+    while (tj < tiles.size() && tiles[tj] == tiles[tj - 1] + 1 && (int64_t)(tj - ti + 1) * 128 <= slab_rows) ++tj;
+    const int64_t q0 = tiles[ti] * 128;
+    const int64_t qc = std::min<int64_t>(n - q0, (int64_t)(tj - ti) * 128);
+    if ((rc = cosine_slab(h, q0, qc, h->ws_slab.as<double>()))) return rc;
+    std::vector<TopQuery> qs;
+    for (; qi < q.size() && q[qi].first < q0 + qc; ++qi) qs.push_back(TopQuery{q[qi].first - q0, q[qi].first, q[qi].second});
+    if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, cosine_perm_device(h), d_ids, d_scores, d_counts)))
+      return rc;
+    ti = tj;
+  }
+  return CMS_OK;
+}
+
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts) {
   if (k < 1 || k > kTopMax) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kTopMax);
   const int64_t n = h->n;
   int rc = CMS_OK;
   if (mfma_eligible(h) && (rc = cosine_prepare(h))) return rc;
-  // slab budget: 2^30 fp64 similarities (8 GiB) -- 1,024 query rows at 1M owners
-  const int64_t slab_rows = std::max<int64_t>(128, ((int64_t(1) << 30) / std::max<int64_t>(1, n)) / 128 * 128);
+  const int64_t slab_rows = slab_rows_for(n);
   if (mfma_eligible(h) && h->n_inexact_rows == 0) {
-    // MFMA slabs over PERMUTED 128-row query tiles that hold a requested owner
-    std::vector<int64_t> tiles;
-    for (int64_t r = row_begin; r < row_begin + row_count; ++r) tiles.push_back(h->h_inv[r] / 128);
-    std::sort(tiles.begin(), tiles.end());
-    tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
-    // a run of consecutive tiles below never exceeds slab_rows rows (nor the tiles present)
-    const int64_t max_run = std::min<int64_t>(slab_rows, (int64_t)tiles.size() * 128);
-    CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(max_run * n)));
-    size_t ti = 0;
-    while (ti < tiles.size()) {
-      // a run of consecutive tiles, at most slab_rows rows
-      size_t tj = ti + 1;
-      while (tj < tiles.size() && tiles[tj] == tiles[tj - 1] + 1 && (int64_t)(tj - ti + 1) * 128 <= slab_rows) ++tj;
-      const int64_t q0 = tiles[ti] * 128;
-      const int64_t qc = std::min<int64_t>(n - q0, (int64_t)(tj - ti) * 128);
-      if ((rc = cosine_slab(h, q0, qc, h->ws_slab.as<double>()))) return rc;
-      std::vector<TopQuery> qs;
-      for (int64_t p = q0; p < q0 + qc; ++p) {
-        const int64_t r = h->h_perm[p];
-        if (r >= row_begin && r < row_begin + row_count) qs.push_back(TopQuery{p - q0, p, r - row_begin});
-      }
-      if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, cosine_perm_device(h), d_ids, d_scores, d_counts)))
-        return rc;
-      ti = tj;
+    std::vector<int64_t> pos(row_count), outp(row_count);
+    for (int64_t r = row_begin; r < row_begin + row_count; ++r) {
+      pos[r - row_begin] = h->h_inv[r];
+      outp[r - row_begin] = r - row_begin;
     }
-    return CMS_OK;
+    return slab_top_k_positions(h, pos, outp, k, d_ids, d_scores, d_counts);
   }
   // exact pair kernel per query row (widths not a multiple of 128, or owners
   // whose norms left the exact fp64 regime)

@@ -185,6 +185,16 @@ class SketchTable:
                                        _ptr(cnt)))
         return ids, sc, cnt
 
+    def top_k_all(self, k):
+        """mostSimilar lists of every owner, [num_owners][k] by owner row
+        (symmetric streaming all-pairs pass)."""
+        n = self.num_owners
+        ids = np.zeros((n, k), np.int64)
+        sc = np.zeros((n, k), np.float64)
+        cnt = np.zeros(n, np.int32)
+        check(self._lib.cms_top_k_all(self._h, int(k), _ptr(ids), _ptr(sc), _ptr(cnt)))
+        return ids, sc, cnt
+
     def read_counters(self, row_begin=0, row_count=None):
         if row_count is None:
             row_count = self.num_owners - row_begin

@@ -333,3 +333,35 @@ def test_top_k_heavy_ties(oracle):
                 eids, esc = oracle.top_users(np.arange(n), sims, k)
                 assert ids[q, :cnt[q]].tolist() == eids.tolist(), (k, q)
                 assert same(sc[q, :cnt[q]], esc), (k, q)
+
+
+@pytest.mark.parametrize("n,d,w,vmax,k,weighted,seed", [
+    (3000, 5, 256, 3, 10, False, 51),     # multi-limb owners, partial last block
+    (2000, 4, 128, 50, 100, False, 52),   # most owners multi-limb: several S x M passes
+    (1800, 3, 256, 1, 64, True, 53),      # weighted: every score is +-1, ties by ID everywhere
+    (700, 5, 512, 2, 5, False, 54),       # fewer than one 256-row block pair per wave
+])
+def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed):
+    """cms_top_k_all (each unordered pair computed once, streamed into both
+    owners' lists) equals the per-row slab path for EVERY owner and the
+    oracle's TopItems restatement on a sample of rows, bit for bit."""
+    items, users = zipf_stream(4000, n, 400_000, seed=seed)
+    vals = np.random.Generator(np.random.PCG64(seed)).integers(1, vmax + 1, size=items.size).astype(np.float32)
+    ot = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42, weighted=weighted) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        ids, sc, cnt = t.top_k_all(k)
+        rids, rsc, rcnt = t.top_k_rows(0, n, k)
+        assert t.stats()["topk_redo"] == 0
+        assert np.array_equal(cnt, rcnt)
+        for q in range(n):
+            assert ids[q, :cnt[q]].tolist() == rids[q, :rcnt[q]].tolist(), q
+            assert same(sc[q, :cnt[q]], rsc[q, :rcnt[q]]), q
+        for q in list(range(0, n, max(1, n // 29))) + [n - 1]:
+            sims = _oracle_row_sims(oracle, ot, q, weighted)
+            eids, esc = oracle.top_users(np.arange(n), sims, k)
+            assert ids[q, :cnt[q]].tolist() == eids.tolist(), q
+            assert same(sc[q, :cnt[q]], esc), q
+        if vmax > 1:
+            assert t.stats()["multi_limb_owners"] > 0
