@@ -160,6 +160,16 @@ int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n,
 /* DoubleCountMinSketch.get(key) of owner `id` (DoubleCountMinSketch.java:94-103),
  * the point query GenericUserBasedRecommender uses (:153-158). */
 int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out);
+/* GenericUserBasedRecommender.doEstimatePreference(user, neighbourhood, item)
+ * with the CosineCM point query (GenericUserBasedRecommender.java:134-184) for
+ * q items at once: out[i] is the float estimate for item_keys[i], NaN when
+ * fewer than two neighbours carry data.  neighbor_ids is the neighbourhood in
+ * the caller's order (NearestNUserNeighborhood order); use_capper applies
+ * EstimatedPreferenceCapper(cap_min, cap_max) (:209-216).  The DataModel's own
+ * preference short cut of estimatePreference (:108-116) stays with the caller. */
+int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neighbor_ids, int64_t m,
+                             const int64_t* item_keys, int64_t q, int32_t use_capper, float cap_min, float cap_max,
+                             float* out);
 /* GenericUserBasedRecommender.mostSimilarUserIDs(id, k) with the CosineCM
  * estimator (:119-127, :231-247) and TopItems.getTopUsers (TopItems.java:91-136):
  * the first k other owners under (similarity desc, ID asc), NaN excluded.

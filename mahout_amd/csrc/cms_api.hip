@@ -494,6 +494,37 @@ int cms_similarity(cms_handle* h, int64_t id1, int64_t id2, double* out) {
   return cms_similarities(h, id1, &id2, 1, out);
 }
 
+int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neighbor_ids, int64_t m,
+                             const int64_t* item_keys, int64_t q, int32_t use_capper, float cap_min, float cap_max,
+                             float* out) {
+  if (!h || m < 0 || q < 0 || (m > 0 && !neighbor_ids) || (q > 0 && (!item_keys || !out)))
+    return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  int64_t urow;
+  if ((rc = row_of(h, user_id, &urow))) return rc;
+  std::vector<int64_t> rows(m);
+  for (int64_t i = 0; i < m; ++i)
+    if ((rc = row_of(h, neighbor_ids[i], &rows[i]))) return rc;
+  if (q == 0) return CMS_OK;
+  DevBuf d_rows, d_sims, d_items, d_out;
+  CMS_HIP(d_rows.ensure(sizeof(int64_t) * std::max<int64_t>(m, 1)));
+  CMS_HIP(d_sims.ensure(sizeof(double) * std::max<int64_t>(m, 1)));
+  CMS_HIP(d_items.ensure(sizeof(int64_t) * q));
+  CMS_HIP(d_out.ensure(sizeof(float) * q));
+  if (m > 0)
+    CMS_HIP(hipMemcpyAsync(d_rows.ptr, rows.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipMemcpyAsync(d_items.ptr, item_keys, sizeof(int64_t) * q, hipMemcpyHostToDevice, h->stream));
+  if ((rc = pair_cosines(h, urow, d_rows.as<int64_t>(), m, d_sims.as<double>()))) return rc;
+  if ((rc = estimate_preferences(h, urow, d_rows.as<int64_t>(), d_sims.as<double>(), m, d_items.as<int64_t>(), q,
+                                 use_capper, cap_min, cap_max, d_out.as<float>())))
+    return rc;
+  CMS_HIP(hipMemcpyAsync(out, d_out.ptr, sizeof(float) * q, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
 int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
   Guard g(h);

@@ -141,6 +141,8 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
 // ---- launchers (cms_query.hip) ----
 int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);
 int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
+                         const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out);
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts);
 // exact top-k (slab path) of the owners at PERMUTED positions pos, written at out_pos

@@ -138,6 +138,61 @@ __global__ void k_point_query(const uint32_t* table, HashParams hp, int64_t row,
   }
 }
 
+// GenericUserBasedRecommender.doEstimatePreference with the CosineCM point
+// query (GenericUserBasedRecommender.java:134-184), one thread per item, the
+// neighbourhood walked in the caller's order so the fp64 sums round as in Java:
+// pref = (float) get(item) of the neighbour's sketch (0 -> no data point),
+// sim = userSimilarity(user, neighbour) (NaN skipped), preference += sim*pref,
+// total += sim; < 2 points -> NaN; (float)(preference/total); then the
+// EstimatedPreferenceCapper clamp when enabled.
+__global__ void k_estimate(const uint32_t* table, HashParams hp, int64_t user_row, const int64_t* nb_rows,
+                           const double* sims, int64_t m, const int64_t* items, int64_t q, int use_capper, float lo,
+                           float hi, float* out) {
+  const int64_t dw = (int64_t)hp.depth * hp.width;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < q; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t kp = reduce_key(items[i]);
+    uint32_t bk[CMS_MAX_DEPTH];
+    for (int d = 0; d < hp.depth; ++d) bk[d] = (uint32_t)d * hp.width + bucket(hp, d, kp);
+    double preference = 0.0, total = 0.0;
+    int count = 0;
+    for (int64_t j = 0; j < m; ++j) {
+      const int64_t r = nb_rows[j];
+      if (r == user_row) continue;
+      double est = DBL_MAX;
+      for (int d = 0; d < hp.depth; ++d) {
+        const double v = (double)table[r * dw + bk[d]];
+        if (v < est) est = v;
+      }
+      const float pref = (float)est;
+      if (pref == 0.0f) continue;
+      const double s = sims[j];
+      if (s != s) continue;
+      preference = __dadd_rn(preference, __dmul_rn(s, (double)pref));
+      total = __dadd_rn(total, s);
+      ++count;
+    }
+    float e = __builtin_nanf("");
+    if (count > 1) {
+      e = (float)__ddiv_rn(preference, total);
+      if (use_capper) {
+        if (e > hi) e = hi;
+        else if (e < lo) e = lo;
+      }
+    }
+    out[i] = e;
+  }
+}
+
+int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
+                         const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out) {
+  if (q <= 0) return CMS_OK;
+  unsigned grid = (unsigned)std::min<int64_t>((q + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_estimate, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->hp, user_row, d_nb_rows, d_sims,
+                     m, d_items, q, use_capper, lo, hi, d_out);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
   if (m <= 0) return CMS_OK;
   unsigned grid = (unsigned)std::min<int64_t>((m + 255) / 256, 4096);

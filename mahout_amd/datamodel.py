@@ -63,6 +63,26 @@ class GenericDataModel:
     def hasPreferenceValues(self):
         return self.values is not None
 
+    def getMinPreference(self):
+        """Smallest preference value (GenericDataModel.java:87-116); +inf when
+        empty; NaN without values (AbstractDataModel.java:31-34)."""
+        if self.values is None:
+            return float("nan")
+        return float(self.values.min()) if self.values.size else float("inf")
+
+    def getMaxPreference(self):
+        if self.values is None:
+            return float("nan")
+        return float(self.values.max()) if self.values.size else float("-inf")
+
+    def getPreferenceValue(self, user_id, item_id):
+        """GenericDataModel.getPreferenceValue (:244-253): the value, or None."""
+        keys, vals = self.getPreferencesFromUser(user_id)
+        j = np.searchsorted(keys, item_id)
+        if j < keys.size and keys[j] == item_id:
+            return None if vals is None else float(vals[j])
+        return None
+
     def getPreferencesFromUser(self, user_id):
         """(item IDs ascending, float values) -- GenericDataModel.java:210-216."""
         i = np.searchsorted(self.user_ids, user_id)

@@ -185,6 +185,17 @@ class SketchTable:
                                        _ptr(cnt)))
         return ids, sc, cnt
 
+    def estimate_preferences(self, user_id, neighbor_ids, item_keys, capper=None):
+        """doEstimatePreference(user, neighbourhood, item) for every item key
+        (CosineCM point-query path); capper = (min, max) or None."""
+        nb = np.ascontiguousarray(neighbor_ids, np.int64)
+        it = np.ascontiguousarray(item_keys, np.int64)
+        out = np.zeros(it.size, np.float32)
+        lo, hi = capper if capper is not None else (0.0, 0.0)
+        check(self._lib.cms_estimate_preferences(self._h, int(user_id), _ptr(nb), nb.size, _ptr(it), it.size,
+                                                 int(capper is not None), float(lo), float(hi), _ptr(out)))
+        return out
+
     def top_k_all(self, k):
         """mostSimilar lists of every owner, [num_owners][k] by owner row
         (symmetric streaming all-pairs pass)."""

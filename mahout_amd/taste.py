@@ -164,3 +164,49 @@ class CosineCM:
 
     def close(self):
         self._table.close()
+
+
+class NearestNUserNeighborhood:
+    """NearestNUserNeighborhood(n, similarity, model): the n most similar
+    users (T/impl/neighborhood/NearestNUserNeighborhood.java) -- TopItems
+    .getTopUsers with minSimilarity -inf and sampling rate 1, i.e. the same
+    order as mostSimilarUserIDs."""
+
+    def __init__(self, n, userSimilarity, dataModel):
+        if n < 1:
+            raise ValueError("n must be at least 1")
+        self.n = n
+        self._sim = userSimilarity
+        self._model = dataModel
+
+    def getUserNeighborhood(self, userID):
+        return self._sim.mostSimilarUserIDs(userID, self.n)
+
+
+class GenericUserBasedRecommender:
+    """GenericUserBasedRecommender(model, neighborhood, CosineCM): the
+    estimate path with the sketch point query
+    (T/impl/recommender/GenericUserBasedRecommender.java:108-116, 134-184),
+    capped by EstimatedPreferenceCapper when the model has min/max (:209-216)."""
+
+    def __init__(self, dataModel, neighborhood, similarity):
+        self._model = dataModel
+        self._nb = neighborhood
+        self._sim = similarity
+        lo, hi = dataModel.getMinPreference(), dataModel.getMaxPreference()
+        self._capper = None if (np.isnan(lo) and np.isnan(hi)) else (lo, hi)
+
+    def estimatePreference(self, userID, itemID):
+        actual = self._model.getPreferenceValue(userID, itemID)
+        if actual is not None:
+            return np.float32(actual)
+        return self.doEstimatePreferences(userID, self._nb.getUserNeighborhood(userID), [itemID])[0]
+
+    def doEstimatePreferences(self, theUserID, theNeighborhood, itemIDs):
+        """doEstimatePreference for many items at once (one GPU launch)."""
+        if len(theNeighborhood) == 0:
+            return np.full(len(itemIDs), np.nan, np.float32)
+        try:
+            return self._sim.table.estimate_preferences(theUserID, theNeighborhood, itemIDs, self._capper)
+        except _lib.CmsError as e:
+            raise _map_error(e, "user")

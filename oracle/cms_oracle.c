@@ -171,6 +171,33 @@ void orc_similarities_row(const double* table, int64_t rows, int32_t depth, int3
   }
 }
 
+float orc_estimate_preference(const double* table, int32_t depth, int32_t width, const int64_t* a, const int64_t* b,
+                              int64_t user_row, const int64_t* nb_rows, int64_t m, int64_t item_key, int weighted,
+                              int use_capper, float cap_min, float cap_max) {
+  const int64_t stride = (int64_t)depth * width;
+  if (m == 0) return NAN;
+  double preference = 0.0, total = 0.0;
+  int count = 0;
+  for (int64_t i = 0; i < m; i++) {
+    const int64_t r = nb_rows[i];
+    if (r == user_row) continue;
+    const float pref = (float)orc_sketch_get(table + r * stride, depth, width, a, b, item_key);
+    if (pref == 0.0f) continue; /* no data point */
+    const double s = orc_cosine_cm(table + user_row * stride, table + r * stride, depth, width, weighted);
+    if (isnan(s)) continue;
+    preference += s * (double)pref;
+    total += s;
+    count++;
+  }
+  if (count <= 1) return NAN;
+  float estimate = (float)(preference / total);
+  if (use_capper) {
+    if (estimate > cap_max) estimate = cap_max;
+    else if (estimate < cap_min) estimate = cap_min;
+  }
+  return estimate;
+}
+
 /* SimilarUser.compareTo (T/impl/recommender/SimilarUser.java:62-78): similarity
  * desc, then ID asc.  Returns <0 if x sorts before y. */
 static int su_cmp(int64_t xid, double xs, int64_t yid, double ys) {

@@ -69,6 +69,18 @@ double orc_cosine_cm(const double* sa, const double* sb, int32_t depth, int32_t 
 void orc_similarities_row(const double* table, int64_t rows, int32_t depth, int32_t width,
                           int64_t q, int weighted, double* out);
 
+/* GenericUserBasedRecommender.doEstimatePreference with the CosineCM point
+ * query (T/impl/recommender/GenericUserBasedRecommender.java:134-184): over
+ * the neighbourhood rows in order (the user's own row skipped), pref =
+ * (float) get(item) of the neighbour's sketch, 0 -> no data; sim =
+ * userSimilarity(user, neighbour), NaN skipped; preference += sim * pref,
+ * total += sim; fewer than 2 data points -> NaN; (float)(preference/total),
+ * then EstimatedPreferenceCapper (:209-216, EstimatedPreferenceCapper.java)
+ * when use_capper. */
+float orc_estimate_preference(const double* table, int32_t depth, int32_t width, const int64_t* a, const int64_t* b,
+                              int64_t user_row, const int64_t* nb_rows, int64_t m, int64_t item_key, int weighted,
+                              int use_capper, float cap_min, float cap_max);
+
 /* TopItems.getTopUsers (T/impl/recommender/TopItems.java:91-136) + SimilarUser.compareTo
  * (T/impl/recommender/SimilarUser.java:62-78), over candidates in ascending ID order.
  * Returns the count written to out_ids (<= k).  scores[i] belongs to ids[i]. */

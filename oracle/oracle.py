@@ -39,6 +39,8 @@ def _load():
         "orc_cosine_cm": (c.c_double, [c.c_void_p, c.c_void_p, c.c_int32, c.c_int32, c.c_int]),
         "orc_similarities_row": (None, [_f64p, c.c_int64, c.c_int32, c.c_int32, c.c_int64, c.c_int, _f64p]),
         "orc_top_users": (c.c_int32, [_i64p, _f64p, c.c_int64, c.c_int32, _i64p, _f64p]),
+        "orc_estimate_preference": (c.c_float, [_f64p, c.c_int32, c.c_int32, _i64p, _i64p, c.c_int64, _i64p, c.c_int64,
+                                                c.c_int64, c.c_int, c.c_int, c.c_float, c.c_float]),
         "orc_fmeasure": (c.c_double, [c.c_int32, c.c_int32, c.c_int32, c.c_int32, c.c_double]),
         "orc_compute_config": (c.c_int, [c.c_int32, c.c_int32, c.c_double, c.POINTER(c.c_int32), c.POINTER(c.c_int32),
                                          c.POINTER(c.c_double), c.POINTER(c.c_double)]),
@@ -131,6 +133,17 @@ def similarities_row(table, q, weighted=False):
     out = np.zeros(rows, np.float64)
     lib().orc_similarities_row(np.ascontiguousarray(table), rows, d, w, q, int(weighted), out)
     return out
+
+
+def estimate_preference(table, a, b, user_row, nb_rows, item_key, weighted=False, capper=None):
+    """GenericUserBasedRecommender.doEstimatePreference with the CosineCM point
+    query; capper = (min, max) or None."""
+    rows, d, w = table.shape
+    nb = np.ascontiguousarray(nb_rows, np.int64)
+    lo, hi = capper if capper is not None else (0.0, 0.0)
+    return lib().orc_estimate_preference(np.ascontiguousarray(table), d, w, np.ascontiguousarray(a, np.int64),
+                                         np.ascontiguousarray(b, np.int64), int(user_row), nb, nb.size,
+                                         int(item_key), int(weighted), int(capper is not None), float(lo), float(hi))
 
 
 def top_users(ids, scores, k):

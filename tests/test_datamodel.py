@@ -38,3 +38,40 @@ def test_generic_csr_layout():
     assert m.offsets.tolist() == [0, 1, 3]
     assert m.keys.tolist() == [1, 1, 3]
     assert m.values.dtype == np.float32
+
+
+def test_min_max_and_preference_value():
+    from mahout_amd.datamodel import GenericDataModel
+    m = GenericDataModel({1: {10: 2.5, 11: 0.5}, 2: {10: 4.0}})
+    assert m.getMinPreference() == 0.5 and m.getMaxPreference() == 4.0
+    assert m.getPreferenceValue(1, 11) == 0.5
+    assert m.getPreferenceValue(2, 11) is None
+
+
+def test_estimate_preference_oracle_hand_kat(oracle):
+    """doEstimatePreference on a collision-free sketch by hand: the point
+    query returns the exact rating, the sketch cosine the exact cosine."""
+    import math
+    import numpy as np
+    keys = [101, 202, 303]
+    d, w = 3, 4096
+    seed = None
+    for s in range(1, 5000):
+        a, b = oracle.hash_params(s, d)
+        h = oracle.hash_keys(a, b, w, np.array(keys, np.int64))
+        if all(len(set(h[:, r].tolist())) == len(keys) for r in range(d)):
+            seed = s
+            break
+    a, b = oracle.hash_params(seed, d)
+    # user 0 rated 101 -> 3; user 1 rated 101 -> 4, 202 -> 2; user 2 rated 101 -> 1, 202 -> 5, 303 -> 2
+    rows = np.array([0, 1, 1, 2, 2, 2], np.int64)
+    ks = np.array([101, 101, 202, 101, 202, 303], np.int64)
+    vals = np.array([3, 4, 2, 1, 5, 2], np.float32)
+    t = oracle.build_table(3, d, w, a, b, rows, ks, vals)
+    s1 = 12.0 / (3.0 * math.sqrt(20.0))         # cosine(u0, u1): every row equal
+    s2 = 3.0 / (3.0 * math.sqrt(30.0))          # cosine(u0, u2)
+    exp = np.float32((s1 * 2.0 + s2 * 5.0) / (s1 + s2))
+    got = oracle.estimate_preference(t, a, b, 0, [1, 2, 0], 202)
+    assert got == exp
+    assert math.isnan(oracle.estimate_preference(t, a, b, 0, [1, 2], 303))  # one data point only
+    assert oracle.estimate_preference(t, a, b, 0, [1, 2], 202, capper=(1.0, 2.5)) == np.float32(2.5)

@@ -365,3 +365,27 @@ def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed)
             assert same(sc[q, :cnt[q]], esc), q
         if vmax > 1:
             assert t.stats()["multi_limb_owners"] > 0
+
+
+@pytest.mark.parametrize("weighted,capper", [(False, None), (False, (1.0, 4.5)), (True, (1.0, 5.0))])
+def test_estimate_preferences_point_query_path(oracle, weighted, capper):
+    """GenericUserBasedRecommender.doEstimatePreference with the CosineCM
+    point query, every item of the universe, bit-exact float estimates."""
+    n_users, n_items, d, w = 300, 2000, 4, 512
+    # owners are users, keys are items (the non-transposed orientation)
+    users, items = zipf_stream(n_items, n_users, 60_000, seed=61)
+    vals = np.random.Generator(np.random.PCG64(61)).integers(1, 6, size=items.size).astype(np.float32)
+    ot = oracle_table(oracle, n_users, d, w, 42, users, items, vals)
+    a, b = oracle.hash_params(42, d)
+    with SketchTable(n_users, depth=d, width=w, seed=42, weighted=weighted) as t:
+        t.ingest(users, items, vals)
+        t.finalize()
+        all_items = np.arange(n_items, dtype=np.int64)
+        for u in [0, 5, 77, 299]:
+            nb, _ = t.most_similar(u, 12)
+            nb = np.concatenate([nb, [u]])  # the user's own ID is skipped, as in the reference
+            got = t.estimate_preferences(u, nb, all_items, capper)
+            exp = np.array([oracle.estimate_preference(ot, a, b, u, nb, it, weighted, capper) for it in all_items],
+                           np.float32)
+            assert same(got, exp), u
+            assert np.isfinite(got).sum() > 0
