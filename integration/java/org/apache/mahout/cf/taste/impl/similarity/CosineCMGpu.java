@@ -145,6 +145,24 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     return nativePointQuery(handle, ownerID, key);
   }
 
+  /**
+   * GenericUserBasedRecommender.doEstimatePreference(user, neighborhood, item)
+   * with the CosineCM point query, for many items in one call; NaN where fewer
+   * than two neighbours carry data. Pass capMin/capMax = NaN for no capper.
+   */
+  public float[] estimatePreferences(long userID, long[] neighborhood, long[] itemIDs, float capMin, float capMax)
+      throws TasteException {
+    return nativeEstimatePreferences(handle, userID, neighborhood, itemIDs, capMin, capMax);
+  }
+
+  /**
+   * mostSimilarIDs for every owner at once (each unordered pair computed once):
+   * row r of the result holds the IDs for the r-th owner in ascending ID order.
+   */
+  public long[][] allMostSimilarIDs(int howMany) throws TasteException {
+    return nativeTopKAll(handle, howMany);
+  }
+
   @Override
   public void refresh(Collection<Refreshable> alreadyRefreshed) {
     super.refresh(alreadyRefreshed);
@@ -177,5 +195,8 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private static native double[] nativeSimilarities(long h, long id1, long[] ids2) throws TasteException;
   private static native long[] nativeMostSimilar(long h, long id, int k) throws TasteException;
   private static native double nativePointQuery(long h, long id, long key) throws TasteException;
+  private static native float[] nativeEstimatePreferences(long h, long user, long[] neighbors, long[] items,
+                                                          float capMin, float capMax) throws TasteException;
+  private static native long[][] nativeTopKAll(long h, int k) throws TasteException;
   private static native void nativeDestroy(long h);
 }

@@ -124,6 +124,56 @@ JNIEXPORT jdouble JNICALL JFN(nativePointQuery)(JNIEnv* env, jclass c, jlong h, 
   return out;
 }
 
+JNIEXPORT jfloatArray JNICALL JFN(nativeEstimatePreferences)(JNIEnv* env, jclass c, jlong h, jlong user,
+                                                               jlongArray nbs, jlongArray items, jfloat cap_min,
+                                                               jfloat cap_max) {
+  (void)c;
+  jsize m = (*env)->GetArrayLength(env, nbs);
+  jsize q = (*env)->GetArrayLength(env, items);
+  int64_t* nb = (int64_t*)malloc(sizeof(int64_t) * (m ? m : 1));
+  int64_t* it = (int64_t*)malloc(sizeof(int64_t) * (q ? q : 1));
+  float* out = (float*)malloc(sizeof(float) * (q ? q : 1));
+  (*env)->GetLongArrayRegion(env, nbs, 0, m, (jlong*)nb);
+  (*env)->GetLongArrayRegion(env, items, 0, q, (jlong*)it);
+  const int use_capper = !(cap_min != cap_min && cap_max != cap_max);  /* both NaN: no capper (:209-216) */
+  int rc = cms_estimate_preferences(H(h), user, nb, m, it, q, use_capper, cap_min, cap_max, out);
+  jfloatArray res = NULL;
+  if (rc == CMS_OK) {
+    res = (*env)->NewFloatArray(env, q);
+    if (res) (*env)->SetFloatArrayRegion(env, res, 0, q, out);
+  }
+  free(nb);
+  free(it);
+  free(out);
+  return fail(env, rc, 0) ? NULL : res;
+}
+
+JNIEXPORT jobjectArray JNICALL JFN(nativeTopKAll)(JNIEnv* env, jclass c, jlong h, jint k) {
+  (void)c;
+  cms_stats st;
+  st.pairs_ingested = 0;
+  if (fail(env, cms_get_stats(H(h), &st), 0)) return NULL;
+  const int64_t n = st.num_owners;
+  int64_t* ids = (int64_t*)malloc(sizeof(int64_t) * (size_t)n * (k > 0 ? k : 1));
+  int32_t* cnt = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+  int rc = cms_top_k_all(H(h), k, ids, NULL, cnt);
+  jobjectArray res = NULL;
+  if (rc == CMS_OK) {
+    jclass longArr = (*env)->FindClass(env, "[J");
+    res = longArr ? (*env)->NewObjectArray(env, (jsize)n, longArr, NULL) : NULL;
+    for (int64_t r = 0; res && r < n; ++r) {
+      jlongArray row = (*env)->NewLongArray(env, cnt[r]);
+      if (!row) { res = NULL; break; }
+      (*env)->SetLongArrayRegion(env, row, 0, cnt[r], (const jlong*)(ids + r * k));
+      (*env)->SetObjectArrayElement(env, res, (jsize)r, row);
+      (*env)->DeleteLocalRef(env, row);
+    }
+  }
+  free(ids);
+  free(cnt);
+  return fail(env, rc, 0) ? NULL : res;
+}
+
 JNIEXPORT void JNICALL JFN(nativeDestroy)(JNIEnv* env, jclass c, jlong h) {
   (void)env;
   (void)c;
