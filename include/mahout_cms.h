@@ -186,6 +186,16 @@ int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t 
  * row, counts[num_owners]; k <= 512. */
 int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts);
 
+/* cms_top_k_all written as FileSimilarItemsWriter does
+ * (T/impl/similarity/precompute/FileSimilarItemsWriter.java:50-61): one line
+ * "itemID,similarItemID,similarity" per similar item, owners in ascending ID
+ * order, each list most similar first; similarity as Java's
+ * String.valueOf(double), narrowed to float first when as_float (the
+ * RecommendedItem values SimilarItems carries, SimilarItems.java:36-47). */
+int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
+/* Java Double.toString(v) into buf (NUL-terminated); returns the length or -1. */
+int cms_format_java_double(double v, char* buf, int32_t cap);
+
 /* Counters of rows [row_begin, row_begin+row_count) as fp64 (the reference's
  * counter type), [row_count][d][w]. */
 int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out);

@@ -607,6 +607,20 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
   return rc;
 }
 
+int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float) {
+  if (!h || !path) return set_error(CMS_E_PARAM, "null argument");
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  return write_similar_items(h, path, k, as_float);
+}
+
+int cms_format_java_double(double v, char* buf, int32_t cap) {
+  if (!buf || cap <= 0) return -1;
+  return java_double_to_string(v, buf, cap);
+}
+
 int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
   Guard g(h);

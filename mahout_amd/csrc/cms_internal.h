@@ -164,6 +164,9 @@ int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint
 int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t k, int64_t* d_ids, double* d_scores,
               int32_t* d_counts);
 int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
+// ---- cms_output.cpp ----
+int java_double_to_string(double v, char* out, int cap);
+int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
 // ---- cms_cosine_mfma.hip ----
 const int64_t* cosine_perm_device(cms_handle* h);
 // ---- cms_cosine_mfma.hip ----

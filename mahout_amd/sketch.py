@@ -6,6 +6,7 @@ builds the same sketches one DoubleCountMinSketch at a time
 (T/impl/common/DoubleCountMinSketch.java, T/impl/similarity/CosineCM.java:41-67).
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -196,6 +197,10 @@ class SketchTable:
                                                  int(capper is not None), float(lo), float(hi), _ptr(out)))
         return out
 
+    def write_similar_items(self, path, k, as_float=True):
+        """cms_top_k_all in FileSimilarItemsWriter's CSV format."""
+        check(self._lib.cms_write_similar_items(self._h, os.fsencode(path), int(k), int(as_float)))
+
     def top_k_all(self, k):
         """mostSimilar lists of every owner, [num_owners][k] by owner row
         (symmetric streaming all-pairs pass)."""
@@ -251,3 +256,12 @@ def _release_scratch(self):
 
 
 SketchTable.release_scratch = _release_scratch
+
+
+def java_double_to_string(v):
+    """Java Double.toString(v) as the library writes it (cms_format_java_double)."""
+    buf = ctypes.create_string_buffer(64)
+    n = _lib.load().cms_format_java_double(float(v), buf, 64)
+    if n < 0:
+        raise ValueError(v)
+    return buf.value.decode()

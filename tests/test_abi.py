@@ -5,6 +5,7 @@ import math
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -90,3 +91,16 @@ def test_vectorised_shard_matches_library(lib):
     for world in [1, 2, 3, 8]:
         got = shard_of_keys(keys, world)
         assert got.tolist() == [shard_of_key(int(k), world) for k in keys]
+
+
+@pytest.mark.parametrize("v,java", [
+    (0.1, "0.1"), (1.0, "1.0"), (float(np.float32(0.1)), "0.10000000149011612"), (1e-4, "1.0E-4"),
+    (1e7, "1.0E7"), (9999999.0, "9999999.0"), (0.001, "0.001"), (-0.0, "-0.0"), (0.0, "0.0"),
+    (float("nan"), "NaN"), (float("inf"), "Infinity"), (float("-inf"), "-Infinity"), (12345678.9, "1.23456789E7"),
+    (0.5, "0.5"), (100.0, "100.0"), (-2.5e-5, "-2.5E-5"), (0.0009999, "9.999E-4"), (0.769846046, "0.769846046"),
+    (float(np.float32(0.45)), "0.44999998807907104"), (1.5e300, "1.5E300")])
+def test_java_double_to_string(v, java):
+    """FileSimilarItemsWriter writes String.valueOf(double): Java's
+    Double.toString layout (plain in [1e-3, 1e7), else d.dddE[-]n)."""
+    from mahout_amd.sketch import java_double_to_string
+    assert java_double_to_string(v) == java

@@ -389,3 +389,24 @@ def test_estimate_preferences_point_query_path(oracle, weighted, capper):
                            np.float32)
             assert same(got, exp), u
             assert np.isfinite(got).sum() > 0
+
+
+def test_write_similar_items_csv(oracle, tmp_path):
+    """FileSimilarItemsWriter lines for every owner: ascending owner ID, each
+    list most similar first, float-narrowed values in Java Double.toString."""
+    from mahout_amd.sketch import java_double_to_string
+    n, d, w, k = 400, 4, 256, 7
+    items, users = zipf_stream(3000, n, 80_000, seed=71)
+    ids_universe = np.arange(n, dtype=np.int64) * 3 + 1000
+    with SketchTable(n, depth=d, width=w, seed=42, owner_ids=ids_universe) as t:
+        t.ingest(ids_universe[items], users)
+        t.finalize()
+        ids, sc, cnt = t.top_k_all(k)
+        path = tmp_path / "similar.csv"
+        t.write_similar_items(str(path), k)
+    lines = path.read_text().splitlines()
+    exp = []
+    for r in range(n):
+        for i in range(cnt[r]):
+            exp.append(f"{ids_universe[r]},{ids[r, i]},{java_double_to_string(float(np.float32(sc[r, i])))}")
+    assert lines == exp
