@@ -185,6 +185,18 @@ int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t 
  * owners' lists (no n x n slab).  ids/scores are [num_owners][k] by owner
  * row, counts[num_owners]; k <= 512. */
 int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts);
+/* With a communicator (cms_comm_init, world G > 1) cms_top_k_all is collective:
+ * rank r computes shard r of the pairs, the partial lists are all-gathered
+ * over RCCL and merged exactly; every rank receives the full result
+ * (G * k <= 1024).  The two pieces are also exported: */
+/* The partial lists of shard `shard` of `nshards` ([num_owners][k] IDs and
+ * scores, counts): every pair is computed by exactly one shard. */
+int cms_top_k_all_partial(cms_handle* h, int32_t k, int32_t shard, int32_t nshards, int64_t* ids, double* scores,
+                          int32_t* counts);
+/* Exact merge of nparts partial lists laid out [nparts][num_owners][k] (counts
+ * [nparts][num_owners]) into the final lists (nparts * k <= 1024). */
+int cms_top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* ids, const double* scores,
+                    const int32_t* counts, int64_t* out_ids, double* out_scores, int32_t* out_counts);
 
 /* cms_top_k_all written as FileSimilarItemsWriter does
  * (T/impl/similarity/precompute/FileSimilarItemsWriter.java:50-61): one line

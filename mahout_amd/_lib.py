@@ -33,7 +33,7 @@ EXPORTS = [
     "cms_ingest_device_rows", "cms_ingest_csr", "cms_ingest_csr_device", "cms_reset", "cms_release_scratch",
     "cms_comm_unique_id",
     "cms_comm_init", "cms_shard_of_key", "cms_finalize", "cms_synchronize", "cms_similarity", "cms_similarities",
-    "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
+    "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_top_k_all_partial", "cms_top_k_merge", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
 ]
 
@@ -101,6 +101,8 @@ _SIGS = {
     "cms_estimate_preferences": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i32, ctypes.c_float, ctypes.c_float, _vp]),
     "cms_write_similar_items": (_int, [_vp, ctypes.c_char_p, _i32, _i32]),
     "cms_format_java_double": (_int, [ctypes.c_double, ctypes.c_char_p, _i32]),
+    "cms_top_k_all_partial": (_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "cms_top_k_merge": (_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cms_top_k_all": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_read_counters": (_int, [_vp, _i64, _i64, _vp]),
     "cms_get_stats": (_int, [_vp, ctypes.POINTER(CmsStats)]),

@@ -595,7 +595,38 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
   CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
   CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
   CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
-  rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
+  if (h->comm && h->world > 1) {
+    // one process per GPU: rank r computes shard r of the pairs, then one
+    // all-gather of the partial lists over xGMI and an exact merge
+    if ((int64_t)h->world * k > kCandCap) return set_error(CMS_E_PARAM, "world * k must be <= %d", kCandCap);
+    const int G = h->world;
+    DevBuf g_ids, g_sc, g_cnt;
+    CMS_HIP(g_ids.ensure(sizeof(int64_t) * n * k * G));
+    CMS_HIP(g_sc.ensure(sizeof(double) * n * k * G));
+    CMS_HIP(g_cnt.ensure(sizeof(int32_t) * n * G));
+    rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>(), h->rank, G);
+    if (rc) return rc;
+    {
+      TimedScope ts(h, "topk_allgather");
+      ncclResult_t r = ncclGroupStart();
+      if (r == ncclSuccess)
+        r = ncclAllGather(o_ids.ptr, g_ids.ptr, (size_t)(n * k), ncclInt64, h->comm, h->stream);
+      if (r == ncclSuccess)
+        r = ncclAllGather(o_sc.ptr, g_sc.ptr, (size_t)(n * k), ncclFloat64, h->comm, h->stream);
+      if (r == ncclSuccess) r = ncclAllGather(o_cnt.ptr, g_cnt.ptr, (size_t)n, ncclInt32, h->comm, h->stream);
+      ncclResult_t r2 = ncclGroupEnd();
+      if (r == ncclSuccess) r = r2;
+      if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather(top-k lists): %s", ncclGetErrorString(r));
+    }
+    rc = top_k_merge(h, k, G, g_ids.as<int64_t>(), g_sc.as<double>(), g_cnt.as<int32_t>(), o_ids.as<int64_t>(),
+                     o_sc.as<double>(), o_cnt.as<int32_t>());
+    if (rc == CMS_OK) {
+      const hipError_t e = hipStreamSynchronize(h->stream);
+      if (e != hipSuccess) rc = hip_fail(e, "top-k merge");
+    }
+  } else {
+    rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
+  }
   if (rc == CMS_OK) {
     hipError_t e = hipMemcpyAsync(ids, o_ids.ptr, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, h->stream);
     if (e == hipSuccess && scores)
@@ -605,6 +636,56 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
     if (e != hipSuccess) rc = hip_fail(e, "top-k copy-out");
   }
   return rc;
+}
+
+int cms_top_k_all_partial(cms_handle* h, int32_t k, int32_t shard, int32_t nshards, int64_t* ids, double* scores,
+                          int32_t* counts) {
+  if (!h || !ids || !scores || !counts) return set_error(CMS_E_PARAM, "null argument");
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  if (nshards < 1 || shard < 0 || shard >= nshards) return set_error(CMS_E_PARAM, "shard %d of %d", shard, nshards);
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  const int64_t n = h->n;
+  DevBuf o_ids, o_sc, o_cnt;
+  CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
+  CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
+  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
+  rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>(), shard, nshards);
+  if (rc) return rc;
+  CMS_HIP(hipMemcpyAsync(ids, o_ids.ptr, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(scores, o_sc.ptr, sizeof(double) * n * k, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(counts, o_cnt.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
+int cms_top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* ids, const double* scores,
+                    const int32_t* counts, int64_t* out_ids, double* out_scores, int32_t* out_counts) {
+  if (!h || !ids || !scores || !counts || !out_ids || !out_scores || !out_counts)
+    return set_error(CMS_E_PARAM, "null argument");
+  if (k < 1 || nparts < 1 || (int64_t)nparts * k > kCandCap)
+    return set_error(CMS_E_PARAM, "need k >= 1 and nparts * k <= %d", kCandCap);
+  Guard g(h);
+  const int64_t n = h->n;
+  DevBuf i_ids, i_sc, i_cnt, o_ids, o_sc, o_cnt;
+  CMS_HIP(i_ids.ensure(sizeof(int64_t) * n * k * nparts));
+  CMS_HIP(i_sc.ensure(sizeof(double) * n * k * nparts));
+  CMS_HIP(i_cnt.ensure(sizeof(int32_t) * n * nparts));
+  CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
+  CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
+  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
+  CMS_HIP(hipMemcpyAsync(i_ids.ptr, ids, sizeof(int64_t) * n * k * nparts, hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipMemcpyAsync(i_sc.ptr, scores, sizeof(double) * n * k * nparts, hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipMemcpyAsync(i_cnt.ptr, counts, sizeof(int32_t) * n * nparts, hipMemcpyHostToDevice, h->stream));
+  int rc = top_k_merge(h, k, nparts, i_ids.as<int64_t>(), i_sc.as<double>(), i_cnt.as<int32_t>(), o_ids.as<int64_t>(),
+                       o_sc.as<double>(), o_cnt.as<int32_t>());
+  if (rc) return rc;
+  CMS_HIP(hipMemcpyAsync(out_ids, o_ids.ptr, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(out_scores, o_sc.ptr, sizeof(double) * n * k, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(out_counts, o_cnt.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
 }
 
 int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float) {

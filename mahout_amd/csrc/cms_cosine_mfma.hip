@@ -1018,15 +1018,28 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
 // A row receives at most 512 offers per wave (its block as A, and as B), and
 // a list is compacted before a pass whenever it holds more than cap - 512, so
 // lists cannot overflow; should one ever do, the row is recomputed exactly.
-int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+// Shard `shard` of `nshards` computes a disjoint share of the pairs (M rows
+// p % nshards, S x M chunks, waves w % nshards) and leaves PARTIAL lists:
+// for every owner the first k of the candidates it saw, sorted.  The union
+// over shards is every pair once, so merging the partial lists
+// (top_k_merge) gives the exact result.  nshards == 1 is the whole job.
+int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts, int32_t shard,
+              int32_t nshards) {
   int rc = cosine_prepare(h);
   if (rc) return rc;
   const int64_t n = h->n, dw = h->dw;
   const BigCfg cfg = big_config(h);
   const int64_t nm = h->n_hot_limb, ns = n - nm;
   if (!cfg.nstage || (nm > 0 && !h->vl_slots) || h->n_inexact_rows != 0 || k > kCandCap / 2) {
-    return top_k_rows(h, 0, n, k, d_ids, d_scores, d_counts);  // per-row slab path
+    if (nshards == 1) return top_k_rows(h, 0, n, k, d_ids, d_scores, d_counts);  // per-row slab path
+    // per-row slab path for this shard's rows only; the other rows stay empty
+    CMS_HIP(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * n, h->stream));
+    for (int64_t r0 = shard; r0 < n; r0 += nshards) {
+      if ((rc = top_k_rows(h, r0, 1, k, d_ids + r0 * k, d_scores + r0 * k, d_counts + r0))) return rc;
+    }
+    return CMS_OK;
   }
+  CMS_HIP(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * n, h->stream));
   const int32_t cap = kCandCap;
   constexpr uint32_t kPerPass = 512;  // most offers one row takes in one pass
   DevBuf& ws = h->ws_cand;
@@ -1059,10 +1072,10 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   // 1. multi-limb rows: exact slab top-k
   if (nm > 0) {
     TimedScope ts(h, "topk_all_multi_rows");
-    std::vector<int64_t> pos(nm), outp(nm);
-    for (int64_t p = 0; p < nm; ++p) {
-      pos[p] = p;
-      outp[p] = h->h_perm[p];
+    std::vector<int64_t> pos, outp;
+    for (int64_t p = shard; p < nm; p += nshards) {
+      pos.push_back(p);
+      outp.push_back(h->h_perm[p]);
     }
     if ((rc = slab_top_k_positions(h, pos, outp, k, d_ids, d_scores, d_counts))) return rc;
   }
@@ -1077,7 +1090,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   if (nm > 0 && ns > 0) {
     const int ls = h->vl_slots, per = 32 / ls;
     const int8_t* vl = h->ws_vl.as<int8_t>();
-    for (int64_t m0 = 0; m0 < nm; m0 += kPerPass) {
+    for (int64_t m0 = (int64_t)shard * kPerPass; m0 < nm; m0 += (int64_t)nshards * kPerPass) {
       if ((rc = cand_compact(h, cb, nm, ns, (uint32_t)cap - kPerPass, k))) return rc;
       BigArgs g = base;
       g.A = vl + (m0 / per) * 32 * dw;
@@ -1095,7 +1108,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   // 3. S x S symmetric waves
   if (ns > 0) {
     const int64_t nb = (ns + kTA - 1) / kTA;
-    for (int64_t wv = 0; wv <= nb / 2; ++wv) {
+    for (int64_t wv = shard; wv <= nb / 2; wv += nshards) {
       int64_t pairs = nb;
       if (wv > 0 && 2 * wv == nb) pairs = nb / 2;  // {I, I + nb/2}: each pair once
       if ((rc = cand_compact(h, cb, nm, ns, (uint32_t)cap - kPerPass, k))) return rc;
@@ -1114,7 +1127,9 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     if ((rc = cand_compact(h, cb, nm, ns, 0, k))) return rc;
     if ((rc = cand_emit(h, cb, nm, ns, k, d_ids, d_scores, d_counts))) return rc;
   }
-  // rows whose list overflowed (not expected): exact per-row recompute
+  // rows whose list overflowed (not expected): exact per-row recompute (whole
+  // row, so a sharded job's merge still sees every pair once per shard at most:
+  // the row's other partial lists are subsets of this exact list)
   std::vector<uint32_t> ovf(ns > 0 ? ns : 1);
   if (ns > 0) CMS_HIP(hipMemcpyAsync(ovf.data(), cb.ovf + nm, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));

@@ -163,7 +163,11 @@ struct CandBufs {
 int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint32_t limit, int32_t k);
 int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t k, int64_t* d_ids, double* d_scores,
               int32_t* d_counts);
-int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
+int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts, int32_t shard = 0,
+              int32_t nshards = 1);
+// merge nparts partial top-k lists ([nparts][n][k] ids by owner ID, scores; [nparts][n] counts)
+int top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* d_ids, const double* d_scores,
+                const int32_t* d_counts, int64_t* d_out_ids, double* d_out_scores, int32_t* d_out_counts);
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);

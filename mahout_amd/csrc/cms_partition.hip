@@ -228,6 +228,7 @@ __global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* H2, const uint
   const uint32_t k0 = blkStart[b], k1 = blkStart[b + 1];
   for (int f = threadIdx.x; f < P2; f += blockDim.x) {
     uint32_t T = 0;
+#pragma unroll 8
     for (uint32_t k = k0; k < k1; ++k) T += H2[(int64_t)k * P2 + f];
     tots[f] = T;
   }
@@ -249,7 +250,19 @@ __global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* H2, const uint
     int64_t r = (int64_t)b * P2 + f;
     if (r < nrows) row_start[r] = base;
     uint32_t run = base;
-    for (uint32_t k = k0; k < k1; ++k) {
+    // the counts were read above; batch the loads so they are in flight together
+    uint32_t k = k0;
+    for (; k + 8 <= k1; k += 8) {
+      uint32_t c[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) c[u] = H2[(int64_t)(k + u) * P2 + f];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        O2[(int64_t)(k + u) * P2 + f] = run;
+        run += c[u];
+      }
+    }
+    for (; k < k1; ++k) {
       uint32_t c = H2[(int64_t)k * P2 + f];
       O2[(int64_t)k * P2 + f] = run;
       run += c;

@@ -514,6 +514,87 @@ __global__ void k_cand_emit(const uint32_t* ccnt, const uint32_t* cidx, const do
   }
 }
 
+// Union of nparts partial lists per owner -> the first k under (score desc,
+// ID asc).  Owner IDs ascend with owner rows, so ID order is the
+// SimilarUser tie order; an ID offered by two parts (a row recomputed whole
+// after an overflow) is kept once.
+__global__ __launch_bounds__(kCandThreads) void k_topk_merge(int32_t nparts, int32_t k, int64_t n, const int64_t* ids,
+                                                             const double* sc, const int32_t* cnt, int64_t* out_ids,
+                                                             double* out_sc, int32_t* out_cnt) {
+  __shared__ uint64_t key[kCandCap];
+  __shared__ int64_t oid[kCandCap];
+  __shared__ double val[kCandCap];
+  __shared__ uint32_t s_m;
+  const int tid = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    if (tid == 0) s_m = 0;
+    __syncthreads();
+    for (int32_t p = 0; p < nparts; ++p) {
+      const int32_t c = min(cnt[(int64_t)p * n + r], k);
+      for (int32_t i = tid; i < c; i += kCandThreads) {
+        const uint32_t pos = atomicAdd(&s_m, 1u);
+        const int64_t src = ((int64_t)p * n + r) * k + i;
+        key[pos] = score_key(sc[src]);
+        oid[pos] = ids[src];
+        val[pos] = sc[src];
+      }
+    }
+    __syncthreads();
+    const uint32_t m = s_m;
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t i = m + tid; i < P; i += kCandThreads) {
+      key[i] = 0;
+      oid[i] = INT64_MAX;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1) {
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = tid; i < P; i += kCandThreads) {
+          const uint32_t jx = i ^ stride;
+          if (jx > i) {
+            const bool up = (i & size) == 0;
+            const bool i_first = key[i] > key[jx] || (key[i] == key[jx] && oid[i] < oid[jx]);
+            if (up != i_first) {
+              const uint64_t tk = key[i];
+              key[i] = key[jx];
+              key[jx] = tk;
+              const int64_t to = oid[i];
+              oid[i] = oid[jx];
+              oid[jx] = to;
+              const double tv = val[i];
+              val[i] = val[jx];
+              val[jx] = tv;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (tid == 0) {  // sequential: drop adjacent duplicates, keep the first k
+      int32_t c = 0;
+      for (uint32_t i = 0; i < m && c < k; ++i) {
+        if (i > 0 && oid[i] == oid[i - 1] && key[i] == key[i - 1]) continue;
+        out_ids[r * k + c] = oid[i];
+        out_sc[r * k + c] = val[i];
+        ++c;
+      }
+      out_cnt[r] = c;
+    }
+    __syncthreads();
+  }
+}
+
+int top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* d_ids, const double* d_scores,
+                const int32_t* d_counts, int64_t* d_out_ids, double* d_out_scores, int32_t* d_out_counts) {
+  if ((int64_t)nparts * k > kCandCap) return set_error(CMS_E_PARAM, "nparts * k must be <= %d", kCandCap);
+  TimedScope ts(h, "topk_merge");
+  hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)std::min<int64_t>(h->n, 8192)), dim3(kCandThreads), 0, h->stream,
+                     nparts, k, h->n, d_ids, d_scores, d_counts, d_out_ids, d_out_scores, d_out_counts);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint32_t limit, int32_t k) {
   if (np <= 0) return CMS_OK;
   CMS_HIP(hipMemsetAsync(cb.list_n, 0, sizeof(uint32_t), h->stream));

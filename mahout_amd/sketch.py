@@ -201,6 +201,28 @@ class SketchTable:
         """cms_top_k_all in FileSimilarItemsWriter's CSV format."""
         check(self._lib.cms_write_similar_items(self._h, os.fsencode(path), int(k), int(as_float)))
 
+    def top_k_all_partial(self, k, shard, nshards):
+        n = self.num_owners
+        ids = np.zeros((n, k), np.int64)
+        sc = np.zeros((n, k), np.float64)
+        cnt = np.zeros(n, np.int32)
+        check(self._lib.cms_top_k_all_partial(self._h, int(k), int(shard), int(nshards), _ptr(ids), _ptr(sc),
+                                              _ptr(cnt)))
+        return ids, sc, cnt
+
+    def top_k_merge(self, k, parts):
+        """parts: list of (ids, scores, counts) partial lists."""
+        n = self.num_owners
+        ids = np.ascontiguousarray(np.stack([p[0] for p in parts]), np.int64)
+        sc = np.ascontiguousarray(np.stack([p[1] for p in parts]), np.float64)
+        cnt = np.ascontiguousarray(np.stack([p[2] for p in parts]), np.int32)
+        oi = np.zeros((n, k), np.int64)
+        os_ = np.zeros((n, k), np.float64)
+        oc = np.zeros(n, np.int32)
+        check(self._lib.cms_top_k_merge(self._h, int(k), len(parts), _ptr(ids), _ptr(sc), _ptr(cnt), _ptr(oi),
+                                        _ptr(os_), _ptr(oc)))
+        return oi, os_, oc
+
     def top_k_all(self, k):
         """mostSimilar lists of every owner, [num_owners][k] by owner row
         (symmetric streaming all-pairs pass)."""

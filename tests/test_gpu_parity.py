@@ -410,3 +410,25 @@ def test_write_similar_items_csv(oracle, tmp_path):
         for i in range(cnt[r]):
             exp.append(f"{ids_universe[r]},{ids[r, i]},{java_double_to_string(float(np.float32(sc[r, i])))}")
     assert lines == exp
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_top_k_all_shards_merge_exact(oracle, nshards):
+    """The multi-GPU decomposition on one GPU: every shard's partial lists
+    (pairs split by M rows, S x M chunks and waves), merged, equal the
+    single-shard result for every owner."""
+    n, d, w, k = 2500, 4, 256, 40
+    items, users = zipf_stream(4000, n, 400_000, seed=81)
+    vals = np.random.Generator(np.random.PCG64(81)).integers(1, 4, size=items.size).astype(np.float32)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        ids, sc, cnt = t.top_k_all(k)
+        parts = [t.top_k_all_partial(k, s, nshards) for s in range(nshards)]
+        # each pair in exactly one shard: partial counts never exceed the final lists' candidates
+        mi, ms, mc = t.top_k_merge(k, parts)
+        assert np.array_equal(mc, cnt)
+        for q in range(n):
+            assert mi[q, :mc[q]].tolist() == ids[q, :cnt[q]].tolist(), q
+            assert same(ms[q, :mc[q]], sc[q, :cnt[q]]), q
+        assert t.stats()["multi_limb_owners"] > 0
