@@ -154,31 +154,79 @@ def allpairs_measure(table, row_begin, row_count, k, n, d, w):
     }
 
 
-def cosine_1m(args, local, device):
-    """Config 4 on one GPU: mostSimilar top-100 for EVERY one of the 1M item
-    sketches (d=5, w=8192; the config-3 table built from a 500M-pair Zipf
-    stream) through cms_top_k_all -- each unordered pair computed once (int8
-    limb MFMA, exact fp64 epilogue) and streamed into both items' lists."""
-    from mahout_amd import SketchTable
+def config3_shard(n_items, n_users, total_pairs, rank, world, device, seed=20261016):
+    """This rank's share of the config-3 stream (the same global stream on
+    every rank, kept where cms_shard_of_key(user) == rank)."""
+    from mahout_amd.sketch import shard_of_keys
     from mahout_amd.synth import zipf_stream_torch
+    shard_tbl = None
+    if world > 1:
+        shard_tbl = torch.from_numpy(shard_of_keys(np.arange(n_users, dtype=np.int64), world)).to(device)
+    out_i, out_u = [], []
+    chunk, done, it = 1 << 26, 0, 0
+    while done < total_pairs:  # the same chunked global stream for every world size
+        m = min(chunk, total_pairs - done)
+        it_, us = zipf_stream_torch(n_users, n_items, m, seed=seed + 7919 * it, device=device)
+        if shard_tbl is not None:
+            keep = shard_tbl[us] == rank
+            it_, us = it_[keep], us[keep]
+        out_i.append(it_)
+        out_u.append(us)
+        done += m
+        it += 1
+    return torch.cat(out_i), torch.cat(out_u)
+
+
+def cosine_1m(args, local, device, rank=0, world=1):
+    """Configs 3 + 4: the 1M-item table (d=5, w=8192) from a 500M-pair Zipf
+    stream -- user-hash sharded over the ranks and merged by the RCCL
+    all-reduce in cms_finalize -- then mostSimilar top-100 for EVERY item
+    through cms_top_k_all: each unordered pair computed once (int8 limb MFMA,
+    exact fp64 epilogue) and streamed into both items' lists; with G ranks
+    the pairs are split G ways and the partial lists all-gathered and merged
+    (strong scaling: the job is fixed)."""
+    from mahout_amd import SketchTable, comm_unique_id
     n, d, w, npairs, k = 1_000_000, 5, 8192, 500_000_000, 100
     t = SketchTable(n, depth=d, width=w, seed=42, device=local)
-    items, users = zipf_stream_torch(10_000_000, n, npairs, seed=20261016, device=device)
-    torch.cuda.synchronize()
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        t.comm_init(uid[0], rank, world)
+    items, users = config3_shard(n, 10_000_000, npairs, rank, world, device)
+    local_pairs = int(items.numel())
+
+    def bar():
+        t.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        v = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        return float(v.item())
+
+    bar()
     t0 = time.perf_counter()
-    t.ingest_device_rows(items, users, None, npairs)
+    t.ingest_device_rows(items, users, None, local_pairs)
     t.finalize()
-    ingest_s = time.perf_counter() - t0
+    bar()
+    ingest_s = max_over_ranks(time.perf_counter() - t0)
     del items, users
     torch.cuda.empty_cache()
     t.release_scratch()
     t.set_timing(True)
-    t.top_k_rows(0, 128, k)  # limb operands prepared, kernels warm
+    t.top_k_rows(0, 128, k)  # limb operands prepared, kernels warm (local work)
     t.reset_timing()
+    bar()
     t0 = time.perf_counter()
     _, _, cnt = t.top_k_all(k)
-    wall = time.perf_counter() - t0
-    tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves"]}
+    bar()
+    wall = max_over_ranks(time.perf_counter() - t0)
+    tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves",
+                                               "topk_allgather", "topk_merge"]}
     waves_ms, waves_n = t.timing("topk_all_waves")
     t.set_timing(False)
     st = t.stats()
@@ -186,24 +234,26 @@ def cosine_1m(args, local, device):
     uniq = n * (n - 1) / 2
     alg_ops = uniq * 2 * d * w  # F = n(n-1)/2 * 2dw
     ns = n - nm
-    wave_ops = ns * (ns - 1) / 2 * 2 * d * w
+    wave_ops = ns * (ns - 1) / 2 * 2 * d * w / world  # this rank's share of the waves
     t.close()
     return {
-        "workload": f"config 4: top-{k} most similar items for every one of {n} items, d={d} w={w} "
-                    f"(table from a {npairs}-pair config-3 Zipf stream on 1 GPU)",
+        "workload": f"configs 3+4: {npairs}-pair Zipf stream -> {n}-item table (d={d} w={w}), user-hash sharded over "
+                    f"{world} GPU(s) + RCCL all-reduce; then top-{k} most similar items for every item",
+        "n_gpus": world, "scaling": "strong",
         "unique_item_pair_cosines_per_s": uniq / wall,
         "wall_s": wall,
         "algorithmic_TOPS": alg_ops / wall / 1e12,
-        "frac_int8_peak": alg_ops / wall / 1e12 / INT8_MFMA_PEAK_TOPS,
+        "frac_int8_peak_per_gpu": alg_ops / wall / 1e12 / INT8_MFMA_PEAK_TOPS / world,
         "roofline": {"bound": "mfma", "kernel": "k_cosine_big<3,1,128> (symmetric waves)",
                      "achieved": wave_ops / (waves_ms * 1e-3) / 1e12 if waves_ms else None,
                      "peak": INT8_MFMA_PEAK_TOPS, "unit": "TOP/s",
                      "frac": wave_ops / (waves_ms * 1e-3) / 1e12 / INT8_MFMA_PEAK_TOPS if waves_ms else None,
                      "avg_launch_ms": waves_ms / waves_n if waves_n else None,
                      "algorithmic_ops_per_launch": wave_ops / waves_n if waves_n else None},
-        "timing_ms": tm,
+        "timing_ms_rank0": tm,
         "multi_limb_owners": nm, "full_lists": int((cnt == k).sum()), "topk_redo_rows": int(st["topk_redo"]),
-        "config3_ingest_1gpu_s": ingest_s,
+        "config3_ingest_merge_s": ingest_s,
+        "config3_updates_per_s": npairs / ingest_s,
     }
 
 
@@ -314,9 +364,12 @@ def main():
     }
 
     off = ckeys = None
-    if rank == 0 and not (args.no_extras and args.no_cpu_baseline):
+    # extras run on a single GPU only: with a communicator, finalize and the
+    # all-pairs top-k are collectives every rank must join
+    extras_on = rank == 0 and world == 1 and not args.no_extras
+    if rank == 0 and (extras_on or not args.no_cpu_baseline):
         off, ckeys = csr_on_device(items, users, n)
-    if rank == 0 and not args.no_extras:
+    if extras_on:
         extras = {}
         # CSR (DataModel layout) ingest of the same stream: no partition pass
         table.reset()
@@ -345,15 +398,22 @@ def main():
         result["extras"] = extras
     if rank == 0 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(off, ckeys, args)
-    if rank == 0 and not args.no_cosine_1m:
-        del off, ckeys
-        table.close()
-        del items, users
-        torch.cuda.empty_cache()
-        result["cosine"] = cosine_1m(args, local, device)
+    del off, ckeys
+    table.close()
+    del items, users
+    torch.cuda.empty_cache()
+    if world > 1:
+        dist.barrier()
+    if not args.no_cosine_1m:
+        try:
+            cos = cosine_1m(args, local, device, rank, world)
+            if rank == 0:
+                result["cosine"] = cos
+        except Exception as e:  # the headline line must still be printed
+            if rank == 0:
+                result["cosine"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0:
         print(json.dumps(result))
-    table.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -56,3 +56,23 @@ def test_user_hash_sharding_allreduce_is_exact(world):
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res)
     assert sum(n for _, _, n in res) == 40000
+
+
+def test_bench_config3_shards_partition_the_global_stream():
+    """bench.config3_shard: for any world size the ranks' shards partition the
+    same global stream, each pair on the rank its user hashes to."""
+    import sys as _sys
+    import os as _os
+    _sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))))
+    import bench
+    from mahout_amd.sketch import shard_of_keys
+    n_items, n_users, total = 1000, 5000, 200_000
+    gi, gu = bench.config3_shard(n_items, n_users, total, 0, 1, "cpu", seed=5)
+    glob = np.sort(gi.numpy() * n_users + gu.numpy())
+    for world in (2, 3):
+        parts = []
+        for r in range(world):
+            i, u = bench.config3_shard(n_items, n_users, total, r, world, "cpu", seed=5)
+            assert np.all(shard_of_keys(u.numpy(), world) == r)
+            parts.append(i.numpy() * n_users + u.numpy())
+        assert np.array_equal(np.sort(np.concatenate(parts)), glob)
