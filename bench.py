@@ -386,6 +386,21 @@ def main():
         dt = time.perf_counter() - t0
         extras["csr_updates_per_s"] = npairs * args.steps / dt
         extras["csr_ms_per_step"] = dt * 1e3 / args.steps
+        # the same stream handed over in HOST memory (cms_ingest: PCIe copy +
+        # validation + the device path), i.e. the JNI boundary's rate
+        h_items = items.cpu().numpy()
+        h_users = users.cpu().numpy()
+        table.reset()
+        table.ingest(h_items, h_users)
+        table.finalize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            table.reset()
+            table.ingest(h_items, h_users)
+            table.finalize()
+        dt = time.perf_counter() - t0
+        extras["host_buffers_updates_per_s"] = npairs * 3 / dt
+        del h_items, h_users
         # all-pairs top-100 over the config-2 table (int8-limb MFMA + exact fp64 epilogue)
         extras["allpairs_top100_cfg2"] = allpairs_measure(table, 0, n, 100, n, d, w)
         # the same lists through the symmetric streaming pass (each unordered pair once)

@@ -446,6 +446,7 @@ struct BigArgs {
   int32_t cap, append_a, append_b;
   // ---- symmetric wave: unordered 256-row block pairs {I, (I + wave) % nb} ----
   int32_t sym, wave, nb;  // sym: block I = positions [s0 + 256 I, ...) of the s_rows region
+  int32_t band;           // sym: waves [wave, wave + band) in one launch
   int64_t s0, s_rows;
 };
 
@@ -472,9 +473,14 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   int64_t vrow0, own0, bcol0;
   bool diag = false;  // symmetric diagonal block: only pairs a < b
   if (g.sym) {
-    // consecutive workgroups = the two 128-column halves of one block pair
-    const int I = lin >> 1, half = lin & 1;
-    const int J = (I + g.wave) % g.nb;
+    // A band of waves: block I meets J = I + wave + t (t < band), both
+    // 128-column halves.  Consecutive workgroups share I (its panel stays in
+    // the XCD's L2 for 2*band workgroups) and neighbouring I share most J.
+    const int per = 2 * g.band;
+    const int I = lin / per, rem = lin - I * per, t = rem >> 1, half = rem & 1;
+    const int wv = g.wave + t;
+    if ((g.nb & 1) == 0 && 2 * wv == g.nb && 2 * I >= g.nb) return;  // {I, I + nb/2} once
+    const int J = (I + wv) % g.nb;
     diag = I == J;
     a_pos0 = g.s0 + (int64_t)I * kTA;
     a_owners = a_vrows = min<int64_t>(kTA, g.s_rows - (int64_t)I * kTA);
@@ -836,7 +842,7 @@ static BigCfg big_config(cms_handle* h) {
 static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t sym_pairs = 0) {
   if (g.sym) {
     g.tilesB = 2;
-    g.nblk = (int)(2 * sym_pairs);
+    g.nblk = (int)(2 * g.band * sym_pairs);
   } else {
     const int oa = kTA / ls;
     const int64_t tilesA = (g.a_owners + oa - 1) / oa;
@@ -1108,20 +1114,34 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   // 3. S x S symmetric waves
   if (ns > 0) {
     const int64_t nb = (ns + kTA - 1) / kTA;
-    for (int64_t wv = shard; wv <= nb / 2; wv += nshards) {
-      int64_t pairs = nb;
-      if (wv > 0 && 2 * wv == nb) pairs = nb / 2;  // {I, I + nb/2}: each pair once
-      if ((rc = cand_compact(h, cb, nm, ns, (uint32_t)cap - kPerPass, k))) return rc;
+    // Bands of waves per launch.  A row takes up to 512 offers per wave, but
+    // once its list has seen m columns its threshold admits about k*512/m of
+    // them; bands grow with the wave index so a launch brings ~25 expected
+    // offers per row (lists are compacted to cap/2 before each band; an
+    // overflow would flag the row for an exact recompute).  Each band reads
+    // its panels from HBM once and reuses them 2*band times from L2.
+    std::vector<std::pair<int64_t, int64_t>> bands;  // (first wave, waves)
+    for (int64_t wv = 0; wv <= nb / 2;) {
+      int64_t L = wv < 8 ? 1 : std::max<int64_t>(1, std::min<int64_t>(32, wv * 25 / std::max(1, k)));
+      L = std::min<int64_t>(L, nb / 2 - wv + 1);
+      bands.push_back({wv, L});
+      wv += L;
+    }
+    for (size_t bi = shard; bi < bands.size(); bi += nshards) {
+      const int64_t wv = bands[bi].first, L = bands[bi].second;
+      const uint32_t limit = L == 1 ? (uint32_t)cap - kPerPass : (uint32_t)cap / 2;
+      if ((rc = cand_compact(h, cb, nm, ns, limit, k))) return rc;
       BigArgs g = base;
       g.A = g.B = limb0;
       g.sym = 1;
       g.wave = (int32_t)wv;
+      g.band = (int32_t)L;
       g.nb = (int32_t)nb;
       g.s0 = nm;
       g.s_rows = ns;
       g.append_a = g.append_b = 1;
       TimedScope ts(h, "topk_all_waves");
-      if ((rc = launch_big(h, cfg, g, 1, pairs))) return rc;
+      if ((rc = launch_big(h, cfg, g, 1, nb))) return rc;
     }
     // 4. final lists -> outputs
     if ((rc = cand_compact(h, cb, nm, ns, 0, k))) return rc;

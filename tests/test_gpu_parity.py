@@ -340,6 +340,7 @@ def test_top_k_heavy_ties(oracle):
     (2000, 4, 128, 50, 100, False, 52),   # most owners multi-limb: several S x M passes
     (1800, 3, 256, 1, 64, True, 53),      # weighted: every score is +-1, ties by ID everywhere
     (700, 5, 512, 2, 5, False, 54),       # fewer than one 256-row block pair per wave
+    (11776, 3, 128, 2, 20, False, 55),    # 46 blocks: multi-wave bands and the half wave
 ])
 def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed):
     """cms_top_k_all (each unordered pair computed once, streamed into both
