@@ -1121,8 +1121,11 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // overflow would flag the row for an exact recompute).  Each band reads
     // its panels from HBM once and reuses them 2*band times from L2.
     std::vector<std::pair<int64_t, int64_t>> bands;  // (first wave, waves)
+    // Weighted similarities are all +-1: thresholds never tighten, so every
+    // later candidate is admitted and only single waves are safe.
+    const bool weighted = h->p.weighting == CMS_WEIGHTED;
     for (int64_t wv = 0; wv <= nb / 2;) {
-      int64_t L = wv < 8 ? 1 : std::max<int64_t>(1, std::min<int64_t>(32, wv * 25 / std::max(1, k)));
+      int64_t L = (wv < 8 || weighted) ? 1 : std::max<int64_t>(1, std::min<int64_t>(32, wv * 25 / std::max(1, k)));
       L = std::min<int64_t>(L, nb / 2 - wv + 1);
       bands.push_back({wv, L});
       wv += L;
