@@ -1033,7 +1033,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
               int32_t nshards) {
   int rc = cosine_prepare(h);
   if (rc) return rc;
-  const int64_t n = h->n, dw = h->dw;
+  const int64_t n = h->n;
   const BigCfg cfg = big_config(h);
   const int64_t nm = h->n_hot_limb, ns = n - nm;
   if (!cfg.nstage || (nm > 0 && !h->vl_slots) || h->n_inexact_rows != 0 || k > kCandCap / 2) {
@@ -1075,16 +1075,6 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
                              hipMemcpyHostToDevice, h->stream));
     CMS_HIP(hipStreamSynchronize(h->stream));
   }
-  // 1. multi-limb rows: exact slab top-k
-  if (nm > 0) {
-    TimedScope ts(h, "topk_all_multi_rows");
-    std::vector<int64_t> pos, outp;
-    for (int64_t p = shard; p < nm; p += nshards) {
-      pos.push_back(p);
-      outp.push_back(h->h_perm[p]);
-    }
-    if ((rc = slab_top_k_positions(h, pos, outp, k, d_ids, d_scores, d_counts))) return rc;
-  }
   BigArgs base = big_base(h);
   base.thr = cb.thr;
   base.ccnt = cb.ccnt;
@@ -1092,23 +1082,14 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   base.cval = cb.cval;
   base.cap = cap;
   const int8_t* limb0 = h->ws_limb0.as<int8_t>();
-  // 2. S rows x M candidates, kPerPass multi-limb owners per pass
-  if (nm > 0 && ns > 0) {
-    const int ls = h->vl_slots, per = 32 / ls;
-    const int8_t* vl = h->ws_vl.as<int8_t>();
+  // 1 + 2. multi-limb rows, kPerPass per chunk: one slab each (M x S as
+  // virtual limb rows, M x M on the MULTI tiles) gives their exact top-k AND
+  // the M candidates of every single-limb row -- each (M, S) pair once
+  if (nm > 0) {
+    TimedScope ts(h, "topk_all_multi_rows");
     for (int64_t m0 = (int64_t)shard * kPerPass; m0 < nm; m0 += (int64_t)nshards * kPerPass) {
-      if ((rc = cand_compact(h, cb, nm, ns, (uint32_t)cap - kPerPass, k))) return rc;
-      BigArgs g = base;
-      g.A = vl + (m0 / per) * 32 * dw;
-      g.a_vrows = h->vl_rows - (m0 / per) * 32;
-      g.a_pos0 = m0;
-      g.a_owners = std::min<int64_t>(kPerPass, nm - m0);
-      g.B = limb0 + nm * dw;
-      g.b_pos0 = nm;
-      g.b_rows = ns;
-      g.append_b = 1;
-      TimedScope ts(h, "topk_all_limbs");
-      if ((rc = launch_big(h, cfg, g, ls))) return rc;
+      const int64_t qc = std::min<int64_t>(kPerPass, nm - m0);
+      if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts))) return rc;
     }
   }
   // 3. S x S symmetric waves
@@ -1124,8 +1105,10 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // Weighted similarities are all +-1: thresholds never tighten, so every
     // later candidate is admitted and only single waves are safe.
     const bool weighted = h->p.weighting == CMS_WEIGHTED;
+    int64_t ramp = 25, lmax = 32;
+    if (const char* e = getenv("CMS_BAND")) sscanf(e, "%ld,%ld", &ramp, &lmax);  // EXPERIMENT
     for (int64_t wv = 0; wv <= nb / 2;) {
-      int64_t L = (wv < 8 || weighted) ? 1 : std::max<int64_t>(1, std::min<int64_t>(32, wv * 25 / std::max(1, k)));
+      int64_t L = (wv < 8 || weighted) ? 1 : std::max<int64_t>(1, std::min<int64_t>(lmax, wv * ramp / std::max(1, k)));
       L = std::min<int64_t>(L, nb / 2 - wv + 1);
       bands.push_back({wv, L});
       wv += L;

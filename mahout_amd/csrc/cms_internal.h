@@ -163,6 +163,10 @@ struct CandBufs {
 int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint32_t limit, int32_t k);
 int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t k, int64_t* d_ids, double* d_scores,
               int32_t* d_counts);
+// slab of positions [m0, m0+qc) against everyone: exact top-k of those rows,
+// and their similarities offered to the lists of columns [c0, c1)
+int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t qc, int64_t c0, int64_t c1, int32_t k,
+                          int64_t* d_ids, double* d_scores, int32_t* d_counts);
 int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts, int32_t shard = 0,
               int32_t nshards = 1);
 // merge nparts partial top-k lists ([nparts][n][k] ids by owner ID, scores; [nparts][n] counts)

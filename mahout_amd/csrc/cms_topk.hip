@@ -616,6 +616,49 @@ int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t
   return CMS_OK;
 }
 
+// Offer the similarities of slab rows (positions [m0, m0+qc)) to the lists
+// of the columns [c0, c1): one thread per column walks the slab rows in order
+// (no contention: a list has one writer here).
+__global__ void k_slab_offer(const double* slab, int64_t ld, int64_t m0, int64_t qc, int64_t c0, int64_t c1,
+                             const double* thr, uint32_t* ccnt, uint32_t* cidx, double* cval, int32_t cap) {
+  for (int64_t c = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < c1; c += (int64_t)gridDim.x * blockDim.x) {
+    const double t = thr[c];
+    uint32_t cnt = ccnt[c];
+    for (int64_t m = 0; m < qc; ++m) {
+      const double v = slab[m * ld + c];
+      if (v != v || v < t || m0 + m == c) continue;
+      if (cnt < (uint32_t)cap) {
+        cidx[c * cap + cnt] = (uint32_t)(m0 + m);
+        cval[c * cap + cnt] = v;
+      }
+      ++cnt;
+    }
+    ccnt[c] = cnt;
+  }
+}
+
+int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t qc, int64_t c0, int64_t c1, int32_t k,
+                          int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  const int64_t n = h->n;
+  int rc;
+  CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(qc * n)));
+  double* slab = h->ws_slab.as<double>();
+  if ((rc = cosine_slab(h, m0, qc, slab))) return rc;
+  // exact top-k of the slab rows
+  std::vector<TopQuery> qs;
+  for (int64_t p = m0; p < m0 + qc; ++p) qs.push_back(TopQuery{p - m0, p, h->h_perm[p]});
+  if ((rc = launch_top_k(h, slab, qs, k, cosine_perm_device(h), d_ids, d_scores, d_counts))) return rc;
+  // and the same similarities for the columns' lists
+  if (c1 > c0) {
+    if ((rc = cand_compact(h, cb, c0, c1 - c0, (uint32_t)(cb.cap - qc), k))) return rc;
+    const unsigned g1 = (unsigned)std::min<int64_t>((c1 - c0 + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_slab_offer, dim3(g1), dim3(256), 0, h->stream, slab, n, m0, qc, c0, c1, cb.thr, cb.ccnt,
+                       cb.cidx, cb.cval, cb.cap);
+    CMS_HIP(hipGetLastError());
+  }
+  return CMS_OK;
+}
+
 // slab budget: 2^30 fp64 similarities (8 GiB) -- 1,024 query rows at 1M owners
 static int64_t slab_rows_for(int64_t n) {
   return std::max<int64_t>(128, ((int64_t(1) << 30) / std::max<int64_t>(1, n)) / 128 * 128);
