@@ -13,12 +13,17 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
 
 
 def build(verbose=False, force=False):
+    """CMS_BOUND_ANALYSIS=1 in the environment builds the bound-analysis
+    variant (kernel parts switchable by CMS_COS_MODE; scripts/cos_modes.sh)."""
+    analysis = os.environ.get("CMS_BOUND_ANALYSIS") == "1"
+    force = force or analysis
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
     deps.append(os.path.join(HERE, "..", "include", "mahout_cms.h"))
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + srcs + ["-o", OUT, "-L/opt/rocm/lib", "-lrccl",
+    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + (["-DCMS_BOUND_ANALYSIS"] if analysis else []) + srcs + ["-o", OUT,
+                                                                                            "-L/opt/rocm/lib", "-lrccl",
                                                    "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))

@@ -434,7 +434,7 @@ struct BigArgs {
   int32_t w, depth;
   int32_t weighted, trans;
   int32_t tilesB, nblk;
-  int32_t mode;  // EXPERIMENT: bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
+  int32_t mode;  // CMS_BOUND_ANALYSIS builds only: bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
   // ---- candidate (streaming top-k) mode: cval != nullptr ----
   // Instead of the slab, every similarity v of a pair (a, b) is offered to
   // row a's candidate list when append_a and v >= thr[a], and to row b's when
@@ -505,13 +505,13 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   const int wr = wid >> 1, wc = wid & 1;
   const int w = g.w;
   const int cstages = w / BK;
+#ifdef CMS_BOUND_ANALYSIS
+  const int kMode = g.mode;  // bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
+#else
+  constexpr int kMode = 0;
+#endif
   const int total = depth * cstages;
 
-  if (g.mode & 32) return;  // EXPERIMENT: launch cost only
-  if (g.mode & 64) {        // EXPERIMENT: skeleton loop only
-    for (int s = 0; s < total; ++s) __builtin_amdgcn_s_barrier();
-    return;
-  }
   // sqrt norms of the panel's owners, straight into LDS by LDS-DMA (256 B
   // per instruction, past-the-end owners land as zeros).  Issued before the
   // first stages, so the stage-0 vmcnt wait covers them, and the first
@@ -527,10 +527,6 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
         __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * 8), 0x00020000);
     double* dst = isA ? s_sa + r * kTA + part * 32 : s_sb + r * kTB + (part - 8) * 32;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
-  }
-  if (g.mode & 128) {  // EXPERIMENT: norms only
-    wait_vmcnt<0>();
-    return;
   }
 
   // buffer descriptors bound the panel: rows past the end land as zeros
@@ -552,7 +548,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
                      ((BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4);
   const int32_t rstep = 8 * RPI * (int32_t)g.dw;
   auto issue = [&](int s) {
-    if (g.mode & 1) return;
+    if (kMode & 1) return;
     const int r = s / cstages, cs = s - r * cstages;
     const int32_t koff = r * w + cs * BK;
     unsigned char* st = lds + (s % NSTAGE) * kStage;
@@ -589,14 +585,14 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     if (s + NSTAGE - 2 < total) wait_vmcnt<OPS * (NSTAGE - 2)>();
     else wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(g.mode & 8)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);  // refill the slot read in iteration s-1
     const unsigned char* A = lds + (s % NSTAGE) * kStage;
     const unsigned char* B = A + kStageA;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      if (g.mode & 2) break;
+      if (kMode & 2) break;
       const int ch = 2 * ks + (lane >> 5);
       i8x16 fa[2], fb[2];
 #pragma unroll
@@ -611,7 +607,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
     const int r = s / cstages;
-    if (s - r * cstages == cstages - 1 && !(g.mode & 4)) {
+    if (s - r * cstages == cstages - 1 && !(kMode & 4)) {
       // ---- fp64 epilogue of sketch row r (DoubleCountMinSketch.java:143-147) ----
       // Branch-free: every term is AB / (sqrtA * sqrtB) with AB >= 0 and a
       // finite den, so no NaN or -0.0 reaches Math.min and it is a plain
@@ -653,7 +649,6 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     }
   }
 
-  if (g.mode & 16) return;  // EXPERIMENT
   // ---- NaN when no row qualified, then normalizeWeightResult; slab or lists ----
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -816,7 +811,9 @@ static BigCfg big_config(cms_handle* h) {
   // 128-B K slices (one cache line per row) in a 3- or 2-deep ring; 64-B
   // slices in a 6-deep ring measured slower (twice the line requests per
   // byte, twice the barriers)
-  if (const char* e = getenv("CMS_COS_BK")) c.bk = atoi(e) == 64 ? 64 : 128;  // EXPERIMENT
+#ifdef CMS_BOUND_ANALYSIS
+  if (const char* e = getenv("CMS_COS_BK")) c.bk = atoi(e) == 64 ? 64 : 128;
+#endif
   if (c.bk == 64) {
     c.nstage = 6 * 384 * 64 + c.norms <= kLdsMax ? 6 : 4 * 384 * 64 + c.norms <= kLdsMax ? 4 : 0;
     if (!c.nstage) c.bk = 128;
@@ -874,7 +871,9 @@ static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t
 
 static BigArgs big_base(cms_handle* h) {
   BigArgs b{};
-  if (const char* m = getenv("CMS_COS_MODE")) b.mode = atoi(m);  // EXPERIMENT
+#ifdef CMS_BOUND_ANALYSIS
+  if (const char* m = getenv("CMS_COS_MODE")) b.mode = atoi(m);
+#endif
   b.perm = h->ws_limbmeta.as<int64_t>();
   b.nsq_t = h->ws_nsq.as<double>();
   b.n = h->n;
@@ -1106,7 +1105,9 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // later candidate is admitted and only single waves are safe.
     const bool weighted = h->p.weighting == CMS_WEIGHTED;
     int64_t ramp = 25, lmax = 32;
-    if (const char* e = getenv("CMS_BAND")) sscanf(e, "%ld,%ld", &ramp, &lmax);  // EXPERIMENT
+#ifdef CMS_BOUND_ANALYSIS
+    if (const char* e = getenv("CMS_BAND")) sscanf(e, "%ld,%ld", &ramp, &lmax);
+#endif
     for (int64_t wv = 0; wv <= nb / 2;) {
       int64_t L = (wv < 8 || weighted) ? 1 : std::max<int64_t>(1, std::min<int64_t>(lmax, wv * ramp / std::max(1, k)));
       L = std::min<int64_t>(L, nb / 2 - wv + 1);
