@@ -63,6 +63,7 @@ class CmsStats(ctypes.Structure):
         ("table_bytes", ctypes.c_int64),
         ("multi_limb_owners", ctypes.c_int64),
         ("topk_redo", ctypes.c_int64),
+        ("deep_limb_owners", ctypes.c_int64),
     ]
 
 

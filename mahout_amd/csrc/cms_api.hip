@@ -245,7 +245,7 @@ void cms_destroy(cms_handle* h) {
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
-                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->ws_vl, &h->ws_nsq, &h->ws_cand};
+                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -730,6 +730,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->table_bytes = (int64_t)sizeof(uint32_t) * h->n * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
+  out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;
   return CMS_OK;
 }
 

@@ -42,9 +42,10 @@ constexpr int kMaxLimbs = 5;    // 35 bits >= any u32 counter
 // ------------------------------------------------------------ preparation --
 
 // Per owner row: limb count (from the largest counter, which the norm
-// passes record), multi-limb flag, inexact-norm count.
+// passes record), multi-limb flags (L > 1, L > 2), inexact-norm count and
+// the count of owners needing all 5 limbs.
 __global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int64_t nrows, const uint64_t* norm,
-                                                    int depth, uint8_t* rowL, uint32_t* multi_flag,
+                                                    int depth, uint8_t* rowL, uint32_t* multi_flag, uint32_t* deep_flag,
                                                     uint32_t* inexact_rows) {
   const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (row >= nrows) return;
@@ -53,16 +54,22 @@ __global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int6
   while (L < kMaxLimbs && (mx >> (7 * L)) != 0) ++L;
   rowL[row] = (uint8_t)L;
   multi_flag[row] = L > 1 ? 1u : 0u;
+  deep_flag[row] = L > 2 ? 1u : 0u;
+  if (L == kMaxLimbs) atomicAdd(inexact_rows + 1, 1u);
   bool inexact = false;
   for (int d = 0; d < depth; ++d) inexact |= norm[row * depth + d] >= (1ULL << 53);
   if (inexact) atomicAdd(inexact_rows, 1u);
 }
 
-// Stable multi-first permutation from the exclusive scan of the multi flags.
-__global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, const uint8_t* rowL, int64_t nrows,
+// Stable permutation: owners with 3+ limbs, then 2 limbs, then single-limb,
+// each class in row order (exclusive scans of the class flags).
+__global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, const uint32_t* dpos,
+                            const uint32_t* deep_flag, const uint8_t* rowL, int64_t nrows, int64_t n_deep,
                             int64_t n_multi, int64_t* perm, int64_t* inv, uint8_t* rowLp) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p = multi_flag[r] ? (int64_t)mpos[r] : n_multi + (r - (int64_t)mpos[r]);
+    const int64_t p = deep_flag[r]    ? (int64_t)dpos[r]
+                      : multi_flag[r] ? n_deep + ((int64_t)mpos[r] - (int64_t)dpos[r])
+                                      : n_multi + (r - (int64_t)mpos[r]);
     perm[p] = r;
     inv[r] = p;
     rowLp[p] = rowL[r];
@@ -696,16 +703,16 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     }
 }
 
-// Virtual limb rows of the multi-limb owners (positions [0, n_multi)) for
-// the LS-slot layout above; missing limbs and the tail are zero rows.
+// Virtual limb rows of the multi-limb owners at positions [o0, o1) for the
+// LS-slot layout above; missing limbs and the tail are zero rows.
 __global__ __launch_bounds__(256) void k_vl_build(const int8_t* limb0, const int8_t* hl, const uint8_t* rowLp,
-                                                  int64_t n_multi, int64_t dw, int LS, int8_t* vl) {
+                                                  int64_t o0, int64_t o1, int64_t dw, int LS, int8_t* vl) {
   const int64_t v = blockIdx.x;
   const int rr = (int)(v & 31), grp = rr >> 3;
   const int limb = grp % LS;
-  const int64_t o = (v >> 5) * (32 / LS) + (grp / LS) * 8 + (rr & 7);
+  const int64_t o = o0 + (v >> 5) * (32 / LS) + (grp / LS) * 8 + (rr & 7);
   const int8_t* src = nullptr;
-  if (o < n_multi) {
+  if (o < o1) {
     if (limb == 0) src = limb0 + o * dw;
     else if (limb < rowLp[o]) src = hl + (o * (kMaxLimbs - 1) + (limb - 1)) * dw;
   }
@@ -722,8 +729,9 @@ int cosine_prepare(cms_handle* h) {
   const int64_t ntiles = (n + kTile - 1) / kTile;
   CMS_HIP(h->ws_limb0.ensure((size_t)n * (size_t)dw));
   // meta: perm[n] i64 | inv[n] i64 | multi_flag[n] u32 | mpos[n] u32 | bsum | rowL[n] | rowLp[n] | tileL[ntiles]
+  //       | deep_flag[n] u32 | dpos[n] u32
   const int64_t nbs = (n + 4095) / 4096 + 1;
-  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (8 + 8 + 4 + 4 + 1 + 1) + 4 * (size_t)nbs + (size_t)ntiles + 64));
+  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (8 + 8 + 4 + 4 + 1 + 1 + 4 + 4) + 4 * (size_t)nbs + (size_t)ntiles + 64));
   int64_t* perm = h->ws_limbmeta.as<int64_t>();
   int64_t* inv = perm + n;
   uint32_t* mflag = reinterpret_cast<uint32_t*>(inv + n);
@@ -732,30 +740,38 @@ int cosine_prepare(cms_handle* h) {
   uint8_t* rowL = reinterpret_cast<uint8_t*>(bsum + nbs);
   uint8_t* rowLp = rowL + n;
   uint8_t* tileL = rowLp + n;
-  uint32_t* cnt = h->d_flags + 8;  // [8] inexact owners
-  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
-  uint32_t host[3];
+  uint32_t* dflag = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(tileL + ntiles) + 15) & ~uintptr_t(15));
+  uint32_t* dpos = dflag + n;
+  uint32_t* cnt = h->d_flags + 8;  // [8] inexact owners, [9] 5-limb owners
+  CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
+  uint32_t host[6];
   {
     TimedScope ts(h, "limb_prep");
     hipLaunchKernelGGL(k_limb_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->d_rowmax, n,
-                       h->d_norm, h->p.depth, rowL, mflag, cnt);
+                       h->d_norm, h->p.depth, rowL, mflag, dflag, cnt);
     int rc = scan_exclusive_u32(h, mflag, mpos, n, bsum);
     if (rc) return rc;
-    CMS_HIP(hipGetLastError());
     CMS_HIP(hipMemcpyAsync(&host[0], mpos + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
     CMS_HIP(hipMemcpyAsync(&host[1], mflag + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
-    CMS_HIP(hipMemcpyAsync(&host[2], cnt, 4, hipMemcpyDeviceToHost, h->stream));
+    rc = scan_exclusive_u32(h, dflag, dpos, n, bsum);
+    if (rc) return rc;
+    CMS_HIP(hipGetLastError());
+    CMS_HIP(hipMemcpyAsync(&host[2], cnt, 8, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[4], dpos + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[5], dflag + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
     CMS_HIP(hipStreamSynchronize(h->stream));
   }
   const int64_t n_multi = (int64_t)host[0] + host[1];
+  const int64_t n_deep = (int64_t)host[4] + host[5];
   h->n_hot_limb = (uint32_t)n_multi;
   h->n_inexact_rows = host[2];
+  const uint32_t n_five = host[3];
   CMS_HIP(h->ws_limbhot.ensure((size_t)std::max<int64_t>(1, n_multi) * (kMaxLimbs - 1) * (size_t)dw));
   {
     TimedScope ts(h, "limb_prep");
     unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, rowL, n, n_multi, perm, inv,
-                       rowLp);
+    hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, rowL, n, n_deep,
+                       n_multi, perm, inv, rowLp);
     hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, dw, perm, rowLp, n_multi,
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
@@ -772,18 +788,23 @@ int cosine_prepare(cms_handle* h) {
   CMS_HIP(hipMemcpyAsync(h->h_perm.data(), perm, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipMemcpyAsync(h->h_inv.data(), inv, sizeof(int64_t) * n, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
-  // virtual limb rows for the multi-limb x single-limb blocks (k_cosine_big<., LS>)
-  int maxL = 1;
-  for (int64_t t = 0; t * kTile < n_multi; ++t) maxL = std::max<int>(maxL, h->tile_limbs[t]);
-  h->vl_slots = n_multi == 0 ? 0 : maxL <= 2 ? 2 : maxL <= 4 ? 4 : 0;
-  h->vl_rows = 0;
-  if (h->vl_slots) {
-    const int per = 32 / h->vl_slots;  // owners per 32-row block
-    h->vl_rows = (n_multi + per - 1) / per * 32;
-    CMS_HIP(h->ws_vl.ensure((size_t)h->vl_rows * (size_t)dw));
+  // virtual limb rows for the multi-limb x single-limb blocks (k_cosine_big<., LS>):
+  // 4 slots for the 3-4-limb owners, 2 slots for the 2-limb ones
+  h->vl_ok = n_five == 0;
+  const int64_t bounds[3] = {0, n_deep, n_multi};
+  const int32_t slots[2] = {4, 2};
+  for (int gi = 0; gi < 2; ++gi) {
+    auto& G = h->vl[gi];
+    G.o0 = bounds[gi];
+    G.o1 = bounds[gi + 1];
+    G.ls = slots[gi];
+    const int per = 32 / G.ls;  // owners per 32-row block
+    G.rows = (G.o1 - G.o0 + per - 1) / per * 32;
+    if (!h->vl_ok || G.rows == 0) continue;
+    CMS_HIP(G.buf.ensure((size_t)G.rows * (size_t)dw));
     TimedScope ts(h, "limb_prep");
-    hipLaunchKernelGGL(k_vl_build, dim3((unsigned)h->vl_rows), dim3(256), 0, h->stream, h->ws_limb0.as<int8_t>(),
-                       h->ws_limbhot.as<int8_t>(), rowLp, n_multi, dw, h->vl_slots, h->ws_vl.as<int8_t>());
+    hipLaunchKernelGGL(k_vl_build, dim3((unsigned)G.rows), dim3(256), 0, h->stream, h->ws_limb0.as<int8_t>(),
+                       h->ws_limbhot.as<int8_t>(), rowLp, G.o0, G.o1, dw, G.ls, G.buf.as<int8_t>());
     CMS_HIP(hipGetLastError());
   }
   h->mfma_ready = true;
@@ -915,7 +936,7 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   const size_t lds = 4 * kTile * kBK + 2 * kTile * sizeof(double);  // 2 buffers x (A + B) + norms
   const int64_t qend = q0 + qc;
 
-  if (cfg.nstage && (nm == 0 || h->vl_slots)) {
+  if (cfg.nstage && (nm == 0 || h->vl_ok)) {
     // Four blocks of the slab in permuted coordinates (M = multi-limb owners
     // [0, nm), S = the rest):  S x S and M x S / S x M on k_cosine_big,
     // M x M on the int64-folding MULTI tile kernel.
@@ -936,17 +957,20 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
       TimedScope ts(h, "cosine_mfma");
       if ((rc = launch(g, 1))) return rc;
     }
-    if (nm > 0) {
-      const int ls = h->vl_slots, per = 32 / ls;
-      const int8_t* vl = h->ws_vl.as<int8_t>();
+    for (int gi = 0; gi < 2 && nm > 0; ++gi) {
+      const auto& G = h->vl[gi];
+      if (G.o1 <= G.o0) continue;
+      const int ls = G.ls, per = 32 / ls;
+      const int8_t* vl = G.buf.as<int8_t>();
       TimedScope ts(h, "cosine_mfma_limbs");
-      if (q0 < nm && nm < n) {  // M x S: multi-limb queries against single-limb candidates
-        const int64_t oa0 = q0 / per * per;
+      if (q0 < G.o1 && qend > G.o0 && nm < n) {  // M x S: multi-limb queries against single-limb candidates
+        const int64_t oa0 = G.o0 + (std::max(q0, G.o0) - G.o0) / per * per;
+        const int64_t blk = (oa0 - G.o0) / per;
         BigArgs g = base;
-        g.A = vl + (oa0 / per) * 32 * dw;
-        g.a_vrows = h->vl_rows - (oa0 / per) * 32;
+        g.A = vl + blk * 32 * dw;
+        g.a_vrows = G.rows - blk * 32;
         g.a_pos0 = oa0;
-        g.a_owners = std::min(qend, nm) - oa0;
+        g.a_owners = std::min(qend, G.o1) - oa0;
         g.B = a.limb0 + nm * dw;
         g.b_pos0 = nm;
         g.b_rows = n - nm;
@@ -955,9 +979,9 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
       if (slo < qend) {  // S x M, computed as M x S and written transposed
         BigArgs g = base;
         g.A = vl;
-        g.a_vrows = h->vl_rows;
-        g.a_pos0 = 0;
-        g.a_owners = nm;
+        g.a_vrows = G.rows;
+        g.a_pos0 = G.o0;
+        g.a_owners = G.o1 - G.o0;
         g.B = a.limb0 + slo * dw;
         g.b_pos0 = slo;
         g.b_rows = qend - slo;
@@ -1035,7 +1059,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   const int64_t n = h->n;
   const BigCfg cfg = big_config(h);
   const int64_t nm = h->n_hot_limb, ns = n - nm;
-  if (!cfg.nstage || (nm > 0 && !h->vl_slots) || h->n_inexact_rows != 0 || k > kCandCap / 2) {
+  if (!cfg.nstage || (nm > 0 && !h->vl_ok) || h->n_inexact_rows != 0 || k > kCandCap / 2) {
     if (nshards == 1) return top_k_rows(h, 0, n, k, d_ids, d_scores, d_counts);  // per-row slab path
     // per-row slab path for this shard's rows only; the other rows stay empty
     CMS_HIP(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * n, h->stream));

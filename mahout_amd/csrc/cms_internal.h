@@ -76,8 +76,15 @@ struct cms_handle {
   uint32_t n_hot_limb = 0;      // owners with counters >= 128 (multi-limb)
   uint32_t n_inexact_rows = 0;  // owners with a norm >= 2^53
   std::vector<uint8_t> tile_limbs;   // per permuted 128-row tile: max limb count
-  int32_t vl_slots = 0;         // limb slots per multi-limb owner in ws_vl (2 or 4; 0 = not built)
-  int64_t vl_rows = 0;          // rows of ws_vl
+  // virtual limb rows of the multi-limb owners, two groups by limb count:
+  // [0] positions [0, n4) with 3-4 limbs (4 slots), [1] [n4, n_multi) with 2 (2 slots)
+  struct VLGroup {
+    int64_t o0 = 0, o1 = 0;  // permuted positions
+    int32_t ls = 0;          // limb slots
+    int64_t rows = 0;        // virtual rows in buf
+    cms::DevBuf buf;
+  } vl[2];
+  bool vl_ok = false;           // every multi-limb owner fits 4 limbs (else the legacy 128x128 path)
   int64_t topk_redo = 0;        // top-k rows the sampled threshold missed (radix-select redo)
   std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
   int64_t pairs_ingested = 0;
@@ -89,7 +96,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out;
-  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_vl, ws_nsq, ws_cand;
+  cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 
   // communicator
   ncclComm_t comm = nullptr;
