@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(HERE, "libmahout_cms.so")
+SO_PATH = os.environ.get("MAHOUT_CMS_LIB") or os.path.join(HERE, "libmahout_cms.so")  # override: experiments
 
 # status codes (include/mahout_cms.h)
 CMS_OK = 0

@@ -90,6 +90,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
     atomic_mode = row_hot[row] >= 0;
     hi = atomic_mode ? lo + slice : off[row + 1];
   }
+#ifdef CMS_BUILD_NOKEYS  // bound analysis only: the write path alone
+  hi = lo;
+#endif
   uint32_t* dst = table + row * dw;
   const bool load_old = accumulate && !atomic_mode;
   if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;

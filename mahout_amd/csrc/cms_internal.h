@@ -43,7 +43,10 @@ struct PendingEvent {
 
 // Row-build tuning: pairs per build work item.
 constexpr int64_t kSlice = 32768;
-constexpr int kBuildThreads = 256;
+#ifndef CMS_BUILD_THREADS
+#define CMS_BUILD_THREADS 256
+#endif
+constexpr int kBuildThreads = CMS_BUILD_THREADS;
 
 }  // namespace cms
 
