@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "cms_internal.h"
 
@@ -245,7 +246,8 @@ void cms_destroy(cms_handle* h) {
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
-                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand};
+                  &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
+                  &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -286,6 +288,85 @@ int cms_hash_keys(cms_handle* h, const int64_t* keys, int64_t n, int32_t* out) {
   return CMS_OK;
 }
 
+namespace {
+
+// Delta log of a merged multi-rank handle (cms_internal.h).  Grows by copy.
+int dlog_reserve(cms_handle* h, int64_t need) {
+  if (need <= h->dlog_cap) return CMS_OK;
+  const int64_t cap = std::max<int64_t>({need, 2 * h->dlog_cap, int64_t(1) << 16});
+  cms::DevBuf nr, nk, nv;
+  CMS_HIP(nr.ensure(sizeof(int64_t) * cap));
+  CMS_HIP(nk.ensure(sizeof(int64_t) * cap));
+  CMS_HIP(nv.ensure(sizeof(float) * cap));
+  if (h->dlog_n > 0) {
+    CMS_HIP(hipMemcpyAsync(nr.ptr, h->dlog_row.ptr, sizeof(int64_t) * h->dlog_n, hipMemcpyDeviceToDevice, h->stream));
+    CMS_HIP(hipMemcpyAsync(nk.ptr, h->dlog_key.ptr, sizeof(int64_t) * h->dlog_n, hipMemcpyDeviceToDevice, h->stream));
+    CMS_HIP(hipMemcpyAsync(nv.ptr, h->dlog_val.ptr, sizeof(float) * h->dlog_n, hipMemcpyDeviceToDevice, h->stream));
+  }
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  h->dlog_row.release();
+  h->dlog_key.release();
+  h->dlog_val.release();
+  std::swap(h->dlog_row, nr);
+  std::swap(h->dlog_key, nk);
+  std::swap(h->dlog_val, nv);
+  h->dlog_cap = cap;
+  return CMS_OK;
+}
+
+// Log a batch (rows already resolved) that went into a merged multi-rank table.
+int dlog_append(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n) {
+  if (!(h->merged && h->comm && h->world > 1) || n <= 0) return CMS_OK;
+  int rc = dlog_reserve(h, h->dlog_n + n);
+  if (rc) return rc;
+  const int64_t o = h->dlog_n;
+  CMS_HIP(hipMemcpyAsync(h->dlog_row.as<int64_t>() + o, d_row, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, h->stream));
+  CMS_HIP(hipMemcpyAsync(h->dlog_key.as<int64_t>() + o, d_key, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, h->stream));
+  if (d_val)
+    CMS_HIP(hipMemcpyAsync(h->dlog_val.as<float>() + o, d_val, sizeof(float) * n, hipMemcpyDeviceToDevice, h->stream));
+  else
+    CMS_HIP(hipMemsetD32Async((hipDeviceptr_t)(h->dlog_val.as<float>() + o), 0x3F800000u, (size_t)n, h->stream));
+  h->dlog_n += n;
+  return CMS_OK;
+}
+
+// Exchange the logs of every rank and apply the other ranks' batches.
+int dlog_exchange(cms_handle* h) {
+  const int G = h->world;
+  CMS_HIP(h->dlog_cnt.ensure(sizeof(int64_t) * (G + 1)));
+  int64_t* cnt = h->dlog_cnt.as<int64_t>();
+  CMS_HIP(hipMemcpyAsync(cnt, &h->dlog_n, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+  ncclResult_t r = ncclAllGather(cnt, cnt + 1, 1, ncclInt64, h->comm, h->stream);
+  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather(delta counts): %s", ncclGetErrorString(r));
+  std::vector<int64_t> counts(G);
+  CMS_HIP(hipMemcpyAsync(counts.data(), cnt + 1, sizeof(int64_t) * G, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  const int64_t m = *std::max_element(counts.begin(), counts.end());
+  if (m == 0) return CMS_OK;
+  int rc = dlog_reserve(h, m);  // the send buffers are read to length m
+  if (rc) return rc;
+  const size_t per = sizeof(int64_t) * 2 + sizeof(float);
+  CMS_HIP(h->dlog_all.ensure(per * (size_t)G * (size_t)m));
+  int64_t* g_row = h->dlog_all.as<int64_t>();
+  int64_t* g_key = g_row + (size_t)G * m;
+  float* g_val = reinterpret_cast<float*>(g_key + (size_t)G * m);
+  ncclGroupStart();
+  ncclAllGather(h->dlog_row.ptr, g_row, (size_t)m, ncclInt64, h->comm, h->stream);
+  ncclAllGather(h->dlog_key.ptr, g_key, (size_t)m, ncclInt64, h->comm, h->stream);
+  ncclAllGather(h->dlog_val.ptr, g_val, (size_t)m, ncclFloat32, h->comm, h->stream);
+  r = ncclGroupEnd();
+  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather(delta logs): %s", ncclGetErrorString(r));
+  for (int q = 0; q < G; ++q) {
+    if (q == h->rank || counts[q] == 0) continue;
+    const size_t o = (size_t)q * m;
+    if ((rc = ingest_coo_device(h, g_row + o, g_key + o, g_val + o, counts[q]))) return rc;
+  }
+  h->dlog_n = 0;
+  return CMS_OK;
+}
+
+}  // namespace
+
 int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t n) {
   if (!h || (n > 0 && (!owner || !key))) return set_error(CMS_E_PARAM, "null argument");
   if (n <= 0) return CMS_OK;
@@ -309,6 +390,7 @@ int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const fl
   if ((rc = check_flags(h, by_id))) return rc;
   rc = ingest_coo_device(h, d_row, h->ws_in_key.as<int64_t>(), val ? h->ws_in_val.as<float>() : nullptr, n);
   if (rc) return rc;
+  if ((rc = dlog_append(h, d_row, h->ws_in_key.as<int64_t>(), val ? h->ws_in_val.as<float>() : nullptr, n))) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
   h->finalized = false;
   rc = check_flags(h, by_id);
@@ -321,6 +403,7 @@ int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d
   if (n <= 0) return CMS_OK;
   Guard g(h);
   int rc = ingest_coo_device(h, d_row, d_key, d_val, n);
+  if (rc == CMS_OK) rc = dlog_append(h, d_row, d_key, d_val, n);
   if (rc == CMS_OK) {
     h->pairs_ingested += n;
     h->finalized = false;
@@ -337,6 +420,8 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
   const int64_t np = offsets[n];
   if (np > 0 && !keys) return set_error(CMS_E_PARAM, "null keys");
   Guard g(h);
+  if (h->merged && h->comm && h->world > 1)
+    return set_error(CMS_E_STATE, "CSR bulk ingest into a merged multi-rank table: cms_reset first, or use COO ingest");
   CMS_HIP(h->ws_in_row.ensure(sizeof(int64_t) * (n + 1)));
   CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * std::max<int64_t>(np, 1)));
   if (vals) CMS_HIP(h->ws_in_val.ensure(sizeof(float) * std::max<int64_t>(np, 1)));
@@ -362,6 +447,8 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
 int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t* d_keys, const float* d_vals) {
   if (!h || !d_offsets) return set_error(CMS_E_PARAM, "null argument");
   Guard g(h);
+  if (h->merged && h->comm && h->world > 1)
+    return set_error(CMS_E_STATE, "CSR bulk ingest into a merged multi-rank table: cms_reset first, or use COO ingest");
   int64_t np = 0;
   CMS_HIP(hipMemcpyAsync(&np, d_offsets + h->n, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
@@ -381,6 +468,8 @@ int cms_reset(cms_handle* h) {
   h->norms_valid = false;
   h->finalized = false;
   h->pairs_ingested = 0;
+  h->merged = false;
+  h->dlog_n = 0;
   return CMS_OK;
 }
 
@@ -390,7 +479,7 @@ int cms_release_scratch(cms_handle* h) {
   CMS_HIP(hipStreamSynchronize(h->stream));
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_hot, &h->ws_query,
-                  &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand};
+                  &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand, &h->ws_srow};
   for (DevBuf* b : ws) b->release();
   return CMS_OK;
 }
@@ -441,7 +530,11 @@ int cms_finalize(cms_handle* h) {
     h->empty = false;
     h->norms_valid = false;
   }
-  if (h->comm && h->world > 1) {
+  if (h->comm && h->world > 1 && h->merged) {
+    TimedScope ts(h, "delta_exchange");
+    int rc = dlog_exchange(h);
+    if (rc) return rc;
+  } else if (h->comm && h->world > 1) {
     TimedScope ts(h, "allreduce");
     ncclResult_t r = ncclAllReduce(h->d_table, h->d_table, (size_t)(h->n * h->dw), ncclUint32, ncclSum, h->comm,
                                    h->stream);
@@ -449,6 +542,8 @@ int cms_finalize(cms_handle* h) {
     r = ncclAllReduce(h->d_row_mass, h->d_row_mass, (size_t)h->n, ncclUint64, ncclSum, h->comm, h->stream);
     if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce(mass): %s", ncclGetErrorString(r));
     h->norms_valid = false;
+    h->merged = true;
+    h->dlog_n = 0;
   }
   int rc = compute_norms(h);
   if (rc) return rc;

@@ -152,8 +152,13 @@ int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_row
 
 // ------------------------------------------------ small-batch atomic path --
 
+// With `track`, the norms and row maxima stay current: a counter moving from
+// c to c+inc adds 2*c*inc + inc^2 to its sum of squares, and the per-update
+// deltas telescope to the exact new sum whatever the atomic order.  A norm
+// reaching 2^53 (inexact fp64 regime) raises flags[2] so finalize recomputes.
 __global__ void k_ingest_atomic(const int64_t* row, const int64_t* key, const float* val, int64_t n, int64_t nrows,
-                                HashParams hp, uint32_t* table, uint64_t* row_mass, uint32_t* flags) {
+                                HashParams hp, uint32_t* table, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
+                                int track, uint32_t* flags) {
   const int64_t dw = (int64_t)hp.depth * hp.width;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = row[i];
@@ -169,9 +174,86 @@ __global__ void k_ingest_atomic(const int64_t* row, const int64_t* key, const fl
     if (inc == 0) continue;
     uint64_t kp = reduce_key(key[i]);
     uint32_t* sk = table + r * dw;
-    for (int d = 0; d < hp.depth; ++d) atomicAdd(sk + (int64_t)d * hp.width + bucket(hp, d, kp), inc);
+    uint32_t cmax = 0;
+    for (int d = 0; d < hp.depth; ++d) {
+      uint32_t c = atomicAdd(sk + (int64_t)d * hp.width + bucket(hp, d, kp), inc);
+      if (track) {
+        uint64_t delta = 2ULL * c * inc + (uint64_t)inc * inc;
+        unsigned long long o = atomicAdd((unsigned long long*)&norm[r * hp.depth + d], (unsigned long long)delta);
+        if (o + delta >= (1ULL << 53)) atomicOr(flags + 2, 1u);
+        cmax = max(cmax, c + inc);
+      }
+    }
+    if (track) atomicMax(&rowmax[r], cmax);
     unsigned long long old = atomicAdd((unsigned long long*)&row_mass[r], (unsigned long long)inc);
     if (old + inc >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+  }
+}
+
+// Incremental batch already grouped by owner (partition_to_csr with per-pair
+// rows): the same exact counter atomics, but the norm / row-max / mass updates
+// of the lanes of one owner are reduced inside the wave first (rows are
+// non-decreasing along the lanes, so each owner is one contiguous lane run),
+// so a hot owner costs one atomic per wave instead of one per pair.
+__device__ __forceinline__ uint64_t seg_suffix_sum(uint64_t v, int32_t r, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint64_t ov = __shfl_down(v, o, 64);
+    int32_t orr = __shfl_down(r, o, 64);
+    if (lane + o < 64 && orr == r) v += ov;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, const int64_t* key, const float* val,
+                                                        const int64_t* count, HashParams hp, uint32_t* table,
+                                                        uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
+                                                        uint32_t* flags) {
+  const int64_t n = *count;  // pairs that survived the partition's row check
+  const int64_t dw = (int64_t)hp.depth * hp.width;
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    int32_t r = -1;
+    uint32_t inc = 0;
+    uint64_t kp = 0;
+    if (i < n) {
+      r = rows[i];
+      if (!load_inc(val, i, inc)) {
+        atomicOr(flags, kFlagBadValue);
+        inc = 0;
+      }
+      kp = reduce_key(key[i]);
+    }
+    const int32_t rprev = __shfl_up(r, 1, 64);
+    const bool head = r >= 0 && (lane == 0 || rprev != r);
+    uint32_t* sk = table + (int64_t)(r < 0 ? 0 : r) * dw;
+    uint32_t cmax = 0;
+    for (int d = 0; d < hp.depth; ++d) {
+      uint64_t delta = 0;
+      if (inc) {
+        uint32_t c = atomicAdd(sk + (int64_t)d * hp.width + bucket(hp, d, kp), inc);
+        delta = 2ULL * c * inc + (uint64_t)inc * inc;
+        cmax = max(cmax, c + inc);
+      }
+      delta = seg_suffix_sum(delta, r, lane);
+      if (head && delta) {
+        unsigned long long o = atomicAdd((unsigned long long*)&norm[(int64_t)r * hp.depth + d], (unsigned long long)delta);
+        if (o + delta >= (1ULL << 53)) atomicOr(flags + 2, 1u);
+      }
+    }
+    uint64_t mass = seg_suffix_sum((uint64_t)inc, r, lane);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      uint32_t om = (uint32_t)__shfl_down((int)cmax, o, 64);
+      int32_t orr = __shfl_down(r, o, 64);
+      if (lane + o < 64 && orr == r) cmax = max(cmax, om);
+    }
+    if (head && mass) {
+      atomicMax(&rowmax[r], cmax);
+      unsigned long long old = atomicAdd((unsigned long long*)&row_mass[r], (unsigned long long)mass);
+      if (old + mass >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+    }
   }
 }
 
@@ -228,7 +310,12 @@ __global__ void k_norm_sqrt(const uint64_t* norm, int64_t cells, double* out, ui
 
 int compute_norms(cms_handle* h) {
   TimedScope ts(h, "norms");
+  uint32_t stale = 0;  // an incremental norm reached the inexact regime
+  CMS_HIP(hipMemcpyAsync(&stale, h->d_flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (stale) h->norms_valid = false;
   if (!h->norms_valid) {
+    CMS_HIP(hipMemsetAsync(h->d_flags + 2, 0, sizeof(uint32_t), h->stream));
     unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
     if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->n, h->hp, h->d_norm,
                                      h->d_rowmax);
@@ -251,8 +338,12 @@ int compute_norms(cms_handle* h) {
 int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs) {
   if (npairs <= 0) return CMS_OK;
   const int64_t n = h->n;
-  // Small batch into a live table: exact global atomics.
-  const bool small = npairs < 262144 || npairs * 8 < n;
+  // Global atomics for a small batch, and for any batch into a live table
+  // unless its atomic traffic (~d sector RMWs per pair) exceeds the
+  // accumulate build's full-table read + write.
+  const double table_bytes = 4.0 * (double)n * (double)h->dw;
+  const bool small = npairs < 262144 || npairs * 8 < n ||
+                     (!h->empty && (double)npairs * h->p.depth * 128.0 < 2.0 * table_bytes);
   if (small || npairs >= (int64_t(1) << 31)) {
     if (npairs >= (int64_t(1) << 31)) {
       // split very large batches into partition-sized pieces
@@ -263,17 +354,34 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
       }
       return CMS_OK;
     }
+    if (!h->empty && h->norms_valid && npairs >= 32768 && n < (int64_t(1) << 31)) {
+      // live table with current norms: group by owner, then wave-reduced atomics
+      int64_t *coff, *ckey;
+      float* cval;
+      CMS_HIP(h->ws_srow.ensure(sizeof(int32_t) * (size_t)npairs));
+      int rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &coff, &ckey, &cval, h->ws_srow.as<int32_t>());
+      if (rc) return rc;
+      TimedScope ts(h, "ingest_atomic");
+      unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
+      hipLaunchKernelGGL(k_ingest_sorted, dim3(grid), dim3(256), 0, h->stream, h->ws_srow.as<int32_t>(), ckey, cval,
+                         coff + n, h->hp, h->d_table, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+      CMS_HIP(hipGetLastError());
+      return CMS_OK;
+    }
     TimedScope ts(h, "ingest_atomic");
     if (h->empty) {
       CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * (size_t)(n * h->dw), h->stream));
       CMS_HIP(hipMemsetAsync(h->d_row_mass, 0, sizeof(uint64_t) * (size_t)n, h->stream));
+      CMS_HIP(hipMemsetAsync(h->d_norm, 0, sizeof(uint64_t) * (size_t)(n * h->p.depth), h->stream));
+      CMS_HIP(hipMemsetAsync(h->d_rowmax, 0, sizeof(uint32_t) * (size_t)n, h->stream));
+      h->norms_valid = true;
     }
+    const int track = h->norms_valid ? 1 : 0;
     unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
     hipLaunchKernelGGL(k_ingest_atomic, dim3(grid), dim3(256), 0, h->stream, d_row, d_key, d_val, npairs, n, h->hp,
-                       h->d_table, h->d_row_mass, h->d_flags);
+                       h->d_table, h->d_row_mass, h->d_norm, h->d_rowmax, track, h->d_flags);
     CMS_HIP(hipGetLastError());
     h->empty = false;
-    h->norms_valid = false;
     return CMS_OK;
   }
 

@@ -98,12 +98,18 @@ struct cms_handle {
   cms::DevBuf ws_p1_row, ws_p1_key, ws_p1_val;   // pass-1 partition output
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
-  cms::DevBuf ws_query, ws_out;
+  cms::DevBuf ws_query, ws_out, ws_srow;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 
   // communicator
   ncclComm_t comm = nullptr;
   int32_t rank = 0, world = 1;
+  // After the first multi-rank finalize every rank holds the summed table; later
+  // COO batches are logged here and only the logs are exchanged at the next
+  // finalize (each rank applies the other ranks' batches).
+  bool merged = false;
+  int64_t dlog_n = 0, dlog_cap = 0;
+  cms::DevBuf dlog_row, dlog_key, dlog_val, dlog_cnt, dlog_all;
 
   // instrumentation
   bool timing = false;
@@ -146,7 +152,8 @@ int scan_exclusive_u32(cms_handle* h, const uint32_t* in, uint32_t* out, int64_t
 // ---- cms_partition.hip ----
 // COO -> CSR grouped by row; outputs live in handle scratch.
 int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                     int64_t** out_off, int64_t** out_key, float** out_val);
+                     int64_t** out_off, int64_t** out_key, float** out_val,
+                     int32_t* out_rows = nullptr);
 
 // ---- launchers (cms_query.hip) ----
 int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);

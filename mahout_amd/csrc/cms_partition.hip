@@ -274,7 +274,8 @@ __global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* H2, const uint
 __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fine, const int64_t* key1,
                                                              const float* val1, const uint32_t* binStart,
                                                              const uint32_t* blkStart, int P1, int64_t CH2, int P2,
-                                                             const uint32_t* O2, int64_t* okey, float* oval) {
+                                                             const uint32_t* O2, int64_t* okey, float* oval,
+                                                             int32_t* orow) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t nblk = blkStart[P1];
   if (blockIdx.x >= nblk) return;
@@ -319,6 +320,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
       uint32_t g = L.cursor[f] + (i - L.off[f]);
       okey[g] = L.key[i];
       if (oval) oval[g] = L.val[i];
+      if (orow) orow[g] = b * P2 + (int32_t)f;
     }
     __syncthreads();
     for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] += L.hist[f];
@@ -333,7 +335,7 @@ static int ceil_log2(int64_t v) {
 }
 
 int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                     int64_t** out_off, int64_t** out_key, float** out_val) {
+                     int64_t** out_off, int64_t** out_key, float** out_val, int32_t* out_rows) {
   const int64_t n = h->n;
   const int B = std::max(1, ceil_log2(n));
   int s2 = std::min(B, 10);
@@ -390,7 +392,7 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
                        binStart, blkStart, P1, CH2, P2, H2);
     hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, H2, binStart, blkStart, P1, P2, n, O2, coff);
     hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2), h->stream, fine,
-                       key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval);
+                       key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     CMS_HIP(hipGetLastError());
   }
   *out_off = coff;

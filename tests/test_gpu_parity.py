@@ -433,3 +433,38 @@ def test_top_k_all_shards_merge_exact(oracle, nshards):
             assert mi[q, :mc[q]].tolist() == ids[q, :cnt[q]].tolist(), q
             assert same(ms[q, :mc[q]], sc[q, :cnt[q]]), q
         assert t.stats()["multi_limb_owners"] > 0
+
+
+def test_streaming_refresh_incremental_norms(oracle):
+    """Config-5 pattern: a bulk-built table, then small batches through the
+    atomic paths (which keep norms and row maxima current incrementally), then a
+    refresh.  Counters, pair similarities and all-pairs top-k equal the oracle
+    on the whole stream and a table built from it in one batch."""
+    n, d, w, k = 2500, 4, 256, 30
+    items, users = zipf_stream(4000, n, 600_000, seed=91)
+    vals = np.random.Generator(np.random.PCG64(91)).integers(1, 4, size=items.size).astype(np.float32)
+    ot = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42) as ref:
+        ref.ingest(items, users, vals)
+        ref.finalize()
+        rids, rsc, rcnt = ref.top_k_all(k)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items[:400_000], users[:400_000], vals[:400_000])
+        t.finalize()
+        t.top_k_all(k)
+        # 3 batches through the owner-grouped path (>= 32768 pairs), 5 through plain atomics
+        cuts = [400_000, 450_000, 500_000, 550_000] + list(range(560_000, 600_001, 10_000))
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            t.ingest(items[lo:hi], users[lo:hi], vals[lo:hi])
+        t.finalize()
+        assert same(t.read_counters(), ot)
+        for q in [0, 3, 999, n - 1]:
+            exp = _oracle_row_sims(oracle, ot, q)
+            exp[q] = oracle.cosine_cm(ot[q], ot[q])
+            assert same(t.similarities(q, np.arange(n)), exp), q
+        ids, sc, cnt = t.top_k_all(k)
+        assert np.array_equal(cnt, rcnt)
+        for q in range(n):
+            assert ids[q, :cnt[q]].tolist() == rids[q, :rcnt[q]].tolist(), q
+            assert same(sc[q, :cnt[q]], rsc[q, :rcnt[q]]), q
+        assert t.stats()["multi_limb_owners"] > 0
