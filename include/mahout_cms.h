@@ -223,6 +223,7 @@ typedef struct cms_stats {
   int64_t multi_limb_owners; /* owners with a counter >= 128 (all-pairs limb split; -1 before the first all-pairs call) */
   int64_t topk_redo;         /* top-k rows that needed the radix-select fallback */
   int64_t deep_limb_owners;  /* of those, owners with a counter >= 2^14 (3+ limbs); -1 before */
+  int64_t fp4_owners;        /* single-limb owners with every counter <= 4 (fp4 MFMA operands); -1 before */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -64,6 +64,7 @@ class CmsStats(ctypes.Structure):
         ("multi_limb_owners", ctypes.c_int64),
         ("topk_redo", ctypes.c_int64),
         ("deep_limb_owners", ctypes.c_int64),
+        ("fp4_owners", ctypes.c_int64),
     ]
 
 

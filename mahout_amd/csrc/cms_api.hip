@@ -247,7 +247,8 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
-                  &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow};
+                  &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
+                  &h->ws_f4};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -826,6 +827,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;
+  out->fp4_owners = h->mfma_ready ? h->n_f4 : -1;
   return CMS_OK;
 }
 

@@ -38,6 +38,7 @@ typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 constexpr int kTile = 128;      // output rows/cols per workgroup
 constexpr int kBK = 128;        // K bytes per stage
 constexpr int kMaxLimbs = 5;    // 35 bits >= any u32 counter
+constexpr uint32_t kF4Max = 4;  // owners whose counters are all <= this also get an fp4 (e2m1) image
 
 // ------------------------------------------------------------ preparation --
 
@@ -45,8 +46,8 @@ constexpr int kMaxLimbs = 5;    // 35 bits >= any u32 counter
 // passes record), multi-limb flags (L > 1, L > 2), inexact-norm count and
 // the count of owners needing all 5 limbs.
 __global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int64_t nrows, const uint64_t* norm,
-                                                    int depth, uint8_t* rowL, uint32_t* multi_flag, uint32_t* deep_flag,
-                                                    uint32_t* inexact_rows) {
+                                                    int depth, int fp4_ok, uint8_t* rowL, uint32_t* multi_flag,
+                                                    uint32_t* deep_flag, uint32_t* f4_flag, uint32_t* inexact_rows) {
   const int64_t row = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (row >= nrows) return;
   const uint32_t mx = rowmax[row];
@@ -55,21 +56,25 @@ __global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int6
   rowL[row] = (uint8_t)L;
   multi_flag[row] = L > 1 ? 1u : 0u;
   deep_flag[row] = L > 2 ? 1u : 0u;
+  f4_flag[row] = (fp4_ok && mx <= kF4Max) ? 1u : 0u;
   if (L == kMaxLimbs) atomicAdd(inexact_rows + 1, 1u);
   bool inexact = false;
   for (int d = 0; d < depth; ++d) inexact |= norm[row * depth + d] >= (1ULL << 53);
   if (inexact) atomicAdd(inexact_rows, 1u);
 }
 
-// Stable permutation: owners with 3+ limbs, then 2 limbs, then single-limb,
-// each class in row order (exclusive scans of the class flags).
+// Stable permutation: owners with 3+ limbs, then 2 limbs, then single-limb
+// owners with a counter above kF4Max, then the fp4 class (every counter
+// <= kF4Max), each class in row order (exclusive scans of the class flags).
 __global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, const uint32_t* dpos,
-                            const uint32_t* deep_flag, const uint8_t* rowL, int64_t nrows, int64_t n_deep,
-                            int64_t n_multi, int64_t* perm, int64_t* inv, uint8_t* rowLp) {
+                            const uint32_t* deep_flag, const uint32_t* fpos, const uint32_t* f4_flag,
+                            const uint8_t* rowL, int64_t nrows, int64_t n_deep, int64_t n_multi, int64_t n_s8,
+                            int64_t* perm, int64_t* inv, uint8_t* rowLp) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = deep_flag[r]    ? (int64_t)dpos[r]
                       : multi_flag[r] ? n_deep + ((int64_t)mpos[r] - (int64_t)dpos[r])
-                                      : n_multi + (r - (int64_t)mpos[r]);
+                      : f4_flag[r]    ? n_multi + n_s8 + (int64_t)fpos[r]
+                                      : n_multi + (r - (int64_t)mpos[r] - (int64_t)fpos[r]);
     perm[p] = r;
     inv[r] = p;
     rowLp[p] = rowL[r];
@@ -94,6 +99,25 @@ __global__ __launch_bounds__(256) void k_limb_write(const uint32_t* table, int64
           make_char4((signed char)((v.x >> sh) & 127u), (signed char)((v.y >> sh) & 127u),
                      (signed char)((v.z >> sh) & 127u), (signed char)((v.w >> sh) & 127u));
     }
+  }
+}
+
+// fp4 (e2m1) image of positions [f0, n): two counters per byte, low nibble
+// first.  Every counter is <= kF4Max, and 0..4 are exact e2m1 codes.
+__global__ __launch_bounds__(256) void k_f4_write(const uint32_t* table, int64_t dw, const int64_t* perm, int64_t f0,
+                                                  uint8_t* f4) {
+  const int64_t p = f0 + blockIdx.x;
+  const uint32_t* src = table + perm[p] * dw;
+  uint8_t* dst = f4 + (int64_t)blockIdx.x * (dw / 2);
+  // e2m1: 0 -> 0x0, 1 -> 0x2 (1.0), 2 -> 0x4 (2.0), 3 -> 0x5 (3.0), 4 -> 0x6 (4.0)
+  constexpr uint32_t kCode = 0x65420u;  // nibble c = code of value c
+  for (int64_t j = threadIdx.x * 8; j < dw; j += 256 * 8) {
+    const uint4 v0 = *reinterpret_cast<const uint4*>(src + j);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(src + j + 4);
+    auto code = [&](uint32_t c) { return (kCode >> (4 * c)) & 15u; };
+    const uint32_t packed = code(v0.x) | code(v0.y) << 4 | code(v0.z) << 8 | code(v0.w) << 12 | code(v1.x) << 16 |
+                            code(v1.y) << 20 | code(v1.z) << 24 | code(v1.w) << 28;
+    *reinterpret_cast<uint32_t*>(dst + j / 2) = packed;
   }
 }
 
@@ -455,11 +479,52 @@ struct BigArgs {
   int32_t sym, wave, nb;  // sym: block I = positions [s0 + 256 I, ...) of the s_rows region
   int32_t band;           // sym: waves [wave, wave + band) in one launch
   int64_t s0, s_rows;
+  // operand images: row stride rs bytes, kw bytes per sketch row (i8: dw, w;
+  // fp4: dw/2, w/2); sym mode reads rows at (position - img0) * rs
+  int64_t rs, img0;
+  int32_t kw;
+  // sym, fsel != 0: only the block pairs with a block below fblk0 (grid of
+  // 2 * fblk0 block slots instead of nb)
+  int32_t fblk0, fsel;
 };
 
-template <int NSTAGE, int LS, int BK>
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
+
+// FMT 0: int8 limbs, v_mfma_i32_32x32x32_i8.  FMT 1: fp4 (e2m1) counters
+// <= 4, v_mfma_f32_32x32x64_f8f6f4 (unscaled): the same 16 B per lane per
+// fragment carries 32 counters instead of 16, so a stage holds twice the K
+// at the same MFMA cycles.  Products <= 16 and row sums <= 16 * 32768 < 2^24
+// keep the f32 accumulation exact.
+template <int FMT>
+struct AccOf {
+  typedef i32x16 type;
+};
+template <>
+struct AccOf<1> {
+  typedef f32x16 type;
+};
+
+template <int FMT>
+__device__ __forceinline__ typename AccOf<FMT>::type mfma_step(const i8x16& a, const i8x16& b,
+                                                               typename AccOf<FMT>::type c) {
+  if constexpr (FMT == 0) {
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+  } else {
+    const i32x4 a4 = __builtin_bit_cast(i32x4, a), b4 = __builtin_bit_cast(i32x4, b);
+    const i32x4 z = {0, 0, 0, 0};
+    const i32x8 a8 = __builtin_shufflevector(a4, z, 0, 1, 2, 3, 4, 5, 6, 7);
+    const i32x8 b8 = __builtin_shufflevector(b4, z, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 0, 0, 0);  // cbsz/blgp 4: e2m1
+  }
+}
+
+template <int NSTAGE, int LS, int BK, int FMT = 0>
 __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   static_assert(BK == 128 || BK == 64, "stage depth");
+  static_assert(FMT == 0 || LS == 1, "fp4 operands are single-limb owners");
+  using AccT = typename AccOf<FMT>::type;
   constexpr int OA = kTA / LS;  // owners per A panel
   constexpr int OG = 4 / LS;    // owner groups per 32-row block in one lane
   constexpr int kStageA = kTA * BK, kStageB = kTB * BK, kStage = kStageA + kStageB;
@@ -484,8 +549,17 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     // 128-column halves.  Consecutive workgroups share I (its panel stays in
     // the XCD's L2 for 2*band workgroups) and neighbouring I share most J.
     const int per = 2 * g.band;
-    const int I = lin / per, rem = lin - I * per, t = rem >> 1, half = rem & 1;
+    const int c = lin / per, rem = lin - c * per, t = rem >> 1, half = rem & 1;
     const int wv = g.wave + t;
+    int I = c;
+    if (g.fsel) {
+      // only the pairs with a block below fblk0: c < fblk0 is that block as I,
+      // c >= fblk0 enumerates J = c - fblk0 < fblk0 with I >= fblk0
+      if (c >= g.fblk0) {
+        I = ((c - g.fblk0 - wv) % g.nb + g.nb) % g.nb;
+        if (I < g.fblk0) return;  // already the first run's pair
+      }
+    }
     if ((g.nb & 1) == 0 && 2 * wv == g.nb && 2 * I >= g.nb) return;  // {I, I + nb/2} once
     const int J = (I + wv) % g.nb;
     diag = I == J;
@@ -494,8 +568,8 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     b_pos0 = g.s0 + (int64_t)J * kTA + half * kTB;
     b_rows = min<int64_t>(kTB, g.s_rows - (int64_t)J * kTA - half * kTB);
     if (b_rows <= 0) return;  // the whole workgroup leaves before any barrier
-    gA = g.A + a_pos0 * g.dw;
-    gB = g.B + b_pos0 * g.dw;
+    gA = g.A + (a_pos0 - g.img0) * g.rs;
+    gB = g.B + (b_pos0 - g.img0) * g.rs;
     vrow0 = own0 = bcol0 = 0;
   } else {
     // A panel fastest: an XCD's co-resident workgroups cover a few candidate
@@ -510,8 +584,9 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid >> 1, wc = wid & 1;
-  const int w = g.w;
-  const int cstages = w / BK;
+  const int kw = g.kw;  // bytes per sketch row in the operand image
+  const int64_t rs = g.rs;
+  const int cstages = kw / BK;
 #ifdef CMS_BOUND_ANALYSIS
   const int kMode = g.mode;  // bit0 skip loads, bit1 skip MFMA, bit2 skip epilogue
 #else
@@ -540,9 +615,9 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, a_vrows - vrow0));
   const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, b_rows - bcol0));
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(gA + vrow0 * g.dw), (short)0, (int)(rowsA * g.dw), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(gA + vrow0 * rs), (short)0, (int)(rowsA * rs), 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(gB + bcol0 * g.dw), (short)0, (int)(rowsB * g.dw), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(gB + bcol0 * rs), (short)0, (int)(rowsB * rs), 0x00020000);
   // Instruction u of wave wid fills LDS rows [(wid + 8u) * RPI, +RPI); lane
   // i lands at byte 16 i, i.e. row (wid + 8u) * RPI + i / (BK/16), slot
   // i % (BK/16), and fetches the chunk the swizzle puts there.  The 8*RPI-row
@@ -551,13 +626,13 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   constexpr int CPR = BK / 16;  // 16-B chunks per row
   const int srow = wid * RPI + lane / CPR;
   const int slot = lane % CPR;
-  const int32_t vo = (int32_t)(srow * g.dw) +
+  const int32_t vo = (int32_t)(srow * rs) +
                      ((BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4);
-  const int32_t rstep = 8 * RPI * (int32_t)g.dw;
+  const int32_t rstep = 8 * RPI * (int32_t)rs;
   auto issue = [&](int s) {
     if (kMode & 1) return;
     const int r = s / cstages, cs = s - r * cstages;
-    const int32_t koff = r * w + cs * BK;
+    const int32_t koff = r * kw + cs * BK;
     unsigned char* st = lds + (s % NSTAGE) * kStage;
 #pragma unroll
     for (int u = 0; u < OPA; ++u)
@@ -570,7 +645,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
           koff, 0, 0);
   };
 
-  i32x16 acc[2][2];
+  AccT acc[2][2];
   double mn[2][2][4 * OG];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -611,7 +686,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
     }
     const int r = s / cstages;
     if (s - r * cstages == cstages - 1 && !(kMode & 4)) {
@@ -729,9 +804,10 @@ int cosine_prepare(cms_handle* h) {
   const int64_t ntiles = (n + kTile - 1) / kTile;
   CMS_HIP(h->ws_limb0.ensure((size_t)n * (size_t)dw));
   // meta: perm[n] i64 | inv[n] i64 | multi_flag[n] u32 | mpos[n] u32 | bsum | rowL[n] | rowLp[n] | tileL[ntiles]
-  //       | deep_flag[n] u32 | dpos[n] u32
+  //       | deep_flag[n] u32 | dpos[n] u32 | f4_flag[n] u32 | fpos[n] u32
   const int64_t nbs = (n + 4095) / 4096 + 1;
-  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (8 + 8 + 4 + 4 + 1 + 1 + 4 + 4) + 4 * (size_t)nbs + (size_t)ntiles + 64));
+  CMS_HIP(h->ws_limbmeta.ensure((size_t)n * (8 + 8 + 4 + 4 + 1 + 1 + 4 + 4 + 4 + 4) + 4 * (size_t)nbs +
+                                (size_t)ntiles + 64));
   int64_t* perm = h->ws_limbmeta.as<int64_t>();
   int64_t* inv = perm + n;
   uint32_t* mflag = reinterpret_cast<uint32_t*>(inv + n);
@@ -742,13 +818,20 @@ int cosine_prepare(cms_handle* h) {
   uint8_t* tileL = rowLp + n;
   uint32_t* dflag = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(tileL + ntiles) + 15) & ~uintptr_t(15));
   uint32_t* dpos = dflag + n;
+  uint32_t* fflag = dpos + n;
+  uint32_t* fpos = fflag + n;
   uint32_t* cnt = h->d_flags + 8;  // [8] inexact owners, [9] 5-limb owners
   CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
-  uint32_t host[6];
+  // fp4 operands need whole 128-B stages of packed counters (256 per stage)
+  int fp4_ok = (h->p.width % 256) == 0 ? 1 : 0;
+#ifdef CMS_BOUND_ANALYSIS
+  if (getenv("CMS_NO_FP4")) fp4_ok = 0;
+#endif
+  uint32_t host[8];
   {
     TimedScope ts(h, "limb_prep");
     hipLaunchKernelGGL(k_limb_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, h->d_rowmax, n,
-                       h->d_norm, h->p.depth, rowL, mflag, dflag, cnt);
+                       h->d_norm, h->p.depth, fp4_ok, rowL, mflag, dflag, fflag, cnt);
     int rc = scan_exclusive_u32(h, mflag, mpos, n, bsum);
     if (rc) return rc;
     CMS_HIP(hipMemcpyAsync(&host[0], mpos + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
@@ -759,10 +842,21 @@ int cosine_prepare(cms_handle* h) {
     CMS_HIP(hipMemcpyAsync(&host[2], cnt, 8, hipMemcpyDeviceToHost, h->stream));
     CMS_HIP(hipMemcpyAsync(&host[4], dpos + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
     CMS_HIP(hipMemcpyAsync(&host[5], dflag + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    rc = scan_exclusive_u32(h, fflag, fpos, n, bsum);
+    if (rc) return rc;
+    CMS_HIP(hipMemcpyAsync(&host[6], fpos + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[7], fflag + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
     CMS_HIP(hipStreamSynchronize(h->stream));
   }
   const int64_t n_multi = (int64_t)host[0] + host[1];
   const int64_t n_deep = (int64_t)host[4] + host[5];
+  const int64_t n_f4 = (int64_t)host[6] + host[7];
+  const int64_t n_s8 = n - n_multi - n_f4;
+  // fp4 image from the first 256-row block of the single-limb region that
+  // holds fp4 owners only (symmetric-wave blocks start at n_multi)
+  const int64_t f0 = std::min<int64_t>(n, n_multi + (n_s8 + kTA - 1) / kTA * kTA);
+  h->n_f4 = n_f4;
+  h->f4_pos0 = f0;
   h->n_hot_limb = (uint32_t)n_multi;
   h->n_inexact_rows = host[2];
   const uint32_t n_five = host[3];
@@ -770,8 +864,8 @@ int cosine_prepare(cms_handle* h) {
   {
     TimedScope ts(h, "limb_prep");
     unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, rowL, n, n_deep,
-                       n_multi, perm, inv, rowLp);
+    hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, fpos, fflag, rowL,
+                       n, n_deep, n_multi, n_s8, perm, inv, rowLp);
     hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, dw, perm, rowLp, n_multi,
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
@@ -779,6 +873,11 @@ int cosine_prepare(cms_handle* h) {
     CMS_HIP(h->ws_nsq.ensure(sizeof(double) * (size_t)n * (size_t)h->p.depth));
     hipLaunchKernelGGL(k_perm_norms, dim3(grid), dim3(256), 0, h->stream, h->d_norm_sqrt, perm, n, h->p.depth,
                        h->ws_nsq.as<double>());
+    if (n > f0) {
+      CMS_HIP(h->ws_f4.ensure((size_t)(n - f0) * (size_t)(dw / 2)));
+      hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), 0, h->stream, h->d_table, dw, perm, f0,
+                         h->ws_f4.as<uint8_t>());
+    }
     CMS_HIP(hipGetLastError());
   }
   h->tile_limbs.resize(ntiles);
@@ -847,7 +946,8 @@ static BigCfg big_config(cms_handle* h) {
                          (const void*)k_cosine_big<2, 4, 128>,   (const void*)k_cosine_big<3, 4, 128>,
                          (const void*)k_cosine_big<4, 1, 64>,    (const void*)k_cosine_big<6, 1, 64>,
                          (const void*)k_cosine_big<4, 2, 64>,    (const void*)k_cosine_big<6, 2, 64>,
-                         (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>};
+                         (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>,
+                         (const void*)k_cosine_big<2, 1, 128, 1>, (const void*)k_cosine_big<3, 1, 128, 1>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
@@ -857,7 +957,7 @@ static BigCfg big_config(cms_handle* h) {
 
 // One k_cosine_big launch.  Rectangular mode: A owners x B rows; symmetric
 // mode (g.sym): sym_pairs block pairs of the wave, two workgroups each.
-static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t sym_pairs = 0) {
+static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t sym_pairs = 0, int fmt = 0) {
   if (g.sym) {
     g.tilesB = 2;
     g.nblk = (int)(2 * g.band * sym_pairs);
@@ -870,6 +970,12 @@ static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t
   if (g.nblk <= 0) return CMS_OK;
   const size_t bytes = (size_t)c.nstage * 384 * c.bk + c.norms;
   const dim3 grid((unsigned)g.nblk), blk(512);
+  if (fmt == 1) {  // fp4 operands: single-limb sym waves, 128-B stages
+    if (c.nstage == 3 && c.bk == 128) hipLaunchKernelGGL((k_cosine_big<3, 1, 128, 1>), grid, blk, bytes, h->stream, g);
+    else hipLaunchKernelGGL((k_cosine_big<2, 1, 128, 1>), grid, blk, (size_t)2 * 384 * 128 + c.norms, h->stream, g);
+    CMS_HIP(hipGetLastError());
+    return CMS_OK;
+  }
 #define CMS_BIG(NS, L, K) hipLaunchKernelGGL((k_cosine_big<NS, L, K>), grid, blk, bytes, h->stream, g)
 #define CMS_BIG_LS(NS, K)              \
   do {                                 \
@@ -903,6 +1009,8 @@ static BigArgs big_base(cms_handle* h) {
   b.w = h->p.width;
   b.depth = h->p.depth;
   b.weighted = h->p.weighting == CMS_WEIGHTED;
+  b.rs = h->dw;
+  b.kw = h->p.width;
   return b;
 }
 
@@ -1115,16 +1223,14 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
       if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts))) return rc;
     }
   }
-  // 3. S x S symmetric waves
+  // 3. S x S symmetric waves.  With fp4 owners (positions [f0, n), whole
+  // 256-row blocks from fblk0 on): waves over the fp4 region on the fp4 image,
+  // then waves over all S blocks restricted to pairs with a block below fblk0
+  // on int8 -- every unordered pair once either way.
   if (ns > 0) {
     const int64_t nb = (ns + kTA - 1) / kTA;
-    // Bands of waves per launch.  A row takes up to 512 offers per wave, but
-    // once its list has seen m columns its threshold admits about k*512/m of
-    // them; bands grow with the wave index so a launch brings ~25 expected
-    // offers per row (lists are compacted to cap/2 before each band; an
-    // overflow would flag the row for an exact recompute).  Each band reads
-    // its panels from HBM once and reuses them 2*band times from L2.
-    std::vector<std::pair<int64_t, int64_t>> bands;  // (first wave, waves)
+    const int64_t f0 = h->f4_pos0;
+    const int64_t fblk0 = f0 < n ? (f0 - nm) / kTA : nb;  // first block of fp4 owners only
     // Weighted similarities are all +-1: thresholds never tighten, so every
     // later candidate is admitted and only single waves are safe.
     const bool weighted = h->p.weighting == CMS_WEIGHTED;
@@ -1132,27 +1238,63 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
 #ifdef CMS_BOUND_ANALYSIS
     if (const char* e = getenv("CMS_BAND")) sscanf(e, "%ld,%ld", &ramp, &lmax);
 #endif
-    for (int64_t wv = 0; wv <= nb / 2;) {
-      int64_t L = (wv < 8 || weighted) ? 1 : std::max<int64_t>(1, std::min<int64_t>(lmax, wv * ramp / std::max(1, k)));
-      L = std::min<int64_t>(L, nb / 2 - wv + 1);
-      bands.push_back({wv, L});
-      wv += L;
-    }
-    for (size_t bi = shard; bi < bands.size(); bi += nshards) {
-      const int64_t wv = bands[bi].first, L = bands[bi].second;
-      const uint32_t limit = L == 1 ? (uint32_t)cap - kPerPass : (uint32_t)cap / 2;
-      if ((rc = cand_compact(h, cb, nm, ns, limit, k))) return rc;
-      BigArgs g = base;
-      g.A = g.B = limb0;
-      g.sym = 1;
-      g.wave = (int32_t)wv;
-      g.band = (int32_t)L;
-      g.nb = (int32_t)nb;
-      g.s0 = nm;
-      g.s_rows = ns;
-      g.append_a = g.append_b = 1;
-      TimedScope ts(h, "topk_all_waves");
-      if ((rc = launch_big(h, cfg, g, 1, nb))) return rc;
+    // Bands of waves per launch.  A row takes up to 512 offers per wave, but
+    // once its list has seen m columns its threshold admits about k*512/m of
+    // them; bands grow with the wave index so a launch brings ~25 expected
+    // offers per row (lists are compacted to cap/2 before each band; an
+    // overflow would flag the row for an exact recompute).  Each band reads
+    // its panels from HBM once and reuses them 2*band times from L2.
+    auto band_list = [&](int64_t nbk) {
+      std::vector<std::pair<int64_t, int64_t>> bands;  // (first wave, waves)
+      for (int64_t wv = 0; wv <= nbk / 2;) {
+        int64_t L = (wv < 8 || weighted) ? 1 : std::max<int64_t>(1, std::min<int64_t>(lmax, wv * ramp / std::max(1, k)));
+        L = std::min<int64_t>(L, nbk / 2 - wv + 1);
+        bands.push_back({wv, L});
+        wv += L;
+      }
+      return bands;
+    };
+    // pass 0: fp4 x fp4 block pairs; pass 1: the rest (all S when no fp4 region)
+    int64_t shard_ctr = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+      const bool fp4 = pass == 0;
+      if (fp4 && fblk0 >= nb) continue;
+      if (!fp4 && fblk0 == 0) continue;
+      const int64_t nbk = fp4 ? (n - f0 + kTA - 1) / kTA : nb;
+      for (const auto& bd : band_list(nbk)) {
+        if (shard_ctr++ % nshards != shard) continue;
+        const int64_t wv = bd.first, L = bd.second;
+        const uint32_t limit = L == 1 ? (uint32_t)cap - kPerPass : (uint32_t)cap / 2;
+        if ((rc = cand_compact(h, cb, nm, ns, limit, k))) return rc;
+        BigArgs g = base;
+        g.sym = 1;
+        g.wave = (int32_t)wv;
+        g.band = (int32_t)L;
+        g.nb = (int32_t)nbk;
+        g.append_a = g.append_b = 1;
+        TimedScope ts(h, "topk_all_waves");
+        if (fp4) {
+          g.A = g.B = h->ws_f4.as<int8_t>();
+          g.img0 = g.s0 = f0;
+          g.s_rows = n - f0;
+          g.rs = h->dw / 2;
+          g.kw = h->p.width / 2;
+          TimedScope t4(h, "topk_all_waves_f4");
+          if ((rc = launch_big(h, cfg, g, 1, nbk, 1))) return rc;
+        } else {
+          g.A = g.B = limb0;
+          g.s0 = nm;
+          g.s_rows = ns;
+          int64_t slots = nbk;
+          if (fblk0 < nb) {
+            g.fsel = 1;
+            g.fblk0 = (int32_t)fblk0;
+            slots = 2 * fblk0;
+          }
+          TimedScope t8(h, "topk_all_waves_i8");
+          if ((rc = launch_big(h, cfg, g, 1, slots))) return rc;
+        }
+      }
     }
     // 4. final lists -> outputs
     if ((rc = cand_compact(h, cb, nm, ns, 0, k))) return rc;

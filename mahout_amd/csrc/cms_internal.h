@@ -87,6 +87,8 @@ struct cms_handle {
     int64_t rows = 0;        // virtual rows in buf
     cms::DevBuf buf;
   } vl[2];
+  int64_t n_f4 = 0;     // single-limb owners whose counters are all <= 4 (fp4-exact)
+  int64_t f4_pos0 = 0;  // first permuted position of the fp4 image (ws_f4); n if none
   bool vl_ok = false;           // every multi-limb owner fits 4 limbs (else the legacy 128x128 path)
   int64_t topk_redo = 0;        // top-k rows the sampled threshold missed (radix-select redo)
   std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
@@ -98,7 +100,7 @@ struct cms_handle {
   cms::DevBuf ws_p1_row, ws_p1_key, ws_p1_val;   // pass-1 partition output
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
-  cms::DevBuf ws_query, ws_out, ws_srow;
+  cms::DevBuf ws_query, ws_out, ws_srow, ws_f4;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 
   // communicator

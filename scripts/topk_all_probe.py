@@ -29,7 +29,8 @@ t.reset_timing()
 t0 = time.perf_counter()
 ids, sc, cnt = t.top_k_all(k)
 wall = time.perf_counter() - t0
-tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves", "cosine_mfma",
+tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves",
+                                           "topk_all_waves_i8", "topk_all_waves_f4", "cand_compact", "cosine_mfma",
                                            "cosine_mfma_limbs", "cosine_mfma_multi", "top_k"]}
 st = t.stats()
 nm = st["multi_limb_owners"]

@@ -341,6 +341,8 @@ def test_top_k_heavy_ties(oracle):
     (1800, 3, 256, 1, 64, True, 53),      # weighted: every score is +-1, ties by ID everywhere
     (700, 5, 512, 2, 5, False, 54),       # fewer than one 256-row block pair per wave
     (11776, 3, 128, 2, 20, False, 55),    # 46 blocks: multi-wave bands and the half wave
+    (12000, 4, 256, 2, 25, False, 56),    # fp4 blocks beside int8 blocks over multi-wave bands
+    (5000, 2, 512, 1, 200, False, 57),    # mostly fp4 owners, long lists
 ])
 def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed):
     """cms_top_k_all (each unordered pair computed once, streamed into both
@@ -353,8 +355,8 @@ def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed)
         t.ingest(items, users, vals)
         t.finalize()
         ids, sc, cnt = t.top_k_all(k)
+        assert t.stats()["topk_redo"] == 0  # no candidate list overflowed
         rids, rsc, rcnt = t.top_k_rows(0, n, k)
-        assert t.stats()["topk_redo"] == 0
         assert np.array_equal(cnt, rcnt)
         for q in range(n):
             assert ids[q, :cnt[q]].tolist() == rids[q, :rcnt[q]].tolist(), q
@@ -366,6 +368,8 @@ def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed)
             assert same(sc[q, :cnt[q]], esc), q
         if vmax > 1:
             assert t.stats()["multi_limb_owners"] > 0
+        if w % 256 == 0:
+            assert t.stats()["fp4_owners"] > 0
 
 
 @pytest.mark.parametrize("weighted,capper", [(False, None), (False, (1.0, 4.5)), (True, (1.0, 5.0))])
