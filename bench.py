@@ -118,6 +118,7 @@ def pmc_traffic(kernel):
 
 
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense peak), MI355X_MICROARCH.md
+FP4_MFMA_PEAK_TOPS = 10000.0  # dense fp4 (e2m1) MFMA, MI355X_MICROARCH.md (FP6/FP4 ~10 PF dense)
 
 
 def allpairs_measure(table, row_begin, row_count, k, n, d, w):
@@ -231,6 +232,8 @@ def cosine_1m(args, local, device, rank=0, world=1):
     tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves",
                                                "topk_allgather", "topk_merge"]}
     waves_ms, waves_n = t.timing("topk_all_waves")
+    f4_ms, f4_n = t.timing("topk_all_waves_f4")
+    i8_ms, i8_n = t.timing("topk_all_waves_i8")
     t.set_timing(False)
     st = t.stats()
     stream = None
@@ -240,7 +243,17 @@ def cosine_1m(args, local, device, rank=0, world=1):
     uniq = n * (n - 1) / 2
     alg_ops = uniq * 2 * d * w  # F = n(n-1)/2 * 2dw
     ns = n - nm
+    nf = max(0, int(st["fp4_owners"]))
     wave_ops = ns * (ns - 1) / 2 * 2 * d * w / world  # this rank's share of the waves
+    # the waves feed two datatypes: fp4 x fp4 block pairs (owners whose
+    # counters are all <= 4) on the fp4 MFMA, the rest on int8; each share is
+    # priced at its own dense peak, so `peak` is the mix's ideal rate
+    f4_ops = nf * (nf - 1) / 2 * 2 * d * w / world
+    i8_ops = wave_ops - f4_ops
+    wave_peak = wave_ops / (f4_ops / FP4_MFMA_PEAK_TOPS + i8_ops / INT8_MFMA_PEAK_TOPS) if wave_ops else None
+    job_f4 = nf * (nf - 1) / 2 * 2 * d * w
+    job_peak = alg_ops / (job_f4 / FP4_MFMA_PEAK_TOPS + (alg_ops - job_f4) / INT8_MFMA_PEAK_TOPS)
+    wave_ach = wave_ops / (waves_ms * 1e-3) / 1e12 if waves_ms else None
     t.close()
     return {
         "workload": f"configs 3+4: {npairs}-pair Zipf stream -> {n}-item table (d={d} w={w}), user-hash sharded over "
@@ -250,12 +263,25 @@ def cosine_1m(args, local, device, rank=0, world=1):
         "wall_s": wall,
         "algorithmic_TOPS": alg_ops / wall / 1e12,
         "frac_int8_peak_per_gpu": alg_ops / wall / 1e12 / INT8_MFMA_PEAK_TOPS / world,
-        "roofline": {"bound": "mfma", "kernel": "k_cosine_big<3,1,128> (symmetric waves)",
-                     "achieved": wave_ops / (waves_ms * 1e-3) / 1e12 if waves_ms else None,
-                     "peak": INT8_MFMA_PEAK_TOPS, "unit": "TOP/s",
-                     "frac": wave_ops / (waves_ms * 1e-3) / 1e12 / INT8_MFMA_PEAK_TOPS if waves_ms else None,
+        "mixed_peak_TOPS": job_peak,
+        "frac_mixed_peak_per_gpu": alg_ops / wall / 1e12 / job_peak / world,
+        "roofline": {"bound": "mfma", "kernel": "k_cosine_big (symmetric waves: fp4 + int8 operands)",
+                     "achieved": wave_ach,
+                     "peak": wave_peak, "unit": "TOP/s",
+                     "peak_basis": f"fp4 {FP4_MFMA_PEAK_TOPS:.0f} TOP/s for the fp4 x fp4 pairs, int8 "
+                                   f"{INT8_MFMA_PEAK_TOPS:.0f} TOP/s for the rest, weighted by their ops",
+                     "frac": wave_ach / wave_peak if wave_ach and wave_peak else None,
                      "avg_launch_ms": waves_ms / waves_n if waves_n else None,
-                     "algorithmic_ops_per_launch": wave_ops / waves_n if waves_n else None},
+                     "algorithmic_ops_per_launch": wave_ops / waves_n if waves_n else None,
+                     "fp4_waves": {"ops": f4_ops, "ms": f4_ms, "launches": f4_n,
+                                   "TOPS": f4_ops / (f4_ms * 1e-3) / 1e12 if f4_ms else None,
+                                   "frac_fp4_peak": f4_ops / (f4_ms * 1e-3) / 1e12 / FP4_MFMA_PEAK_TOPS
+                                   if f4_ms else None},
+                     "int8_waves": {"ops": i8_ops, "ms": i8_ms, "launches": i8_n,
+                                    "TOPS": i8_ops / (i8_ms * 1e-3) / 1e12 if i8_ms else None,
+                                    "frac_int8_peak": i8_ops / (i8_ms * 1e-3) / 1e12 / INT8_MFMA_PEAK_TOPS
+                                    if i8_ms else None}},
+        "fp4_owners": nf,
         "timing_ms_rank0": tm,
         "multi_limb_owners": nm, "full_lists": int((cnt == k).sum()), "topk_redo_rows": int(st["topk_redo"]),
         "config3_ingest_merge_s": ingest_s,
