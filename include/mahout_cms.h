@@ -42,7 +42,7 @@ extern "C" {
 
 /* ---- status codes (mapped to Java exceptions by the JNI shim) ---------- */
 #define CMS_OK 0
-#define CMS_E_PARAM 1      /* IllegalArgumentException / CMException (AbstractCountMinSketch.java:170-175) */
+#define CMS_E_PARAM 1      /* IllegalArgumentException / CMException (AbstractCountMinSketch.java:71-76) */
 #define CMS_E_SHAPE 2      /* checkArgument w/d mismatch (DoubleCountMinSketch.java:117-118) */
 #define CMS_E_NO_SUCH_ID 3 /* NoSuchUserException / NoSuchItemException (GenericDataModel.java:210-215) */
 #define CMS_E_STATE 4      /* call-order violation (query before finalize, ...) */
@@ -60,10 +60,10 @@ extern "C" {
 
 typedef struct cms_params {
   uint32_t struct_size; /* = sizeof(cms_params); filled by cms_params_init */
-  int32_t depth;        /* d, 1..32 (AbstractCountMinSketch.java:155-157) */
+  int32_t depth;        /* d, 1..32 (AbstractCountMinSketch.java:34-44 init; bound of this build) */
   int32_t width;        /* w, 1..2^20 */
   int32_t counter_type; /* CMS_COUNTER_* */
-  int64_t seed;         /* HashFunctionBuilder(long seed) (HashFunctionBuilder.java:59) */
+  int64_t seed;         /* HashFunctionBuilder(long seed) (HashFunctionBuilder.java:23) */
   int64_t num_owners;   /* n: rows of the sketch table */
   int32_t weighting;    /* CMS_UNWEIGHTED | CMS_WEIGHTED (CosineCM.java:33) */
   int32_t device;       /* HIP device ordinal; -1 = current device */
@@ -75,7 +75,7 @@ typedef struct cms_handle cms_handle;
 int cms_params_init(cms_params* p);
 
 /* AbstractCountMinSketch(double delta, double epsilon, ...) shape rule
- * (T/impl/common/AbstractCountMinSketch.java:168-182): w = ceil(e/eps),
+ * (T/impl/common/AbstractCountMinSketch.java:69-83): w = ceil(e/eps),
  * d = ceil(ln(1/delta)); CMS_E_PARAM for the CMException ranges. */
 int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, int32_t* depth);
 
@@ -93,7 +93,7 @@ int cms_abi_version(void);
 int cms_set_owner_ids(cms_handle* h, const int64_t* ids, int64_t n);
 
 /* The d hash parameters (a_i, b_i) of HashFunctionBuilder(seed)
- * (HashFunctionBuilder.java:76-97). */
+ * (HashFunctionBuilder.java:40-61). */
 int cms_hash_params(cms_handle* h, int64_t* a, int64_t* b);
 
 /* HashFunction.hash(key) for every row i < d, computed on the GPU

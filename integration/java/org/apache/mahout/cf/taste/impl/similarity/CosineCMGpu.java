@@ -46,7 +46,7 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
 
   /**
    * @param hfBuilderSeed the seed a HashFunctionBuilder(seed) would be built with
-   *        (HashFunctionBuilder.java:59); the same seed gives the same buckets
+   *        (HashFunctionBuilder.java:23); the same seed gives the same buckets
    */
   public CosineCMGpu(DataModel dataModel, int depth, int width, long hfBuilderSeed, Weighting weighting, int device)
       throws TasteException {

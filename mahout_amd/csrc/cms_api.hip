@@ -65,7 +65,7 @@ TimedScope::~TimedScope() {
   h->pending.push_back(PendingEvent{name, start, stop});
 }
 
-// java.util.Random restated for HashFunctionBuilder (HashFunctionBuilder.java:59-97):
+// java.util.Random restated for HashFunctionBuilder (HashFunctionBuilder.java:23-61):
 // (a_i, b_i) = (Math.abs(nextLong()), Math.abs(nextLong())) for i = 0..d-1.
 static void java_hash_params(int64_t seed, int depth, int64_t* a, int64_t* b) {
   const uint64_t mult = 0x5DEECE66DULL, add = 0xBULL, mask = (1ULL << 48) - 1;

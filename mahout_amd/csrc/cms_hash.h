@@ -1,7 +1,7 @@
 // cms_hash.h -- exact count-min-sketch hash for gfx950 (and the host).
 //
 // Restates HashFunction.hash (T/impl/common/HashFunction.java:31-34):
-//     ((a * key + b) mod p) mod w,   p = 2^63 - 25  (HashFunctionBuilder.java:60)
+//     ((a * key + b) mod p) mod w,   p = 2^63 - 25  (HashFunctionBuilder.java:24)
 // evaluated by the reference in java.math.BigInteger (non-negative mod).
 //
 // The GPU form never builds a 128-bit signed value: a, b and key are reduced

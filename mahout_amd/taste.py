@@ -38,7 +38,7 @@ class Weighting:
 
 
 class HashFunctionBuilder:
-    """HashFunctionBuilder(long seed) (T/impl/common/HashFunctionBuilder.java:59-65)."""
+    """HashFunctionBuilder(long seed) (T/impl/common/HashFunctionBuilder.java:23-29)."""
 
     def __init__(self, seed):
         self.seed = int(seed)

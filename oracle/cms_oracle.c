@@ -16,7 +16,7 @@
 /* ------------------------------------------------------------------------ */
 /* java.util.Random: 48-bit LCG, multiplier 0x5DEECE66D, addend 0xB.          */
 /* Restated from the JDK's published algorithm (third-party, not under        */
-/* /root/reference; used at T/impl/common/HashFunctionBuilder.java:63,82-83). */
+/* /root/reference; used at T/impl/common/HashFunctionBuilder.java:27,46-47). */
 /* ------------------------------------------------------------------------ */
 #define JR_MULT 0x5DEECE66DULL
 #define JR_ADD 0xBULL
@@ -44,7 +44,7 @@ int64_t orc_jrandom_next_long(orc_jrandom* r) {
 static int64_t java_abs_long(int64_t v) { return v < 0 ? (int64_t)(0 - (uint64_t)v) : v; }
 
 /* HashFunctionBuilder(seed) + getHashFunction(i, w) for i = 0..d-1:
- * T/impl/common/HashFunctionBuilder.java:59-65 (Random(seed)), :80-88 (lazy
+ * T/impl/common/HashFunctionBuilder.java:23-29 (Random(seed)), :42-56 (lazy
  * (a_i, b_i) = (abs(nextLong), abs(nextLong)) in row order).  The parameters
  * depend only on the row index (w enters at hash time, :93). */
 void orc_hash_params(int64_t seed, int32_t depth, int64_t* a, int64_t* b) {
@@ -58,7 +58,7 @@ void orc_hash_params(int64_t seed, int32_t depth, int64_t* a, int64_t* b) {
 
 /* HashFunction.hash (T/impl/common/HashFunction.java:31-34):
  * a.multiply(k).add(b).mod(p).mod(w).intValue(), p = 2^63-25
- * (HashFunctionBuilder.java:60).  BigInteger.mod is non-negative. */
+ * (HashFunctionBuilder.java:24).  BigInteger.mod is non-negative. */
 #define ORC_PRIME 9223372036854775783LL
 int32_t orc_hash(int64_t a, int64_t b, int32_t width, int64_t key) {
   __int128 x = (__int128)a * (__int128)key + (__int128)b;
@@ -73,7 +73,7 @@ void orc_hash_many(const int64_t* a, const int64_t* b, int32_t depth, int32_t wi
     for (int32_t r = 0; r < depth; r++) out[i * depth + r] = orc_hash(a[r], b[r], width, keys[i]);
 }
 
-/* AbstractCountMinSketch(delta, epsilon) (T/impl/common/AbstractCountMinSketch.java:168-182) */
+/* AbstractCountMinSketch(delta, epsilon) (T/impl/common/AbstractCountMinSketch.java:69-83) */
 int orc_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, int32_t* depth) {
   if (delta <= 0 || delta > exp(-1.0)) return -1;
   if (epsilon <= 0 || epsilon > exp(1.0)) return -1;
@@ -263,20 +263,20 @@ int32_t orc_top_users(const int64_t* ids, const double* scores, int64_t n, int32
   return size;
 }
 
-/* CountMinSketchConfig.probaInserted (T/impl/common/CountMinSketchConfig.java:268-276) */
+/* CountMinSketchConfig.probaInserted (T/impl/common/CountMinSketchConfig.java:170-178) */
 double orc_proba_inserted(int32_t w, int32_t d, int32_t n, int32_t u) {
   double W = w, D = d, N = n, U = u;
   double falseP = pow(1 - pow(1 - 1 / W, N), D);
   return N / (N + falseP * (U - N));
 }
 
-/* probaNotExactRetrieve (:288-294) */
+/* probaNotExactRetrieve (:190-196) */
 double orc_proba_not_exact_retrieve(int32_t w, int32_t d, int32_t n) {
   double W = w, D = d, N = n;
   return pow(1 - pow(1 - 1 / W, N), D);
 }
 
-/* Fmeasure (:308-317) */
+/* Fmeasure (:210-219) */
 double orc_fmeasure(int32_t w, int32_t d, int32_t n, int32_t u, double q) {
   double beta = 1 - orc_proba_not_exact_retrieve(w, d, n);
   double p = 1 - orc_proba_inserted(w, d, n, u);
@@ -285,7 +285,7 @@ double orc_fmeasure(int32_t w, int32_t d, int32_t n, int32_t u, double q) {
   return (1 + 2) * beta * p / (q2 * beta + p);
 }
 
-/* computeConfig inner search for one owner (:226-250): d in [1,25), w in [d,n],
+/* computeConfig inner search for one owner (:120-158): d in [1,25), w in [d,n],
  * ties to the LAST maximiser (>=). */
 int orc_compute_config(int32_t n, int32_t u, double q, int32_t* best_w, int32_t* best_d,
                        double* delta, double* epsilon) {

@@ -30,7 +30,7 @@ void    orc_jrandom_init(orc_jrandom* r, int64_t seed);
 int32_t orc_jrandom_next_int(orc_jrandom* r);
 int64_t orc_jrandom_next_long(orc_jrandom* r);
 
-/* T/impl/common/HashFunctionBuilder.java:59-97 */
+/* T/impl/common/HashFunctionBuilder.java:23-61 */
 void orc_hash_params(int64_t seed, int32_t depth, int64_t* a, int64_t* b);
 
 /* T/impl/common/HashFunction.java:31-34 */
@@ -38,7 +38,7 @@ int32_t orc_hash(int64_t a, int64_t b, int32_t width, int64_t key);
 void orc_hash_many(const int64_t* a, const int64_t* b, int32_t depth, int32_t width,
                    const int64_t* keys, int64_t n, int32_t* out /* [n][depth] */);
 
-/* T/impl/common/AbstractCountMinSketch.java:168-182: (delta, epsilon) -> (w, d).
+/* T/impl/common/AbstractCountMinSketch.java:69-83: (delta, epsilon) -> (w, d).
  * Returns 0 on success, -1 for the CMException cases. */
 int orc_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, int32_t* depth);
 
@@ -87,7 +87,7 @@ float orc_estimate_preference(const double* table, int32_t depth, int32_t width,
 int32_t orc_top_users(const int64_t* ids, const double* scores, int64_t n, int32_t k,
                       int64_t* out_ids, double* out_scores);
 
-/* CountMinSketchConfig (T/impl/common/CountMinSketchConfig.java:268-317, 218-256) */
+/* CountMinSketchConfig (T/impl/common/CountMinSketchConfig.java:120-158, 170-219) */
 double orc_proba_inserted(int32_t w, int32_t d, int32_t n, int32_t u);
 double orc_proba_not_exact_retrieve(int32_t w, int32_t d, int32_t n);
 double orc_fmeasure(int32_t w, int32_t d, int32_t n, int32_t u, double q);

@@ -13,7 +13,7 @@ T/ = mr/src/main/java/org/apache/mahout/cf/taste/ under the reference.
 MULT = 0x5DEECE66D
 ADD = 0xB
 MASK = (1 << 48) - 1
-PRIME = 9223372036854775783  # T/impl/common/HashFunctionBuilder.java:60 (2^63 - 25)
+PRIME = 9223372036854775783  # T/impl/common/HashFunctionBuilder.java:24 (2^63 - 25)
 
 
 def _to_int(v: int, bits: int) -> int:
@@ -45,7 +45,7 @@ def java_abs_long(v: int) -> int:
 
 def hash_params(seed: int, depth: int):
     """HashFunctionBuilder(seed).getHashFunction(i, w) params, i < depth
-    (T/impl/common/HashFunctionBuilder.java:59-65, 80-88)."""
+    (T/impl/common/HashFunctionBuilder.java:23-29, 42-56)."""
     r = JavaRandom(seed)
     a, b = [], []
     for _ in range(depth):

@@ -4,7 +4,7 @@ Provenance of every value (the reference is Java; no JDK exists in this
 image and no reference test exercises the sketch path):
 
   jdk_random      published java.util.Random known answers (JDK behaviour the
-                  reference relies on at HashFunctionBuilder.java:63,82-83);
+                  reference relies on at HashFunctionBuilder.java:27,46-47);
                   NOT derived from the oracle -- they pin it.
   reference_kats  known answers held by the reference's own tests for the
                   exact cosine the sketch reproduces when it is collision
