@@ -51,6 +51,8 @@ extern "C" {
 #define CMS_E_HIP 7        /* HIP runtime error */
 #define CMS_E_RCCL 8       /* RCCL error */
 #define CMS_E_OOM 9        /* device or host allocation failed */
+#define CMS_E_SKETCH 10    /* TasteException: CMException inside exportProfile (CosineCM.java:45-46) or no
+                              configuration solution (CountMinSketchConfig.java:145-147) */
 
 /* ---- parameters ----------------------------------------------------------- */
 #define CMS_COUNTER_U32 0 /* exact integer counters (non-negative integer increments) */
@@ -211,6 +213,43 @@ int cms_format_java_double(double v, char* buf, int32_t cap);
 /* Counters of rows [row_begin, row_begin+row_count) as fp64 (the reference's
  * counter type), [row_count][d][w]. */
 int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out);
+
+/* ---- per-owner sketch shapes: CosineCM with its CountMinSketchConfig --------
+ * The reference sizes every owner's sketch separately.  CountMinSketchConfig
+ * (T/impl/common/CountMinSketchConfig.java:120-158) picks (d, w) per owner and
+ * stores delta = exp(-d), epsilon = e/w; CosineCM.userSimilarity(u1, u2)
+ * builds u1's sketch with u2's (delta, epsilon) and compares it with u2's own
+ * cached sketch (T/impl/similarity/CosineCM.java:60-67,83-96), so the
+ * similarity is asymmetric.  A per-owner handle keeps the DataModel (one
+ * cms_ingest_csr / cms_ingest_csr_device call; a later call replaces it)
+ * resident on the GPU; cms_finalize builds every owner's own sketch, and the
+ * similarity kernels hash u1's preferences at u2's shape on the fly.
+ * p->depth / p->width are ignored.  cms_similarity(ies), cms_point_query,
+ * cms_estimate_preferences, cms_most_similar, cms_top_k_rows, cms_top_k_all
+ * and cms_write_similar_items work as for fixed shapes; the COO ingests,
+ * cms_read_counters, cms_hash_keys, cms_top_k_all_partial and cms_comm_init
+ * return CMS_E_STATE (per-owner mode is single-GPU). */
+int cms_create_per_owner(const cms_params* p, cms_handle** out);
+/* CountMinSketchConfig(q).configure(dataModel) -> computeConfig on the GPU:
+ * per owner n = its CSR row length (PreferenceArray.length()), u = num_keys
+ * (dataModel.getNumItems()); maximise Fmeasure(w, d, n, u, q) (:210-219) over
+ * d in [1, 25), w in [d, n], ties to the last (>=, :137); delta = exp(-d),
+ * epsilon = e/w.  Needs the DataModel first.  CMS_E_SKETCH for an owner with
+ * no solution (the TasteException of :145-147). */
+int cms_configure_owner_shapes(cms_handle* h, double q, int64_t num_keys);
+/* Caller-supplied configuration: the getDelta(id) / getEpsilon(id) values of
+ * a CountMinSketchConfig (:230-251), in owner-row order.  An owner whose pair
+ * is outside the CMException ranges (AbstractCountMinSketch.java:71-76; e.g.
+ * the 0.0 trove returns for a missing owner) fails, with CMS_E_SKETCH, exactly
+ * the calls that need its shape with CMS_E_SKETCH (exportProfile, CosineCM.java:41-58).  Shapes
+ * beyond this build (depth > 32, width > 2^24) are refused here. */
+int cms_set_owner_delta_epsilon(cms_handle* h, const double* delta, const double* epsilon);
+/* The configuration and the shape new DoubleCountMinSketch(delta, epsilon, ...)
+ * derives from it (width = depth = 0: CMException).  Outputs may be NULL. */
+int cms_get_owner_shapes(cms_handle* h, double* delta, double* epsilon, int32_t* width, int32_t* depth);
+/* getExportedCMProfile(id) (CosineCM.java:60-67): the owner's own sketch as
+ * fp64 [depth][width] (capacity in doubles; out NULL returns the shape only). */
+int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capacity, int32_t* width, int32_t* depth);
 
 /* ---- instrumentation ------------------------------------------------------- */
 typedef struct cms_stats {

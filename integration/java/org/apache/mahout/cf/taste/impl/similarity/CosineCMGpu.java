@@ -7,9 +7,11 @@
  * NOTE: written against the reference's Taste interfaces; no JDK exists in
  * the build image, so this file is not compiled here (see INTEGRATION.md).
  *
- * Shape: every owner gets the same (depth, width) -- the fixed-shape configs
- * of this path.  The reference's per-owner (delta, epsilon) sizing
- * (CountMinSketchConfig) is not carried over yet.
+ * Shape: either every owner gets the same (depth, width) -- the fixed-shape
+ * configs of this path -- or, as the reference does, each owner is sized by a
+ * CountMinSketchConfig (per-owner (delta, epsilon); CosineCM.java:26-39,83-96):
+ * the config's getDelta/getEpsilon values are handed to the library once, or
+ * the Fmeasure search itself runs on the GPU (the q constructor).
  */
 package org.apache.mahout.cf.taste.impl.similarity;
 
@@ -20,6 +22,7 @@ import org.apache.mahout.cf.taste.common.NoSuchUserException;
 import org.apache.mahout.cf.taste.common.Refreshable;
 import org.apache.mahout.cf.taste.common.TasteException;
 import org.apache.mahout.cf.taste.common.Weighting;
+import org.apache.mahout.cf.taste.impl.common.CountMinSketchConfig;
 import org.apache.mahout.cf.taste.impl.common.LongPrimitiveIterator;
 import org.apache.mahout.cf.taste.model.DataModel;
 import org.apache.mahout.cf.taste.model.PreferenceArray;
@@ -39,6 +42,8 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
 
   private final int depth;
   private final int width;
+  private final CountMinSketchConfig config;  // per-owner shapes from the caller's config, or null
+  private final double q;                     // per-owner shapes searched on the GPU (NaN: not used)
   private final long seed;
   private final boolean weighted;
   private final int device;
@@ -56,10 +61,57 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     }
     this.depth = depth;
     this.width = width;
+    this.config = null;
+    this.q = Double.NaN;
     this.seed = hfBuilderSeed;
     this.weighted = weighting == Weighting.WEIGHTED;
     this.device = device;
     build();
+  }
+
+  /**
+   * The reference's CosineCM(dataModel, weighting, conf, hfBuilder) (CosineCM.java:33-39):
+   * each owner's sketch is sized by conf.getDelta/getEpsilon (the caller has run
+   * conf.configure(dataModel, name) as before, or loaded its ser/ cache).
+   */
+  public CosineCMGpu(DataModel dataModel, Weighting weighting, CountMinSketchConfig conf, long hfBuilderSeed,
+                     int device) throws TasteException {
+    super(dataModel);
+    if (!dataModel.hasPreferenceValues()) {  // CosineCM.java:38
+      throw new IllegalArgumentException("DataModel doesn't have preference values");
+    }
+    this.depth = 0;
+    this.width = 0;
+    this.config = conf;
+    this.q = Double.NaN;
+    this.seed = hfBuilderSeed;
+    this.weighted = weighting == Weighting.WEIGHTED;
+    this.device = device;
+    build();
+  }
+
+  /**
+   * Per-owner shapes with CountMinSketchConfig(q)'s Fmeasure search
+   * (CountMinSketchConfig.java:120-158) run on the GPU instead of the JVM.
+   */
+  public CosineCMGpu(DataModel dataModel, Weighting weighting, double q, long hfBuilderSeed, int device)
+      throws TasteException {
+    super(dataModel);
+    if (!dataModel.hasPreferenceValues()) {  // CosineCM.java:38
+      throw new IllegalArgumentException("DataModel doesn't have preference values");
+    }
+    this.depth = 0;
+    this.width = 0;
+    this.config = null;
+    this.q = q;
+    this.seed = hfBuilderSeed;
+    this.weighted = weighting == Weighting.WEIGHTED;
+    this.device = device;
+    build();
+  }
+
+  private boolean perOwner() {
+    return config != null || !Double.isNaN(q);
   }
 
   public CosineCMGpu(DataModel dataModel, int depth, int width, long hfBuilderSeed) throws TasteException {
@@ -91,10 +143,22 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
         vals[base + j] = prefs.getValue(j);
       }
     }
-    long h = nativeCreate(depth, width, seed, n, weighted, device);
+    long h = perOwner() ? nativeCreatePerOwner(seed, n, weighted, device)
+                        : nativeCreate(depth, width, seed, n, weighted, device);
     try {
       nativeSetOwnerIds(h, ids);
       nativeIngestCsr(h, offsets, keys, vals);
+      if (config != null) {
+        double[] delta = new double[n];
+        double[] epsilon = new double[n];
+        for (int i = 0; i < n; i++) {
+          delta[i] = config.getDelta(ids[i]);
+          epsilon[i] = config.getEpsilon(ids[i]);
+        }
+        nativeSetOwnerDeltaEpsilon(h, delta, epsilon);
+      } else if (perOwner()) {
+        nativeConfigureOwnerShapes(h, q, model.getNumItems());
+      }
       nativeFinalize(h);
     } catch (TasteException | RuntimeException e) {
       nativeDestroy(h);
@@ -182,12 +246,18 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
 
   @Override
   public String toString() {
-    return "CosineCMGpu[dataModel:" + getDataModel() + ",d:" + depth + ",w:" + width + ']';
+    return "CosineCMGpu[dataModel:" + getDataModel()
+        + (perOwner() ? ",per-owner shapes" : ",d:" + depth + ",w:" + width) + ']';
   }
 
   // --- JNI (integration/jni/mahout_cms_jni.c) --------------------------------
   private static native long nativeCreate(int depth, int width, long seed, long numOwners, boolean weighted,
                                           int device) throws TasteException;
+  private static native long nativeCreatePerOwner(long seed, long numOwners, boolean weighted, int device)
+      throws TasteException;
+  private static native void nativeConfigureOwnerShapes(long h, double q, long numKeys) throws TasteException;
+  private static native void nativeSetOwnerDeltaEpsilon(long h, double[] delta, double[] epsilon)
+      throws TasteException;
   private static native void nativeSetOwnerIds(long h, long[] ids) throws TasteException;
   private static native void nativeIngestCsr(long h, long[] offsets, long[] keys, float[] vals) throws TasteException;
   private static native void nativeFinalize(long h) throws TasteException;

@@ -52,6 +52,36 @@ JNIEXPORT jlong JNICALL JFN(nativeCreate)(JNIEnv* env, jclass c, jint depth, jin
   return (jlong)(intptr_t)h;
 }
 
+JNIEXPORT jlong JNICALL JFN(nativeCreatePerOwner)(JNIEnv* env, jclass c, jlong seed, jlong n, jboolean weighted,
+                                                  jint device) {
+  (void)c;
+  cms_params p;
+  cms_params_init(&p);
+  p.seed = seed;
+  p.num_owners = n;
+  p.weighting = weighted ? CMS_WEIGHTED : CMS_UNWEIGHTED;
+  p.device = device;
+  cms_handle* h = NULL;
+  if (fail(env, cms_create_per_owner(&p, &h), 0)) return 0;
+  return (jlong)(intptr_t)h;
+}
+
+JNIEXPORT void JNICALL JFN(nativeConfigureOwnerShapes)(JNIEnv* env, jclass c, jlong h, jdouble q, jlong num_keys) {
+  (void)c;
+  fail(env, cms_configure_owner_shapes(H(h), q, num_keys), 0);
+}
+
+JNIEXPORT void JNICALL JFN(nativeSetOwnerDeltaEpsilon)(JNIEnv* env, jclass c, jlong h, jdoubleArray delta,
+                                                       jdoubleArray epsilon) {
+  (void)c;
+  jdouble* pd = (*env)->GetPrimitiveArrayCritical(env, delta, NULL);
+  jdouble* pe = (*env)->GetPrimitiveArrayCritical(env, epsilon, NULL);
+  int rc = cms_set_owner_delta_epsilon(H(h), (const double*)pd, (const double*)pe);
+  (*env)->ReleasePrimitiveArrayCritical(env, epsilon, pe, JNI_ABORT);
+  (*env)->ReleasePrimitiveArrayCritical(env, delta, pd, JNI_ABORT);
+  fail(env, rc, 0);
+}
+
 JNIEXPORT void JNICALL JFN(nativeSetOwnerIds)(JNIEnv* env, jclass c, jlong h, jlongArray ids) {
   (void)c;
   jsize n = (*env)->GetArrayLength(env, ids);

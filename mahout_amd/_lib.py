@@ -21,6 +21,7 @@ CMS_E_OVERFLOW = 6
 CMS_E_HIP = 7
 CMS_E_RCCL = 8
 CMS_E_OOM = 9
+CMS_E_SKETCH = 10
 
 CMS_COUNTER_U32 = 0
 CMS_UNWEIGHTED = 0
@@ -35,6 +36,8 @@ EXPORTS = [
     "cms_comm_init", "cms_shard_of_key", "cms_finalize", "cms_synchronize", "cms_similarity", "cms_similarities",
     "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_top_k_all_partial", "cms_top_k_merge", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
+    "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
+    "cms_read_owner_sketch",
 ]
 
 
@@ -111,6 +114,11 @@ _SIGS = {
     "cms_set_timing": (_int, [_vp, _i32]),
     "cms_get_timing": (_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_dbl), ctypes.POINTER(_i64)]),
     "cms_reset_timing": (_int, [_vp]),
+    "cms_create_per_owner": (_int, [ctypes.POINTER(CmsParams), ctypes.POINTER(_vp)]),
+    "cms_configure_owner_shapes": (_int, [_vp, _dbl, _i64]),
+    "cms_set_owner_delta_epsilon": (_int, [_vp, _vp, _vp]),
+    "cms_get_owner_shapes": (_int, [_vp, _vp, _vp, _vp, _vp]),
+    "cms_read_owner_sketch": (_int, [_vp, _i64, _vp, _i64, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
 }
 
 _lib = None

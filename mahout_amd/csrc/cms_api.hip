@@ -134,6 +134,12 @@ struct Guard {
   ~Guard() { h->mu.unlock(); }
 };
 
+static int refuse_per_owner(cms_handle* h, const char* what) {
+  if (h->per_owner)
+    return set_error(CMS_E_STATE, "%s: not available on a per-owner-shape handle (cms_create_per_owner)", what);
+  return CMS_OK;
+}
+
 static int require_finalized(cms_handle* h) {
   if (!h->finalized) return set_error(CMS_E_STATE, "call cms_finalize before queries");
   return CMS_OK;
@@ -174,18 +180,26 @@ int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, i
   return CMS_OK;
 }
 
-int cms_create(const cms_params* p, cms_handle** out) {
+static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   if (!p || !out) return set_error(CMS_E_PARAM, "null argument");
   if (p->struct_size != sizeof(cms_params)) return set_error(CMS_E_PARAM, "cms_params ABI mismatch");
-  if (p->depth < 1 || p->depth > CMS_MAX_DEPTH) return set_error(CMS_E_PARAM, "depth must be in [1, %d]", CMS_MAX_DEPTH);
-  if (p->width < 1 || p->width > (1 << 15))
-    return set_error(CMS_E_PARAM, "width must be in [1, 32768] (LDS-staged sketch rows)");
+  if (!per_owner) {
+    if (p->depth < 1 || p->depth > CMS_MAX_DEPTH)
+      return set_error(CMS_E_PARAM, "depth must be in [1, %d]", CMS_MAX_DEPTH);
+    if (p->width < 1 || p->width > (1 << 15))
+      return set_error(CMS_E_PARAM, "width must be in [1, 32768] (LDS-staged sketch rows)");
+  }
   if (p->num_owners < 1 || p->num_owners > (int64_t(1) << 24))
     return set_error(CMS_E_PARAM, "num_owners must be in [1, 2^24]");
   if (p->counter_type != CMS_COUNTER_U32) return set_error(CMS_E_PARAM, "unsupported counter type");
   cms_handle* h = new (std::nothrow) cms_handle();
   if (!h) return set_error(CMS_E_OOM, "host allocation failed");
   h->p = *p;
+  h->per_owner = per_owner;
+  if (per_owner) {  // every owner may use up to CMS_MAX_DEPTH rows; no shared table
+    h->p.depth = CMS_MAX_DEPTH;
+    h->p.width = 1;
+  }
   int dev = p->device;
   if (dev < 0) {
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -198,25 +212,26 @@ int cms_create(const cms_params* p, cms_handle** out) {
   }
   h->n = p->num_owners;
   h->dw = (int64_t)p->depth * p->width;
-  java_hash_params(p->seed, p->depth, h->a, h->b);
+  java_hash_params(p->seed, h->p.depth, h->a, h->b);
   HashParams& hp = h->hp;
   std::memset(&hp, 0, sizeof(hp));
-  for (int i = 0; i < p->depth; ++i) {
+  for (int i = 0; i < h->p.depth; ++i) {
     hp.ap[i] = reduce_key(h->a[i]);
     hp.bp[i] = reduce_key(h->b[i]);
   }
-  hp.width = (uint32_t)p->width;
-  hp.depth = p->depth;
-  hp.pow2 = (p->width & (p->width - 1)) == 0;
-  hp.wmask = hp.pow2 ? (uint32_t)(p->width - 1) : 0u;
-  hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)p->width;
+  hp.width = (uint32_t)h->p.width;
+  hp.depth = h->p.depth;
+  hp.pow2 = (h->p.width & (h->p.width - 1)) == 0;
+  hp.wmask = hp.pow2 ? (uint32_t)(h->p.width - 1) : 0u;
+  hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)h->p.width;
+  if (per_owner) h->dw = 0;
 
   size_t tbytes = sizeof(uint32_t) * (size_t)h->n * (size_t)h->dw;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
-      (e = hipMalloc(&h->d_table, tbytes)) != hipSuccess ||
+      (!per_owner && (e = hipMalloc(&h->d_table, tbytes)) != hipSuccess) ||
       (e = hipMalloc(&h->d_row_mass, sizeof(uint64_t) * h->n)) != hipSuccess ||
-      (e = hipMalloc(&h->d_norm, sizeof(uint64_t) * h->n * p->depth)) != hipSuccess ||
-      (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess ||
+      (!per_owner && (e = hipMalloc(&h->d_norm, sizeof(uint64_t) * h->n * p->depth)) != hipSuccess) ||
+      (!per_owner && (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess) ||
       (e = hipMalloc(&h->d_rowmax, sizeof(uint32_t) * h->n)) != hipSuccess ||
       (e = hipMalloc(&h->d_flags, 64 * sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_flags, 0, 64 * sizeof(uint32_t))) != hipSuccess ||
@@ -230,6 +245,10 @@ int cms_create(const cms_params* p, cms_handle** out) {
   *out = h;
   return CMS_OK;
 }
+
+int cms_create(const cms_params* p, cms_handle** out) { return create_impl(p, false, out); }
+
+int cms_create_per_owner(const cms_params* p, cms_handle** out) { return create_impl(p, true, out); }
 
 void cms_destroy(cms_handle* h) {
   if (!h) return;
@@ -248,7 +267,8 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
-                  &h->ws_f4};
+                  &h->ws_f4, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
+                  &h->po_scratch};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -277,6 +297,7 @@ int cms_hash_params(cms_handle* h, int64_t* a, int64_t* b) {
 
 int cms_hash_keys(cms_handle* h, const int64_t* keys, int64_t n, int32_t* out) {
   if (!h || (n > 0 && (!keys || !out))) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "cms_hash_keys")) return rc0;
   if (n <= 0) return CMS_OK;
   Guard g(h);
   CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * n));
@@ -370,6 +391,7 @@ int dlog_exchange(cms_handle* h) {
 
 int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t n) {
   if (!h || (n > 0 && (!owner || !key))) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "COO ingest (per-owner mode takes the DataModel as CSR)")) return rc0;
   if (n <= 0) return CMS_OK;
   Guard g(h);
   CMS_HIP(h->ws_in_row.ensure(sizeof(int64_t) * n));
@@ -401,6 +423,7 @@ int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const fl
 
 int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n) {
   if (!h || (n > 0 && (!d_row || !d_key))) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "COO ingest (per-owner mode takes the DataModel as CSR)")) return rc0;
   if (n <= 0) return CMS_OK;
   Guard g(h);
   int rc = ingest_coo_device(h, d_row, d_key, d_val, n);
@@ -432,6 +455,18 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
   if (vals && np > 0)
     CMS_HIP(hipMemcpyAsync(h->ws_in_val.ptr, vals, sizeof(float) * np, hipMemcpyHostToDevice, h->stream));
   int rc;
+  if (h->per_owner) {  // the DataModel itself stays resident; sketches are built at finalize
+    rc = po_load_csr(h, h->ws_in_row.as<int64_t>(), h->ws_in_key.as<int64_t>(), vals ? h->ws_in_val.as<float>() : nullptr,
+                     np, offsets);
+    if (rc) return rc;
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    if ((rc = check_flags(h, false))) {
+      h->po_loaded = false;
+      return rc;
+    }
+    h->pairs_ingested = np;
+    return CMS_OK;
+  }
   if (vals && (rc = validate_batch(h, nullptr, h->ws_in_val.as<float>(), np))) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
   if ((rc = check_flags(h, false))) return rc;
@@ -453,6 +488,22 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
   int64_t np = 0;
   CMS_HIP(hipMemcpyAsync(&np, d_offsets + h->n, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
+  if (h->per_owner) {
+    std::vector<int64_t> off(h->n + 1);
+    CMS_HIP(hipMemcpy(off.data(), d_offsets, sizeof(int64_t) * (h->n + 1), hipMemcpyDeviceToHost));
+    if (off[0] != 0) return set_error(CMS_E_PARAM, "offsets[0] must be 0");
+    for (int64_t r = 0; r < h->n; ++r)
+      if (off[r + 1] < off[r]) return set_error(CMS_E_PARAM, "offsets must be non-decreasing");
+    int rc = po_load_csr(h, d_offsets, d_keys, d_vals, np, off.data());
+    if (rc) return rc;
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    if ((rc = check_flags(h, false))) {
+      h->po_loaded = false;
+      return rc;
+    }
+    h->pairs_ingested = np;
+    return CMS_OK;
+  }
   int rc = ingest_csr_device(h, d_offsets, d_keys, d_vals, np);
   if (rc == CMS_OK) {
     h->pairs_ingested += np;
@@ -464,6 +515,7 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
 int cms_reset(cms_handle* h) {
   if (!h) return set_error(CMS_E_PARAM, "null handle");
   Guard g(h);
+  h->po_loaded = false;
   CMS_HIP(hipMemsetAsync(h->d_row_mass, 0, sizeof(uint64_t) * h->n, h->stream));
   h->empty = true;
   h->norms_valid = false;
@@ -498,6 +550,7 @@ int cms_comm_unique_id(void* out) {
 int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t world) {
   if (!h || !unique_id) return set_error(CMS_E_PARAM, "null argument");
   if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
+  if (int rc0 = refuse_per_owner(h, "cms_comm_init")) return rc0;
   Guard g(h);
   if (h->comm) {
     (void)ncclCommDestroy(h->comm);
@@ -526,6 +579,13 @@ int32_t cms_shard_of_key(int64_t key, int32_t world) {
 int cms_finalize(cms_handle* h) {
   if (!h) return set_error(CMS_E_PARAM, "null handle");
   Guard g(h);
+  if (h->per_owner) {
+    int rc = po_finalize(h);
+    if (rc) return rc;
+    if ((rc = check_flags(h, false))) return rc;
+    h->finalized = true;
+    return CMS_OK;
+  }
   if (h->empty) {
     CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * h->n * h->dw, h->stream));
     h->empty = false;
@@ -577,10 +637,18 @@ int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n,
   std::vector<int64_t> rows(n);
   for (int64_t i = 0; i < n; ++i)
     if ((rc = row_of(h, ids2[i], &rows[i]))) return rc;
-  CMS_HIP(h->ws_query.ensure(sizeof(int64_t) * n));
+  CMS_HIP(h->ws_query.ensure(sizeof(int64_t) * (n + 1)));
   CMS_HIP(h->ws_small.ensure(sizeof(double) * n));
-  CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, rows.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
-  if ((rc = pair_cosines(h, q, h->ws_query.as<int64_t>(), n, h->ws_small.as<double>()))) return rc;
+  if (h->per_owner) {  // u2's shape decides each pair (CosineCM.java:86)
+    if ((rc = po_require_shapes(h, rows.data(), n))) return rc;
+    rows.push_back(q);
+    CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, rows.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+    rc = po_pair_cosines(h, h->ws_query.as<int64_t>() + n, 1, h->ws_query.as<int64_t>(), n, h->ws_small.as<double>());
+  } else {
+    CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, rows.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+    rc = pair_cosines(h, q, h->ws_query.as<int64_t>(), n, h->ws_small.as<double>());
+  }
+  if (rc) return rc;
   CMS_HIP(hipMemcpyAsync(out, h->ws_small.ptr, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
   return CMS_OK;
@@ -612,10 +680,25 @@ int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neig
   if (m > 0)
     CMS_HIP(hipMemcpyAsync(d_rows.ptr, rows.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, h->stream));
   CMS_HIP(hipMemcpyAsync(d_items.ptr, item_keys, sizeof(int64_t) * q, hipMemcpyHostToDevice, h->stream));
-  if ((rc = pair_cosines(h, urow, d_rows.as<int64_t>(), m, d_sims.as<double>()))) return rc;
-  if ((rc = estimate_preferences(h, urow, d_rows.as<int64_t>(), d_sims.as<double>(), m, d_items.as<int64_t>(), q,
-                                 use_capper, cap_min, cap_max, d_out.as<float>())))
-    return rc;
+  if (h->per_owner) {
+    std::vector<int64_t> others;  // every neighbour but the user needs its own profile (:154-156)
+    for (int64_t r : rows)
+      if (r != urow) others.push_back(r);
+    if ((rc = po_require_shapes(h, others.data(), (int64_t)others.size()))) return rc;
+    DevBuf d_u;
+    CMS_HIP(d_u.ensure(sizeof(int64_t)));
+    CMS_HIP(hipMemcpyAsync(d_u.ptr, &urow, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+    if ((rc = po_pair_cosines(h, d_u.as<int64_t>(), 1, d_rows.as<int64_t>(), m, d_sims.as<double>()))) return rc;
+    rc = po_estimate_preferences(h, urow, d_rows.as<int64_t>(), d_sims.as<double>(), m, d_items.as<int64_t>(), q,
+                                 use_capper, cap_min, cap_max, d_out.as<float>());
+    if (rc == CMS_OK) rc = hipStreamSynchronize(h->stream) == hipSuccess ? CMS_OK : set_error(CMS_E_HIP, "estimate");
+    if (rc) return rc;
+  } else {
+    if ((rc = pair_cosines(h, urow, d_rows.as<int64_t>(), m, d_sims.as<double>()))) return rc;
+    if ((rc = estimate_preferences(h, urow, d_rows.as<int64_t>(), d_sims.as<double>(), m, d_items.as<int64_t>(), q,
+                                   use_capper, cap_min, cap_max, d_out.as<float>())))
+      return rc;
+  }
   CMS_HIP(hipMemcpyAsync(out, d_out.ptr, sizeof(float) * q, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
   return CMS_OK;
@@ -631,7 +714,13 @@ int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out) {
   CMS_HIP(h->ws_query.ensure(sizeof(int64_t)));
   CMS_HIP(h->ws_small.ensure(sizeof(double)));
   CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, &key, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-  if ((rc = point_queries(h, row, h->ws_query.as<int64_t>(), 1, h->ws_small.as<double>()))) return rc;
+  if (h->per_owner) {
+    if ((rc = po_require_shapes(h, &row, 1))) return rc;
+    rc = po_point_queries(h, row, h->ws_query.as<int64_t>(), 1, h->ws_small.as<double>());
+  } else {
+    rc = point_queries(h, row, h->ws_query.as<int64_t>(), 1, h->ws_small.as<double>());
+  }
+  if (rc) return rc;
   CMS_HIP(hipMemcpyAsync(out, h->ws_small.ptr, sizeof(double), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
   return CMS_OK;
@@ -737,6 +826,7 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
 int cms_top_k_all_partial(cms_handle* h, int32_t k, int32_t shard, int32_t nshards, int64_t* ids, double* scores,
                           int32_t* counts) {
   if (!h || !ids || !scores || !counts) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "cms_top_k_all_partial")) return rc0;
   if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
   if (nshards < 1 || shard < 0 || shard >= nshards) return set_error(CMS_E_PARAM, "shard %d of %d", shard, nshards);
   Guard g(h);
@@ -800,6 +890,7 @@ int cms_format_java_double(double v, char* buf, int32_t cap) {
 
 int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "cms_read_counters (use cms_read_owner_sketch)")) return rc0;
   Guard g(h);
   if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
   size_t cnt = (size_t)(row_count * h->dw);
@@ -814,16 +905,38 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
   return CMS_OK;
 }
 
+int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capacity, int32_t* width, int32_t* depth) {
+  if (!h) return set_error(CMS_E_PARAM, "null argument");
+  if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: use cms_read_counters");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  int64_t row;
+  if ((rc = row_of(h, id, &row))) return rc;
+  if ((rc = po_require_shapes(h, &row, 1))) return rc;
+  const int64_t w = h->h_po_w[row], d = h->h_po_d[row];
+  if (width) *width = (int32_t)w;
+  if (depth) *depth = (int32_t)d;
+  if (!out) return CMS_OK;
+  if (capacity < w * d) return set_error(CMS_E_PARAM, "capacity %lld < %lld counters", (long long)capacity, (long long)(w * d));
+  int64_t soff = 0;
+  for (int64_t r = 0; r < row; ++r) soff += (int64_t)h->h_po_w[r] * h->h_po_d[r];
+  std::vector<uint32_t> tmp(w * d);
+  CMS_HIP(hipMemcpy(tmp.data(), h->po_sk.as<uint32_t>() + soff, sizeof(uint32_t) * w * d, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < w * d; ++i) out[i] = (double)tmp[i];
+  return CMS_OK;
+}
+
 int cms_get_stats(cms_handle* h, cms_stats* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
   out->pairs_ingested = h->pairs_ingested;
   out->num_owners = h->n;
-  out->depth = h->p.depth;
-  out->width = h->p.width;
+  out->depth = h->per_owner ? h->po_max_d : h->p.depth;
+  out->width = h->per_owner ? h->po_max_w : h->p.width;
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
-  out->table_bytes = (int64_t)sizeof(uint32_t) * h->n * h->dw;
+  out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes : (int64_t)sizeof(uint32_t) * h->n * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;

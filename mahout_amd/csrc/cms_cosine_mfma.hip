@@ -1162,6 +1162,10 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
 // (top_k_merge) gives the exact result.  nshards == 1 is the whole job.
 int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts, int32_t shard,
               int32_t nshards) {
+  if (h->per_owner) {  // asymmetric similarities: every row scans every candidate
+    if (nshards != 1) return set_error(CMS_E_STATE, "per-owner shapes: all-pairs top-k is single-GPU");
+    return top_k_rows(h, 0, h->n, k, d_ids, d_scores, d_counts);
+  }
   int rc = cosine_prepare(h);
   if (rc) return rc;
   const int64_t n = h->n;

@@ -82,4 +82,24 @@ __device__ __forceinline__ uint64_t block_sum_u64_sat(uint64_t v, uint64_t* scra
   return s;
 }
 
+// Math.min(a, b) for doubles (NaN wins; -0.0 < +0.0).
+__device__ __forceinline__ double java_min(double a, double b) {
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+  return (a <= b) ? a : b;
+}
+
+// normalizeWeightResult(result, count=1, num=0) (AbstractSimilarity.java:313-330):
+// WEIGHTED scales by 1 - count/(num+1) = 0, i.e. +-1; then the clamp to [-1, 1].
+__device__ __forceinline__ double normalize_weight(double r, int weighted) {
+  if (weighted) {
+    const double scale = __dsub_rn(1.0, 1.0 / 1.0);  // 1 - count/(num+1) = 0
+    if (r < 0.0) r = __dadd_rn(-1.0, __dmul_rn(scale, __dadd_rn(1.0, r)));
+    else r = __dsub_rn(1.0, __dmul_rn(scale, __dsub_rn(1.0, r)));
+  }
+  if (r < -1.0) r = -1.0;
+  else if (r > 1.0) r = 1.0;
+  return r;
+}
+
 }  // namespace cms

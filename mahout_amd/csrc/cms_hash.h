@@ -75,4 +75,15 @@ CMS_HD uint32_t bucket(const HashParams& hp, int r, uint64_t kp) {
   return (uint32_t)rem;
 }
 
+// Bucket for an arbitrary width w with its Barrett constant floor((2^64-1)/w)
+// (per-owner sketch shapes: CosineCM hashes u1 at u2's width).
+CMS_HD uint32_t bucket_wb(const HashParams& hp, int r, uint64_t kp, uint32_t w, uint64_t barrett) {
+  uint64_t s = mulmod_p(hp.ap[r], kp) + hp.bp[r];
+  if (s >= kPrime) s -= kPrime;
+  uint64_t q = (uint64_t)(((unsigned __int128)s * barrett) >> 64);
+  uint64_t rem = s - q * w;
+  while (rem >= w) rem -= w;
+  return (uint32_t)rem;
+}
+
 }  // namespace cms

@@ -113,6 +113,21 @@ struct cms_handle {
   int64_t dlog_n = 0, dlog_cap = 0;
   cms::DevBuf dlog_row, dlog_key, dlog_val, dlog_cnt, dlog_all;
 
+  // per-owner shapes (CosineCM with its CountMinSketchConfig, cms_create_per_owner):
+  // the DataModel stays resident as CSR and each owner carries its own (d, w);
+  // userSimilarity(u1, u2) hashes u1's preferences at u2's shape on the fly
+  bool per_owner = false;
+  bool po_loaded = false, po_configured = false;
+  int64_t po_npairs = 0;
+  int32_t po_max_w = 0, po_max_d = 0;
+  std::vector<int64_t> h_po_off;                 // [n+1] CSR offsets (DataModel)
+  std::vector<double> h_po_delta, h_po_eps;      // CountMinSketchConfig.getDelta/getEpsilon
+  std::vector<int32_t> h_po_w, h_po_d;           // AbstractCountMinSketch(delta, epsilon) shape; 0 = CMException
+  cms::DevBuf po_off, po_kp, po_inc;             // CSR offsets, keys mod p, u32 increments
+  cms::DevBuf po_shape;                          // PoShape [n]
+  cms::DevBuf po_sk, po_norm, po_nsq;            // own sketches [sum d*w] u32; norms [sum d] u64 / f64 sqrt
+  cms::DevBuf po_scratch;                        // per-block bucket rows for widths beyond LDS
+
   // instrumentation
   bool timing = false;
   std::map<std::string, cms::TimingAcc> timing_acc;
@@ -191,6 +206,34 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
 // merge nparts partial top-k lists ([nparts][n][k] ids by owner ID, scores; [nparts][n] counts)
 int top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* d_ids, const double* d_scores,
                 const int32_t* d_counts, int64_t* d_out_ids, double* d_out_scores, int32_t* d_out_counts);
+// ---- cms_profiles.hip (per-owner shapes) ----
+struct PoShape {
+  int64_t soff;      // first counter of the owner's own sketch
+  int64_t roff;      // first (owner, row) norm slot
+  uint64_t barrett;  // floor((2^64-1)/w)
+  int32_t w, d;      // 0 when the owner's (delta, epsilon) raise CMException
+};
+int po_load_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs,
+                const int64_t* h_off);
+int po_finalize(cms_handle* h);
+// similarities of (qrows[i / m], crows[i % m]) into out[i] (crows null: identity)
+int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m, double* d_out);
+int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
+                            const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out);
+int po_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
+                  int32_t* d_counts);
+// shape check of every owner in rows (all owners when rows is null)
+int po_require_shapes(cms_handle* h, const int64_t* rows, int64_t m);
+// ---- cms_topk.hip (shared by both modes) ----
+struct TopQuery {
+  int64_t slab_row;  // row of the slab holding this query's similarities
+  int64_t self_col;  // slab column of the query itself (excluded)
+  int64_t out_pos;   // output slot
+};
+int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k, const int64_t* d_perm,
+                 int64_t* d_ids, double* d_scores, int32_t* d_counts);
+int64_t slab_rows_for(int64_t n);
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);

@@ -1,0 +1,570 @@
+// cms_profiles.hip -- CosineCM with per-owner sketch shapes on gfx950.
+//
+// The reference sizes every owner's sketch on its own.  CountMinSketchConfig
+// (T/impl/common/CountMinSketchConfig.java:120-158) picks (d, w) per owner by
+// maximising Fmeasure (:210-219) and stores delta = exp(-d), epsilon = e/w;
+// CosineCM.userSimilarity(u1, u2) (T/impl/similarity/CosineCM.java:83-96)
+// then builds u1's sketch with u2's (delta, epsilon) (exportProfile :41-58),
+// takes u2's own sketch from its cache (getExportedCMProfile :60-67) and
+// returns the min-over-rows cosine (DoubleCountMinSketch.java:114-149).
+//
+// Here the DataModel stays resident in HBM as CSR (keys reduced mod p once,
+// u32 increments).  Own sketches are built once at finalize into one ragged
+// u32 array with exact u64 row norms.  A similarity never materialises u1's
+// sketch in HBM: one wave per (u1, u2) pair hashes u1's preferences at u2's
+// shape into an LDS bucket row (global scratch past kPoHist), and per sketch
+// row forms
+//   valueAB = sum_k v_k * B[h(k)]   (exact: u64, every term an integer)
+//   valueA  = sum_j A[j]^2          (the LDS row; exact while < 2^53)
+// -- the integers the reference's fp64 loops produce bit for bit while the
+// sums stay below 2^53; past that the wave replays the reference's
+// sequential fp64 loop in j order.  The epilogue is the same correctly
+// rounded sqrt / mul / div and Math.min as the fixed-shape kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+#include "cms_device.h"
+#include "cms_internal.h"
+
+namespace cms {
+
+constexpr int kPoThreads = 64;     // one wave per (u1, u2) pair
+constexpr int kPoHist = 4096;      // LDS bucket row (u32); wider shapes use global scratch
+constexpr int kPoGrid = 8192;      // pair-kernel blocks with LDS rows
+constexpr int kPoGridWide = 1024;  // pair-kernel blocks when some width exceeds kPoHist
+constexpr int kCfgThreads = 256;
+
+// ------------------------------------------------ CountMinSketchConfig --
+
+// Fmeasure(w, d, n, u, q) (:210-219) with probaNotExactRetrieve (:190-196)
+// and probaInserted (:170-178) written out as the reference evaluates them.
+__device__ __forceinline__ double po_fmeasure(int w, int d, int n, int u, double q2) {
+  const double W = (double)w, D = (double)d, N = (double)n, U = (double)u;
+  const double falseP = pow(1.0 - pow(1.0 - 1.0 / W, N), D);
+  const double beta = 1.0 - falseP;
+  const double p = 1.0 - N / (N + falseP * (U - N));
+  if (beta == 0.0 || p == 0.0) return 0.0;
+  return 3.0 * beta * p / (q2 * beta + p);
+}
+
+// computeConfig (:120-158), one workgroup per owner: every (d, w) with d in
+// [1, 25) and w in [d, n] is scored; the loop keeps the LAST position whose
+// score is >= the running best (which starts at 0), i.e. the last maximiser
+// among scores >= 0 -- reduced here as max over (score, position).
+__global__ __launch_bounds__(kCfgThreads) void k_po_config(const int64_t* off, int64_t n_owners, int32_t u,
+                                                           double q2, int32_t* best_w, int32_t* best_d) {
+  __shared__ double sf[kCfgThreads / 64];
+  __shared__ uint64_t si[kCfgThreads / 64];
+  for (int64_t r = blockIdx.x; r < n_owners; r += gridDim.x) {
+    const int64_t len = off[r + 1] - off[r];
+    const int nn = (int)std::min<int64_t>(len, 0x7fffffff);
+    double bf = -1.0;  // no candidate yet
+    uint64_t bi = 0;
+    for (int d = 1; d < 25; ++d)
+      for (int w = d + (int)threadIdx.x; w <= nn; w += kCfgThreads) {
+        const double x = po_fmeasure(w, d, nn, u, q2);
+        const uint64_t idx = ((uint64_t)d << 32) | (uint32_t)w;
+        if (x >= 0.0 && (x > bf || (x == bf && idx > bi))) {
+          bf = x;
+          bi = idx;
+        }
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double of = __shfl_xor(bf, o, 64);
+      const uint64_t oi = __shfl_xor(bi, o, 64);
+      if (of > bf || (of == bf && oi > bi)) {
+        bf = of;
+        bi = oi;
+      }
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sf[threadIdx.x >> 6] = bf;
+      si[threadIdx.x >> 6] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int i = 1; i < kCfgThreads / 64; ++i)
+        if (sf[i] > bf || (sf[i] == bf && si[i] > bi)) {
+          bf = sf[i];
+          bi = si[i];
+        }
+      best_w[r] = bf < 0.0 ? 0 : (int32_t)(uint32_t)bi;
+      best_d[r] = bf < 0.0 ? 0 : (int32_t)(bi >> 32);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------ DataModel --
+
+__global__ void k_po_prep(const int64_t* key, const float* val, int64_t np, uint64_t* kp, uint32_t* inc,
+                          uint32_t* flags) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
+    kp[i] = reduce_key(key[i]);
+    uint32_t v;
+    if (!load_inc(val, i, v)) atomicOr(flags, kFlagBadValue);
+    inc[i] = v;
+  }
+}
+
+// An owner's total mass bounds every counter of its sketch at any shape.
+__global__ __launch_bounds__(256) void k_po_mass(const int64_t* off, int64_t n, const uint32_t* inc,
+                                                 uint32_t* flags) {
+  __shared__ uint64_t red[4];
+  for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    uint64_t s = 0;
+    for (int64_t i = off[r] + threadIdx.x; i < off[r + 1]; i += 256) s += inc[i];
+    s = block_sum_u64_sat(s, red);
+    if (threadIdx.x == 0 && s >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+  }
+}
+
+// ----------------------------------------------------------- own sketches --
+
+// getExportedCMProfile(u) for every owner: update(key, inc) at the owner's own
+// shape (DoubleCountMinSketch.update :72-80), exact u32 global atomics.
+__global__ __launch_bounds__(256) void k_po_build(const int64_t* off, const uint64_t* kp, const uint32_t* inc,
+                                                  const PoShape* shp, HashParams hp, int64_t n, uint32_t* sk) {
+  for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const PoShape s = shp[r];
+    if (s.w <= 0) continue;
+    for (int64_t i = off[r] + threadIdx.x; i < off[r + 1]; i += 256) {
+      const uint64_t k = kp[i];
+      const uint32_t v = inc[i];
+      for (int d = 0; d < s.d; ++d)
+        atomicAdd(&sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, k, (uint32_t)s.w, s.barrett)], v);
+    }
+  }
+}
+
+// Exact per-(owner, row) sum of squares and Math.sqrt of the reference's
+// valueB: the integer sum below 2^53, else the sequential fp64 sum in j order.
+__global__ __launch_bounds__(256) void k_po_norms(const PoShape* shp, int64_t n, const uint32_t* sk, uint64_t* norm,
+                                                  double* nsq) {
+  __shared__ uint64_t red[4];
+  for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const PoShape s = shp[r];
+    for (int d = 0; d < s.d; ++d) {
+      const uint32_t* row = sk + s.soff + (int64_t)d * s.w;
+      uint64_t q = 0;
+      for (int j = threadIdx.x; j < s.w; j += 256) q = sat_add(q, (uint64_t)row[j] * row[j]);
+      q = block_sum_u64_sat(q, red);
+      if (threadIdx.x == 0) {
+        double v;
+        if (q < (1ULL << 53)) {
+          v = (double)q;
+        } else {
+          v = 0.0;
+          for (int j = 0; j < s.w; ++j) {
+            const double x = (double)row[j];
+            v = __dadd_rn(v, __dmul_rn(x, x));
+          }
+        }
+        norm[s.roff + d] = q;
+        nsq[s.roff + d] = __dsqrt_rn(v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ similarity --
+
+struct PoPairArgs {
+  const int64_t* off;
+  const uint64_t* kp;
+  const uint32_t* inc;
+  const PoShape* shp;
+  const uint32_t* sk;
+  const uint64_t* norm;
+  const double* nsq;
+  const int64_t* qrows;  // [nq]
+  const int64_t* crows;  // [m] or null (identity)
+  int64_t nq, m;
+  uint32_t* scratch;     // [gridDim][max_w] zeroed u32 rows (widths > kPoHist)
+  int64_t scratch_w;
+  double* out;           // [nq][m]
+  int32_t weighted;
+};
+
+__device__ __forceinline__ uint64_t po_wave_sum(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = sat_add(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// userSimilarity(u1 = qrows[t / m], u2 = crows[t % m]): one wave per pair.
+__global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParams hp) {
+  __shared__ uint32_t lds[kPoHist];
+  const int lane = threadIdx.x;
+  for (int j = lane; j < kPoHist; j += kPoThreads) lds[j] = 0u;
+  __syncthreads();
+  uint32_t* gsc = a.scratch ? a.scratch + (int64_t)blockIdx.x * a.scratch_w : nullptr;
+  const int64_t total = a.nq * a.m;
+  for (int64_t t = blockIdx.x; t < total; t += gridDim.x) {
+    const int64_t u1 = a.qrows[t / a.m];
+    const int64_t c = t % a.m;
+    const int64_t u2 = a.crows ? a.crows[c] : c;
+    const PoShape s = a.shp[u2];
+    const uint32_t w = (uint32_t)s.w;
+    uint32_t* hist = (w <= (uint32_t)kPoHist) ? lds : gsc;
+    const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+    double minc = DBL_MAX;
+    for (int d = 0; d < s.d; ++d) {
+      const uint32_t* brow = a.sk + s.soff + (int64_t)d * w;
+      uint64_t ab = 0;
+      for (int64_t i = k0 + lane; i < k1; i += kPoThreads) {
+        const uint32_t j = bucket_wb(hp, d, a.kp[i], w, s.barrett);
+        const uint32_t v = a.inc[i];
+        atomicAdd(&hist[j], v);
+        ab = sat_add(ab, (uint64_t)v * brow[j]);
+      }
+      __syncthreads();
+      uint64_t a2 = 0;
+      for (uint32_t j = lane; j < w; j += kPoThreads) a2 = sat_add(a2, (uint64_t)hist[j] * hist[j]);
+      a2 = po_wave_sum(a2);
+      ab = po_wave_sum(ab);
+      const uint64_t b2 = a.norm[s.roff + d];
+      double valueAB, den;
+      if (a2 < (1ULL << 53) && b2 < (1ULL << 53)) {
+        valueAB = (double)ab;  // ab <= sqrt(a2 * b2) < 2^53: exact
+        den = __dmul_rn(__dsqrt_rn((double)a2), a.nsq[s.roff + d]);
+      } else {  // the reference's sequential fp64 loop (:128-134), every lane alike
+        double A = 0.0, B = 0.0, AB = 0.0;
+        for (uint32_t j = 0; j < w; ++j) {
+          const double xa = (double)hist[j], xb = (double)brow[j];
+          A = __dadd_rn(A, __dmul_rn(xa, xa));
+          B = __dadd_rn(B, __dmul_rn(xb, xb));
+          AB = __dadd_rn(AB, __dmul_rn(xa, xb));
+        }
+        valueAB = AB;
+        den = __dmul_rn(__dsqrt_rn(A), __dsqrt_rn(B));
+      }
+      __syncthreads();
+      for (uint32_t j = lane; j < w; j += kPoThreads) hist[j] = 0u;  // keep the row zero for the next use
+      __syncthreads();
+      if (den != 0.0) minc = java_min(minc, __ddiv_rn(valueAB, den));
+    }
+    if (lane == 0) {
+      double r = (minc == DBL_MAX) ? __builtin_nan("") : minc;
+      if (r == r) r = normalize_weight(r, a.weighted);
+      a.out[t] = r;
+    }
+  }
+}
+
+// DoubleCountMinSketch.get(key) (:94-103) of the owner's own sketch.
+__global__ void k_po_point(const PoShape* shp, const uint32_t* sk, HashParams hp, int64_t row, const int64_t* keys,
+                           int64_t m, double* out) {
+  const PoShape s = shp[row];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t kp = reduce_key(keys[i]);
+    double est = DBL_MAX;
+    for (int d = 0; d < s.d; ++d) {
+      const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, kp, (uint32_t)s.w, s.barrett)];
+      if (v < est) est = v;
+    }
+    out[i] = est;
+  }
+}
+
+// doEstimatePreference with the point query of each neighbour's own sketch
+// (GenericUserBasedRecommender.java:134-184), as k_estimate for fixed shapes.
+__global__ void k_po_estimate(const PoShape* shp, const uint32_t* sk, HashParams hp, int64_t user_row,
+                              const int64_t* nb_rows, const double* sims, int64_t m, const int64_t* items, int64_t q,
+                              int use_capper, float lo, float hi, float* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < q; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t kp = reduce_key(items[i]);
+    double preference = 0.0, total = 0.0;
+    int count = 0;
+    for (int64_t j = 0; j < m; ++j) {
+      const int64_t r = nb_rows[j];
+      if (r == user_row) continue;
+      const PoShape s = shp[r];
+      double est = DBL_MAX;
+      for (int d = 0; d < s.d; ++d) {
+        const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, kp, (uint32_t)s.w, s.barrett)];
+        if (v < est) est = v;
+      }
+      const float pref = (float)est;
+      if (pref == 0.0f) continue;
+      const double sim = sims[j];
+      if (sim != sim) continue;
+      preference = __dadd_rn(preference, __dmul_rn(sim, (double)pref));
+      total = __dadd_rn(total, sim);
+      ++count;
+    }
+    float e = __builtin_nanf("");
+    if (count > 1) {
+      e = (float)__ddiv_rn(preference, total);
+      if (use_capper) {
+        if (e > hi) e = hi;
+        else if (e < lo) e = lo;
+      }
+    }
+    out[i] = e;
+  }
+}
+
+// ---------------------------------------------------------------- host --
+
+static unsigned grid_for(int64_t work, int64_t cap) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(work, cap));
+}
+
+int po_load_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs,
+                const int64_t* h_off) {
+  const int64_t n = h->n;
+  CMS_HIP(h->po_off.ensure(sizeof(int64_t) * (n + 1)));
+  CMS_HIP(h->po_kp.ensure(sizeof(uint64_t) * std::max<int64_t>(npairs, 1)));
+  CMS_HIP(h->po_inc.ensure(sizeof(uint32_t) * std::max<int64_t>(npairs, 1)));
+  CMS_HIP(hipMemcpyAsync(h->po_off.ptr, d_off, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, h->stream));
+  if (npairs > 0)
+    hipLaunchKernelGGL(k_po_prep, dim3(grid_for((npairs + 255) / 256, 8192)), dim3(256), 0, h->stream, d_key, d_val,
+                       npairs, h->po_kp.as<uint64_t>(), h->po_inc.as<uint32_t>(), h->d_flags);
+  hipLaunchKernelGGL(k_po_mass, dim3(grid_for(n, 65536)), dim3(256), 0, h->stream, h->po_off.as<int64_t>(), n,
+                     h->po_inc.as<uint32_t>(), h->d_flags);
+  CMS_HIP(hipGetLastError());
+  h->h_po_off.assign(h_off, h_off + n + 1);
+  h->po_npairs = npairs;
+  h->po_loaded = true;
+  h->finalized = false;
+  return CMS_OK;
+}
+
+// shapes from (delta, epsilon) as new DoubleCountMinSketch(delta, epsilon, hfb)
+// derives them (AbstractCountMinSketch.java:69-83); 0 marks a CMException
+static int po_set_config(cms_handle* h, const double* delta, const double* eps) {
+  const int64_t n = h->n;
+  std::vector<int32_t> W(n), D(n);
+  for (int64_t r = 0; r < n; ++r) {
+    int32_t w = 0, d = 0;
+    const double de = delta[r], ep = eps[r];
+    const bool ok = !(de <= 0 || de > std::exp(-1.0)) && !(ep <= 0 || ep > std::exp(1.0));
+    if (ok) {
+      const double wf = std::ceil(std::exp(1.0) / ep), df = std::ceil(std::log(1.0 / de));
+      if (!(wf <= (double)(1 << 24)) || !(df <= (double)CMS_MAX_DEPTH))
+        return set_error(CMS_E_PARAM,
+                         "owner row %lld: sketch shape %.0f x %.0f exceeds this build (width <= 2^24, depth <= %d)",
+                         (long long)r, wf, df, CMS_MAX_DEPTH);
+      w = (int32_t)wf;
+      d = (int32_t)df;
+    }
+    W[r] = w;
+    D[r] = d;
+  }
+  std::vector<PoShape> shp(n);
+  int64_t so = 0, ro = 0;
+  int32_t mw = 0, md = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    shp[r].soff = so;
+    shp[r].roff = ro;
+    shp[r].w = W[r];
+    shp[r].d = D[r];
+    shp[r].barrett = W[r] > 0 ? (~0ULL) / (uint64_t)W[r] : 0;
+    so += (int64_t)W[r] * D[r];
+    ro += D[r];
+    mw = std::max(mw, W[r]);
+    md = std::max(md, D[r]);
+  }
+  CMS_HIP(h->po_shape.ensure(sizeof(PoShape) * n));
+  CMS_HIP(hipMemcpyAsync(h->po_shape.ptr, shp.data(), sizeof(PoShape) * n, hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  h->h_po_delta.assign(delta, delta + n);
+  h->h_po_eps.assign(eps, eps + n);
+  h->h_po_w.swap(W);
+  h->h_po_d.swap(D);
+  h->po_max_w = mw;
+  h->po_max_d = md;
+  h->po_configured = true;
+  h->finalized = false;
+  return CMS_OK;
+}
+
+int po_require_shapes(cms_handle* h, const int64_t* rows, int64_t m) {
+  const int64_t cnt = rows ? m : h->n;
+  for (int64_t i = 0; i < cnt; ++i) {
+    const int64_t r = rows ? rows[i] : i;
+    if (h->h_po_w[r] <= 0)
+      return set_error(CMS_E_SKETCH,
+                       "CountMinSketch error: delta/epsilon of owner %lld outside (0, e^-1] x (0, e] (CMException)",
+                       (long long)(h->h_owner_ids.empty() ? r : h->h_owner_ids[r]));
+  }
+  return CMS_OK;
+}
+
+int po_finalize(cms_handle* h) {
+  if (!h->po_loaded) return set_error(CMS_E_STATE, "per-owner mode: ingest the DataModel (CSR) first");
+  if (!h->po_configured)
+    return set_error(CMS_E_STATE, "delta is null, call configure method first (cms_configure_owner_shapes)");
+  const int64_t n = h->n;
+  int64_t total = 0, rtot = 0;
+  for (int64_t r = 0; r < n; ++r) {
+    total += (int64_t)h->h_po_w[r] * h->h_po_d[r];
+    rtot += h->h_po_d[r];
+  }
+  CMS_HIP(h->po_sk.ensure(sizeof(uint32_t) * std::max<int64_t>(total, 1)));
+  CMS_HIP(h->po_norm.ensure(sizeof(uint64_t) * std::max<int64_t>(rtot, 1)));
+  CMS_HIP(h->po_nsq.ensure(sizeof(double) * std::max<int64_t>(rtot, 1)));
+  CMS_HIP(hipMemsetAsync(h->po_sk.ptr, 0, sizeof(uint32_t) * std::max<int64_t>(total, 1), h->stream));
+  {
+    TimedScope ts(h, "po_build");
+    hipLaunchKernelGGL(k_po_build, dim3(grid_for(n, 65536)), dim3(256), 0, h->stream, h->po_off.as<int64_t>(),
+                       h->po_kp.as<uint64_t>(), h->po_inc.as<uint32_t>(), h->po_shape.as<PoShape>(), h->hp, n,
+                       h->po_sk.as<uint32_t>());
+    hipLaunchKernelGGL(k_po_norms, dim3(grid_for(n, 65536)), dim3(256), 0, h->stream, h->po_shape.as<PoShape>(), n,
+                       h->po_sk.as<uint32_t>(), h->po_norm.as<uint64_t>(), h->po_nsq.as<double>());
+    CMS_HIP(hipGetLastError());
+  }
+  if (h->po_max_w > kPoHist) {
+    const size_t need = sizeof(uint32_t) * (size_t)kPoGridWide * (size_t)h->po_max_w;
+    if (h->po_scratch.bytes < need) {
+      CMS_HIP(h->po_scratch.ensure(need));
+      CMS_HIP(hipMemsetAsync(h->po_scratch.ptr, 0, h->po_scratch.bytes, h->stream));
+    }
+  }
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
+int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m,
+                    double* d_out) {
+  if (nq <= 0 || m <= 0) return CMS_OK;
+  PoPairArgs a;
+  a.off = h->po_off.as<int64_t>();
+  a.kp = h->po_kp.as<uint64_t>();
+  a.inc = h->po_inc.as<uint32_t>();
+  a.shp = h->po_shape.as<PoShape>();
+  a.sk = h->po_sk.as<uint32_t>();
+  a.norm = h->po_norm.as<uint64_t>();
+  a.nsq = h->po_nsq.as<double>();
+  a.qrows = d_qrows;
+  a.crows = d_crows;
+  a.nq = nq;
+  a.m = m;
+  const bool wide = h->po_max_w > kPoHist;
+  a.scratch = wide ? h->po_scratch.as<uint32_t>() : nullptr;
+  a.scratch_w = wide ? h->po_max_w : 0;
+  a.out = d_out;
+  a.weighted = h->p.weighting == CMS_WEIGHTED;
+  TimedScope ts(h, "po_pair_cosine");
+  hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(nq * m, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
+                     h->stream, a, h->hp);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
+  if (m <= 0) return CMS_OK;
+  hipLaunchKernelGGL(k_po_point, dim3(grid_for((m + 255) / 256, 4096)), dim3(256), 0, h->stream,
+                     h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->hp, row, d_keys, m, d_out);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
+                            const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out) {
+  if (q <= 0) return CMS_OK;
+  hipLaunchKernelGGL(k_po_estimate, dim3(grid_for((q + 255) / 256, 4096)), dim3(256), 0, h->stream,
+                     h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->hp, user_row, d_nb_rows, d_sims, m,
+                     d_items, q, use_capper, lo, hi, d_out);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+// mostSimilar for query rows [row_begin, row_begin + row_count): a slab of
+// userSimilarity(query, candidate) over every candidate (the MostSimilarEstimator
+// argument order, GenericUserBasedRecommender.java:231-247), then the shared
+// TopItems.getTopUsers selection (cms_topk.hip).
+int po_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
+                  int32_t* d_counts) {
+  if (k < 1 || k > 1024) return set_error(CMS_E_PARAM, "k must be in [1, 1024]");
+  int rc = po_require_shapes(h, nullptr, 0);
+  if (rc) return rc;
+  const int64_t n = h->n;
+  const int64_t qb = std::min<int64_t>(row_count, slab_rows_for(n));
+  CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(qb * n)));
+  CMS_HIP(h->ws_query.ensure(sizeof(int64_t) * (size_t)qb));
+  std::vector<int64_t> qrows(qb);
+  for (int64_t r0 = 0; r0 < row_count; r0 += qb) {
+    const int64_t rcnt = std::min(qb, row_count - r0);
+    std::vector<TopQuery> qs;
+    for (int64_t q = 0; q < rcnt; ++q) {
+      qrows[q] = row_begin + r0 + q;
+      qs.push_back(TopQuery{q, row_begin + r0 + q, r0 + q});
+    }
+    CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, qrows.data(), sizeof(int64_t) * rcnt, hipMemcpyHostToDevice, h->stream));
+    if ((rc = po_pair_cosines(h, h->ws_query.as<int64_t>(), rcnt, nullptr, n, h->ws_slab.as<double>()))) return rc;
+    if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, nullptr, d_ids, d_scores, d_counts))) return rc;
+  }
+  return CMS_OK;
+}
+
+}  // namespace cms
+
+using namespace cms;
+
+extern "C" {
+
+int cms_configure_owner_shapes(cms_handle* h, double q, int64_t num_keys) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: shapes come from cms_params");
+  if (num_keys < 0 || num_keys > 0x7fffffff) return set_error(CMS_E_PARAM, "num_keys must be an int (getNumItems)");
+  std::lock_guard<std::mutex> g(h->mu);
+  (void)hipSetDevice(h->device);
+  if (!h->po_loaded) return set_error(CMS_E_STATE, "per-owner mode: ingest the DataModel (CSR) first");
+  const int64_t n = h->n;
+  DevBuf bw, bd;
+  CMS_HIP(bw.ensure(sizeof(int32_t) * n));
+  CMS_HIP(bd.ensure(sizeof(int32_t) * n));
+  {
+    TimedScope ts(h, "po_config");
+    hipLaunchKernelGGL(k_po_config, dim3(grid_for(n, 65536)), dim3(kCfgThreads), 0, h->stream,
+                       h->po_off.as<int64_t>(), n, (int32_t)num_keys, std::pow(q, 2.0), bw.as<int32_t>(),
+                       bd.as<int32_t>());
+    CMS_HIP(hipGetLastError());
+  }
+  std::vector<int32_t> W(n), D(n);
+  CMS_HIP(hipMemcpyAsync(W.data(), bw.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipMemcpyAsync(D.data(), bd.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  bw.release();
+  bd.release();
+  std::vector<double> delta(n), eps(n);
+  for (int64_t r = 0; r < n; ++r) {
+    if (W[r] == 0 && D[r] == 0)  // CountMinSketchConfig.java:145-147
+      return set_error(CMS_E_SKETCH, "No solution found (this should not happen) (w=0 and d=0) for owner %lld",
+                       (long long)(h->h_owner_ids.empty() ? r : h->h_owner_ids[r]));
+    eps[r] = std::exp(1.0) / (double)W[r];
+    delta[r] = std::exp(-(double)D[r]);
+  }
+  return po_set_config(h, delta.data(), eps.data());
+}
+
+int cms_set_owner_delta_epsilon(cms_handle* h, const double* delta, const double* epsilon) {
+  if (!h || !delta || !epsilon) return set_error(CMS_E_PARAM, "null argument");
+  if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: shapes come from cms_params");
+  std::lock_guard<std::mutex> g(h->mu);
+  (void)hipSetDevice(h->device);
+  return po_set_config(h, delta, epsilon);
+}
+
+int cms_get_owner_shapes(cms_handle* h, double* delta, double* epsilon, int32_t* width, int32_t* depth) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: shapes come from cms_params");
+  std::lock_guard<std::mutex> g(h->mu);
+  if (!h->po_configured)
+    return set_error(CMS_E_STATE, "delta is null, call configure method first (cms_configure_owner_shapes)");
+  const size_t n = (size_t)h->n;
+  if (delta) std::copy(h->h_po_delta.begin(), h->h_po_delta.begin() + n, delta);
+  if (epsilon) std::copy(h->h_po_eps.begin(), h->h_po_eps.begin() + n, epsilon);
+  if (width) std::copy(h->h_po_w.begin(), h->h_po_w.begin() + n, width);
+  if (depth) std::copy(h->h_po_d.begin(), h->h_po_d.begin() + n, depth);
+  return CMS_OK;
+}
+
+}  // extern "C"

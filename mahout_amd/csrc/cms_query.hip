@@ -17,27 +17,10 @@
 #include <algorithm>
 #include <cfloat>
 
+#include "cms_device.h"
 #include "cms_internal.h"
 
 namespace cms {
-
-__device__ __forceinline__ double java_min(double a, double b) {
-  if (a != a) return a;
-  if (a == 0.0 && b == 0.0 && signbit(b)) return b;
-  return (a <= b) ? a : b;
-}
-
-// normalizeWeightResult(result, count=1, num=0)
-__device__ __forceinline__ double normalize_weight(double r, int weighted) {
-  if (weighted) {
-    const double scale = __dsub_rn(1.0, 1.0 / 1.0);  // 1 - count/(num+1) = 0
-    if (r < 0.0) r = __dadd_rn(-1.0, __dmul_rn(scale, __dadd_rn(1.0, r)));
-    else r = __dsub_rn(1.0, __dmul_rn(scale, __dsub_rn(1.0, r)));
-  }
-  if (r < -1.0) r = -1.0;
-  else if (r > 1.0) r = 1.0;
-  return r;
-}
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll

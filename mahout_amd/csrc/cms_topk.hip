@@ -29,11 +29,6 @@ __device__ __forceinline__ uint64_t score_key(double s) {
   return (u >> 63) ? ~u : (u | (1ULL << 63));
 }
 
-struct TopQuery {
-  int64_t slab_row;  // row of the slab holding this query's similarities
-  int64_t self_col;  // slab column of the query itself (excluded)
-  int64_t out_pos;   // output slot
-};
 
 __device__ __forceinline__ uint32_t block_count(uint32_t v, uint32_t* wsum) {
 #pragma unroll
@@ -372,7 +367,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_k_fast(const double* slab, 
   if (tid == 0) counts[Q.out_pos] = (int32_t)kk;
 }
 
-static int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k,
+int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k,
                         const int64_t* d_perm, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
   if (qs.empty()) return CMS_OK;
   CMS_HIP(h->ws_topq.ensure(sizeof(TopQuery) * qs.size()));
@@ -660,7 +655,7 @@ int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t
 }
 
 // slab budget: 2^30 fp64 similarities (8 GiB) -- 1,024 query rows at 1M owners
-static int64_t slab_rows_for(int64_t n) {
+int64_t slab_rows_for(int64_t n) {
   return std::max<int64_t>(128, ((int64_t(1) << 30) / std::max<int64_t>(1, n)) / 128 * 128);
 }
 
@@ -701,6 +696,7 @@ int slab_top_k_positions(cms_handle* h, const std::vector<int64_t>& pos, const s
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts) {
   if (k < 1 || k > kTopMax) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kTopMax);
+  if (h->per_owner) return po_top_k_rows(h, row_begin, row_count, k, d_ids, d_scores, d_counts);
   const int64_t n = h->n;
   int rc = CMS_OK;
   if (mfma_eligible(h) && (rc = cosine_prepare(h))) return rc;

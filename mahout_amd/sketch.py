@@ -58,7 +58,8 @@ def comm_unique_id():
 
 
 class SketchTable:
-    def __init__(self, num_owners, depth=5, width=4096, seed=42, weighted=False, device=-1, owner_ids=None):
+    def __init__(self, num_owners, depth=5, width=4096, seed=42, weighted=False, device=-1, owner_ids=None,
+                 per_owner=False):
         lib = _lib.load()
         p = _lib.CmsParams()
         check(lib.cms_params_init(ctypes.byref(p)))
@@ -69,7 +70,9 @@ class SketchTable:
         p.weighting = _lib.CMS_WEIGHTED if weighted else _lib.CMS_UNWEIGHTED
         p.device = device
         h = ctypes.c_void_p()
-        check(lib.cms_create(ctypes.byref(p), ctypes.byref(h)))
+        create = lib.cms_create_per_owner if per_owner else lib.cms_create
+        check(create(ctypes.byref(p), ctypes.byref(h)))
+        self.per_owner = per_owner
         self._lib = lib
         self._h = h
         self.num_owners = num_owners
@@ -232,6 +235,42 @@ class SketchTable:
         cnt = np.zeros(n, np.int32)
         check(self._lib.cms_top_k_all(self._h, int(k), _ptr(ids), _ptr(sc), _ptr(cnt)))
         return ids, sc, cnt
+
+    # -- per-owner shapes (CountMinSketchConfig) --
+    @classmethod
+    def per_owner_shapes(cls, num_owners, seed=42, weighted=False, device=-1, owner_ids=None):
+        """A handle whose owners each carry their own (d, w): CosineCM with
+        its CountMinSketchConfig (cms_create_per_owner)."""
+        return cls(num_owners, seed=seed, weighted=weighted, device=device, owner_ids=owner_ids, per_owner=True)
+
+    def configure_owner_shapes(self, q, num_keys):
+        """CountMinSketchConfig(q).configure(dataModel) on the GPU."""
+        check(self._lib.cms_configure_owner_shapes(self._h, float(q), int(num_keys)))
+
+    def set_owner_delta_epsilon(self, delta, epsilon):
+        de = np.ascontiguousarray(delta, np.float64)
+        ep = np.ascontiguousarray(epsilon, np.float64)
+        if de.size != self.num_owners or ep.size != self.num_owners:
+            raise ValueError("one (delta, epsilon) per owner")
+        check(self._lib.cms_set_owner_delta_epsilon(self._h, _ptr(de), _ptr(ep)))
+
+    def owner_shapes(self):
+        """(delta, epsilon, width, depth) per owner row."""
+        n = self.num_owners
+        de, ep = np.zeros(n, np.float64), np.zeros(n, np.float64)
+        w, d = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        check(self._lib.cms_get_owner_shapes(self._h, _ptr(de), _ptr(ep), _ptr(w), _ptr(d)))
+        return de, ep, w, d
+
+    def read_owner_sketch(self, owner_id):
+        """getExportedCMProfile(owner_id): [depth][width] fp64."""
+        w = ctypes.c_int32()
+        d = ctypes.c_int32()
+        check(self._lib.cms_read_owner_sketch(self._h, int(owner_id), None, 0, ctypes.byref(w), ctypes.byref(d)))
+        out = np.zeros((d.value, w.value), np.float64)
+        check(self._lib.cms_read_owner_sketch(self._h, int(owner_id), _ptr(out), out.size, ctypes.byref(w),
+                                              ctypes.byref(d)))
+        return out
 
     def read_counters(self, row_begin=0, row_count=None):
         if row_count is None:

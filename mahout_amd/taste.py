@@ -8,7 +8,8 @@ ItemSimilarity (T/similarity/ItemSimilarity.java:31-64); every similarity
 is computed by libmahout_cms.so on the GPU.
 
 Shape: the reference sizes each owner's sketch from CountMinSketchConfig's
-(delta, epsilon) (CosineCM.java:63,86).  The fixed-shape configs of this
+(delta, epsilon) (CosineCM.java:63,86).  ``CountMinSketchConfig`` keeps that
+per-owner mode (u1 hashed at u2's shape on the GPU).  The fixed-shape configs of this
 path (d, w for every owner) are expressed by ``FixedShapeConfig``, whose
 getDelta/getEpsilon return exp(-d) and e/w -- the subclass override the
 reference allows (CountMinSketchConfig.getDelta/getEpsilon are public,
@@ -62,6 +63,44 @@ class FixedShapeConfig:
         return shape_from_delta_epsilon(self.getDelta(), self.getEpsilon())
 
 
+class CountMinSketchConfig:
+    """CountMinSketchConfig(q) (T/impl/common/CountMinSketchConfig.java:57-60):
+    per-owner (delta, epsilon) chosen by the Fmeasure search.  configure()
+    runs computeConfig (:120-158) on the GPU when the CosineCM that owns the
+    data is built; setConfig() takes (delta, epsilon) arrays computed
+    elsewhere (the ser/ cache of :74-95 in the reference).  getDelta /
+    getEpsilon before configuration raise TasteException, as :230-251 do."""
+
+    def __init__(self, q):
+        self.q = float(q)
+        self._explicit = None
+        self._result = None  # (owner ids, delta, epsilon) once configured
+
+    def setConfig(self, delta, epsilon):
+        self._explicit = (np.asarray(delta, np.float64), np.asarray(epsilon, np.float64))
+
+    def _configure(self, table, dataModel):
+        if self._explicit is not None:
+            table.set_owner_delta_epsilon(*self._explicit)
+        else:
+            table.configure_owner_shapes(self.q, dataModel.getNumItems())
+        de, ep, _, _ = table.owner_shapes()
+        self._result = (dataModel.getUserIDs(), de, ep)
+
+    def _lookup(self, arr, userID):
+        if self._result is None:
+            raise TasteException("delta is null, call configure method first")
+        ids = self._result[0]
+        i = np.searchsorted(ids, userID)
+        return float(arr[i]) if i < ids.size and ids[i] == userID else 0.0  # trove: missing key -> 0.0
+
+    def getDelta(self, userID):
+        return self._lookup(self._result[1] if self._result else None, userID)
+
+    def getEpsilon(self, userID):
+        return self._lookup(self._result[2] if self._result else None, userID)
+
+
 def _map_error(e, owner_kind="user"):
     if e.code == _lib.CMS_E_NO_SUCH_ID:
         return NoSuchUserException(str(e)) if owner_kind == "user" else NoSuchItemException(str(e))
@@ -81,7 +120,11 @@ class CosineCM:
     def __init__(self, dataModel, conf, hfBuilder, weighting=Weighting.UNWEIGHTED, device=-1):
         if not dataModel.hasPreferenceValues():  # CosineCM.java:38
             raise ValueError("DataModel doesn't have preference values")
-        width, depth = conf.shape() if hasattr(conf, "shape") else (conf.width, conf.depth)
+        self._per_owner = isinstance(conf, CountMinSketchConfig)
+        if self._per_owner:
+            width = depth = None  # each owner has its own shape
+        else:
+            width, depth = conf.shape() if hasattr(conf, "shape") else (conf.width, conf.depth)
         self._model = dataModel
         self._conf = conf
         self._hfb = hfBuilder
@@ -93,10 +136,17 @@ class CosineCM:
 
     def _build(self):
         m = self._model
-        self._table = SketchTable(m.getNumUsers(), depth=self.depth, width=self.width, seed=self._hfb.seed,
-                                  weighted=self._weighted, device=self._device, owner_ids=m.getUserIDs())
         try:
-            self._table.ingest_csr(m.offsets, m.keys, m.values)
+            if self._per_owner:
+                self._table = SketchTable.per_owner_shapes(m.getNumUsers(), seed=self._hfb.seed,
+                                                           weighted=self._weighted, device=self._device,
+                                                           owner_ids=m.getUserIDs())
+                self._table.ingest_csr(m.offsets, m.keys, m.values)
+                self._conf._configure(self._table, m)
+            else:
+                self._table = SketchTable(m.getNumUsers(), depth=self.depth, width=self.width, seed=self._hfb.seed,
+                                          weighted=self._weighted, device=self._device, owner_ids=m.getUserIDs())
+                self._table.ingest_csr(m.offsets, m.keys, m.values)
             self._table.finalize()
         except _lib.CmsError as e:
             raise _map_error(e)

@@ -186,3 +186,50 @@ def build_rows_reuse(offsets, keys, vals, lo, hi, depth, width, a, b):
     n = lib().orc_build_rows_reuse(np.ascontiguousarray(offsets, np.int64), np.ascontiguousarray(keys, np.int64),
                                    _vp(v), lo, hi, depth, width, a, b, ctypes.byref(cs))
     return n, cs.value
+
+
+# ---- per-owner shapes (CountMinSketchConfig + CosineCM), composed from the
+# restated primitives above.  Test infrastructure only.
+
+def owner_config(offsets, u_items, q):
+    """CountMinSketchConfig.computeConfig (T/impl/common/CountMinSketchConfig.java:120-158)
+    for every owner: (delta, epsilon) arrays; n = the owner's preference count."""
+    offsets = np.asarray(offsets, np.int64)
+    n = offsets.size - 1
+    de = np.zeros(n, np.float64)
+    ep = np.zeros(n, np.float64)
+    for r in range(n):
+        _, _, de[r], ep[r] = compute_config(int(offsets[r + 1] - offsets[r]), int(u_items), float(q))
+    return de, ep
+
+
+def owner_shapes(delta, epsilon):
+    """AbstractCountMinSketch(delta, epsilon) shape per owner; (0, 0) for CMException."""
+    w = np.zeros(len(delta), np.int32)
+    d = np.zeros(len(delta), np.int32)
+    for r, (de, ep) in enumerate(zip(delta, epsilon)):
+        try:
+            w[r], d[r] = shape_from_delta_epsilon(float(de), float(ep))
+        except ValueError:
+            pass
+    return w, d
+
+
+def export_profile(offsets, keys, vals, row, width, depth, a, b):
+    """CosineCM.exportProfile(row, delta, epsilon) (T/impl/similarity/CosineCM.java:41-58):
+    a fresh [depth][width] sketch of the owner's preferences, in their order."""
+    lo, hi = int(offsets[row]), int(offsets[row + 1])
+    v = None if vals is None else np.asarray(vals, np.float32)[lo:hi]
+    k = np.asarray(keys, np.int64)[lo:hi]
+    return build_table(1, depth, width, a, b, np.zeros(hi - lo, np.int64), k, v)[0]
+
+
+def per_owner_similarity(offsets, keys, vals, shapes, a, b, u1, u2, weighted=False):
+    """CosineCM.userSimilarity(u1, u2) (CosineCM.java:83-96): u1's sketch built
+    with u2's (delta, epsilon), against u2's own sketch."""
+    w, d = int(shapes[0][u2]), int(shapes[1][u2])
+    if w == 0:
+        raise ValueError("CMException")
+    s1 = export_profile(offsets, keys, vals, u1, w, d, a, b)
+    s2 = export_profile(offsets, keys, vals, u2, w, d, a, b)
+    return cosine_cm(s1, s2, weighted)
