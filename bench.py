@@ -408,7 +408,8 @@ def main():
     value = total_updates / elapsed
 
     breakdown = {}
-    for name in ["partition", "build_plan", "build_rows", "reduce_hot", "norms", "allreduce"]:
+    for name in ["partition", "build_plan", "build_rows", "reduce_hot", "norms", "merge_bounds", "merge_pack",
+                 "allreduce", "merge_unpack"]:
         ms, n = table.timing(name)
         if n:
             breakdown[name] = round(ms / args.steps, 4)
@@ -437,7 +438,8 @@ def main():
             "workload": f"config 2: Zipf {args.n_users} users x {n} items, {npairs} pairs per rank, d={d} w={w}; "
                         "unordered COO (item, user) stream -> finished u32 sketch table + norms",
             "n_items": n, "n_users": args.n_users, "pairs_per_rank": npairs, "depth": d, "width": w,
-            "sharding": "user-hash (splitmix64) across ranks, RCCL all-reduce of u32 counters",
+            "sharding": "user-hash (splitmix64) across ranks; RCCL all-reduce of the counters, counter-width-adaptive "
+                        "packed (bit-identical to a u32 sum)",
         },
         "roofline": {
             "bound": "hbm",
@@ -458,6 +460,10 @@ def main():
         },
         "breakdown_ms_per_step": breakdown,
     }
+    if world > 1:
+        mw = table.stats()["merge_words"]
+        result["merge"] = {"allreduce_bytes_per_step": mw * 8, "u32_table_bytes": table_bytes,
+                           "payload_ratio": mw * 8 / table_bytes}
 
     off = ckeys = None
     # extras run on a single GPU only: with a communicator, finalize and the

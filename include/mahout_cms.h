@@ -145,8 +145,21 @@ int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t wo
 int32_t cms_shard_of_key(int64_t key, int32_t world);
 
 /* Merge (RCCL all-reduce when a communicator is attached), then derive the
- * per-(owner,row) norms the cosine needs.  Queries require it. */
+ * per-(owner,row) norms the cosine needs.  Queries require it.
+ * The merge is counter-width adaptive: one all-reduce of (row mass, largest
+ * local counter) per owner bounds every merged counter of that owner, and the
+ * counters then travel as bit fields of exactly that width packed into u64
+ * words whose u64 sums cannot carry between fields -- the merged table is
+ * bit-identical to a u32 all-reduce at a fraction of the xGMI bytes. */
 int cms_finalize(cms_handle* h);
+/* The same merge through a caller-supplied collective instead of RCCL (an MPI,
+ * torch.distributed or Spark transport): fn(d_buf, count, user) must replace
+ * the count u64 words at device pointer d_buf (on the handle's device; the
+ * handle's stream is idle) by their sum over all ranks, and return 0.  It is
+ * called a fixed number of times, with identical counts on every rank.  The
+ * merged table takes no further ingest until cms_reset (CMS_E_STATE). */
+typedef int (*cms_allreduce_fn)(void* d_buf, int64_t count, void* user);
+int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user);
 int cms_synchronize(cms_handle* h);
 
 /* ---- queries (after cms_finalize) ---------------------------------------- */
@@ -263,6 +276,7 @@ typedef struct cms_stats {
   int64_t topk_redo;         /* top-k rows that needed the radix-select fallback */
   int64_t deep_limb_owners;  /* of those, owners with a counter >= 2^14 (3+ limbs); -1 before */
   int64_t fp4_owners;        /* single-limb owners with every counter <= 4 (fp4 MFMA operands); -1 before */
+  int64_t merge_words;       /* u64 words the last multi-rank merge all-reduced (packed counters) */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -37,7 +37,7 @@ EXPORTS = [
     "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_top_k_all_partial", "cms_top_k_merge", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
-    "cms_read_owner_sketch",
+    "cms_read_owner_sketch", "cms_finalize_with",
 ]
 
 
@@ -68,6 +68,7 @@ class CmsStats(ctypes.Structure):
         ("topk_redo", ctypes.c_int64),
         ("deep_limb_owners", ctypes.c_int64),
         ("fp4_owners", ctypes.c_int64),
+        ("merge_words", ctypes.c_int64),
     ]
 
 
@@ -76,6 +77,9 @@ _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
 _int = ctypes.c_int
 _dbl = ctypes.c_double
+
+# int (*cms_allreduce_fn)(void* d_buf, int64_t count, void* user)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 
 _SIGS = {
     "cms_params_init": (_int, [ctypes.POINTER(CmsParams)]),
@@ -115,6 +119,7 @@ _SIGS = {
     "cms_get_timing": (_int, [_vp, ctypes.c_char_p, ctypes.POINTER(_dbl), ctypes.POINTER(_i64)]),
     "cms_reset_timing": (_int, [_vp]),
     "cms_create_per_owner": (_int, [ctypes.POINTER(CmsParams), ctypes.POINTER(_vp)]),
+    "cms_finalize_with": (_int, [_vp, _vp, _vp]),
     "cms_configure_owner_shapes": (_int, [_vp, _dbl, _i64]),
     "cms_set_owner_delta_epsilon": (_int, [_vp, _vp, _vp]),
     "cms_get_owner_shapes": (_int, [_vp, _vp, _vp, _vp, _vp]),

@@ -390,6 +390,8 @@ int dlog_exchange(cms_handle* h) {
 }  // namespace
 
 int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t n) {
+  if (h && h->ext_merged)
+    return set_error(CMS_E_STATE, "table merged through cms_finalize_with: cms_reset starts a new epoch");
   if (!h || (n > 0 && (!owner || !key))) return set_error(CMS_E_PARAM, "null argument");
   if (int rc0 = refuse_per_owner(h, "COO ingest (per-owner mode takes the DataModel as CSR)")) return rc0;
   if (n <= 0) return CMS_OK;
@@ -422,6 +424,8 @@ int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const fl
 }
 
 int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n) {
+  if (h && h->ext_merged)
+    return set_error(CMS_E_STATE, "table merged through cms_finalize_with: cms_reset starts a new epoch");
   if (!h || (n > 0 && (!d_row || !d_key))) return set_error(CMS_E_PARAM, "null argument");
   if (int rc0 = refuse_per_owner(h, "COO ingest (per-owner mode takes the DataModel as CSR)")) return rc0;
   if (n <= 0) return CMS_OK;
@@ -436,6 +440,8 @@ int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d
 }
 
 int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, const float* vals) {
+  if (h && h->ext_merged)
+    return set_error(CMS_E_STATE, "table merged through cms_finalize_with: cms_reset starts a new epoch");
   if (!h || !offsets) return set_error(CMS_E_PARAM, "null argument");
   const int64_t n = h->n;
   if (offsets[0] != 0) return set_error(CMS_E_PARAM, "offsets[0] must be 0");
@@ -481,6 +487,8 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
 }
 
 int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t* d_keys, const float* d_vals) {
+  if (h && h->ext_merged)
+    return set_error(CMS_E_STATE, "table merged through cms_finalize_with: cms_reset starts a new epoch");
   if (!h || !d_offsets) return set_error(CMS_E_PARAM, "null argument");
   Guard g(h);
   if (h->merged && h->comm && h->world > 1)
@@ -522,6 +530,7 @@ int cms_reset(cms_handle* h) {
   h->finalized = false;
   h->pairs_ingested = 0;
   h->merged = false;
+  h->ext_merged = false;
   h->dlog_n = 0;
   return CMS_OK;
 }
@@ -596,13 +605,14 @@ int cms_finalize(cms_handle* h) {
     int rc = dlog_exchange(h);
     if (rc) return rc;
   } else if (h->comm && h->world > 1) {
-    TimedScope ts(h, "allreduce");
-    ncclResult_t r = ncclAllReduce(h->d_table, h->d_table, (size_t)(h->n * h->dw), ncclUint32, ncclSum, h->comm,
-                                   h->stream);
-    if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce(table): %s", ncclGetErrorString(r));
-    r = ncclAllReduce(h->d_row_mass, h->d_row_mass, (size_t)h->n, ncclUint64, ncclSum, h->comm, h->stream);
-    if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce(mass): %s", ncclGetErrorString(r));
-    h->norms_valid = false;
+    // counter-width-adaptive packed sums over RCCL (cms_merge.hip)
+    auto rccl = [h](uint64_t* buf, int64_t count) -> int {
+      ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclUint64, ncclSum, h->comm, h->stream);
+      if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+      return CMS_OK;
+    };
+    int rc = merge_packed(h, rccl);
+    if (rc) return rc;
     h->merged = true;
     h->dlog_n = 0;
   }
@@ -611,6 +621,37 @@ int cms_finalize(cms_handle* h) {
   CMS_HIP(hipStreamSynchronize(h->stream));
   rc = check_flags(h, false);
   if (rc) return rc;
+  uint32_t inexact = 0;
+  CMS_HIP(hipMemcpy(&inexact, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  h->exact_norms = inexact == 0;
+  h->mfma_ready = false;
+  h->finalized = true;
+  return CMS_OK;
+}
+
+int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
+  if (!h || !fn) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "cms_finalize_with")) return rc0;
+  Guard g(h);
+  if (h->comm) return set_error(CMS_E_STATE, "handle has an RCCL communicator: use cms_finalize");
+  if (h->ext_merged) return set_error(CMS_E_STATE, "already merged: cms_reset starts a new epoch");
+  if (h->empty) {
+    CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * h->n * h->dw, h->stream));
+    h->empty = false;
+    h->norms_valid = false;
+  }
+  auto ext = [h, fn, user](uint64_t* buf, int64_t count) -> int {
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    const int r = fn(buf, count, user);
+    if (r != 0) return set_error(CMS_E_RCCL, "caller all-reduce returned %d", r);
+    return CMS_OK;
+  };
+  int rc = merge_packed(h, ext);
+  if (rc) return rc;
+  h->ext_merged = true;
+  if ((rc = compute_norms(h))) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if ((rc = check_flags(h, false))) return rc;
   uint32_t inexact = 0;
   CMS_HIP(hipMemcpy(&inexact, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
   h->exact_norms = inexact == 0;
@@ -941,6 +982,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;
   out->fp4_owners = h->mfma_ready ? h->n_f4 : -1;
+  out->merge_words = h->merge_words;
   return CMS_OK;
 }
 

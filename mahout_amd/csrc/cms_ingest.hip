@@ -308,6 +308,15 @@ __global__ void k_norm_sqrt(const uint64_t* norm, int64_t cells, double* out, ui
   }
 }
 
+int local_norms(cms_handle* h) {
+  const unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
+  if (grid > 0)
+    hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->n, h->hp, h->d_norm, h->d_rowmax);
+  CMS_HIP(hipGetLastError());
+  h->norms_valid = true;
+  return CMS_OK;
+}
+
 int compute_norms(cms_handle* h) {
   TimedScope ts(h, "norms");
   uint32_t stale = 0;  // an incremental norm reached the inexact regime

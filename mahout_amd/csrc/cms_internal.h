@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -25,6 +26,24 @@ enum : uint32_t {
 struct DevBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), bytes(o.bytes) {
+    o.ptr = nullptr;
+    o.bytes = 0;
+  }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      ptr = o.ptr;
+      bytes = o.bytes;
+      o.ptr = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }  // scoped scratch frees itself (hipFree waits for the device)
   hipError_t ensure(size_t need);
   template <class T>
   T* as() const { return reinterpret_cast<T*>(ptr); }
@@ -110,6 +129,8 @@ struct cms_handle {
   // COO batches are logged here and only the logs are exchanged at the next
   // finalize (each rank applies the other ranks' batches).
   bool merged = false;
+  bool ext_merged = false;  // merged through cms_finalize_with (no delta log: refuse later ingests)
+  int64_t merge_words = 0;  // u64 words the last packed merge moved
   int64_t dlog_n = 0, dlog_cap = 0;
   cms::DevBuf dlog_row, dlog_key, dlog_val, dlog_cnt, dlog_all;
 
@@ -162,6 +183,14 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
 // owner IDs -> rows by binary search over h->d_owner_ids.
 int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_rows);
 int compute_norms(cms_handle* h);
+// norms + row maxima of the local table (k_norms)
+int local_norms(cms_handle* h);
+// ---- cms_merge.hip ----
+// in-place u64 sum over all ranks of count words of a device buffer
+using AllReduceU64 = std::function<int(uint64_t*, int64_t)>;
+// merge the per-rank tables (and row masses) through the counter-width-adaptive
+// packed all-reduce; leaves the merged table, norms and row maxima
+int merge_packed(cms_handle* h, const AllReduceU64& allreduce);
 // flags rows outside [0,n) and increments the counter type cannot hold.
 int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n);
 int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d_out);

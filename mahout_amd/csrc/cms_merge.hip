@@ -1,0 +1,175 @@
+// cms_merge.hip -- counter-width-adaptive merge of per-rank sketch tables.
+//
+// Each rank holds a full-shape partial table built from its user-hash shard of
+// the stream; the merged table is the elementwise sum (counters are linear).
+// Summing the u32 table as is moves 4 B per counter over xGMI.  Most of it is
+// headroom: a merged counter of owner o can never exceed
+//     bound(o) = min(sum_g mass_g(o), sum_g max_g(o))
+// (mass = the owner's total increment, max = its largest local counter), and
+// both sums are one small all-reduce of 2n words.  So each owner's counters
+// travel as b(o) = bit_length(bound(o)) -bit fields packed floor(64/b) to a
+// u64 word (no field straddles a word), and the packed words are all-reduced
+// as plain u64 sums: every partial sum of a field is <= its final value <
+// 2^b, so no carry ever crosses a field and the packed sum IS the packed
+// merged table, bit for bit.  Owners with bound 0 send nothing.
+//
+// The unpack writes the merged u32 table and, in the same pass, the exact
+// per-row norms and row maxima the cosine needs (no second table read).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "cms_device.h"
+#include "cms_internal.h"
+
+namespace cms {
+
+// [0, n): local row mass (copied in), [n, 2n): local row max, widened to u64.
+__global__ void k_merge_bounds_in(const uint64_t* mass, const uint32_t* rowmax, int64_t n, uint64_t* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    out[i] = mass[i];
+    out[n + i] = rowmax[i];
+  }
+}
+
+// After the bounds all-reduce: merged mass back into row_mass (overflow check:
+// a row whose total increment reaches 2^32 could overflow a u32 counter).
+__global__ void k_merge_bounds_out(const uint64_t* sums, int64_t n, uint64_t* mass, uint32_t* flags) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    mass[i] = sums[i];
+    if (sums[i] >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+  }
+}
+
+struct PackLayout {
+  const uint8_t* bits;   // [n] field width per owner (0: owner sends nothing)
+  const int64_t* woff;   // [n+1] first packed word per owner
+};
+
+// One workgroup per owner: word i carries counters [i*F, (i+1)*F) of the owner.
+__global__ __launch_bounds__(256) void k_merge_pack(const uint32_t* table, int64_t n, int64_t dw, PackLayout L,
+                                                   uint64_t* words) {
+  for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
+    const int b = L.bits[o];
+    if (b == 0) continue;
+    const int F = 64 / b;
+    const int64_t w0 = L.woff[o], nw = L.woff[o + 1] - w0;
+    const uint32_t* src = table + o * dw;
+    for (int64_t i = threadIdx.x; i < nw; i += 256) {
+      const int64_t c0 = i * F;
+      const int cnt = (int)std::min<int64_t>(F, dw - c0);
+      uint64_t wv = 0;
+      for (int f = 0; f < cnt; ++f) wv |= (uint64_t)src[c0 + f] << (f * b);
+      words[w0 + i] = wv;
+    }
+  }
+}
+
+// Merged words -> u32 table, with the exact per-row sum of squares and the
+// owner's largest counter (as k_norms computes them).
+__global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int64_t n, HashParams hp, PackLayout L,
+                                                      uint32_t* table, uint64_t* norm, uint32_t* rowmax) {
+  __shared__ uint64_t red[4];
+  __shared__ uint32_t smax[4];
+  const int w = (int)hp.width;
+  const int64_t dw = (int64_t)hp.depth * w;
+  for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
+    const int b = L.bits[o];
+    uint32_t* dst = table + o * dw;
+    if (b == 0) {  // every rank's counters of this owner are zero
+      for (int64_t i = threadIdx.x; i < dw; i += 256) dst[i] = 0u;
+      if (threadIdx.x < hp.depth) norm[o * hp.depth + threadIdx.x] = 0;
+      if (threadIdx.x == 0) rowmax[o] = 0;
+      continue;
+    }
+    const uint32_t F = 64u / (uint32_t)b;
+    const uint64_t mask = b >= 64 ? ~0ULL : ((1ULL << b) - 1);
+    const uint64_t* src = words + L.woff[o];
+    uint32_t vmax = 0;
+    for (int d = 0; d < hp.depth; ++d) {
+      uint64_t sq = 0;
+      for (int j = threadIdx.x; j < w; j += 256) {
+        const uint32_t idx = (uint32_t)(d * w + j);
+        const uint32_t wi = idx / F, f = idx - wi * F;
+        const uint32_t c = (uint32_t)((src[wi] >> (f * (uint32_t)b)) & mask);
+        dst[idx] = c;
+        sq = sat_add(sq, (uint64_t)c * c);
+        vmax = max(vmax, c);
+      }
+      const uint64_t tot = block_sum_u64_sat(sq, red);
+      if (threadIdx.x == 0) norm[o * hp.depth + d] = tot;
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, s, 64));
+    if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) rowmax[o] = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+    __syncthreads();
+  }
+}
+
+int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
+  const int64_t n = h->n, dw = h->dw;
+  // 1. local row maxima (the build passes leave them current with the norms)
+  int rc;
+  if (!h->norms_valid && (rc = local_norms(h))) return rc;
+  // 2. one all-reduce of (mass, max) per owner
+  DevBuf bnd;
+  CMS_HIP(bnd.ensure(sizeof(uint64_t) * 2 * n));
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_merge_bounds_in, dim3(g), dim3(256), 0, h->stream, h->d_row_mass, h->d_rowmax, n,
+                     bnd.as<uint64_t>());
+  CMS_HIP(hipGetLastError());
+  {
+    TimedScope ts(h, "merge_bounds");
+    if ((rc = allreduce(bnd.as<uint64_t>(), 2 * n))) return rc;
+  }
+  hipLaunchKernelGGL(k_merge_bounds_out, dim3(g), dim3(256), 0, h->stream, bnd.as<uint64_t>(), n, h->d_row_mass,
+                     h->d_flags);
+  CMS_HIP(hipGetLastError());
+  // 3. field widths and word offsets (identical on every rank: same sums)
+  std::vector<uint64_t> sums(2 * n);
+  CMS_HIP(hipMemcpyAsync(sums.data(), bnd.ptr, sizeof(uint64_t) * 2 * n, hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  std::vector<uint8_t> bits(n);
+  std::vector<int64_t> woff(n + 1);
+  int64_t words = 0;
+  for (int64_t o = 0; o < n; ++o) {
+    const uint64_t bound = std::min(sums[o], sums[n + o]);
+    const int b = bound == 0 ? 0 : 64 - __builtin_clzll(bound);
+    bits[o] = (uint8_t)b;
+    woff[o] = words;
+    if (b) words += (dw + (64 / b) - 1) / (64 / b);
+  }
+  woff[n] = words;
+  h->merge_words = words;
+  DevBuf d_bits, d_woff, packed;
+  CMS_HIP(d_bits.ensure(std::max<int64_t>(n, 1)));
+  CMS_HIP(d_woff.ensure(sizeof(int64_t) * (n + 1)));
+  CMS_HIP(packed.ensure(sizeof(uint64_t) * std::max<int64_t>(words, 1)));
+  CMS_HIP(hipMemcpyAsync(d_bits.ptr, bits.data(), n, hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipMemcpyAsync(d_woff.ptr, woff.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+  PackLayout L{d_bits.as<uint8_t>(), d_woff.as<int64_t>()};
+  const unsigned go = (unsigned)std::min<int64_t>(n, 65536);
+  {
+    TimedScope ts(h, "merge_pack");
+    hipLaunchKernelGGL(k_merge_pack, dim3(go), dim3(256), 0, h->stream, h->d_table, n, dw, L, packed.as<uint64_t>());
+    CMS_HIP(hipGetLastError());
+  }
+  {
+    TimedScope ts(h, "allreduce");
+    if (words > 0 && (rc = allreduce(packed.as<uint64_t>(), words))) return rc;
+  }
+  {
+    TimedScope ts(h, "merge_unpack");
+    hipLaunchKernelGGL(k_merge_unpack, dim3(go), dim3(256), 0, h->stream, packed.as<uint64_t>(), n, h->hp, L,
+                       h->d_table, h->d_norm, h->d_rowmax);
+    CMS_HIP(hipGetLastError());
+  }
+  CMS_HIP(hipStreamSynchronize(h->stream));  // scratch is freed on return
+  h->norms_valid = true;                     // the unpack wrote the merged norms
+  return CMS_OK;
+}
+
+}  // namespace cms

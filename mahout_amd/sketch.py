@@ -154,6 +154,21 @@ class SketchTable:
     def finalize(self):
         check(self._lib.cms_finalize(self._h))
 
+    def finalize_with(self, allreduce):
+        """cms_finalize_with: merge through a caller collective.
+        allreduce(d_ptr, count) must sum `count` u64 words at device address
+        d_ptr over all ranks, in place."""
+        def thunk(ptr, count, _user):
+            try:
+                allreduce(int(ptr), int(count))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported as a status code
+                import traceback
+                traceback.print_exc()
+                return 1
+        cb = _lib.ALLREDUCE_FN(thunk)
+        check(self._lib.cms_finalize_with(self._h, cb, None))
+
     def synchronize(self):
         check(self._lib.cms_synchronize(self._h))
 
