@@ -8,7 +8,7 @@
 // (mass = the owner's total increment, max = its largest local counter), and
 // both sums are one small all-reduce of 2n words.  So each owner's counters
 // travel as b(o) = bit_length(bound(o)) -bit fields packed floor(64/b) to a
-// u64 word (no field straddles a word), and the packed words are all-reduced
+// u64 word (no field straddles a word; field f of word i is counter f*NW + i), and the packed words are all-reduced
 // as plain u64 sums: every partial sum of a field is <= its final value <
 // 2^b, so no carry ever crosses a field and the packed sum IS the packed
 // merged table, bit for bit.  Owners with bound 0 send nothing.
@@ -47,7 +47,9 @@ struct PackLayout {
   const int64_t* woff;   // [n+1] first packed word per owner
 };
 
-// One workgroup per owner: word i carries counters [i*F, (i+1)*F) of the owner.
+// One workgroup per owner.  Field f of the owner's word i holds counter
+// f*NW + i (NW = the owner's word count): both the pack's reads and the
+// unpack's word reads are then consecutive across the lanes of a wave.
 __global__ __launch_bounds__(256) void k_merge_pack(const uint32_t* table, int64_t n, int64_t dw, PackLayout L,
                                                    uint64_t* words) {
   for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
@@ -57,10 +59,11 @@ __global__ __launch_bounds__(256) void k_merge_pack(const uint32_t* table, int64
     const int64_t w0 = L.woff[o], nw = L.woff[o + 1] - w0;
     const uint32_t* src = table + o * dw;
     for (int64_t i = threadIdx.x; i < nw; i += 256) {
-      const int64_t c0 = i * F;
-      const int cnt = (int)std::min<int64_t>(F, dw - c0);
       uint64_t wv = 0;
-      for (int f = 0; f < cnt; ++f) wv |= (uint64_t)src[c0 + f] << (f * b);
+      for (int f = 0; f < F; ++f) {
+        const int64_t idx = (int64_t)f * nw + i;
+        if (idx < dw) wv |= (uint64_t)src[idx] << (f * b);
+      }
       words[w0 + i] = wv;
     }
   }
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
       if (threadIdx.x == 0) rowmax[o] = 0;
       continue;
     }
-    const uint32_t F = 64u / (uint32_t)b;
+    const uint32_t nw = (uint32_t)(L.woff[o + 1] - L.woff[o]);
     const uint64_t mask = b >= 64 ? ~0ULL : ((1ULL << b) - 1);
     const uint64_t* src = words + L.woff[o];
     uint32_t vmax = 0;
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
       uint64_t sq = 0;
       for (int j = threadIdx.x; j < w; j += 256) {
         const uint32_t idx = (uint32_t)(d * w + j);
-        const uint32_t wi = idx / F, f = idx - wi * F;
+        const uint32_t f = idx / nw, wi = idx - f * nw;
         const uint32_t c = (uint32_t)((src[wi] >> (f * (uint32_t)b)) & mask);
         dst[idx] = c;
         sq = sat_add(sq, (uint64_t)c * c);
