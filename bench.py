@@ -104,6 +104,52 @@ def cpu_baseline(off_d, keys_d, args, budget_s=12.0):
                       f"{dt:.1f} s; fp64 DoubleCountMinSketch rebuilt per owner + 128-bit BigInteger-equivalent hash"}
 
 
+def cosine_cpu_baseline(items, users, n, d, w, budget_s=10.0, sample_owners=192, seed=5):
+    """Config-4 similarity on the host, 1 core, two restatements of the
+    reference (oracle/cms_oracle.c):
+      faithful  -- the CosineCM cost model: u1's fp64 sketch rebuilt per call
+                   (exportProfile), u2's from a cache, min-over-rows cosine
+                   (orc_faithful_pairs);
+      prebuilt  -- every sketch built once, then the same fp64 cosine per pair
+                   (orc_similarities_row).
+    Sample: `sample_owners` random items of the config-3/4 stream with all their
+    (item, user) pairs; pairs (i, j), i != j, of the sample until the budget."""
+    from oracle import oracle as O
+    from mahout_amd.synth import to_csr
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pick = np.sort(rng.choice(n, size=sample_owners, replace=False))
+    sel = torch.isin(items, torch.from_numpy(pick).to(items.device))
+    it = items[sel].cpu().numpy()
+    us = users[sel].cpu().numpy()
+    rows = np.searchsorted(pick, it)
+    off, keys, _ = to_csr(rows, us, sample_owners)
+    a, b = O.hash_params(42, d)
+    S = sample_owners
+    done, t0 = 0, time.perf_counter()
+    i0 = 0
+    while time.perf_counter() - t0 < budget_s / 2:
+        # 8 query rows x every other sampled row per call (u2's cache is per call)
+        pi = np.array([i for i in range(i0, i0 + 8) for j in range(S) if j != i % S], np.int64) % S
+        pj = np.array([j for i in range(i0, i0 + 8) for j in range(S) if j != i % S], np.int64)
+        O.faithful_pairs(off, keys, None, S, d, w, a, b, pi, pj)
+        done += pi.size
+        i0 += 8
+    faithful = done / (time.perf_counter() - t0)
+    table = O.build_table(S, d, w, a, b, rows, us)
+    done, t0 = 0, time.perf_counter()
+    q = 0
+    while time.perf_counter() - t0 < budget_s / 2:
+        O.similarities_row(table, q % S)
+        done += S - 1
+        q += 1
+    prebuilt = done / (time.perf_counter() - t0)
+    return {"value": faithful, "unit": "item-pair cosines/s", "cores": 1, "kind": "port",
+            "prebuilt_sketches_value": prebuilt,
+            "sample": f"{S} random items of the config-3/4 stream ({int(keys.size)} pairs), d={d} w={w}: "
+                      f"faithful CosineCM cost model (u1 rebuilt per call) for {budget_s / 2:.0f} s, then prebuilt "
+                      f"fp64 sketches for {budget_s / 2:.0f} s"}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/<round>/pmc_summary.json, scripts/profile.sh on this bench command:
@@ -218,6 +264,9 @@ def cosine_1m(args, local, device, rank=0, world=1):
     t.finalize()
     bar()
     ingest_s = max_over_ranks(time.perf_counter() - t0)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cosine_cpu_baseline(items, users, n, d, w)
     del items, users
     torch.cuda.empty_cache()
     t.release_scratch()
@@ -287,6 +336,7 @@ def cosine_1m(args, local, device, rank=0, world=1):
         "config3_ingest_merge_s": ingest_s,
         "config3_updates_per_s": npairs / ingest_s,
         "config5_streaming": stream,
+        "cpu_baseline": cpu,
     }
 
 
