@@ -220,6 +220,22 @@ int cms_top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* ids
  * String.valueOf(double), narrowed to float first when as_float (the
  * RecommendedItem values SimilarItems carries, SimilarItems.java:36-47). */
 int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
+/* The same all-pairs lists in the output formats of the other similarity
+ * drivers a sketch cosine can stand in for:
+ *   CMS_FORMAT_ITEM_SIMILARITY_JOB -- ItemSimilarityJob's text result
+ *     (T/hadoop/similarity/item/ItemSimilarityJob.java:181-233): each pair of
+ *     a list once as "aID\tbID\tsimilarity" with aID < bID, sorted by (aID, bID)
+ *     (EntityEntityWritable.java:64-71); for a pair listed by both owners the
+ *     lower ID's value is kept.
+ *   CMS_FORMAT_SPARK_ITEMSIMILARITY -- spark-itemsimilarity's
+ *     TextDelimitedIndexedDatasetWriter, default schema
+ *     (spark/src/main/scala/org/apache/mahout/drivers/TextDelimitedReaderWriter.scala:244-303):
+ *     "ID\tID1:s1 ID2:s2 ..." per owner, non-zero similarities by strength
+ *     descending; a bare "ID" when the list is empty.
+ * Values print as Java's Double.toString (fp64). */
+#define CMS_FORMAT_ITEM_SIMILARITY_JOB 1
+#define CMS_FORMAT_SPARK_ITEMSIMILARITY 2
+int cms_write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format);
 /* Java Double.toString(v) into buf (NUL-terminated); returns the length or -1. */
 int cms_format_java_double(double v, char* buf, int32_t cap);
 

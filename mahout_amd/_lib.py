@@ -24,6 +24,8 @@ CMS_E_OOM = 9
 CMS_E_SKETCH = 10
 
 CMS_COUNTER_U32 = 0
+CMS_FORMAT_ITEM_SIMILARITY_JOB = 1
+CMS_FORMAT_SPARK_ITEMSIMILARITY = 2
 CMS_UNWEIGHTED = 0
 CMS_WEIGHTED = 1
 
@@ -37,7 +39,7 @@ EXPORTS = [
     "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_top_k_all_partial", "cms_top_k_merge", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
-    "cms_read_owner_sketch", "cms_finalize_with",
+    "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities",
 ]
 
 
@@ -120,6 +122,7 @@ _SIGS = {
     "cms_reset_timing": (_int, [_vp]),
     "cms_create_per_owner": (_int, [ctypes.POINTER(CmsParams), ctypes.POINTER(_vp)]),
     "cms_finalize_with": (_int, [_vp, _vp, _vp]),
+    "cms_write_similarities": (_int, [_vp, ctypes.c_char_p, _i32, _i32]),
     "cms_configure_owner_shapes": (_int, [_vp, _dbl, _i64]),
     "cms_set_owner_delta_epsilon": (_int, [_vp, _vp, _vp]),
     "cms_get_owner_shapes": (_int, [_vp, _vp, _vp, _vp, _vp]),

@@ -924,6 +924,17 @@ int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t 
   return write_similar_items(h, path, k, as_float);
 }
 
+int cms_write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format) {
+  if (!h || !path) return set_error(CMS_E_PARAM, "null argument");
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  if (format != CMS_FORMAT_ITEM_SIMILARITY_JOB && format != CMS_FORMAT_SPARK_ITEMSIMILARITY)
+    return set_error(CMS_E_PARAM, "unknown output format %d", format);
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  return write_similarities(h, path, k, format);
+}
+
 int cms_format_java_double(double v, char* buf, int32_t cap) {
   if (!buf || cap <= 0) return -1;
   return java_double_to_string(v, buf, cap);

@@ -266,6 +266,7 @@ int64_t slab_rows_for(int64_t n);
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
+int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format);
 // ---- cms_cosine_mfma.hip ----
 const int64_t* cosine_perm_device(cms_handle* h);
 // ---- cms_cosine_mfma.hip ----

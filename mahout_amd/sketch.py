@@ -219,6 +219,13 @@ class SketchTable:
         """cms_top_k_all in FileSimilarItemsWriter's CSV format."""
         check(self._lib.cms_write_similar_items(self._h, os.fsencode(path), int(k), int(as_float)))
 
+    def write_similarities(self, path, k, fmt):
+        """cms_write_similarities: fmt 'item_similarity_job' (MR ItemSimilarityJob
+        text result) or 'spark_itemsimilarity' (TextDelimitedIndexedDatasetWriter)."""
+        code = {"item_similarity_job": _lib.CMS_FORMAT_ITEM_SIMILARITY_JOB,
+                "spark_itemsimilarity": _lib.CMS_FORMAT_SPARK_ITEMSIMILARITY}[fmt]
+        check(self._lib.cms_write_similarities(self._h, os.fsencode(path), int(k), code))
+
     def top_k_all_partial(self, k, shard, nshards):
         n = self.num_owners
         ids = np.zeros((n, k), np.int64)

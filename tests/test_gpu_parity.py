@@ -417,6 +417,34 @@ def test_write_similar_items_csv(oracle, tmp_path):
     assert lines == exp
 
 
+def test_write_similarities_other_driver_formats(oracle, tmp_path):
+    """ItemSimilarityJob's text result and spark-itemsimilarity's
+    TextDelimitedIndexedDatasetWriter lines, from the same all-pairs lists."""
+    from mahout_amd.sketch import java_double_to_string as jd
+    n, d, w, k = 300, 4, 256, 6
+    items, users = zipf_stream(2000, n, 40_000, seed=73)
+    ids_universe = np.arange(n, dtype=np.int64) * 7 - 500  # negative IDs included
+    with SketchTable(n, depth=d, width=w, seed=42, owner_ids=ids_universe) as t:
+        t.ingest(ids_universe[items], users)
+        t.finalize()
+        ids, sc, cnt = t.top_k_all(k)
+        p1, p2 = tmp_path / "isj.txt", tmp_path / "spark.tsv"
+        t.write_similarities(str(p1), k, "item_similarity_job")
+        t.write_similarities(str(p2), k, "spark_itemsimilarity")
+    pairs = {}
+    for r in range(n):
+        for i in range(cnt[r]):
+            a, b = sorted((int(ids_universe[r]), int(ids[r, i])))
+            pairs.setdefault((a, b), float(sc[r, i]))  # lower ID's list first (rows ascend with IDs)
+    exp1 = [f"{a}\t{b}\t{jd(v)}" for (a, b), v in sorted(pairs.items())]
+    assert p1.read_text().splitlines() == exp1
+    exp2 = []
+    for r in range(n):
+        el = [f"{ids[r, i]}:{jd(float(sc[r, i]))}" for i in range(cnt[r]) if sc[r, i] != 0.0]
+        exp2.append(f"{ids_universe[r]}\t" + " ".join(el) if el else f"{ids_universe[r]}")
+    assert p2.read_text().splitlines() == exp2
+
+
 @pytest.mark.parametrize("nshards", [2, 3, 8])
 def test_top_k_all_shards_merge_exact(oracle, nshards):
     """The multi-GPU decomposition on one GPU: every shard's partial lists
