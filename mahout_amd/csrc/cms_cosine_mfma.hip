@@ -486,6 +486,10 @@ struct BigArgs {
   // sym, fsel != 0: only the block pairs with a block below fblk0 (grid of
   // 2 * fblk0 block slots instead of nb)
   int32_t fblk0, fsel;
+  // sym, rect != 0: the band's (I, J) pairs enumerated by si x sj rectangles
+  // of blocks (njc J-chunks per I-block), so the ~32 workgroups an XCD runs
+  // together share si A panels and sj B blocks instead of 1 and 16-32
+  int32_t rect, si, sj, njc;
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -548,9 +552,24 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     // A band of waves: block I meets J = I + wave + t (t < band), both
     // 128-column halves.  Consecutive workgroups share I (its panel stays in
     // the XCD's L2 for 2*band workgroups) and neighbouring I share most J.
-    const int per = 2 * g.band;
-    const int c = lin / per, rem = lin - c * per, t = rem >> 1, half = rem & 1;
-    const int wv = g.wave + t;
+    int c, half, wv;
+    if (g.rect) {
+      const int per = 2 * g.si * g.sj;
+      const int blk = lin / per, loc = lin - blk * per;
+      const int ib = blk / g.njc, jc = blk - ib * g.njc;
+      half = loc & 1;
+      const int li = (loc >> 1) / g.sj, lj = (loc >> 1) - li * g.sj;
+      c = ib * g.si + li;
+      if (c >= g.nb) return;
+      wv = ib * g.si + g.wave + jc * g.sj + lj - c;  // unwrapped J' - I
+      if (wv < g.wave || wv >= g.wave + g.band) return;
+    } else {
+      const int per = 2 * g.band;
+      c = lin / per;
+      const int rem = lin - c * per;
+      half = rem & 1;
+      wv = g.wave + (rem >> 1);
+    }
     int I = c;
     if (g.fsel) {
       // only the pairs with a block below fblk0: c < fblk0 is that block as I,
@@ -961,6 +980,10 @@ static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t
   if (g.sym) {
     g.tilesB = 2;
     g.nblk = (int)(2 * g.band * sym_pairs);
+    if (g.rect) {
+      g.njc = (g.si + g.band - 1 + g.sj - 1) / g.sj;
+      g.nblk = (int)(((sym_pairs + g.si - 1) / g.si) * g.njc * g.si * g.sj * 2);
+    }
   } else {
     const int oa = kTA / ls;
     const int64_t tilesA = (g.a_owners + oa - 1) / oa;
@@ -1276,6 +1299,10 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
         g.band = (int32_t)L;
         g.nb = (int32_t)nbk;
         g.append_a = g.append_b = 1;
+        // wide bands of plain (non-fsel) waves: rectangle enumeration
+        g.rect = (L >= 8 && !(fp4 ? false : fblk0 < nb) && !getenv("CMS_NO_RECT")) ? 1 : 0;
+        g.si = 4;
+        g.sj = 4;
         TimedScope ts(h, "topk_all_waves");
         if (fp4) {
           g.A = g.B = h->ws_f4.as<int8_t>();
