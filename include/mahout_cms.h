@@ -46,7 +46,7 @@ extern "C" {
 #define CMS_E_SHAPE 2      /* checkArgument w/d mismatch (DoubleCountMinSketch.java:117-118) */
 #define CMS_E_NO_SUCH_ID 3 /* NoSuchUserException / NoSuchItemException (GenericDataModel.java:210-215) */
 #define CMS_E_STATE 4      /* call-order violation (query before finalize, ...) */
-#define CMS_E_VALUE 5      /* increment not representable in the counter type */
+#define CMS_E_VALUE 5      /* increment not a non-negative multiple of 2^-frac_bits below 2^(32-frac_bits) */
 #define CMS_E_OVERFLOW 6   /* a counter could exceed the counter type */
 #define CMS_E_HIP 7        /* HIP runtime error */
 #define CMS_E_RCCL 8       /* RCCL error */
@@ -69,11 +69,16 @@ typedef struct cms_params {
   int64_t num_owners;   /* n: rows of the sketch table */
   int32_t weighting;    /* CMS_UNWEIGHTED | CMS_WEIGHTED (CosineCM.java:33) */
   int32_t device;       /* HIP device ordinal; -1 = current device */
+  int32_t frac_bits;    /* 0..31: preferences are multiples of 2^-frac_bits (1 for half-star
+                           ratings); counters hold pref * 2^frac_bits.  Similarities are
+                           scale-invariant bit for bit; point queries / counters read back
+                           in preference units.  0 = integer preferences. */
+  int32_t reserved;
 } cms_params;
 
 typedef struct cms_handle cms_handle;
 
-/* Defaults: d=5, w=4096, u32, seed=42, n=0, unweighted, device -1. */
+/* Defaults: d=5, w=4096, u32, seed=42, n=0, unweighted, device -1, frac_bits 0. */
 int cms_params_init(cms_params* p);
 
 /* AbstractCountMinSketch(double delta, double epsilon, ...) shape rule

@@ -143,8 +143,9 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
         vals[base + j] = prefs.getValue(j);
       }
     }
-    long h = perOwner() ? nativeCreatePerOwner(seed, n, weighted, device)
-                        : nativeCreate(depth, width, seed, n, weighted, device);
+    int fracBits = fracBits(vals);
+    long h = perOwner() ? nativeCreatePerOwner(seed, n, weighted, device, fracBits)
+                        : nativeCreate(depth, width, seed, n, weighted, device, fracBits);
     try {
       nativeSetOwnerIds(h, ids);
       nativeIngestCsr(h, offsets, keys, vals);
@@ -169,6 +170,32 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     if (old != 0) {
       nativeDestroy(old);
     }
+  }
+
+  /**
+   * Smallest s with every preference * 2^s an integer (1 for half-star
+   * ratings): the library keeps counters in units of 2^-s, which leaves every
+   * similarity bit-identical and point queries in preference units.
+   */
+  static int fracBits(float[] vals) throws TasteException {
+    int s = 0;
+    for (float v : vals) {
+      if (v == 0.0f || Float.isNaN(v) || Float.isInfinite(v)) {
+        continue;  // non-finite values are refused by the library (CMS_E_VALUE)
+      }
+      int bits = Float.floatToIntBits(Math.abs(v));
+      int exp = ((bits >>> 23) & 0xff) - 150;  // v = mant * 2^exp with a 24-bit mant
+      int mant = (bits & 0x7fffff) | (((bits >>> 23) & 0xff) == 0 ? 0 : 0x800000);
+      if (((bits >>> 23) & 0xff) == 0) {
+        exp = -149;
+      }
+      exp += Integer.numberOfTrailingZeros(mant);
+      s = Math.max(s, -exp);
+    }
+    if (s > 31) {
+      throw new TasteException("preference values need more than 31 fractional bits");
+    }
+    return s;
   }
 
   /** CosineCM.userSimilarity (CosineCM.java:83-96). */
@@ -252,9 +279,9 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
 
   // --- JNI (integration/jni/mahout_cms_jni.c) --------------------------------
   private static native long nativeCreate(int depth, int width, long seed, long numOwners, boolean weighted,
-                                          int device) throws TasteException;
-  private static native long nativeCreatePerOwner(long seed, long numOwners, boolean weighted, int device)
-      throws TasteException;
+                                          int device, int fracBits) throws TasteException;
+  private static native long nativeCreatePerOwner(long seed, long numOwners, boolean weighted, int device,
+                                                  int fracBits) throws TasteException;
   private static native void nativeConfigureOwnerShapes(long h, double q, long numKeys) throws TasteException;
   private static native void nativeSetOwnerDeltaEpsilon(long h, double[] delta, double[] epsilon)
       throws TasteException;

@@ -37,7 +37,7 @@ static int fail(JNIEnv* env, int rc, int item_ids) {
 #define JFN(name) Java_org_apache_mahout_cf_taste_impl_similarity_CosineCMGpu_##name
 
 JNIEXPORT jlong JNICALL JFN(nativeCreate)(JNIEnv* env, jclass c, jint depth, jint width, jlong seed, jlong n,
-                                          jboolean weighted, jint device) {
+                                          jboolean weighted, jint device, jint frac_bits) {
   (void)c;
   cms_params p;
   cms_params_init(&p);
@@ -47,13 +47,14 @@ JNIEXPORT jlong JNICALL JFN(nativeCreate)(JNIEnv* env, jclass c, jint depth, jin
   p.num_owners = n;
   p.weighting = weighted ? CMS_WEIGHTED : CMS_UNWEIGHTED;
   p.device = device;
+  p.frac_bits = frac_bits;
   cms_handle* h = NULL;
   if (fail(env, cms_create(&p, &h), 0)) return 0;
   return (jlong)(intptr_t)h;
 }
 
 JNIEXPORT jlong JNICALL JFN(nativeCreatePerOwner)(JNIEnv* env, jclass c, jlong seed, jlong n, jboolean weighted,
-                                                  jint device) {
+                                                  jint device, jint frac_bits) {
   (void)c;
   cms_params p;
   cms_params_init(&p);
@@ -61,6 +62,7 @@ JNIEXPORT jlong JNICALL JFN(nativeCreatePerOwner)(JNIEnv* env, jclass c, jlong s
   p.num_owners = n;
   p.weighting = weighted ? CMS_WEIGHTED : CMS_UNWEIGHTED;
   p.device = device;
+  p.frac_bits = frac_bits;
   cms_handle* h = NULL;
   if (fail(env, cms_create_per_owner(&p, &h), 0)) return 0;
   return (jlong)(intptr_t)h;

@@ -53,6 +53,8 @@ class CmsParams(ctypes.Structure):
         ("num_owners", ctypes.c_int64),
         ("weighting", ctypes.c_int32),
         ("device", ctypes.c_int32),
+        ("frac_bits", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

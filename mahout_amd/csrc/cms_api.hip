@@ -192,6 +192,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   if (p->num_owners < 1 || p->num_owners > (int64_t(1) << 24))
     return set_error(CMS_E_PARAM, "num_owners must be in [1, 2^24]");
   if (p->counter_type != CMS_COUNTER_U32) return set_error(CMS_E_PARAM, "unsupported counter type");
+  if (p->frac_bits < 0 || p->frac_bits > 31) return set_error(CMS_E_PARAM, "frac_bits must be in [0, 31]");
   cms_handle* h = new (std::nothrow) cms_handle();
   if (!h) return set_error(CMS_E_OOM, "host allocation failed");
   h->p = *p;
@@ -224,6 +225,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   hp.pow2 = (h->p.width & (h->p.width - 1)) == 0;
   hp.wmask = hp.pow2 ? (uint32_t)(h->p.width - 1) : 0u;
   hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)h->p.width;
+  hp.frac_bits = p->frac_bits;
   if (per_owner) h->dw = 0;
 
   size_t tbytes = sizeof(uint32_t) * (size_t)h->n * (size_t)h->dw;
@@ -953,7 +955,7 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
     return CMS_OK;
   }
   CMS_HIP(hipMemcpy(tmp.data(), h->d_table + row_begin * h->dw, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < cnt; ++i) out[i] = (double)tmp[i];
+  for (size_t i = 0; i < cnt; ++i) out[i] = std::ldexp((double)tmp[i], -h->p.frac_bits);
   return CMS_OK;
 }
 
@@ -975,7 +977,7 @@ int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capaci
   for (int64_t r = 0; r < row; ++r) soff += (int64_t)h->h_po_w[r] * h->h_po_d[r];
   std::vector<uint32_t> tmp(w * d);
   CMS_HIP(hipMemcpy(tmp.data(), h->po_sk.as<uint32_t>() + soff, sizeof(uint32_t) * w * d, hipMemcpyDeviceToHost));
-  for (int64_t i = 0; i < w * d; ++i) out[i] = (double)tmp[i];
+  for (int64_t i = 0; i < w * d; ++i) out[i] = std::ldexp((double)tmp[i], -h->p.frac_bits);
   return CMS_OK;
 }
 

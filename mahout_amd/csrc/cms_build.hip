@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
       if (i < hi) {
         int64_t key = keys[i];
         uint32_t inc;
-        if (!load_inc(vals, i, inc)) {
+        if (!load_inc(vals, i, inc, hp.frac_bits)) {
           badv = true;
           inc = 0;
         }
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
           inc4[u] = 0;
           if (i < hi) {
             uint32_t inc;
-            if (!load_inc(vals, i, inc)) {
+            if (!load_inc(vals, i, inc, hp.frac_bits)) {
               badv = true;
               inc = 0;
             }

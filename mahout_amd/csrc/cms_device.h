@@ -5,14 +5,19 @@
 
 namespace cms {
 
-// Increment of pair i: 1 for implicit streams, else the float preference,
-// which u32 counters accept only as a non-negative integer < 2^32.
-__device__ __forceinline__ bool load_inc(const float* val, int64_t i, uint32_t& inc) {
+// Increment of pair i in counter units: 1 << fb for implicit streams, else the
+// float preference scaled by 2^fb (the handle's frac_bits), which u32 counters
+// accept only as a non-negative integer < 2^32.  Scaling by a power of two is
+// exact, and every fp64 quantity the reference derives from such counters
+// (sums of products, sqrt, products, quotients) scales exactly with it, so the
+// similarities are the reference's bit for bit and point queries are the
+// counter times 2^-fb.
+__device__ __forceinline__ bool load_inc(const float* val, int64_t i, uint32_t& inc, int fb) {
   if (val == nullptr) {
-    inc = 1u;
+    inc = 1u << fb;
     return true;
   }
-  float v = val[i];
+  float v = ldexpf(val[i], fb);
   if (!(v >= 0.0f) || v != floorf(v) || v >= 4294967296.0f) {
     inc = 0u;
     return false;

@@ -34,6 +34,7 @@ struct HashParams {
   uint32_t wmask;              // w-1 when w is a power of two
   int32_t depth;
   int32_t pow2;
+  int32_t frac_bits;           // counters hold preference * 2^frac_bits
 };
 
 // key mod p in [0, p) for any signed 64-bit key.

@@ -120,7 +120,7 @@ __global__ void k_map_ids(const int64_t* ids, int64_t n, const int64_t* sorted, 
 }
 
 // Pre-ingest validation of host-supplied batches (all-or-nothing ingest).
-__global__ void k_validate(const int64_t* rows, const float* val, int64_t n, int64_t nrows, uint32_t* flags) {
+__global__ void k_validate(const int64_t* rows, const float* val, int64_t n, int64_t nrows, int fb, uint32_t* flags) {
   uint32_t f = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (rows) {
@@ -128,7 +128,7 @@ __global__ void k_validate(const int64_t* rows, const float* val, int64_t n, int
       if (r < 0 || r >= nrows) f |= kFlagBadRow;
     }
     uint32_t inc;
-    if (val && !load_inc(val, i, inc)) f |= kFlagBadValue;
+    if (val && !load_inc(val, i, inc, fb)) f |= kFlagBadValue;
   }
   if (f) atomicOr(flags, f);
 }
@@ -136,7 +136,7 @@ __global__ void k_validate(const int64_t* rows, const float* val, int64_t n, int
 int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n) {
   if (n <= 0 || (!d_rows && !d_val)) return CMS_OK;
   unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_validate, dim3(grid), dim3(256), 0, h->stream, d_rows, d_val, n, h->n, h->d_flags);
+  hipLaunchKernelGGL(k_validate, dim3(grid), dim3(256), 0, h->stream, d_rows, d_val, n, h->n, h->hp.frac_bits, h->d_flags);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
@@ -167,7 +167,7 @@ __global__ void k_ingest_atomic(const int64_t* row, const int64_t* key, const fl
       continue;
     }
     uint32_t inc;
-    if (!load_inc(val, i, inc)) {
+    if (!load_inc(val, i, inc, hp.frac_bits)) {
       atomicOr(flags, kFlagBadValue);
       continue;
     }
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, cons
     uint64_t kp = 0;
     if (i < n) {
       r = rows[i];
-      if (!load_inc(val, i, inc)) {
+      if (!load_inc(val, i, inc, hp.frac_bits)) {
         atomicOr(flags, kFlagBadValue);
         inc = 0;
       }

@@ -102,12 +102,12 @@ __global__ __launch_bounds__(kCfgThreads) void k_po_config(const int64_t* off, i
 
 // ------------------------------------------------------------ DataModel --
 
-__global__ void k_po_prep(const int64_t* key, const float* val, int64_t np, uint64_t* kp, uint32_t* inc,
+__global__ void k_po_prep(const int64_t* key, const float* val, int64_t np, int fb, uint64_t* kp, uint32_t* inc,
                           uint32_t* flags) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
     kp[i] = reduce_key(key[i]);
     uint32_t v;
-    if (!load_inc(val, i, v)) atomicOr(flags, kFlagBadValue);
+    if (!load_inc(val, i, v, fb)) atomicOr(flags, kFlagBadValue);
     inc[i] = v;
   }
 }
@@ -268,7 +268,7 @@ __global__ void k_po_point(const PoShape* shp, const uint32_t* sk, HashParams hp
       const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, kp, (uint32_t)s.w, s.barrett)];
       if (v < est) est = v;
     }
-    out[i] = est;
+    out[i] = ldexp(est, -hp.frac_bits);
   }
 }
 
@@ -290,7 +290,7 @@ __global__ void k_po_estimate(const PoShape* shp, const uint32_t* sk, HashParams
         const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, kp, (uint32_t)s.w, s.barrett)];
         if (v < est) est = v;
       }
-      const float pref = (float)est;
+      const float pref = (float)ldexp(est, -hp.frac_bits);
       if (pref == 0.0f) continue;
       const double sim = sims[j];
       if (sim != sim) continue;
@@ -325,7 +325,7 @@ int po_load_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const
   CMS_HIP(hipMemcpyAsync(h->po_off.ptr, d_off, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, h->stream));
   if (npairs > 0)
     hipLaunchKernelGGL(k_po_prep, dim3(grid_for((npairs + 255) / 256, 8192)), dim3(256), 0, h->stream, d_key, d_val,
-                       npairs, h->po_kp.as<uint64_t>(), h->po_inc.as<uint32_t>(), h->d_flags);
+                       npairs, h->hp.frac_bits, h->po_kp.as<uint64_t>(), h->po_inc.as<uint32_t>(), h->d_flags);
   hipLaunchKernelGGL(k_po_mass, dim3(grid_for(n, 65536)), dim3(256), 0, h->stream, h->po_off.as<int64_t>(), n,
                      h->po_inc.as<uint32_t>(), h->d_flags);
   CMS_HIP(hipGetLastError());

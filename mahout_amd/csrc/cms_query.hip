@@ -117,7 +117,7 @@ __global__ void k_point_query(const uint32_t* table, HashParams hp, int64_t row,
       double v = (double)table[row * dw + (int64_t)d * hp.width + bucket(hp, d, kp)];
       if (v < est) est = v;
     }
-    out[i] = est;
+    out[i] = ldexp(est, -hp.frac_bits);
   }
 }
 
@@ -146,7 +146,7 @@ __global__ void k_estimate(const uint32_t* table, HashParams hp, int64_t user_ro
         const double v = (double)table[r * dw + bk[d]];
         if (v < est) est = v;
       }
-      const float pref = (float)est;
+      const float pref = (float)ldexp(est, -hp.frac_bits);
       if (pref == 0.0f) continue;
       const double s = sims[j];
       if (s != s) continue;

@@ -47,6 +47,19 @@ def shape_from_delta_epsilon(delta, epsilon):
     return w.value, d.value
 
 
+def frac_bits_for(values, max_bits=31):
+    """Smallest frac_bits with every value * 2^frac_bits an integer (the
+    preference granularity a u32 handle needs); ValueError when none <= max_bits."""
+    v = np.asarray(values, np.float32).astype(np.float64)
+    if v.size == 0:
+        return 0
+    for fb in range(max_bits + 1):
+        x = np.ldexp(v, fb)
+        if np.all(x == np.floor(x)):
+            return fb
+    raise ValueError("preference values need more than %d fractional bits" % max_bits)
+
+
 def shard_of_key(key, world):
     return _lib.load().cms_shard_of_key(int(key), int(world))
 
@@ -59,7 +72,7 @@ def comm_unique_id():
 
 class SketchTable:
     def __init__(self, num_owners, depth=5, width=4096, seed=42, weighted=False, device=-1, owner_ids=None,
-                 per_owner=False):
+                 per_owner=False, frac_bits=0):
         lib = _lib.load()
         p = _lib.CmsParams()
         check(lib.cms_params_init(ctypes.byref(p)))
@@ -69,6 +82,7 @@ class SketchTable:
         p.num_owners = num_owners
         p.weighting = _lib.CMS_WEIGHTED if weighted else _lib.CMS_UNWEIGHTED
         p.device = device
+        p.frac_bits = frac_bits
         h = ctypes.c_void_p()
         create = lib.cms_create_per_owner if per_owner else lib.cms_create
         check(create(ctypes.byref(p), ctypes.byref(h)))
@@ -260,10 +274,11 @@ class SketchTable:
 
     # -- per-owner shapes (CountMinSketchConfig) --
     @classmethod
-    def per_owner_shapes(cls, num_owners, seed=42, weighted=False, device=-1, owner_ids=None):
+    def per_owner_shapes(cls, num_owners, seed=42, weighted=False, device=-1, owner_ids=None, frac_bits=0):
         """A handle whose owners each carry their own (d, w): CosineCM with
         its CountMinSketchConfig (cms_create_per_owner)."""
-        return cls(num_owners, seed=seed, weighted=weighted, device=device, owner_ids=owner_ids, per_owner=True)
+        return cls(num_owners, seed=seed, weighted=weighted, device=device, owner_ids=owner_ids, per_owner=True,
+                   frac_bits=frac_bits)
 
     def configure_owner_shapes(self, q, num_keys):
         """CountMinSketchConfig(q).configure(dataModel) on the GPU."""

@@ -22,7 +22,7 @@ import numpy as np
 
 from . import _lib
 from .datamodel import NoSuchUserException
-from .sketch import SketchTable, shape_from_delta_epsilon
+from .sketch import SketchTable, frac_bits_for, shape_from_delta_epsilon
 
 
 class TasteException(Exception):
@@ -136,16 +136,22 @@ class CosineCM:
 
     def _build(self):
         m = self._model
+        # preference granularity: half-star ratings need 1 fractional bit, etc.
+        try:
+            fb = 0 if m.values is None else frac_bits_for(m.values)
+        except ValueError as e:
+            raise TasteException(str(e))
         try:
             if self._per_owner:
                 self._table = SketchTable.per_owner_shapes(m.getNumUsers(), seed=self._hfb.seed,
                                                            weighted=self._weighted, device=self._device,
-                                                           owner_ids=m.getUserIDs())
+                                                           owner_ids=m.getUserIDs(), frac_bits=fb)
                 self._table.ingest_csr(m.offsets, m.keys, m.values)
                 self._conf._configure(self._table, m)
             else:
                 self._table = SketchTable(m.getNumUsers(), depth=self.depth, width=self.width, seed=self._hfb.seed,
-                                          weighted=self._weighted, device=self._device, owner_ids=m.getUserIDs())
+                                          weighted=self._weighted, device=self._device, owner_ids=m.getUserIDs(),
+                                          frac_bits=fb)
                 self._table.ingest_csr(m.offsets, m.keys, m.values)
             self._table.finalize()
         except _lib.CmsError as e:

@@ -43,7 +43,8 @@ def test_params_init_defaults(lib):
     from mahout_amd._lib import CmsParams
     p = CmsParams()
     assert lib.cms_params_init(ctypes.byref(p)) == 0
-    assert p.struct_size == ctypes.sizeof(CmsParams) == 40
+    assert p.struct_size == ctypes.sizeof(CmsParams) == 48
+    assert p.frac_bits == 0
     assert (p.depth, p.width, p.seed, p.device) == (5, 4096, 42, -1)
 
 
@@ -104,3 +105,15 @@ def test_java_double_to_string(v, java):
     Double.toString layout (plain in [1e-3, 1e7), else d.dddE[-]n)."""
     from mahout_amd.sketch import java_double_to_string
     assert java_double_to_string(v) == java
+
+
+def test_frac_bits_for_preference_granularity():
+    """The smallest scale that makes every preference an integer (CPU only)."""
+    import numpy as np
+    from mahout_amd.sketch import frac_bits_for
+    assert frac_bits_for(np.array([1, 2, 5], np.float32)) == 0
+    assert frac_bits_for(np.array([1.5, 4.0, 0.5], np.float32)) == 1
+    assert frac_bits_for(np.array([0.25, 3.0], np.float32)) == 2
+    assert frac_bits_for(np.array([0.1], np.float32)) == 27  # 0.1f = 13421773 * 2^-27
+    with pytest.raises(ValueError):
+        frac_bits_for(np.array([1e-12], np.float32))

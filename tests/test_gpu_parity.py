@@ -90,6 +90,67 @@ def test_integer_values_and_bad_value(oracle):
         assert ei.value.code == CMS_E_VALUE
 
 
+@pytest.mark.parametrize("path", ["coo", "csr"])
+def test_fractional_preferences_scaled_counters(oracle, path):
+    """Half-star ratings (frac_bits 1) through both build paths and the atomic
+    path: counters read back in preference units, similarities, point queries
+    and estimates bit-exact against the oracle's plain fp64 accumulation."""
+    n, d, w = 400, 4, 512
+    items, users = zipf_stream(6000, n, 200_000, seed=21)
+    vals = (np.random.Generator(np.random.PCG64(2)).integers(1, 11, size=items.size) / 2.0).astype(np.float32)
+    exp = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42, frac_bits=1) as t:
+        if path == "coo":
+            t.ingest(items, users, vals)
+        else:
+            off, keys, v2 = to_csr(items, users, n, vals)
+            t.ingest_csr(off, keys, v2)
+        t.ingest(items[:1000], users[:1000], vals[:1000])  # small batch: the atomic path on a live table
+        t.finalize()
+        exp = oracle_table(oracle, n, d, w, 42, np.concatenate([items, items[:1000]]),
+                           np.concatenate([users, users[:1000]]), np.concatenate([vals, vals[:1000]]))
+        assert same(t.read_counters(), exp)
+        for q in [0, 7, 123]:
+            ref = _oracle_row_sims(oracle, exp, q)
+            ref[q] = oracle.cosine_cm(exp[q], exp[q])
+            assert same(t.similarities(q, np.arange(n)), ref)
+        a, b = oracle.hash_params(42, d)
+        for key in [int(users[0]), 5, -9]:
+            assert t.point_query(3, key) == oracle.sketch_get(exp[3], a, b, key)
+        nb, its = [5, 9, 3, 77], users[:40]
+        got = t.estimate_preferences(3, nb, its)
+        ref = np.array([oracle.estimate_preference(exp, a, b, 3, nb, int(k)) for k in its], np.float32)
+        assert same(got, ref)
+    with SketchTable(n, depth=d, width=w, seed=42, frac_bits=1) as t:
+        bad = vals.copy()
+        bad[77] = 0.25
+        with pytest.raises(CmsError) as ei:
+            t.ingest(items, users, bad)
+        assert ei.value.code == CMS_E_VALUE
+
+
+def test_float_preferences_like_tastetestcase(oracle):
+    """Arbitrary float preferences (0.1 .. 0.8, TasteTestCase's values): the
+    smallest exact scale frac_bits_for picks, similarities bit-exact."""
+    from mahout_amd.sketch import frac_bits_for
+    n, d, w = 50, 3, 64
+    rng = np.random.Generator(np.random.PCG64(4))
+    items = rng.integers(0, n, 600).astype(np.int64)
+    users = rng.integers(0, 40, 600).astype(np.int64)
+    vals = rng.choice(np.array([0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8], np.float32), 600)
+    fb = frac_bits_for(vals)
+    assert fb > 20
+    exp = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42, frac_bits=fb) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        assert same(t.read_counters(), exp)
+        for q in range(0, n, 7):
+            ref = _oracle_row_sims(oracle, exp, q)
+            ref[q] = oracle.cosine_cm(exp[q], exp[q])
+            assert same(t.similarities(q, np.arange(n)), ref)
+
+
 def test_owner_ids_and_errors(oracle):
     ids = np.array([-50, 3, 10, 11, 1000], np.int64)
     with SketchTable(5, depth=4, width=128, seed=42, owner_ids=ids) as t:
