@@ -228,9 +228,11 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   hp.frac_bits = p->frac_bits;
   if (per_owner) h->dw = 0;
 
-  size_t tbytes = sizeof(uint32_t) * (size_t)h->n * (size_t)h->dw;
+  size_t tbytes = sizeof(uint16_t) * (size_t)h->n * (size_t)h->dw;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
-      (!per_owner && (e = hipMalloc(&h->d_table, tbytes)) != hipSuccess) ||
+      (!per_owner && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
+      (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||
+      (!per_owner && (e = hipMemset(h->d_hidx, 0xff, sizeof(int32_t) * h->n)) != hipSuccess) ||
       (e = hipMalloc(&h->d_row_mass, sizeof(uint64_t) * h->n)) != hipSuccess ||
       (!per_owner && (e = hipMalloc(&h->d_norm, sizeof(uint64_t) * h->n * p->depth)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess) ||
@@ -261,7 +263,7 @@ void cms_destroy(cms_handle* h) {
     (void)hipEventDestroy(pe.stop);
   }
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  void* bufs[] = {h->d_table, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
+  void* bufs[] = {h->d_t16, h->d_hidx, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
@@ -270,7 +272,7 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
                   &h->ws_f4, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
-                  &h->po_scratch};
+                  &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -598,7 +600,8 @@ int cms_finalize(cms_handle* h) {
     return CMS_OK;
   }
   if (h->empty) {
-    CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * h->n * h->dw, h->stream));
+    CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * h->n * h->dw, h->stream));
+    if (int rc0 = reset_table_layout(h)) return rc0;
     h->empty = false;
     h->norms_valid = false;
   }
@@ -638,7 +641,8 @@ int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   if (h->comm) return set_error(CMS_E_STATE, "handle has an RCCL communicator: use cms_finalize");
   if (h->ext_merged) return set_error(CMS_E_STATE, "already merged: cms_reset starts a new epoch");
   if (h->empty) {
-    CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * h->n * h->dw, h->stream));
+    CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * h->n * h->dw, h->stream));
+    if (int rc0 = reset_table_layout(h)) return rc0;
     h->empty = false;
     h->norms_valid = false;
   }
@@ -948,14 +952,30 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
   Guard g(h);
   if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
   size_t cnt = (size_t)(row_count * h->dw);
-  std::vector<uint32_t> tmp(cnt);
   CMS_HIP(hipStreamSynchronize(h->stream));
   if (h->empty) {
     std::fill(out, out + cnt, 0.0);
     return CMS_OK;
   }
-  CMS_HIP(hipMemcpy(tmp.data(), h->d_table + row_begin * h->dw, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < cnt; ++i) out[i] = std::ldexp((double)tmp[i], -h->p.frac_bits);
+  // narrow rows straight from the u16 table, hot rows from their slots
+  std::vector<uint16_t> t16(cnt);
+  std::vector<int32_t> hidx(std::max<int64_t>(row_count, 1));
+  std::vector<uint32_t> hot((size_t)h->dw);
+  if (row_count > 0) {
+    CMS_HIP(hipMemcpy(t16.data(), h->d_t16 + row_begin * h->dw, sizeof(uint16_t) * cnt, hipMemcpyDeviceToHost));
+    CMS_HIP(hipMemcpy(hidx.data(), h->d_hidx + row_begin, sizeof(int32_t) * row_count, hipMemcpyDeviceToHost));
+  }
+  for (int64_t r = 0; r < row_count; ++r) {
+    double* o = out + r * h->dw;
+    if (hidx[r] >= 0) {
+      CMS_HIP(hipMemcpy(hot.data(), h->hot_tab.as<uint32_t>() + (int64_t)hidx[r] * h->dw, sizeof(uint32_t) * h->dw,
+                        hipMemcpyDeviceToHost));
+      for (int64_t j = 0; j < h->dw; ++j) o[j] = std::ldexp((double)hot[j], -h->p.frac_bits);
+    } else {
+      const uint16_t* s16 = t16.data() + r * h->dw;
+      for (int64_t j = 0; j < h->dw; ++j) o[j] = std::ldexp((double)s16[j], -h->p.frac_bits);
+    }
+  }
   return CMS_OK;
 }
 
@@ -990,7 +1010,8 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
-  out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes : (int64_t)sizeof(uint32_t) * h->n * h->dw;
+  out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
+                                   : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * h->hot_used * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;

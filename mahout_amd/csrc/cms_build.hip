@@ -52,13 +52,35 @@ __global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, i
   }
 }
 
-// Zero the table rows of hot owners (bulk build only); grid (max_hot, depth).
-__global__ __launch_bounds__(256) void k_zero_hot(const HotInfo* hot, const uint32_t* counters, HashParams hp,
-                                                  uint32_t* table) {
-  if (blockIdx.x >= counters[0]) return;
-  const int64_t dw = (int64_t)hp.depth * hp.width;
-  uint32_t* p = table + hot[blockIdx.x].row * dw + (int64_t)blockIdx.y * hp.width;
-  for (int j = threadIdx.x; j < (int)hp.width; j += blockDim.x) p[j] = 0u;
+// Upper bound of every counter of each row after the coming build (the row's
+// mass in counter units, old mass included when accumulating), and the rows
+// whose keys are split over several workgroups (their slices add with u32
+// atomics): both need a hot slot before the launch.
+__global__ void k_row_bound_implicit(const int64_t* off, int64_t nrows, int fb, int64_t slice, const uint64_t* old_mass,
+                                     uint64_t* bound, uint8_t* force) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = off[r + 1] - off[r];
+    bound[r] = ((uint64_t)c << fb) + (old_mass ? old_mass[r] : 0ULL);
+    force[r] = c > slice ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* off, const float* vals, int64_t nrows, int fb,
+                                                          int64_t slice, const uint64_t* old_mass, uint64_t* bound,
+                                                          uint8_t* force) {
+  __shared__ uint64_t red[4];
+  for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    uint64_t s = 0;
+    for (int64_t i = off[r] + threadIdx.x; i < off[r + 1]; i += 256) {
+      uint32_t inc;
+      if (load_inc(vals, i, inc, fb)) s += inc;  // bad values are flagged by the build itself
+    }
+    s = block_sum_u64_sat(s, red);
+    if (threadIdx.x == 0) {
+      bound[r] = sat_add(s, old_mass ? old_mass[r] : 0ULL);
+      force[r] = (off[r + 1] - off[r]) > slice ? 1 : 0;
+    }
+  }
 }
 
 // grid = emax + nrows: blocks [0, emax) build extra slices of hot owners (heavy
@@ -66,7 +88,7 @@ __global__ __launch_bounds__(256) void k_zero_hot(const HotInfo* hot, const uint
 __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
     const int64_t* off, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp, int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
-    uint32_t* table, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate) {
+    TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w]
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -93,7 +115,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
 #ifdef CMS_BUILD_NOKEYS  // bound analysis only: the write path alone
   hi = lo;
 #endif
-  uint32_t* dst = table + row * dw;
+  // a hot row (slot) is u32, any other row u16 (promote_rows ran before the launch)
+  const int32_t slot = tv.hidx[row];
+  uint32_t* dst = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
+  uint16_t* dst16 = tv.t16 + row * dw;
   const bool load_old = accumulate && !atomic_mode;
   if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
   if (tid == 0) {
@@ -127,14 +152,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
       }
     }
   }
-  // LDS slot for sketch row 0
-  if ((w & 3) == 0) {
-    uint4* l4 = reinterpret_cast<uint4*>(lds);
-    const uint4* s4 = reinterpret_cast<const uint4*>(dst);
-    for (int j = tid; j < (w >> 2); j += kBuildThreads) l4[j] = load_old ? s4[j] : make_uint4(0, 0, 0, 0);
-  } else {
-    for (int j = tid; j < w; j += kBuildThreads) lds[j] = load_old ? dst[j] : 0u;
-  }
+  // LDS slot for sketch row 0 (the old counters when accumulating)
+  for (int j = tid; j < w; j += kBuildThreads) lds[j] = load_old ? (dst ? dst[j] : (uint32_t)dst16[j]) : 0u;
   __syncthreads();
 
   for (int d = 0; d < hp.depth; ++d) {
@@ -170,24 +189,37 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
     }
     __syncthreads();
     // ---- write-out of row d, zero/load the slot for row d+1, sum of squares ----
-    uint32_t* dst_d = dst + (int64_t)d * w;
-    const uint32_t* nxt = (load_old && d + 1 < hp.depth) ? dst + (int64_t)(d + 1) * w : nullptr;
-    if (atomic_mode) {
+    const int64_t rofs = (int64_t)d * w;
+    const bool more = load_old && d + 1 < hp.depth;
+    if (atomic_mode) {  // slices of a split row: always a hot (u32) row
       for (int j = tid; j < w; j += kBuildThreads) {
         uint32_t v = lds[j];
         lds[j] = 0u;
-        if (v) atomicAdd(dst_d + j, v);
+        if (v) atomicAdd(dst + rofs + j, v);
       }
     } else {
       uint64_t sq = 0;
-      if ((w & 3) == 0) {
+      // 16-B u32 stores for slots, 8-B u16 stores for narrow rows (when the
+      // row offset keeps them aligned); the next sketch row's old counters
+      // are loaded into the slot as it is drained
+      const bool vec = (w & 3) == 0 && (dst != nullptr || ((row * dw) & 3) == 0);
+      if (vec) {
         uint4* l4 = reinterpret_cast<uint4*>(lds);
-        uint4* d4 = reinterpret_cast<uint4*>(dst_d);
-        const uint4* n4 = reinterpret_cast<const uint4*>(nxt);
         for (int j = tid; j < (w >> 2); j += kBuildThreads) {
-          uint4 v = l4[j];
-          l4[j] = nxt ? n4[j] : make_uint4(0, 0, 0, 0);
-          d4[j] = v;
+          const uint4 v = l4[j];
+          uint4 nv = make_uint4(0, 0, 0, 0);
+          if (more) {
+            if (dst) {
+              nv = reinterpret_cast<const uint4*>(dst + rofs + w)[j];
+            } else {
+              const ushort4 o = reinterpret_cast<const ushort4*>(dst16 + rofs + w)[j];
+              nv = make_uint4(o.x, o.y, o.z, o.w);
+            }
+          }
+          l4[j] = nv;
+          if (dst) reinterpret_cast<uint4*>(dst + rofs)[j] = v;
+          else reinterpret_cast<ushort4*>(dst16 + rofs)[j] = make_ushort4((unsigned short)v.x, (unsigned short)v.y,
+                                                                          (unsigned short)v.z, (unsigned short)v.w);
           vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
           sq = sat_add(sq, (uint64_t)v.x * v.x);
           sq = sat_add(sq, (uint64_t)v.y * v.y);
@@ -196,9 +228,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
         }
       } else {
         for (int j = tid; j < w; j += kBuildThreads) {
-          uint32_t v = lds[j];
-          lds[j] = nxt ? nxt[j] : 0u;
-          dst_d[j] = v;
+          const uint32_t v = lds[j];
+          lds[j] = more ? (dst ? dst[rofs + w + j] : (uint32_t)dst16[rofs + w + j]) : 0u;
+          if (dst) dst[rofs + j] = v;
+          else dst16[rofs + j] = (uint16_t)v;
           vmax = max(vmax, v);
           sq = sat_add(sq, (uint64_t)v * v);
         }
@@ -236,13 +269,13 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
 
 // Sum of squares of the hot rows after every slice landed; grid (max_hot, depth, chunks of 1024).
 __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uint32_t* counters, HashParams hp,
-                                                   const uint32_t* table, uint64_t* norm, uint32_t* rowmax) {
+                                                   TableView tv, uint64_t* norm, uint32_t* rowmax) {
   __shared__ uint64_t red[4];
   if (blockIdx.x >= counters[0]) return;
   const int64_t row = hot[blockIdx.x].row;
   const int d = blockIdx.y;
   const int w = (int)hp.width;
-  const uint32_t* p = table + row * (int64_t)hp.depth * w + (int64_t)d * w;
+  const uint32_t* p = tv.hot + (int64_t)tv.hidx[row] * tv.dw + (int64_t)d * w;  // split rows are slots
   uint64_t sq = 0;
   uint32_t vmax = 0;
   for (int j = blockIdx.z * 1024 + threadIdx.x; j < min(w, (int)(blockIdx.z + 1) * 1024); j += 256) {
@@ -257,8 +290,22 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
   if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
 }
 
+int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,
+               uint64_t* bound, uint8_t* force) {
+  const int64_t n = h->n;
+  if (d_val)
+    hipLaunchKernelGGL(k_row_bound_values, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(n, 65536))),
+                       dim3(256), 0, h->stream, d_off, d_val, n, h->hp.frac_bits, slice, old_mass, bound, force);
+  else
+    hipLaunchKernelGGL(k_row_bound_implicit, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))),
+                       dim3(256), 0, h->stream, d_off, n, h->hp.frac_bits, slice, old_mass, bound, force);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs) {
   const int64_t n = h->n;
+  int rc0;
   const int accumulate = h->empty ? 0 : 1;
   const int64_t max_hot = std::min<int64_t>(n, npairs / kSlice + 1);
   const int64_t emax = npairs / kSlice + 1;
@@ -272,28 +319,38 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
   int2* extra_map = reinterpret_cast<int2*>(base + sz_rowhot + sz_hot);
   uint32_t* counters = h->d_flags + 4;  // [4..7]
   CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
+  // table layout: rows that could reach 2^16, and split rows, get u32 slots
+  {
+    TimedScope ts(h, "build_plan");
+    if (!accumulate && (rc0 = reset_table_layout(h))) return rc0;
+    DevBuf& bound = h->ws_bound;
+    DevBuf& force = h->ws_force;
+    CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1)));
+    CMS_HIP(force.ensure((size_t)std::max<int64_t>(n, 1)));
+    if ((rc0 = row_bounds(h, d_off, d_val, accumulate ? h->d_row_mass : nullptr, kSlice, bound.as<uint64_t>(),
+                          force.as<uint8_t>())))
+      return rc0;
+    if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0))) return rc0;
+  }
   {
     TimedScope ts(h, "build_plan");
     unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
     hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_off, n, kSlice, row_hot, hot, extra_map,
                        counters, h->d_norm, h->d_rowmax, h->p.depth);
-    if (!accumulate)
-      hipLaunchKernelGGL(k_zero_hot, dim3((unsigned)max_hot, (unsigned)h->p.depth), dim3(256), 0, h->stream, hot,
-                         counters, h->hp, h->d_table);
     CMS_HIP(hipGetLastError());
   }
   const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
   {
     TimedScope ts(h, "build_rows");
     hipLaunchKernelGGL(k_build_rows, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_off, d_key,
-                       d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->d_table, h->d_row_mass,
+                       d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
                        h->d_norm, h->d_rowmax, h->d_flags, accumulate);
     CMS_HIP(hipGetLastError());
   }
   {
     TimedScope ts(h, "hot_norms");
     dim3 grid((unsigned)max_hot, (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
-    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->d_table, h->d_norm,
+    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
                        h->d_rowmax);
     CMS_HIP(hipGetLastError());
   }

@@ -83,14 +83,14 @@ __global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, co
 
 // Limb images in permuted order: limb0[p] = c & 127 for every owner;
 // hl[p][k-1] = (c >> 7k) & 127 for the multi-limb prefix p < n_multi.
-__global__ __launch_bounds__(256) void k_limb_write(const uint32_t* table, int64_t dw, const int64_t* perm,
+__global__ __launch_bounds__(256) void k_limb_write(TableView tv, int64_t dw, const int64_t* perm,
                                                     const uint8_t* rowLp, int64_t n_multi, int8_t* limb0, int8_t* hl) {
   const int64_t p = blockIdx.x;
-  const uint32_t* src = table + perm[p] * dw;
+  const int64_t row = perm[p];
   int8_t* dst = limb0 + p * dw;
   const int L = p < n_multi ? rowLp[p] : 1;
   for (int64_t j = threadIdx.x * 4; j < dw; j += 256 * 4) {
-    uint4 v = *reinterpret_cast<const uint4*>(src + j);
+    const uint4 v = tv.get4(row, j);
     *reinterpret_cast<char4*>(dst + j) = make_char4((signed char)(v.x & 127u), (signed char)(v.y & 127u),
                                                     (signed char)(v.z & 127u), (signed char)(v.w & 127u));
     for (int k = 1; k < L; ++k) {
@@ -104,16 +104,16 @@ __global__ __launch_bounds__(256) void k_limb_write(const uint32_t* table, int64
 
 // fp4 (e2m1) image of positions [f0, n): two counters per byte, low nibble
 // first.  Every counter is <= kF4Max, and 0..4 are exact e2m1 codes.
-__global__ __launch_bounds__(256) void k_f4_write(const uint32_t* table, int64_t dw, const int64_t* perm, int64_t f0,
+__global__ __launch_bounds__(256) void k_f4_write(TableView tv, int64_t dw, const int64_t* perm, int64_t f0,
                                                   uint8_t* f4) {
   const int64_t p = f0 + blockIdx.x;
-  const uint32_t* src = table + perm[p] * dw;
+  const int64_t row = perm[p];
   uint8_t* dst = f4 + (int64_t)blockIdx.x * (dw / 2);
   // e2m1: 0 -> 0x0, 1 -> 0x2 (1.0), 2 -> 0x4 (2.0), 3 -> 0x5 (3.0), 4 -> 0x6 (4.0)
   constexpr uint32_t kCode = 0x65420u;  // nibble c = code of value c
   for (int64_t j = threadIdx.x * 8; j < dw; j += 256 * 8) {
-    const uint4 v0 = *reinterpret_cast<const uint4*>(src + j);
-    const uint4 v1 = *reinterpret_cast<const uint4*>(src + j + 4);
+    const uint4 v0 = tv.get4(row, j);
+    const uint4 v1 = tv.get4(row, j + 4);
     auto code = [&](uint32_t c) { return (kCode >> (4 * c)) & 15u; };
     const uint32_t packed = code(v0.x) | code(v0.y) << 4 | code(v0.z) << 8 | code(v0.w) << 12 | code(v1.x) << 16 |
                             code(v1.y) << 20 | code(v1.z) << 24 | code(v1.w) << 28;
@@ -885,7 +885,7 @@ int cosine_prepare(cms_handle* h) {
     unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, fpos, fflag, rowL,
                        n, n_deep, n_multi, n_s8, perm, inv, rowLp);
-    hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->d_table, dw, perm, rowLp, n_multi,
+    hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->tview(), dw, perm, rowLp, n_multi,
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
                        tileL);
@@ -894,7 +894,7 @@ int cosine_prepare(cms_handle* h) {
                        h->ws_nsq.as<double>());
     if (n > f0) {
       CMS_HIP(h->ws_f4.ensure((size_t)(n - f0) * (size_t)(dw / 2)));
-      hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), 0, h->stream, h->d_table, dw, perm, f0,
+      hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), 0, h->stream, h->tview(), dw, perm, f0,
                          h->ws_f4.as<uint8_t>());
     }
     CMS_HIP(hipGetLastError());

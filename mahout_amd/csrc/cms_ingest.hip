@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 
 #include "cms_device.h"
 #include "cms_internal.h"
@@ -152,14 +153,40 @@ int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_row
 
 // ------------------------------------------------ small-batch atomic path --
 
+// counter c of row r += inc; returns the old value.  Narrow rows add into
+// their half of the aligned 32-bit word: promote_rows guarantees the row's
+// bound stays < 2^16, so no carry reaches the neighbouring half.
+__device__ __forceinline__ uint32_t table_add(const TableView& tv, int64_t r, int64_t c, uint32_t inc) {
+  const int32_t s = tv.hidx[r];
+  if (s >= 0) return atomicAdd(tv.hot + (int64_t)s * tv.dw + c, inc);
+  const int64_t g = r * tv.dw + c;
+  const uint32_t sh = (uint32_t)(g & 1) << 4;
+  const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(tv.t16) + (g >> 1), inc << sh);
+  return (old >> sh) & 0xffffu;
+}
+
+// batch mass per row (counter units) for the promotion check of unsorted batches
+__global__ void k_batch_mass(const int64_t* row, const float* val, int64_t n, int64_t nrows, int fb, uint64_t* delta) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = row[i];
+    uint32_t inc;
+    if (r < 0 || r >= nrows || !load_inc(val, i, inc, fb) || inc == 0) continue;
+    atomicAdd((unsigned long long*)&delta[r], (unsigned long long)inc);
+  }
+}
+
+__global__ void k_bound_from_delta(const uint64_t* delta, const uint64_t* mass, int64_t n, uint64_t* bound) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    bound[r] = delta[r] ? sat_add(delta[r], mass[r]) : 0ULL;
+}
+
 // With `track`, the norms and row maxima stay current: a counter moving from
 // c to c+inc adds 2*c*inc + inc^2 to its sum of squares, and the per-update
 // deltas telescope to the exact new sum whatever the atomic order.  A norm
 // reaching 2^53 (inexact fp64 regime) raises flags[2] so finalize recomputes.
 __global__ void k_ingest_atomic(const int64_t* row, const int64_t* key, const float* val, int64_t n, int64_t nrows,
-                                HashParams hp, uint32_t* table, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
+                                HashParams hp, TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
                                 int track, uint32_t* flags) {
-  const int64_t dw = (int64_t)hp.depth * hp.width;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = row[i];
     if (r < 0 || r >= nrows) {
@@ -173,10 +200,9 @@ __global__ void k_ingest_atomic(const int64_t* row, const int64_t* key, const fl
     }
     if (inc == 0) continue;
     uint64_t kp = reduce_key(key[i]);
-    uint32_t* sk = table + r * dw;
     uint32_t cmax = 0;
     for (int d = 0; d < hp.depth; ++d) {
-      uint32_t c = atomicAdd(sk + (int64_t)d * hp.width + bucket(hp, d, kp), inc);
+      uint32_t c = table_add(tv, r, (int64_t)d * hp.width + bucket(hp, d, kp), inc);
       if (track) {
         uint64_t delta = 2ULL * c * inc + (uint64_t)inc * inc;
         unsigned long long o = atomicAdd((unsigned long long*)&norm[r * hp.depth + d], (unsigned long long)delta);
@@ -206,11 +232,10 @@ __device__ __forceinline__ uint64_t seg_suffix_sum(uint64_t v, int32_t r, int la
 }
 
 __global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, const int64_t* key, const float* val,
-                                                        const int64_t* count, HashParams hp, uint32_t* table,
+                                                        const int64_t* count, HashParams hp, TableView tv,
                                                         uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
                                                         uint32_t* flags) {
   const int64_t n = *count;  // pairs that survived the partition's row check
-  const int64_t dw = (int64_t)hp.depth * hp.width;
   const int lane = threadIdx.x & 63;
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = base + threadIdx.x;
@@ -227,12 +252,11 @@ __global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, cons
     }
     const int32_t rprev = __shfl_up(r, 1, 64);
     const bool head = r >= 0 && (lane == 0 || rprev != r);
-    uint32_t* sk = table + (int64_t)(r < 0 ? 0 : r) * dw;
     uint32_t cmax = 0;
     for (int d = 0; d < hp.depth; ++d) {
       uint64_t delta = 0;
       if (inc) {
-        uint32_t c = atomicAdd(sk + (int64_t)d * hp.width + bucket(hp, d, kp), inc);
+        uint32_t c = table_add(tv, r, (int64_t)d * hp.width + bucket(hp, d, kp), inc);
         delta = 2ULL * c * inc + (uint64_t)inc * inc;
         cmax = max(cmax, c + inc);
       }
@@ -259,21 +283,19 @@ __global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, cons
 
 // --------------------------------------------------------- norms pass ----
 
-__global__ __launch_bounds__(256) void k_norms(const uint32_t* table, int64_t nrows, HashParams hp, uint64_t* norm,
+__global__ __launch_bounds__(256) void k_norms(TableView tv, int64_t nrows, HashParams hp, uint64_t* norm,
                                                uint32_t* rowmax) {
   __shared__ uint64_t red[4];
   __shared__ uint32_t smax[4];
-  const int64_t dw = (int64_t)hp.depth * hp.width;
   const int w = (int)hp.width;
   for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
     uint32_t vmax = 0;
     for (int d = 0; d < hp.depth; ++d) {
-      const uint32_t* p = table + row * dw + (int64_t)d * w;
+      const int64_t c0 = (int64_t)d * w;
       uint64_t sq = 0;
       if ((w & 3) == 0) {
-        const uint4* p4 = reinterpret_cast<const uint4*>(p);
         for (int j = threadIdx.x; j < (w >> 2); j += blockDim.x) {
-          uint4 v = p4[j];
+          const uint4 v = tv.get4(row, c0 + 4 * j);
           vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
           sq = sat_add(sq, (uint64_t)v.x * v.x);
           sq = sat_add(sq, (uint64_t)v.y * v.y);
@@ -282,8 +304,9 @@ __global__ __launch_bounds__(256) void k_norms(const uint32_t* table, int64_t nr
         }
       } else {
         for (int j = threadIdx.x; j < w; j += blockDim.x) {
-          sq = sat_add(sq, (uint64_t)p[j] * p[j]);
-          vmax = max(vmax, p[j]);
+          const uint32_t v = tv.get(row, c0 + j);
+          sq = sat_add(sq, (uint64_t)v * v);
+          vmax = max(vmax, v);
         }
       }
       uint64_t tot = block_sum_u64_sat(sq, red);
@@ -311,7 +334,7 @@ __global__ void k_norm_sqrt(const uint64_t* norm, int64_t cells, double* out, ui
 int local_norms(cms_handle* h) {
   const unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
   if (grid > 0)
-    hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->n, h->hp, h->d_norm, h->d_rowmax);
+    hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->n, h->hp, h->d_norm, h->d_rowmax);
   CMS_HIP(hipGetLastError());
   h->norms_valid = true;
   return CMS_OK;
@@ -326,7 +349,7 @@ int compute_norms(cms_handle* h) {
   if (!h->norms_valid) {
     CMS_HIP(hipMemsetAsync(h->d_flags + 2, 0, sizeof(uint32_t), h->stream));
     unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
-    if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->n, h->hp, h->d_norm,
+    if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->n, h->hp, h->d_norm,
                                      h->d_rowmax);
     CMS_HIP(hipGetLastError());
     h->norms_valid = true;
@@ -370,25 +393,52 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
       CMS_HIP(h->ws_srow.ensure(sizeof(int32_t) * (size_t)npairs));
       int rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &coff, &ckey, &cval, h->ws_srow.as<int32_t>());
       if (rc) return rc;
+      {  // rows this batch could lift to 2^16 move to u32 slots first
+        DevBuf& bound = h->ws_bound;
+        DevBuf& force = h->ws_force;
+        CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)n));
+        CMS_HIP(force.ensure((size_t)n));
+        if ((rc = row_bounds(h, coff, cval, h->d_row_mass, INT64_MAX, bound.as<uint64_t>(), force.as<uint8_t>())))
+          return rc;
+        if ((rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true))) return rc;
+      }
       TimedScope ts(h, "ingest_atomic");
       unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
       hipLaunchKernelGGL(k_ingest_sorted, dim3(grid), dim3(256), 0, h->stream, h->ws_srow.as<int32_t>(), ckey, cval,
-                         coff + n, h->hp, h->d_table, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+                         coff + n, h->hp, h->tview(), h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       CMS_HIP(hipGetLastError());
       return CMS_OK;
     }
     TimedScope ts(h, "ingest_atomic");
     if (h->empty) {
-      CMS_HIP(hipMemsetAsync(h->d_table, 0, sizeof(uint32_t) * (size_t)(n * h->dw), h->stream));
+      CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * (size_t)(n * h->dw), h->stream));
+      int rc = reset_table_layout(h);
+      if (rc) return rc;
       CMS_HIP(hipMemsetAsync(h->d_row_mass, 0, sizeof(uint64_t) * (size_t)n, h->stream));
       CMS_HIP(hipMemsetAsync(h->d_norm, 0, sizeof(uint64_t) * (size_t)(n * h->p.depth), h->stream));
       CMS_HIP(hipMemsetAsync(h->d_rowmax, 0, sizeof(uint32_t) * (size_t)n, h->stream));
       h->norms_valid = true;
     }
+    {  // rows this batch could lift to 2^16 move to u32 slots first
+      DevBuf& delta = h->ws_partials;  // scratch reused: [n] batch masses
+      DevBuf& bound = h->ws_bound;
+      CMS_HIP(delta.ensure(sizeof(uint64_t) * (size_t)n));
+      CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)n));
+      CMS_HIP(hipMemsetAsync(delta.ptr, 0, sizeof(uint64_t) * (size_t)n, h->stream));
+      const unsigned gp = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
+      const unsigned gn = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+      hipLaunchKernelGGL(k_batch_mass, dim3(gp), dim3(256), 0, h->stream, d_row, d_val, npairs, n, h->hp.frac_bits,
+                         delta.as<uint64_t>());
+      hipLaunchKernelGGL(k_bound_from_delta, dim3(gn), dim3(256), 0, h->stream, delta.as<uint64_t>(), h->d_row_mass, n,
+                         bound.as<uint64_t>());
+      CMS_HIP(hipGetLastError());
+      int rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true);
+      if (rc) return rc;
+    }
     const int track = h->norms_valid ? 1 : 0;
     unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
     hipLaunchKernelGGL(k_ingest_atomic, dim3(grid), dim3(256), 0, h->stream, d_row, d_key, d_val, npairs, n, h->hp,
-                       h->d_table, h->d_row_mass, h->d_norm, h->d_rowmax, track, h->d_flags);
+                       h->tview(), h->d_row_mass, h->d_norm, h->d_rowmax, track, h->d_flags);
     CMS_HIP(hipGetLastError());
     h->empty = false;
     return CMS_OK;

@@ -60,6 +60,32 @@ struct PendingEvent {
   hipEvent_t start, stop;
 };
 
+// The sketch table.  A counter never exceeds its owner's total increment
+// (row mass), so rows whose mass bound is below 2^16 are stored as u16 and
+// only the others ("hot" rows: mass >= 2^16, or split over several build
+// workgroups) get a u32 row in the slot table -- at config 2 that halves the
+// bytes the row build writes.  Writers promote a row to a slot before its
+// bound can reach 2^16 (promote_rows), so a u16 counter never overflows.
+constexpr uint64_t kNarrowLimit = 1ULL << 16;
+
+struct TableView {
+  uint16_t* t16;        // [n][dw] narrow rows
+  uint32_t* hot;        // [hot_cap][dw] u32 rows
+  const int32_t* hidx;  // [n] slot of a hot row, -1 for a narrow one
+  int64_t dw;
+  __device__ __forceinline__ uint32_t get(int64_t row, int64_t j) const {
+    const int32_t s = hidx[row];
+    return s >= 0 ? hot[(int64_t)s * dw + j] : (uint32_t)t16[row * dw + j];
+  }
+  // counters j..j+3 of a row (j % 4 == 0 and dw % 4 == 0: aligned vector loads)
+  __device__ __forceinline__ uint4 get4(int64_t row, int64_t j) const {
+    const int32_t s = hidx[row];
+    if (s >= 0) return *reinterpret_cast<const uint4*>(hot + (int64_t)s * dw + j);
+    const ushort4 v = *reinterpret_cast<const ushort4*>(t16 + row * dw + j);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+};
+
 // Row-build tuning: pairs per build work item.
 constexpr int64_t kSlice = 32768;
 #ifndef CMS_BUILD_THREADS
@@ -81,7 +107,14 @@ struct cms_handle {
 
   int64_t n = 0;       // rows
   int64_t dw = 0;      // d*w counters per row
-  uint32_t* d_table = nullptr;      // [n][d][w]
+  uint16_t* d_t16 = nullptr;        // [n][d][w] narrow counters
+  int32_t* d_hidx = nullptr;        // [n] hot slot or -1
+  cms::DevBuf hot_tab;              // [hot_cap][d][w] u32 counters of the hot rows
+  cms::DevBuf ws_bound, ws_force, ws_plist;  // promotion scratch: u64 [n], u8 [n], i32 [n] + count
+  int64_t hot_cap = 0, hot_used = 0;
+  cms::TableView tview() const {
+    return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw};
+  }
   uint64_t* d_row_mass = nullptr;   // [n] total increment mass per row
   uint64_t* d_norm = nullptr;       // [n][d] exact sum of squares (saturating)
   double* d_norm_sqrt = nullptr;    // [n][d] Math.sqrt((double) norm)
@@ -185,6 +218,17 @@ int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_row
 int compute_norms(cms_handle* h);
 // norms + row maxima of the local table (k_norms)
 int local_norms(cms_handle* h);
+// Every row whose bound[r] (a u64 upper bound of its counters after the
+// coming write, in counter units; or any row with force[r]) reaches 2^16
+// gets a hot slot; copy_old copies its narrow counters into the slot (else the
+// slot is zeroed).  bound may be null when only force is used.
+int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old);
+// per-row counter bounds after a CSR batch (mass in counter units + old_mass)
+// and the rows split over more than `slice` keys (cms_build.hip)
+int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,
+               uint64_t* bound, uint8_t* force);
+// all rows narrow and zero-able again (empty table)
+int reset_table_layout(cms_handle* h);
 // ---- cms_merge.hip ----
 // in-place u64 sum over all ranks of count words of a device buffer
 using AllReduceU64 = std::function<int(uint64_t*, int64_t)>;

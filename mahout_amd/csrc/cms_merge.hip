@@ -50,19 +50,21 @@ struct PackLayout {
 // One workgroup per owner.  Field f of the owner's word i holds counter
 // f*NW + i (NW = the owner's word count): both the pack's reads and the
 // unpack's word reads are then consecutive across the lanes of a wave.
-__global__ __launch_bounds__(256) void k_merge_pack(const uint32_t* table, int64_t n, int64_t dw, PackLayout L,
+__global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int64_t dw, PackLayout L,
                                                    uint64_t* words) {
   for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
     const int b = L.bits[o];
     if (b == 0) continue;
     const int F = 64 / b;
     const int64_t w0 = L.woff[o], nw = L.woff[o + 1] - w0;
-    const uint32_t* src = table + o * dw;
+    const int32_t slot = tv.hidx[o];
+    const uint32_t* s32 = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
+    const uint16_t* s16 = tv.t16 + o * dw;
     for (int64_t i = threadIdx.x; i < nw; i += 256) {
       uint64_t wv = 0;
       for (int f = 0; f < F; ++f) {
         const int64_t idx = (int64_t)f * nw + i;
-        if (idx < dw) wv |= (uint64_t)src[idx] << (f * b);
+        if (idx < dw) wv |= (uint64_t)(s32 ? s32[idx] : (uint32_t)s16[idx]) << (f * b);
       }
       words[w0 + i] = wv;
     }
@@ -72,16 +74,21 @@ __global__ __launch_bounds__(256) void k_merge_pack(const uint32_t* table, int64
 // Merged words -> u32 table, with the exact per-row sum of squares and the
 // owner's largest counter (as k_norms computes them).
 __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int64_t n, HashParams hp, PackLayout L,
-                                                      uint32_t* table, uint64_t* norm, uint32_t* rowmax) {
+                                                      TableView tv, uint64_t* norm, uint32_t* rowmax) {
   __shared__ uint64_t red[4];
   __shared__ uint32_t smax[4];
   const int w = (int)hp.width;
   const int64_t dw = (int64_t)hp.depth * w;
   for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
     const int b = L.bits[o];
-    uint32_t* dst = table + o * dw;
+    const int32_t slot = tv.hidx[o];  // rows whose merged mass reaches 2^16 were promoted
+    uint32_t* dst = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
+    uint16_t* dst16 = tv.t16 + o * dw;
     if (b == 0) {  // every rank's counters of this owner are zero
-      for (int64_t i = threadIdx.x; i < dw; i += 256) dst[i] = 0u;
+      for (int64_t i = threadIdx.x; i < dw; i += 256) {
+        if (dst) dst[i] = 0u;
+        else dst16[i] = 0;
+      }
       if (threadIdx.x < hp.depth) norm[o * hp.depth + threadIdx.x] = 0;
       if (threadIdx.x == 0) rowmax[o] = 0;
       continue;
@@ -96,7 +103,8 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
         const uint32_t idx = (uint32_t)(d * w + j);
         const uint32_t f = idx / nw, wi = idx - f * nw;
         const uint32_t c = (uint32_t)((src[wi] >> (f * (uint32_t)b)) & mask);
-        dst[idx] = c;
+        if (dst) dst[idx] = c;
+        else dst16[idx] = (uint16_t)c;
         sq = sat_add(sq, (uint64_t)c * c);
         vmax = max(vmax, c);
       }
@@ -157,17 +165,19 @@ int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
   const unsigned go = (unsigned)std::min<int64_t>(n, 65536);
   {
     TimedScope ts(h, "merge_pack");
-    hipLaunchKernelGGL(k_merge_pack, dim3(go), dim3(256), 0, h->stream, h->d_table, n, dw, L, packed.as<uint64_t>());
+    hipLaunchKernelGGL(k_merge_pack, dim3(go), dim3(256), 0, h->stream, h->tview(), n, dw, L, packed.as<uint64_t>());
     CMS_HIP(hipGetLastError());
   }
   {
     TimedScope ts(h, "allreduce");
     if (words > 0 && (rc = allreduce(packed.as<uint64_t>(), words))) return rc;
   }
+  // rows whose merged mass reaches 2^16 need u32 slots (row_mass is merged)
+  if ((rc = promote_rows(h, h->d_row_mass, nullptr, false))) return rc;
   {
     TimedScope ts(h, "merge_unpack");
     hipLaunchKernelGGL(k_merge_unpack, dim3(go), dim3(256), 0, h->stream, packed.as<uint64_t>(), n, h->hp, L,
-                       h->d_table, h->d_norm, h->d_rowmax);
+                       h->tview(), h->d_norm, h->d_rowmax);
     CMS_HIP(hipGetLastError());
   }
   CMS_HIP(hipStreamSynchronize(h->stream));  // scratch is freed on return

@@ -29,12 +29,13 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 
 // Reference-order sequential fp64 sums for one sketch row (inexact regime).
-__device__ void seq_row_sums(const uint32_t* a, const uint32_t* b, int w, double& A, double& B, double& AB) {
+__device__ void seq_row_sums(const TableView& tv, int64_t ra, int64_t rb, int64_t c0, int w, double& A, double& B,
+                             double& AB) {
   A = 0.0;
   B = 0.0;
   AB = 0.0;
   for (int j = 0; j < w; ++j) {
-    double xa = (double)a[j], xb = (double)b[j];
+    double xa = (double)tv.get(ra, c0 + j), xb = (double)tv.get(rb, c0 + j);
     A = __dadd_rn(A, __dmul_rn(xa, xa));
     B = __dadd_rn(B, __dmul_rn(xb, xb));
     AB = __dadd_rn(AB, __dmul_rn(xa, xb));
@@ -42,7 +43,7 @@ __device__ void seq_row_sums(const uint32_t* a, const uint32_t* b, int w, double
 }
 
 // One workgroup (256 threads) per (query, target) pair.
-__global__ __launch_bounds__(256) void k_pair_cosine(const uint32_t* table, const uint64_t* norm, const double* nsqrt,
+__global__ __launch_bounds__(256) void k_pair_cosine(TableView tv, const uint64_t* norm, const double* nsqrt,
                                                      HashParams hp, int64_t q_row, const int64_t* rows, int64_t m,
                                                      int64_t nrows, int weighted, double* out) {
   __shared__ uint64_t red[4];
@@ -54,27 +55,21 @@ __global__ __launch_bounds__(256) void k_pair_cosine(const uint32_t* table, cons
     return;
   }
   const int w = (int)hp.width;
-  const int64_t dw = (int64_t)hp.depth * w;
-  const uint32_t* pa = table + q_row * dw;
-  const uint32_t* pb = table + r2 * dw;
   double minc = DBL_MAX;
   for (int d = 0; d < hp.depth; ++d) {
-    const uint32_t* ra = pa + (int64_t)d * w;
-    const uint32_t* rb = pb + (int64_t)d * w;
+    const int64_t c0 = (int64_t)d * w;
     const uint64_t Na = norm[q_row * hp.depth + d], Nb = norm[r2 * hp.depth + d];
     const bool exact = Na < (1ULL << 53) && Nb < (1ULL << 53);
     double valueAB, den;
     if (exact) {
       uint64_t dot = 0;
       if ((w & 3) == 0) {
-        const uint4* a4 = reinterpret_cast<const uint4*>(ra);
-        const uint4* b4 = reinterpret_cast<const uint4*>(rb);
         for (int j = threadIdx.x; j < (w >> 2); j += 256) {
-          uint4 x = a4[j], y = b4[j];
+          const uint4 x = tv.get4(q_row, c0 + 4 * j), y = tv.get4(r2, c0 + 4 * j);
           dot += (uint64_t)x.x * y.x + (uint64_t)x.y * y.y + (uint64_t)x.z * y.z + (uint64_t)x.w * y.w;
         }
       } else {
-        for (int j = threadIdx.x; j < w; j += 256) dot += (uint64_t)ra[j] * rb[j];
+        for (int j = threadIdx.x; j < w; j += 256) dot += (uint64_t)tv.get(q_row, c0 + j) * tv.get(r2, c0 + j);
       }
       dot = wave_sum_u64(dot);
       if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dot;
@@ -85,7 +80,7 @@ __global__ __launch_bounds__(256) void k_pair_cosine(const uint32_t* table, cons
       den = __dmul_rn(nsqrt[q_row * hp.depth + d], nsqrt[r2 * hp.depth + d]);
     } else {
       double A, B;
-      seq_row_sums(ra, rb, w, A, B, valueAB);  // every thread (uniform result)
+      seq_row_sums(tv, q_row, r2, c0, w, A, B, valueAB);  // every thread (uniform result)
       den = __dmul_rn(__dsqrt_rn(A), __dsqrt_rn(B));
     }
     if (den != 0.0) minc = java_min(minc, __ddiv_rn(valueAB, den));
@@ -100,21 +95,20 @@ __global__ __launch_bounds__(256) void k_pair_cosine(const uint32_t* table, cons
 int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out) {
   if (m <= 0) return CMS_OK;
   TimedScope ts(h, "pair_cosine");
-  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), 0, h->stream, h->d_table, h->d_norm,
+  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), 0, h->stream, h->tview(), h->d_norm,
                      h->d_norm_sqrt, h->hp, q_row, d_rows, m, h->n, (int)h->p.weighting, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
 // DoubleCountMinSketch.get(key) (:94-103): min over rows, from Double.MAX_VALUE.
-__global__ void k_point_query(const uint32_t* table, HashParams hp, int64_t row, const int64_t* keys, int64_t m,
+__global__ void k_point_query(TableView tv, HashParams hp, int64_t row, const int64_t* keys, int64_t m,
                               double* out) {
-  const int64_t dw = (int64_t)hp.depth * hp.width;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t kp = reduce_key(keys[i]);
     double est = DBL_MAX;
     for (int d = 0; d < hp.depth; ++d) {
-      double v = (double)table[row * dw + (int64_t)d * hp.width + bucket(hp, d, kp)];
+      double v = (double)tv.get(row, (int64_t)d * hp.width + bucket(hp, d, kp));
       if (v < est) est = v;
     }
     out[i] = ldexp(est, -hp.frac_bits);
@@ -128,10 +122,9 @@ __global__ void k_point_query(const uint32_t* table, HashParams hp, int64_t row,
 // sim = userSimilarity(user, neighbour) (NaN skipped), preference += sim*pref,
 // total += sim; < 2 points -> NaN; (float)(preference/total); then the
 // EstimatedPreferenceCapper clamp when enabled.
-__global__ void k_estimate(const uint32_t* table, HashParams hp, int64_t user_row, const int64_t* nb_rows,
+__global__ void k_estimate(TableView tv, HashParams hp, int64_t user_row, const int64_t* nb_rows,
                            const double* sims, int64_t m, const int64_t* items, int64_t q, int use_capper, float lo,
                            float hi, float* out) {
-  const int64_t dw = (int64_t)hp.depth * hp.width;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < q; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t kp = reduce_key(items[i]);
     uint32_t bk[CMS_MAX_DEPTH];
@@ -143,7 +136,7 @@ __global__ void k_estimate(const uint32_t* table, HashParams hp, int64_t user_ro
       if (r == user_row) continue;
       double est = DBL_MAX;
       for (int d = 0; d < hp.depth; ++d) {
-        const double v = (double)table[r * dw + bk[d]];
+        const double v = (double)tv.get(r, bk[d]);
         if (v < est) est = v;
       }
       const float pref = (float)ldexp(est, -hp.frac_bits);
@@ -170,7 +163,7 @@ int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_ro
                          const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out) {
   if (q <= 0) return CMS_OK;
   unsigned grid = (unsigned)std::min<int64_t>((q + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_estimate, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->hp, user_row, d_nb_rows, d_sims,
+  hipLaunchKernelGGL(k_estimate, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->hp, user_row, d_nb_rows, d_sims,
                      m, d_items, q, use_capper, lo, hi, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
@@ -179,7 +172,7 @@ int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_ro
 int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
   if (m <= 0) return CMS_OK;
   unsigned grid = (unsigned)std::min<int64_t>((m + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_point_query, dim3(grid), dim3(256), 0, h->stream, h->d_table, h->hp, row, d_keys, m, d_out);
+  hipLaunchKernelGGL(k_point_query, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->hp, row, d_keys, m, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

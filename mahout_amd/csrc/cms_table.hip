@@ -1,0 +1,78 @@
+// cms_table.hip -- layout of the sketch table: u16 narrow rows + u32 hot slots.
+//
+// DoubleCountMinSketch keeps fp64 counters (T/impl/common/DoubleCountMinSketch.java:21);
+// with integer increments every counter is an integer no larger than its
+// owner's total increment (the row mass).  Rows whose mass stays below 2^16
+// -- at config 2 all but the ~70 head items of the Zipf stream -- are stored
+// as u16, the rest in a growable table of u32 rows ("hot slots").  A writer
+// that could lift a row's mass to 2^16 promotes the row first (promote_rows),
+// so no u16 counter can overflow and every stored value is the exact counter.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "cms_internal.h"
+
+namespace cms {
+
+__global__ void k_promote_list(const uint64_t* bound, const uint8_t* force, const int32_t* hidx, int64_t n,
+                               uint32_t* cnt, int32_t* list) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    if (hidx[r] >= 0) continue;
+    const bool need = (bound && bound[r] >= kNarrowLimit) || (force && force[r]);
+    if (need) list[atomicAdd(cnt, 1u)] = (int32_t)r;
+  }
+}
+
+// one workgroup per promoted row: slot base + i, old narrow counters copied (or zeros)
+__global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64_t count, int64_t base, TableView tv,
+                                                      int32_t* hidx, int copy_old) {
+  for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const int64_t r = list[i];
+    const int64_t slot = base + i;
+    uint32_t* dst = tv.hot + slot * tv.dw;
+    const uint16_t* src = tv.t16 + r * tv.dw;
+    for (int64_t j = threadIdx.x; j < tv.dw; j += 256) dst[j] = copy_old ? (uint32_t)src[j] : 0u;
+    if (threadIdx.x == 0) hidx[r] = (int32_t)slot;
+  }
+}
+
+int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old) {
+  const int64_t n = h->n;
+  CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
+  int32_t* list = h->ws_plist.as<int32_t>();
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(list + n);
+  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_promote_list, dim3(g), dim3(256), 0, h->stream, d_bound, d_force, h->d_hidx, n, cnt, list);
+  CMS_HIP(hipGetLastError());
+  uint32_t c = 0;
+  CMS_HIP(hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (c == 0) return CMS_OK;
+  const int64_t need = h->hot_used + c;
+  if (need > h->hot_cap) {  // grow: new slot table, live slots copied over
+    const int64_t cap = std::min<int64_t>(n, std::max<int64_t>({need, h->hot_cap + h->hot_cap / 2, 64}));
+    DevBuf nb;
+    CMS_HIP(nb.ensure(sizeof(uint32_t) * (size_t)cap * (size_t)h->dw));
+    if (h->hot_used > 0)
+      CMS_HIP(hipMemcpyAsync(nb.ptr, h->hot_tab.ptr, sizeof(uint32_t) * (size_t)h->hot_used * (size_t)h->dw,
+                             hipMemcpyDeviceToDevice, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    h->hot_tab = std::move(nb);
+    h->hot_cap = cap;
+  }
+  hipLaunchKernelGGL(k_promote_rows, dim3((unsigned)std::min<int64_t>(c, 65536)), dim3(256), 0, h->stream, list,
+                     (int64_t)c, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
+  CMS_HIP(hipGetLastError());
+  h->hot_used = need;
+  return CMS_OK;
+}
+
+int reset_table_layout(cms_handle* h) {
+  CMS_HIP(hipMemsetAsync(h->d_hidx, 0xff, sizeof(int32_t) * (size_t)h->n, h->stream));
+  h->hot_used = 0;
+  return CMS_OK;
+}
+
+}  // namespace cms

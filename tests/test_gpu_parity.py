@@ -151,6 +151,49 @@ def test_float_preferences_like_tastetestcase(oracle):
             assert same(t.similarities(q, np.arange(n)), ref)
 
 
+@pytest.mark.parametrize("frac_bits", [0, 2])
+def test_narrow_and_hot_rows_at_the_u16_boundary(oracle, frac_bits):
+    """Rows whose mass stays below 2^16 are stored as u16, the others in u32
+    slots.  Row 0 ends the bulk build at counter 65535 (narrow), row 1 at
+    65540 (hot); small batches then push row 0 to 2^16 (promotion on the atomic
+    path), keep row 2 narrow, and a big accumulate batch promotes row 3."""
+    n, d, w = 6, 2, 64
+    sc = 2.0 ** -frac_bits
+    rows = np.concatenate([np.zeros(13107, np.int64), np.ones(13108, np.int64), np.full(500, 2, np.int64),
+                           np.full(5000, 3, np.int64)])
+    keys = np.concatenate([np.full(13107, 7, np.int64), np.full(13108, 9, np.int64), np.arange(500, dtype=np.int64),
+                           np.arange(5000, dtype=np.int64) % 50])
+    vals = np.concatenate([np.full(13107, 5, np.float32), np.full(13108, 5, np.float32), np.ones(500, np.float32),
+                           np.ones(5000, np.float32)]) * np.float32(sc)
+    batches = [(rows, keys, vals)]
+    with SketchTable(n, depth=d, width=w, seed=42, frac_bits=frac_bits) as t:
+        off, ck, cv = to_csr(rows, keys, n, vals)
+        t.ingest_csr(off, ck, cv)  # the LDS row build (bulk path)
+        t.finalize()
+        assert same(t.read_counters(), oracle_table(oracle, n, d, w, 42, rows, keys, vals))
+        assert t.stats()["table_bytes"] < n * d * w * 4  # mostly narrow
+        b2 = (np.array([0, 2, 2], np.int64), np.array([7, 1, 2], np.int64), np.full(3, sc, np.float32))
+        t.ingest(*b2)  # atomic path: row 0 reaches 65536 in counter units
+        batches.append(b2)
+        big_r = np.concatenate([np.full(300_000, 3, np.int64), np.full(1000, 5, np.int64)])
+        big_k = np.concatenate([np.arange(300_000, dtype=np.int64) % 97, np.arange(1000, dtype=np.int64)])
+        big_v = np.full(big_r.size, sc, np.float32)
+        t.ingest(big_r, big_k, big_v)  # accumulate build (or sorted atomics): row 3 becomes hot
+        batches.append((big_r, big_k, big_v))
+        t.finalize()
+        exp = oracle_table(oracle, n, d, w, 42, np.concatenate([b[0] for b in batches]),
+                           np.concatenate([b[1] for b in batches]), np.concatenate([b[2] for b in batches]))
+        assert same(t.read_counters(), exp)
+        assert exp[0].max() == 65536 * sc and exp[1].max() == 65540 * sc
+        for q in range(n):
+            ref = _oracle_row_sims(oracle, exp, q)
+            ref[q] = oracle.cosine_cm(exp[q], exp[q])
+            assert same(t.similarities(q, np.arange(n)), ref)
+        a, b = oracle.hash_params(42, d)
+        for r in range(n):
+            assert t.point_query(r, 7) == oracle.sketch_get(exp[r], a, b, 7)
+
+
 def test_owner_ids_and_errors(oracle):
     ids = np.array([-50, 3, 10, 11, 1000], np.int64)
     with SketchTable(5, depth=4, width=128, seed=42, owner_ids=ids) as t:
