@@ -24,6 +24,10 @@
 
 namespace cms {
 
+#ifdef CMS_BUILD_CHEAPHASH  // bound analysis only: a trivial hash instead of the exact mod-p one
+#define bucket(hp, d, kp) ((uint32_t)(((kp) >> (d)) & (hp).wmask))
+#endif
+
 struct HotInfo {
   int64_t row;
   int32_t nslices;
@@ -101,6 +105,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
   bool atomic_mode;
   if (blockIdx.x < emax) {
     if (blockIdx.x >= counters[2]) return;
+#ifdef CMS_BUILD_NOSLICES  // bound analysis only: hot rows' extra slices skipped
+    return;
+#endif
     int2 m = extra_map[blockIdx.x];
     row = hot[m.x].row;
     lo = off[row] + (int64_t)m.y * slice;
@@ -217,6 +224,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_rows(
             }
           }
           l4[j] = nv;
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+          if (v.x == 0xFFFFFFFFu)
+#endif
           if (dst) reinterpret_cast<uint4*>(dst + rofs)[j] = v;
           else reinterpret_cast<ushort4*>(dst16 + rofs)[j] = make_ushort4((unsigned short)v.x, (unsigned short)v.y,
                                                                           (unsigned short)v.z, (unsigned short)v.w);
