@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* off, co
 
 // grid = emax + nrows: blocks [0, emax) build extra slices of hot owners (heavy
 // work first), blocks [emax, emax + nrows) one owner each (slice 0 if hot).
-__global__ __launch_bounds__(kBuildThreads) void k_build_rows(
+__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_rows(
     const int64_t* off, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp, int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
     TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate) {
