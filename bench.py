@@ -150,12 +150,12 @@ def cosine_cpu_baseline(items, users, n, d, w, budget_s=10.0, sample_owners=192,
                       f"fp64 sketches for {budget_s / 2:.0f} s"}
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, name="pmc_summary.json"):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/<round>/pmc_summary.json, scripts/profile.sh on this bench command:
     2 * FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name)))
     if not files:
         return None, None
     data = json.load(open(files[-1]))
@@ -303,6 +303,7 @@ def cosine_1m(args, local, device, rank=0, world=1):
     job_f4 = nf * (nf - 1) / 2 * 2 * d * w
     job_peak = alg_ops / (job_f4 / FP4_MFMA_PEAK_TOPS + (alg_ops - job_f4) / INT8_MFMA_PEAK_TOPS)
     wave_ach = wave_ops / (waves_ms * 1e-3) / 1e12 if waves_ms else None
+    cos_traffic = pmc_traffic("void cms::k_cosine_big<3, 1, 128, 1>", "cosine_pmc_summary.json")
     t.close()
     return {
         "workload": f"configs 3+4: {npairs}-pair Zipf stream -> {n}-item table (d={d} w={w}), user-hash sharded over "
@@ -322,7 +323,8 @@ def cosine_1m(args, local, device, rank=0, world=1):
                      "frac": f4_ops / (f4_ms * 1e-3) / 1e12 / FP4_MFMA_PEAK_TOPS if f4_ms else None,
                      "avg_launch_ms": f4_ms / f4_n if f4_n else None,
                      "algorithmic_ops_per_launch": f4_ops / f4_n if f4_n else None,
-                     "traffic": None},
+                     "traffic": cos_traffic[0], "traffic_unit": "bytes per launch (2 x FETCH_SIZE)",
+                     "traffic_source": cos_traffic[1]},
         "roofline_int8_waves": {"bound": "mfma", "kernel": "k_cosine_big<3,1,128,0> (int8 symmetric waves)",
                                 "achieved": i8_ops / (i8_ms * 1e-3) / 1e12 if i8_ms else None,
                                 "peak": INT8_MFMA_PEAK_TOPS, "unit": "TOP/s",
