@@ -210,7 +210,23 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       // row offset keeps them aligned); the next sketch row's old counters
       // are loaded into the slot as it is drained
       const bool vec = (w & 3) == 0 && (dst != nullptr || ((row * dw) & 3) == 0);
-      if (vec) {
+      if (vec && !dst && !more) {
+        // narrow row, fresh build (the common case): every counter < 2^16, so
+        // the squares are full-rate 24-bit products and no sum can saturate
+        uint4* l4 = reinterpret_cast<uint4*>(lds);
+        uint2* d2 = reinterpret_cast<uint2*>(dst16 + rofs);
+        for (int j = tid; j < (w >> 2); j += kBuildThreads) {
+          const uint4 v = l4[j];
+          l4[j] = make_uint4(0, 0, 0, 0);
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+          if (v.x == 0xFFFFFFFFu)
+#endif
+          d2[j] = make_uint2(v.x | (v.y << 16), v.z | (v.w << 16));
+          vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
+          sq += (uint64_t)__umul24(v.x, v.x) + __umul24(v.y, v.y);
+          sq += (uint64_t)__umul24(v.z, v.z) + __umul24(v.w, v.w);
+        }
+      } else if (vec) {
         uint4* l4 = reinterpret_cast<uint4*>(lds);
         for (int j = tid; j < (w >> 2); j += kBuildThreads) {
           const uint4 v = l4[j];
