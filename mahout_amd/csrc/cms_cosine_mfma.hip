@@ -20,6 +20,7 @@
 // Tile: 128 x 128 outputs per 256-thread workgroup (2 x 2 waves, each 64 x 64
 // = 2 x 2 MFMA 32x32 tiles), K staged 128 bytes per row per stage through a
 // double-buffered, XOR-swizzled LDS image (conflict-free ds_read_b128).
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -490,6 +491,7 @@ struct BigArgs {
   // of blocks (njc J-chunks per I-block), so the ~32 workgroups an XCD runs
   // together share si A panels and sj B blocks instead of 1 and 16-32
   int32_t rect, si, sj, njc;
+  int32_t noscreen;  // 1: exact epilogue for every pair (A/B of the screening)
 };
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -540,6 +542,10 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   const int depth = g.depth;
   double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][256] (OA used)
   double* s_sb = s_sa + depth * kTA;                                 // [depth][128]
+  // candidate mode: the panels' admission thresholds as fp16 rounded toward
+  // -inf ([256] A owners, [128] B rows), for the fp32 screening epilogue
+  __half* s_ta = reinterpret_cast<__half*>(s_sb + depth * kTB);
+  __half* s_tb = s_ta + kTA;
   const int nblk = g.nblk;
   const int bx = blockIdx.x, xcd = bx & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
@@ -630,6 +636,22 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
   }
 
+  // Screening (candidate mode, unweighted, single-limb): once a pair's fp32
+  // estimate of one row cosine is below both owners' thresholds by more than
+  // its error bound, min over rows can only be lower, so the pair can never
+  // be admitted and its exact fp64 epilogue is skipped; a wave runs the exact
+  // epilogue only while one of its pairs is still alive.
+  const bool screen = g.cval != nullptr && !g.weighted && LS == 1 && !g.noscreen;
+  if (screen) {
+    for (int i = tid; i < kTA + kTB; i += 512) {
+      const bool isA = i < kTA;
+      const int64_t o = isA ? own0 + i : bcol0 + (i - kTA);
+      const int64_t lim = isA ? a_owners : b_rows;
+      const double t = o < lim ? g.thr[(isA ? a_pos0 : b_pos0) + o] : __builtin_inf();
+      (isA ? s_ta : s_tb - kTA)[i] = __float2half_rd(__double2float_rd(t));  // never above the threshold
+    }
+  }
+
   // buffer descriptors bound the panel: rows past the end land as zeros
   const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, a_vrows - vrow0));
   const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, b_rows - bcol0));
@@ -666,6 +688,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
 
   AccT acc[2][2];
   double mn[2][2][4 * OG];
+  uint64_t alive = ~0ULL;  // bit (i*2+j)*16 + og*4 + q: the pair may still be admitted
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -717,6 +740,35 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
       double sb[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) sb[j] = s_sb[r * kTB + wc * 64 + j * 32 + (lane & 31)];
+      if (screen) {
+        // fp32 estimate AB / (sa * sb): relative error < 2^-20 (exact AB < 2^27
+        // and two conversions, one v_rcp_f32 (1 ulp) and two products)
+        float rb[2], tb[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          rb[j] = __builtin_amdgcn_rcpf((float)sb[j]);
+          tb[j] = __half2float(s_tb[wc * 64 + j * 32 + (lane & 31)]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int og = 0; og < OG; ++og)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int ol = (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
+              const float sa = (float)s_sa[r * kTA + ol];
+              const float ra = __builtin_amdgcn_rcpf(sa);
+              const float ta = __half2float(s_ta[ol]);
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const int bit = (i * 2 + j) * 16 + og * 4 + q;
+                const float est = (float)acc[i][j][q + 4 * og] * ra * rb[j];
+                const bool dead = sa != 0.0f && (float)sb[j] != 0.0f && est < fminf(ta, tb[j]) - 4e-6f;
+                if (dead) alive &= ~(1ULL << bit);
+              }
+            }
+      }
+      if (!screen || __any(alive != 0ULL)) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -727,6 +779,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
             const double sa = s_sa[r * kTA + ol];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
+              if (screen && !((alive >> ((i * 2 + j) * 16 + og * 4 + q)) & 1ULL)) continue;
               double valueAB;
               if constexpr (LS == 1) {
                 valueAB = (double)acc[i][j][q + 4 * og];
@@ -742,11 +795,14 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
               m = (den != 0.0 && v < m) ? v : m;
             }
           }
+      }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
-      }
     }
   }
 
@@ -764,6 +820,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
         for (int q = 0; q < 4; ++q) {
           const int64_t ai = own0 + (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
           if (ai >= a_owners || bi >= b_rows) continue;
+          if (screen && !((alive >> ((i * 2 + j) * 16 + og * 4 + q)) & 1ULL)) continue;  // never admitted
           const int64_t ap = a_pos0 + ai;
           double rr = mn[i][j][og * 4 + q];
           rr = rr == DBL_MAX ? __builtin_nan("") : rr;
@@ -945,7 +1002,7 @@ struct BigCfg {
 
 static BigCfg big_config(cms_handle* h) {
   BigCfg c;
-  c.norms = (size_t)h->p.depth * (kTA + kTB) * sizeof(double);
+  c.norms = (size_t)h->p.depth * (kTA + kTB) * sizeof(double) + (kTA + kTB) * sizeof(__half);
   constexpr size_t kLdsMax = 160 * 1024;
   // 128-B K slices (one cache line per row) in a 3- or 2-deep ring; 64-B
   // slices in a 6-deep ring measured slower (twice the line requests per
@@ -1021,6 +1078,7 @@ static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t
 
 static BigArgs big_base(cms_handle* h) {
   BigArgs b{};
+  b.noscreen = getenv("CMS_NO_SCREEN") ? 1 : 0;
 #ifdef CMS_BOUND_ANALYSIS
   if (const char* m = getenv("CMS_COS_MODE")) b.mode = atoi(m);
 #endif
