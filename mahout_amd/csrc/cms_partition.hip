@@ -22,9 +22,80 @@
 namespace cms {
 
 constexpr int kPartThreads = 512;
-constexpr int kPartPer = 8;
+#ifndef CMS_PART_PER
+#define CMS_PART_PER 8
+#endif
+constexpr int kPartPer = CMS_PART_PER;  // pairs per thread per tile
 constexpr int kPartTile = kPartThreads * kPartPer;  // pairs staged per tile
 constexpr int kMaxBins = 4096;
+
+// aggregation rounds per LDS histogram (lds_bin_add); 0 = plain atomics
+#ifndef CMS_PEEL_P1H
+#define CMS_PEEL_P1H 0
+#endif
+#ifndef CMS_PEEL_P1S
+#define CMS_PEEL_P1S 0
+#endif
+#ifndef CMS_PEEL_P2H
+#define CMS_PEEL_P2H 1
+#endif
+#ifndef CMS_PEEL_P2S
+#define CMS_PEEL_P2S 0
+#endif
+// fine bits of the two-pass split (pass 2 fan-out 2^CMS_PART_S2)
+#ifndef CMS_PART_S2
+#define CMS_PART_S2 10
+#endif
+// pass-1 stream chunks (workgroups) for large batches
+#ifndef CMS_P1_BLOCKS
+#define CMS_P1_BLOCKS 2048
+#endif
+// issue the next tile's loads before this tile's write-out
+#ifndef CMS_P1_PREFETCH
+#define CMS_P1_PREFETCH 1
+#endif
+#ifndef CMS_P2_PREFETCH
+#define CMS_P2_PREFETCH 1
+#endif
+
+// LDS histogram increment aggregated across the wave.  Zipf streams put most
+// lanes of a wave on the same few bins (the head items: 3/4 of config 2's
+// pairs fall in coarse bin 0), and same-address LDS atomics serialise lane by
+// lane.  kPeel times, the pending lanes that share the bin of the lowest
+// pending lane are counted by one atomic of their population count; the rest
+// then increment one by one.  With kRank the lane's rank within its bin is
+// returned (unique and contiguous per bin, as a plain atomicAdd's would be).
+// Call from converged code: the ballots see only the active lanes.
+template <int kPeel, bool kRank>
+__device__ __forceinline__ uint32_t lds_bin_add(uint32_t* hist, uint32_t bin, bool active) {
+  uint32_t rank = 0;
+  bool pending = active;
+  const int lane = (int)__lane_id();
+#pragma unroll
+  for (int r = 0; r < kPeel; ++r) {
+    const unsigned long long pm = __ballot(pending);
+    if (pm == 0ULL) return rank;
+    const int lead = __builtin_ctzll(pm);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, lead);
+    const bool mine = pending && bin == b0;
+    const unsigned long long m = __ballot(mine);
+    uint32_t base = 0;
+    if (lane == lead) {
+      if (kRank) base = atomicAdd(&hist[b0], (uint32_t)__popcll(m));
+      else atomicAdd(&hist[b0], (uint32_t)__popcll(m));
+    }
+    if (kRank) {
+      base = (uint32_t)__builtin_amdgcn_readlane((int)base, lead);
+      if (mine) rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    }
+    pending = pending && !mine;
+  }
+  if (pending) {
+    if (kRank) rank = atomicAdd(&hist[bin], 1u);
+    else atomicAdd(&hist[bin], 1u);
+  }
+  return rank;
+}
 
 __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, int64_t chunk, int s2, int P1,
                                                  int64_t nrows, uint32_t* H1, int NB, uint32_t* flags) {
@@ -42,12 +113,26 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
   }
   const int64_t npair = (hi - lo2) / 2;
   const longlong2* r2 = reinterpret_cast<const longlong2*>(row + lo2);
-  for (int64_t i = threadIdx.x; i < npair; i += blockDim.x) {
-    longlong2 v = r2[i];
-    if (v.x < 0 || v.x >= nrows) bad = true;
-    else atomicAdd(&lh[(uint32_t)(v.x >> s2)], 1u);
-    if (v.y < 0 || v.y >= nrows) bad = true;
-    else atomicAdd(&lh[(uint32_t)(v.y >> s2)], 1u);
+  // whole waves step together so the aggregated increments see converged
+  // lanes; four 16-byte loads in flight per lane
+  constexpr int kU = 4;
+  const int64_t span = (int64_t)blockDim.x * kU;
+  const int64_t nstep = (npair + span - 1) / span * span;
+  for (int64_t i0 = threadIdx.x; i0 < nstep; i0 += span) {
+    longlong2 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      v[u] = i < npair ? r2[i] : longlong2{-1, -1};
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const bool in = i0 + (int64_t)u * blockDim.x < npair;
+      const bool okx = v[u].x >= 0 && v[u].x < nrows, oky = v[u].y >= 0 && v[u].y < nrows;
+      if (in && (!okx || !oky)) bad = true;
+      lds_bin_add<CMS_PEEL_P1H, false>(lh, okx ? (uint32_t)(v[u].x >> s2) : 0u, okx);
+      lds_bin_add<CMS_PEEL_P1H, false>(lh, oky ? (uint32_t)(v[u].y >> s2) : 0u, oky);
+    }
   }
   if (threadIdx.x == 0 && lo2 + 2 * npair < hi) {
     int64_t r = row[hi - 1];
@@ -57,6 +142,14 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
   if (bad) atomicOr(flags, kFlagBadRow);
   __syncthreads();
   for (int b = threadIdx.x; b < P1; b += blockDim.x) H1[(int64_t)b * NB + blockIdx.x] = lh[b];
+}
+
+// Workgroup barrier that orders LDS only: global loads issued before it stay
+// in flight (__syncthreads would drain them with its vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // Exclusive scan of hist[0..P) into off[] by the whole block (P <= 4096).
@@ -85,21 +178,28 @@ struct TileLds {
   uint32_t* scr;
 };
 
-__device__ __forceinline__ TileLds carve(unsigned char* smem, int P) {
+// LDS image of a tile: keys, then values and fine indices only when the pass
+// carries them (a smaller image lets more workgroups share a CU).
+__device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_val, bool has_fine) {
   TileLds t;
-  t.key = reinterpret_cast<int64_t*>(smem);
-  t.val = reinterpret_cast<float*>(t.key + kPartTile);
-  t.fine = reinterpret_cast<uint16_t*>(t.val + kPartTile);
-  t.bin = t.fine + kPartTile;
-  t.cursor = reinterpret_cast<uint32_t*>(t.bin + kPartTile);
+  unsigned char* q = smem;
+  t.key = reinterpret_cast<int64_t*>(q);
+  q += sizeof(int64_t) * kPartTile;
+  t.val = reinterpret_cast<float*>(q);
+  if (has_val) q += sizeof(float) * kPartTile;
+  t.fine = reinterpret_cast<uint16_t*>(q);
+  if (has_fine) q += sizeof(uint16_t) * kPartTile;
+  t.bin = reinterpret_cast<uint16_t*>(q);
+  q += sizeof(uint16_t) * kPartTile;
+  t.cursor = reinterpret_cast<uint32_t*>(q);
   t.hist = t.cursor + P;
   t.off = t.hist + P;
   t.scr = t.off + P;
   return t;
 }
 
-static size_t tile_lds_bytes(int P) {
-  return (size_t)kPartTile * (8 + 4 + 2 + 2) + (size_t)3 * P * 4 + 64 * 4;
+static size_t tile_lds_bytes(int P, bool has_val, bool has_fine) {
+  return (size_t)kPartTile * (8 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4;
 }
 
 // Pass 1: block b owns stream chunk [b*chunk, (b+1)*chunk); output region of
@@ -109,56 +209,79 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
                                                              const uint32_t* O1, int NB, uint16_t* ofine,
                                                              int64_t* okey, float* oval) {
   extern __shared__ __align__(16) unsigned char smem[];
-  TileLds L = carve(smem, P1);
+  TileLds L = carve(smem, P1, val != nullptr, true);
   const int tid = threadIdx.x;
   for (int b = tid; b < P1; b += kPartThreads) L.cursor[b] = O1[(int64_t)b * NB + blockIdx.x];
   const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   const uint32_t fmask = (1u << s2) - 1u;
+  for (int b = tid; b < P1; b += kPartThreads) L.hist[b] = 0;
+  // software pipeline: the next tile's loads are issued before this tile's
+  // write-out and stay in flight across the LDS-only barriers
+  int64_t rr[kPartPer], kk[kPartPer];
+  float vv[kPartPer];
+  auto load = [&](int64_t tb) {
+#pragma unroll
+    for (int u = 0; u < kPartPer; ++u) {
+      const int64_t e = tb + tid + (int64_t)u * kPartThreads;
+      rr[u] = -1;
+      if (e < hi) {
+        rr[u] = row[e];
+        kk[u] = key[e];
+        vv[u] = val ? val[e] : 0.f;
+      }
+    }
+  };
+  if (lo < hi) load(lo);
+  __syncthreads();
   for (int64_t tb = lo; tb < hi; tb += kPartTile) {
-    for (int b = tid; b < P1; b += kPartThreads) L.hist[b] = 0;
-    __syncthreads();
-    int64_t kk[kPartPer];
-    float vv[kPartPer];
+#if !CMS_P1_PREFETCH
+    if (tb != lo) load(tb);
+#endif
     uint32_t bb[kPartPer], rk[kPartPer];
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
-      int64_t e = tb + tid + (int64_t)u * kPartThreads;
-      rk[u] = 0xFFFFFFFFu;
-      if (e < hi) {
-        int64_t r = row[e];
-        kk[u] = key[e];
-        vv[u] = val ? val[e] : 0.f;
-        if (r >= 0 && r < nrows) {
-          bb[u] = (uint32_t)r;
-          rk[u] = atomicAdd(&L.hist[(uint32_t)(r >> s2)], 1u);
-        }
-      }
+      const bool ok = rr[u] >= 0 && rr[u] < nrows;
+      bb[u] = ok ? (uint32_t)rr[u] : 0u;
+      const uint32_t q = lds_bin_add<CMS_PEEL_P1S, true>(L.hist, bb[u] >> s2, ok);
+      rk[u] = ok ? q : 0xFFFFFFFFu;
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t cnt = scan_bins(L.hist, L.off, P1, L.scr);
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
       if (rk[u] != 0xFFFFFFFFu) {
         uint32_t bin = bb[u] >> s2;
         uint32_t p = L.off[bin] + rk[u];
         L.key[p] = kk[u];
-        L.val[p] = vv[u];
+        if (val) L.val[p] = vv[u];
         L.fine[p] = (uint16_t)(bb[u] & fmask);
         L.bin[p] = (uint16_t)bin;
       }
     }
-    __syncthreads();
+#if CMS_P1_PREFETCH
+    if (tb + kPartTile < hi) load(tb + kPartTile);
+#endif
+    lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t bin = L.bin[i];
       uint32_t g = L.cursor[bin] + (i - L.off[bin]);
+#ifdef CMS_PART_LINEAR  // bound analysis only: contiguous instead of per-bin destinations
+      g = (uint32_t)(tb + i);
+#endif
+#ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
+      if (g != 0xFFFFFFFFu) continue;
+#endif
       okey[g] = L.key[i];
       ofine[g] = L.fine[i];
       if (oval) oval[g] = L.val[i];
     }
-    __syncthreads();
-    for (int b = tid; b < P1; b += kPartThreads) L.cursor[b] += L.hist[b];
-    __syncthreads();
+    lds_barrier();
+    for (int b = tid; b < P1; b += kPartThreads) {
+      L.cursor[b] += L.hist[b];
+      L.hist[b] = 0;
+    }
+    lds_barrier();
   }
 }
 
@@ -212,7 +335,24 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
   __syncthreads();
   int64_t lo = binStart[b] + (int64_t)(blockIdx.x - blkStart[b]) * CH2;
   int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) atomicAdd(&lh[fine[i]], 1u);
+  // 8 fine indices per 16-byte load; the unaligned head and tail one by one
+  const int64_t a0 = min(hi, (lo + 7) & ~int64_t(7));
+  const int64_t nv = (hi - a0) / 8;
+  const int64_t a1 = a0 + nv * 8;
+  if ((int64_t)threadIdx.x < a0 - lo) atomicAdd(&lh[fine[lo + threadIdx.x]], 1u);
+  if ((int64_t)threadIdx.x < hi - a1) atomicAdd(&lh[fine[a1 + threadIdx.x]], 1u);
+  const uint4* f8 = reinterpret_cast<const uint4*>(fine + a0);
+  const int64_t nstep = (nv + blockDim.x - 1) / blockDim.x * blockDim.x;
+  for (int64_t i = threadIdx.x; i < nstep; i += blockDim.x) {
+    const bool in = i < nv;
+    const uint4 v = in ? f8[i] : make_uint4(0, 0, 0, 0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      lds_bin_add<CMS_PEEL_P2H, false>(lh, w[c] & 0xFFFFu, in);
+      lds_bin_add<CMS_PEEL_P2H, false>(lh, w[c] >> 16, in);
+    }
+  }
   __syncthreads();
   for (int f = threadIdx.x; f < P2; f += blockDim.x) H2[(int64_t)blockIdx.x * P2 + f] = lh[f];
 }
@@ -279,52 +419,76 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t nblk = blkStart[P1];
   if (blockIdx.x >= nblk) return;
-  TileLds L = carve(smem, P2);
+  TileLds L = carve(smem, P2, val1 != nullptr, false);
   const int tid = threadIdx.x;
   const int b = find_bin(blkStart, P1, blockIdx.x);
   for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] = O2[(int64_t)blockIdx.x * P2 + f];
   const int64_t lo = binStart[b] + (int64_t)(blockIdx.x - blkStart[b]) * CH2;
   const int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
-  for (int64_t tb = lo; tb < hi; tb += kPartTile) {
-    for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
-    __syncthreads();
-    int64_t kk[kPartPer];
-    float vv[kPartPer];
-    uint32_t ff[kPartPer], rk[kPartPer];
+  for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
+  int64_t kk[kPartPer];
+  float vv[kPartPer];
+  uint32_t ff[kPartPer];
+  auto load = [&](int64_t tb) {
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
-      int64_t e = tb + tid + (int64_t)u * kPartThreads;
-      rk[u] = 0xFFFFFFFFu;
+      const int64_t e = tb + tid + (int64_t)u * kPartThreads;
+      ff[u] = 0xFFFFFFFFu;
       if (e < hi) {
         ff[u] = fine[e];
         kk[u] = key1[e];
         vv[u] = val1 ? val1[e] : 0.f;
-        rk[u] = atomicAdd(&L.hist[ff[u]], 1u);
       }
     }
-    __syncthreads();
+  };
+  if (lo < hi) load(lo);
+  __syncthreads();
+  for (int64_t tb = lo; tb < hi; tb += kPartTile) {
+#if !CMS_P2_PREFETCH
+    if (tb != lo) load(tb);
+#endif
+    uint32_t rk[kPartPer];
+#pragma unroll
+    for (int u = 0; u < kPartPer; ++u) {
+      const bool ok = ff[u] != 0xFFFFFFFFu;
+      const uint32_t q = lds_bin_add<CMS_PEEL_P2S, true>(L.hist, ok ? ff[u] : 0u, ok);
+      rk[u] = ok ? q : 0xFFFFFFFFu;
+    }
+    lds_barrier();
     const uint32_t cnt = scan_bins(L.hist, L.off, P2, L.scr);
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
       if (rk[u] != 0xFFFFFFFFu) {
         uint32_t p = L.off[ff[u]] + rk[u];
         L.key[p] = kk[u];
-        L.val[p] = vv[u];
+        if (val1) L.val[p] = vv[u];
         L.bin[p] = (uint16_t)ff[u];
       }
     }
-    __syncthreads();
+#if CMS_P2_PREFETCH
+    if (tb + kPartTile < hi) load(tb + kPartTile);
+#endif
+    lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t f = L.bin[i];
       uint32_t g = L.cursor[f] + (i - L.off[f]);
+#ifdef CMS_PART_LINEAR  // bound analysis only: contiguous instead of per-bin destinations
+      g = (uint32_t)(tb + i);
+#endif
+#ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
+      if (g != 0xFFFFFFFFu) continue;
+#endif
       okey[g] = L.key[i];
       if (oval) oval[g] = L.val[i];
       if (orow) orow[g] = b * P2 + (int32_t)f;
     }
-    __syncthreads();
-    for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] += L.hist[f];
-    __syncthreads();
+    lds_barrier();
+    for (int f = tid; f < P2; f += kPartThreads) {
+      L.cursor[f] += L.hist[f];
+      L.hist[f] = 0;
+    }
+    lds_barrier();
   }
 }
 
@@ -338,13 +502,13 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
                      int64_t** out_off, int64_t** out_key, float** out_val, int32_t* out_rows) {
   const int64_t n = h->n;
   const int B = std::max(1, ceil_log2(n));
-  int s2 = std::min(B, 10);
+  int s2 = std::min(B, CMS_PART_S2);
   if (B - s2 > 12) s2 = B - 12;
   const int P2 = 1 << s2;
   const int P1 = (int)((n + P2 - 1) / P2);
   if (P1 > kMaxBins || P2 > kMaxBins)
     return set_error(CMS_E_PARAM, "num_owners %lld too large for the partition", (long long)n);
-  const int64_t chunk1 = std::max<int64_t>(4 * kPartTile, (npairs + 2047) / 2048);
+  const int64_t chunk1 = std::max<int64_t>(4 * kPartTile, (npairs + CMS_P1_BLOCKS - 1) / CMS_P1_BLOCKS);
   const int NB = (int)((npairs + chunk1 - 1) / chunk1);
   const int64_t CH2 = 4 * kPartTile;
   const int64_t nb2max = npairs / CH2 + P1 + 1;
@@ -385,13 +549,13 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
                        P1, n, H1, NB, h->d_flags);
     int rc = scan_exclusive_u32(h, H1, O1, L1, bsum);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_p1_scatter, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P1), h->stream, d_row, d_key,
+    hipLaunchKernelGGL(k_p1_scatter, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P1, d_val != nullptr, true), h->stream, d_row, d_key,
                        d_val, npairs, chunk1, s2, P1, n, O1, NB, fine, key1, val1);
     hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, O1, H1, NB, P1, CH2, binStart, blkStart);
     hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)nb2max), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,
                        binStart, blkStart, P1, CH2, P2, H2);
     hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, H2, binStart, blkStart, P1, P2, n, O2, coff);
-    hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2), h->stream, fine,
+    hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2, d_val != nullptr, false), h->stream, fine,
                        key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     CMS_HIP(hipGetLastError());
   }
