@@ -34,7 +34,9 @@ struct HotInfo {
   int32_t pad;
 };
 
-constexpr int kKeyRegs = 4;  // keys cached per thread: owners up to 1024 keys are read once
+constexpr int kKeyRegs = 4;
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // keys cached per thread: owners up to 1024 keys are read once
 
 __global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
                              int2* extra_map, uint32_t* counters /* [0]=hot rows [2]=extra slices */,
@@ -163,12 +165,21 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   for (int j = tid; j < w; j += kBuildThreads) lds[j] = load_old ? (dst ? dst[j] : (uint32_t)dst16[j]) : 0u;
   __syncthreads();
 
-  for (int d = 0; d < hp.depth; ++d) {
-    // ---- updates of sketch row d ----
+  // Narrow rows of a fresh build pair their sketch rows: every counter of such
+  // a row is below 2^16 (promote_rows guarantees it), so row d counts in the
+  // low and row d+1 in the high half of the same LDS word without a carry
+  // between them -- d = 5 takes three update/write-out phases instead of five.
+  const bool pair_rows = !dst && !load_old && !atomic_mode && (w & 3) == 0;
+  for (int d = 0; d < hp.depth;) {
+    const bool two = pair_rows && d + 1 < hp.depth;
+    // ---- updates of sketch row d (and d+1) ----
     if (cached) {
 #pragma unroll
       for (int k = 0; k < kKeyRegs; ++k)
-        if (ik[k]) atomicAdd(&lds[bucket(hp, d, kp[k])], ik[k]);
+        if (ik[k]) {
+          atomicAdd(&lds[bucket(hp, d, kp[k])], ik[k]);
+          if (two) atomicAdd(&lds[bucket(hp, d + 1, kp[k])], ik[k] << 16);
+        }
     } else {
       for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
         int64_t kk[4];
@@ -189,7 +200,11 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          if (inc4[u]) atomicAdd(&lds[bucket(hp, d, reduce_key(kk[u]))], inc4[u]);
+          if (inc4[u]) {
+            const uint64_t kr = reduce_key(kk[u]);
+            atomicAdd(&lds[bucket(hp, d, kr)], inc4[u]);
+            if (two) atomicAdd(&lds[bucket(hp, d + 1, kr)], inc4[u] << 16);
+          }
           if (d == 0) mass += inc4[u];
         }
       }
@@ -203,6 +218,38 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
         uint32_t v = lds[j];
         lds[j] = 0u;
         if (v) atomicAdd(dst + rofs + j, v);
+      }
+    } else if (two) {
+      // rows d and d+1 leave LDS together; squares by v_dot2_u32_u16 on the
+      // packed store words: a narrow row's sum of squares is at most
+      // mass * max < 2^32, so u32 partial sums are exact
+      uint4* l4 = reinterpret_cast<uint4*>(lds);
+      uint2* da = reinterpret_cast<uint2*>(dst16 + rofs);
+      uint2* db = reinterpret_cast<uint2*>(dst16 + rofs + w);
+      uint32_t sqa = 0, sqb = 0;
+      u16x2 pm = {0, 0};
+      for (int j = tid; j < (w >> 2); j += kBuildThreads) {
+        const uint4 v = l4[j];
+        l4[j] = make_uint4(0, 0, 0, 0);
+        const uint32_t a0 = __builtin_amdgcn_perm(v.y, v.x, 0x05040100u), a1 = __builtin_amdgcn_perm(v.w, v.z, 0x05040100u);
+        const uint32_t b0 = __builtin_amdgcn_perm(v.y, v.x, 0x07060302u), b1 = __builtin_amdgcn_perm(v.w, v.z, 0x07060302u);
+        da[j] = make_uint2(a0, a1);
+        db[j] = make_uint2(b0, b1);
+        const u16x2 pa0 = __builtin_bit_cast(u16x2, a0), pa1 = __builtin_bit_cast(u16x2, a1);
+        const u16x2 pb0 = __builtin_bit_cast(u16x2, b0), pb1 = __builtin_bit_cast(u16x2, b1);
+        sqa = __builtin_amdgcn_udot2(pa0, pa0, sqa, false);
+        sqa = __builtin_amdgcn_udot2(pa1, pa1, sqa, false);
+        sqb = __builtin_amdgcn_udot2(pb0, pb0, sqb, false);
+        sqb = __builtin_amdgcn_udot2(pb1, pb1, sqb, false);
+        pm = __builtin_elementwise_max(pm, __builtin_elementwise_max(__builtin_elementwise_max(pa0, pa1),
+                                                                     __builtin_elementwise_max(pb0, pb1)));
+      }
+      vmax = max(vmax, max((uint32_t)pm.x, (uint32_t)pm.y));
+      sqa = wave_sum_u32(sqa);
+      sqb = wave_sum_u32(sqb);
+      if ((tid & 63) == 0) {
+        atomicAdd(&s_norm[d], (unsigned long long)sqa);
+        atomicAdd(&s_norm[d + 1], (unsigned long long)sqb);
       }
     } else {
       uint64_t sq = 0;
@@ -269,6 +316,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       if ((tid & 63) == 0) atomicAdd(&s_norm[d], (unsigned long long)sq);
     }
     __syncthreads();
+    d += two ? 2 : 1;
   }
 
   if (badv) atomicOr(flags, kFlagBadValue);
