@@ -262,17 +262,23 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
         // the squares are full-rate 24-bit products and no sum can saturate
         uint4* l4 = reinterpret_cast<uint4*>(lds);
         uint2* d2 = reinterpret_cast<uint2*>(dst16 + rofs);
+        uint32_t sq32 = 0;  // < 2^32: see the paired write-out
+        u16x2 pm = {0, 0};
         for (int j = tid; j < (w >> 2); j += kBuildThreads) {
           const uint4 v = l4[j];
           l4[j] = make_uint4(0, 0, 0, 0);
+          const uint32_t a0 = __builtin_amdgcn_perm(v.y, v.x, 0x05040100u), a1 = __builtin_amdgcn_perm(v.w, v.z, 0x05040100u);
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
           if (v.x == 0xFFFFFFFFu)
 #endif
-          d2[j] = make_uint2(v.x | (v.y << 16), v.z | (v.w << 16));
-          vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
-          sq += (uint64_t)__umul24(v.x, v.x) + __umul24(v.y, v.y);
-          sq += (uint64_t)__umul24(v.z, v.z) + __umul24(v.w, v.w);
+          d2[j] = make_uint2(a0, a1);
+          const u16x2 pa0 = __builtin_bit_cast(u16x2, a0), pa1 = __builtin_bit_cast(u16x2, a1);
+          sq32 = __builtin_amdgcn_udot2(pa0, pa0, sq32, false);
+          sq32 = __builtin_amdgcn_udot2(pa1, pa1, sq32, false);
+          pm = __builtin_elementwise_max(pm, __builtin_elementwise_max(pa0, pa1));
         }
+        vmax = max(vmax, max((uint32_t)pm.x, (uint32_t)pm.y));
+        sq = sq32;
       } else if (vec) {
         uint4* l4 = reinterpret_cast<uint4*>(lds);
         for (int j = tid; j < (w >> 2); j += kBuildThreads) {
