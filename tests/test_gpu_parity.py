@@ -63,6 +63,36 @@ def test_ingest_partition_path_with_hot_rows(oracle, n, d, w, npairs):
     assert np.bincount(items, minlength=n).max() > 32768  # a hot row was split into slices
 
 
+@pytest.mark.parametrize("shape", ["u32_max", "one_wide", "negative", "edge"])
+def test_partition_key_width_modes(oracle, shape):
+    """Keys at the u32 boundary, a single key past it, negative keys and the
+    int64 edge values through the COO partition (and a second batch through
+    the same partition workspace) give the oracle's table bit for bit."""
+    n, d, w = 900, 5, 512
+    items, users = zipf_stream(30000, n, 400_000, seed=17)
+    keys = users.astype(np.int64).copy()
+    if shape == "u32_max":
+        keys[::7] = 2 ** 32 - 1 - keys[::7]  # still narrow, top of the u32 range
+    elif shape == "one_wide":
+        keys[len(keys) // 2] = 2 ** 32  # a single key needs the 8-byte path
+    elif shape == "negative":
+        keys[-1] = -1
+    else:
+        keys[: len(EDGE)] = EDGE
+    with SketchTable(n, depth=d, width=w, seed=7) as t:
+        t.ingest(items, keys)
+        t.finalize()
+        got = t.read_counters()
+        assert same(got, oracle_table(oracle, n, d, w, 7, items, keys))
+        # a second batch through the same partition workspace (live-table path)
+        t.ingest(items, users)
+        t.finalize()
+        got2 = t.read_counters()
+    both_i = np.concatenate([items, items])
+    both_k = np.concatenate([keys, users.astype(np.int64)])
+    assert same(got2, oracle_table(oracle, n, d, w, 7, both_i, both_k))
+
+
 def test_ingest_csr_matches_coo(oracle):
     n, d, w = 2000, 5, 512
     items, users = zipf_stream(50000, n, 500_000, seed=3)
