@@ -166,6 +166,14 @@ int cms_finalize(cms_handle* h);
 typedef int (*cms_allreduce_fn)(void* d_buf, int64_t count, void* user);
 int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user);
 int cms_synchronize(cms_handle* h);
+/* Stream ordering without a host wait (stream: a hipStream_t of the handle's
+ * device, e.g. the caller's current torch stream; NULL = legacy default).
+ * cms_wait_stream: the handle's later work waits for everything queued on
+ * `stream` so far (inputs written there are complete before they are read).
+ * cms_release_to_stream: later work queued on `stream` waits for the handle's
+ * work queued so far (device inputs may then be freed / reused on `stream`). */
+int cms_wait_stream(cms_handle* h, void* stream);
+int cms_release_to_stream(cms_handle* h, void* stream);
 
 /* ---- queries (after cms_finalize) ---------------------------------------- */
 
@@ -301,7 +309,11 @@ typedef struct cms_stats {
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 
-/* Per-kernel HIP-event timing on the handle's stream (off by default). */
+/* Per-kernel HIP-event timing on the handle's stream (off by default).
+ * level 1: the roofline kernels' scopes only ("build_rows", "ingest_atomic",
+ * "allreduce", the cosine / top-k families); level >= 2: every scope, the
+ * ingest phases ("partition", "build_plan", "hot_norms", "norms", merge
+ * phases) included -- each recorded event costs the stream a few us. */
 int cms_set_timing(cms_handle* h, int32_t enabled);
 /* Accumulated (total ms, launches) for a kernel family name, e.g.
  * "build_rows", "partition", "norms", "allreduce", "cosine". */

@@ -35,7 +35,7 @@ EXPORTS = [
     "cms_abi_version", "cms_set_owner_ids", "cms_hash_params", "cms_hash_keys", "cms_ingest",
     "cms_ingest_device_rows", "cms_ingest_csr", "cms_ingest_csr_device", "cms_reset", "cms_release_scratch",
     "cms_comm_unique_id",
-    "cms_comm_init", "cms_shard_of_key", "cms_finalize", "cms_synchronize", "cms_similarity", "cms_similarities",
+    "cms_comm_init", "cms_shard_of_key", "cms_finalize", "cms_synchronize", "cms_wait_stream", "cms_release_to_stream", "cms_similarity", "cms_similarities",
     "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_top_k_all_partial", "cms_top_k_merge", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
@@ -106,6 +106,8 @@ _SIGS = {
     "cms_shard_of_key": (_i32, [_i64, _i32]),
     "cms_finalize": (_int, [_vp]),
     "cms_synchronize": (_int, [_vp]),
+    "cms_wait_stream": (_int, [_vp, _vp]),
+    "cms_release_to_stream": (_int, [_vp, _vp]),
     "cms_similarity": (_int, [_vp, _i64, _i64, ctypes.POINTER(_dbl)]),
     "cms_similarities": (_int, [_vp, _i64, _vp, _i64, _vp]),
     "cms_point_query": (_int, [_vp, _i64, _i64, ctypes.POINTER(_dbl)]),

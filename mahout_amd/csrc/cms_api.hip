@@ -50,17 +50,40 @@ void DevBuf::release() {
   bytes = 0;
 }
 
+// Phase scopes of the ingest step whose events are recorded only at timing
+// level 2: every timing event is a marker in the stream that costs the GPU a
+// few microseconds, so the timed bench steps (level 1) bracket the roofline
+// kernels alone.
+static bool fine_scope(const char* nm) {
+  static const char* const kFine[] = {"partition", "build_plan", "hot_norms", "norms", "reduce_hot",
+                                      "merge_bounds", "merge_pack", "merge_unpack"};
+  for (const char* f : kFine)
+    if (!strcmp(nm, f)) return true;
+  return false;
+}
+
+static hipEvent_t pooled_event(cms_handle* h) {
+  hipEvent_t e = nullptr;
+  if (!h->event_pool.empty()) {
+    e = h->event_pool.back();
+    h->event_pool.pop_back();
+  } else if (hipEventCreate(&e) != hipSuccess) {
+    e = nullptr;
+  }
+  return e;
+}
+
 TimedScope::TimedScope(cms_handle* hh, const char* nm) : h(hh), name(nm) {
-  if (h->timing) {
-    if (hipEventCreate(&start) == hipSuccess) (void)hipEventRecord(start, h->stream);
-    else start = nullptr;
+  if (h->timing >= (fine_scope(nm) ? 2 : 1)) {
+    start = pooled_event(h);
+    if (start) (void)hipEventRecord(start, h->stream);
   }
 }
 
 TimedScope::~TimedScope() {
-  if (!h->timing || !start) return;
-  hipEvent_t stop;
-  if (hipEventCreate(&stop) != hipSuccess) return;
+  if (!start) return;
+  hipEvent_t stop = pooled_event(h);
+  if (!stop) return;
   (void)hipEventRecord(stop, h->stream);
   h->pending.push_back(PendingEvent{name, start, stop});
 }
@@ -86,9 +109,16 @@ static void java_hash_params(int64_t seed, int depth, int64_t* a, int64_t* b) {
   }
 }
 
+static int flags_error(cms_handle* h, uint32_t f, bool by_id);
+
 static int check_flags(cms_handle* h, bool by_id) {
   uint32_t f = 0;
   CMS_HIP(hipMemcpy(&f, h->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return flags_error(h, f, by_id);
+}
+
+// error flags word f (already read back): clear it on the device and report
+static int flags_error(cms_handle* h, uint32_t f, bool by_id) {
   if (f == 0) return CMS_OK;
   CMS_HIP(hipMemset(h->d_flags, 0, sizeof(uint32_t)));
   if (f & kFlagBadRow)
@@ -106,8 +136,8 @@ static int resolve_timing(cms_handle* h) {
     auto& acc = h->timing_acc[pe.name];
     acc.total_ms += ms;
     acc.launches += 1;
-    (void)hipEventDestroy(pe.start);
-    (void)hipEventDestroy(pe.stop);
+    h->event_pool.push_back(pe.start);
+    h->event_pool.push_back(pe.stop);
   }
   h->pending.clear();
   return CMS_OK;
@@ -238,6 +268,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
       (!per_owner && (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess) ||
       (e = hipMalloc(&h->d_rowmax, sizeof(uint32_t) * h->n)) != hipSuccess ||
       (e = hipMalloc(&h->d_flags, 64 * sizeof(uint32_t))) != hipSuccess ||
+      (e = hipHostMalloc((void**)&h->h_pin, 16 * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess ||
       (e = hipMemset(h->d_flags, 0, 64 * sizeof(uint32_t))) != hipSuccess ||
       (e = hipMemset(h->d_row_mass, 0, sizeof(uint64_t) * h->n)) != hipSuccess) {
     int rc = hip_fail(e, "cms_create allocation");
@@ -262,10 +293,13 @@ void cms_destroy(cms_handle* h) {
     (void)hipEventDestroy(pe.start);
     (void)hipEventDestroy(pe.stop);
   }
+  for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
+  if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   void* bufs[] = {h->d_t16, h->d_hidx, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (h->h_pin) (void)hipHostFree(h->h_pin);
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_small, &h->ws_partials,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
@@ -623,11 +657,12 @@ int cms_finalize(cms_handle* h) {
   }
   int rc = compute_norms(h);
   if (rc) return rc;
+  // error word and inexact-norm count in one pinned read-back: the step's only sync
+  CMS_HIP(hipMemcpyAsync(h->h_pin, h->d_flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
-  rc = check_flags(h, false);
+  const uint32_t inexact = h->h_pin[1];
+  rc = flags_error(h, h->h_pin[0], false);
   if (rc) return rc;
-  uint32_t inexact = 0;
-  CMS_HIP(hipMemcpy(&inexact, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
   h->exact_norms = inexact == 0;
   h->mfma_ready = false;
   h->finalized = true;
@@ -671,6 +706,25 @@ int cms_synchronize(cms_handle* h) {
   Guard g(h);
   CMS_HIP(hipStreamSynchronize(h->stream));
   return check_flags(h, false);
+}
+
+static int order_streams(cms_handle* h, hipStream_t from, hipStream_t to) {
+  if (!h->order_ev) CMS_HIP(hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming));
+  CMS_HIP(hipEventRecord(h->order_ev, from));
+  CMS_HIP(hipStreamWaitEvent(to, h->order_ev, 0));
+  return CMS_OK;
+}
+
+int cms_wait_stream(cms_handle* h, void* stream) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  Guard g(h);
+  return order_streams(h, (hipStream_t)stream, h->stream);
+}
+
+int cms_release_to_stream(cms_handle* h, void* stream) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  Guard g(h);
+  return order_streams(h, h->stream, (hipStream_t)stream);
 }
 
 int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n, double* out) {
@@ -1003,6 +1057,7 @@ int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capaci
 
 int cms_get_stats(cms_handle* h, cms_stats* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
   out->pairs_ingested = h->pairs_ingested;
   out->num_owners = h->n;
   out->depth = h->per_owner ? h->po_max_d : h->p.depth;
@@ -1010,8 +1065,13 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
+  int64_t hot_rows = 0;
+  if (!h->per_owner && h->d_hidx) {
+    int rc = count_hot_rows(h, &hot_rows);
+    if (rc) return rc;
+  }
   out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
-                                   : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * h->hot_used * h->dw;
+                                   : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;
@@ -1022,7 +1082,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
 
 int cms_set_timing(cms_handle* h, int32_t enabled) {
   if (!h) return set_error(CMS_E_PARAM, "null handle");
-  h->timing = enabled != 0;
+  h->timing = enabled <= 0 ? 0 : enabled == 1 ? 1 : 2;
   return CMS_OK;
 }
 

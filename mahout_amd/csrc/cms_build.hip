@@ -410,7 +410,16 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
     if ((rc0 = row_bounds(h, d_off, d_val, accumulate ? h->d_row_mass : nullptr, kSlice, bound.as<uint64_t>(),
                           force.as<uint8_t>())))
       return rc0;
-    if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0))) return rc0;
+    // A fresh build with implicit (unit) increments: a row needs a slot when
+    // its mass reaches 2^16 (at most total / 2^16 rows) or it is split into
+    // slices (more than kSlice keys: at most npairs / (kSlice + 1) rows), a
+    // bound the host knows without reading anything back.
+    int64_t max_new = -1;
+    if (!accumulate && !d_val && h->hp.frac_bits < 32) {
+      const uint64_t total = (uint64_t)npairs << h->hp.frac_bits;
+      max_new = (int64_t)(total / kNarrowLimit) + npairs / (kSlice + 1) + 1;
+    }
+    if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0, max_new))) return rc0;
   }
   {
     TimedScope ts(h, "build_plan");

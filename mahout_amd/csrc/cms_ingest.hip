@@ -342,10 +342,12 @@ int local_norms(cms_handle* h) {
 
 int compute_norms(cms_handle* h) {
   TimedScope ts(h, "norms");
-  uint32_t stale = 0;  // an incremental norm reached the inexact regime
-  CMS_HIP(hipMemcpyAsync(&stale, h->d_flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-  CMS_HIP(hipStreamSynchronize(h->stream));
-  if (stale) h->norms_valid = false;
+  if (h->stale_possible && h->norms_valid) {  // an incremental norm may have reached the inexact regime
+    CMS_HIP(hipMemcpyAsync(h->h_pin + 2, h->d_flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    if (h->h_pin[2]) h->norms_valid = false;
+  }
+  h->stale_possible = false;
   if (!h->norms_valid) {
     CMS_HIP(hipMemsetAsync(h->d_flags + 2, 0, sizeof(uint32_t), h->stream));
     unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
@@ -403,6 +405,7 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
         if ((rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true))) return rc;
       }
       TimedScope ts(h, "ingest_atomic");
+      h->stale_possible = true;
       unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
       hipLaunchKernelGGL(k_ingest_sorted, dim3(grid), dim3(256), 0, h->stream, h->ws_srow.as<int32_t>(), ckey, cval,
                          coff + n, h->hp, h->tview(), h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
@@ -436,6 +439,7 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
       if (rc) return rc;
     }
     const int track = h->norms_valid ? 1 : 0;
+    h->stale_possible = true;
     unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
     hipLaunchKernelGGL(k_ingest_atomic, dim3(grid), dim3(256), 0, h->stream, d_row, d_key, d_val, npairs, n, h->hp,
                        h->tview(), h->d_row_mass, h->d_norm, h->d_rowmax, track, h->d_flags);

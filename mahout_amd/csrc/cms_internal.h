@@ -120,6 +120,8 @@ struct cms_handle {
   double* d_norm_sqrt = nullptr;    // [n][d] Math.sqrt((double) norm)
   uint32_t* d_rowmax = nullptr;     // [n] largest counter of the owner (valid with the norms)
   uint32_t* d_flags = nullptr;      // error flags word + counters
+  uint32_t* h_pin = nullptr;        // pinned host words: flag read-back without a staged copy
+  bool stale_possible = true;       // an incremental ingest may have raised flags[2] since the last check
   int64_t* d_owner_ids = nullptr;   // [n] sorted IDs (null => identity)
   std::vector<int64_t> h_owner_ids;
 
@@ -183,9 +185,11 @@ struct cms_handle {
   cms::DevBuf po_scratch;                        // per-block bucket rows for widths beyond LDS
 
   // instrumentation
-  bool timing = false;
+  int timing = 0;  // 0 off, 1 the roofline kernels' scopes only, 2 every scope (phase breakdown)
   std::map<std::string, cms::TimingAcc> timing_acc;
   std::vector<cms::PendingEvent> pending;
+  std::vector<hipEvent_t> event_pool;  // recycled timing events (no create/destroy per scope)
+  hipEvent_t order_ev = nullptr;       // cms_wait_stream / cms_release_to_stream (timing disabled)
 };
 
 namespace cms {
@@ -222,7 +226,11 @@ int local_norms(cms_handle* h);
 // coming write, in counter units; or any row with force[r]) reaches 2^16
 // gets a hot slot; copy_old copies its narrow counters into the slot (else the
 // slot is zeroed).  bound may be null when only force is used.
-int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old);
+// max_new >= 0: a proven bound on the rows this call can promote (no host
+// round trip: that many slots are reserved and claimed on the device).
+int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new = -1);
+// rows holding a u32 slot (synchronises the stream)
+int count_hot_rows(cms_handle* h, int64_t* out);
 // per-row counter bounds after a CSR batch (mass in counter units + old_mass)
 // and the rows split over more than `slice` keys (cms_build.hip)
 int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,

@@ -15,18 +15,31 @@
 
 namespace cms {
 
-__global__ void k_promote_list(const uint64_t* bound, const uint8_t* force, const int32_t* hidx, int64_t n,
-                               uint32_t* cnt, int32_t* list) {
+// claim >= 0: the list entry i also takes slot claim + i here (the caller
+// reserved `reserved` slots, a proven bound), so the promotion needs no count
+// on the host; a broken bound flags an overflow instead of writing past them.
+__global__ void k_promote_list(const uint64_t* bound, const uint8_t* force, int32_t* hidx, int64_t n,
+                               uint32_t* cnt, int32_t* list, int64_t claim, int64_t reserved, uint32_t* flags) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     if (hidx[r] >= 0) continue;
     const bool need = (bound && bound[r] >= kNarrowLimit) || (force && force[r]);
-    if (need) list[atomicAdd(cnt, 1u)] = (int32_t)r;
+    if (need) {
+      const uint32_t i = atomicAdd(cnt, 1u);
+      if (claim >= 0 && (int64_t)i >= reserved) {
+        atomicOr(flags, kFlagOverflow);
+        continue;
+      }
+      list[i] = (int32_t)r;
+      if (claim >= 0) hidx[r] = (int32_t)(claim + i);
+    }
   }
 }
 
-// one workgroup per promoted row: slot base + i, old narrow counters copied (or zeros)
-__global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64_t count, int64_t base, TableView tv,
-                                                      int32_t* hidx, int copy_old) {
+// one workgroup per promoted row: slot base + i, old narrow counters copied
+// (or zeros); dcount != nullptr: the list length is read on the device
+__global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64_t count, const uint32_t* dcount,
+                                                      int64_t base, TableView tv, int32_t* hidx, int copy_old) {
+  if (dcount) count = min<int64_t>(count, (int64_t)*dcount);
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int64_t r = list[i];
     const int64_t slot = base + i;
@@ -37,22 +50,10 @@ __global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64
   }
 }
 
-int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old) {
-  const int64_t n = h->n;
-  CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
-  int32_t* list = h->ws_plist.as<int32_t>();
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(list + n);
-  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-  hipLaunchKernelGGL(k_promote_list, dim3(g), dim3(256), 0, h->stream, d_bound, d_force, h->d_hidx, n, cnt, list);
-  CMS_HIP(hipGetLastError());
-  uint32_t c = 0;
-  CMS_HIP(hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
-  CMS_HIP(hipStreamSynchronize(h->stream));
-  if (c == 0) return CMS_OK;
-  const int64_t need = h->hot_used + c;
-  if (need > h->hot_cap) {  // grow: new slot table, live slots copied over
-    const int64_t cap = std::min<int64_t>(n, std::max<int64_t>({need, h->hot_cap + h->hot_cap / 2, 64}));
+static int grow_hot(cms_handle* h, int64_t need) {
+  if (need <= h->hot_cap) return CMS_OK;
+  {  // grow: new slot table, live slots copied over
+    const int64_t cap = std::min<int64_t>(h->n, std::max<int64_t>({need, h->hot_cap + h->hot_cap / 2, 64}));
     DevBuf nb;
     CMS_HIP(nb.ensure(sizeof(uint32_t) * (size_t)cap * (size_t)h->dw));
     if (h->hot_used > 0)
@@ -62,10 +63,69 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
     h->hot_tab = std::move(nb);
     h->hot_cap = cap;
   }
+  return CMS_OK;
+}
+
+int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new) {
+  const int64_t n = h->n;
+  CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
+  int32_t* list = h->ws_plist.as<int32_t>();
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(list + n);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+  if (max_new >= 0) {
+    // The caller bounds the rows this call can promote: reserve that many
+    // slots, claim them on the device -- no host round trip inside the build.
+    // Unclaimed reserved slots stay unused until the next layout reset.
+    max_new = std::min<int64_t>(max_new, n);
+    if (max_new == 0) return CMS_OK;
+    if (h->hot_used + max_new > n) return promote_rows(h, d_bound, d_force, copy_old, -1);  // reservations spent
+    int rc = grow_hot(h, h->hot_used + max_new);
+    if (rc) return rc;
+    CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+    hipLaunchKernelGGL(k_promote_list, dim3(g), dim3(256), 0, h->stream, d_bound, d_force, h->d_hidx, n, cnt, list,
+                       h->hot_used, max_new, h->d_flags);
+    hipLaunchKernelGGL(k_promote_rows, dim3((unsigned)std::min<int64_t>(max_new, 65536)), dim3(256), 0, h->stream,
+                       list, max_new, cnt, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
+    CMS_HIP(hipGetLastError());
+    h->hot_used += max_new;
+    return CMS_OK;
+  }
+  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+  hipLaunchKernelGGL(k_promote_list, dim3(g), dim3(256), 0, h->stream, d_bound, d_force, h->d_hidx, n, cnt, list,
+                     (int64_t)-1, (int64_t)0, h->d_flags);
+  CMS_HIP(hipGetLastError());
+  uint32_t c = 0;
+  CMS_HIP(hipMemcpyAsync(&c, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (c == 0) return CMS_OK;
+  const int64_t need = h->hot_used + c;
+  int rc = grow_hot(h, need);
+  if (rc) return rc;
   hipLaunchKernelGGL(k_promote_rows, dim3((unsigned)std::min<int64_t>(c, 65536)), dim3(256), 0, h->stream, list,
-                     (int64_t)c, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
+                     (int64_t)c, (const uint32_t*)nullptr, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
   CMS_HIP(hipGetLastError());
   h->hot_used = need;
+  return CMS_OK;
+}
+
+__global__ void k_count_hot(const int32_t* hidx, int64_t n, unsigned long long* out) {
+  uint32_t c = 0;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    c += hidx[r] >= 0;
+  if (c) atomicAdd(out, (unsigned long long)c);
+}
+
+int count_hot_rows(cms_handle* h, int64_t* out) {
+  DevBuf tmp;
+  CMS_HIP(tmp.ensure(sizeof(unsigned long long)));
+  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, sizeof(unsigned long long), h->stream));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_count_hot, dim3(g), dim3(256), 0, h->stream, h->d_hidx, h->n, tmp.as<unsigned long long>());
+  CMS_HIP(hipGetLastError());
+  unsigned long long c = 0;
+  CMS_HIP(hipMemcpyAsync(&c, tmp.ptr, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  *out = (int64_t)c;
   return CMS_OK;
 }
 

@@ -27,15 +27,15 @@ def _dev_ptr(x):
     return ctypes.c_void_p(x.data_ptr())
 
 
-def _producers_done(*xs):
-    """The library's stream does not order against torch's (possibly
-    non-default) current stream: wait for the kernels that wrote the inputs."""
+def _torch_stream(*xs):
+    """Current torch stream (hipStream_t) of the first device tensor (0: the
+    legacy default stream), or None when no input is a device tensor."""
     import torch
 
     for x in xs:
         if isinstance(x, torch.Tensor) and x.is_cuda:
-            torch.cuda.current_stream(x.device).synchronize()
-            return
+            return torch.cuda.current_stream(x.device).cuda_stream
+    return None
 
 
 def shape_from_delta_epsilon(delta, epsilon):
@@ -141,9 +141,19 @@ class SketchTable:
         check(self._lib.cms_ingest(self._h, _ptr(owner), _ptr(key), _ptr(v), owner.size))
 
     def ingest_device_rows(self, d_row, d_key, d_val, n):
-        _producers_done(d_row, d_key, d_val)
+        # stream-ordered both ways (no host wait): the library's stream waits
+        # for the producers on torch's current stream, and torch's stream waits
+        # for the ingest, so the inputs may be freed once this returns.  The
+        # library stream is a blocking stream, so against torch's legacy
+        # default stream (s == 0) that ordering is implicit.
+        s = _torch_stream(d_row, d_key, d_val)
+        if s:
+            check(self._lib.cms_wait_stream(self._h, ctypes.c_void_p(s)))
         check(self._lib.cms_ingest_device_rows(self._h, _dev_ptr(d_row), _dev_ptr(d_key), _dev_ptr(d_val), int(n)))
-        self.synchronize()  # the inputs may be freed once this returns
+        if s:
+            check(self._lib.cms_release_to_stream(self._h, ctypes.c_void_p(s)))
+        elif s is None:
+            self.synchronize()
 
     def ingest_csr(self, offsets, keys, vals=None):
         offsets = np.ascontiguousarray(offsets, np.int64)
@@ -154,9 +164,14 @@ class SketchTable:
         check(self._lib.cms_ingest_csr(self._h, _ptr(offsets), _ptr(keys), _ptr(v)))
 
     def ingest_csr_device(self, d_offsets, d_keys, d_vals=None):
-        _producers_done(d_offsets, d_keys, d_vals)
+        s = _torch_stream(d_offsets, d_keys, d_vals)
+        if s:
+            check(self._lib.cms_wait_stream(self._h, ctypes.c_void_p(s)))
         check(self._lib.cms_ingest_csr_device(self._h, _dev_ptr(d_offsets), _dev_ptr(d_keys), _dev_ptr(d_vals)))
-        self.synchronize()  # the inputs may be freed once this returns
+        if s:
+            check(self._lib.cms_release_to_stream(self._h, ctypes.c_void_p(s)))
+        elif s is None:
+            self.synchronize()
 
     def reset(self):
         check(self._lib.cms_reset(self._h))
@@ -322,8 +337,11 @@ class SketchTable:
         check(self._lib.cms_get_stats(self._h, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in s._fields_}
 
-    def set_timing(self, enabled=True):
-        check(self._lib.cms_set_timing(self._h, 1 if enabled else 0))
+    def set_timing(self, enabled=True, level=2):
+        """HIP-event timing of the library's kernel scopes.  level 1 brackets
+        only the roofline kernels (cheap enough for timed steps), level 2 every
+        phase scope as well (each event costs the stream a few us)."""
+        check(self._lib.cms_set_timing(self._h, int(level) if enabled else 0))
 
     def timing(self, name):
         ms = ctypes.c_double()

@@ -383,16 +383,38 @@ def test_movielens_shape_config1(oracle):
             assert t.most_similar(int(item_ids[q]), 10)[0].tolist() == eids.tolist()
 
 
+def test_device_ingest_orders_against_a_side_stream(oracle):
+    """Inputs produced on a non-default torch stream and freed right after the
+    (asynchronous) device ingest: event ordering both ways, table exact."""
+    import torch
+    n, d, w = 300, 4, 256
+    items, users = zipf_stream(5000, n, 400_000, seed=41)
+    side = torch.cuda.Stream()
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        with torch.cuda.stream(side):
+            r = torch.from_numpy(items).to("cuda", non_blocking=True)
+            k = torch.from_numpy(users).to("cuda", non_blocking=True)
+            r2 = (r * 3 - 2 * r).contiguous()  # produced on the side stream
+            k2 = (k + 7 - 7).contiguous()
+            t.ingest_device_rows(r2, k2, None, int(r2.numel()))
+            del r2, k2
+            junk = torch.full((items.size * 4,), -1, dtype=torch.int64, device="cuda")  # may reuse the freed blocks
+            del junk
+        t.finalize()
+        assert same(t.read_counters(), oracle_table(oracle, n, d, w, 42, items, users))
+
+
 def test_bad_row_index_device_path():
     import torch
     with SketchTable(10, depth=2, width=64) as t:
         rows = torch.tensor([0, 1, 10], dtype=torch.int64, device="cuda")
         keys = torch.tensor([1, 2, 3], dtype=torch.int64, device="cuda")
-        # device ingest is asynchronous in the C ABI; the Python wrapper
-        # synchronizes (the inputs may be freed after it returns), so the
-        # bad row surfaces from the ingest call itself
+        # device ingest is asynchronous (stream-ordered against torch's
+        # stream, no host wait), so the bad row surfaces from the next
+        # synchronising call
+        t.ingest_device_rows(rows, keys, None, 3)
         with pytest.raises(CmsError) as ei:
-            t.ingest_device_rows(rows, keys, None, 3)
+            t.finalize()
         assert ei.value.code == CMS_E_PARAM
 
 
