@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
         }
       }
     }
-    __syncthreads();
+    lds_barrier();  // LDS order only: the write-out stores stay in flight
     // ---- write-out of row d, zero/load the slot for row d+1, sum of squares ----
     const int64_t rofs = (int64_t)d * w;
     const bool more = load_old && d + 1 < hp.depth;
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       if (sq > (1ULL << 60)) sq = 1ULL << 60;
       if ((tid & 63) == 0) atomicAdd(&s_norm[d], (unsigned long long)sq);
     }
-    __syncthreads();
+    lds_barrier();  // LDS order only: the write-out stores stay in flight
     d += two ? 2 : 1;
   }
 

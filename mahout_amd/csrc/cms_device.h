@@ -107,4 +107,12 @@ __device__ __forceinline__ double normalize_weight(double r, int weighted) {
   return r;
 }
 
+// Workgroup barrier that orders LDS only: global loads and stores issued
+// before it stay in flight (__syncthreads would drain them with its vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 }  // namespace cms

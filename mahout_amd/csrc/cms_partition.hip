@@ -144,14 +144,6 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
   for (int b = threadIdx.x; b < P1; b += blockDim.x) H1[(int64_t)b * NB + blockIdx.x] = lh[b];
 }
 
-// Workgroup barrier that orders LDS only: global loads issued before it stay
-// in flight (__syncthreads would drain them with its vmcnt(0)).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 // Exclusive scan of hist[0..P) into off[] by the whole block (P <= 4096).
 __device__ __forceinline__ uint32_t scan_bins(const uint32_t* hist, uint32_t* off, int P, uint32_t* scr) {
   const int per = (P + kPartThreads - 1) / kPartThreads;
