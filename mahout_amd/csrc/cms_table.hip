@@ -53,7 +53,9 @@ __global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64
 static int grow_hot(cms_handle* h, int64_t need) {
   if (need <= h->hot_cap) return CMS_OK;
   {  // grow: new slot table, live slots copied over
-    const int64_t cap = std::min<int64_t>(h->n, std::max<int64_t>({need, h->hot_cap + h->hot_cap / 2, 64}));
+    // at least `need` (reserved-but-unclaimed slots can make it exceed n)
+    const int64_t cap =
+        std::max<int64_t>(need, std::min<int64_t>(h->n, std::max<int64_t>({need, h->hot_cap + h->hot_cap / 2, 64})));
     DevBuf nb;
     CMS_HIP(nb.ensure(sizeof(uint32_t) * (size_t)cap * (size_t)h->dw));
     if (h->hot_used > 0)

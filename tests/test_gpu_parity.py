@@ -93,6 +93,28 @@ def test_partition_key_width_modes(oracle, shape):
     assert same(got2, oracle_table(oracle, n, d, w, 7, both_i, both_k))
 
 
+def test_reserved_hot_slots_then_late_promotion(oracle):
+    """A fresh build reserves hot slots for every owner its bound allows (here
+    all of a tiny universe) and claims them on the device; a later batch that
+    lifts a still-narrow row past 2^16 promotes it into a slot beyond the
+    reservation.  Counters stay exact."""
+    n, d, w = 8, 2, 64
+    rng = np.random.Generator(np.random.PCG64(5))
+    rows1 = np.concatenate([np.zeros(200_000, np.int64), rng.integers(1, 8, 100_000).astype(np.int64)])
+    keys1 = rng.integers(0, 1000, rows1.size).astype(np.int64)
+    rows2 = np.full(300_000, 7, np.int64)
+    keys2 = rng.integers(0, 1000, rows2.size).astype(np.int64)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(rows1, keys1)
+        t.finalize()
+        assert same(t.read_counters(), oracle_table(oracle, n, d, w, 42, rows1, keys1))
+        t.ingest(rows2, keys2)
+        t.finalize()
+        got = t.read_counters()
+        assert t.stats()["table_bytes"] > 2 * n * d * w  # rows 0 and 7 hold u32 slots
+    assert same(got, oracle_table(oracle, n, d, w, 42, np.concatenate([rows1, rows2]), np.concatenate([keys1, keys2])))
+
+
 def test_ingest_csr_matches_coo(oracle):
     n, d, w = 2000, 5, 512
     items, users = zipf_stream(50000, n, 500_000, seed=3)
