@@ -177,6 +177,9 @@ struct CosArgs {
 };
 
 __device__ int8_t g_zero16[16];  // source of the zero rows (past n, missing limbs)
+#ifdef CMS_SCREEN_PROBE  // bound analysis only: waves / workgroups with every pair screened out, per row boundary
+__device__ unsigned long long g_probe[4][32][2];  // [fmt*2 + wg][row][any alive]
+#endif
 
 // One stage of one operand (128 rows x 128 B = 16 KiB) by direct global->LDS
 // loads: wave v, instruction u fills the 1 KiB (8 rows) at block 4v+u; lane i
@@ -768,6 +771,18 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
               }
             }
       }
+#ifdef CMS_SCREEN_PROBE
+      if (screen) {
+        __shared__ int s_probe[32];
+        const bool wa = __any(alive != 0ULL);
+        if (lane == 0) atomicAdd(&g_probe[FMT * 2][r][wa ? 1 : 0], 1ull);
+        if (tid < 32 && s - r * cstages == cstages - 1 && r == 0) s_probe[tid] = 0;
+        __syncthreads();
+        if (lane == 0 && wa) atomicOr(&s_probe[r], 1);
+        __syncthreads();
+        if (tid == 0) atomicAdd(&g_probe[FMT * 2 + 1][r][s_probe[r] ? 1 : 0], 1ull);
+      }
+#endif
       if (!screen || __any(alive != 0ULL)) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -1003,7 +1018,11 @@ struct BigCfg {
 static BigCfg big_config(cms_handle* h) {
   BigCfg c;
   c.norms = (size_t)h->p.depth * (kTA + kTB) * sizeof(double) + (kTA + kTB) * sizeof(__half);
+#ifdef CMS_SCREEN_PROBE
+  constexpr size_t kLdsMax = 160 * 1024 - 2048;  // the probe's static LDS (2-stage ring)
+#else
   constexpr size_t kLdsMax = 160 * 1024;
+#endif
   // 128-B K slices (one cache line per row) in a 3- or 2-deep ring; 64-B
   // slices in a 6-deep ring measured slower (twice the line requests per
   // byte, twice the barriers)
@@ -1024,7 +1043,7 @@ static BigCfg big_config(cms_handle* h) {
                          (const void*)k_cosine_big<4, 2, 64>,    (const void*)k_cosine_big<6, 2, 64>,
                          (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>,
                          (const void*)k_cosine_big<2, 1, 128, 1>, (const void*)k_cosine_big<3, 1, 128, 1>};
-    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
     return true;
   }();
   (void)attr;
@@ -1388,6 +1407,18 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // 4. final lists -> outputs
     if ((rc = cand_compact(h, cb, nm, ns, 0, k))) return rc;
     if ((rc = cand_emit(h, cb, nm, ns, k, d_ids, d_scores, d_counts))) return rc;
+#ifdef CMS_SCREEN_PROBE
+    {
+      unsigned long long pr[4][32][2];
+      CMS_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_probe), sizeof(pr), 0, hipMemcpyDeviceToHost));
+      for (int f = 0; f < 4; ++f)
+        for (int r = 0; r < h->p.depth; ++r) {
+          const unsigned long long dead = pr[f][r][0], live = pr[f][r][1];
+          fprintf(stderr, "probe %s %s row %d: dead %llu alive %llu (%.1f%% dead)\n", f / 2 ? "fp4" : "i8",
+                  f % 2 ? "WG" : "wave", r, dead, live, 100.0 * dead / (double)std::max(1ULL, dead + live));
+        }
+    }
+#endif
   }
   // rows whose list overflowed (not expected): exact per-row recompute (whole
   // row, so a sharded job's merge still sees every pair once per shard at most:
