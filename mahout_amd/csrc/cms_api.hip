@@ -306,7 +306,8 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
                   &h->ws_f4, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
-                  &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist};
+                  &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist,
+                  &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -579,7 +580,8 @@ int cms_release_scratch(cms_handle* h) {
   CMS_HIP(hipStreamSynchronize(h->stream));
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_hist, &h->ws_hot, &h->ws_query,
-                  &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand, &h->ws_srow};
+                  &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand, &h->ws_srow,
+                  &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked};
   for (DevBuf* b : ws) b->release();
   return CMS_OK;
 }

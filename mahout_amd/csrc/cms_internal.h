@@ -152,6 +152,7 @@ struct cms_handle {
   // scratch
   cms::DevBuf ws_in_row, ws_in_key, ws_in_val;   // host-ingest staging
   cms::DevBuf ws_p1_row, ws_p1_key, ws_p1_val;   // pass-1 partition output
+  cms::DevBuf ws_mbnd, ws_mbits, ws_mwoff, ws_mpacked;  // packed multi-rank merge (bounds, layout, words)
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out, ws_srow, ws_f4;

@@ -25,6 +25,8 @@
 
 namespace cms {
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
 // [0, n): local row mass (copied in), [n, 2n): local row max, widened to u64.
 __global__ void k_merge_bounds_in(const uint64_t* mass, const uint32_t* rowmax, int64_t n, uint64_t* out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -50,8 +52,11 @@ struct PackLayout {
 // One workgroup per owner.  Field f of the owner's word i holds counter
 // f*NW + i (NW = the owner's word count): both the pack's reads and the
 // unpack's word reads are then consecutive across the lanes of a wave.
+// use_img: a narrow owner's d x w counters are first staged in LDS with
+// 16-byte loads, and the words are assembled from there.
 __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int64_t dw, PackLayout L,
-                                                   uint64_t* words) {
+                                                   uint64_t* words, int use_img) {
+  extern __shared__ __align__(16) uint16_t img[];  // [dw] (use_img)
   for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
     const int b = L.bits[o];
     if (b == 0) continue;
@@ -60,6 +65,20 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
     const int32_t slot = tv.hidx[o];
     const uint32_t* s32 = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
     const uint16_t* s16 = tv.t16 + o * dw;
+    if (use_img && !s32) {
+      const uint4* g4 = reinterpret_cast<const uint4*>(s16);
+      uint4* l4 = reinterpret_cast<uint4*>(img);
+      for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) l4[j] = g4[j];
+      __syncthreads();
+      for (int64_t i = threadIdx.x; i < nw; i += 256) {
+        uint64_t wv = 0;
+        int64_t idx = i;
+        for (int f = 0; f < F && idx < dw; ++f, idx += nw) wv |= (uint64_t)img[idx] << (f * b);
+        words[w0 + i] = wv;
+      }
+      __syncthreads();
+      continue;
+    }
     for (int64_t i = threadIdx.x; i < nw; i += 256) {
       uint64_t wv = 0;
       for (int f = 0; f < F; ++f) {
@@ -72,11 +91,16 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
 }
 
 // Merged words -> u32 table, with the exact per-row sum of squares and the
-// owner's largest counter (as k_norms computes them).
+// owner's largest counter (as k_norms computes them).  use_img: a narrow
+// owner's fields are first scattered into an LDS image of its d x w u16
+// counters (one word read per F counters, no per-counter division), which
+// then leaves as 16-byte row-major stores while the norms are summed.
 __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int64_t n, HashParams hp, PackLayout L,
-                                                      TableView tv, uint64_t* norm, uint32_t* rowmax) {
+                                                      TableView tv, uint64_t* norm, uint32_t* rowmax, int use_img) {
+  extern __shared__ __align__(16) uint16_t img[];  // [dw] (use_img)
   __shared__ uint64_t red[4];
   __shared__ uint32_t smax[4];
+  __shared__ unsigned long long s_sq[CMS_MAX_DEPTH];
   const int w = (int)hp.width;
   const int64_t dw = (int64_t)hp.depth * w;
   for (int64_t o = blockIdx.x; o < n; o += gridDim.x) {
@@ -97,6 +121,52 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
     const uint64_t mask = b >= 64 ? ~0ULL : ((1ULL << b) - 1);
     const uint64_t* src = words + L.woff[o];
     uint32_t vmax = 0;
+    if (use_img && !dst) {  // narrow owner: merged counters < 2^16, so b <= 16
+      const int F = 64 / b;
+      for (uint32_t i0 = threadIdx.x; i0 < nw; i0 += 4 * 256) {  // four word loads in flight per lane
+        uint64_t wv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t i = i0 + u * 256;
+          wv[u] = i < nw ? src[i] : 0ULL;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t i = i0 + u * 256;
+          if (i >= nw) break;
+          uint32_t idx = i;
+          for (int f = 0; f < F && idx < (uint32_t)dw; ++f, idx += nw)
+            img[idx] = (uint16_t)((wv[u] >> (f * b)) & mask);
+        }
+      }
+      if (threadIdx.x < hp.depth) s_sq[threadIdx.x] = 0;
+      __syncthreads();
+      // a narrow row's sum of squares is at most mass * max < 2^32: u32 partial
+      // sums by v_dot2_u32_u16 are exact; one wave atomic per row, one barrier
+      u16x2 pm = {0, 0};
+      for (int d = 0; d < hp.depth; ++d) {
+        uint32_t sq = 0;
+        const uint4* r4 = reinterpret_cast<const uint4*>(img + (int64_t)d * w);
+        uint4* g4 = reinterpret_cast<uint4*>(dst16 + (int64_t)d * w);
+        for (int j = threadIdx.x; j < (w >> 3); j += 256) {
+          const uint4 v = r4[j];
+          g4[j] = v;
+          const u16x2 a = __builtin_bit_cast(u16x2, v.x), bq = __builtin_bit_cast(u16x2, v.y),
+                      c = __builtin_bit_cast(u16x2, v.z), e = __builtin_bit_cast(u16x2, v.w);
+          sq = __builtin_amdgcn_udot2(a, a, sq, false);
+          sq = __builtin_amdgcn_udot2(bq, bq, sq, false);
+          sq = __builtin_amdgcn_udot2(c, c, sq, false);
+          sq = __builtin_amdgcn_udot2(e, e, sq, false);
+          pm = __builtin_elementwise_max(pm, __builtin_elementwise_max(__builtin_elementwise_max(a, bq),
+                                                                       __builtin_elementwise_max(c, e)));
+        }
+        const uint32_t tot = wave_sum_u32(sq);
+        if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&s_sq[d], (unsigned long long)tot);
+      }
+      vmax = max((uint32_t)pm.x, (uint32_t)pm.y);
+      __syncthreads();
+      if (threadIdx.x < hp.depth) norm[o * hp.depth + threadIdx.x] = s_sq[threadIdx.x];
+    } else {
     for (int d = 0; d < hp.depth; ++d) {
       uint64_t sq = 0;
       for (int j = threadIdx.x; j < w; j += 256) {
@@ -110,6 +180,7 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
       }
       const uint64_t tot = block_sum_u64_sat(sq, red);
       if (threadIdx.x == 0) norm[o * hp.depth + d] = tot;
+    }
     }
 #pragma unroll
     for (int s = 32; s > 0; s >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, s, 64));
@@ -126,7 +197,7 @@ int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
   int rc;
   if (!h->norms_valid && (rc = local_norms(h))) return rc;
   // 2. one all-reduce of (mass, max) per owner
-  DevBuf bnd;
+  DevBuf& bnd = h->ws_mbnd;  // merge scratch stays allocated across steps
   CMS_HIP(bnd.ensure(sizeof(uint64_t) * 2 * n));
   const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(k_merge_bounds_in, dim3(g), dim3(256), 0, h->stream, h->d_row_mass, h->d_rowmax, n,
@@ -155,17 +226,30 @@ int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
   }
   woff[n] = words;
   h->merge_words = words;
-  DevBuf d_bits, d_woff, packed;
+  DevBuf& d_bits = h->ws_mbits;
+  DevBuf& d_woff = h->ws_mwoff;
+  DevBuf& packed = h->ws_mpacked;
   CMS_HIP(d_bits.ensure(std::max<int64_t>(n, 1)));
   CMS_HIP(d_woff.ensure(sizeof(int64_t) * (n + 1)));
   CMS_HIP(packed.ensure(sizeof(uint64_t) * std::max<int64_t>(words, 1)));
   CMS_HIP(hipMemcpyAsync(d_bits.ptr, bits.data(), n, hipMemcpyHostToDevice, h->stream));
   CMS_HIP(hipMemcpyAsync(d_woff.ptr, woff.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));  // bits / woff are host locals (the stream is idle here anyway)
   PackLayout L{d_bits.as<uint8_t>(), d_woff.as<int64_t>()};
   const unsigned go = (unsigned)std::min<int64_t>(n, 65536);
+  // LDS image path for narrow owners when the image leaves room for 2 blocks per CU
+  const size_t img = sizeof(uint16_t) * (size_t)dw;
+  const int use_img = (h->p.width % 8 == 0 && img <= 80 * 1024) ? 1 : 0;
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_merge_pack, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_merge_unpack, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    return true;
+  }();
+  (void)attr;
   {
     TimedScope ts(h, "merge_pack");
-    hipLaunchKernelGGL(k_merge_pack, dim3(go), dim3(256), 0, h->stream, h->tview(), n, dw, L, packed.as<uint64_t>());
+    hipLaunchKernelGGL(k_merge_pack, dim3(go), dim3(256), use_img ? img : 0, h->stream, h->tview(), n, dw, L,
+                       packed.as<uint64_t>(), use_img);
     CMS_HIP(hipGetLastError());
   }
   {
@@ -176,12 +260,11 @@ int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
   if ((rc = promote_rows(h, h->d_row_mass, nullptr, false))) return rc;
   {
     TimedScope ts(h, "merge_unpack");
-    hipLaunchKernelGGL(k_merge_unpack, dim3(go), dim3(256), 0, h->stream, packed.as<uint64_t>(), n, h->hp, L,
-                       h->tview(), h->d_norm, h->d_rowmax);
+    hipLaunchKernelGGL(k_merge_unpack, dim3(go), dim3(256), use_img ? img : 0, h->stream, packed.as<uint64_t>(), n,
+                       h->hp, L, h->tview(), h->d_norm, h->d_rowmax, use_img);
     CMS_HIP(hipGetLastError());
   }
-  CMS_HIP(hipStreamSynchronize(h->stream));  // scratch is freed on return
-  h->norms_valid = true;                     // the unpack wrote the merged norms
+  h->norms_valid = true;  // the unpack wrote the merged norms
   return CMS_OK;
 }
 
