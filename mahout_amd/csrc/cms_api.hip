@@ -663,6 +663,7 @@ int cms_finalize(cms_handle* h) {
   CMS_HIP(hipMemcpyAsync(h->h_pin, h->d_flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
   const uint32_t inexact = h->h_pin[1];
+  h->inexact_zero = inexact == 0;
   rc = flags_error(h, h->h_pin[0], false);
   if (rc) return rc;
   h->exact_norms = inexact == 0;
@@ -697,6 +698,7 @@ int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   if ((rc = check_flags(h, false))) return rc;
   uint32_t inexact = 0;
   CMS_HIP(hipMemcpy(&inexact, h->d_flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  h->inexact_zero = inexact == 0;
   h->exact_norms = inexact == 0;
   h->mfma_ready = false;
   h->finalized = true;

@@ -357,7 +357,8 @@ int compute_norms(cms_handle* h) {
     h->norms_valid = true;
   }
   int64_t cells = h->n * h->p.depth;
-  CMS_HIP(hipMemsetAsync(h->d_flags + 1, 0, sizeof(uint32_t), h->stream));
+  if (!h->inexact_zero) CMS_HIP(hipMemsetAsync(h->d_flags + 1, 0, sizeof(uint32_t), h->stream));
+  h->inexact_zero = false;  // until a read-back sees 0
   if (cells > 0) {
     unsigned grid = (unsigned)std::min<int64_t>((cells + 255) / 256, 8192);
     hipLaunchKernelGGL(k_norm_sqrt, dim3(grid), dim3(256), 0, h->stream, h->d_norm, cells, h->d_norm_sqrt,

@@ -122,6 +122,7 @@ struct cms_handle {
   uint32_t* d_flags = nullptr;      // error flags word + counters
   uint32_t* h_pin = nullptr;        // pinned host words: flag read-back without a staged copy
   bool stale_possible = true;       // an incremental ingest may have raised flags[2] since the last check
+  bool inexact_zero = true;         // flags[1] (inexact-norm count) is known to be 0 on the device
   int64_t* d_owner_ids = nullptr;   // [n] sorted IDs (null => identity)
   std::vector<int64_t> h_owner_ids;
 
