@@ -349,19 +349,45 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
   for (int f = threadIdx.x; f < P2; f += blockDim.x) H2[(int64_t)blockIdx.x * P2 + f] = lh[f];
 }
 
-// One block per coarse bin: offsets of (block, fine bin) and the CSR row
-// starts of the bin's rows.
-__global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* H2, const uint32_t* binStart,
-                                                  const uint32_t* blkStart, int P1, int P2, int64_t nrows,
-                                                  uint32_t* O2, int64_t* row_start) {
-  __shared__ uint32_t sc[1024 / 64 + 1];
-  __shared__ uint32_t tots[kMaxBins];
-  const int b = blockIdx.x;
+// Offsets of (pass-2 block, fine bin) and the CSR row starts, in three
+// kernels so that no single workgroup walks a Zipf-heavy coarse bin's whole
+// column of block histograms: each coarse bin's blocks are cut into
+// kP2Split chunks whose column sums are taken in parallel (k_p2_colsum), one
+// workgroup per bin scans the bin's totals over fine bins and turns the chunk
+// sums into chunk prefixes (k_p2_scan), and the chunks write their blocks'
+// offsets in parallel (k_p2_offsets).
+constexpr int kP2Split = 16;
+
+__device__ __forceinline__ void p2_chunk(const uint32_t* blkStart, int b, int c, uint32_t& ka, uint32_t& kb) {
   const uint32_t k0 = blkStart[b], k1 = blkStart[b + 1];
+  const uint32_t per = (k1 - k0 + kP2Split - 1) / kP2Split;
+  ka = min(k1, k0 + (uint32_t)c * per);
+  kb = min(k1, ka + per);
+}
+
+__global__ __launch_bounds__(1024) void k_p2_colsum(const uint32_t* H2, const uint32_t* blkStart, int P2,
+                                                    uint32_t* PS) {
+  const int b = blockIdx.x / kP2Split, c = blockIdx.x % kP2Split;
+  uint32_t ka, kb;
+  p2_chunk(blkStart, b, c, ka, kb);
   for (int f = threadIdx.x; f < P2; f += blockDim.x) {
     uint32_t T = 0;
 #pragma unroll 8
-    for (uint32_t k = k0; k < k1; ++k) T += H2[(int64_t)k * P2 + f];
+    for (uint32_t k = ka; k < kb; ++k) T += H2[(int64_t)k * P2 + f];
+    PS[(int64_t)blockIdx.x * P2 + f] = T;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* binStart, int P1, int P2, int64_t nrows,
+                                                  uint32_t* PS, int64_t* row_start) {
+  __shared__ uint32_t sc[1024 / 64 + 1];
+  __shared__ uint32_t tots[kMaxBins];
+  const int b = blockIdx.x;
+  uint32_t* ps = PS + (int64_t)b * kP2Split * P2;
+  for (int f = threadIdx.x; f < P2; f += blockDim.x) {
+    uint32_t T = 0;
+#pragma unroll
+    for (int c = 0; c < kP2Split; ++c) T += ps[(int64_t)c * P2 + f];
     tots[f] = T;
   }
   __syncthreads();
@@ -378,29 +404,44 @@ __global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* H2, const uint
   }
   __syncthreads();
   for (int f = threadIdx.x; f < P2; f += blockDim.x) {
-    uint32_t base = binStart[b] + tots[f];
-    int64_t r = (int64_t)b * P2 + f;
+    const uint32_t base = binStart[b] + tots[f];
+    const int64_t r = (int64_t)b * P2 + f;
     if (r < nrows) row_start[r] = base;
-    uint32_t run = base;
-    // the counts were read above; batch the loads so they are in flight together
-    uint32_t k = k0;
-    for (; k + 8 <= k1; k += 8) {
-      uint32_t c[8];
+    uint32_t run = base;  // chunk sums -> chunk prefixes, in place
 #pragma unroll
-      for (int u = 0; u < 8; ++u) c[u] = H2[(int64_t)(k + u) * P2 + f];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        O2[(int64_t)(k + u) * P2 + f] = run;
-        run += c[u];
-      }
-    }
-    for (; k < k1; ++k) {
-      uint32_t c = H2[(int64_t)k * P2 + f];
-      O2[(int64_t)k * P2 + f] = run;
-      run += c;
+    for (int c = 0; c < kP2Split; ++c) {
+      const uint32_t t = ps[(int64_t)c * P2 + f];
+      ps[(int64_t)c * P2 + f] = run;
+      run += t;
     }
   }
   if (b == P1 - 1 && threadIdx.x == 0) row_start[nrows] = binStart[P1];
+}
+
+__global__ __launch_bounds__(1024) void k_p2_offsets(const uint32_t* H2, const uint32_t* blkStart, int P2,
+                                                     const uint32_t* PS, uint32_t* O2) {
+  const int b = blockIdx.x / kP2Split, c = blockIdx.x % kP2Split;
+  uint32_t ka, kb;
+  p2_chunk(blkStart, b, c, ka, kb);
+  for (int f = threadIdx.x; f < P2; f += blockDim.x) {
+    uint32_t run = PS[(int64_t)blockIdx.x * P2 + f];
+    uint32_t k = ka;
+    for (; k + 8 <= kb; k += 8) {  // the counts' loads in flight together
+      uint32_t cnt[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cnt[u] = H2[(int64_t)(k + u) * P2 + f];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        O2[(int64_t)(k + u) * P2 + f] = run;
+        run += cnt[u];
+      }
+    }
+    for (; k < kb; ++k) {
+      const uint32_t cnt = H2[(int64_t)k * P2 + f];
+      O2[(int64_t)k * P2 + f] = run;
+      run += cnt;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fine, const int64_t* key1,
@@ -513,7 +554,7 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
   CMS_HIP(h->ws_csr_off.ensure(sizeof(int64_t) * (size_t)(n + 1)));
   const int64_t L1 = (int64_t)P1 * NB, L2 = nb2max * P2;
   const int64_t nbs = (L1 + 4095) / 4096 + 1;
-  const size_t hist_words = (size_t)(2 * L1 + 2 * L2 + nbs + 2 * (P1 + 1) + 64);
+  const size_t hist_words = (size_t)(2 * L1 + 2 * L2 + nbs + 2 * (P1 + 1) + 64) + (size_t)P1 * kP2Split * P2;
   CMS_HIP(h->ws_hist.ensure(sizeof(uint32_t) * hist_words));
   uint32_t* H1 = h->ws_hist.as<uint32_t>();
   uint32_t* O1 = H1 + L1;
@@ -522,6 +563,7 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
   uint32_t* bsum = O2 + L2;
   uint32_t* binStart = bsum + nbs;
   uint32_t* blkStart = binStart + (P1 + 1);
+  uint32_t* PS = blkStart + (P1 + 1) + 64;  // [P1][kP2Split][P2] chunk column sums / prefixes
 
   uint16_t* fine = h->ws_p1_row.as<uint16_t>();
   int64_t* key1 = h->ws_p1_key.as<int64_t>();
@@ -546,7 +588,9 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
     hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, O1, H1, NB, P1, CH2, binStart, blkStart);
     hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)nb2max), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,
                        binStart, blkStart, P1, CH2, P2, H2);
-    hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, H2, binStart, blkStart, P1, P2, n, O2, coff);
+    hipLaunchKernelGGL(k_p2_colsum, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS);
+    hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, binStart, P1, P2, n, PS, coff);
+    hipLaunchKernelGGL(k_p2_offsets, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS, O2);
     hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2, d_val != nullptr, false), h->stream, fine,
                        key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     CMS_HIP(hipGetLastError());
