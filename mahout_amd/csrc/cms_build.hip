@@ -34,27 +34,47 @@ struct HotInfo {
   int32_t pad;
 };
 
-constexpr int kKeyRegs = 4;
+#ifndef CMS_KEY_REGS
+#define CMS_KEY_REGS 4
+#endif
+constexpr int kKeyRegs = CMS_KEY_REGS;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // keys cached per thread: owners up to 1024 keys are read once
 
 __global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
-                             int2* extra_map, uint32_t* counters /* [0]=hot rows [2]=extra slices */,
+                             int2* extra_map, uint32_t* counters /* [0]=hot rows [1]=extra slices */,
                              uint64_t* norm, uint32_t* rowmax, int depth) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
-    int64_t c = off[r + 1] - off[r];
-    if (c <= slice) {
-      row_hot[r] = -1;
-      continue;
+  const int lane = (int)__lane_id();
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nrows; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = base + threadIdx.x;
+    const int64_t c = r < nrows ? off[r + 1] - off[r] : 0;
+    const bool is_hot = c > slice;
+    if (r < nrows && !is_hot) row_hot[r] = -1;
+    int32_t ns = 0;
+    uint32_t hidx = 0, e0 = 0;
+    if (is_hot) {
+      ns = (int32_t)((c + slice - 1) / slice);
+      // one 64-bit atomic claims the hot index (low word) and the extra slices (high word)
+      const unsigned long long old =
+          atomicAdd(reinterpret_cast<unsigned long long*>(counters), ((unsigned long long)(ns - 1) << 32) | 1ULL);
+      hidx = (uint32_t)old;
+      e0 = (uint32_t)(old >> 32);
+      hot[hidx] = HotInfo{r, ns, 0};
+      row_hot[r] = (int32_t)hidx;
+      for (int d = 0; d < depth; ++d) norm[r * depth + d] = 0;
+      rowmax[r] = 0;
     }
-    int32_t ns = (int32_t)((c + slice - 1) / slice);
-    uint32_t hidx = atomicAdd(&counters[0], 1u);
-    uint32_t e0 = atomicAdd(&counters[2], (uint32_t)(ns - 1));
-    hot[hidx] = HotInfo{r, ns, 0};
-    row_hot[r] = (int32_t)hidx;
-    for (int32_t s = 1; s < ns; ++s) extra_map[e0 + s - 1] = make_int2((int)hidx, s);
-    for (int d = 0; d < depth; ++d) norm[r * depth + d] = 0;
-    rowmax[r] = 0;
+    // the wave writes each hot row's slice map together (a Zipf head row has
+    // hundreds of slices)
+    unsigned long long m = __ballot(is_hot);
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const int32_t nsl = __builtin_amdgcn_readlane(ns, l);
+      const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hidx, l);
+      const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)e0, l);
+      for (int32_t sl = 1 + lane; sl < nsl; sl += 64) extra_map[el + sl - 1] = make_int2((int)hl, sl);
+    }
   }
 }
 
@@ -106,7 +126,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   int64_t row, lo, hi;
   bool atomic_mode;
   if (blockIdx.x < emax) {
-    if (blockIdx.x >= counters[2]) return;
+    if (blockIdx.x >= counters[1]) return;
 #ifdef CMS_BUILD_NOSLICES  // bound analysis only: hot rows' extra slices skipped
     return;
 #endif
@@ -347,12 +367,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   }
 }
 
-// Sum of squares of the hot rows after every slice landed; grid (max_hot, depth, chunks of 1024).
+// Sum of squares of the hot rows after every slice landed; grid (<= 256, depth,
+// chunks of 1024), blocks striding over the hot rows the plan counted (the
+// host's bound on them is loose, and empty blocks still cost launch time).
 __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uint32_t* counters, HashParams hp,
                                                    TableView tv, uint64_t* norm, uint32_t* rowmax) {
   __shared__ uint64_t red[4];
-  if (blockIdx.x >= counters[0]) return;
-  const int64_t row = hot[blockIdx.x].row;
+  const uint32_t nhot = counters[0];
+  for (uint32_t hb = blockIdx.x; hb < nhot; hb += gridDim.x) {
+  const int64_t row = hot[hb].row;
   const int d = blockIdx.y;
   const int w = (int)hp.width;
   const uint32_t* p = tv.hot + (int64_t)tv.hidx[row] * tv.dw + (int64_t)d * w;  // split rows are slots
@@ -368,6 +391,7 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
   uint64_t tot = block_sum_u64_sat(sq, red);
   if (tot > (1ULL << 60)) tot = 1ULL << 60;
   if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
+  }
 }
 
 int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,
@@ -397,7 +421,7 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
   int32_t* row_hot = reinterpret_cast<int32_t*>(base);
   HotInfo* hot = reinterpret_cast<HotInfo*>(base + sz_rowhot);
   int2* extra_map = reinterpret_cast<int2*>(base + sz_rowhot + sz_hot);
-  uint32_t* counters = h->d_flags + 4;  // [4..7]
+  uint32_t* counters = h->d_flags + 4;  // [4..7]: hot rows, extra slices (one u64 atomic), spare
   CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
   // table layout: rows that could reach 2^16, and split rows, get u32 slots
   {
@@ -411,13 +435,18 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
                           force.as<uint8_t>())))
       return rc0;
     // A fresh build with implicit (unit) increments: a row needs a slot when
-    // its mass reaches 2^16 (at most total / 2^16 rows) or it is split into
-    // slices (more than kSlice keys: at most npairs / (kSlice + 1) rows), a
-    // bound the host knows without reading anything back.
+    // it is split into slices (more than kSlice keys: at most
+    // npairs / (kSlice + 1) rows) or its mass reaches 2^16 (at most
+    // total / 2^16 rows; with 2^(16 - s) > kSlice keys such a row is split
+    // anyway) -- a bound the host knows without reading anything back.
+    // Reserving costs slot memory, so only a bound worth at most 2 GB of
+    // slots takes this path; a larger job reads the count back.
     int64_t max_new = -1;
-    if (!accumulate && !d_val && h->hp.frac_bits < 32) {
-      const uint64_t total = (uint64_t)npairs << h->hp.frac_bits;
-      max_new = (int64_t)(total / kNarrowLimit) + npairs / (kSlice + 1) + 1;
+    if (!accumulate && !d_val && h->hp.frac_bits < 16) {
+      const int64_t split = npairs / (kSlice + 1) + 1;
+      const int64_t heavy = (int64_t)(((uint64_t)npairs << h->hp.frac_bits) / kNarrowLimit);
+      const int64_t slots = (int64_t(1) << (16 - h->hp.frac_bits)) > kSlice ? split : split + heavy;
+      if ((double)slots * (double)h->dw * 4.0 <= 2.0e9) max_new = slots;
     }
     if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0, max_new))) return rc0;
   }
@@ -438,7 +467,7 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
   }
   {
     TimedScope ts(h, "hot_norms");
-    dim3 grid((unsigned)max_hot, (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
+    dim3 grid((unsigned)std::min<int64_t>(max_hot, 256), (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
     hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
                        h->d_rowmax);
     CMS_HIP(hipGetLastError());

@@ -87,7 +87,10 @@ struct TableView {
 };
 
 // Row-build tuning: pairs per build work item.
-constexpr int64_t kSlice = 32768;
+#ifndef CMS_SLICE
+#define CMS_SLICE 8192  // keys per row-build workgroup of a split (hot) owner
+#endif
+constexpr int64_t kSlice = CMS_SLICE;
 #ifndef CMS_BUILD_THREADS
 #define CMS_BUILD_THREADS 256
 #endif

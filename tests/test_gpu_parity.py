@@ -60,7 +60,7 @@ def test_ingest_partition_path_with_hot_rows(oracle, n, d, w, npairs):
         got = t.read_counters()
     exp = oracle_table(oracle, n, d, w, 7, items, users)
     assert same(got, exp)
-    assert np.bincount(items, minlength=n).max() > 32768  # a hot row was split into slices
+    assert np.bincount(items, minlength=n).max() > 32768  # a hot row was split into several slices
 
 
 @pytest.mark.parametrize("shape", ["u32_max", "one_wide", "negative", "edge"])
