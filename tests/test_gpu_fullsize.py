@@ -1,0 +1,68 @@
+"""Config 2 at full size (BASELINE.json configs[1]: Zipf 1M users x 100K items,
+50M pairs, d=5, w=4096) through the device COO path the bench times.
+
+The oracle cannot rebuild 50M pairs in seconds, so the whole table is checked
+through size-independent properties of DoubleCountMinSketch.update
+(`T/impl/common/DoubleCountMinSketch.java:72-80`): every update adds its
+increment once to each of the d rows, so with unit increments each row of an
+owner's sketch sums to that owner's pair count (a checksum per owner per row,
+all 100K owners); the table does not depend on stream order (a shuffled copy
+of the stream builds the identical table); and the owners the hot-row paths
+handle (the hottest ones) plus a random sample are rebuilt by the oracle from
+their own pairs and compared bit for bit.
+"""
+import numpy as np
+import pytest
+
+from mahout_amd import SketchTable
+from mahout_amd.synth import zipf_stream_torch
+
+pytestmark = pytest.mark.gpu
+
+N_USERS, N_ITEMS, N_PAIRS, D, W, SEED = 1_000_000, 100_000, 50_000_000, 5, 4096, 42
+CHUNK = 2500  # owners per read-back: 2500 x 5 x 4096 fp64 = 410 MB of host memory
+
+
+def _build(items, users):
+    t = SketchTable(N_ITEMS, depth=D, width=W, seed=SEED)
+    t.ingest_device_rows(items, users, None, items.numel())
+    t.finalize()
+    t.synchronize()
+    return t
+
+
+def test_config2_full_size_properties(oracle):
+    import torch
+
+    items, users = zipf_stream_torch(N_USERS, N_ITEMS, N_PAIRS, device="cuda")
+    counts = torch.bincount(items, minlength=N_ITEMS).cpu().numpy()
+    assert int(counts.sum()) == N_PAIRS
+
+    perm = torch.randperm(N_PAIRS, device="cuda", generator=torch.Generator(device="cuda").manual_seed(7))
+    t1 = _build(items, users)
+    t2 = _build(items[perm], users[perm])
+    del perm
+    try:
+        # checksum of checksums: every row of every owner sums to its pair count
+        for o in range(0, N_ITEMS, CHUNK):
+            c1 = t1.read_counters(o, CHUNK)
+            sums = c1.sum(axis=2)
+            np.testing.assert_array_equal(sums, np.repeat(counts[o:o + CHUNK, None], D, axis=1).astype(np.float64))
+            if (o // CHUNK) % 8 == 0:  # order independence, 1 chunk in 8 (the read-back dominates the test)
+                np.testing.assert_array_equal(t2.read_counters(o, CHUNK), c1)
+            del c1
+
+        # bit-exact owners: the 4 hottest (the 8192-key slice / hot-row path) and 12 random ones
+        rng = np.random.default_rng(2026)
+        hot = np.argsort(counts)[-4:]
+        sample = np.concatenate([hot, rng.choice(np.flatnonzero(counts), 12, replace=False)])
+        a, b = oracle.hash_params(SEED, D)
+        for owner in sample.tolist():
+            mask = items == owner
+            keys = users[mask].cpu().numpy()
+            assert keys.size == counts[owner]
+            want = oracle.build_table(1, D, W, a, b, np.zeros(keys.size, np.int64), keys)
+            np.testing.assert_array_equal(t1.read_counters(owner, 1), want)
+    finally:
+        t1.close()
+        t2.close()
