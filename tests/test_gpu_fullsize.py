@@ -66,3 +66,29 @@ def test_config2_full_size_properties(oracle):
     finally:
         t1.close()
         t2.close()
+
+
+def test_config2_full_size_csr_equals_coo():
+    """The DataModel layout (per-owner CSR, `GenericDataModel.java:91`) and the
+    unordered COO stream build the same config-2 table."""
+    import torch
+
+    items, users = zipf_stream_torch(N_USERS, N_ITEMS, N_PAIRS, seed=11, device="cuda")
+    order = torch.sort(items, stable=True).indices
+    offsets = torch.zeros(N_ITEMS + 1, dtype=torch.int64, device="cuda")
+    offsets[1:] = torch.cumsum(torch.bincount(items, minlength=N_ITEMS), 0)
+    csr_keys = users[order].contiguous()
+    del order
+    t1 = _build(items, users)
+    t2 = SketchTable(N_ITEMS, depth=D, width=W, seed=SEED)
+    try:
+        t2.ingest_csr_device(offsets, csr_keys)
+        t2.finalize()
+        t2.synchronize()
+        for o in range(0, N_ITEMS, 4 * CHUNK):  # 1 chunk in 4, the hottest owners are spread by the permutation
+            np.testing.assert_array_equal(t2.read_counters(o, CHUNK), t1.read_counters(o, CHUNK))
+        hot = int(torch.argmax(offsets[1:] - offsets[:-1]))
+        np.testing.assert_array_equal(t2.read_counters(hot, 1), t1.read_counters(hot, 1))
+    finally:
+        t1.close()
+        t2.close()
