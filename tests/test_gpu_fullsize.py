@@ -92,3 +92,40 @@ def test_config2_full_size_csr_equals_coo():
     finally:
         t1.close()
         t2.close()
+
+
+def test_config2_full_size_top_k_all(oracle):
+    """All-pairs top-100 over the whole config-2 table: the
+    symmetric streaming pass (`cms_top_k_all`) equals the per-row slab path on
+    sampled row blocks, every list is full and ordered (score desc, ID asc,
+    `SimilarUser.java:62-78`), and sampled scores equal the oracle's
+    `CosineCM` on the owners' fp64 sketches."""
+    import torch
+
+    k = 100
+    items, users = zipf_stream_torch(N_USERS, N_ITEMS, N_PAIRS, device="cuda")
+    t = _build(items, users)
+    del items, users
+    try:
+        ids, sc, cnt = t.top_k_all(k)
+        assert (cnt == k).mean() > 0.99  # only owners with (almost) no pairs can have short lists
+        valid = np.arange(k)[None, :] < cnt[:, None]
+        assert not np.isnan(sc[valid]).any()
+        pair = valid[:, 1:]
+        assert (np.diff(sc, axis=1)[pair] <= 0).all()
+        tie = pair & (np.diff(sc, axis=1) == 0)
+        assert (np.diff(ids, axis=1)[tie] > 0).all()
+        assert (ids != np.arange(N_ITEMS)[:, None])[valid].all()  # self is NaN, never listed
+        for begin in (0, 41_000, N_ITEMS - 512):
+            ri, rs, rc = t.top_k_rows(begin, 512, k)
+            np.testing.assert_array_equal(rc, cnt[begin:begin + 512])
+            np.testing.assert_array_equal(ri, ids[begin:begin + 512])
+            np.testing.assert_array_equal(rs, sc[begin:begin + 512])
+        rng = np.random.default_rng(5)
+        for row in rng.choice(np.flatnonzero(cnt == k), 3, replace=False).tolist():
+            sa = t.read_counters(row, 1)[0]
+            for j in (0, 1, k // 2, k - 1):
+                want = oracle.cosine_cm(sa, t.read_counters(int(ids[row, j]), 1)[0])
+                assert sc[row, j] == want
+    finally:
+        t.close()
