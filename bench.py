@@ -408,13 +408,62 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     }
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, child_argv, port=None, timeout=None):
+    """One process per GPU when bench.py is started without a launcher:
+    children get RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+    exactly as torch.distributed.run sets them (127.0.0.1 rendezvous).  No
+    GPU is touched here.  Returns non-zero if any rank fails."""
+    import subprocess
+    port = port or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(child_argv, env=env))
+    rcs = [None] * n
+    try:
+        for r, p in enumerate(procs):
+            rcs[r] = p.wait(timeout=timeout)
+            if rcs[r] != 0:  # a failed rank would leave the others waiting in a collective
+                for q in procs:
+                    if q.poll() is None:
+                        q.kill()
+    finally:
+        for r, p in enumerate(procs):
+            if p.poll() is None:
+                p.kill()
+            rcs[r] = p.wait()
+    bad = [r for r, c in enumerate(rcs) if c != 0]
+    if bad:
+        print(f"bench: ranks {bad} failed (exit codes {[rcs[r] for r in bad]})", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # self-launch: one rank per GPU (before any GPU call in this process)
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            sys.exit(2)
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     device = f"cuda:{local}"
     if world > 1:

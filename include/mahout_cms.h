@@ -165,6 +165,20 @@ int cms_finalize(cms_handle* h);
  * merged table takes no further ingest until cms_reset (CMS_E_STATE). */
 typedef int (*cms_allreduce_fn)(void* d_buf, int64_t count, void* user);
 int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user);
+/* A whole multi-rank communicator supplied by the caller instead of RCCL (an
+ * MPI, torch.distributed or Spark transport).  After this call the handle
+ * behaves exactly as after cms_comm_init: cms_finalize merges through
+ * `allreduce` (as cms_finalize_with), later COO batches go into the delta log
+ * and the next cms_finalize exchanges the logs through `allgather`, and
+ * cms_top_k_all is collective (partial lists gathered through `allgather`,
+ * merged exactly).  allgather(d_send, d_recv, bytes, user) must write the
+ * `bytes` bytes of every rank's d_send, concatenated in rank order, to d_recv
+ * (world * bytes, device memory on the handle's device; the handle's stream
+ * is idle during the call) and return 0.  Every rank makes the same sequence
+ * of calls with identical sizes.  world == 1 detaches any communicator. */
+typedef int (*cms_allgather_fn)(const void* d_send, void* d_recv, int64_t bytes, void* user);
+int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allreduce_fn allreduce,
+                            cms_allgather_fn allgather, void* user);
 int cms_synchronize(cms_handle* h);
 /* Stream ordering without a host wait (stream: a hipStream_t of the handle's
  * device, e.g. the caller's current torch stream; NULL = legacy default).
@@ -255,6 +269,12 @@ int cms_format_java_double(double v, char* buf, int32_t cap);
 /* Counters of rows [row_begin, row_begin+row_count) as fp64 (the reference's
  * counter type), [row_count][d][w]. */
 int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, double* out);
+/* The same counters without leaving the device: u32 in counter units (the
+ * preference times 2^frac_bits), [row_count][d][w], written to d_out on the
+ * handle's stream (asynchronous, like the device ingests) -- for a device-side
+ * consumer of the sketches (getExportedCMProfile for many owners,
+ * CosineCM.java:60-67) and for whole-table checks at sizes the host cannot hold. */
+int cms_read_counters_device(cms_handle* h, int64_t row_begin, int64_t row_count, uint32_t* d_out);
 
 /* ---- per-owner sketch shapes: CosineCM with its CountMinSketchConfig --------
  * The reference sizes every owner's sketch separately.  CountMinSketchConfig

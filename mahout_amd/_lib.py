@@ -40,6 +40,7 @@ EXPORTS = [
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
     "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities",
+    "cms_comm_init_transport", "cms_read_counters_device",
 ]
 
 
@@ -84,6 +85,8 @@ _dbl = ctypes.c_double
 
 # int (*cms_allreduce_fn)(void* d_buf, int64_t count, void* user)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+# int (*cms_allgather_fn)(const void* d_send, void* d_recv, int64_t bytes, void* user)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
 
 _SIGS = {
     "cms_params_init": (_int, [ctypes.POINTER(CmsParams)]),
@@ -126,6 +129,8 @@ _SIGS = {
     "cms_reset_timing": (_int, [_vp]),
     "cms_create_per_owner": (_int, [ctypes.POINTER(CmsParams), ctypes.POINTER(_vp)]),
     "cms_finalize_with": (_int, [_vp, _vp, _vp]),
+    "cms_comm_init_transport": (_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
+    "cms_read_counters_device": (_int, [_vp, _i64, _i64, _vp]),
     "cms_write_similarities": (_int, [_vp, ctypes.c_char_p, _i32, _i32]),
     "cms_configure_owner_shapes": (_int, [_vp, _dbl, _i64]),
     "cms_set_owner_delta_epsilon": (_int, [_vp, _vp, _vp]),

@@ -175,6 +175,32 @@ static int require_finalized(cms_handle* h) {
   return CMS_OK;
 }
 
+int coll_allreduce_u64(cms_handle* h, uint64_t* d_buf, int64_t count) {
+  if (count <= 0) return CMS_OK;
+  if (h->ext_comm) {
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    const int r = h->x_allreduce(d_buf, count, h->x_user);
+    if (r != 0) return set_error(CMS_E_RCCL, "caller all-reduce returned %d", r);
+    return CMS_OK;
+  }
+  ncclResult_t r = ncclAllReduce(d_buf, d_buf, (size_t)count, ncclUint64, ncclSum, h->comm, h->stream);
+  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+  return CMS_OK;
+}
+
+int coll_allgather(cms_handle* h, const void* d_send, void* d_recv, int64_t bytes) {
+  if (bytes <= 0) return CMS_OK;
+  if (h->ext_comm) {
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    const int r = h->x_allgather(d_send, d_recv, bytes, h->x_user);
+    if (r != 0) return set_error(CMS_E_RCCL, "caller all-gather returned %d", r);
+    return CMS_OK;
+  }
+  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes, ncclUint8, h->comm, h->stream);
+  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+  return CMS_OK;
+}
+
 }  // namespace cms
 
 using namespace cms;
@@ -377,7 +403,7 @@ int dlog_reserve(cms_handle* h, int64_t need) {
 
 // Log a batch (rows already resolved) that went into a merged multi-rank table.
 int dlog_append(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n) {
-  if (!(h->merged && h->comm && h->world > 1) || n <= 0) return CMS_OK;
+  if (!(h->merged && h->multi()) || n <= 0) return CMS_OK;
   int rc = dlog_reserve(h, h->dlog_n + n);
   if (rc) return rc;
   const int64_t o = h->dlog_n;
@@ -397,26 +423,24 @@ int dlog_exchange(cms_handle* h) {
   CMS_HIP(h->dlog_cnt.ensure(sizeof(int64_t) * (G + 1)));
   int64_t* cnt = h->dlog_cnt.as<int64_t>();
   CMS_HIP(hipMemcpyAsync(cnt, &h->dlog_n, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-  ncclResult_t r = ncclAllGather(cnt, cnt + 1, 1, ncclInt64, h->comm, h->stream);
-  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather(delta counts): %s", ncclGetErrorString(r));
+  int rc = coll_allgather(h, cnt, cnt + 1, sizeof(int64_t));
+  if (rc) return rc;
   std::vector<int64_t> counts(G);
   CMS_HIP(hipMemcpyAsync(counts.data(), cnt + 1, sizeof(int64_t) * G, hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
   const int64_t m = *std::max_element(counts.begin(), counts.end());
   if (m == 0) return CMS_OK;
-  int rc = dlog_reserve(h, m);  // the send buffers are read to length m
+  rc = dlog_reserve(h, m);  // the send buffers are read to length m
   if (rc) return rc;
   const size_t per = sizeof(int64_t) * 2 + sizeof(float);
   CMS_HIP(h->dlog_all.ensure(per * (size_t)G * (size_t)m));
   int64_t* g_row = h->dlog_all.as<int64_t>();
   int64_t* g_key = g_row + (size_t)G * m;
   float* g_val = reinterpret_cast<float*>(g_key + (size_t)G * m);
-  ncclGroupStart();
-  ncclAllGather(h->dlog_row.ptr, g_row, (size_t)m, ncclInt64, h->comm, h->stream);
-  ncclAllGather(h->dlog_key.ptr, g_key, (size_t)m, ncclInt64, h->comm, h->stream);
-  ncclAllGather(h->dlog_val.ptr, g_val, (size_t)m, ncclFloat32, h->comm, h->stream);
-  r = ncclGroupEnd();
-  if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather(delta logs): %s", ncclGetErrorString(r));
+  if ((rc = coll_allgather(h, h->dlog_row.ptr, g_row, (int64_t)sizeof(int64_t) * m)) ||
+      (rc = coll_allgather(h, h->dlog_key.ptr, g_key, (int64_t)sizeof(int64_t) * m)) ||
+      (rc = coll_allgather(h, h->dlog_val.ptr, g_val, (int64_t)sizeof(float) * m)))
+    return rc;
   for (int q = 0; q < G; ++q) {
     if (q == h->rank || counts[q] == 0) continue;
     const size_t o = (size_t)q * m;
@@ -489,7 +513,7 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
   const int64_t np = offsets[n];
   if (np > 0 && !keys) return set_error(CMS_E_PARAM, "null keys");
   Guard g(h);
-  if (h->merged && h->comm && h->world > 1)
+  if (h->merged && h->multi())
     return set_error(CMS_E_STATE, "CSR bulk ingest into a merged multi-rank table: cms_reset first, or use COO ingest");
   CMS_HIP(h->ws_in_row.ensure(sizeof(int64_t) * (n + 1)));
   CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * std::max<int64_t>(np, 1)));
@@ -530,7 +554,7 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
     return set_error(CMS_E_STATE, "table merged through cms_finalize_with: cms_reset starts a new epoch");
   if (!h || !d_offsets) return set_error(CMS_E_PARAM, "null argument");
   Guard g(h);
-  if (h->merged && h->comm && h->world > 1)
+  if (h->merged && h->multi())
     return set_error(CMS_E_STATE, "CSR bulk ingest into a merged multi-rank table: cms_reset first, or use COO ingest");
   int64_t np = 0;
   CMS_HIP(hipMemcpyAsync(&np, d_offsets + h->n, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
@@ -605,6 +629,7 @@ int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t wo
     (void)ncclCommDestroy(h->comm);
     h->comm = nullptr;
   }
+  h->ext_comm = false;
   h->rank = rank;
   h->world = world;
   if (world == 1) return CMS_OK;
@@ -612,6 +637,26 @@ int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t wo
   std::memcpy(&id, unique_id, sizeof(id));
   ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
   if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  return CMS_OK;
+}
+
+int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allreduce_fn allreduce,
+                            cms_allgather_fn allgather, void* user) {
+  if (!h) return set_error(CMS_E_PARAM, "null handle");
+  if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
+  if (world > 1 && (!allreduce || !allgather)) return set_error(CMS_E_PARAM, "null transport function");
+  if (int rc0 = refuse_per_owner(h, "cms_comm_init_transport")) return rc0;
+  Guard g(h);
+  if (h->comm) {
+    (void)ncclCommDestroy(h->comm);
+    h->comm = nullptr;
+  }
+  h->rank = world > 1 ? rank : 0;
+  h->world = world;
+  h->ext_comm = world > 1;
+  h->x_allreduce = allreduce;
+  h->x_allgather = allgather;
+  h->x_user = user;
   return CMS_OK;
 }
 
@@ -641,18 +686,14 @@ int cms_finalize(cms_handle* h) {
     h->empty = false;
     h->norms_valid = false;
   }
-  if (h->comm && h->world > 1 && h->merged) {
+  if (h->multi() && h->merged) {
     TimedScope ts(h, "delta_exchange");
     int rc = dlog_exchange(h);
     if (rc) return rc;
-  } else if (h->comm && h->world > 1) {
-    // counter-width-adaptive packed sums over RCCL (cms_merge.hip)
-    auto rccl = [h](uint64_t* buf, int64_t count) -> int {
-      ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, ncclUint64, ncclSum, h->comm, h->stream);
-      if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-      return CMS_OK;
-    };
-    int rc = merge_packed(h, rccl);
+  } else if (h->multi()) {
+    // counter-width-adaptive packed sums over RCCL / the transport (cms_merge.hip)
+    auto sum = [h](uint64_t* buf, int64_t count) -> int { return coll_allreduce_u64(h, buf, count); };
+    int rc = merge_packed(h, sum);
     if (rc) return rc;
     h->merged = true;
     h->dlog_n = 0;
@@ -676,7 +717,7 @@ int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   if (!h || !fn) return set_error(CMS_E_PARAM, "null argument");
   if (int rc0 = refuse_per_owner(h, "cms_finalize_with")) return rc0;
   Guard g(h);
-  if (h->comm) return set_error(CMS_E_STATE, "handle has an RCCL communicator: use cms_finalize");
+  if (h->comm || h->ext_comm) return set_error(CMS_E_STATE, "handle has a communicator: use cms_finalize");
   if (h->ext_merged) return set_error(CMS_E_STATE, "already merged: cms_reset starts a new epoch");
   if (h->empty) {
     CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * h->n * h->dw, h->stream));
@@ -885,10 +926,10 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
   CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
   CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
   CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
-  if (h->comm && h->world > 1) {
+  if (h->multi()) {
     // one process per GPU: rank r computes shard r of the pairs, then one
-    // all-gather of the partial lists over xGMI and an exact merge
-    if ((int64_t)h->world * k > kCandCap) return set_error(CMS_E_PARAM, "world * k must be <= %d", kCandCap);
+    // all-gather of the partial lists over xGMI and an exact merge (in rounds
+    // of kCandCap / k lists when world * k exceeds a merge workgroup's LDS)
     const int G = h->world;
     DevBuf g_ids, g_sc, g_cnt;
     CMS_HIP(g_ids.ensure(sizeof(int64_t) * n * k * G));
@@ -898,15 +939,10 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
     if (rc) return rc;
     {
       TimedScope ts(h, "topk_allgather");
-      ncclResult_t r = ncclGroupStart();
-      if (r == ncclSuccess)
-        r = ncclAllGather(o_ids.ptr, g_ids.ptr, (size_t)(n * k), ncclInt64, h->comm, h->stream);
-      if (r == ncclSuccess)
-        r = ncclAllGather(o_sc.ptr, g_sc.ptr, (size_t)(n * k), ncclFloat64, h->comm, h->stream);
-      if (r == ncclSuccess) r = ncclAllGather(o_cnt.ptr, g_cnt.ptr, (size_t)n, ncclInt32, h->comm, h->stream);
-      ncclResult_t r2 = ncclGroupEnd();
-      if (r == ncclSuccess) r = r2;
-      if (r != ncclSuccess) return set_error(CMS_E_RCCL, "ncclAllGather(top-k lists): %s", ncclGetErrorString(r));
+      if ((rc = coll_allgather(h, o_ids.ptr, g_ids.ptr, (int64_t)sizeof(int64_t) * n * k)) ||
+          (rc = coll_allgather(h, o_sc.ptr, g_sc.ptr, (int64_t)sizeof(double) * n * k)) ||
+          (rc = coll_allgather(h, o_cnt.ptr, g_cnt.ptr, (int64_t)sizeof(int32_t) * n)))
+        return rc;
     }
     rc = top_k_merge(h, k, G, g_ids.as<int64_t>(), g_sc.as<double>(), g_cnt.as<int32_t>(), o_ids.as<int64_t>(),
                      o_sc.as<double>(), o_cnt.as<int32_t>());
@@ -955,8 +991,8 @@ int cms_top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* ids
                     const int32_t* counts, int64_t* out_ids, double* out_scores, int32_t* out_counts) {
   if (!h || !ids || !scores || !counts || !out_ids || !out_scores || !out_counts)
     return set_error(CMS_E_PARAM, "null argument");
-  if (k < 1 || nparts < 1 || (int64_t)nparts * k > kCandCap)
-    return set_error(CMS_E_PARAM, "need k >= 1 and nparts * k <= %d", kCandCap);
+  if (k < 1 || k > kCandCap / 2 || nparts < 1)
+    return set_error(CMS_E_PARAM, "need k in [1, %d] and nparts >= 1", kCandCap / 2);
   Guard g(h);
   const int64_t n = h->n;
   DevBuf i_ids, i_sc, i_cnt, o_ids, o_sc, o_cnt;
@@ -1035,6 +1071,14 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
     }
   }
   return CMS_OK;
+}
+
+int cms_read_counters_device(cms_handle* h, int64_t row_begin, int64_t row_count, uint32_t* d_out) {
+  if (!h || (row_count > 0 && !d_out)) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "cms_read_counters_device")) return rc0;
+  Guard g(h);
+  if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
+  return read_counters_device(h, row_begin, row_count, d_out);
 }
 
 int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capacity, int32_t* width, int32_t* depth) {

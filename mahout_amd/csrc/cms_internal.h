@@ -162,9 +162,14 @@ struct cms_handle {
   cms::DevBuf ws_query, ws_out, ws_srow, ws_f4;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 
-  // communicator
+  // communicator: RCCL (cms_comm_init) or a caller transport (cms_comm_init_transport)
   ncclComm_t comm = nullptr;
   int32_t rank = 0, world = 1;
+  cms_allreduce_fn x_allreduce = nullptr;  // caller transport (ext_comm)
+  cms_allgather_fn x_allgather = nullptr;
+  void* x_user = nullptr;
+  bool ext_comm = false;
+  bool multi() const { return world > 1 && (comm != nullptr || ext_comm); }
   // After the first multi-rank finalize every rank holds the summed table; later
   // COO batches are logged here and only the logs are exchanged at the next
   // finalize (each rank applies the other ranks' batches).
@@ -240,8 +245,15 @@ int count_hot_rows(cms_handle* h, int64_t* out);
 // and the rows split over more than `slice` keys (cms_build.hip)
 int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,
                uint64_t* bound, uint8_t* force);
+// counters of rows [r0, r0 + rc) as u32 into a device buffer (stream-ordered)
+int read_counters_device(cms_handle* h, int64_t r0, int64_t rc, uint32_t* d_out);
 // all rows narrow and zero-able again (empty table)
 int reset_table_layout(cms_handle* h);
+// ---- collectives over the handle's communicator (cms_api.hip) ----
+// in-place u64 sum over all ranks (RCCL all-reduce or the caller transport)
+int coll_allreduce_u64(cms_handle* h, uint64_t* d_buf, int64_t count);
+// recv = the `bytes` of every rank's send, concatenated in rank order
+int coll_allgather(cms_handle* h, const void* d_send, void* d_recv, int64_t bytes);
 // ---- cms_merge.hip ----
 // in-place u64 sum over all ranks of count words of a device buffer
 using AllReduceU64 = std::function<int(uint64_t*, int64_t)>;

@@ -131,6 +131,37 @@ int count_hot_rows(cms_handle* h, int64_t* out) {
   return CMS_OK;
 }
 
+// counters of rows [r0, r0 + rc) as u32, [rc][dw] (cms_read_counters_device)
+__global__ void k_read_u32(TableView tv, int64_t r0, int64_t rc, uint32_t* out, int vec) {
+  const int64_t total = rc * tv.dw;
+  for (int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4; i < total;
+       i += (int64_t)gridDim.x * blockDim.x * 4) {
+    const int64_t r = i / tv.dw, j = i - r * tv.dw;
+    if (vec) {
+      *reinterpret_cast<uint4*>(out + i) = tv.get4(r0 + r, j);
+    } else {
+      for (int64_t e = i; e < min(i + 4, total); ++e) {
+        const int64_t re = e / tv.dw;
+        out[e] = tv.get(r0 + re, e - re * tv.dw);
+      }
+    }
+  }
+}
+
+int read_counters_device(cms_handle* h, int64_t r0, int64_t rc, uint32_t* d_out) {
+  if (rc <= 0) return CMS_OK;
+  if (h->empty) {
+    CMS_HIP(hipMemsetAsync(d_out, 0, sizeof(uint32_t) * (size_t)rc * (size_t)h->dw, h->stream));
+    return CMS_OK;
+  }
+  const int64_t quads = (rc * h->dw + 3) / 4;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((quads + 255) / 256, 65536));
+  const int vec = (h->dw & 3) == 0 && ((uintptr_t)d_out & 15) == 0;
+  hipLaunchKernelGGL(k_read_u32, dim3(g), dim3(256), 0, h->stream, h->tview(), r0, rc, d_out, vec);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int reset_table_layout(cms_handle* h) {
   CMS_HIP(hipMemsetAsync(h->d_hidx, 0xff, sizeof(int32_t) * (size_t)h->n, h->stream));
   h->hot_used = 0;

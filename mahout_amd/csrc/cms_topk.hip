@@ -582,11 +582,43 @@ __global__ __launch_bounds__(kCandThreads) void k_topk_merge(int32_t nparts, int
 
 int top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* d_ids, const double* d_scores,
                 const int32_t* d_counts, int64_t* d_out_ids, double* d_out_scores, int32_t* d_out_counts) {
-  if ((int64_t)nparts * k > kCandCap) return set_error(CMS_E_PARAM, "nparts * k must be <= %d", kCandCap);
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
   TimedScope ts(h, "topk_merge");
-  hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)std::min<int64_t>(h->n, 8192)), dim3(kCandThreads), 0, h->stream,
-                     nparts, k, h->n, d_ids, d_scores, d_counts, d_out_ids, d_out_scores, d_out_counts);
+  const int64_t n = h->n;
+  const unsigned grid = (unsigned)std::min<int64_t>(n, 8192);
+  // A merge workgroup holds kCandCap candidates in LDS, so more than
+  // kCandCap / k lists merge in rounds: groups of g lists -> one list each.
+  // Exact: the first k of a union under the (score desc, ID asc) total order
+  // are the first k of the union of each group's first k (the shards' pair
+  // sets are disjoint, so no owner appears twice).
+  const int32_t g = kCandCap / k;
+  DevBuf tmp[2];
+  int cur = -1;
+  while (nparts > g) {
+    const int32_t groups = (nparts + g - 1) / g;
+    DevBuf& o = tmp[(cur + 1) & 1];
+    CMS_HIP(o.ensure((sizeof(int64_t) + sizeof(double)) * (size_t)groups * n * k + sizeof(int32_t) * (size_t)groups * n));
+    int64_t* oi = o.as<int64_t>();
+    double* os = reinterpret_cast<double*>(oi + (size_t)groups * n * k);
+    int32_t* oc = reinterpret_cast<int32_t*>(os + (size_t)groups * n * k);
+    for (int32_t q = 0; q < groups; ++q) {
+      const int64_t p0 = (int64_t)q * g;
+      const int32_t np = (int32_t)std::min<int64_t>(g, nparts - p0);
+      hipLaunchKernelGGL(k_topk_merge, dim3(grid), dim3(kCandThreads), 0, h->stream, np, k, n, d_ids + p0 * n * k,
+                         d_scores + p0 * n * k, d_counts + p0 * n, oi + (int64_t)q * n * k, os + (int64_t)q * n * k,
+                         oc + (int64_t)q * n);
+    }
+    CMS_HIP(hipGetLastError());
+    d_ids = oi;
+    d_scores = os;
+    d_counts = oc;
+    nparts = groups;
+    cur = (cur + 1) & 1;
+  }
+  hipLaunchKernelGGL(k_topk_merge, dim3(grid), dim3(kCandThreads), 0, h->stream, nparts, k, n, d_ids, d_scores,
+                     d_counts, d_out_ids, d_out_scores, d_out_counts);
   CMS_HIP(hipGetLastError());
+  if (cur >= 0) CMS_HIP(hipStreamSynchronize(h->stream));  // the round buffers free on return
   return CMS_OK;
 }
 

@@ -180,6 +180,34 @@ class SketchTable:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
         check(self._lib.cms_comm_init(self._h, buf, rank, world))
 
+    def comm_init_transport(self, rank, world, allreduce, allgather):
+        """cms_comm_init_transport: a caller-supplied communicator in place of
+        RCCL.  allreduce(d_ptr, count) sums `count` u64 words at device address
+        d_ptr over all ranks in place; allgather(d_send, d_recv, nbytes) writes
+        every rank's `nbytes` bytes at d_send, in rank order, to d_recv.  See
+        mahout_amd.transport for a torch.distributed implementation."""
+        def ar(ptr, count, _user):
+            try:
+                allreduce(int(ptr), int(count))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported as a status code
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def ag(send, recv, nbytes, _user):
+            try:
+                allgather(int(send), int(recv), int(nbytes))
+                return 0
+            except Exception:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+        # the C side keeps the function pointers: hold the thunks for the handle's life
+        self._transport = (_lib.ALLREDUCE_FN(ar), _lib.ALLGATHER_FN(ag))
+        check(self._lib.cms_comm_init_transport(self._h, int(rank), int(world), self._transport[0],
+                                                self._transport[1], None))
+
     def finalize(self):
         check(self._lib.cms_finalize(self._h))
 
@@ -329,6 +357,20 @@ class SketchTable:
             row_count = self.num_owners - row_begin
         out = np.zeros((row_count, self.depth, self.width), np.float64)
         check(self._lib.cms_read_counters(self._h, int(row_begin), int(row_count), _ptr(out)))
+        return out
+
+    def read_counters_device(self, row_begin=0, row_count=None, out=None):
+        """Counters as a u32 torch tensor [row_count][d][w] on the handle's
+        device, in counter units (cms_read_counters_device)."""
+        import torch
+        if row_count is None:
+            row_count = self.num_owners - row_begin
+        if out is None:
+            out = torch.empty((row_count, self.depth, self.width), dtype=torch.int32, device="cuda")
+        check(self._lib.cms_read_counters_device(self._h, int(row_begin), int(row_count), ctypes.c_void_p(out.data_ptr())))
+        s = torch.cuda.current_stream(out.device).cuda_stream
+        if s:  # later torch work on this stream waits for the copy
+            check(self._lib.cms_release_to_stream(self._h, ctypes.c_void_p(s)))
         return out
 
     # -- instrumentation --

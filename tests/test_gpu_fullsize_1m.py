@@ -1,0 +1,122 @@
+"""Configs 3 + 4 at full size on one GPU (BASELINE.json configs[2], configs[3]):
+a 500M-pair Zipf stream (10M users x 1M items) into the d=5, w=8192 table --
+163.8 GB as u32, 82 GB as this build's u16 narrow rows -- then the all-pairs
+top-100 of every one of the 1M items through cms_top_k_all.
+
+The oracle cannot hold a 1M x 40960 fp64 table, so the check is split the way
+the domain allows:
+  * checksum of checksums -- every update adds its increment once to each of
+    the d rows (`T/impl/common/DoubleCountMinSketch.java:72-80`), so each row
+    of every one of the 1M sketches sums to that owner's pair count (read on
+    the device, cms_read_counters_device, compared with an independent
+    torch.bincount of the stream);
+  * the 16 hottest owners (the 8192-key slice / u32 hot-row path) and 32
+    random ones rebuilt by the oracle from their own pairs, bit for bit;
+  * all-pairs top-100 (`TopItems.java:91-136`, `SimilarUser.java:62-78`):
+    ordering rules on every list and no overflow redo; for sampled rows whose
+    lists come from fp4 x fp4 blocks, int8 blocks and multi-limb owners, the
+    list equals the oracle's TopItems loop over that row's similarities to ALL
+    1M owners (computed by the exact pair kernel), and those similarities are
+    checked against the oracle's CosineCM on the read-back sketches for the
+    listed owners plus random partners.
+"""
+import numpy as np
+import pytest
+
+from mahout_amd import SketchTable
+from mahout_amd.synth import zipf_stream_torch
+
+pytestmark = pytest.mark.gpu
+
+N_USERS, N_ITEMS, N_PAIRS, D, W, SEED, K = 10_000_000, 1_000_000, 500_000_000, 5, 8192, 42, 100
+CHUNK = 16384  # owners per device read-back: 16384 x 40960 u32 = 2.7 GB
+
+
+def _same(a, b):
+    return bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+@pytest.mark.timeout(900)
+def test_config34_full_size(oracle):
+    import torch
+
+    items, users = zipf_stream_torch(N_USERS, N_ITEMS, N_PAIRS, seed=20261016, device="cuda")
+    counts_d = torch.bincount(items, minlength=N_ITEMS)
+    counts = counts_d.cpu().numpy()
+    assert int(counts.sum()) == N_PAIRS
+    t = SketchTable(N_ITEMS, depth=D, width=W, seed=SEED)
+    try:
+        t.ingest_device_rows(items, users, None, N_PAIRS)
+        t.finalize()
+        t.synchronize()
+
+        # 1. checksum of checksums over all 1M owners, and each owner's largest counter
+        rowmax = torch.empty(N_ITEMS, dtype=torch.int64, device="cuda")
+        buf = torch.empty((CHUNK, D, W), dtype=torch.int32, device="cuda")
+        for o in range(0, N_ITEMS, CHUNK):
+            c = min(CHUNK, N_ITEMS - o)
+            v = t.read_counters_device(o, c, buf[:c])
+            sums = v.sum(dim=2, dtype=torch.int64)
+            want = counts_d[o:o + c, None].expand(c, D)
+            assert torch.equal(sums, want), o
+            rowmax[o:o + c] = v.view(c, -1).amax(dim=1).to(torch.int64)
+        del buf, v, sums
+        rowmax = rowmax.cpu().numpy()
+
+        # 2. the hottest 16 and 32 random owners bit for bit against the oracle
+        rng = np.random.default_rng(2027)
+        hot = np.argsort(counts)[-16:]
+        sample = np.unique(np.concatenate([hot, rng.choice(np.flatnonzero(counts), 32, replace=False)]))
+        sel = torch.isin(items, torch.from_numpy(sample).cuda())
+        si = items[sel].cpu().numpy()
+        su = users[sel].cpu().numpy()
+        del sel
+        order = np.argsort(si, kind="stable")
+        si, su = si[order], su[order]
+        a, b = oracle.hash_params(SEED, D)
+        for owner in sample.tolist():
+            lo, hi = np.searchsorted(si, owner), np.searchsorted(si, owner, side="right")
+            assert hi - lo == counts[owner]
+            want = oracle.build_table(1, D, W, a, b, np.zeros(hi - lo, np.int64), su[lo:hi])
+            np.testing.assert_array_equal(t.read_counters(owner, 1), want, err_msg=str(owner))
+        del si, su, items, users, counts_d
+        torch.cuda.empty_cache()
+        t.release_scratch()
+
+        # 3. all-pairs top-100 of every owner
+        ids, sc, cnt = t.top_k_all(K)
+        st = t.stats()
+        assert st["topk_redo"] == 0
+        assert st["fp4_owners"] > 0 and st["multi_limb_owners"] > 0
+        assert (cnt == K).mean() > 0.99
+        valid = np.arange(K)[None, :] < cnt[:, None]
+        assert not np.isnan(sc[valid]).any()
+        pair = valid[:, 1:]
+        dsc = np.diff(sc, axis=1)
+        assert (dsc[pair] <= 0).all()
+        assert (np.diff(ids, axis=1)[pair & (dsc == 0)] > 0).all()  # ties by ID ascending
+        assert (ids != np.arange(N_ITEMS)[:, None])[valid].all()  # self never listed
+
+        # 4. sampled rows from every operand class against the oracle's TopItems loop
+        fp4 = np.flatnonzero((rowmax <= 4) & (counts > 0))
+        i8 = np.flatnonzero((rowmax > 4) & (rowmax < 128))
+        ml = np.flatnonzero(rowmax >= 128)
+        rows = np.concatenate([rng.choice(fp4, 2, replace=False), rng.choice(i8, 2, replace=False),
+                               rng.choice(ml, 2, replace=False)])
+        all_ids = np.arange(N_ITEMS, dtype=np.int64)
+        for row in rows.tolist():
+            sims = t.similarities(row, all_ids)  # exact pair kernel over all 1M owners
+            sims[row] = np.nan  # MostSimilarEstimator: the owner itself is NaN
+            eids, esc = oracle.top_users(all_ids, sims, K)
+            assert ids[row, :cnt[row]].tolist() == eids.tolist(), row
+            assert _same(sc[row, :cnt[row]], esc), row
+            sa = t.read_counters(row, 1)[0]
+            partners = np.concatenate([ids[row, :cnt[row]], rng.choice(N_ITEMS, 100, replace=False)])
+            for p in partners.tolist():
+                if p == row:
+                    continue
+                want = oracle.cosine_cm(sa, t.read_counters(p, 1)[0])
+                assert _same(np.array([sims[p]]), np.array([want])), (row, p)
+    finally:
+        t.close()
+        torch.cuda.empty_cache()

@@ -441,7 +441,8 @@ def test_bad_row_index_device_path():
 
 
 @pytest.mark.parametrize("n,d,w,vmax,seed", [(700, 5, 256, 5, 31), (260, 4, 128, 50, 32), (129, 3, 512, 1, 33), (3000, 5, 256, 1, 34),
-     (1500, 8, 128, 3, 35), (600, 25, 128, 2, 36)])
+     (1500, 8, 128, 3, 35), (600, 25, 128, 2, 36),
+     (3000, 5, 8192, 3, 37)])  # the config-3/4 shape: d=5, w=8192 (K = 40960), counters <= 4 and > 127
 def test_all_pairs_mfma_every_similarity(oracle, n, d, w, vmax, seed):
     """cms_top_k_rows with k = n-1 returns every other owner sorted by
     (similarity desc, ID asc): the whole similarity matrix through the
@@ -521,6 +522,7 @@ def test_top_k_heavy_ties(oracle):
     (11776, 3, 128, 2, 20, False, 55),    # 46 blocks: multi-wave bands and the half wave
     (12000, 4, 256, 2, 25, False, 56),    # fp4 blocks beside int8 blocks over multi-wave bands
     (5000, 2, 512, 1, 200, False, 57),    # mostly fp4 owners, long lists
+    (3000, 5, 8192, 3, 100, False, 58),   # the config-4 shape (d=5, w=8192): fp4, int8 and multi-limb owners
 ])
 def test_top_k_all_streaming_symmetric(oracle, n, d, w, vmax, k, weighted, seed):
     """cms_top_k_all (each unordered pair computed once, streamed into both
