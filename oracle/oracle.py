@@ -48,6 +48,16 @@ def _load():
                                            _i64p, _i64p, c.c_int64, _f64p]),
         "orc_build_rows_reuse": (c.c_int64, [_i64p, _i64p, c.c_void_p, c.c_int64, c.c_int64, c.c_int32, c.c_int32,
                                              _i64p, _i64p, c.POINTER(c.c_double)]),
+        "orc_ingest_faithful_par": (c.c_int64, [_i64p, _i64p, c.c_void_p, c.c_int64, c.c_int64, c.c_int32, c.c_int32,
+                                                _i64p, _i64p, c.c_int32, c.POINTER(c.c_double)]),
+        "orc_ingest_efficient_par": (c.c_int64, [_i64p, _i64p, c.c_void_p, c.c_int64, c.c_int64, c.c_int32,
+                                                 c.c_int32, _i64p, _i64p, c.c_int32, c.c_void_p,
+                                                 c.POINTER(c.c_double)]),
+        "orc_faithful_pairs_par": (c.c_int64, [_i64p, _i64p, c.c_void_p, c.c_int64, c.c_int32, c.c_int32, _i64p,
+                                               _i64p, _i64p, _i64p, c.c_int64, c.c_int32, c.POINTER(c.c_double)]),
+        "orc_allpairs_efficient_par": (c.c_int64, [_f64p, c.c_int64, c.c_int32, c.c_int32, c.c_int64, c.c_int64,
+                                                   c.c_int32, c.POINTER(c.c_double)]),
+        "orc_max_threads": (c.c_int32, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -233,3 +243,47 @@ def per_owner_similarity(offsets, keys, vals, shapes, a, b, u1, u2, weighted=Fal
     s1 = export_profile(offsets, keys, vals, u1, w, d, a, b)
     s2 = export_profile(offsets, keys, vals, u2, w, d, a, b)
     return cosine_cm(s1, s2, weighted)
+
+
+# ---- CPU baselines (oracle/cms_baseline.c; bench.py's cpu_baseline legs) ----
+
+def max_threads():
+    return lib().orc_max_threads()
+
+
+def ingest_faithful(offsets, keys, vals, lo, hi, depth, width, a, b, threads):
+    v = None if vals is None else np.ascontiguousarray(vals, np.float32)
+    cs = ctypes.c_double()
+    n = lib().orc_ingest_faithful_par(np.ascontiguousarray(offsets, np.int64), np.ascontiguousarray(keys, np.int64),
+                                      _vp(v), lo, hi, depth, width, np.ascontiguousarray(a, np.int64),
+                                      np.ascontiguousarray(b, np.int64), threads, ctypes.byref(cs))
+    return n, cs.value
+
+
+def ingest_efficient(offsets, keys, vals, lo, hi, depth, width, a, b, threads, table=None):
+    v = None if vals is None else np.ascontiguousarray(vals, np.float32)
+    if table is None:
+        table = np.empty((hi - lo) * depth * width, np.uint32)
+    cs = ctypes.c_double()
+    n = lib().orc_ingest_efficient_par(np.ascontiguousarray(offsets, np.int64), np.ascontiguousarray(keys, np.int64),
+                                       _vp(v), lo, hi, depth, width, np.ascontiguousarray(a, np.int64),
+                                       np.ascontiguousarray(b, np.int64), threads, _vp(table), ctypes.byref(cs))
+    return n, cs.value, table
+
+
+def faithful_pairs_par(offsets, keys, vals, rows, depth, width, a, b, pi, pj, threads):
+    v = None if vals is None else np.ascontiguousarray(vals, np.float32)
+    cs = ctypes.c_double()
+    n = lib().orc_faithful_pairs_par(np.ascontiguousarray(offsets, np.int64), np.ascontiguousarray(keys, np.int64),
+                                     _vp(v), rows, depth, width, np.ascontiguousarray(a, np.int64),
+                                     np.ascontiguousarray(b, np.int64), np.ascontiguousarray(pi, np.int64),
+                                     np.ascontiguousarray(pj, np.int64), len(pi), threads, ctypes.byref(cs))
+    return n, cs.value
+
+
+def allpairs_efficient(table, i_lo, i_hi, threads):
+    t = np.ascontiguousarray(table, np.float64)
+    rows, d, w = t.shape
+    cs = ctypes.c_double()
+    n = lib().orc_allpairs_efficient_par(t.reshape(-1), rows, d, w, i_lo, i_hi, threads, ctypes.byref(cs))
+    return n, cs.value
