@@ -105,11 +105,23 @@ __global__ __launch_bounds__(256) void k_limb_write(TableView tv, int64_t dw, co
 
 // fp4 (e2m1) image of positions [f0, n): two counters per byte, low nibble
 // first.  Every counter is <= kF4Max, and 0..4 are exact e2m1 codes.
+//
+// K-blocked layout: the image is cut into blocks of kImgBlk rows, and inside a
+// block every 128-byte K slice of its rows is one contiguous 16 KiB run
+// ([slice][row][128 B]); a stage of a 128-row operand block is then one
+// contiguous run instead of 128 lines a row stride apart (DRAM page
+// locality for the symmetric waves' fills).  Rows past the end of the image
+// (the last block's padding) are zero.
+constexpr int kImgBlk = 128;
+__device__ __forceinline__ int64_t blk_off(int64_t row, int64_t kb, int64_t rs) {
+  return (row / kImgBlk) * (kImgBlk * rs) + (kb >> 7) * (kImgBlk * 128) + (row % kImgBlk) * 128 + (kb & 127);
+}
+
 __global__ __launch_bounds__(256) void k_f4_write(TableView tv, int64_t dw, const int64_t* perm, int64_t f0,
                                                   uint8_t* f4) {
   const int64_t p = f0 + blockIdx.x;
   const int64_t row = perm[p];
-  uint8_t* dst = f4 + (int64_t)blockIdx.x * (dw / 2);
+  const int64_t rs = dw / 2;
   // e2m1: 0 -> 0x0, 1 -> 0x2 (1.0), 2 -> 0x4 (2.0), 3 -> 0x5 (3.0), 4 -> 0x6 (4.0)
   constexpr uint32_t kCode = 0x65420u;  // nibble c = code of value c
   for (int64_t j = threadIdx.x * 8; j < dw; j += 256 * 8) {
@@ -118,7 +130,7 @@ __global__ __launch_bounds__(256) void k_f4_write(TableView tv, int64_t dw, cons
     auto code = [&](uint32_t c) { return (kCode >> (4 * c)) & 15u; };
     const uint32_t packed = code(v0.x) | code(v0.y) << 4 | code(v0.z) << 8 | code(v0.w) << 12 | code(v1.x) << 16 |
                             code(v1.y) << 20 | code(v1.z) << 24 | code(v1.w) << 28;
-    *reinterpret_cast<uint32_t*>(dst + j / 2) = packed;
+    *reinterpret_cast<uint32_t*>(f4 + blk_off(blockIdx.x, j / 2, rs)) = packed;
   }
 }
 
@@ -655,13 +667,19 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
     }
   }
 
-  // buffer descriptors bound the panel: rows past the end land as zeros
+  // buffer descriptors bound the panel: rows past the end land as zeros.
+  // fp4 operands use the K-blocked image (k_f4_write; sym panels start on a
+  // block): a panel's rows past the end inside its last block are the
+  // image's zero padding, the rows beyond that block fall outside the bound.
+  constexpr bool BLK = FMT == 1;
   const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, a_vrows - vrow0));
   const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, b_rows - bcol0));
+  const int64_t recA = BLK ? (rowsA + kImgBlk - 1) / kImgBlk * kImgBlk * rs : rowsA * rs;
+  const int64_t recB = BLK ? (rowsB + kImgBlk - 1) / kImgBlk * kImgBlk * rs : rowsB * rs;
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(gA + vrow0 * rs), (short)0, (int)(rowsA * rs), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(gA + vrow0 * rs), (short)0, (int)recA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(gB + bcol0 * rs), (short)0, (int)(rowsB * rs), 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(gB + bcol0 * rs), (short)0, (int)recB, 0x00020000);
   // Instruction u of wave wid fills LDS rows [(wid + 8u) * RPI, +RPI); lane
   // i lands at byte 16 i, i.e. row (wid + 8u) * RPI + i / (BK/16), slot
   // i % (BK/16), and fetches the chunk the swizzle puts there.  The 8*RPI-row
@@ -670,24 +688,29 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   constexpr int CPR = BK / 16;  // 16-B chunks per row
   const int srow = wid * RPI + lane / CPR;
   const int slot = lane % CPR;
-  const int32_t vo = (int32_t)(srow * rs) +
-                     ((BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4);
+  const int32_t chunk = (BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4;
+  // row-major image: row r at r * rs; K-blocked image (BLK, BK == 128): row r
+  // at (r / 128) * 128 * rs + (r % 128) * 128, K slice s at s * 16 KiB
+  const int32_t vo = BLK ? (int32_t)(srow * 128) + chunk : (int32_t)(srow * rs) + chunk;
   const int32_t rstep = 8 * RPI * (int32_t)rs;
+  const int32_t bstep = kImgBlk * (int32_t)rs;
+#define UOFF(u) (BLK ? vo + ((u) & 1) * (64 * 128) + ((u) >> 1) * bstep : vo + (u) * rstep)
   auto issue = [&](int s) {
     if (kMode & 1) return;
     const int r = s / cstages, cs = s - r * cstages;
-    const int32_t koff = r * kw + cs * BK;
+    const int32_t koff = BLK ? s * (kImgBlk * 128) : r * kw + cs * BK;
     unsigned char* st = lds + (s % NSTAGE) * kStage;
 #pragma unroll
     for (int u = 0; u < OPA; ++u)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + 8 * u) * 1024),
-                                               16, vo + u * rstep, koff, 0, 0);
+                                               16, UOFF(u), koff, 0, 0);
 #pragma unroll
     for (int u = 0; u < OPB; ++u)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + 8 * u) * 1024), 16, vo + u * rstep,
+          rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + 8 * u) * 1024), 16, UOFF(u),
           koff, 0, 0);
   };
+#undef UOFF
 
   AccT acc[2][2];
   double mn[2][2][4 * OG];
@@ -965,7 +988,11 @@ int cosine_prepare(cms_handle* h) {
     hipLaunchKernelGGL(k_perm_norms, dim3(grid), dim3(256), 0, h->stream, h->d_norm_sqrt, perm, n, h->p.depth,
                        h->ws_nsq.as<double>());
     if (n > f0) {
-      CMS_HIP(h->ws_f4.ensure((size_t)(n - f0) * (size_t)(dw / 2)));
+      // whole kImgBlk-row blocks; the last block's padding rows are zero
+      const int64_t blocks = (n - f0 + kImgBlk - 1) / kImgBlk;
+      CMS_HIP(h->ws_f4.ensure((size_t)blocks * kImgBlk * (size_t)(dw / 2)));
+      CMS_HIP(hipMemsetAsync(h->ws_f4.as<uint8_t>() + (size_t)(blocks - 1) * kImgBlk * (dw / 2), 0,
+                             (size_t)kImgBlk * (dw / 2), h->stream));
       hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), 0, h->stream, h->tview(), dw, perm, f0,
                          h->ws_f4.as<uint8_t>());
     }

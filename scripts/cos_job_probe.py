@@ -1,0 +1,51 @@
+"""Config 4 job alone for profiling: the 1M-item d=5 w=8192 table from the
+500M-pair config-3 stream, then ONE cms_top_k_all(100) (no spot checks, so
+every k_cosine_big dispatch after the warm-up belongs to the job)."""
+import json
+import sys
+import time
+
+sys.path.insert(0, ".")
+import torch  # noqa: E402
+from mahout_amd import SketchTable  # noqa: E402
+from mahout_amd.synth import zipf_stream_torch  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+pairs = int(sys.argv[2]) if len(sys.argv) > 2 else 500_000_000
+w = int(sys.argv[3]) if len(sys.argv) > 3 else 8192
+k = int(sys.argv[4]) if len(sys.argv) > 4 else 100
+d = 5
+# the bench's config-3 stream (bench.config3_shard at one rank): chunks of 2^26 pairs
+chunks, done, it = [], 0, 0
+while done < pairs:
+    m = min(1 << 26, pairs - done)
+    chunks.append(zipf_stream_torch(1_000_000 if n <= 100_000 else 10_000_000, n, m, seed=20261016 + 7919 * it,
+                                    device="cuda"))
+    done += m
+    it += 1
+items = torch.cat([c[0] for c in chunks])
+users = torch.cat([c[1] for c in chunks])
+del chunks
+t = SketchTable(n, depth=d, width=w, seed=42, device=0)
+t.ingest_device_rows(items, users, None, pairs)
+t.finalize()
+del items, users
+torch.cuda.empty_cache()
+t.release_scratch()
+t0 = time.perf_counter()
+t.top_k_all(k)  # first call: the limb / fp4 operand images are prepared
+wall_first = time.perf_counter() - t0
+reps = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+walls = []
+for _ in range(reps):  # untimed kernels: the job's wall clock
+    t0 = time.perf_counter()
+    t.top_k_all(k)
+    walls.append(time.perf_counter() - t0)
+t.set_timing(True)
+t0 = time.perf_counter()
+ids, sc, cnt = t.top_k_all(k)
+wall = time.perf_counter() - t0
+tm = {name: t.timing(name) for name in ["topk_all_multi_rows", "topk_all_waves", "topk_all_waves_i8",
+                                        "topk_all_waves_f4", "cand_compact"]}
+print(json.dumps({"n": n, "w": w, "k": k, "wall_first_s": wall_first, "walls_untimed_s": walls, "wall_timed_s": wall, "timing_ms": tm, "full_lists": int((cnt == k).sum()),
+                  "stats": t.stats()}), flush=True)
