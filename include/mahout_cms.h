@@ -56,6 +56,13 @@ extern "C" {
 
 /* ---- parameters ----------------------------------------------------------- */
 #define CMS_COUNTER_U32 0 /* exact integer counters (non-negative integer increments) */
+#define CMS_COUNTER_F64 1 /* fp64 counters: DoubleCountMinSketch's own type, any float preference
+                             (negative, non-dyadic); increments are applied per owner in ingest
+                             order (the DataModel order CosineCM.exportProfile uses) and every sum
+                             is the reference's sequential fp64 chain.  Single-GPU; fixed shapes
+                             up to width 16384, and per-owner shapes (cms_create_per_owner);
+                             owners are built by CSR ingest or host COO ingest (stable by
+                             owner), not by cms_ingest_device_rows. */
 
 #define CMS_UNWEIGHTED 0 /* org.apache.mahout.cf.taste.common.Weighting */
 #define CMS_WEIGHTED 1

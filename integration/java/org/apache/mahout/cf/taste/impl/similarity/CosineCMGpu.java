@@ -143,7 +143,7 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
         vals[base + j] = prefs.getValue(j);
       }
     }
-    int fracBits = fracBits(vals);
+    int fracBits = counterUnits(offsets, vals);
     long h = perOwner() ? nativeCreatePerOwner(seed, n, weighted, device, fracBits)
                         : nativeCreate(depth, width, seed, n, weighted, device, fracBits);
     try {
@@ -173,6 +173,39 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   }
 
   /**
+   * Counter representation for this DataModel.  Returns the smallest s with
+   * every preference * 2^s an integer (1 for half-star ratings) when exact u32
+   * counters in units of 2^-s can hold every owner's total (mass * 2^s < 2^32):
+   * every similarity is then bit-identical and fast.  Otherwise -- negative,
+   * non-finite or non-dyadic preferences, or masses past 2^32 units -- returns
+   * -1: DoubleCountMinSketch's own fp64 counters (CMS_COUNTER_F64), which add
+   * the preferences in DataModel order exactly as the reference does.
+   */
+  static int counterUnits(long[] offsets, float[] vals) {
+    int s;
+    try {
+      s = fracBits(vals);
+    } catch (TasteException e) {
+      return -1;
+    }
+    for (float v : vals) {
+      if (v < 0.0f || Float.isNaN(v) || Float.isInfinite(v)) {
+        return -1;
+      }
+    }
+    for (int r = 0; r + 1 < offsets.length; r++) {
+      double mass = 0.0;
+      for (long i = offsets[r]; i < offsets[r + 1]; i++) {
+        mass += Math.scalb((double) vals[(int) i], s);
+      }
+      if (mass >= 4294967296.0) {
+        return -1;
+      }
+    }
+    return s;
+  }
+
+  /**
    * Smallest s with every preference * 2^s an integer (1 for half-star
    * ratings): the library keeps counters in units of 2^-s, which leaves every
    * similarity bit-identical and point queries in preference units.
@@ -181,7 +214,7 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     int s = 0;
     for (float v : vals) {
       if (v == 0.0f || Float.isNaN(v) || Float.isInfinite(v)) {
-        continue;  // non-finite values are refused by the library (CMS_E_VALUE)
+        continue;  // counterUnits() sends non-finite values to the fp64 counters
       }
       int bits = Float.floatToIntBits(Math.abs(v));
       int exp = ((bits >>> 23) & 0xff) - 150;  // v = mant * 2^exp with a 24-bit mant

@@ -12,8 +12,10 @@
  * CMS_E_PARAM / CMS_E_SHAPE -> IllegalArgumentException
  * (AbstractCountMinSketch CMException / DoubleCountMinSketch checkArgument),
  * anything else -> TasteException.  NaN similarities are values, not errors.
- * Java arrays are pinned only for the duration of the copy into the library
- * (GetPrimitiveArrayCritical); the library never retains host pointers.
+ * The DataModel arrays are copied out with Get*ArrayRegion before the library
+ * call (no critical region spans GPU work); small query arrays are pinned
+ * only around a host-side copy.  The library never retains host pointers.
+ * frac_bits < 0 from the Java side selects fp64 counters (CMS_COUNTER_F64).
  */
 #include <jni.h>
 #include <stdint.h>
@@ -22,6 +24,11 @@
 #include "mahout_cms.h"
 
 #define CLS "org/apache/mahout/cf/taste/"
+
+static void throw_named(JNIEnv* env, const char* cls, const char* msg) {
+  jclass ex = (*env)->FindClass(env, cls);
+  if (ex) (*env)->ThrowNew(env, ex, msg);
+}
 
 static int fail(JNIEnv* env, int rc, int item_ids) {
   if (rc == CMS_OK) return 0;
@@ -47,7 +54,10 @@ JNIEXPORT jlong JNICALL JFN(nativeCreate)(JNIEnv* env, jclass c, jint depth, jin
   p.num_owners = n;
   p.weighting = weighted ? CMS_WEIGHTED : CMS_UNWEIGHTED;
   p.device = device;
-  p.frac_bits = frac_bits;
+  /* frac_bits < 0: the preferences need DoubleCountMinSketch's fp64 counters
+     (negative, non-dyadic, or masses a u32 counter cannot hold) */
+  p.counter_type = frac_bits < 0 ? CMS_COUNTER_F64 : CMS_COUNTER_U32;
+  p.frac_bits = frac_bits < 0 ? 0 : frac_bits;
   cms_handle* h = NULL;
   if (fail(env, cms_create(&p, &h), 0)) return 0;
   return (jlong)(intptr_t)h;
@@ -62,7 +72,8 @@ JNIEXPORT jlong JNICALL JFN(nativeCreatePerOwner)(JNIEnv* env, jclass c, jlong s
   p.num_owners = n;
   p.weighting = weighted ? CMS_WEIGHTED : CMS_UNWEIGHTED;
   p.device = device;
-  p.frac_bits = frac_bits;
+  p.counter_type = frac_bits < 0 ? CMS_COUNTER_F64 : CMS_COUNTER_U32;
+  p.frac_bits = frac_bits < 0 ? 0 : frac_bits;
   cms_handle* h = NULL;
   if (fail(env, cms_create_per_owner(&p, &h), 0)) return 0;
   return (jlong)(intptr_t)h;
@@ -93,17 +104,49 @@ JNIEXPORT void JNICALL JFN(nativeSetOwnerIds)(JNIEnv* env, jclass c, jlong h, jl
   fail(env, rc, 0);
 }
 
+/* The arrays are copied out with Get*ArrayRegion before the library call (which
+   takes the handle's mutex and runs kernels): no critical region, and so no GC
+   stall, spans GPU work.  offsets must hold num_owners + 1 entries and
+   offsets[num_owners] must not run past the keys (or the values). */
 JNIEXPORT void JNICALL JFN(nativeIngestCsr)(JNIEnv* env, jclass c, jlong h, jlongArray off, jlongArray keys,
                                             jfloatArray vals) {
   (void)c;
-  jlong* po = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
-  jlong* pk = (*env)->GetPrimitiveArrayCritical(env, keys, NULL);
-  jfloat* pv = vals ? (*env)->GetPrimitiveArrayCritical(env, vals, NULL) : NULL;
-  int rc = cms_ingest_csr(H(h), (const int64_t*)po, (const int64_t*)pk, (const float*)pv);
-  if (pv) (*env)->ReleasePrimitiveArrayCritical(env, vals, pv, JNI_ABORT);
-  (*env)->ReleasePrimitiveArrayCritical(env, keys, pk, JNI_ABORT);
-  (*env)->ReleasePrimitiveArrayCritical(env, off, po, JNI_ABORT);
-  fail(env, rc, 0);
+  if (!off || !keys) {
+    throw_named(env, "java/lang/IllegalArgumentException", "null offsets or keys");
+    return;
+  }
+  cms_stats st;
+  if (fail(env, cms_get_stats(H(h), &st), 0)) return;
+  const jsize no = (*env)->GetArrayLength(env, off);
+  const jsize nk = (*env)->GetArrayLength(env, keys);
+  if ((int64_t)no != st.num_owners + 1) {
+    throw_named(env, "java/lang/IllegalArgumentException", "offsets must hold num_owners + 1 entries");
+    return;
+  }
+  int64_t* po = (int64_t*)malloc(sizeof(int64_t) * (size_t)no);
+  int64_t* pk = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nk ? nk : 1));
+  float* pv = vals ? (float*)malloc(sizeof(float) * (size_t)(nk ? nk : 1)) : NULL;
+  if (!po || !pk || (vals && !pv)) {
+    free(po);
+    free(pk);
+    free(pv);
+    throw_named(env, "java/lang/OutOfMemoryError", "host staging for the DataModel");
+    return;
+  }
+  (*env)->GetLongArrayRegion(env, off, 0, no, (jlong*)po);
+  (*env)->GetLongArrayRegion(env, keys, 0, nk, (jlong*)pk);
+  const char* bad = NULL;
+  if (po[no - 1] > (int64_t)nk) bad = "offsets[num_owners] runs past the keys";
+  if (vals && !bad) {
+    if ((*env)->GetArrayLength(env, vals) < nk) bad = "fewer values than keys";
+    else (*env)->GetFloatArrayRegion(env, vals, 0, nk, pv);
+  }
+  int rc = bad ? CMS_OK : cms_ingest_csr(H(h), po, pk, pv);
+  free(po);
+  free(pk);
+  free(pv);
+  if (bad) throw_named(env, "java/lang/IllegalArgumentException", bad);
+  else fail(env, rc, 0);
 }
 
 JNIEXPORT void JNICALL JFN(nativeFinalize)(JNIEnv* env, jclass c, jlong h) {

@@ -24,6 +24,7 @@ CMS_E_OOM = 9
 CMS_E_SKETCH = 10
 
 CMS_COUNTER_U32 = 0
+CMS_COUNTER_F64 = 1
 CMS_FORMAT_ITEM_SIMILARITY_JOB = 1
 CMS_FORMAT_SPARK_ITEMSIMILARITY = 2
 CMS_UNWEIGHTED = 0

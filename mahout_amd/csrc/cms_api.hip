@@ -247,12 +247,17 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   }
   if (p->num_owners < 1 || p->num_owners > (int64_t(1) << 24))
     return set_error(CMS_E_PARAM, "num_owners must be in [1, 2^24]");
-  if (p->counter_type != CMS_COUNTER_U32) return set_error(CMS_E_PARAM, "unsupported counter type");
+  if (p->counter_type != CMS_COUNTER_U32 && p->counter_type != CMS_COUNTER_F64)
+    return set_error(CMS_E_PARAM, "unsupported counter type");
+  const bool f64 = p->counter_type == CMS_COUNTER_F64;
+  if (f64 && !per_owner && p->width > 16384) return set_error(CMS_E_PARAM, "fp64 counters: width must be <= 16384 (LDS sketch row)");
   if (p->frac_bits < 0 || p->frac_bits > 31) return set_error(CMS_E_PARAM, "frac_bits must be in [0, 31]");
   cms_handle* h = new (std::nothrow) cms_handle();
   if (!h) return set_error(CMS_E_OOM, "host allocation failed");
   h->p = *p;
   h->per_owner = per_owner;
+  h->f64 = f64;
+  if (f64) h->p.frac_bits = 0;  // raw (double) float preferences
   if (per_owner) {  // every owner may use up to CMS_MAX_DEPTH rows; no shared table
     h->p.depth = CMS_MAX_DEPTH;
     h->p.width = 1;
@@ -286,7 +291,8 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
 
   size_t tbytes = sizeof(uint16_t) * (size_t)h->n * (size_t)h->dw;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
-      (!per_owner && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
+      (!per_owner && !f64 && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
+      (f64 && (e = hipMalloc(&h->d_t64, 4 * tbytes)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||
       (!per_owner && (e = hipMemset(h->d_hidx, 0xff, sizeof(int32_t) * h->n)) != hipSuccess) ||
       (e = hipMalloc(&h->d_row_mass, sizeof(uint64_t) * h->n)) != hipSuccess ||
@@ -322,7 +328,7 @@ void cms_destroy(cms_handle* h) {
   for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
   if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  void* bufs[] = {h->d_t16, h->d_hidx, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
+  void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -459,6 +465,7 @@ int cms_ingest(cms_handle* h, const int64_t* owner, const int64_t* key, const fl
   if (int rc0 = refuse_per_owner(h, "COO ingest (per-owner mode takes the DataModel as CSR)")) return rc0;
   if (n <= 0) return CMS_OK;
   Guard g(h);
+  if (h->f64) return f64_ingest_coo_host(h, owner, key, val, n);
   CMS_HIP(h->ws_in_row.ensure(sizeof(int64_t) * n));
   CMS_HIP(h->ws_in_key.ensure(sizeof(int64_t) * n));
   if (val) CMS_HIP(h->ws_in_val.ensure(sizeof(float) * n));
@@ -493,6 +500,9 @@ int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d
   if (int rc0 = refuse_per_owner(h, "COO ingest (per-owner mode takes the DataModel as CSR)")) return rc0;
   if (n <= 0) return CMS_OK;
   Guard g(h);
+  if (h->f64)
+    return set_error(CMS_E_STATE, "fp64 counters take the owners' order from CSR or host COO ingest, not from an "
+                                  "unordered device stream");
   int rc = ingest_coo_device(h, d_row, d_key, d_val, n);
   if (rc == CMS_OK) rc = dlog_append(h, d_row, d_key, d_val, n);
   if (rc == CMS_OK) {
@@ -536,6 +546,15 @@ int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, c
     h->pairs_ingested = np;
     return CMS_OK;
   }
+  if (h->f64) {  // any float preference; the CSR order is the update order
+    if ((rc = f64_ingest_csr(h, h->ws_in_row.as<int64_t>(), h->ws_in_key.as<int64_t>(),
+                             vals ? h->ws_in_val.as<float>() : nullptr)))
+      return rc;
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    h->finalized = false;
+    h->pairs_ingested += np;
+    return CMS_OK;
+  }
   if (vals && (rc = validate_batch(h, nullptr, h->ws_in_val.as<float>(), np))) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
   if ((rc = check_flags(h, false))) return rc;
@@ -575,7 +594,7 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
     h->pairs_ingested = np;
     return CMS_OK;
   }
-  int rc = ingest_csr_device(h, d_offsets, d_keys, d_vals, np);
+  int rc = h->f64 ? f64_ingest_csr(h, d_offsets, d_keys, d_vals) : ingest_csr_device(h, d_offsets, d_keys, d_vals, np);
   if (rc == CMS_OK) {
     h->pairs_ingested += np;
     h->finalized = false;
@@ -624,6 +643,8 @@ int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t wo
   if (!h || !unique_id) return set_error(CMS_E_PARAM, "null argument");
   if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
   if (int rc0 = refuse_per_owner(h, "cms_comm_init")) return rc0;
+  if (h->f64 && world > 1)
+    return set_error(CMS_E_STATE, "fp64 counters are single-GPU: shard sums would not round in the reference's order");
   Guard g(h);
   if (h->comm) {
     (void)ncclCommDestroy(h->comm);
@@ -646,6 +667,8 @@ int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allr
   if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
   if (world > 1 && (!allreduce || !allgather)) return set_error(CMS_E_PARAM, "null transport function");
   if (int rc0 = refuse_per_owner(h, "cms_comm_init_transport")) return rc0;
+  if (h->f64 && world > 1)
+    return set_error(CMS_E_STATE, "fp64 counters are single-GPU: shard sums would not round in the reference's order");
   Guard g(h);
   if (h->comm) {
     (void)ncclCommDestroy(h->comm);
@@ -676,6 +699,19 @@ int cms_finalize(cms_handle* h) {
   if (h->per_owner) {
     int rc = po_finalize(h);
     if (rc) return rc;
+    if ((rc = check_flags(h, false))) return rc;
+    h->finalized = true;
+    return CMS_OK;
+  }
+  if (h->f64) {
+    if (h->empty) {
+      CMS_HIP(hipMemsetAsync(h->d_t64, 0, sizeof(double) * h->n * h->dw, h->stream));
+      h->empty = false;
+      h->norms_valid = false;
+    }
+    int rc = h->norms_valid ? CMS_OK : f64_norms(h);
+    if (rc) return rc;
+    CMS_HIP(hipStreamSynchronize(h->stream));
     if ((rc = check_flags(h, false))) return rc;
     h->finalized = true;
     return CMS_OK;
@@ -716,6 +752,7 @@ int cms_finalize(cms_handle* h) {
 int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   if (!h || !fn) return set_error(CMS_E_PARAM, "null argument");
   if (int rc0 = refuse_per_owner(h, "cms_finalize_with")) return rc0;
+  if (h->f64) return set_error(CMS_E_STATE, "fp64 counters are single-GPU: use cms_finalize");
   Guard g(h);
   if (h->comm || h->ext_comm) return set_error(CMS_E_STATE, "handle has a communicator: use cms_finalize");
   if (h->ext_merged) return set_error(CMS_E_STATE, "already merged: cms_reset starts a new epoch");
@@ -1051,6 +1088,10 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
     std::fill(out, out + cnt, 0.0);
     return CMS_OK;
   }
+  if (h->f64) {
+    if (cnt) CMS_HIP(hipMemcpy(out, h->d_t64 + row_begin * h->dw, sizeof(double) * cnt, hipMemcpyDeviceToHost));
+    return CMS_OK;
+  }
   // narrow rows straight from the u16 table, hot rows from their slots
   std::vector<uint16_t> t16(cnt);
   std::vector<int32_t> hidx(std::max<int64_t>(row_count, 1));
@@ -1076,6 +1117,7 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
 int cms_read_counters_device(cms_handle* h, int64_t row_begin, int64_t row_count, uint32_t* d_out) {
   if (!h || (row_count > 0 && !d_out)) return set_error(CMS_E_PARAM, "null argument");
   if (int rc0 = refuse_per_owner(h, "cms_read_counters_device")) return rc0;
+  if (h->f64) return set_error(CMS_E_STATE, "fp64 counters: use cms_read_counters");
   Guard g(h);
   if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
   return read_counters_device(h, row_begin, row_count, d_out);
@@ -1097,6 +1139,10 @@ int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capaci
   if (capacity < w * d) return set_error(CMS_E_PARAM, "capacity %lld < %lld counters", (long long)capacity, (long long)(w * d));
   int64_t soff = 0;
   for (int64_t r = 0; r < row; ++r) soff += (int64_t)h->h_po_w[r] * h->h_po_d[r];
+  if (h->f64) {
+    CMS_HIP(hipMemcpy(out, h->po_sk.as<double>() + soff, sizeof(double) * w * d, hipMemcpyDeviceToHost));
+    return CMS_OK;
+  }
   std::vector<uint32_t> tmp(w * d);
   CMS_HIP(hipMemcpy(tmp.data(), h->po_sk.as<uint32_t>() + soff, sizeof(uint32_t) * w * d, hipMemcpyDeviceToHost));
   for (int64_t i = 0; i < w * d; ++i) out[i] = std::ldexp((double)tmp[i], -h->p.frac_bits);
@@ -1114,12 +1160,13 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->world = h->world;
   out->rank = h->rank;
   int64_t hot_rows = 0;
-  if (!h->per_owner && h->d_hidx) {
+  if (!h->per_owner && !h->f64 && h->d_hidx) {
     int rc = count_hot_rows(h, &hot_rows);
     if (rc) return rc;
   }
   out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
-                                   : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
+                    : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
+                                  : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;

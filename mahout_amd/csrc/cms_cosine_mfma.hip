@@ -1030,7 +1030,7 @@ int cosine_prepare(cms_handle* h) {
 
 const int64_t* cosine_perm_device(cms_handle* h) { return h->ws_limbmeta.as<int64_t>(); }
 
-bool mfma_eligible(cms_handle* h) { return (h->p.width % kBK) == 0; }
+bool mfma_eligible(cms_handle* h) { return !h->f64 && (h->p.width % kBK) == 0; }
 
 // Similarities of the owners at PERMUTED positions [q0, q0+qc) against every
 // owner into slab [qc][n] (fp64, column = permuted position; owner row =
@@ -1292,6 +1292,14 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   if (h->per_owner) {  // asymmetric similarities: every row scans every candidate
     if (nshards != 1) return set_error(CMS_E_STATE, "per-owner shapes: all-pairs top-k is single-GPU");
     return top_k_rows(h, 0, h->n, k, d_ids, d_scores, d_counts);
+  }
+  if (h->f64) {  // fp64 counters: the exact sequential kernels, one slab of query rows at a time
+    if (nshards == 1) return top_k_rows(h, 0, h->n, k, d_ids, d_scores, d_counts);
+    CMS_HIP(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * h->n, h->stream));
+    for (int64_t r0 = shard; r0 < h->n; r0 += nshards) {
+      if (int rc = top_k_rows(h, r0, 1, k, d_ids + r0 * k, d_scores + r0 * k, d_counts + r0)) return rc;
+    }
+    return CMS_OK;
   }
   int rc = cosine_prepare(h);
   if (rc) return rc;

@@ -111,6 +111,8 @@ struct cms_handle {
   int64_t n = 0;       // rows
   int64_t dw = 0;      // d*w counters per row
   uint16_t* d_t16 = nullptr;        // [n][d][w] narrow counters
+  bool f64 = false;                 // CMS_COUNTER_F64: fp64 counters in d_t64 (cms_f64.hip), no u16/u32 table
+  double* d_t64 = nullptr;          // [n][d][w] fp64 counters
   int32_t* d_hidx = nullptr;        // [n] hot slot or -1
   cms::DevBuf hot_tab;              // [hot_cap][d][w] u32 counters of the hot rows
   cms::DevBuf ws_bound, ws_force, ws_plist;  // promotion scratch: u64 [n], u8 [n], i32 [n] + count
@@ -190,6 +192,7 @@ struct cms_handle {
   std::vector<double> h_po_delta, h_po_eps;      // CountMinSketchConfig.getDelta/getEpsilon
   std::vector<int32_t> h_po_w, h_po_d;           // AbstractCountMinSketch(delta, epsilon) shape; 0 = CMException
   cms::DevBuf po_off, po_kp, po_inc;             // CSR offsets, keys mod p, u32 increments
+  cms::DevBuf po_v64;                            // fp64 counters: (double) preferences in CSR order
   cms::DevBuf po_shape;                          // PoShape [n]
   cms::DevBuf po_sk, po_norm, po_nsq;            // own sketches [sum d*w] u32; norms [sum d] u64 / f64 sqrt
   cms::DevBuf po_scratch;                        // per-block bucket rows for widths beyond LDS
@@ -332,6 +335,25 @@ struct TopQuery {
 int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k, const int64_t* d_perm,
                  int64_t* d_ids, double* d_scores, int32_t* d_counts);
 int64_t slab_rows_for(int64_t n);
+// ---- cms_f64.hip (CMS_COUNTER_F64) ----
+int f64_ingest_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val);
+int f64_ingest_coo_host(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t np);
+// per-owner shapes on fp64 counters
+int po_f64_load(cms_handle* h, const int64_t* d_key, const float* d_val, int64_t npairs);
+int po_f64_finalize(cms_handle* h, int64_t total_counters, int64_t total_rows);
+int po_f64_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m,
+                        double* d_out);
+int po_f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int po_f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims,
+                                int64_t m, const int64_t* d_items, int64_t q, int use_capper, float lo, float hi,
+                                float* d_out);
+int f64_norms(cms_handle* h);
+int f64_pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);
+int f64_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_slab);
+int f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims,
+                             int64_t m, const int64_t* d_items, int64_t q, int use_capper, float lo, float hi,
+                             float* d_out);
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);

@@ -323,6 +323,14 @@ int po_load_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const
   CMS_HIP(h->po_kp.ensure(sizeof(uint64_t) * std::max<int64_t>(npairs, 1)));
   CMS_HIP(h->po_inc.ensure(sizeof(uint32_t) * std::max<int64_t>(npairs, 1)));
   CMS_HIP(hipMemcpyAsync(h->po_off.ptr, d_off, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToDevice, h->stream));
+  if (h->f64) {  // fp64 counters: (double) preferences, any value
+    if (int rc = po_f64_load(h, d_key, d_val, npairs)) return rc;
+    h->h_po_off.assign(h_off, h_off + n + 1);
+    h->po_npairs = npairs;
+    h->po_loaded = true;
+    h->finalized = false;
+    return CMS_OK;
+  }
   if (npairs > 0)
     hipLaunchKernelGGL(k_po_prep, dim3(grid_for((npairs + 255) / 256, 8192)), dim3(256), 0, h->stream, d_key, d_val,
                        npairs, h->hp.frac_bits, h->po_kp.as<uint64_t>(), h->po_inc.as<uint32_t>(), h->d_flags);
@@ -407,6 +415,11 @@ int po_finalize(cms_handle* h) {
     total += (int64_t)h->h_po_w[r] * h->h_po_d[r];
     rtot += h->h_po_d[r];
   }
+  if (h->f64) {
+    if (int rc = po_f64_finalize(h, total, rtot)) return rc;
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    return CMS_OK;
+  }
   CMS_HIP(h->po_sk.ensure(sizeof(uint32_t) * std::max<int64_t>(total, 1)));
   CMS_HIP(h->po_norm.ensure(sizeof(uint64_t) * std::max<int64_t>(rtot, 1)));
   CMS_HIP(h->po_nsq.ensure(sizeof(double) * std::max<int64_t>(rtot, 1)));
@@ -434,6 +447,7 @@ int po_finalize(cms_handle* h) {
 int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m,
                     double* d_out) {
   if (nq <= 0 || m <= 0) return CMS_OK;
+  if (h->f64) return po_f64_pair_cosines(h, d_qrows, nq, d_crows, m, d_out);
   PoPairArgs a;
   a.off = h->po_off.as<int64_t>();
   a.kp = h->po_kp.as<uint64_t>();
@@ -460,6 +474,7 @@ int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int
 
 int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
   if (m <= 0) return CMS_OK;
+  if (h->f64) return po_f64_point_queries(h, row, d_keys, m, d_out);
   hipLaunchKernelGGL(k_po_point, dim3(grid_for((m + 255) / 256, 4096)), dim3(256), 0, h->stream,
                      h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->hp, row, d_keys, m, d_out);
   CMS_HIP(hipGetLastError());
@@ -469,6 +484,7 @@ int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t 
 int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
                             const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out) {
   if (q <= 0) return CMS_OK;
+  if (h->f64) return po_f64_estimate_preferences(h, user_row, d_nb_rows, d_sims, m, d_items, q, use_capper, lo, hi, d_out);
   hipLaunchKernelGGL(k_po_estimate, dim3(grid_for((q + 255) / 256, 4096)), dim3(256), 0, h->stream,
                      h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->hp, user_row, d_nb_rows, d_sims, m,
                      d_items, q, use_capper, lo, hi, d_out);

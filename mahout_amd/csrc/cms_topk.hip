@@ -755,9 +755,11 @@ int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, i
   for (int64_t r0 = 0; r0 < row_count; r0 += qb) {
     const int64_t rcnt = std::min(qb, row_count - r0);
     std::vector<TopQuery> qs;
+    if (h->f64 && (rc = f64_slab(h, row_begin + r0, rcnt, h->ws_slab.as<double>()))) return rc;
     for (int64_t q = 0; q < rcnt; ++q) {
       const int64_t row = row_begin + r0 + q;
-      if ((rc = pair_cosines(h, row, h->ws_query.as<int64_t>(), n, h->ws_slab.as<double>() + q * n))) return rc;
+      if (!h->f64 && (rc = pair_cosines(h, row, h->ws_query.as<int64_t>(), n, h->ws_slab.as<double>() + q * n)))
+        return rc;
       qs.push_back(TopQuery{q, row, r0 + q});
     }
     if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, nullptr, d_ids, d_scores, d_counts))) return rc;

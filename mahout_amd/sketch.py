@@ -72,10 +72,13 @@ def comm_unique_id():
 
 class SketchTable:
     def __init__(self, num_owners, depth=5, width=4096, seed=42, weighted=False, device=-1, owner_ids=None,
-                 per_owner=False, frac_bits=0):
+                 per_owner=False, frac_bits=0, counters="u32"):
+        """counters: "u32" (exact integer counters in units of 2^-frac_bits) or
+        "f64" (DoubleCountMinSketch's fp64 counters for any float preference)."""
         lib = _lib.load()
         p = _lib.CmsParams()
         check(lib.cms_params_init(ctypes.byref(p)))
+        p.counter_type = {"u32": _lib.CMS_COUNTER_U32, "f64": _lib.CMS_COUNTER_F64}[counters]
         p.depth = depth
         p.width = width
         p.seed = seed
@@ -87,6 +90,7 @@ class SketchTable:
         create = lib.cms_create_per_owner if per_owner else lib.cms_create
         check(create(ctypes.byref(p), ctypes.byref(h)))
         self.per_owner = per_owner
+        self.counters = counters
         self._lib = lib
         self._h = h
         self.num_owners = num_owners

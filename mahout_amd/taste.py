@@ -101,6 +101,30 @@ class CountMinSketchConfig:
         return self._lookup(self._result[2] if self._result else None, userID)
 
 
+def counter_units(offsets, values):
+    """(frac_bits, counters) for a DataModel: exact u32 counters in units of
+    2^-frac_bits when every preference is a non-negative multiple of
+    2^-frac_bits and every owner's total stays below 2^32 such units (the
+    integer fast paths, bit-identical similarities); otherwise
+    DoubleCountMinSketch's own fp64 counters, filled in DataModel order."""
+    if values is None:
+        return 0, "u32"
+    v = np.asarray(values, np.float32)
+    if v.size and (not np.all(np.isfinite(v)) or (v < 0).any()):
+        return 0, "f64"
+    try:
+        fb = frac_bits_for(v)
+    except ValueError:
+        return 0, "f64"
+    off = np.asarray(offsets, np.int64)
+    if v.size:
+        mass = np.add.reduceat(np.ldexp(v.astype(np.float64), fb), off[:-1].clip(max=v.size - 1))
+        mass[off[1:] == off[:-1]] = 0.0
+        if (mass >= 2.0 ** 32).any():
+            return 0, "f64"
+    return fb, "u32"
+
+
 def _map_error(e, owner_kind="user"):
     if e.code == _lib.CMS_E_NO_SUCH_ID:
         return NoSuchUserException(str(e)) if owner_kind == "user" else NoSuchItemException(str(e))
@@ -136,22 +160,18 @@ class CosineCM:
 
     def _build(self):
         m = self._model
-        # preference granularity: half-star ratings need 1 fractional bit, etc.
-        try:
-            fb = 0 if m.values is None else frac_bits_for(m.values)
-        except ValueError as e:
-            raise TasteException(str(e))
+        fb, counters = counter_units(m.offsets, m.values)
         try:
             if self._per_owner:
-                self._table = SketchTable.per_owner_shapes(m.getNumUsers(), seed=self._hfb.seed,
-                                                           weighted=self._weighted, device=self._device,
-                                                           owner_ids=m.getUserIDs(), frac_bits=fb)
+                self._table = SketchTable(m.getNumUsers(), seed=self._hfb.seed, weighted=self._weighted,
+                                          device=self._device, owner_ids=m.getUserIDs(), per_owner=True,
+                                          frac_bits=fb, counters=counters)
                 self._table.ingest_csr(m.offsets, m.keys, m.values)
                 self._conf._configure(self._table, m)
             else:
                 self._table = SketchTable(m.getNumUsers(), depth=self.depth, width=self.width, seed=self._hfb.seed,
                                           weighted=self._weighted, device=self._device, owner_ids=m.getUserIDs(),
-                                          frac_bits=fb)
+                                          frac_bits=fb, counters=counters)
                 self._table.ingest_csr(m.offsets, m.keys, m.values)
             self._table.finalize()
         except _lib.CmsError as e:

@@ -75,3 +75,20 @@ def test_estimate_preference_oracle_hand_kat(oracle):
     assert got == exp
     assert math.isnan(oracle.estimate_preference(t, a, b, 0, [1, 2], 303))  # one data point only
     assert oracle.estimate_preference(t, a, b, 0, [1, 2], 202, capper=(1.0, 2.5)) == np.float32(2.5)
+
+
+def test_counter_units_picks_exact_u32_or_fp64():
+    """taste.counter_units: exact u32 counters in units of 2^-s while every
+    preference is a non-negative multiple of 2^-s and every owner's total
+    stays below 2^32 units; DoubleCountMinSketch's fp64 counters otherwise."""
+    import numpy as np
+    from mahout_amd.taste import counter_units
+    off = np.array([0, 2, 4], np.int64)
+    assert counter_units(off, None) == (0, "u32")
+    assert counter_units(off, np.array([1, 2, 3, 4], np.float32)) == (0, "u32")
+    assert counter_units(off, np.array([0.5, 2, 3, 4.5], np.float32)) == (1, "u32")
+    assert counter_units(off, np.array([0.1, 2, 3, 4], np.float32)) == (27, "u32")  # small masses still fit
+    assert counter_units(np.array([0, 40], np.int64), np.full(40, 4.1, np.float32)) == (0, "f64")  # 2^32 units
+    assert counter_units(off, np.array([-1, 2, 3, 4], np.float32)) == (0, "f64")
+    assert counter_units(off, np.array([np.nan, 2, 3, 4], np.float32)) == (0, "f64")
+    assert counter_units(np.array([0, 0, 4], np.int64), np.array([1e9, 2e9, 3e9, 4], np.float32)) == (0, "f64")
