@@ -88,7 +88,7 @@ def test_counter_units_picks_exact_u32_or_fp64():
     assert counter_units(off, np.array([1, 2, 3, 4], np.float32)) == (0, "u32")
     assert counter_units(off, np.array([0.5, 2, 3, 4.5], np.float32)) == (1, "u32")
     assert counter_units(off, np.array([0.1, 2, 3, 4], np.float32)) == (27, "u32")  # small masses still fit
-    assert counter_units(np.array([0, 40], np.int64), np.full(40, 4.1, np.float32)) == (0, "f64")  # 2^32 units
+    assert counter_units(np.array([0, 400], np.int64), np.full(400, 0.1, np.float32)) == (0, "f64")  # 2^32 units
     assert counter_units(off, np.array([-1, 2, 3, 4], np.float32)) == (0, "f64")
     assert counter_units(off, np.array([np.nan, 2, 3, 4], np.float32)) == (0, "f64")
     assert counter_units(np.array([0, 0, 4], np.int64), np.array([1e9, 2e9, 3e9, 4], np.float32)) == (0, "f64")
