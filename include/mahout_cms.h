@@ -135,7 +135,16 @@ int cms_ingest_device_rows(cms_handle* h, const int64_t* d_row, const int64_t* d
  * -- the DataModel layout (one PreferenceArray per owner,
  * GenericUserPreferenceArray.java:52-54).  offsets has num_owners+1 entries. */
 int cms_ingest_csr(cms_handle* h, const int64_t* offsets, const int64_t* keys, const float* vals);
-/* CSR resident on the device. Asynchronous. */
+/* CSR resident on the device.  The offsets are checked on the device before
+ * any counter is touched (offsets[0] == 0, non-decreasing; CMS_E_PARAM
+ * otherwise), so the build reads keys[0 .. offsets[num_owners]) only; d_keys
+ * (and d_vals) must hold that many entries.  Asynchronous after that check.
+ *
+ * Device ingests are not all-or-nothing for the VALUES (unlike the host
+ * ingests, which validate the whole batch first): a pair whose row is outside
+ * [0, num_owners) (COO) or whose increment the counter type cannot take is
+ * skipped, the others are applied, and the next synchronising call
+ * (cms_synchronize / cms_finalize) reports CMS_E_PARAM / CMS_E_VALUE. */
 int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t* d_keys, const float* d_vals);
 
 /* Forget all counters (next ingest rebuilds the table from zero). */

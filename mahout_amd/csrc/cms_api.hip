@@ -576,8 +576,15 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
   if (h->merged && h->multi())
     return set_error(CMS_E_STATE, "CSR bulk ingest into a merged multi-rank table: cms_reset first, or use COO ingest");
   int64_t np = 0;
+  if (!h->per_owner) {  // the build reads keys[offsets[r] .. offsets[r+1]): check the offsets first
+    int rc0 = check_offsets_device(h, d_offsets);
+    if (rc0) return rc0;
+  }
   CMS_HIP(hipMemcpyAsync(&np, d_offsets + h->n, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
+  if (!h->per_owner) {
+    if (int rc0 = check_flags(h, false)) return set_error(rc0, "CSR offsets must start at 0 and be non-decreasing");
+  }
   if (h->per_owner) {
     std::vector<int64_t> off(h->n + 1);
     CMS_HIP(hipMemcpy(off.data(), d_offsets, sizeof(int64_t) * (h->n + 1), hipMemcpyDeviceToHost));

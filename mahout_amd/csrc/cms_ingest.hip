@@ -134,6 +134,24 @@ __global__ void k_validate(const int64_t* rows, const float* val, int64_t n, int
   if (f) atomicOr(flags, f);
 }
 
+// CSR offsets from the caller: offsets[0] == 0 and non-decreasing, so every
+// owner's range lies inside [0, offsets[n]).
+__global__ void k_check_offsets(const int64_t* off, int64_t n, uint32_t* flags) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    if ((r == 0 && off[0] != 0) || off[r + 1] < off[r]) {
+      atomicOr(flags, kFlagBadRow);
+      return;
+    }
+  }
+}
+
+int check_offsets_device(cms_handle* h, const int64_t* d_off) {
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_check_offsets, dim3(grid), dim3(256), 0, h->stream, d_off, h->n, h->d_flags);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n) {
   if (n <= 0 || (!d_rows && !d_val)) return CMS_OK;
   unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);

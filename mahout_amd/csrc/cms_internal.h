@@ -265,6 +265,8 @@ using AllReduceU64 = std::function<int(uint64_t*, int64_t)>;
 int merge_packed(cms_handle* h, const AllReduceU64& allreduce);
 // flags rows outside [0,n) and increments the counter type cannot hold.
 int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int64_t n);
+// offsets[0] == 0 and non-decreasing (flags kFlagBadRow otherwise)
+int check_offsets_device(cms_handle* h, const int64_t* d_off);
 int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d_out);
 int scan_exclusive_u32(cms_handle* h, const uint32_t* in, uint32_t* out, int64_t L, uint32_t* bsum);
 // ---- cms_partition.hip ----

@@ -115,3 +115,23 @@ def test_overflow_guard_and_bad_params():
         with pytest.raises(CmsError) as e:
             t.similarity(0, 1)  # before finalize
         assert e.value.code == CMS_E_STATE
+
+
+def test_device_csr_offsets_checked_before_the_build():
+    """cms_ingest_csr_device checks offsets[0] == 0 and non-decreasing on the
+    device before any counter is touched (the build would otherwise read keys
+    outside the caller's buffer); the table stays as it was."""
+    import torch
+    from mahout_amd._lib import CMS_E_PARAM, CmsError
+    with SketchTable(4, depth=2, width=64) as t:
+        keys = torch.arange(10, dtype=torch.int64, device="cuda")
+        good = torch.tensor([0, 3, 6, 8, 10], dtype=torch.int64, device="cuda")
+        t.ingest_csr_device(good, keys)
+        t.finalize()
+        before = t.read_counters()
+        for bad in ([0, 3, 2, 8, 10], [1, 3, 6, 8, 10]):
+            with pytest.raises(CmsError) as ei:
+                t.ingest_csr_device(torch.tensor(bad, dtype=torch.int64, device="cuda"), keys)
+            assert ei.value.code == CMS_E_PARAM
+        t.finalize()
+        assert np.array_equal(t.read_counters(), before)
