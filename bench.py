@@ -158,6 +158,45 @@ def cpu_baseline(off_d, keys_d, args, budget_s=3.0):
             "modes": modes, "best_updates_per_s": best["updates_per_s"], "host": host_cpu_info(), "note": BASELINE_NOTE}
 
 
+def query_latency(table, n, calls=2000, threads=8):
+    """The drop-in's per-call cost: CosineCM.userSimilarity(u1, u2) as one
+    cms_similarity from the host (CosineCMGpu's route), serially and from 8
+    threads at once (queries after finalize share the handle: leased streams
+    and scratch, MultithreadedBatchItemSimilarities.java:78)."""
+    import threading
+    rng = np.random.Generator(np.random.PCG64(9))
+    a = rng.integers(0, n, calls)
+    b = rng.integers(0, n, calls)
+    for i in range(50):
+        table.similarity(int(a[i]), int(b[i]))
+    t0 = time.perf_counter()
+    for i in range(calls):
+        table.similarity(int(a[i]), int(b[i]))
+    serial = (time.perf_counter() - t0) / calls
+
+    def worker(k):
+        for i in range(k, calls, threads):
+            table.similarity(int(a[i]), int(b[i]))
+
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    batch = rng.integers(0, n, 10_000)
+    table.similarities(int(a[0]), batch)
+    t0 = time.perf_counter()
+    for i in range(20):
+        table.similarities(int(a[i]), batch)
+    bdt = (time.perf_counter() - t0) / 20
+    return {"single_pair_us": serial * 1e6, "threads": threads, "threaded_pairs_per_s": calls / dt,
+            "batched_10k_pairs_ms": bdt * 1e3, "batched_pairs_per_s": batch.size / bdt,
+            "note": "cms_similarity per call from Python ctypes (host round trip + one k_pair_cosine launch); "
+                    "itemSimilarities(id, ids[]) as one batched call"}
+
+
 def cosine_cpu_baseline(items, users, n, d, w, budget_s=3.0, sample_owners=192, seed=5):
     """Config-4 similarity on the host cores, two modes x {1 thread, all
     threads} (oracle/cms_baseline.c):
@@ -367,12 +406,60 @@ def cosine_1m(args, local, device, rank=0, world=1):
         dist.all_reduce(v, op=dist.ReduceOp.MAX)
         return float(v.item())
 
+    # config 3 as a measured step: reset + ingest of this rank's shard + finalize
+    # (with G ranks the packed RCCL all-reduce of the 1M-item table); 1 warm-up
+    # step, then c3_steps timed steps; the last one leaves the table for config 4
+    c3_steps = 5
+
+    def c3_step():
+        t.reset()
+        t.ingest_device_rows(items, users, None, local_pairs)
+        t.finalize()
+
+    c3_step()
+    t.set_timing(True, level=1)
+    t.reset_timing()
     bar()
     t0 = time.perf_counter()
-    t.ingest_device_rows(items, users, None, local_pairs)
-    t.finalize()
+    for _ in range(c3_steps):
+        c3_step()
     bar()
-    ingest_s = max_over_ranks(time.perf_counter() - t0)
+    ingest_s = max_over_ranks(time.perf_counter() - t0) / c3_steps
+    b_ms, b_n = t.timing("build_rows")
+    ar_ms, ar_n = t.timing("allreduce")
+    t.set_timing(True, level=2)
+    t.reset_timing()
+    c3_step()
+    t.synchronize()
+    c3_break = {}
+    for name in ["partition", "build_plan", "build_rows", "hot_norms", "norms", "merge_bounds", "merge_pack",
+                 "allreduce", "merge_unpack"]:
+        ms_, n_ = t.timing(name)
+        if n_:
+            c3_break[name] = round(ms_, 3)
+    t.set_timing(False)
+    tb = n * d * w * 4  # the table priced at 4 B per counter (the build stores u16 for all but hot rows)
+    c3_build_bytes = local_pairs * 8 + (n + 1) * 8 + tb  # CSR keys + offsets read, table written once
+    c3_step_bytes = local_pairs * 16 + tb  # per GPU: B_g = N/G * 16 + n*d*w*4
+    config3 = {
+        "workload": f"config 3: {npairs}-pair Zipf stream (10M users x {n} items), d={d} w={w}, user-hash sharded over "
+                    f"{world} GPU(s); one step = reset + ingest of the rank's shard + finalize"
+                    + (" (packed RCCL all-reduce of the table)" if world > 1 else ""),
+        "pairs_per_rank": local_pairs, "steps": c3_steps, "warmup": 1,
+        "ms_per_step": ingest_s * 1e3, "updates_per_s": npairs / ingest_s,
+        "roofline": {"bound": "hbm", "kernel": "k_build_rows",
+                     "achieved": c3_build_bytes / (b_ms / b_n * 1e-3) / 1e9 if b_n else None,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": c3_build_bytes / (b_ms / b_n * 1e-3) / 1e9 / HBM_PEAK_GBPS if b_n else None,
+                     "algorithmic_bytes_per_launch": c3_build_bytes,
+                     "avg_launch_ms": b_ms / b_n if b_n else None,
+                     "u16_table_write_GBps": (n * d * w * 2) / (b_ms / b_n * 1e-3) / 1e9 if b_n else None},
+        "step_roofline": {"algorithmic_bytes_per_gpu": c3_step_bytes,
+                          "achieved_GBps": c3_step_bytes / ingest_s / 1e9,
+                          "frac": c3_step_bytes / ingest_s / 1e9 / HBM_PEAK_GBPS},
+        "allreduce_ms_per_step": ar_ms / ar_n if ar_n else None,
+        "breakdown_ms_one_step": c3_break,
+    }
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cosine_cpu_baseline(items, users, n, d, w)
@@ -449,6 +536,7 @@ def cosine_1m(args, local, device, rank=0, world=1):
         "multi_limb_owners": nm, "full_lists": int((cnt == k).sum()), "topk_redo_rows": int(st["topk_redo"]),
         "config3_ingest_merge_s": ingest_s,
         "config3_updates_per_s": npairs / ingest_s,
+        "config3": config3,
         "config5_streaming": stream,
         "cpu_baseline": cpu,
     }
@@ -729,6 +817,7 @@ def main():
         dt = time.perf_counter() - t0
         extras["host_buffers_updates_per_s"] = npairs * 3 / dt
         del h_items, h_users
+        extras["query_latency"] = query_latency(table, n)
         # all-pairs top-100 over the config-2 table (int8-limb MFMA + exact fp64 epilogue)
         extras["allpairs_top100_cfg2"] = allpairs_measure(table, 0, n, 100, n, d, w)
         # the same lists through the symmetric streaming pass (each unordered pair once)

@@ -73,8 +73,8 @@ static hipEvent_t pooled_event(cms_handle* h) {
   return e;
 }
 
-TimedScope::TimedScope(cms_handle* hh, const char* nm) : h(hh), name(nm) {
-  if (h->timing >= (fine_scope(nm) ? 2 : 1)) {
+TimedScope::TimedScope(cms_handle* hh, const char* nm, bool on) : h(hh), name(nm) {
+  if (on && h->timing >= (fine_scope(nm) ? 2 : 1)) {
     start = pooled_event(h);
     if (start) (void)hipEventRecord(start, h->stream);
   }
@@ -163,6 +163,49 @@ struct Guard {
   }
   ~Guard() { h->mu.unlock(); }
 };
+
+// Point queries after cms_finalize: shared with each other, exclusive of writers.
+struct SharedGuard {
+  cms_handle* h;
+  explicit SharedGuard(cms_handle* hh) : h(hh) {
+    h->mu.lock_shared();
+    (void)hipSetDevice(h->device);
+  }
+  ~SharedGuard() { h->mu.unlock_shared(); }
+};
+
+// A query context (stream + scratch) leased from the handle's pool for one call.
+struct CtxLease {
+  cms_handle* h;
+  QueryCtx* c = nullptr;
+  explicit CtxLease(cms_handle* hh) : h(hh) {
+    std::lock_guard<std::mutex> g(h->pool_mu);
+    if (!h->qpool.empty()) {
+      c = h->qpool.back();
+      h->qpool.pop_back();
+    }
+  }
+  int ready() {
+    if (c) return CMS_OK;
+    c = new (std::nothrow) QueryCtx();
+    if (!c) return set_error(CMS_E_OOM, "host allocation failed");
+    CMS_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return CMS_OK;
+  }
+  ~CtxLease() {
+    if (!c) return;
+    std::lock_guard<std::mutex> g(h->pool_mu);
+    h->qpool.push_back(c);
+  }
+};
+
+static void free_query_pool(cms_handle* h) {
+  for (QueryCtx* c : h->qpool) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+  }
+  h->qpool.clear();
+}
 
 static int refuse_per_owner(cms_handle* h, const char* what) {
   if (h->per_owner)
@@ -327,6 +370,7 @@ void cms_destroy(cms_handle* h) {
   }
   for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
   if (h->order_ev) (void)hipEventDestroy(h->order_ev);
+  free_query_pool(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
@@ -816,9 +860,9 @@ int cms_release_to_stream(cms_handle* h, void* stream) {
   return order_streams(h, h->stream, (hipStream_t)stream);
 }
 
-int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n, double* out) {
-  if (!h || (n > 0 && (!ids2 || !out))) return set_error(CMS_E_PARAM, "null argument");
-  Guard g(h);
+// userSimilarity(id1, ids2[i]) on stream st with scratch (qb, ob)
+static int similarities_on(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n, double* out, hipStream_t st,
+                           DevBuf& qb, DevBuf& ob, bool shared) {
   int rc = require_finalized(h);
   if (rc) return rc;
   int64_t q;
@@ -827,33 +871,45 @@ int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n,
   std::vector<int64_t> rows(n);
   for (int64_t i = 0; i < n; ++i)
     if ((rc = row_of(h, ids2[i], &rows[i]))) return rc;
-  CMS_HIP(h->ws_query.ensure(sizeof(int64_t) * (n + 1)));
-  CMS_HIP(h->ws_small.ensure(sizeof(double) * n));
+  CMS_HIP(qb.ensure(sizeof(int64_t) * (n + 1)));
+  CMS_HIP(ob.ensure(sizeof(double) * n));
+  hipStream_t ks = shared ? st : nullptr;  // kernels on the context's stream (untimed) or the handle's
   if (h->per_owner) {  // u2's shape decides each pair (CosineCM.java:86)
     if ((rc = po_require_shapes(h, rows.data(), n))) return rc;
     rows.push_back(q);
-    CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, rows.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, h->stream));
-    rc = po_pair_cosines(h, h->ws_query.as<int64_t>() + n, 1, h->ws_query.as<int64_t>(), n, h->ws_small.as<double>());
+    CMS_HIP(hipMemcpyAsync(qb.ptr, rows.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    rc = po_pair_cosines(h, qb.as<int64_t>() + n, 1, qb.as<int64_t>(), n, ob.as<double>(), ks);
   } else {
-    CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, rows.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
-    rc = pair_cosines(h, q, h->ws_query.as<int64_t>(), n, h->ws_small.as<double>());
+    CMS_HIP(hipMemcpyAsync(qb.ptr, rows.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st));
+    rc = pair_cosines(h, q, qb.as<int64_t>(), n, ob.as<double>(), ks);
   }
   if (rc) return rc;
-  CMS_HIP(hipMemcpyAsync(out, h->ws_small.ptr, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
-  CMS_HIP(hipStreamSynchronize(h->stream));
+  CMS_HIP(hipMemcpyAsync(out, ob.ptr, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+  CMS_HIP(hipStreamSynchronize(st));
   return CMS_OK;
+}
+
+int cms_similarities(cms_handle* h, int64_t id1, const int64_t* ids2, int64_t n, double* out) {
+  if (!h || (n > 0 && (!ids2 || !out))) return set_error(CMS_E_PARAM, "null argument");
+  {
+    SharedGuard g(h);
+    if (!po_shared_scratch(h)) {  // concurrent readers, each on its own stream and scratch
+      CtxLease L(h);
+      if (int rc = L.ready()) return rc;
+      return similarities_on(h, id1, ids2, n, out, L.c->stream, L.c->q, L.c->o, true);
+    }
+  }
+  Guard g(h);
+  return similarities_on(h, id1, ids2, n, out, h->stream, h->ws_query, h->ws_small, false);
 }
 
 int cms_similarity(cms_handle* h, int64_t id1, int64_t id2, double* out) {
   return cms_similarities(h, id1, &id2, 1, out);
 }
 
-int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neighbor_ids, int64_t m,
-                             const int64_t* item_keys, int64_t q, int32_t use_capper, float cap_min, float cap_max,
-                             float* out) {
-  if (!h || m < 0 || q < 0 || (m > 0 && !neighbor_ids) || (q > 0 && (!item_keys || !out)))
-    return set_error(CMS_E_PARAM, "null argument");
-  Guard g(h);
+static int estimate_on(cms_handle* h, int64_t user_id, const int64_t* neighbor_ids, int64_t m,
+                       const int64_t* item_keys, int64_t q, int32_t use_capper, float cap_min, float cap_max,
+                       float* out, hipStream_t st, QueryCtx& c, bool shared) {
   int rc = require_finalized(h);
   if (rc) return rc;
   int64_t urow;
@@ -862,57 +918,78 @@ int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neig
   for (int64_t i = 0; i < m; ++i)
     if ((rc = row_of(h, neighbor_ids[i], &rows[i]))) return rc;
   if (q == 0) return CMS_OK;
-  DevBuf d_rows, d_sims, d_items, d_out;
-  CMS_HIP(d_rows.ensure(sizeof(int64_t) * std::max<int64_t>(m, 1)));
-  CMS_HIP(d_sims.ensure(sizeof(double) * std::max<int64_t>(m, 1)));
-  CMS_HIP(d_items.ensure(sizeof(int64_t) * q));
-  CMS_HIP(d_out.ensure(sizeof(float) * q));
-  if (m > 0)
-    CMS_HIP(hipMemcpyAsync(d_rows.ptr, rows.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, h->stream));
-  CMS_HIP(hipMemcpyAsync(d_items.ptr, item_keys, sizeof(int64_t) * q, hipMemcpyHostToDevice, h->stream));
+  hipStream_t ks = shared ? st : nullptr;
+  // c.r: neighbour rows then the user's row; c.x: similarities; c.q: item keys; c.o: estimates
+  CMS_HIP(c.r.ensure(sizeof(int64_t) * (size_t)(m + 1)));
+  CMS_HIP(c.x.ensure(sizeof(double) * (size_t)std::max<int64_t>(m, 1)));
+  CMS_HIP(c.q.ensure(sizeof(int64_t) * (size_t)q));
+  CMS_HIP(c.o.ensure(sizeof(float) * (size_t)q));
+  rows.push_back(urow);
+  CMS_HIP(hipMemcpyAsync(c.r.ptr, rows.data(), sizeof(int64_t) * (size_t)(m + 1), hipMemcpyHostToDevice, st));
+  CMS_HIP(hipMemcpyAsync(c.q.ptr, item_keys, sizeof(int64_t) * q, hipMemcpyHostToDevice, st));
+  int64_t* d_rows = c.r.as<int64_t>();
+  double* d_sims = c.x.as<double>();
   if (h->per_owner) {
     std::vector<int64_t> others;  // every neighbour but the user needs its own profile (:154-156)
-    for (int64_t r : rows)
-      if (r != urow) others.push_back(r);
+    for (int64_t i = 0; i < m; ++i)
+      if (rows[i] != urow) others.push_back(rows[i]);
     if ((rc = po_require_shapes(h, others.data(), (int64_t)others.size()))) return rc;
-    DevBuf d_u;
-    CMS_HIP(d_u.ensure(sizeof(int64_t)));
-    CMS_HIP(hipMemcpyAsync(d_u.ptr, &urow, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
-    if ((rc = po_pair_cosines(h, d_u.as<int64_t>(), 1, d_rows.as<int64_t>(), m, d_sims.as<double>()))) return rc;
-    rc = po_estimate_preferences(h, urow, d_rows.as<int64_t>(), d_sims.as<double>(), m, d_items.as<int64_t>(), q,
-                                 use_capper, cap_min, cap_max, d_out.as<float>());
-    if (rc == CMS_OK) rc = hipStreamSynchronize(h->stream) == hipSuccess ? CMS_OK : set_error(CMS_E_HIP, "estimate");
-    if (rc) return rc;
+    if ((rc = po_pair_cosines(h, d_rows + m, 1, d_rows, m, d_sims, ks))) return rc;
+    rc = po_estimate_preferences(h, urow, d_rows, d_sims, m, c.q.as<int64_t>(), q, use_capper, cap_min, cap_max,
+                                 c.o.as<float>(), ks);
   } else {
-    if ((rc = pair_cosines(h, urow, d_rows.as<int64_t>(), m, d_sims.as<double>()))) return rc;
-    if ((rc = estimate_preferences(h, urow, d_rows.as<int64_t>(), d_sims.as<double>(), m, d_items.as<int64_t>(), q,
-                                   use_capper, cap_min, cap_max, d_out.as<float>())))
-      return rc;
+    if ((rc = pair_cosines(h, urow, d_rows, m, d_sims, ks))) return rc;
+    rc = estimate_preferences(h, urow, d_rows, d_sims, m, c.q.as<int64_t>(), q, use_capper, cap_min, cap_max,
+                              c.o.as<float>(), ks);
   }
-  CMS_HIP(hipMemcpyAsync(out, d_out.ptr, sizeof(float) * q, hipMemcpyDeviceToHost, h->stream));
-  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (rc) return rc;
+  CMS_HIP(hipMemcpyAsync(out, c.o.ptr, sizeof(float) * q, hipMemcpyDeviceToHost, st));
+  CMS_HIP(hipStreamSynchronize(st));
   return CMS_OK;
+}
+
+int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neighbor_ids, int64_t m,
+                             const int64_t* item_keys, int64_t q, int32_t use_capper, float cap_min, float cap_max,
+                             float* out) {
+  if (!h || m < 0 || q < 0 || (m > 0 && !neighbor_ids) || (q > 0 && (!item_keys || !out)))
+    return set_error(CMS_E_PARAM, "null argument");
+  {
+    SharedGuard g(h);
+    if (!po_shared_scratch(h)) {
+      CtxLease L(h);
+      if (int rc = L.ready()) return rc;
+      return estimate_on(h, user_id, neighbor_ids, m, item_keys, q, use_capper, cap_min, cap_max, out, L.c->stream,
+                         *L.c, true);
+    }
+  }
+  Guard g(h);
+  QueryCtx tmp;  // exclusive path: the handle's stream, call-local scratch
+  return estimate_on(h, user_id, neighbor_ids, m, item_keys, q, use_capper, cap_min, cap_max, out, h->stream, tmp,
+                     false);
 }
 
 int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
-  Guard g(h);
+  SharedGuard g(h);
   int rc = require_finalized(h);
   if (rc) return rc;
   int64_t row;
   if ((rc = row_of(h, id, &row))) return rc;
-  CMS_HIP(h->ws_query.ensure(sizeof(int64_t)));
-  CMS_HIP(h->ws_small.ensure(sizeof(double)));
-  CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, &key, sizeof(int64_t), hipMemcpyHostToDevice, h->stream));
+  CtxLease L(h);
+  if ((rc = L.ready())) return rc;
+  QueryCtx& c = *L.c;
+  CMS_HIP(c.q.ensure(sizeof(int64_t)));
+  CMS_HIP(c.o.ensure(sizeof(double)));
+  CMS_HIP(hipMemcpyAsync(c.q.ptr, &key, sizeof(int64_t), hipMemcpyHostToDevice, c.stream));
   if (h->per_owner) {
     if ((rc = po_require_shapes(h, &row, 1))) return rc;
-    rc = po_point_queries(h, row, h->ws_query.as<int64_t>(), 1, h->ws_small.as<double>());
+    rc = po_point_queries(h, row, c.q.as<int64_t>(), 1, c.o.as<double>(), c.stream);
   } else {
-    rc = point_queries(h, row, h->ws_query.as<int64_t>(), 1, h->ws_small.as<double>());
+    rc = point_queries(h, row, c.q.as<int64_t>(), 1, c.o.as<double>(), c.stream);
   }
   if (rc) return rc;
-  CMS_HIP(hipMemcpyAsync(out, h->ws_small.ptr, sizeof(double), hipMemcpyDeviceToHost, h->stream));
-  CMS_HIP(hipStreamSynchronize(h->stream));
+  CMS_HIP(hipMemcpyAsync(out, c.o.ptr, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+  CMS_HIP(hipStreamSynchronize(c.stream));
   return CMS_OK;
 }
 

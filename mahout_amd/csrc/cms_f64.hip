@@ -398,10 +398,10 @@ int f64_norms(cms_handle* h) {
   return CMS_OK;
 }
 
-int f64_pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out) {
+int f64_pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out, hipStream_t s) {
   if (m <= 0) return CMS_OK;
-  TimedScope ts(h, "pair_cosine");
-  hipLaunchKernelGGL(k_f64_pairs, dim3(grid_for(m)), dim3(256), 0, h->stream, h->d_t64, h->d_norm_sqrt, h->p.depth,
+  TimedScope ts(h, "pair_cosine", s == nullptr);
+  hipLaunchKernelGGL(k_f64_pairs, dim3(grid_for(m)), dim3(256), 0, s ? s : h->stream, h->d_t64, h->d_norm_sqrt, h->p.depth,
                      h->p.width, q_row, d_rows, m, h->n, (int)h->p.weighting, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
@@ -416,18 +416,18 @@ int f64_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_slab) {
   return CMS_OK;
 }
 
-int f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
+int f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s) {
   if (m <= 0) return CMS_OK;
-  hipLaunchKernelGGL(k_f64_point, dim3(grid_for(m)), dim3(256), 0, h->stream, h->d_t64, h->hp, row, d_keys, m, d_out);
+  hipLaunchKernelGGL(k_f64_point, dim3(grid_for(m)), dim3(256), 0, s ? s : h->stream, h->d_t64, h->hp, row, d_keys, m, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
 int f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims,
                              int64_t m, const int64_t* d_items, int64_t q, int use_capper, float lo, float hi,
-                             float* d_out) {
+                             float* d_out, hipStream_t s) {
   if (q <= 0) return CMS_OK;
-  hipLaunchKernelGGL(k_f64_estimate, dim3(grid_for(q)), dim3(256), 0, h->stream, h->d_t64, h->hp, user_row, d_nb_rows,
+  hipLaunchKernelGGL(k_f64_estimate, dim3(grid_for(q)), dim3(256), 0, s ? s : h->stream, h->d_t64, h->hp, user_row, d_nb_rows,
                      d_sims, m, d_items, q, use_capper, lo, hi, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
@@ -468,7 +468,8 @@ int po_f64_finalize(cms_handle* h, int64_t total_counters, int64_t total_rows) {
 }
 
 int po_f64_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m,
-                        double* d_out) {
+                        double* d_out, hipStream_t s) {
+  (void)s;  // exclusive callers only: the workgroups' scratch rows belong to the handle
   TimedScope ts(h, "po_pair_cosine");
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nq * m, po_f64_grid(h)));
   hipLaunchKernelGGL(k_po_f64_pairs, dim3(grid), dim3(kF64Threads), 0, h->stream, h->po_off.as<int64_t>(),
@@ -479,8 +480,8 @@ int po_f64_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const
   return CMS_OK;
 }
 
-int po_f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
-  hipLaunchKernelGGL(k_po_f64_point, dim3(grid_for(m)), dim3(256), 0, h->stream, h->po_shape.as<PoShape>(),
+int po_f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_po_f64_point, dim3(grid_for(m)), dim3(256), 0, s ? s : h->stream, h->po_shape.as<PoShape>(),
                      h->po_sk.as<double>(), h->hp, row, d_keys, m, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
@@ -488,8 +489,8 @@ int po_f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int6
 
 int po_f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims,
                                 int64_t m, const int64_t* d_items, int64_t q, int use_capper, float lo, float hi,
-                                float* d_out) {
-  hipLaunchKernelGGL(k_po_f64_estimate, dim3(grid_for(q)), dim3(256), 0, h->stream, h->po_shape.as<PoShape>(),
+                                float* d_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_po_f64_estimate, dim3(grid_for(q)), dim3(256), 0, s ? s : h->stream, h->po_shape.as<PoShape>(),
                      h->po_sk.as<double>(), h->hp, user_row, d_nb_rows, d_sims, m, d_items, q, use_capper, lo, hi,
                      d_out);
   CMS_HIP(hipGetLastError());

@@ -7,6 +7,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -98,11 +99,25 @@ constexpr int kBuildThreads = CMS_BUILD_THREADS;
 
 }  // namespace cms
 
+namespace cms {
+// Scratch of one concurrent query (similarity / point query / estimate): its
+// own stream and buffers, taken from the handle's pool for the call.
+struct QueryCtx {
+  hipStream_t stream = nullptr;
+  DevBuf q, o, r, x;
+};
+}  // namespace cms
+
 struct cms_handle {
   cms_params p{};
   int device = 0;
   hipStream_t stream = nullptr;
-  std::mutex mu;
+  // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
+  // the point queries after cms_finalize hold it shared and run concurrently,
+  // each on a QueryCtx of its own (the table and norms are read-only then).
+  std::shared_mutex mu;
+  std::mutex pool_mu;
+  std::vector<cms::QueryCtx*> qpool;
 
   int64_t a[CMS_MAX_DEPTH] = {};  // HashFunctionBuilder parameters as drawn
   int64_t b[CMS_MAX_DEPTH] = {};
@@ -221,7 +236,7 @@ struct TimedScope {
   cms_handle* h;
   hipEvent_t start = nullptr;
   const char* name;
-  TimedScope(cms_handle* hh, const char* nm);
+  TimedScope(cms_handle* hh, const char* nm, bool on = true);
   ~TimedScope();
 };
 
@@ -276,10 +291,14 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
                      int32_t* out_rows = nullptr);
 
 // ---- launchers (cms_query.hip) ----
-int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);
-int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+// s: the stream to launch on (null = the handle's stream; a query context's
+// stream is never timed)
+int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out,
+                 hipStream_t s = nullptr);
+int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s = nullptr);
 int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
-                         const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out);
+                         const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
+                         hipStream_t s = nullptr);
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts);
 // exact top-k (slab path) of the owners at PERMUTED positions pos, written at out_pos
@@ -320,14 +339,19 @@ int po_load_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const
                 const int64_t* h_off);
 int po_finalize(cms_handle* h);
 // similarities of (qrows[i / m], crows[i % m]) into out[i] (crows null: identity)
-int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m, double* d_out);
-int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m, double* d_out,
+                    hipStream_t s = nullptr);
+int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out,
+                     hipStream_t s = nullptr);
 int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
-                            const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out);
+                            const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
+                            hipStream_t s = nullptr);
 int po_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                   int32_t* d_counts);
 // shape check of every owner in rows (all owners when rows is null)
 int po_require_shapes(cms_handle* h, const int64_t* rows, int64_t m);
+// the per-owner pair kernel needs the handle's global scratch (fp64, or widths past LDS)
+bool po_shared_scratch(cms_handle* h);
 // ---- cms_topk.hip (shared by both modes) ----
 struct TopQuery {
   int64_t slab_row;  // row of the slab holding this query's similarities
@@ -344,18 +368,18 @@ int f64_ingest_coo_host(cms_handle* h, const int64_t* owner, const int64_t* key,
 int po_f64_load(cms_handle* h, const int64_t* d_key, const float* d_val, int64_t npairs);
 int po_f64_finalize(cms_handle* h, int64_t total_counters, int64_t total_rows);
 int po_f64_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m,
-                        double* d_out);
-int po_f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+                        double* d_out, hipStream_t s);
+int po_f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s);
 int po_f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims,
                                 int64_t m, const int64_t* d_items, int64_t q, int use_capper, float lo, float hi,
-                                float* d_out);
+                                float* d_out, hipStream_t s);
 int f64_norms(cms_handle* h);
-int f64_pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out);
+int f64_pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out, hipStream_t s);
 int f64_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_slab);
-int f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out);
+int f64_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s);
 int f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims,
                              int64_t m, const int64_t* d_items, int64_t q, int use_capper, float lo, float hi,
-                             float* d_out);
+                             float* d_out, hipStream_t s);
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);

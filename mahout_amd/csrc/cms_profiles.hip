@@ -393,6 +393,8 @@ static int po_set_config(cms_handle* h, const double* delta, const double* eps) 
   return CMS_OK;
 }
 
+bool po_shared_scratch(cms_handle* h) { return h->per_owner && (h->f64 || h->po_max_w > kPoHist); }
+
 int po_require_shapes(cms_handle* h, const int64_t* rows, int64_t m) {
   const int64_t cnt = rows ? m : h->n;
   for (int64_t i = 0; i < cnt; ++i) {
@@ -445,9 +447,9 @@ int po_finalize(cms_handle* h) {
 }
 
 int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int64_t* d_crows, int64_t m,
-                    double* d_out) {
+                    double* d_out, hipStream_t s) {
   if (nq <= 0 || m <= 0) return CMS_OK;
-  if (h->f64) return po_f64_pair_cosines(h, d_qrows, nq, d_crows, m, d_out);
+  if (h->f64) return po_f64_pair_cosines(h, d_qrows, nq, d_crows, m, d_out, s);
   PoPairArgs a;
   a.off = h->po_off.as<int64_t>();
   a.kp = h->po_kp.as<uint64_t>();
@@ -465,27 +467,29 @@ int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int
   a.scratch_w = wide ? h->po_max_w : 0;
   a.out = d_out;
   a.weighted = h->p.weighting == CMS_WEIGHTED;
-  TimedScope ts(h, "po_pair_cosine");
+  TimedScope ts(h, "po_pair_cosine", s == nullptr);
   hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(nq * m, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
-                     h->stream, a, h->hp);
+                     s ? s : h->stream, a, h->hp);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
-int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
+int po_point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s) {
   if (m <= 0) return CMS_OK;
-  if (h->f64) return po_f64_point_queries(h, row, d_keys, m, d_out);
-  hipLaunchKernelGGL(k_po_point, dim3(grid_for((m + 255) / 256, 4096)), dim3(256), 0, h->stream,
+  if (h->f64) return po_f64_point_queries(h, row, d_keys, m, d_out, s);
+  hipLaunchKernelGGL(k_po_point, dim3(grid_for((m + 255) / 256, 4096)), dim3(256), 0, s ? s : h->stream,
                      h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->hp, row, d_keys, m, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
 int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
-                            const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out) {
+                            const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
+                            hipStream_t s) {
   if (q <= 0) return CMS_OK;
-  if (h->f64) return po_f64_estimate_preferences(h, user_row, d_nb_rows, d_sims, m, d_items, q, use_capper, lo, hi, d_out);
-  hipLaunchKernelGGL(k_po_estimate, dim3(grid_for((q + 255) / 256, 4096)), dim3(256), 0, h->stream,
+  if (h->f64)
+    return po_f64_estimate_preferences(h, user_row, d_nb_rows, d_sims, m, d_items, q, use_capper, lo, hi, d_out, s);
+  hipLaunchKernelGGL(k_po_estimate, dim3(grid_for((q + 255) / 256, 4096)), dim3(256), 0, s ? s : h->stream,
                      h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->hp, user_row, d_nb_rows, d_sims, m,
                      d_items, q, use_capper, lo, hi, d_out);
   CMS_HIP(hipGetLastError());
@@ -530,7 +534,7 @@ int cms_configure_owner_shapes(cms_handle* h, double q, int64_t num_keys) {
   if (!h) return set_error(CMS_E_PARAM, "null handle");
   if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: shapes come from cms_params");
   if (num_keys < 0 || num_keys > 0x7fffffff) return set_error(CMS_E_PARAM, "num_keys must be an int (getNumItems)");
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::shared_mutex> g(h->mu);
   (void)hipSetDevice(h->device);
   if (!h->po_loaded) return set_error(CMS_E_STATE, "per-owner mode: ingest the DataModel (CSR) first");
   const int64_t n = h->n;
@@ -564,7 +568,7 @@ int cms_configure_owner_shapes(cms_handle* h, double q, int64_t num_keys) {
 int cms_set_owner_delta_epsilon(cms_handle* h, const double* delta, const double* epsilon) {
   if (!h || !delta || !epsilon) return set_error(CMS_E_PARAM, "null argument");
   if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: shapes come from cms_params");
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::shared_mutex> g(h->mu);
   (void)hipSetDevice(h->device);
   return po_set_config(h, delta, epsilon);
 }
@@ -572,7 +576,7 @@ int cms_set_owner_delta_epsilon(cms_handle* h, const double* delta, const double
 int cms_get_owner_shapes(cms_handle* h, double* delta, double* epsilon, int32_t* width, int32_t* depth) {
   if (!h) return set_error(CMS_E_PARAM, "null handle");
   if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: shapes come from cms_params");
-  std::lock_guard<std::mutex> g(h->mu);
+  std::lock_guard<std::shared_mutex> g(h->mu);
   if (!h->po_configured)
     return set_error(CMS_E_STATE, "delta is null, call configure method first (cms_configure_owner_shapes)");
   const size_t n = (size_t)h->n;

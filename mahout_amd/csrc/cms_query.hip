@@ -92,11 +92,11 @@ __global__ __launch_bounds__(256) void k_pair_cosine(TableView tv, const uint64_
   }
 }
 
-int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out) {
+int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out, hipStream_t s) {
   if (m <= 0) return CMS_OK;
-  if (h->f64) return f64_pair_cosines(h, q_row, d_rows, m, d_out);
-  TimedScope ts(h, "pair_cosine");
-  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), 0, h->stream, h->tview(), h->d_norm,
+  if (h->f64) return f64_pair_cosines(h, q_row, d_rows, m, d_out, s);
+  TimedScope ts(h, "pair_cosine", s == nullptr);
+  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), 0, s ? s : h->stream, h->tview(), h->d_norm,
                      h->d_norm_sqrt, h->hp, q_row, d_rows, m, h->n, (int)h->p.weighting, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
@@ -161,21 +161,23 @@ __global__ void k_estimate(TableView tv, HashParams hp, int64_t user_row, const 
 }
 
 int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
-                         const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out) {
+                         const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
+                         hipStream_t s) {
   if (q <= 0) return CMS_OK;
-  if (h->f64) return f64_estimate_preferences(h, user_row, d_nb_rows, d_sims, m, d_items, q, use_capper, lo, hi, d_out);
+  if (h->f64)
+    return f64_estimate_preferences(h, user_row, d_nb_rows, d_sims, m, d_items, q, use_capper, lo, hi, d_out, s);
   unsigned grid = (unsigned)std::min<int64_t>((q + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_estimate, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->hp, user_row, d_nb_rows, d_sims,
+  hipLaunchKernelGGL(k_estimate, dim3(grid), dim3(256), 0, s ? s : h->stream, h->tview(), h->hp, user_row, d_nb_rows, d_sims,
                      m, d_items, q, use_capper, lo, hi, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
-int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out) {
+int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s) {
   if (m <= 0) return CMS_OK;
-  if (h->f64) return f64_point_queries(h, row, d_keys, m, d_out);
+  if (h->f64) return f64_point_queries(h, row, d_keys, m, d_out, s);
   unsigned grid = (unsigned)std::min<int64_t>((m + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_point_query, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->hp, row, d_keys, m, d_out);
+  hipLaunchKernelGGL(k_point_query, dim3(grid), dim3(256), 0, s ? s : h->stream, h->tview(), h->hp, row, d_keys, m, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
