@@ -41,13 +41,13 @@ constexpr int kKeyRegs = CMS_KEY_REGS;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // keys cached per thread: owners up to 1024 keys are read once
 
-__global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
+__global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
                              int2* extra_map, uint32_t* counters /* [0]=hot rows [1]=extra slices */,
                              uint64_t* norm, uint32_t* rowmax, int depth) {
   const int lane = (int)__lane_id();
   for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nrows; base += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = base + threadIdx.x;
-    const int64_t c = r < nrows ? off[r + 1] - off[r] : 0;
+    const int64_t c = r < nrows ? hi_[r] - lo_[r] : 0;
     const bool is_hot = c > slice;
     if (r < nrows && !is_hot) row_hot[r] = -1;
     int32_t ns = 0;
@@ -82,29 +82,29 @@ __global__ void k_build_plan(const int64_t* off, int64_t nrows, int64_t slice, i
 // mass in counter units, old mass included when accumulating), and the rows
 // whose keys are split over several workgroups (their slices add with u32
 // atomics): both need a hot slot before the launch.
-__global__ void k_row_bound_implicit(const int64_t* off, int64_t nrows, int fb, int64_t slice, const uint64_t* old_mass,
+__global__ void k_row_bound_implicit(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int fb, int64_t slice, const uint64_t* old_mass,
                                      uint64_t* bound, uint8_t* force) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = off[r + 1] - off[r];
+    const int64_t c = hi_[r] - lo_[r];
     bound[r] = ((uint64_t)c << fb) + (old_mass ? old_mass[r] : 0ULL);
     force[r] = c > slice ? 1 : 0;
   }
 }
 
-__global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* off, const float* vals, int64_t nrows, int fb,
+__global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* lo_, const int64_t* hi_, const float* vals, int64_t nrows, int fb,
                                                           int64_t slice, const uint64_t* old_mass, uint64_t* bound,
                                                           uint8_t* force) {
   __shared__ uint64_t red[4];
   for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
     uint64_t s = 0;
-    for (int64_t i = off[r] + threadIdx.x; i < off[r + 1]; i += 256) {
+    for (int64_t i = lo_[r] + threadIdx.x; i < hi_[r]; i += 256) {
       uint32_t inc;
       if (load_inc(vals, i, inc, fb)) s += inc;  // bad values are flagged by the build itself
     }
     s = block_sum_u64_sat(s, red);
     if (threadIdx.x == 0) {
       bound[r] = sat_add(s, old_mass ? old_mass[r] : 0ULL);
-      force[r] = (off[r + 1] - off[r]) > slice ? 1 : 0;
+      force[r] = (hi_[r] - lo_[r]) > slice ? 1 : 0;
     }
   }
 }
@@ -112,7 +112,8 @@ __global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* off, co
 // grid = emax + nrows: blocks [0, emax) build extra slices of hot owners (heavy
 // work first), blocks [emax, emax + nrows) one owner each (slice 0 if hot).
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_rows(
-    const int64_t* off, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp, int64_t slice,
+    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
+    int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
     TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w]
@@ -132,14 +133,14 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
 #endif
     int2 m = extra_map[blockIdx.x];
     row = hot[m.x].row;
-    lo = off[row] + (int64_t)m.y * slice;
-    hi = min(off[row + 1], lo + slice);
+    lo = lo_[row] + (int64_t)m.y * slice;
+    hi = min(hi_[row], lo + slice);
     atomic_mode = true;
   } else {
     row = (int64_t)blockIdx.x - emax;
-    lo = off[row];
+    lo = lo_[row];
     atomic_mode = row_hot[row] >= 0;
-    hi = atomic_mode ? lo + slice : off[row + 1];
+    hi = atomic_mode ? lo + slice : hi_[row];
   }
 #ifdef CMS_BUILD_NOKEYS  // bound analysis only: the write path alone
   hi = lo;
@@ -394,20 +395,25 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
   }
 }
 
-int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,
-               uint64_t* bound, uint8_t* force) {
+int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,
+               int64_t slice, uint64_t* bound, uint8_t* force) {
   const int64_t n = h->n;
   if (d_val)
     hipLaunchKernelGGL(k_row_bound_values, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(n, 65536))),
-                       dim3(256), 0, h->stream, d_off, d_val, n, h->hp.frac_bits, slice, old_mass, bound, force);
+                       dim3(256), 0, h->stream, d_lo, d_hi, d_val, n, h->hp.frac_bits, slice, old_mass, bound, force);
   else
     hipLaunchKernelGGL(k_row_bound_implicit, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))),
-                       dim3(256), 0, h->stream, d_off, n, h->hp.frac_bits, slice, old_mass, bound, force);
+                       dim3(256), 0, h->stream, d_lo, d_hi, n, h->hp.frac_bits, slice, old_mass, bound, force);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
 int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs) {
+  return ingest_spans_device(h, d_off, d_off + 1, d_key, d_val, npairs);
+}
+
+int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const int64_t* d_key, const float* d_val,
+                        int64_t npairs) {
   const int64_t n = h->n;
   int rc0;
   const int accumulate = h->empty ? 0 : 1;
@@ -431,7 +437,7 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
     DevBuf& force = h->ws_force;
     CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1)));
     CMS_HIP(force.ensure((size_t)std::max<int64_t>(n, 1)));
-    if ((rc0 = row_bounds(h, d_off, d_val, accumulate ? h->d_row_mass : nullptr, kSlice, bound.as<uint64_t>(),
+    if ((rc0 = row_bounds(h, d_lo, d_hi, d_val, accumulate ? h->d_row_mass : nullptr, kSlice, bound.as<uint64_t>(),
                           force.as<uint8_t>())))
       return rc0;
     // A fresh build with implicit (unit) increments: a row needs a slot when
@@ -453,14 +459,14 @@ int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key,
   {
     TimedScope ts(h, "build_plan");
     unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-    hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_off, n, kSlice, row_hot, hot, extra_map,
+    hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_lo, d_hi, n, kSlice, row_hot, hot, extra_map,
                        counters, h->d_norm, h->d_rowmax, h->p.depth);
     CMS_HIP(hipGetLastError());
   }
   const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
   {
     TimedScope ts(h, "build_rows");
-    hipLaunchKernelGGL(k_build_rows, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_off, d_key,
+    hipLaunchKernelGGL(k_build_rows, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                        d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
                        h->d_norm, h->d_rowmax, h->d_flags, accumulate);
     CMS_HIP(hipGetLastError());

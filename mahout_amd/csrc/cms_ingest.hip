@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "cms_device.h"
 #include "cms_internal.h"
@@ -419,7 +420,8 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
         DevBuf& force = h->ws_force;
         CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)n));
         CMS_HIP(force.ensure((size_t)n));
-        if ((rc = row_bounds(h, coff, cval, h->d_row_mass, INT64_MAX, bound.as<uint64_t>(), force.as<uint8_t>())))
+        if ((rc = row_bounds(h, coff, coff + 1, cval, h->d_row_mass, INT64_MAX, bound.as<uint64_t>(),
+                             force.as<uint8_t>())))
           return rc;
         if ((rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true))) return rc;
       }
@@ -468,12 +470,16 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
   }
 
   // ---- group by owner (cms_partition.hip), then the LDS row build ----
-  int64_t* coff;
-  int64_t* ckey;
+  int64_t *clo, *chi, *ckey;
   float* cval;
-  int rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &coff, &ckey, &cval);
+  int rc = kNoSpans;
+  if (!getenv("CMS_NO_HOT_ROUTING")) rc = partition_to_spans(h, d_row, d_key, d_val, npairs, &clo, &chi, &ckey, &cval);
+  if (rc == kNoSpans) {
+    rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &clo, &ckey, &cval);
+    chi = clo + 1;
+  }
   if (rc) return rc;
-  return ingest_csr_device(h, coff, ckey, cval, npairs);
+  return ingest_spans_device(h, clo, chi, ckey, cval, npairs);
 }
 
 }  // namespace cms

@@ -174,7 +174,8 @@ struct cms_handle {
   cms::DevBuf ws_in_row, ws_in_key, ws_in_val;   // host-ingest staging
   cms::DevBuf ws_p1_row, ws_p1_key, ws_p1_val;   // pass-1 partition output
   cms::DevBuf ws_mbnd, ws_mbits, ws_mwoff, ws_mpacked;  // packed multi-rank merge (bounds, layout, words)
-  cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off;
+  cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off, ws_csr_hi;
+  cms::DevBuf ws_hotpart;  // hot-owner routing of the partition: slot keys [1024] u64, sample counts [n] u32
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_query, ws_out, ws_srow, ws_f4;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
@@ -245,6 +246,10 @@ struct TimedScope {
 int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t n);
 // CSR (offsets int64 [n+1]) -> table.
 int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs);
+// owner spans -> table: row r's keys are d_key[d_lo[r], d_hi[r]) (the spans
+// need not be in row order; a CSR is d_lo = off, d_hi = off + 1).
+int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const int64_t* d_key, const float* d_val,
+                        int64_t npairs);
 // owner IDs -> rows by binary search over h->d_owner_ids.
 int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_rows);
 int compute_norms(cms_handle* h);
@@ -261,8 +266,8 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 int count_hot_rows(cms_handle* h, int64_t* out);
 // per-row counter bounds after a CSR batch (mass in counter units + old_mass)
 // and the rows split over more than `slice` keys (cms_build.hip)
-int row_bounds(cms_handle* h, const int64_t* d_off, const float* d_val, const uint64_t* old_mass, int64_t slice,
-               uint64_t* bound, uint8_t* force);
+int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,
+               int64_t slice, uint64_t* bound, uint8_t* force);
 // counters of rows [r0, r0 + rc) as u32 into a device buffer (stream-ordered)
 int read_counters_device(cms_handle* h, int64_t r0, int64_t rc, uint32_t* d_out);
 // all rows narrow and zero-able again (empty table)
@@ -289,6 +294,12 @@ int scan_exclusive_u32(cms_handle* h, const uint32_t* in, uint32_t* out, int64_t
 int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
                      int64_t** out_off, int64_t** out_key, float** out_val,
                      int32_t* out_rows = nullptr);
+// COO -> owner spans with the hottest owners routed straight to their final
+// place by pass 1 (only the other pairs take pass 2).  Returns kNoSpans when
+// the shape does not allow it (the caller then uses partition_to_csr).
+constexpr int kNoSpans = 1;
+int partition_to_spans(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
+                       int64_t** out_lo, int64_t** out_hi, int64_t** out_key, float** out_val);
 
 // ---- launchers (cms_query.hip) ----
 // s: the stream to launch on (null = the handle's stream; a query context's

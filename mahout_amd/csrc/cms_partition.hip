@@ -97,10 +97,82 @@ __device__ __forceinline__ uint32_t lds_bin_add(uint32_t* hist, uint32_t bin, bo
   return rank;
 }
 
+// ---- hot-owner routing (partition_to_spans) ----
+// A Zipf stream puts most pairs on a few owners (config 2: the top ~1000 of
+// 100K items hold ~3/4 of the pairs).  Those owners get bins of their own in
+// pass 1, so their keys land at their final place at once and only the other
+// pairs take pass 2.  The hot set comes from a strided sample: every owner
+// with >= tau sample hits bids for slot hslot(owner) of a kHotBins-entry
+// table, the one with the most hits wins (ties: larger owner; an owner that
+// loses its slot simply stays on the two-pass path -- correctness never
+// depends on who is hot).
+constexpr int kHotBins = 1024;
+__device__ __forceinline__ uint32_t hslot(int64_t o) {
+  return (uint32_t)(((uint64_t)o * 0x9E3779B97F4A7C15ULL) >> 54);  // top 10 bits
+}
+
+// Sample counts: each block counts its share of the strided sample in an LDS
+// hash table first (a Zipf head owner takes a good part of every block's
+// samples, and same-address global atomics serialise at the memory side),
+// then adds each owner's block count with one global atomic.
+constexpr int kSampleTab = 4096;  // LDS entries (owner + 1, count)
+constexpr int kSamplePerBlock = 4096;
+__global__ __launch_bounds__(256) void k_hot_sample(const int64_t* row, int64_t stride, int64_t S, int64_t nrows,
+                                                    uint32_t* cnt) {
+  __shared__ uint32_t tkey[kSampleTab], tcnt[kSampleTab];
+  for (int i = threadIdx.x; i < kSampleTab; i += blockDim.x) tkey[i] = tcnt[i] = 0u;
+  __syncthreads();
+  const int64_t s0 = (int64_t)blockIdx.x * kSamplePerBlock, s1 = min(S, s0 + kSamplePerBlock);
+  for (int64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
+    const int64_t r = row[i * stride];
+    if (r < 0 || r >= nrows) continue;
+    const uint32_t k = (uint32_t)r + 1u;
+    uint32_t slot = (uint32_t)(((uint64_t)r * 0x9E3779B97F4A7C15ULL) >> 52) & (kSampleTab - 1);
+    bool done = false;
+    for (int probe = 0; probe < 32 && !done; ++probe) {
+      const uint32_t old = atomicCAS(&tkey[slot], 0u, k);
+      if (old == 0u || old == k) {
+        atomicAdd(&tcnt[slot], 1u);
+        done = true;
+      }
+      slot = (slot + 1) & (kSampleTab - 1);
+    }
+    if (!done) atomicAdd(&cnt[r], 1u);  // table crowded: count directly
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSampleTab; i += blockDim.x)
+    if (tkey[i]) atomicAdd(&cnt[tkey[i] - 1u], tcnt[i]);
+}
+
+__global__ __launch_bounds__(256) void k_hot_claim(const uint32_t* cnt, int64_t nrows, uint32_t tau,
+                                                   unsigned long long* slotkey) {
+  for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < nrows; o += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = cnt[o];
+    if (c >= tau) atomicMax(&slotkey[hslot(o)], ((unsigned long long)c << 32) | (unsigned long long)(o + 1));
+  }
+}
+
+// LDS copy of the hot table (owner + 1 per slot, 0 = empty); bin of a row:
+// its hot bin P1 + slot, else its coarse bin.
+__device__ __forceinline__ void load_hot_table(const unsigned long long* slotkey, uint32_t* tab) {
+  for (int t = threadIdx.x; t < kHotBins; t += blockDim.x) tab[t] = (uint32_t)slotkey[t];
+}
+__device__ __forceinline__ uint32_t bin_of(uint32_t r, int s2, int P1, const uint32_t* tab) {
+  if (tab) {
+    const uint32_t t = hslot(r);
+    if (tab[t] == r + 1u) return (uint32_t)P1 + t;
+  }
+  return r >> s2;
+}
+
 __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, int64_t chunk, int s2, int P1,
-                                                 int64_t nrows, uint32_t* H1, int NB, uint32_t* flags) {
+                                                 int64_t nrows, uint32_t* H1, int NB, uint32_t* flags,
+                                                 const unsigned long long* hotkey) {
   extern __shared__ uint32_t lh[];
-  for (int b = threadIdx.x; b < P1; b += blockDim.x) lh[b] = 0;
+  const int P = P1 + (hotkey ? kHotBins : 0);  // bins: coarse, then hot
+  uint32_t* tab = hotkey ? lh + P : nullptr;
+  for (int b = threadIdx.x; b < P; b += blockDim.x) lh[b] = 0;
+  if (tab) load_hot_table(hotkey, tab);
   __syncthreads();
   int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   bool bad = false;
@@ -109,13 +181,16 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
   if (lo2 > lo && threadIdx.x == 0 && lo < hi) {
     int64_t r = row[lo];
     if (r < 0 || r >= nrows) bad = true;
-    else atomicAdd(&lh[(uint32_t)(r >> s2)], 1u);
+    else atomicAdd(&lh[bin_of((uint32_t)r, s2, P1, tab)], 1u);
   }
   const int64_t npair = (hi - lo2) / 2;
   const longlong2* r2 = reinterpret_cast<const longlong2*>(row + lo2);
   // whole waves step together so the aggregated increments see converged
-  // lanes; four 16-byte loads in flight per lane
-  constexpr int kU = 4;
+  // lanes; CMS_P1H_U 16-byte loads in flight per lane
+#ifndef CMS_P1H_U
+#define CMS_P1H_U 4
+#endif
+  constexpr int kU = CMS_P1H_U;
   const int64_t span = (int64_t)blockDim.x * kU;
   const int64_t nstep = (npair + span - 1) / span * span;
   for (int64_t i0 = threadIdx.x; i0 < nstep; i0 += span) {
@@ -130,18 +205,18 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
       const bool in = i0 + (int64_t)u * blockDim.x < npair;
       const bool okx = v[u].x >= 0 && v[u].x < nrows, oky = v[u].y >= 0 && v[u].y < nrows;
       if (in && (!okx || !oky)) bad = true;
-      lds_bin_add<CMS_PEEL_P1H, false>(lh, okx ? (uint32_t)(v[u].x >> s2) : 0u, okx);
-      lds_bin_add<CMS_PEEL_P1H, false>(lh, oky ? (uint32_t)(v[u].y >> s2) : 0u, oky);
+      lds_bin_add<CMS_PEEL_P1H, false>(lh, okx ? bin_of((uint32_t)v[u].x, s2, P1, tab) : 0u, okx);
+      lds_bin_add<CMS_PEEL_P1H, false>(lh, oky ? bin_of((uint32_t)v[u].y, s2, P1, tab) : 0u, oky);
     }
   }
   if (threadIdx.x == 0 && lo2 + 2 * npair < hi) {
     int64_t r = row[hi - 1];
     if (r < 0 || r >= nrows) bad = true;
-    else atomicAdd(&lh[(uint32_t)(r >> s2)], 1u);
+    else atomicAdd(&lh[bin_of((uint32_t)r, s2, P1, tab)], 1u);
   }
   if (bad) atomicOr(flags, kFlagBadRow);
   __syncthreads();
-  for (int b = threadIdx.x; b < P1; b += blockDim.x) H1[(int64_t)b * NB + blockIdx.x] = lh[b];
+  for (int b = threadIdx.x; b < P; b += blockDim.x) H1[(int64_t)blockIdx.x * P + b] = lh[b];  // block-major, coalesced
 }
 
 // Exclusive scan of hist[0..P) into off[] by the whole block (P <= 4096).
@@ -190,23 +265,31 @@ __device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_va
   return t;
 }
 
-static size_t tile_lds_bytes(int P, bool has_val, bool has_fine) {
-  return (size_t)kPartTile * (8 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4;
+static size_t tile_lds_bytes(int P, bool has_val, bool has_fine, bool hot = false) {
+  return (size_t)kPartTile * (8 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4 +
+         (hot ? sizeof(uint32_t) * kHotBins : 0);
 }
 
 // Pass 1: block b owns stream chunk [b*chunk, (b+1)*chunk); output region of
 // (coarse bin, block) starts at O1[bin*NB + b].
+// With hotkey: bins [P1, P1 + kHotBins) are hot owners, whose keys (and
+// values) go straight to okey_hot / oval_hot -- their final place.
 __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row, const int64_t* key, const float* val,
                                                              int64_t n, int64_t chunk, int s2, int P1, int64_t nrows,
                                                              const uint32_t* O1, int NB, uint16_t* ofine,
-                                                             int64_t* okey, float* oval) {
+                                                             int64_t* okey, float* oval,
+                                                             const unsigned long long* hotkey, int64_t* okey_hot,
+                                                             float* oval_hot) {
   extern __shared__ __align__(16) unsigned char smem[];
-  TileLds L = carve(smem, P1, val != nullptr, true);
+  const int P = P1 + (hotkey ? kHotBins : 0);
+  TileLds L = carve(smem, P, val != nullptr, true);
+  uint32_t* tab = hotkey ? L.scr + 64 : nullptr;
   const int tid = threadIdx.x;
-  for (int b = tid; b < P1; b += kPartThreads) L.cursor[b] = O1[(int64_t)b * NB + blockIdx.x];
+  if (tab) load_hot_table(hotkey, tab);
+  for (int b = tid; b < P; b += kPartThreads) L.cursor[b] = O1[(int64_t)blockIdx.x * P + b];
   const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   const uint32_t fmask = (1u << s2) - 1u;
-  for (int b = tid; b < P1; b += kPartThreads) L.hist[b] = 0;
+  for (int b = tid; b < P; b += kPartThreads) L.hist[b] = 0;
   // software pipeline: the next tile's loads are issued before this tile's
   // write-out and stay in flight across the LDS-only barriers
   int64_t rr[kPartPer], kk[kPartPer];
@@ -229,21 +312,22 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
 #if !CMS_P1_PREFETCH
     if (tb != lo) load(tb);
 #endif
-    uint32_t bb[kPartPer], rk[kPartPer];
+    uint32_t bb[kPartPer], bn[kPartPer], rk[kPartPer];
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
       const bool ok = rr[u] >= 0 && rr[u] < nrows;
       bb[u] = ok ? (uint32_t)rr[u] : 0u;
-      const uint32_t q = lds_bin_add<CMS_PEEL_P1S, true>(L.hist, bb[u] >> s2, ok);
+      bn[u] = ok ? bin_of(bb[u], s2, P1, tab) : 0u;
+      const uint32_t q = lds_bin_add<CMS_PEEL_P1S, true>(L.hist, bn[u], ok);
       rk[u] = ok ? q : 0xFFFFFFFFu;
     }
     lds_barrier();
-    const uint32_t cnt = scan_bins(L.hist, L.off, P1, L.scr);
+    const uint32_t cnt = scan_bins(L.hist, L.off, P, L.scr);
     lds_barrier();
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
       if (rk[u] != 0xFFFFFFFFu) {
-        uint32_t bin = bb[u] >> s2;
+        const uint32_t bin = bn[u];
         uint32_t p = L.off[bin] + rk[u];
         L.key[p] = kk[u];
         if (val) L.val[p] = vv[u];
@@ -264,12 +348,17 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
 #ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
       if (g != 0xFFFFFFFFu) continue;
 #endif
+      if ((int)bin >= P1) {  // hot owner: final place
+        okey_hot[g] = L.key[i];
+        if (oval) oval_hot[g] = L.val[i];
+        continue;
+      }
       okey[g] = L.key[i];
       ofine[g] = L.fine[i];
       if (oval) oval[g] = L.val[i];
     }
     lds_barrier();
-    for (int b = tid; b < P1; b += kPartThreads) {
+    for (int b = tid; b < P; b += kPartThreads) {
       L.cursor[b] += L.hist[b];
       L.hist[b] = 0;
     }
@@ -277,32 +366,28 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
   }
 }
 
-// binStart[b] = O1[b*NB] (exclusive, bin-major), binStart[P1] = total;
-// blkStart = exclusive scan of ceil(size_b / CH2).  One block.
-__global__ __launch_bounds__(1024) void k_p2_plan(const uint32_t* O1, const uint32_t* H1, int NB, int P1,
-                                                  int64_t CH2, uint32_t* binStart, uint32_t* blkStart) {
+// bs1[b] = first position of pass-1 bin b (b <= P1: bs1[P1] = end of the
+// coarse bins); binStart = bs1[0..P1], blkStart = exclusive scan of
+// ceil(size_b / CH2).  One block.
+__global__ __launch_bounds__(1024) void k_p2_plan(const uint32_t* bs1, int P1, int64_t CH2, uint32_t* binStart,
+                                                  uint32_t* blkStart) {
   __shared__ uint32_t sc[1024 / 64 + 1];
-  const uint32_t total = O1[(int64_t)(P1 - 1) * NB + NB - 1] + H1[(int64_t)(P1 - 1) * NB + NB - 1];
   int per = (P1 + 1023) / 1024;
   int lo = threadIdx.x * per, hi = min(P1, lo + per);
   uint32_t s = 0;
   for (int b = lo; b < hi; ++b) {
-    uint32_t start = O1[(int64_t)b * NB];
-    uint32_t end = (b + 1 < P1) ? O1[(int64_t)(b + 1) * NB] : total;
-    binStart[b] = start;
-    s += (uint32_t)((end - start + CH2 - 1) / CH2);
+    binStart[b] = bs1[b];
+    s += (uint32_t)((bs1[b + 1] - bs1[b] + CH2 - 1) / CH2);
   }
   uint32_t tot;
   uint32_t off = block_excl_scan_u32(s, sc, &tot);
   for (int b = lo; b < hi; ++b) {
-    uint32_t start = O1[(int64_t)b * NB];
-    uint32_t end = (b + 1 < P1) ? O1[(int64_t)(b + 1) * NB] : total;
     blkStart[b] = off;
-    off += (uint32_t)((end - start + CH2 - 1) / CH2);
+    off += (uint32_t)((bs1[b + 1] - bs1[b] + CH2 - 1) / CH2);
   }
   if (threadIdx.x == 0) {
     blkStart[P1] = tot;
-    binStart[P1] = total;
+    binStart[P1] = bs1[P1];
   }
 }
 
@@ -418,6 +503,45 @@ __global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* binStart, int 
   if (b == P1 - 1 && threadIdx.x == 0) row_start[nrows] = binStart[P1];
 }
 
+// Pass 1 has ONE segment of NB blocks over P bins: the bin totals' exclusive
+// scan gives bs1[0..P] (bs1[P] = every valid pair), and the chunk sums become
+// chunk prefixes for k_p2_offsets.  One block.
+__global__ __launch_bounds__(1024) void k_p1_scan(int P, uint32_t* PS, uint32_t* bs1) {
+  __shared__ uint32_t sc[1024 / 64 + 1];
+  __shared__ uint32_t tots[kMaxBins];
+  for (int f = threadIdx.x; f < P; f += blockDim.x) {
+    uint32_t T = 0;
+#pragma unroll
+    for (int c = 0; c < kP2Split; ++c) T += PS[(int64_t)c * P + f];
+    tots[f] = T;
+  }
+  __syncthreads();
+  const int per = (P + 1023) / 1024;
+  const int f0 = threadIdx.x * per, f1 = min(P, f0 + per);
+  uint32_t s = 0;
+  for (int f = f0; f < f1; ++f) s += tots[f];
+  uint32_t total;
+  uint32_t ex = block_excl_scan_u32(s, sc, &total);
+  for (int f = f0; f < f1; ++f) {
+    uint32_t t = tots[f];
+    tots[f] = ex;
+    ex += t;
+  }
+  __syncthreads();
+  for (int f = threadIdx.x; f < P; f += blockDim.x) {
+    const uint32_t base = tots[f];
+    bs1[f] = base;
+    uint32_t run = base;
+#pragma unroll
+    for (int c = 0; c < kP2Split; ++c) {
+      const uint32_t t = PS[(int64_t)c * P + f];
+      PS[(int64_t)c * P + f] = run;
+      run += t;
+    }
+  }
+  if (threadIdx.x == 0) bs1[P] = total;
+}
+
 __global__ __launch_bounds__(1024) void k_p2_offsets(const uint32_t* H2, const uint32_t* blkStart, int P2,
                                                      const uint32_t* PS, uint32_t* O2) {
   const int b = blockIdx.x / kP2Split, c = blockIdx.x % kP2Split;
@@ -531,8 +655,24 @@ static int ceil_log2(int64_t v) {
   return b;
 }
 
-int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                     int64_t** out_off, int64_t** out_key, float** out_val, int32_t* out_rows) {
+// Spans of the hot owners (their bins of pass 1) and the end of every other
+// owner's CSR range; hot owners have empty ranges in the two-pass CSR.
+__global__ void k_spans_hi(const int64_t* coff, int64_t nrows, int64_t* hi) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
+    hi[r] = coff[r + 1];
+}
+__global__ void k_spans_hot(const unsigned long long* slotkey, const uint32_t* bs1, int P1, int64_t* lo, int64_t* hi) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= kHotBins) return;
+  const uint32_t o1 = (uint32_t)slotkey[t];
+  if (o1 == 0) return;
+  lo[o1 - 1] = bs1[P1 + t];
+  hi[o1 - 1] = bs1[P1 + t + 1];
+}
+
+static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
+                          bool hot, int64_t** out_lo, int64_t** out_hi, int64_t** out_key, float** out_val,
+                          int32_t* out_rows) {
   const int64_t n = h->n;
   const int B = std::max(1, ceil_log2(n));
   int s2 = std::min(B, CMS_PART_S2);
@@ -541,6 +681,8 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
   const int P1 = (int)((n + P2 - 1) / P2);
   if (P1 > kMaxBins || P2 > kMaxBins)
     return set_error(CMS_E_PARAM, "num_owners %lld too large for the partition", (long long)n);
+  if (hot && (P1 + kHotBins > kMaxBins || out_rows || n >= (int64_t(1) << 31))) return kNoSpans;
+  const int P = P1 + (hot ? kHotBins : 0);  // pass-1 bins
   const int64_t chunk1 = std::max<int64_t>(4 * kPartTile, (npairs + CMS_P1_BLOCKS - 1) / CMS_P1_BLOCKS);
   const int NB = (int)((npairs + chunk1 - 1) / chunk1);
   const int64_t CH2 = 4 * kPartTile;
@@ -552,18 +694,24 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
   CMS_HIP(h->ws_csr_key.ensure(sizeof(int64_t) * (size_t)npairs));
   if (d_val) CMS_HIP(h->ws_csr_val.ensure(sizeof(float) * (size_t)npairs));
   CMS_HIP(h->ws_csr_off.ensure(sizeof(int64_t) * (size_t)(n + 1)));
-  const int64_t L1 = (int64_t)P1 * NB, L2 = nb2max * P2;
-  const int64_t nbs = (L1 + 4095) / 4096 + 1;
-  const size_t hist_words = (size_t)(2 * L1 + 2 * L2 + nbs + 2 * (P1 + 1) + 64) + (size_t)P1 * kP2Split * P2;
+  if (hot) {
+    CMS_HIP(h->ws_csr_hi.ensure(sizeof(int64_t) * (size_t)n));
+    CMS_HIP(h->ws_hotpart.ensure(sizeof(unsigned long long) * kHotBins + sizeof(uint32_t) * (size_t)n));
+  }
+  const int64_t L1 = (int64_t)P * NB, L2 = nb2max * P2;
+  const size_t hist_words = (size_t)(2 * L1 + 2 * L2 + 2 * (P1 + 1) + 64) + (size_t)P1 * kP2Split * P2 +
+                            (size_t)kP2Split * P + (P + 1) + 2;
   CMS_HIP(h->ws_hist.ensure(sizeof(uint32_t) * hist_words));
   uint32_t* H1 = h->ws_hist.as<uint32_t>();
   uint32_t* O1 = H1 + L1;
   uint32_t* H2 = O1 + L1;
   uint32_t* O2 = H2 + L2;
-  uint32_t* bsum = O2 + L2;
-  uint32_t* binStart = bsum + nbs;
+  uint32_t* binStart = O2 + L2;
   uint32_t* blkStart = binStart + (P1 + 1);
   uint32_t* PS = blkStart + (P1 + 1) + 64;  // [P1][kP2Split][P2] chunk column sums / prefixes
+  uint32_t* PS1 = PS + (size_t)P1 * kP2Split * P2;  // [kP2Split][P] pass-1 chunk sums / prefixes
+  uint32_t* bs1 = PS1 + (size_t)kP2Split * P;     // [P + 1] pass-1 bin starts
+  uint32_t* seg1 = bs1 + (P + 1);                 // {0, NB}: pass 1 is one segment of NB blocks
 
   uint16_t* fine = h->ws_p1_row.as<uint16_t>();
   int64_t* key1 = h->ws_p1_key.as<int64_t>();
@@ -571,6 +719,7 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
   int64_t* ckey = h->ws_csr_key.as<int64_t>();
   float* cval = d_val ? h->ws_csr_val.as<float>() : nullptr;
   int64_t* coff = h->ws_csr_off.as<int64_t>();
+  unsigned long long* slotkey = hot ? h->ws_hotpart.as<unsigned long long>() : nullptr;
   static bool lds_attr = [] {
     (void)hipFuncSetAttribute((const void*)k_p1_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)k_p2_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -579,13 +728,33 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
   (void)lds_attr;
   {
     TimedScope ts(h, "partition");
-    hipLaunchKernelGGL(k_p1_hist, dim3(NB), dim3(256), sizeof(uint32_t) * P1, h->stream, d_row, npairs, chunk1, s2,
-                       P1, n, H1, NB, h->d_flags);
-    int rc = scan_exclusive_u32(h, H1, O1, L1, bsum);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_p1_scatter, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P1, d_val != nullptr, true), h->stream, d_row, d_key,
-                       d_val, npairs, chunk1, s2, P1, n, O1, NB, fine, key1, val1);
-    hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, O1, H1, NB, P1, CH2, binStart, blkStart);
+    if (hot) {
+      // strided sample of up to 2^18 pairs; an owner is a candidate when its
+      // hits predict >= kHotMinPairs pairs
+      constexpr int64_t kSample = int64_t(1) << 18, kHotMinPairs = 2048;
+      const int64_t S = std::min(npairs, kSample), stride = npairs / S;
+      const uint32_t tau = (uint32_t)std::max<int64_t>(2, (kHotMinPairs * S + npairs - 1) / npairs);
+      uint32_t* cnt = reinterpret_cast<uint32_t*>(slotkey + kHotBins);
+      CMS_HIP(hipMemsetAsync(slotkey, 0, sizeof(unsigned long long) * kHotBins + sizeof(uint32_t) * (size_t)n,
+                             h->stream));
+      hipLaunchKernelGGL(k_hot_sample, dim3((unsigned)((S + kSamplePerBlock - 1) / kSamplePerBlock)), dim3(256), 0,
+                         h->stream, d_row, stride, S, n, cnt);
+      hipLaunchKernelGGL(k_hot_claim, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                         h->stream, cnt, n, tau, slotkey);
+    }
+    hipLaunchKernelGGL(k_p1_hist, dim3(NB), dim3(256), sizeof(uint32_t) * (P + (hot ? kHotBins : 0)), h->stream, d_row,
+                       npairs, chunk1, s2, P1, n, H1, NB, h->d_flags, slotkey);
+    // block-major (block, bin) offsets: chunked column sums, one scan over
+    // the bins, chunk prefixes (the pass-2 kernels with one segment)
+    CMS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(seg1), 0, 1, h->stream));
+    CMS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(seg1 + 1), NB, 1, h->stream));
+    hipLaunchKernelGGL(k_p2_colsum, dim3(kP2Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1);
+    hipLaunchKernelGGL(k_p1_scan, dim3(1), dim3(1024), 0, h->stream, P, PS1, bs1);
+    hipLaunchKernelGGL(k_p2_offsets, dim3(kP2Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1, O1);
+    hipLaunchKernelGGL(k_p1_scatter, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P, d_val != nullptr, true, hot),
+                       h->stream, d_row, d_key, d_val, npairs, chunk1, s2, P1, n, O1, NB, fine, key1, val1, slotkey,
+                       ckey, cval);
+    hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, bs1, P1, CH2, binStart, blkStart);
     hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)nb2max), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,
                        binStart, blkStart, P1, CH2, P2, H2);
     hipLaunchKernelGGL(k_p2_colsum, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS);
@@ -593,12 +762,32 @@ int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, 
     hipLaunchKernelGGL(k_p2_offsets, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS, O2);
     hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2, d_val != nullptr, false), h->stream, fine,
                        key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
+    if (hot) {
+      int64_t* chi = h->ws_csr_hi.as<int64_t>();
+      hipLaunchKernelGGL(k_spans_hi, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
+                         h->stream, coff, n, chi);
+      hipLaunchKernelGGL(k_spans_hot, dim3(kHotBins / 256), dim3(256), 0, h->stream, slotkey, bs1, P1, coff, chi);
+      *out_hi = chi;
+    } else {
+      *out_hi = coff + 1;
+    }
     CMS_HIP(hipGetLastError());
   }
-  *out_off = coff;
+  *out_lo = coff;
   *out_key = ckey;
   *out_val = cval;
   return CMS_OK;
+}
+
+int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
+                     int64_t** out_off, int64_t** out_key, float** out_val, int32_t* out_rows) {
+  int64_t* hi;
+  return partition_impl(h, d_row, d_key, d_val, npairs, false, out_off, &hi, out_key, out_val, out_rows);
+}
+
+int partition_to_spans(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
+                       int64_t** out_lo, int64_t** out_hi, int64_t** out_key, float** out_val) {
+  return partition_impl(h, d_row, d_key, d_val, npairs, true, out_lo, out_hi, out_key, out_val, nullptr);
 }
 
 }  // namespace cms

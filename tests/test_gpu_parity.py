@@ -93,6 +93,40 @@ def test_partition_key_width_modes(oracle, shape):
     assert same(got2, oracle_table(oracle, n, d, w, 7, both_i, both_k))
 
 
+@pytest.mark.parametrize("n,npairs,vals", [(20000, 3_000_000, False), (20000, 1_500_000, True), (1_000_000, 2_000_000, False)])
+def test_partition_hot_routing_equals_two_pass(oracle, n, npairs, vals, monkeypatch):
+    """Bulk COO builds route the sampled hottest owners straight to their
+    final place in pass 1 (partition_to_spans); the table equals the plain
+    two-pass partition's and the oracle's bit for bit, with and without
+    preference values, and at 1M owners (pass-1 fan-out 977 coarse + 1024 hot
+    bins)."""
+    d, w = 3, 256
+    items, users = zipf_stream(200_000, n, npairs, seed=n + npairs)
+    v = None
+    if vals:
+        v = np.random.Generator(np.random.PCG64(2)).integers(1, 6, size=items.size).astype(np.float32)
+    import torch
+    cnt = np.bincount(items, minlength=n)
+    # the 16 hottest owners and 2000 random ones are checked against the oracle
+    sel = np.unique(np.concatenate([np.argsort(-cnt, kind="stable")[:16],
+                                    np.random.Generator(np.random.PCG64(4)).integers(0, n, 2000)]))
+    got = {}
+    for mode in ("hot", "two_pass"):
+        if mode == "two_pass":
+            monkeypatch.setenv("CMS_NO_HOT_ROUTING", "1")
+        with SketchTable(n, depth=d, width=w, seed=11) as t:
+            t.ingest(items, users, v)
+            t.finalize()
+            got[mode] = t.read_counters_device().cpu()
+            torch.cuda.synchronize()
+    assert torch.equal(got["hot"], got["two_pass"])
+    remap = np.full(n, -1, np.int64)
+    remap[sel] = np.arange(sel.size)
+    m = remap[items] >= 0
+    exp = oracle_table(oracle, sel.size, d, w, 11, remap[items[m]], users[m], None if v is None else v[m])
+    assert same(got["hot"].numpy()[sel].astype(np.float64), exp)
+
+
 def test_reserved_hot_slots_then_late_promotion(oracle):
     """A fresh build reserves hot slots for every owner its bound allows (here
     all of a tiny universe) and claims them on the device; a later batch that
