@@ -279,6 +279,14 @@ int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t 
 #define CMS_FORMAT_ITEM_SIMILARITY_JOB 1
 #define CMS_FORMAT_SPARK_ITEMSIMILARITY 2
 int cms_write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format);
+/* cms_write_similarities with RowSimilarityJob's --threshold: pairs whose
+ * similarity is below `threshold` are left out (of the lists before the top-k,
+ * which for a top-k list is the same as dropping them afterwards;
+ * RowSimilarityJob.java, ItemSimilarityJob.java:128-129).  In the
+ * ItemSimilarityJob format a pair also needs similarity > Double.MIN_VALUE,
+ * the TopSimilarItemsQueue sentinel (TopSimilarItemsQueue.java:50-58,
+ * ItemSimilarityJob.java:203-209). */
+int cms_write_similarities_threshold(cms_handle* h, const char* path, int32_t k, int32_t format, double threshold);
 /* Java Double.toString(v) into buf (NUL-terminated); returns the length or -1. */
 int cms_format_java_double(double v, char* buf, int32_t cap);
 

@@ -40,7 +40,7 @@ EXPORTS = [
     "cms_point_query", "cms_estimate_preferences", "cms_most_similar", "cms_top_k_rows", "cms_top_k_all", "cms_top_k_all_partial", "cms_top_k_merge", "cms_write_similar_items", "cms_format_java_double", "cms_read_counters", "cms_get_stats",
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
-    "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities",
+    "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities", "cms_write_similarities_threshold",
     "cms_comm_init_transport", "cms_read_counters_device",
 ]
 
@@ -133,6 +133,7 @@ _SIGS = {
     "cms_comm_init_transport": (_int, [_vp, _i32, _i32, _vp, _vp, _vp]),
     "cms_read_counters_device": (_int, [_vp, _i64, _i64, _vp]),
     "cms_write_similarities": (_int, [_vp, ctypes.c_char_p, _i32, _i32]),
+    "cms_write_similarities_threshold": (_int, [_vp, ctypes.c_char_p, _i32, _i32, ctypes.c_double]),
     "cms_configure_owner_shapes": (_int, [_vp, _dbl, _i64]),
     "cms_set_owner_delta_epsilon": (_int, [_vp, _vp, _vp]),
     "cms_get_owner_shapes": (_int, [_vp, _vp, _vp, _vp, _vp]),

@@ -1146,14 +1146,19 @@ int cms_write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t 
 }
 
 int cms_write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format) {
+  return cms_write_similarities_threshold(h, path, k, format, -__builtin_inf());
+}
+
+int cms_write_similarities_threshold(cms_handle* h, const char* path, int32_t k, int32_t format, double threshold) {
   if (!h || !path) return set_error(CMS_E_PARAM, "null argument");
+  if (threshold != threshold) return set_error(CMS_E_PARAM, "threshold is NaN");
   if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
   if (format != CMS_FORMAT_ITEM_SIMILARITY_JOB && format != CMS_FORMAT_SPARK_ITEMSIMILARITY)
     return set_error(CMS_E_PARAM, "unknown output format %d", format);
   Guard g(h);
   int rc = require_finalized(h);
   if (rc) return rc;
-  return write_similarities(h, path, k, format);
+  return write_similarities(h, path, k, format, threshold);
 }
 
 int cms_format_java_double(double v, char* buf, int32_t cap) {

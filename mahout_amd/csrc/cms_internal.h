@@ -394,7 +394,7 @@ int f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_n
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
-int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format);
+int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format, double threshold);
 // ---- cms_cosine_mfma.hip ----
 const int64_t* cosine_perm_device(cms_handle* h);
 // ---- cms_cosine_mfma.hip ----

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -120,7 +121,7 @@ static int host_lists(cms_handle* h, int32_t k, std::vector<int64_t>& ids, std::
 // EntityEntityWritable order (aID, then bID; EntityEntityWritable.java:64-71),
 // "aID\tbID\tsimilarity" with DoubleWritable's Double.toString.
 static int write_item_similarity_job(cms_handle* h, OutBuf& o, int32_t k, const std::vector<int64_t>& ids,
-                                     const std::vector<double>& sc, const std::vector<int32_t>& cnt) {
+                                     const std::vector<double>& sc, const std::vector<int32_t>& cnt, double thr) {
   struct P {
     int64_t a, b;
     double v;
@@ -130,7 +131,11 @@ static int write_item_similarity_job(cms_handle* h, OutBuf& o, int32_t k, const 
     const int64_t owner = h->h_owner_ids.empty() ? r : h->h_owner_ids[r];
     for (int32_t i = 0; i < cnt[r]; ++i) {
       const int64_t other = ids[(size_t)r * k + i];
-      pairs.push_back(P{std::min(owner, other), std::max(owner, other), sc[(size_t)r * k + i]});
+      const double v = sc[(size_t)r * k + i];
+      // TopSimilarItemsQueue admits only similarity > its sentinel's
+      // Double.MIN_VALUE (zero is not a non-zero of the similarity vector anyway)
+      if (!(v > std::numeric_limits<double>::denorm_min()) || v < thr) continue;
+      pairs.push_back(P{std::min(owner, other), std::max(owner, other), v});
     }
   }
   // stable: for a pair listed by both owners the lower ID's list comes first
@@ -155,14 +160,14 @@ static int write_item_similarity_job(cms_handle* h, OutBuf& o, int32_t k, const 
 // "ID\tID1:s1 ID2:s2 ..." over the non-zero similarities sorted by strength
 // descending (stable: ties stay in list order), a bare "ID" when none.
 static int write_spark_itemsimilarity(cms_handle* h, OutBuf& o, int32_t k, const std::vector<int64_t>& ids,
-                                      const std::vector<double>& sc, const std::vector<int32_t>& cnt) {
+                                      const std::vector<double>& sc, const std::vector<int32_t>& cnt, double thr) {
   for (int64_t r = 0; r < h->n; ++r) {
     const int64_t owner = h->h_owner_ids.empty() ? r : h->h_owner_ids[r];
     o.put_id(owner);
     bool first = true;
     for (int32_t i = 0; i < cnt[r]; ++i) {
       const double v = sc[(size_t)r * k + i];
-      if (v == 0.0) continue;  // not a non-zero of the similarity vector
+      if (v == 0.0 || v < thr) continue;  // not a non-zero of the similarity vector / below the threshold
       o.put(first ? "\t" : " ", 1);
       first = false;
       o.put_id(ids[(size_t)r * k + i]);
@@ -174,7 +179,7 @@ static int write_spark_itemsimilarity(cms_handle* h, OutBuf& o, int32_t k, const
   return CMS_OK;
 }
 
-int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format) {
+int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format, double threshold) {
   std::vector<int64_t> ids;
   std::vector<double> sc;
   std::vector<int32_t> cnt;
@@ -184,8 +189,8 @@ int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t forma
   o.f = std::fopen(path, "wb");
   if (!o.f) return set_error(CMS_E_PARAM, "cannot open %s for writing", path);
   o.buf.reserve(1 << 22);
-  rc = format == CMS_FORMAT_ITEM_SIMILARITY_JOB ? write_item_similarity_job(h, o, k, ids, sc, cnt)
-                                                : write_spark_itemsimilarity(h, o, k, ids, sc, cnt);
+  rc = format == CMS_FORMAT_ITEM_SIMILARITY_JOB ? write_item_similarity_job(h, o, k, ids, sc, cnt, threshold)
+                                                : write_spark_itemsimilarity(h, o, k, ids, sc, cnt, threshold);
   o.flush();
   const bool closed = std::fclose(o.f) == 0;
   if (rc) return rc;

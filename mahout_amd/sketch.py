@@ -280,12 +280,17 @@ class SketchTable:
         """cms_top_k_all in FileSimilarItemsWriter's CSV format."""
         check(self._lib.cms_write_similar_items(self._h, os.fsencode(path), int(k), int(as_float)))
 
-    def write_similarities(self, path, k, fmt):
+    def write_similarities(self, path, k, fmt, threshold=None):
         """cms_write_similarities: fmt 'item_similarity_job' (MR ItemSimilarityJob
-        text result) or 'spark_itemsimilarity' (TextDelimitedIndexedDatasetWriter)."""
+        text result) or 'spark_itemsimilarity' (TextDelimitedIndexedDatasetWriter);
+        threshold: RowSimilarityJob's --threshold (cms_write_similarities_threshold)."""
         code = {"item_similarity_job": _lib.CMS_FORMAT_ITEM_SIMILARITY_JOB,
                 "spark_itemsimilarity": _lib.CMS_FORMAT_SPARK_ITEMSIMILARITY}[fmt]
-        check(self._lib.cms_write_similarities(self._h, os.fsencode(path), int(k), code))
+        if threshold is None:
+            check(self._lib.cms_write_similarities(self._h, os.fsencode(path), int(k), code))
+        else:
+            check(self._lib.cms_write_similarities_threshold(self._h, os.fsencode(path), int(k), code,
+                                                             float(threshold)))
 
     def top_k_all_partial(self, k, shard, nshards):
         n = self.num_owners

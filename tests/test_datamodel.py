@@ -19,10 +19,59 @@ def test_sorted_owners_and_keys(tmp_path):
 
 
 def test_last_value_wins_and_removal(tmp_path):
-    m = FileDataModel(write(tmp_path, ["1,5,2", "1,5,4", "1,6,1", "1,6,", "# comment", "", "2\t5\t1"]))
+    m = FileDataModel(write(tmp_path, ["1,5,2", "1,5,4", "1,6,1", "1,6,", "# comment", "", "2,5,1", "3,7,2", "3,7,"]))
     ids, vals = m.getPreferencesFromUser(1)
     assert ids.tolist() == [5] and vals.tolist() == [4.0]
-    assert m.getUserIDs().tolist() == [1, 2]
+    # user 3 lost its only preference but stays (GenericDataModel.toDataMap keeps the emptied collection)
+    assert m.getUserIDs().tolist() == [1, 2, 3]
+    assert m.getPreferencesFromUser(3)[0].size == 0
+
+
+def test_delimiter_from_first_line_and_boolean_files(tmp_path):
+    """FileDataModel.determineDelimiter (:344-352): ',' if the first data
+    line holds one, else tab -- and only that character splits every line;
+    a first line without a third token makes a boolean model (:210-214)."""
+    import pytest
+    m = FileDataModel(write(tmp_path, ["# c", "", "1\t5\t2.5", "2\t5\t1"]))
+    assert m.getPreferencesFromUser(1)[1].tolist() == [2.5]
+    with pytest.raises(ValueError):  # '1,2' is not a long once tab is the delimiter
+        FileDataModel(write(tmp_path, ["1\t5\t2", "1,2\t7\t1"]))
+    b = FileDataModel(write(tmp_path, ["1,5", "1,6", "2,5", "1,6,"]))
+    assert not b.hasPreferenceValues()
+    assert b.getPreferencesFromUser(1)[0].tolist() == [5]
+    from mahout_amd.taste import CosineCM, FixedShapeConfig, HashFunctionBuilder
+    with pytest.raises(ValueError):  # CosineCM.java:38 checkArgument(hasPreferenceValues)
+        CosineCM(b, FixedShapeConfig(2, 64), HashFunctionBuilder(1))
+
+
+def test_java_parse_float_and_long():
+    """Float.parseFloat: trimmed, sign, NaN/Infinity, hex significands,
+    f/F/d/D suffixes, one rounding of the exact decimal to float32 (no
+    decimal -> double -> float double rounding); Long.parseLong: digits and
+    an optional sign only, within range."""
+    import pytest
+    from fractions import Fraction
+    from mahout_amd.datamodel import java_parse_float as pf, java_parse_long as pl
+    assert pf(" 3.5 ") == np.float32(3.5) and pf("2.5f") == np.float32(2.5) and pf("4D") == np.float32(4.0)
+    assert pf("0x1p-2") == np.float32(0.25) and pf("-0x1.8p1") == np.float32(-3.0)
+    assert np.isnan(pf("NaN")) and pf("-Infinity") == -np.inf and pf("1e39") == np.inf
+    assert pf("1.4e-45") == np.float32(1e-45) and pf("7e-46") == 0.0
+    assert str(pf("-0")) == "-0.0"
+    # a decimal just above a float32 midpoint whose nearest double IS the midpoint:
+    # Java rounds the exact value up; decimal -> double -> float would round to even (down)
+    lo = np.float32(1.0)
+    hi = np.nextafter(lo, np.float32(2.0))
+    mid = (Fraction(1) + Fraction(float(hi))) / 2
+    s = "1.000000059604644775390625000000000001"  # mid + 1e-36
+    assert Fraction(s) > mid and float(Fraction(s)) == float(mid)
+    assert pf(s) == hi and np.float32(float(s)) == lo
+    for bad in ["", "3.5.1", "1e", "0x", "abc", "4,5"]:
+        with pytest.raises(ValueError):
+            pf(bad)
+    assert pl("+5") == 5 and pl("-9223372036854775808") == -2 ** 63
+    for bad in [" 5", "5 ", "9223372036854775808", "1.0", "0x10", ""]:
+        with pytest.raises(ValueError):
+            pl(bad)
 
 
 def test_transpose(tmp_path):
