@@ -381,7 +381,7 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
-                  &h->ws_f4, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
+                  &h->ws_f4, &h->ws_i8blk, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
                   &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist,
                   &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked};
   for (DevBuf* b : ws) b->release();
@@ -796,6 +796,7 @@ int cms_finalize(cms_handle* h) {
   if (rc) return rc;
   h->exact_norms = inexact == 0;
   h->mfma_ready = false;
+  h->i8blk_ready = false;
   h->finalized = true;
   return CMS_OK;
 }
@@ -830,6 +831,7 @@ int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   h->inexact_zero = inexact == 0;
   h->exact_norms = inexact == 0;
   h->mfma_ready = false;
+  h->i8blk_ready = false;
   h->finalized = true;
   return CMS_OK;
 }

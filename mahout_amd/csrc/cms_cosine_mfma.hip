@@ -30,11 +30,9 @@
 
 #include "cms_device.h"
 #include "cms_internal.h"
+#include "cms_mfma.h"
 
 namespace cms {
-
-typedef int8_t i8x16 __attribute__((ext_vector_type(16)));
-typedef int32_t i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTile = 128;      // output rows/cols per workgroup
 constexpr int kBK = 128;        // K bytes per stage
@@ -106,19 +104,8 @@ __global__ __launch_bounds__(256) void k_limb_write(TableView tv, int64_t dw, co
 // fp4 (e2m1) image of positions [f0, n): two counters per byte, low nibble
 // first.  Every counter is <= kF4Max, and 0..4 are exact e2m1 codes.
 //
-// K-blocked layout: the image is cut into blocks of kImgBlk rows, and inside a
-// block every 128-byte K slice of its rows is one contiguous 16 KiB run
-// ([slice][row][128 B]); a stage of a 128-row operand block is then one
-// contiguous run instead of 128 lines a row stride apart (DRAM page
-// locality for the symmetric waves' fills).  Rows past the end of the image
-// (the last block's padding) are zero.
-constexpr int kImgBlk = 128;
-__device__ __forceinline__ int64_t blk_off(int64_t row, int64_t kb, int64_t rs) {
-  return (row / kImgBlk) * (kImgBlk * rs) + (kb >> 7) * (kImgBlk * 128) + (row % kImgBlk) * 128 + (kb & 127);
-}
-
 __global__ __launch_bounds__(256) void k_f4_write(TableView tv, int64_t dw, const int64_t* perm, int64_t f0,
-                                                  uint8_t* f4) {
+                                                  uint8_t* f4, int sw) {
   const int64_t p = f0 + blockIdx.x;
   const int64_t row = perm[p];
   const int64_t rs = dw / 2;
@@ -130,7 +117,21 @@ __global__ __launch_bounds__(256) void k_f4_write(TableView tv, int64_t dw, cons
     auto code = [&](uint32_t c) { return (kCode >> (4 * c)) & 15u; };
     const uint32_t packed = code(v0.x) | code(v0.y) << 4 | code(v0.z) << 8 | code(v0.w) << 12 | code(v1.x) << 16 |
                             code(v1.y) << 20 | code(v1.z) << 24 | code(v1.w) << 28;
-    *reinterpret_cast<uint32_t*>(f4 + blk_off(blockIdx.x, j / 2, rs)) = packed;
+    *reinterpret_cast<uint32_t*>(f4 + blk_off(blockIdx.x, j / 2, rs, sw)) = packed;
+  }
+}
+
+// int8 limb-0 image of positions [p0, p0 + rows) in the K-blocked layout of
+// the fp4 image (blk_off): the symmetric int8 waves' operands, so a stage of
+// a 128-row block is one contiguous 16 KiB run instead of 128 lines a row
+// stride apart.  The last block's padding rows are zero.
+__global__ __launch_bounds__(256) void k_i8blk_write(const int8_t* limb0, int64_t dw, int64_t p0, int64_t rows,
+                                                     int8_t* img, int sw) {
+  const int64_t r = blockIdx.x;  // image row (whole blocks: padding rows write zeros)
+  const int8_t* src = r < rows ? limb0 + (p0 + r) * dw : nullptr;
+  for (int64_t j = threadIdx.x * 16; j < dw; j += 256 * 16) {
+    const int4 v = src ? *reinterpret_cast<const int4*>(src + j) : make_int4(0, 0, 0, 0);
+    *reinterpret_cast<int4*>(img + blk_off(r, j, dw, sw)) = v;
   }
 }
 
@@ -447,22 +448,6 @@ __global__ __launch_bounds__(256, MULTI ? 1 : 2) void k_cosine_tile(CosArgs a, c
 // multi-limb candidates: cosine(a, b) == cosine(b, a) bit for bit.
 constexpr int kTA = 256, kTB = 128;
 
-// LDS image of a BK-byte K slice of R rows: row-major, the 16-B chunk index
-// XOR-swizzled so that each 16-lane ds_read_b128 group (16 consecutive rows,
-// one chunk) hits 16 distinct 16-B slots of a 256-B bank line.
-template <int BK>
-__device__ __forceinline__ int lds_off_bk(int row, int ch) {
-  if constexpr (BK == 128) return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
-  else return row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);  // BK == 64
-}
-
-// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt fields at their maxima), gfx9 encoding.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
 struct BigArgs {
   const int8_t* A;      // operand rows (limb0 image or ws_vl), first row of this launch
   int64_t a_vrows;      // operand rows available from A
@@ -507,39 +492,8 @@ struct BigArgs {
   // together share si A panels and sj B blocks instead of 1 and 16-32
   int32_t rect, si, sj, njc;
   int32_t noscreen;  // 1: exact epilogue for every pair (A/B of the screening)
+  int32_t blk;       // int8 operands from a K-blocked image (k_i8blk_write); fp4 images always are
 };
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-typedef int32_t i32x8 __attribute__((ext_vector_type(8)));
-
-// FMT 0: int8 limbs, v_mfma_i32_32x32x32_i8.  FMT 1: fp4 (e2m1) counters
-// <= 4, v_mfma_f32_32x32x64_f8f6f4 (unscaled): the same 16 B per lane per
-// fragment carries 32 counters instead of 16, so a stage holds twice the K
-// at the same MFMA cycles.  Products <= 16 and row sums <= 16 * 32768 < 2^24
-// keep the f32 accumulation exact.
-template <int FMT>
-struct AccOf {
-  typedef i32x16 type;
-};
-template <>
-struct AccOf<1> {
-  typedef f32x16 type;
-};
-
-template <int FMT>
-__device__ __forceinline__ typename AccOf<FMT>::type mfma_step(const i8x16& a, const i8x16& b,
-                                                               typename AccOf<FMT>::type c) {
-  if constexpr (FMT == 0) {
-    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
-  } else {
-    const i32x4 a4 = __builtin_bit_cast(i32x4, a), b4 = __builtin_bit_cast(i32x4, b);
-    const i32x4 z = {0, 0, 0, 0};
-    const i32x8 a8 = __builtin_shufflevector(a4, z, 0, 1, 2, 3, 4, 5, 6, 7);
-    const i32x8 b8 = __builtin_shufflevector(b4, z, 0, 1, 2, 3, 4, 5, 6, 7);
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 0, 0, 0);  // cbsz/blgp 4: e2m1
-  }
-}
 
 template <int NSTAGE, int LS, int BK, int FMT = 0>
 __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
@@ -671,7 +625,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   // fp4 operands use the K-blocked image (k_f4_write; sym panels start on a
   // block): a panel's rows past the end inside its last block are the
   // image's zero padding, the rows beyond that block fall outside the bound.
-  constexpr bool BLK = FMT == 1;
+  const bool BLK = FMT == 1 || g.blk != 0;
   const int64_t rowsA = max<int64_t>(0, min<int64_t>(kTA, a_vrows - vrow0));
   const int64_t rowsB = max<int64_t>(0, min<int64_t>(kTB, b_rows - bcol0));
   const int64_t recA = BLK ? (rowsA + kImgBlk - 1) / kImgBlk * kImgBlk * rs : rowsA * rs;
@@ -689,16 +643,18 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
   const int srow = wid * RPI + lane / CPR;
   const int slot = lane % CPR;
   const int32_t chunk = (BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4;
-  // row-major image: row r at r * rs; K-blocked image (BLK, BK == 128): row r
-  // at (r / 128) * 128 * rs + (r % 128) * 128, K slice s at s * 16 KiB
-  const int32_t vo = BLK ? (int32_t)(srow * 128) + chunk : (int32_t)(srow * rs) + chunk;
+  // row-major image: row r at r * rs; K-blocked image (BLK, slices of BK
+  // bytes): row r at (r / 128) * 128 * rs + (r % 128) * BK, K slice s at
+  // s * 128 * BK; instruction u's rows start at 8 u RPI (block, row in block)
   const int32_t rstep = 8 * RPI * (int32_t)rs;
   const int32_t bstep = kImgBlk * (int32_t)rs;
-#define UOFF(u) (BLK ? vo + ((u) & 1) * (64 * 128) + ((u) >> 1) * bstep : vo + (u) * rstep)
+  const int32_t vo = BLK ? (srow / kImgBlk) * bstep + (srow % kImgBlk) * BK + chunk : (int32_t)(srow * rs) + chunk;
+#define UOFF(u) \
+  (BLK ? vo + ((8 * (u) * RPI) / kImgBlk) * bstep + ((8 * (u) * RPI) % kImgBlk) * BK : vo + (u) * rstep)
   auto issue = [&](int s) {
     if (kMode & 1) return;
     const int r = s / cstages, cs = s - r * cstages;
-    const int32_t koff = BLK ? s * (kImgBlk * 128) : r * kw + cs * BK;
+    const int32_t koff = BLK ? s * (kImgBlk * BK) : r * kw + cs * BK;
     unsigned char* st = lds + (s % NSTAGE) * kStage;
 #pragma unroll
     for (int u = 0; u < OPA; ++u)
@@ -938,6 +894,10 @@ int cosine_prepare(cms_handle* h) {
   CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
   // fp4 operands need whole 128-B stages of packed counters (256 per stage)
   int fp4_ok = (h->p.width % 256) == 0 ? 1 : 0;
+  // stage depth of the symmetric waves = K slice width of their blocked images
+  // (k_cosine_sym stages 64 B; CMS_OLD_SYM=1 keeps k_cosine_big's 128-B waves)
+  h->sym_sw = getenv("CMS_OLD_SYM") ? 128 : sym_stage_bytes();
+  if (const char* e = getenv("CMS_SYM_BK")) h->sym_sw = atoi(e) == 64 ? 64 : 128;
 #ifdef CMS_BOUND_ANALYSIS
   if (getenv("CMS_NO_FP4")) fp4_ok = 0;
 #endif
@@ -966,9 +926,9 @@ int cosine_prepare(cms_handle* h) {
   const int64_t n_deep = (int64_t)host[4] + host[5];
   const int64_t n_f4 = (int64_t)host[6] + host[7];
   const int64_t n_s8 = n - n_multi - n_f4;
-  // fp4 image from the first 256-row block of the single-limb region that
+  // fp4 image from the first 768-row block of the single-limb region that
   // holds fp4 owners only (symmetric-wave blocks start at n_multi)
-  const int64_t f0 = std::min<int64_t>(n, n_multi + (n_s8 + kTA - 1) / kTA * kTA);
+  const int64_t f0 = std::min<int64_t>(n, n_multi + (n_s8 + kSymBlk - 1) / kSymBlk * kSymBlk);
   h->n_f4 = n_f4;
   h->f4_pos0 = f0;
   h->n_hot_limb = (uint32_t)n_multi;
@@ -994,7 +954,7 @@ int cosine_prepare(cms_handle* h) {
       CMS_HIP(hipMemsetAsync(h->ws_f4.as<uint8_t>() + (size_t)(blocks - 1) * kImgBlk * (dw / 2), 0,
                              (size_t)kImgBlk * (dw / 2), h->stream));
       hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), 0, h->stream, h->tview(), dw, perm, f0,
-                         h->ws_f4.as<uint8_t>());
+                         h->ws_f4.as<uint8_t>(), h->sym_sw);
     }
     CMS_HIP(hipGetLastError());
   }
@@ -1042,8 +1002,9 @@ struct BigCfg {
   size_t norms = 0;
 };
 
-static BigCfg big_config(cms_handle* h) {
+static BigCfg big_config(cms_handle* h, int force_bk = 0) {
   BigCfg c;
+  if (force_bk) c.bk = force_bk;
   c.norms = (size_t)h->p.depth * (kTA + kTB) * sizeof(double) + (kTA + kTB) * sizeof(__half);
 #ifdef CMS_SCREEN_PROBE
   constexpr size_t kLdsMax = 160 * 1024 - 2048;  // the probe's static LDS (2-stage ring)
@@ -1069,7 +1030,8 @@ static BigCfg big_config(cms_handle* h) {
                          (const void*)k_cosine_big<4, 1, 64>,    (const void*)k_cosine_big<6, 1, 64>,
                          (const void*)k_cosine_big<4, 2, 64>,    (const void*)k_cosine_big<6, 2, 64>,
                          (const void*)k_cosine_big<4, 4, 64>,    (const void*)k_cosine_big<6, 4, 64>,
-                         (const void*)k_cosine_big<2, 1, 128, 1>, (const void*)k_cosine_big<3, 1, 128, 1>};
+                         (const void*)k_cosine_big<2, 1, 128, 1>, (const void*)k_cosine_big<3, 1, 128, 1>,
+                         (const void*)k_cosine_big<4, 1, 64, 1>,  (const void*)k_cosine_big<6, 1, 64, 1>};
     for (const void* f : fns) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsMax);
     return true;
   }();
@@ -1097,8 +1059,14 @@ static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t
   const size_t bytes = (size_t)c.nstage * 384 * c.bk + c.norms;
   const dim3 grid((unsigned)g.nblk), blk(512);
   if (fmt == 1) {  // fp4 operands: single-limb sym waves, 128-B stages
-    if (c.nstage == 3 && c.bk == 128) hipLaunchKernelGGL((k_cosine_big<3, 1, 128, 1>), grid, blk, bytes, h->stream, g);
-    else hipLaunchKernelGGL((k_cosine_big<2, 1, 128, 1>), grid, blk, (size_t)2 * 384 * 128 + c.norms, h->stream, g);
+    if (c.bk == 64) {
+      if (c.nstage == 6) hipLaunchKernelGGL((k_cosine_big<6, 1, 64, 1>), grid, blk, bytes, h->stream, g);
+      else hipLaunchKernelGGL((k_cosine_big<4, 1, 64, 1>), grid, blk, bytes, h->stream, g);
+    } else if (c.nstage == 3) {
+      hipLaunchKernelGGL((k_cosine_big<3, 1, 128, 1>), grid, blk, bytes, h->stream, g);
+    } else {
+      hipLaunchKernelGGL((k_cosine_big<2, 1, 128, 1>), grid, blk, (size_t)2 * 384 * 128 + c.norms, h->stream, g);
+    }
     CMS_HIP(hipGetLastError());
     return CMS_OK;
   }
@@ -1316,7 +1284,13 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     return CMS_OK;
   }
   CMS_HIP(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * n, h->stream));
-  const int32_t cap = kCandCap;
+  // symmetric waves on k_cosine_sym (256 x 192 tiles, 768-row blocks) when
+  // the table allows it and the images are staged 64 B deep
+  int32_t rb8 = 0, rb4 = 0;
+  const bool sym_img = h->sym_sw == sym_stage_bytes() && !getenv("CMS_OLD_SYM");
+  const bool sym8 = sym_img && sym_eligible(h, 0, &rb8);
+  const bool sym4 = sym_img && sym_eligible(h, 1, &rb4);
+  const int32_t cap = (sym8 || sym4) ? kCandCapSym : kCandCap;
   constexpr uint32_t kPerPass = 512;  // most offers one row takes in one pass
   DevBuf& ws = h->ws_cand;
   const size_t off_cidx = (sizeof(uint32_t) * (size_t)n + 255) & ~size_t(255);
@@ -1393,49 +1367,113 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
       }
       return bands;
     };
-    // pass 0: fp4 x fp4 block pairs; pass 1: the rest (all S when no fp4 region)
+    // The int8 waves read their operands from a K-blocked copy of the
+    // single-limb image (a stage of a block is one contiguous run) when the
+    // device has room for it next to everything else
+    bool i8blk = false;
+    if (fblk0 > 0 && !getenv("CMS_NO_I8BLK")) {
+      const int64_t blocks = (ns + kImgBlk - 1) / kImgBlk;
+      const size_t bytes = (size_t)blocks * kImgBlk * (size_t)h->dw;
+      size_t free_b = 0, total_b = 0;
+      if (h->i8blk_ready) {
+        i8blk = true;
+      } else if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > bytes + ((size_t)4 << 30) &&
+                 h->ws_i8blk.ensure(bytes) == hipSuccess) {
+        TimedScope ts(h, "limb_prep");
+        hipLaunchKernelGGL(k_i8blk_write, dim3((unsigned)(blocks * kImgBlk)), dim3(256), 0, h->stream, limb0, h->dw,
+                           nm, ns, h->ws_i8blk.as<int8_t>(), h->sym_sw);
+        CMS_HIP(hipGetLastError());
+        h->i8blk_ready = i8blk = true;
+      }
+    }
+    const BigCfg scfg = big_config(h, h->sym_sw);  // the blocked images' stage depth
+    // pass 0: fp4 x fp4 block pairs; pass 1: the rest (all S when no fp4 region).
+    // Each pass picks its kernel: k_cosine_sym (768-row blocks) or
+    // k_cosine_big (256-row blocks); the passes' row sets do not depend on it.
     int64_t shard_ctr = 0;
     for (int pass = 0; pass < 2; ++pass) {
       const bool fp4 = pass == 0;
       if (fp4 && fblk0 >= nb) continue;
       if (!fp4 && fblk0 == 0) continue;
-      const int64_t nbk = fp4 ? (n - f0 + kTA - 1) / kTA : nb;
+      const bool use_sym = fp4 ? sym4 : (sym8 && i8blk);
+      const int64_t blk = use_sym ? kSymBlk : kTA;
+      const int64_t nb_s = (ns + blk - 1) / blk;                        // blocks of the whole S region
+      const int64_t fb0 = f0 < n ? (f0 - nm) / blk : nb_s;              // first block of fp4 owners only
+      const int64_t nbk = fp4 ? (n - f0 + blk - 1) / blk : nb_s;
       for (const auto& bd : band_list(nbk)) {
         if (shard_ctr++ % nshards != shard) continue;
         const int64_t wv = bd.first, L = bd.second;
-        const uint32_t limit = L == 1 ? (uint32_t)cap - kPerPass : (uint32_t)cap / 2;
+        // a row takes up to 2 * blk offers per wave (its block as A and as B)
+        const uint32_t limit = L == 1 ? (uint32_t)(cap - 2 * blk) : (uint32_t)cap / 2;
         if ((rc = cand_compact(h, cb, nm, ns, limit, k))) return rc;
+        // wide bands of plain (non-fsel) waves: rectangle enumeration
+        const int rect = (L >= 8 && !(fp4 ? false : fb0 < nb_s) && !getenv("CMS_NO_RECT")) ? 1 : 0;
+        TimedScope ts(h, "topk_all_waves");
+        TimedScope tsub(h, fp4 ? "topk_all_waves_f4" : "topk_all_waves_i8");
+        if (use_sym) {
+          SymArgs g{};
+          g.img = fp4 ? h->ws_f4.as<int8_t>() : h->ws_i8blk.as<int8_t>();
+          g.img0 = g.s0 = fp4 ? f0 : nm;
+          g.s_rows = fp4 ? n - f0 : ns;
+          g.rs = fp4 ? h->dw / 2 : h->dw;
+          g.kw = fp4 ? h->p.width / 2 : h->p.width;
+          g.depth = h->p.depth;
+          g.nsq_t = h->ws_nsq.as<double>();
+          g.n = n;
+          g.nb = (int32_t)nbk;
+          g.wave = (int32_t)wv;
+          g.band = (int32_t)L;
+          g.rect = rect;
+          g.si = 4;
+          g.sj = 4;
+          if (const char* e = getenv("CMS_SYM_RECT")) sscanf(e, "%d,%d", &g.si, &g.sj);
+          g.thr = cb.thr;
+          g.ccnt = cb.ccnt;
+          g.cidx = cb.cidx;
+          g.cval = cb.cval;
+          g.cap = cap;
+          g.rbits = fp4 ? rb4 : rb8;
+          int64_t slots = nbk;
+          if (!fp4 && fb0 < nb_s) {
+            g.fsel = 1;
+            g.fblk0 = (int32_t)fb0;
+            slots = 2 * fb0;
+          }
+          if ((rc = launch_sym(h, g, fp4 ? 1 : 0, slots))) return rc;
+          continue;
+        }
         BigArgs g = base;
         g.sym = 1;
         g.wave = (int32_t)wv;
         g.band = (int32_t)L;
         g.nb = (int32_t)nbk;
         g.append_a = g.append_b = 1;
-        // wide bands of plain (non-fsel) waves: rectangle enumeration
-        g.rect = (L >= 8 && !(fp4 ? false : fblk0 < nb) && !getenv("CMS_NO_RECT")) ? 1 : 0;
+        g.rect = rect;
         g.si = 4;
         g.sj = 4;
-        TimedScope ts(h, "topk_all_waves");
         if (fp4) {
           g.A = g.B = h->ws_f4.as<int8_t>();
           g.img0 = g.s0 = f0;
           g.s_rows = n - f0;
           g.rs = h->dw / 2;
           g.kw = h->p.width / 2;
-          TimedScope t4(h, "topk_all_waves_f4");
-          if ((rc = launch_big(h, cfg, g, 1, nbk, 1))) return rc;
+          if ((rc = launch_big(h, scfg, g, 1, nbk, 1))) return rc;
         } else {
           g.A = g.B = limb0;
+          if (i8blk) {  // the K-blocked copy, positions from nm
+            g.A = g.B = h->ws_i8blk.as<int8_t>();
+            g.img0 = nm;
+            g.blk = 1;
+          }
           g.s0 = nm;
           g.s_rows = ns;
           int64_t slots = nbk;
-          if (fblk0 < nb) {
+          if (fb0 < nb_s) {
             g.fsel = 1;
-            g.fblk0 = (int32_t)fblk0;
-            slots = 2 * fblk0;
+            g.fblk0 = (int32_t)fb0;
+            slots = 2 * fb0;
           }
-          TimedScope t8(h, "topk_all_waves_i8");
-          if ((rc = launch_big(h, cfg, g, 1, slots))) return rc;
+          if ((rc = launch_big(h, i8blk ? scfg : cfg, g, 1, slots))) return rc;
         }
       }
     }

@@ -1,0 +1,362 @@
+// cms_cosine_sym.hip -- the all-pairs top-k's symmetric waves with 256 x 192
+// tiles (config 4's hot loop; DoubleCountMinSketch.cosine,
+// T/impl/common/DoubleCountMinSketch.java:114-149, offered to both owners'
+// candidate lists as TopItems.getTopUsers would rank them, TopItems.java:91-136).
+//
+// Why a second kernel.  k_cosine_big's 256 x 128 tile keeps every pair's
+// running Math.min as an fp64 value (2 registers per output, 128 of its 234
+// VGPRs).  Its waves are bound by the rate at which a CU can pull operand
+// bytes into LDS (~30 B/clk from L2), so the lever is bytes per MFMA, i.e. a
+// bigger tile -- which the fp64 state does not leave room for.  Here the state
+// is ONE register per output: the sketch row r* that holds the minimum so far
+// and its exact integer dot AB* (u32: AB* << rbits | r*).  The row cosine is
+// AB / (sqrt(A) * sqrt(B)) with sqrt(A), sqrt(B) in LDS for every sketch row,
+// so any state value can be re-derived exactly:
+//   - at each row boundary the new row's value and the stored one are first
+//     compared by fp32 estimates (relative error < 2^-20 each); only when the
+//     two lie within 2^-17 of each other are both recomputed in fp64
+//     (__dmul_rn / __ddiv_rn, as Java does) and compared exactly;
+//   - the admitted value is recomputed once at the end from (r*, AB*).
+// So the minimum, and the value reported, are the reference's exactly.  The
+// same fp32 estimate drives the threshold screening (a pair whose estimate is
+// below both owners' admission thresholds can never be admitted).
+//
+// Geometry.  Blocks of kSymBlk = 768 rows; a block pair {I, J} is 3 x 4
+// workgroups (A panels of 256 rows, B panels of 192); 8 waves in 4 x 2, each
+// 64 x 96 outputs = 2 x 3 MFMA 32x32 tiles (96 accumulators + 96 states per
+// lane).  K is staged 64 B per row per stage by buffer LDS-DMA from the
+// K-blocked images (kImgBlk-row blocks, a stage of a panel is a few
+// contiguous runs) into a 5-deep ring of 28 KiB stages.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+
+#include "cms_device.h"
+#include "cms_internal.h"
+#include "cms_mfma.h"
+
+namespace cms {
+
+constexpr int kSA = 256, kSB = 192;  // A panel rows x B panel rows per workgroup
+constexpr int kPA = kSymBlk / kSA;   // 3 A panels per block
+constexpr int kPB = kSymBlk / kSB;   // 4 B panels per block
+constexpr int kSub = kPA * kPB;      // 12 workgroups per block pair
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;  // no sketch row qualified yet (NaN)
+
+__device__ __forceinline__ uint32_t block_map(int bx, int nblk) {
+  // contiguous ranges of the linear index per XCD (workgroup bx runs on XCD bx % 8)
+  const int xcd = bx & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  return (uint32_t)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3));
+}
+
+template <int NSTAGE, int BK, int FMT>
+__global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
+  using AccT = typename AccOf<FMT>::type;
+  constexpr int kStageA = kSA * BK, kStageB = kSB * BK, kStage = kStageA + kStageB;
+  constexpr int RPI = 1024 / BK;                 // rows per 1-KiB LDS-DMA instruction
+  constexpr int OPA = kSA / RPI / 8;             // A instructions per wave per stage
+  constexpr int RB = kSB / RPI;                  // B instructions per stage (all waves)
+  constexpr int OPB_HI = (RB + 7) / 8, OPB_LO = RB / 8;  // waves < RB % 8 issue one more
+  static_assert(kSA % (8 * RPI) == 0, "A rows per round");
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int depth = g.depth;
+  double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][256]
+  double* s_sb = s_sa + depth * kSA;                                  // [depth][192]
+  __half* s_ta = reinterpret_cast<__half*>(s_sb + depth * kSB);      // admission thresholds, rounded down
+  __half* s_tb = s_ta + kSA;
+
+  // ---- which tile: band of waves, block pair {I, J}, A panel, B panel ----
+  const int lin = (int)block_map(blockIdx.x, g.nblk);
+  int c, sub, wv;
+  if (g.rect) {
+    const int per = kSub * g.si * g.sj;
+    const int blk = lin / per, loc = lin - blk * per;
+    const int ib = blk / g.njc, jc = blk - ib * g.njc;
+    sub = loc % kSub;
+    const int rest = loc / kSub;
+    const int li = rest / g.sj, lj = rest - li * g.sj;
+    c = ib * g.si + li;
+    if (c >= g.nb) return;
+    wv = ib * g.si + g.wave + jc * g.sj + lj - c;  // unwrapped J' - I
+    if (wv < g.wave || wv >= g.wave + g.band) return;
+  } else {
+    const int per = kSub * g.band;
+    c = lin / per;
+    const int rem = lin - c * per;
+    sub = rem % kSub;
+    wv = g.wave + rem / kSub;
+  }
+  int I = c;
+  if (g.fsel) {  // only pairs with a block below fblk0 (see k_cosine_big)
+    if (c >= g.fblk0) {
+      I = ((c - g.fblk0 - wv) % g.nb + g.nb) % g.nb;
+      if (I < g.fblk0) return;
+    }
+  }
+  if ((g.nb & 1) == 0 && 2 * wv == g.nb && 2 * I >= g.nb) return;  // {I, I + nb/2} once
+  const int J = (I + wv) % g.nb;
+  const bool diag = I == J;
+  const int pa = sub / kPB, pb = sub - pa * kPB;
+  const int64_t a_pos0 = g.s0 + (int64_t)I * kSymBlk + pa * kSA;
+  const int64_t b_pos0 = g.s0 + (int64_t)J * kSymBlk + pb * kSB;
+  const int64_t a_rows = min<int64_t>(kSA, g.s0 + g.s_rows - a_pos0);
+  const int64_t b_rows = min<int64_t>(kSB, g.s0 + g.s_rows - b_pos0);
+  if (a_rows <= 0 || b_rows <= 0) return;          // the whole workgroup leaves before any barrier
+  if (diag && a_pos0 >= b_pos0 + kSB - 1) return;  // every pair of the tile has a >= b
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int64_t rs = g.rs;
+  const int cstages = g.kw / BK;
+  const int total = depth * cstages;
+
+  // sqrt norms of the panels' owners by LDS-DMA (256 B = 32 doubles per
+  // instruction; past-the-end owners land as zeros), thresholds as fp16
+  // rounded toward -inf (never above the threshold)
+  constexpr int kPartsA = kSA / 32, kParts = (kSA + kSB) / 32;
+  for (int k = wid; k < kParts * depth; k += 8) {
+    const int r = k / kParts, part = k % kParts;
+    const bool isA = part < kPartsA;
+    const int64_t first = isA ? part * 32 : (part - kPartsA) * 32;
+    const int64_t lim = isA ? a_rows : b_rows;
+    const int64_t cnt = max<int64_t>(0, min<int64_t>(32, lim - first));
+    const double* src = g.nsq_t + (int64_t)r * g.n + (isA ? a_pos0 : b_pos0) + first;
+    const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * 8), 0x00020000);
+    double* dst = isA ? s_sa + r * kSA + first : s_sb + r * kSB + first;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsn, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
+  }
+  for (int i = tid; i < kSA + kSB; i += 512) {
+    const bool isA = i < kSA;
+    const int64_t o = isA ? i : i - kSA;
+    const int64_t lim = isA ? a_rows : b_rows;
+    const double t = o < lim ? g.thr[(isA ? a_pos0 : b_pos0) + o] : __builtin_inf();
+    (isA ? s_ta : s_tb - kSA)[i] = __float2half_rd(__double2float_rd(t));
+  }
+
+  // ---- operand fills: K-blocked images, panels start on a kImgBlk block ----
+  const int64_t recA = (a_rows + kImgBlk - 1) / kImgBlk * kImgBlk * rs;
+  const int64_t recB = (b_rows + kImgBlk - 1) / kImgBlk * kImgBlk * rs;
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + (a_pos0 - g.img0) * rs), (short)0, (int)recA, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + (b_pos0 - g.img0) * rs), (short)0, (int)recB, 0x00020000);
+  // instruction u of wave wid fills panel rows [(wid + 8u) RPI, +RPI); lane i
+  // lands at byte 16 i (row (wid + 8u) RPI + i / CPR, slot i % CPR) and
+  // fetches the chunk the XOR swizzle puts there
+  constexpr int CPR = BK / 16;
+  const int srow = wid * RPI + lane / CPR;
+  const int slot = lane % CPR;
+  const int32_t chunk = (BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4;
+  const int32_t bstep = kImgBlk * (int32_t)rs;
+  const int32_t vo = (srow / kImgBlk) * bstep + (srow % kImgBlk) * BK + chunk;
+  constexpr int UROWS = 8 * RPI;  // panel rows per round of instructions (a multiple of kImgBlk)
+  static_assert(UROWS % kImgBlk == 0, "rounds start on image blocks");
+  const int opb = wid < (RB % 8 == 0 ? 8 : RB % 8) ? OPB_HI : OPB_LO;
+  auto issue = [&](int s) {
+    const int32_t koff = s * (kImgBlk * BK);
+    unsigned char* st = lds + (s % NSTAGE) * kStage;
+#pragma unroll
+    for (int u = 0; u < OPA; ++u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + 8 * u) * 1024),
+                                               16, vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
+#pragma unroll
+    for (int u = 0; u < OPB_HI; ++u)
+      if (u < opb)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + 8 * u) * 1024), 16,
+            vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
+  };
+
+  AccT acc[2][3];
+  uint32_t st[2][3][16];
+  uint32_t alive[3] = {~0u, ~0u, ~0u};  // bit (i*3+j)*16 + e: the pair may still be admitted
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        acc[i][j][e] = 0;
+        st[i][j][e] = kEmpty;
+      }
+  const uint32_t rbits = (uint32_t)g.rbits, rmask = (1u << rbits) - 1u;
+
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < total) issue(s);
+
+  for (int s = 0; s < total; ++s) {
+    // stage s landed: at most the (NSTAGE-2) younger stages stay in flight
+    asm volatile("" ::: "memory");
+    if (s + NSTAGE - 2 < total) {
+      if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 2)>();
+      else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 2)>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);  // refill the slot read in iteration s-1
+    const unsigned char* A = lds + (s % NSTAGE) * kStage;
+    const unsigned char* B = A + kStageA;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int ch = 2 * ks + (lane >> 5);
+      i8x16 fb[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const i8x16 fa = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa, fb[j], acc[i][j]);
+      }
+    }
+    const int r = s / cstages;
+    if (s - r * cstages != cstages - 1) continue;
+    // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
+    const double* sa_r = s_sa + r * kSA;
+    const double* sb_r = s_sb + r * kSB;
+    if (__any((alive[0] | alive[1] | alive[2]) != 0u)) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int col = wc * 96 + j * 32 + (lane & 31);
+        const double sb = sb_r[col];
+        const float rb = __builtin_amdgcn_rcpf((float)sb);
+        const float tb = __half2float(s_tb[col]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int bit = (i * 3 + j) * 16 + e;
+            const uint32_t m = 1u << (bit & 31);
+            if (!(alive[bit >> 5] & m)) continue;
+            const int row = wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            const double sa = sa_r[row];
+            if (sa == 0.0 || sb == 0.0) continue;  // den == 0: this sketch row does not qualify
+            const uint32_t ab = (uint32_t)acc[i][j][e];
+            const float est = (float)ab * __builtin_amdgcn_rcpf((float)sa) * rb;
+            if (est < fminf(__half2float(s_ta[row]), tb) - 4e-6f) {  // can never be admitted
+              alive[bit >> 5] &= ~m;
+              continue;
+            }
+            uint32_t& sv = st[i][j][e];
+            bool take = sv == kEmpty;
+            if (!take) {
+              const int rr = (int)(sv & rmask);
+              const uint32_t ab0 = sv >> rbits;
+              const double sa0 = s_sa[rr * kSA + row], sb0 = s_sb[rr * kSB + col];
+              const float est0 = (float)ab0 * __builtin_amdgcn_rcpf((float)sa0) * __builtin_amdgcn_rcpf((float)sb0);
+              if (est < est0 * (1.0f - 0x1p-17f)) {
+                take = true;
+              } else if (est <= est0 * (1.0f + 0x1p-17f)) {  // too close for fp32: the exact values
+                const double v = __ddiv_rn((double)ab, __dmul_rn(sa, sb));
+                const double v0 = __ddiv_rn((double)ab0, __dmul_rn(sa0, sb0));
+                take = v < v0;
+              }
+            }
+            if (take) sv = (ab << rbits) | (uint32_t)r;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+  }
+
+  // ---- the exact value of each surviving pair, offered to both lists ----
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int col = wc * 96 + j * 32 + (lane & 31);
+    const int64_t bp = b_pos0 + col;
+    const double tb = col < b_rows ? g.thr[bp] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int bit = (i * 3 + j) * 16 + e;
+        if (!((alive[bit >> 5] >> (bit & 31)) & 1u)) continue;
+        const uint32_t sv = st[i][j][e];
+        if (sv == kEmpty) continue;  // NaN: never offered
+        const int row = wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (row >= a_rows || col >= b_rows) continue;
+        const int64_t ap = a_pos0 + row;
+        if (ap == bp || (diag && ap > bp)) continue;
+        const int rr = (int)(sv & rmask);
+        double v = __ddiv_rn((double)(sv >> rbits), __dmul_rn(s_sa[rr * kSA + row], s_sb[rr * kSB + col]));
+        if (v > 1.0) v = 1.0;  // normalizeWeightResult, unweighted (values are >= 0)
+        if (v >= g.thr[ap]) {
+          const uint32_t slot = atomicAdd(&g.ccnt[ap], 1u);
+          if (slot < (uint32_t)g.cap) {
+            g.cidx[ap * g.cap + slot] = (uint32_t)bp;
+            g.cval[ap * g.cap + slot] = v;
+          }
+        }
+        if (v >= tb) {
+          const uint32_t slot = atomicAdd(&g.ccnt[bp], 1u);
+          if (slot < (uint32_t)g.cap) {
+            g.cidx[bp * g.cap + slot] = (uint32_t)ap;
+            g.cval[bp * g.cap + slot] = v;
+          }
+        }
+      }
+  }
+}
+
+#ifndef CMS_SYM_NS
+#define CMS_SYM_NS 5
+#endif
+#ifndef CMS_SYM_BK
+#define CMS_SYM_BK 64
+#endif
+constexpr int kSymNS = CMS_SYM_NS, kSymBK = CMS_SYM_BK;  // ring depth, bytes per row per stage
+
+int sym_stage_bytes() { return kSymBK; }
+
+size_t sym_lds_bytes(int depth) {
+  return (size_t)kSymNS * (kSA + kSB) * kSymBK + (size_t)depth * (kSA + kSB) * sizeof(double) +
+         (kSA + kSB) * sizeof(__half);
+}
+
+bool sym_eligible(cms_handle* h, int fmt, int32_t* rbits) {
+  int rb = 0;
+  while ((1 << rb) < h->p.depth) ++rb;
+  rb = std::max(rb, 1);
+  // largest exact dot of one sketch row: fp4 counters <= 4, int8 limbs <= 127
+  const double max_ab = (fmt == 1 ? 16.0 : 16129.0) * (double)h->p.width;
+  *rbits = rb;
+  return h->p.weighting != CMS_WEIGHTED && max_ab < (double)((1ULL << (32 - rb)) - 1) &&
+         sym_lds_bytes(h->p.depth) <= 160 * 1024 && (h->p.width % (fmt == 1 ? 2 * kSymBK : kSymBK)) == 0;
+}
+
+int launch_sym(cms_handle* h, SymArgs g, int fmt, int64_t pair_slots) {
+  g.nblk = (int32_t)(kSub * g.band * pair_slots);
+  if (g.rect) {
+    g.njc = (g.si + g.band - 1 + g.sj - 1) / g.sj;
+    g.nblk = (int32_t)(((pair_slots + g.si - 1) / g.si) * g.njc * g.si * g.sj * kSub);
+  }
+  if (g.nblk <= 0) return CMS_OK;
+  const size_t bytes = sym_lds_bytes(g.depth);
+  static bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  if (fmt == 1) hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 1>), dim3(g.nblk), dim3(512), bytes, h->stream, g);
+  else hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 0>), dim3(g.nblk), dim3(512), bytes, h->stream, g);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+}  // namespace cms

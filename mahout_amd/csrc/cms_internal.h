@@ -164,6 +164,8 @@ struct cms_handle {
   } vl[2];
   int64_t n_f4 = 0;     // single-limb owners whose counters are all <= 4 (fp4-exact)
   int64_t f4_pos0 = 0;  // first permuted position of the fp4 image (ws_f4); n if none
+  int32_t sym_sw = 128;      // K slice width (bytes) of the K-blocked images = the symmetric waves' stage depth
+  bool i8blk_ready = false;  // ws_i8blk holds the K-blocked int8 image of positions [n_multi, n)
   bool vl_ok = false;           // every multi-limb owner fits 4 limbs (else the legacy 128x128 path)
   int64_t topk_redo = 0;        // top-k rows the sampled threshold missed (radix-select redo)
   std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
@@ -177,7 +179,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off, ws_csr_hi;
   cms::DevBuf ws_hotpart;  // hot-owner routing of the partition: slot keys [1024] u64, sample counts [n] u32
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
-  cms::DevBuf ws_query, ws_out, ws_srow, ws_f4;
+  cms::DevBuf ws_query, ws_out, ws_srow, ws_f4, ws_i8blk;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 
   // communicator: RCCL (cms_comm_init) or a caller transport (cms_comm_init_transport)
@@ -317,6 +319,7 @@ int slab_top_k_positions(cms_handle* h, const std::vector<int64_t>& pos, const s
                          int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
 // candidate lists of the streaming all-pairs top-k
 constexpr int kCandCap = 1024;  // entries per row
+constexpr int kCandCapSym = 2048;  // entries per row with the 768-row symmetric blocks (up to 1536 offers per wave)
 struct CandBufs {
   uint32_t* ccnt;  // [n]
   uint32_t* cidx;  // [n][cap]
@@ -395,6 +398,31 @@ int f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_n
 int java_double_to_string(double v, char* out, int cap);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
 int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format, double threshold);
+// ---- cms_cosine_sym.hip: symmetric all-pairs waves, 256 x 192 tiles ----
+struct SymArgs {
+  const int8_t* img;  // K-blocked operand image (int8 limb 0 or fp4), row 0 = position img0
+  int64_t img0;
+  int64_t rs;         // bytes per image row
+  int32_t kw;         // bytes per sketch row in the image
+  int32_t depth;
+  const double* nsq_t;  // [d][n] sqrt norms by permuted position
+  int64_t n;
+  int64_t s0, s_rows;   // the region's positions; blocks of kSymBlk rows from s0
+  int32_t nb, wave, band, nblk;
+  int32_t fsel, fblk0;              // only block pairs with a block below fblk0
+  int32_t rect, si, sj, njc;        // band enumerated by si x sj block rectangles
+  const double* thr;                // candidate lists (CandBufs)
+  uint32_t* ccnt;
+  uint32_t* cidx;
+  double* cval;
+  int32_t cap;
+  int32_t rbits;  // bits of the sketch-row index in the packed running-min state
+};
+// the kernel can run this table's waves (unweighted, its exact dot fits the
+// packed state, LDS budget); fmt 0 int8, 1 fp4
+bool sym_eligible(cms_handle* h, int fmt, int32_t* rbits);
+int launch_sym(cms_handle* h, SymArgs g, int fmt, int64_t pair_slots);
+int sym_stage_bytes();  // k_cosine_sym's K slice per stage = the images' slice width
 // ---- cms_cosine_mfma.hip ----
 const int64_t* cosine_perm_device(cms_handle* h);
 // ---- cms_cosine_mfma.hip ----

@@ -426,10 +426,10 @@ __global__ __launch_bounds__(kCandThreads) void k_cand_compact(const uint32_t* l
                                                                uint32_t* ccnt, uint32_t* cidx, double* cval,
                                                                int32_t cap, int32_t k, const int64_t* perm,
                                                                double* thr, uint32_t* ovf) {
-  __shared__ uint64_t key[kCandCap];
-  __shared__ uint32_t row[kCandCap];
-  __shared__ uint32_t pid[kCandCap];
-  __shared__ double val[kCandCap];
+  __shared__ uint64_t key[kCandCapSym];
+  __shared__ uint32_t row[kCandCapSym];
+  __shared__ uint32_t pid[kCandCapSym];
+  __shared__ double val[kCandCapSym];
   const uint32_t nl = *list_n;
   const int tid = threadIdx.x;
   for (uint32_t e = blockIdx.x; e < nl; e += gridDim.x) {
