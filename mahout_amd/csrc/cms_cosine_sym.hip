@@ -37,6 +37,10 @@
 #include "cms_internal.h"
 #include "cms_mfma.h"
 
+#ifndef CMS_SYM_PREFETCH
+#define CMS_SYM_PREFETCH 0  // 1: double-buffered fragments across k-steps
+#endif
+
 namespace cms {
 
 constexpr int kSA = 256, kSB = 192;  // A panel rows x B panel rows per workgroup
@@ -202,20 +206,45 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
     if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);  // refill the slot read in iteration s-1
     const unsigned char* A = lds + (s % NSTAGE) * kStage;
     const unsigned char* B = A + kStageA;
+#if CMS_SYM_PREFETCH
+    // fragments of k-step ks+1 are read while k-step ks's MFMAs run
+    i8x16 fa[2][2], fb[2][3];
+    auto frag = [&](int ks, int b) {
+      const int ch = 2 * ks + (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        fb[b][j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[b][i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
+    };
+    frag(0, 0);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
+      if (ks + 1 < BK / 32) frag(ks + 1, (ks + 1) & 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[ks & 1][i], fb[ks & 1][j], acc[i][j]);
+    }
+#else
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      // the k-step's five fragments first, then its six MFMAs
       const int ch = 2 * ks + (lane >> 5);
-      i8x16 fb[3];
+      i8x16 fb[3], fa[2];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const i8x16 fa = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
+      for (int i = 0; i < 2; ++i)
+        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa, fb[j], acc[i][j]);
-      }
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
     }
+#endif
     const int r = s / cstages;
     if (s - r * cstages != cstages - 1) continue;
     // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
@@ -316,6 +345,9 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
 #endif
 #ifndef CMS_SYM_BK
 #define CMS_SYM_BK 64
+#endif
+#ifndef CMS_SYM_PREFETCH
+#define CMS_SYM_PREFETCH 0
 #endif
 constexpr int kSymNS = CMS_SYM_NS, kSymBK = CMS_SYM_BK;  // ring depth, bytes per row per stage
 
