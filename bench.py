@@ -295,6 +295,29 @@ def config1(budget_s=3.0):
         dt = time.perf_counter() - t0
     out["gpu"] = {"top100_all_items_s": dt, "unique_item_pair_cosines_per_s": total / dt,
                   "full_lists": int((cnt == 100).sum())}
+    # the reference's native per-owner mode: CosineCM with
+    # CountMinSketchConfig(q=1) -- every item its own (d, w) from the Fmeasure
+    # search, u1 hashed at u2's shape; all n*(n-1) ORDERED pairs (asymmetric)
+    po = {}
+    with SketchTable.per_owner_shapes(n, seed=42, owner_ids=ids) as t:
+        t.ingest_csr(off, keys, vals)
+        t0 = time.perf_counter()
+        t.configure_owner_shapes(1.0, np.unique(users).size)
+        po["configure_s"] = time.perf_counter() - t0
+        t.finalize()
+        _, eps, ws, ds = t.owner_shapes()
+        t.top_k_all(100)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, _, cnt = t.top_k_all(100)
+        dt = time.perf_counter() - t0
+        po.update({"workload": "CountMinSketchConfig(q=1) shapes per item; top-100 of every item over all ordered "
+                               "pairs (userSimilarity(u1, u2) hashes u1 at u2's shape)",
+                   "ordered_pairs": n * (n - 1), "top100_all_items_s": dt,
+                   "ordered_pairs_per_s": n * (n - 1) / dt, "full_lists": int((cnt == 100).sum()),
+                   "width_range": [int(ws.min()), int(ws.max())], "depth_range": [int(ds.min()), int(ds.max())],
+                   "sketch_counters": int((ws.astype(np.int64) * ds).sum())})
+    out["gpu_per_owner_shapes"] = po
     return out
 
 
@@ -585,6 +608,11 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
             it_, us = it_[keep], us[keep]
         batches.append((it_.contiguous(), us.contiguous()))
     local = sum(int(b[0].numel()) for b in batches)
+    # owners the batches touch: an exact incremental refresh must recompute
+    # every pair with a touched owner (its score may fall, so the untouched
+    # side's list needs its (k+1)-th candidate), i.e. 1 - (1 - f)^2 of the pairs
+    touched_all = torch.unique(torch.cat([b[0] for b in batches])).numel() / n
+    touched_one = sum(torch.unique(b[0]).numel() for b in batches) / (n * nb)
     t.set_timing(True)
     t.reset_timing()
     bar()
@@ -623,6 +651,9 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "refresh_topk_all_s": topk_s,
         "refresh_latency_s": fin_s + topk_s,
         "full_lists": int((cnt == k).sum()),
+        "touched_owner_frac": {"all_batches": touched_all, "per_batch": touched_one,
+                               "pairs_to_recompute_all_batches": 1 - (1 - touched_all) ** 2,
+                               "pairs_to_recompute_per_batch": 1 - (1 - touched_one) ** 2},
     }
 
 

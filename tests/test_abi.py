@@ -99,7 +99,9 @@ def test_vectorised_shard_matches_library(lib):
     (1e7, "1.0E7"), (9999999.0, "9999999.0"), (0.001, "0.001"), (-0.0, "-0.0"), (0.0, "0.0"),
     (float("nan"), "NaN"), (float("inf"), "Infinity"), (float("-inf"), "-Infinity"), (12345678.9, "1.23456789E7"),
     (0.5, "0.5"), (100.0, "100.0"), (-2.5e-5, "-2.5E-5"), (0.0009999, "9.999E-4"), (0.769846046, "0.769846046"),
-    (float(np.float32(0.45)), "0.44999998807907104"), (1.5e300, "1.5E300")])
+    (float(np.float32(0.45)), "0.44999998807907104"), (1.5e300, "1.5E300"),
+    # JDK 19+ digits (JDK-4511638); Java 1.7's FloatingDecimal prints 2.0000000000000002E23 / 8.41E21 as 8.409999999999999E21
+    (2e23, "2.0E23"), (8.41e21, "8.41E21"), (1.0e23, "1.0E23")])
 def test_java_double_to_string(v, java):
     """FileSimilarItemsWriter writes String.valueOf(double): Java's
     Double.toString layout (plain in [1e-3, 1e7), else d.dddE[-]n)."""
