@@ -165,8 +165,13 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t r, int s2, int P1, const uin
   return r >> s2;
 }
 
-__global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, int64_t chunk, int s2, int P1,
-                                                 int64_t nrows, uint32_t* H1, int NB, uint32_t* flags,
+// Pass-1 work is cut into tiles of kPartTile pairs, and block b takes tiles
+// b, b + NB, b + 2 NB, ... (the same assignment in k_p1_hist and
+// k_p1_scatter): at any moment the blocks stream one contiguous window of the
+// stream instead of NB separate regions (DRAM page locality; the contiguous
+// per-block chunks streamed the owner column at ~3.4 TB/s).
+__global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, int s2, int P1, int64_t nrows,
+                                                 uint32_t* H1, int NB, uint32_t* flags,
                                                  const unsigned long long* hotkey) {
   extern __shared__ uint32_t lh[];
   const int P = P1 + (hotkey ? kHotBins : 0);  // bins: coarse, then hot
@@ -174,45 +179,34 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
   for (int b = threadIdx.x; b < P; b += blockDim.x) lh[b] = 0;
   if (tab) load_hot_table(hotkey, tab);
   __syncthreads();
-  int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   bool bad = false;
-  // two rows per 16-byte load
-  const int64_t lo2 = (lo + 1) & ~int64_t(1);
-  if (lo2 > lo && threadIdx.x == 0 && lo < hi) {
-    int64_t r = row[lo];
-    if (r < 0 || r >= nrows) bad = true;
-    else atomicAdd(&lh[bin_of((uint32_t)r, s2, P1, tab)], 1u);
-  }
-  const int64_t npair = (hi - lo2) / 2;
-  const longlong2* r2 = reinterpret_cast<const longlong2*>(row + lo2);
-  // whole waves step together so the aggregated increments see converged
-  // lanes; CMS_P1H_U 16-byte loads in flight per lane
-#ifndef CMS_P1H_U
-#define CMS_P1H_U 4
-#endif
-  constexpr int kU = CMS_P1H_U;
-  const int64_t span = (int64_t)blockDim.x * kU;
-  const int64_t nstep = (npair + span - 1) / span * span;
-  for (int64_t i0 = threadIdx.x; i0 < nstep; i0 += span) {
-    longlong2 v[kU];
+  const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
+  const bool vec = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+  // 256 threads x 8 16-byte loads = one 4096-pair tile, all loads in flight;
+  // whole waves step together so the aggregated increments see converged lanes
+  constexpr int kL = kPartTile / 2 / 256;
+  static_assert(kL * 2 * 256 == kPartTile, "tile = 256 threads x kL pair loads");
+  for (int64_t t = blockIdx.x; t < ntiles; t += NB) {
+    const int64_t t0 = t * kPartTile, tn = min<int64_t>(kPartTile, n - t0);
+    longlong2 v[kL];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t i = i0 + (int64_t)u * blockDim.x;
-      v[u] = i < npair ? r2[i] : longlong2{-1, -1};
+    for (int u = 0; u < kL; ++u) {
+      const int64_t i = 2 * ((int64_t)u * 256 + threadIdx.x);  // pair index within the tile
+      if (vec && i + 1 < tn) {
+        v[u] = *reinterpret_cast<const longlong2*>(row + t0 + i);
+      } else {
+        v[u].x = i < tn ? row[t0 + i] : -1;
+        v[u].y = i + 1 < tn ? row[t0 + i + 1] : -1;
+      }
     }
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const bool in = i0 + (int64_t)u * blockDim.x < npair;
+    for (int u = 0; u < kL; ++u) {
+      const int64_t i = 2 * ((int64_t)u * 256 + threadIdx.x);
       const bool okx = v[u].x >= 0 && v[u].x < nrows, oky = v[u].y >= 0 && v[u].y < nrows;
-      if (in && (!okx || !oky)) bad = true;
+      if ((i < tn && !okx) || (i + 1 < tn && !oky)) bad = true;
       lds_bin_add<CMS_PEEL_P1H, false>(lh, okx ? bin_of((uint32_t)v[u].x, s2, P1, tab) : 0u, okx);
       lds_bin_add<CMS_PEEL_P1H, false>(lh, oky ? bin_of((uint32_t)v[u].y, s2, P1, tab) : 0u, oky);
     }
-  }
-  if (threadIdx.x == 0 && lo2 + 2 * npair < hi) {
-    int64_t r = row[hi - 1];
-    if (r < 0 || r >= nrows) bad = true;
-    else atomicAdd(&lh[bin_of((uint32_t)r, s2, P1, tab)], 1u);
   }
   if (bad) atomicOr(flags, kFlagBadRow);
   __syncthreads();
@@ -270,12 +264,12 @@ static size_t tile_lds_bytes(int P, bool has_val, bool has_fine, bool hot = fals
          (hot ? sizeof(uint32_t) * kHotBins : 0);
 }
 
-// Pass 1: block b owns stream chunk [b*chunk, (b+1)*chunk); output region of
+// Pass 1: block b owns tiles b, b + NB, ... of the stream; output region of
 // (coarse bin, block) starts at O1[bin*NB + b].
 // With hotkey: bins [P1, P1 + kHotBins) are hot owners, whose keys (and
 // values) go straight to okey_hot / oval_hot -- their final place.
 __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row, const int64_t* key, const float* val,
-                                                             int64_t n, int64_t chunk, int s2, int P1, int64_t nrows,
+                                                             int64_t n, int s2, int P1, int64_t nrows,
                                                              const uint32_t* O1, int NB, uint16_t* ofine,
                                                              int64_t* okey, float* oval,
                                                              const unsigned long long* hotkey, int64_t* okey_hot,
@@ -287,14 +281,16 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
   const int tid = threadIdx.x;
   if (tab) load_hot_table(hotkey, tab);
   for (int b = tid; b < P; b += kPartThreads) L.cursor[b] = O1[(int64_t)blockIdx.x * P + b];
-  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
   const uint32_t fmask = (1u << s2) - 1u;
   for (int b = tid; b < P; b += kPartThreads) L.hist[b] = 0;
+  // tiles blockIdx.x, + NB, + 2 NB, ... (k_p1_hist's assignment)
+  const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
   // software pipeline: the next tile's loads are issued before this tile's
   // write-out and stay in flight across the LDS-only barriers
   int64_t rr[kPartPer], kk[kPartPer];
   float vv[kPartPer];
-  auto load = [&](int64_t tb) {
+  auto load = [&](int64_t t) {
+    const int64_t tb = t * kPartTile, hi = min(n, tb + kPartTile);
 #pragma unroll
     for (int u = 0; u < kPartPer; ++u) {
       const int64_t e = tb + tid + (int64_t)u * kPartThreads;
@@ -306,11 +302,11 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
       }
     }
   };
-  if (lo < hi) load(lo);
+  if ((int64_t)blockIdx.x < ntiles) load(blockIdx.x);
   __syncthreads();
-  for (int64_t tb = lo; tb < hi; tb += kPartTile) {
+  for (int64_t t = blockIdx.x; t < ntiles; t += NB) {
 #if !CMS_P1_PREFETCH
-    if (tb != lo) load(tb);
+    if (t != (int64_t)blockIdx.x) load(t);
 #endif
     uint32_t bb[kPartPer], bn[kPartPer], rk[kPartPer];
 #pragma unroll
@@ -336,14 +332,14 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
       }
     }
 #if CMS_P1_PREFETCH
-    if (tb + kPartTile < hi) load(tb + kPartTile);
+    if (t + NB < ntiles) load(t + NB);
 #endif
     lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t bin = L.bin[i];
       uint32_t g = L.cursor[bin] + (i - L.off[bin]);
 #ifdef CMS_PART_LINEAR  // bound analysis only: contiguous instead of per-bin destinations
-      g = (uint32_t)(tb + i);
+      g = (uint32_t)(t * kPartTile + i);
 #endif
 #ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
       if (g != 0xFFFFFFFFu) continue;
@@ -443,18 +439,20 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
 // offsets in parallel (k_p2_offsets).
 constexpr int kP2Split = 16;
 
+template <int SPLIT>
 __device__ __forceinline__ void p2_chunk(const uint32_t* blkStart, int b, int c, uint32_t& ka, uint32_t& kb) {
   const uint32_t k0 = blkStart[b], k1 = blkStart[b + 1];
-  const uint32_t per = (k1 - k0 + kP2Split - 1) / kP2Split;
+  const uint32_t per = (k1 - k0 + SPLIT - 1) / SPLIT;
   ka = min(k1, k0 + (uint32_t)c * per);
   kb = min(k1, ka + per);
 }
 
+template <int SPLIT>
 __global__ __launch_bounds__(1024) void k_p2_colsum(const uint32_t* H2, const uint32_t* blkStart, int P2,
                                                     uint32_t* PS) {
-  const int b = blockIdx.x / kP2Split, c = blockIdx.x % kP2Split;
+  const int b = blockIdx.x / SPLIT, c = blockIdx.x % SPLIT;
   uint32_t ka, kb;
-  p2_chunk(blkStart, b, c, ka, kb);
+  p2_chunk<SPLIT>(blkStart, b, c, ka, kb);
   for (int f = threadIdx.x; f < P2; f += blockDim.x) {
     uint32_t T = 0;
 #pragma unroll 8
@@ -506,13 +504,14 @@ __global__ __launch_bounds__(1024) void k_p2_scan(const uint32_t* binStart, int 
 // Pass 1 has ONE segment of NB blocks over P bins: the bin totals' exclusive
 // scan gives bs1[0..P] (bs1[P] = every valid pair), and the chunk sums become
 // chunk prefixes for k_p2_offsets.  One block.
+constexpr int kP1Split = 16;  // pass-1 chunks of the block column (NB <= 2048 rows: 128 per chunk)
 __global__ __launch_bounds__(1024) void k_p1_scan(int P, uint32_t* PS, uint32_t* bs1) {
   __shared__ uint32_t sc[1024 / 64 + 1];
   __shared__ uint32_t tots[kMaxBins];
   for (int f = threadIdx.x; f < P; f += blockDim.x) {
     uint32_t T = 0;
 #pragma unroll
-    for (int c = 0; c < kP2Split; ++c) T += PS[(int64_t)c * P + f];
+    for (int c = 0; c < kP1Split; ++c) T += PS[(int64_t)c * P + f];
     tots[f] = T;
   }
   __syncthreads();
@@ -532,8 +531,8 @@ __global__ __launch_bounds__(1024) void k_p1_scan(int P, uint32_t* PS, uint32_t*
     const uint32_t base = tots[f];
     bs1[f] = base;
     uint32_t run = base;
-#pragma unroll
-    for (int c = 0; c < kP2Split; ++c) {
+#pragma unroll 8
+    for (int c = 0; c < kP1Split; ++c) {
       const uint32_t t = PS[(int64_t)c * P + f];
       PS[(int64_t)c * P + f] = run;
       run += t;
@@ -542,11 +541,12 @@ __global__ __launch_bounds__(1024) void k_p1_scan(int P, uint32_t* PS, uint32_t*
   if (threadIdx.x == 0) bs1[P] = total;
 }
 
+template <int SPLIT>
 __global__ __launch_bounds__(1024) void k_p2_offsets(const uint32_t* H2, const uint32_t* blkStart, int P2,
                                                      const uint32_t* PS, uint32_t* O2) {
-  const int b = blockIdx.x / kP2Split, c = blockIdx.x % kP2Split;
+  const int b = blockIdx.x / SPLIT, c = blockIdx.x % SPLIT;
   uint32_t ka, kb;
-  p2_chunk(blkStart, b, c, ka, kb);
+  p2_chunk<SPLIT>(blkStart, b, c, ka, kb);
   for (int f = threadIdx.x; f < P2; f += blockDim.x) {
     uint32_t run = PS[(int64_t)blockIdx.x * P2 + f];
     uint32_t k = ka;
@@ -683,8 +683,7 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     return set_error(CMS_E_PARAM, "num_owners %lld too large for the partition", (long long)n);
   if (hot && (P1 + kHotBins > kMaxBins || out_rows || n >= (int64_t(1) << 31))) return kNoSpans;
   const int P = P1 + (hot ? kHotBins : 0);  // pass-1 bins
-  const int64_t chunk1 = std::max<int64_t>(4 * kPartTile, (npairs + CMS_P1_BLOCKS - 1) / CMS_P1_BLOCKS);
-  const int NB = (int)((npairs + chunk1 - 1) / chunk1);
+  const int NB = (int)std::max<int64_t>(1, std::min<int64_t>(CMS_P1_BLOCKS, (npairs + kPartTile - 1) / kPartTile));
   const int64_t CH2 = 4 * kPartTile;
   const int64_t nb2max = npairs / CH2 + P1 + 1;
 
@@ -700,7 +699,7 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
   }
   const int64_t L1 = (int64_t)P * NB, L2 = nb2max * P2;
   const size_t hist_words = (size_t)(2 * L1 + 2 * L2 + 2 * (P1 + 1) + 64) + (size_t)P1 * kP2Split * P2 +
-                            (size_t)kP2Split * P + (P + 1) + 2;
+                            (size_t)kP1Split * P + (P + 1) + 2;
   CMS_HIP(h->ws_hist.ensure(sizeof(uint32_t) * hist_words));
   uint32_t* H1 = h->ws_hist.as<uint32_t>();
   uint32_t* O1 = H1 + L1;
@@ -709,8 +708,8 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
   uint32_t* binStart = O2 + L2;
   uint32_t* blkStart = binStart + (P1 + 1);
   uint32_t* PS = blkStart + (P1 + 1) + 64;  // [P1][kP2Split][P2] chunk column sums / prefixes
-  uint32_t* PS1 = PS + (size_t)P1 * kP2Split * P2;  // [kP2Split][P] pass-1 chunk sums / prefixes
-  uint32_t* bs1 = PS1 + (size_t)kP2Split * P;     // [P + 1] pass-1 bin starts
+  uint32_t* PS1 = PS + (size_t)P1 * kP2Split * P2;  // [kP1Split][P] pass-1 chunk sums / prefixes
+  uint32_t* bs1 = PS1 + (size_t)kP1Split * P;     // [P + 1] pass-1 bin starts
   uint32_t* seg1 = bs1 + (P + 1);                 // {0, NB}: pass 1 is one segment of NB blocks
 
   uint16_t* fine = h->ws_p1_row.as<uint16_t>();
@@ -743,23 +742,23 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
                          h->stream, cnt, n, tau, slotkey);
     }
     hipLaunchKernelGGL(k_p1_hist, dim3(NB), dim3(256), sizeof(uint32_t) * (P + (hot ? kHotBins : 0)), h->stream, d_row,
-                       npairs, chunk1, s2, P1, n, H1, NB, h->d_flags, slotkey);
+                       npairs, s2, P1, n, H1, NB, h->d_flags, slotkey);
     // block-major (block, bin) offsets: chunked column sums, one scan over
     // the bins, chunk prefixes (the pass-2 kernels with one segment)
     CMS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(seg1), 0, 1, h->stream));
     CMS_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(seg1 + 1), NB, 1, h->stream));
-    hipLaunchKernelGGL(k_p2_colsum, dim3(kP2Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1);
+    hipLaunchKernelGGL(k_p2_colsum<kP1Split>, dim3(kP1Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1);
     hipLaunchKernelGGL(k_p1_scan, dim3(1), dim3(1024), 0, h->stream, P, PS1, bs1);
-    hipLaunchKernelGGL(k_p2_offsets, dim3(kP2Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1, O1);
+    hipLaunchKernelGGL(k_p2_offsets<kP1Split>, dim3(kP1Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1, O1);
     hipLaunchKernelGGL(k_p1_scatter, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P, d_val != nullptr, true, hot),
-                       h->stream, d_row, d_key, d_val, npairs, chunk1, s2, P1, n, O1, NB, fine, key1, val1, slotkey,
+                       h->stream, d_row, d_key, d_val, npairs, s2, P1, n, O1, NB, fine, key1, val1, slotkey,
                        ckey, cval);
     hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, bs1, P1, CH2, binStart, blkStart);
     hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)nb2max), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,
                        binStart, blkStart, P1, CH2, P2, H2);
-    hipLaunchKernelGGL(k_p2_colsum, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS);
+    hipLaunchKernelGGL(k_p2_colsum<kP2Split>, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS);
     hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, binStart, P1, P2, n, PS, coff);
-    hipLaunchKernelGGL(k_p2_offsets, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS, O2);
+    hipLaunchKernelGGL(k_p2_offsets<kP2Split>, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS, O2);
     hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2, d_val != nullptr, false), h->stream, fine,
                        key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     if (hot) {
