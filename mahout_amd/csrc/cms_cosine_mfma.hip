@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cfloat>
 #include <cstdlib>
 #include <vector>
@@ -669,7 +670,15 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
 #undef UOFF
 
   AccT acc[2][2];
-  double mn[2][2][4 * OG];
+  // running Math.min of each pair.  Single-limb rows keep the fp64 value.
+  // Multi-limb rows keep (exact dot << 5 | sketch row) of the row holding it
+  // (k_cosine_sym's packed state, 64-bit: dots < 2^53): rows are compared by
+  // fp32 estimates, exactly only inside a 2^-17 margin, and the value is
+  // divided out once, exactly, at the end.
+  constexpr bool kPacked = LS > 1;
+  using StT = typename std::conditional<kPacked, uint64_t, double>::type;
+  constexpr StT kEmptySt = kPacked ? (StT)~0ULL : (StT)DBL_MAX;
+  StT mn[2][2][4 * OG];
   uint64_t alive = ~0ULL;  // bit (i*2+j)*16 + og*4 + q: the pair may still be admitted
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -678,7 +687,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
 #pragma unroll
-      for (int e = 0; e < 4 * OG; ++e) mn[i][j][e] = DBL_MAX;
+      for (int e = 0; e < 4 * OG; ++e) mn[i][j][e] = kEmptySt;
     }
 
 #pragma unroll
@@ -771,22 +780,42 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
           for (int q = 0; q < 4; ++q) {
             const int ol = (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
             const double sa = s_sa[r * kTA + ol];
+            if constexpr (!kPacked) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                if (screen && !((alive >> ((i * 2 + j) * 16 + og * 4 + q)) & 1ULL)) continue;
+                const double den = __dmul_rn(sa, sb[j]);
+                const double v = __ddiv_rn((double)acc[i][j][q + 4 * og], den);
+                StT& m = mn[i][j][og * 4 + q];
+                m = (den != 0.0 && v < m) ? v : m;
+              }
+            } else {
+            if (sa == 0.0) continue;  // den == 0: this sketch row does not qualify
+            const float ra = __builtin_amdgcn_rcpf((float)sa);
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
               if (screen && !((alive >> ((i * 2 + j) * 16 + og * 4 + q)) & 1ULL)) continue;
-              double valueAB;
-              if constexpr (LS == 1) {
-                valueAB = (double)acc[i][j][q + 4 * og];
-              } else {
-                int64_t dot = 0;
+              if (sb[j] == 0.0) continue;
+              int64_t dot = 0;
 #pragma unroll
-                for (int l = 0; l < LS; ++l) dot += (int64_t)acc[i][j][q + 4 * (og * LS + l)] << (7 * l);
-                valueAB = (double)dot;
+              for (int l = 0; l < LS; ++l) dot += (int64_t)acc[i][j][q + 4 * (og * LS + l)] << (7 * l);
+              StT& m = mn[i][j][og * 4 + q];
+              bool take = m == kEmptySt;
+              if (!take) {
+                const int col = wc * 64 + j * 32 + (lane & 31);
+                const int r0 = (int)(m & 31ULL);
+                const int64_t d0 = (int64_t)(m >> 5);
+                const double sa0 = s_sa[r0 * kTA + ol], sb0 = s_sb[r0 * kTB + col];
+                const float est = (float)dot * ra * __builtin_amdgcn_rcpf((float)sb[j]);
+                const float est0 = (float)d0 * __builtin_amdgcn_rcpf((float)sa0) * __builtin_amdgcn_rcpf((float)sb0);
+                if (est < est0 * (1.0f - 0x1p-17f)) {
+                  take = true;
+                } else if (est <= est0 * (1.0f + 0x1p-17f)) {  // too close for fp32: the exact values
+                  take = __ddiv_rn((double)dot, __dmul_rn(sa, sb[j])) < __ddiv_rn((double)d0, __dmul_rn(sa0, sb0));
+                }
               }
-              const double den = __dmul_rn(sa, sb[j]);
-              const double v = __ddiv_rn(valueAB, den);
-              double& m = mn[i][j][og * 4 + q];
-              m = (den != 0.0 && v < m) ? v : m;
+              if (take) m = ((uint64_t)dot << 5) | (uint64_t)r;
+            }
             }
           }
       }
@@ -816,8 +845,18 @@ __global__ __launch_bounds__(512, 1) void k_cosine_big(BigArgs g) {
           if (ai >= a_owners || bi >= b_rows) continue;
           if (screen && !((alive >> ((i * 2 + j) * 16 + og * 4 + q)) & 1ULL)) continue;  // never admitted
           const int64_t ap = a_pos0 + ai;
-          double rr = mn[i][j][og * 4 + q];
-          rr = rr == DBL_MAX ? __builtin_nan("") : rr;
+          const StT m = mn[i][j][og * 4 + q];
+          double rr = __builtin_nan("");
+          if constexpr (kPacked) {
+            if (m != kEmptySt) {
+              const int r0 = (int)(m & 31ULL);
+              const int ol = (wr * 64 + i * 32) / LS + og * 8 + q + 4 * (lane >> 5);
+              rr = __ddiv_rn((double)(int64_t)(m >> 5),
+                             __dmul_rn(s_sa[r0 * kTA + ol], s_sb[r0 * kTB + wc * 64 + j * 32 + (lane & 31)]));
+            }
+          } else {
+            rr = m == kEmptySt ? rr : m;
+          }
           if (rr == rr) {
             if (g.weighted) rr = rr < 0.0 ? -1.0 : 1.0;  // scaleFactor 1 - 1/(0+1) = 0
             if (rr < -1.0) rr = -1.0;

@@ -43,7 +43,13 @@
 
 namespace cms {
 
-constexpr int kSA = 256, kSB = 192;  // A panel rows x B panel rows per workgroup
+#ifndef CMS_SYM_WAVES
+#define CMS_SYM_WAVES 8
+#endif
+constexpr int kSymNW = CMS_SYM_WAVES;  // waves per workgroup (8: two per SIMD, 4: one)
+// A panel rows x B panel rows per workgroup: 256 x 192 on 8 waves (64 x 96 per
+// wave), 192 x 192 on 4 waves (96 x 96 per wave, 512 registers)
+constexpr int kSA = kSymNW == 4 ? 192 : 256, kSB = 192;
 constexpr int kPA = kSymBlk / kSA;   // 3 A panels per block
 constexpr int kPB = kSymBlk / kSB;   // 4 B panels per block
 constexpr int kSub = kPA * kPB;      // 12 workgroups per block pair
@@ -55,15 +61,19 @@ __device__ __forceinline__ uint32_t block_map(int bx, int nblk) {
   return (uint32_t)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3));
 }
 
-template <int NSTAGE, int BK, int FMT>
-__global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
+template <int NSTAGE, int BK, int FMT, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
   using AccT = typename AccOf<FMT>::type;
+  // NW waves in (NW/2) x 2; a wave holds TI x 3 MFMA tiles (TI = 2 at 8 waves;
+  // 3 at 4 waves: one wave per SIMD with 512 registers, 6 fragments per 9 MFMAs)
+  constexpr int NT = 64 * NW, TI = kSA / (NW / 2) / 32, WROWS = 32 * TI, NAW = (TI * 48 + 31) / 32;
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int kStageA = kSA * BK, kStageB = kSB * BK, kStage = kStageA + kStageB;
   constexpr int RPI = 1024 / BK;                 // rows per 1-KiB LDS-DMA instruction
-  constexpr int OPA = kSA / RPI / 8;             // A instructions per wave per stage
+  constexpr int OPA = kSA / RPI / NW;            // A instructions per wave per stage
   constexpr int RB = kSB / RPI;                  // B instructions per stage (all waves)
-  constexpr int OPB_HI = (RB + 7) / 8, OPB_LO = RB / 8;  // waves < RB % 8 issue one more
-  static_assert(kSA % (8 * RPI) == 0, "A rows per round");
+  constexpr int OPB_HI = (RB + NW - 1) / NW, OPB_LO = RB / NW;  // waves < RB % NW issue one more
+  static_assert(kSA % (NW * RPI) == 0, "A rows per round");
   extern __shared__ __align__(16) unsigned char lds[];
   const int depth = g.depth;
   double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][256]
@@ -111,7 +121,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
   if (diag && a_pos0 >= b_pos0 + kSB - 1) return;  // every pair of the tile has a >= b
 
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid >> 1, wc = wid & 1;  // wave rows [wr * WROWS, +WROWS), columns [wc * 96, +96)
   const int64_t rs = g.rs;
   const int cstages = g.kw / BK;
   const int total = depth * cstages;
@@ -120,7 +130,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
   // instruction; past-the-end owners land as zeros), thresholds as fp16
   // rounded toward -inf (never above the threshold)
   constexpr int kPartsA = kSA / 32, kParts = (kSA + kSB) / 32;
-  for (int k = wid; k < kParts * depth; k += 8) {
+  for (int k = wid; k < kParts * depth; k += NW) {
     const int r = k / kParts, part = k % kParts;
     const bool isA = part < kPartsA;
     const int64_t first = isA ? part * 32 : (part - kPartsA) * 32;
@@ -131,7 +141,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
     double* dst = isA ? s_sa + r * kSA + first : s_sb + r * kSB + first;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsn, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
   }
-  for (int i = tid; i < kSA + kSB; i += 512) {
+  for (int i = tid; i < kSA + kSB; i += NT) {
     const bool isA = i < kSA;
     const int64_t o = isA ? i : i - kSA;
     const int64_t lim = isA ? a_rows : b_rows;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + (a_pos0 - g.img0) * rs), (short)0, (int)recA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + (b_pos0 - g.img0) * rs), (short)0, (int)recB, 0x00020000);
-  // instruction u of wave wid fills panel rows [(wid + 8u) RPI, +RPI); lane i
+  // instruction u of wave wid fills panel rows [(wid + NW u) RPI, +RPI); lane i
   // lands at byte 16 i (row (wid + 8u) RPI + i / CPR, slot i % CPR) and
   // fetches the chunk the XOR swizzle puts there
   constexpr int CPR = BK / 16;
@@ -155,29 +165,31 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
   const int32_t chunk = (BK == 128 ? (slot ^ ((srow >> 1) & 7)) : (slot ^ ((srow >> 2) & 3))) << 4;
   const int32_t bstep = kImgBlk * (int32_t)rs;
   const int32_t vo = (srow / kImgBlk) * bstep + (srow % kImgBlk) * BK + chunk;
-  constexpr int UROWS = 8 * RPI;  // panel rows per round of instructions (a multiple of kImgBlk)
+  constexpr int UROWS = NW * RPI;  // panel rows per round of instructions (a multiple of kImgBlk)
   static_assert(UROWS % kImgBlk == 0, "rounds start on image blocks");
-  const int opb = wid < (RB % 8 == 0 ? 8 : RB % 8) ? OPB_HI : OPB_LO;
+  const int opb = wid < (RB % NW == 0 ? NW : RB % NW) ? OPB_HI : OPB_LO;
   auto issue = [&](int s) {
     const int32_t koff = s * (kImgBlk * BK);
     unsigned char* st = lds + (s % NSTAGE) * kStage;
 #pragma unroll
     for (int u = 0; u < OPA; ++u)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + 8 * u) * 1024),
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + NW * u) * 1024),
                                                16, vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
 #pragma unroll
     for (int u = 0; u < OPB_HI; ++u)
       if (u < opb)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + 8 * u) * 1024), 16,
+            rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + NW * u) * 1024), 16,
             vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
   };
 
-  AccT acc[2][3];
-  uint32_t st[2][3][16];
-  uint32_t alive[3] = {~0u, ~0u, ~0u};  // bit (i*3+j)*16 + e: the pair may still be admitted
+  AccT acc[TI][3];
+  uint32_t st[TI][3][16];
+  uint32_t alive[NAW];  // bit (i*3+j)*16 + e: the pair may still be admitted
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int w = 0; w < NAW; ++w) alive[w] = ~0u;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -208,22 +220,22 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
     const unsigned char* B = A + kStageA;
 #if CMS_SYM_PREFETCH
     // fragments of k-step ks+1 are read while k-step ks's MFMAs run
-    i8x16 fa[2][2], fb[2][3];
+    i8x16 fa[2][TI], fb[2][3];
     auto frag = [&](int ks, int b) {
       const int ch = 2 * ks + (lane >> 5);
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         fb[b][j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[b][i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
+      for (int i = 0; i < TI; ++i)
+        fa[b][i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * WROWS + i * 32 + (lane & 31), ch));
     };
     frag(0, 0);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       if (ks + 1 < BK / 32) frag(ks + 1, (ks + 1) & 1);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[ks & 1][i], fb[ks & 1][j], acc[i][j]);
     }
@@ -232,15 +244,15 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
     for (int ks = 0; ks < BK / 32; ++ks) {
       // the k-step's five fragments first, then its six MFMAs
       const int ch = 2 * ks + (lane >> 5);
-      i8x16 fb[3], fa[2];
+      i8x16 fb[3], fa[TI];
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
+      for (int i = 0; i < TI; ++i)
+        fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * WROWS + i * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
     }
@@ -250,7 +262,10 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
     // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
     const double* sa_r = s_sa + r * kSA;
     const double* sb_r = s_sb + r * kSB;
-    if (__any((alive[0] | alive[1] | alive[2]) != 0u)) {
+    uint32_t any_alive = 0u;
+#pragma unroll
+    for (int w = 0; w < NAW; ++w) any_alive |= alive[w];
+    if (__any(any_alive != 0u)) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int col = wc * 96 + j * 32 + (lane & 31);
@@ -258,13 +273,13 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
         const float rb = __builtin_amdgcn_rcpf((float)sb);
         const float tb = __half2float(s_tb[col]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < TI; ++i) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int bit = (i * 3 + j) * 16 + e;
             const uint32_t m = 1u << (bit & 31);
             if (!(alive[bit >> 5] & m)) continue;
-            const int row = wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            const int row = wr * WROWS + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
             const double sa = sa_r[row];
             if (sa == 0.0 || sb == 0.0) continue;  // den == 0: this sketch row does not qualify
             const uint32_t ab = (uint32_t)acc[i][j][e];
@@ -294,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j)
 #pragma unroll
@@ -308,14 +323,14 @@ __global__ __launch_bounds__(512, 1) void k_cosine_sym(SymArgs g) {
     const int64_t bp = b_pos0 + col;
     const double tb = col < b_rows ? g.thr[bp] : 0.0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int bit = (i * 3 + j) * 16 + e;
         if (!((alive[bit >> 5] >> (bit & 31)) & 1u)) continue;
         const uint32_t sv = st[i][j][e];
         if (sv == kEmpty) continue;  // NaN: never offered
-        const int row = wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int row = wr * WROWS + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
         if (row >= a_rows || col >= b_rows) continue;
         const int64_t ap = a_pos0 + row;
         if (ap == bp || (diag && ap > bp)) continue;
@@ -378,15 +393,15 @@ int launch_sym(cms_handle* h, SymArgs g, int fmt, int64_t pair_slots) {
   if (g.nblk <= 0) return CMS_OK;
   const size_t bytes = sym_lds_bytes(g.depth);
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 0, kSymNW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 1, kSymNW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     return true;
   }();
   (void)attr;
-  if (fmt == 1) hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 1>), dim3(g.nblk), dim3(512), bytes, h->stream, g);
-  else hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 0>), dim3(g.nblk), dim3(512), bytes, h->stream, g);
+  if (fmt == 1) hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 1, kSymNW>), dim3(g.nblk), dim3(64 * kSymNW), bytes, h->stream, g);
+  else hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 0, kSymNW>), dim3(g.nblk), dim3(64 * kSymNW), bytes, h->stream, g);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
