@@ -37,8 +37,8 @@
 #include "cms_internal.h"
 #include "cms_mfma.h"
 
-#ifndef CMS_SYM_PREFETCH
-#define CMS_SYM_PREFETCH 0  // 1: double-buffered fragments across k-steps
+#ifndef CMS_SYM_SCHED
+#define CMS_SYM_SCHED 2  // 0: refill loads before the MFMAs, 1: interleaved with them, 2: also the next k-step's fragments
 #endif
 
 namespace cms {
@@ -168,19 +168,26 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
   constexpr int UROWS = NW * RPI;  // panel rows per round of instructions (a multiple of kImgBlk)
   static_assert(UROWS % kImgBlk == 0, "rounds start on image blocks");
   const int opb = wid < (RB % NW == 0 ? NW : RB % NW) ? OPB_HI : OPB_LO;
-  auto issue = [&](int s) {
+  // stage s's data into ring slot `slot`; `part` 1: the loads every wave
+  // issues, 2: the extra B load of waves < RB % NW, 3: both
+  auto issue = [&](int s, int slot, int part) {
     const int32_t koff = s * (kImgBlk * BK);
-    unsigned char* st = lds + (s % NSTAGE) * kStage;
+    unsigned char* st = lds + (slot % NSTAGE) * kStage;
+    if (part & 1) {
 #pragma unroll
-    for (int u = 0; u < OPA; ++u)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + NW * u) * 1024),
-                                               16, vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
+      for (int u = 0; u < OPA; ++u)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(st + (wid + NW * u) * 1024),
+                                                 16, vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
 #pragma unroll
-    for (int u = 0; u < OPB_HI; ++u)
-      if (u < opb)
+      for (int u = 0; u < OPB_LO; ++u)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + NW * u) * 1024), 16,
             vo + (u * UROWS / kImgBlk) * bstep, koff, 0, 0);
+    }
+    if ((part & 2) && OPB_HI > OPB_LO && opb == OPB_HI)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsB, (__attribute__((address_space(3))) void*)(st + kStageA + (wid + NW * OPB_LO) * 1024), 16,
+          vo + (OPB_LO * UROWS / kImgBlk) * bstep, koff, 0, 0);
   };
 
   AccT acc[TI][3];
@@ -201,45 +208,76 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
 
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
-    if (s < total) issue(s);
+#if CMS_SYM_SCHED
+    issue(min(s, total - 1), s, 3);  // every iteration issues: one vmcnt count for all stages
+#else
+    if (s < total) issue(s, s, 3);
+#endif
 
   for (int s = 0; s < total; ++s) {
     // stage s landed: at most the (NSTAGE-2) younger stages stay in flight
     asm volatile("" ::: "memory");
+#if CMS_SYM_SCHED
+    if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 2)>();
+    else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 2)>();
+#else
     if (s + NSTAGE - 2 < total) {
       if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 2)>();
       else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 2)>();
     } else {
       wait_vmcnt<0>();
     }
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);  // refill the slot read in iteration s-1
     const unsigned char* A = lds + (s % NSTAGE) * kStage;
     const unsigned char* B = A + kStageA;
-#if CMS_SYM_PREFETCH
-    // fragments of k-step ks+1 are read while k-step ks's MFMAs run
-    i8x16 fa[2][TI], fb[2][3];
-    auto frag = [&](int ks, int b) {
-      const int ch = 2 * ks + (lane >> 5);
+#if CMS_SYM_SCHED
+    // refill the slot read in iteration s-1 (past the last stage: a repeat of
+    // it into that free slot, so every iteration issues the same loads), the
+    // common loads between the first k-step's MFMAs, the extra one after the MFMAs
+    {
+      const int sn = min(s + NSTAGE - 1, total - 1);
 #pragma unroll
-      for (int j = 0; j < 3; ++j)
-        fb[b][j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        const int ch = 2 * ks + (lane >> 5);
+        i8x16 fb[3], fa[TI];
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
-        fa[b][i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * WROWS + i * 32 + (lane & 31), ch));
-    };
-    frag(0, 0);
+        for (int j = 0; j < 3; ++j)
+          fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      if (ks + 1 < BK / 32) frag(ks + 1, (ks + 1) & 1);
+        for (int i = 0; i < TI; ++i)
+          fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * WROWS + i * 32 + (lane & 31), ch));
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[ks & 1][i], fb[ks & 1][j], acc[i][j]);
+          for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
+        if (ks == 0) issue(sn, s + NSTAGE - 1, 1);
+      }
+      constexpr int NV = OPA + OPB_LO, NF = TI + 3, NM = TI * 3, KS = BK / 32;
+      static_assert(NV <= NM * KS && NF >= 3 && NM >= 4, "schedule shape");
+      // per k-step: its MFMAs one at a time, the refill loads one after each
+      // MFMA from the first on; CMS_SYM_SCHED 2 also reads the next k-step's
+      // fragments behind the last four MFMAs (as the registers they replace free up)
+      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);  // k-step 0 fragments
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (ks * NM + m < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          if (CMS_SYM_SCHED == 2 && ks + 1 < KS && m >= NM - 4) {
+            if (m == NM - 1) __builtin_amdgcn_sched_group_barrier(0x100, NF - 3, 0);
+            else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+        }
+        if (CMS_SYM_SCHED != 2 && ks + 1 < KS) __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+      }
+      issue(sn, s + NSTAGE - 1, 2);
     }
 #else
+    if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1, s + NSTAGE - 1, 3);  // refill the slot read in iteration s-1
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       // the k-step's five fragments first, then its six MFMAs
@@ -315,6 +353,9 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
   }
+#if CMS_SYM_SCHED
+  wait_vmcnt<0>();  // the repeat loads land before the workgroup's LDS is released
+#endif
 
   // ---- the exact value of each surviving pair, offered to both lists ----
 #pragma unroll
@@ -360,9 +401,6 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
 #endif
 #ifndef CMS_SYM_BK
 #define CMS_SYM_BK 64
-#endif
-#ifndef CMS_SYM_PREFETCH
-#define CMS_SYM_PREFETCH 0
 #endif
 constexpr int kSymNS = CMS_SYM_NS, kSymBK = CMS_SYM_BK;  // ring depth, bytes per row per stage
 
