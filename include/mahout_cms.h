@@ -255,6 +255,19 @@ int cms_top_k_all_partial(cms_handle* h, int32_t k, int32_t shard, int32_t nshar
  * [nparts][num_owners]) into the final lists (nparts * k <= 1024). */
 int cms_top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* ids, const double* scores,
                     const int32_t* counts, int64_t* out_ids, double* out_scores, int32_t* out_counts);
+/* The periodic top-k refresh of a streaming table (config 5; the Refreshable
+ * contract of the precomputed similarities, T/common/Refreshable.java:51,
+ * feeding GenericItemSimilarity): returns exactly what cms_top_k_all returns
+ * for the current table.  The first call (or one with another k, or after a
+ * CSR ingest, cms_reset or the first multi-rank merge) runs the whole job and
+ * keeps every owner's list 2k deep on the device; later calls recompute only
+ * the pairs with an owner a COO ingest touched since, fold them into the kept
+ * lists, and recompute whole any list that lost its exactness margin.
+ * Collective like cms_top_k_all with a communicator. */
+int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts);
+/* Statistics of the last cms_top_k_refresh: owners touched (num_owners for a
+ * whole job), lists recomputed whole, whole jobs so far. */
+int cms_refresh_stats(cms_handle* h, int64_t* touched, int64_t* redone, int64_t* full_jobs);
 
 /* cms_top_k_all written as FileSimilarItemsWriter does
  * (T/impl/similarity/precompute/FileSimilarItemsWriter.java:50-61): one line

@@ -41,7 +41,7 @@ EXPORTS = [
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
     "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities", "cms_write_similarities_threshold",
-    "cms_comm_init_transport", "cms_read_counters_device",
+    "cms_comm_init_transport", "cms_read_counters_device", "cms_top_k_refresh", "cms_refresh_stats",
 ]
 
 
@@ -123,6 +123,8 @@ _SIGS = {
     "cms_top_k_all_partial": (_int, [_vp, _i32, _i32, _i32, _vp, _vp, _vp]),
     "cms_top_k_merge": (_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cms_top_k_all": (_int, [_vp, _i32, _vp, _vp, _vp]),
+    "cms_top_k_refresh": (_int, [_vp, _i32, _vp, _vp, _vp]),
+    "cms_refresh_stats": (_int, [_vp, _vp, _vp, _vp]),
     "cms_read_counters": (_int, [_vp, _i64, _i64, _vp]),
     "cms_get_stats": (_int, [_vp, ctypes.POINTER(CmsStats)]),
     "cms_set_timing": (_int, [_vp, _i32]),

@@ -383,7 +383,8 @@ void cms_destroy(cms_handle* h) {
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
                   &h->ws_f4, &h->ws_i8blk, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
                   &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist,
-                  &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked};
+                  &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked, &h->rf_ids, &h->rf_sc, &h->rf_cnt,
+                  &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -645,6 +646,7 @@ int cms_ingest_csr_device(cms_handle* h, const int64_t* d_offsets, const int64_t
     h->pairs_ingested = np;
     return CMS_OK;
   }
+  h->rf_valid = false;  // CSR ingest does not mark touched owners: the next refresh is a full job
   int rc = h->f64 ? f64_ingest_csr(h, d_offsets, d_keys, d_vals) : ingest_csr_device(h, d_offsets, d_keys, d_vals, np);
   if (rc == CMS_OK) {
     h->pairs_ingested += np;
@@ -665,6 +667,7 @@ int cms_reset(cms_handle* h) {
   h->merged = false;
   h->ext_merged = false;
   h->dlog_n = 0;
+  h->rf_valid = false;
   return CMS_OK;
 }
 
@@ -675,7 +678,8 @@ int cms_release_scratch(cms_handle* h) {
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
                   &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_csr_hi, &h->ws_hotpart, &h->ws_hist, &h->ws_hot, &h->ws_query,
                   &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand, &h->ws_srow,
-                  &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked};
+                  &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked, &h->rf_ids, &h->rf_sc, &h->rf_cnt,
+                  &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};
   for (DevBuf* b : ws) b->release();
   return CMS_OK;
 }
@@ -782,6 +786,7 @@ int cms_finalize(cms_handle* h) {
     auto sum = [h](uint64_t* buf, int64_t count) -> int { return coll_allreduce_u64(h, buf, count); };
     int rc = merge_packed(h, sum);
     if (rc) return rc;
+    h->rf_valid = false;  // every rank's table changed wholesale
     h->merged = true;
     h->dlog_n = 0;
   }
@@ -1038,6 +1043,50 @@ int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t 
   return top_k_host(h, row_begin, row_count, k, ids, scores, counts);
 }
 
+extern "C++" {
+namespace cms {
+int top_k_all_job(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  const int64_t n = h->n;
+  if (!h->multi()) return top_k_all(h, k, d_ids, d_scores, d_counts);
+  // one process per GPU: rank r computes shard r of the pairs, then one
+  // all-gather of the partial lists over xGMI and an exact merge (in rounds
+  // of kCandCap / k lists when world * k exceeds a merge workgroup's LDS)
+  const int G = h->world;
+  DevBuf g_ids, g_sc, g_cnt;
+  CMS_HIP(g_ids.ensure(sizeof(int64_t) * n * k * G));
+  CMS_HIP(g_sc.ensure(sizeof(double) * n * k * G));
+  CMS_HIP(g_cnt.ensure(sizeof(int32_t) * n * G));
+  int rc = top_k_all(h, k, d_ids, d_scores, d_counts, h->rank, G);
+  if (rc) return rc;
+  {
+    TimedScope ts(h, "topk_allgather");
+    if ((rc = coll_allgather(h, d_ids, g_ids.ptr, (int64_t)sizeof(int64_t) * n * k)) ||
+        (rc = coll_allgather(h, d_scores, g_sc.ptr, (int64_t)sizeof(double) * n * k)) ||
+        (rc = coll_allgather(h, d_counts, g_cnt.ptr, (int64_t)sizeof(int32_t) * n)))
+      return rc;
+  }
+  rc = top_k_merge(h, k, G, g_ids.as<int64_t>(), g_sc.as<double>(), g_cnt.as<int32_t>(), d_ids, d_scores, d_counts);
+  if (rc == CMS_OK) {
+    const hipError_t e = hipStreamSynchronize(h->stream);  // the gather buffers free on return
+    if (e != hipSuccess) rc = hip_fail(e, "top-k merge");
+  }
+  return rc;
+}
+}  // namespace cms
+}
+
+static int copy_out_lists(cms_handle* h, int64_t k, const DevBuf& o_ids, const DevBuf& o_sc, const DevBuf& o_cnt,
+                          int64_t* ids, double* scores, int32_t* counts) {
+  const int64_t n = h->n;
+  hipError_t e = hipMemcpyAsync(ids, o_ids.ptr, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess && scores)
+    e = hipMemcpyAsync(scores, o_sc.ptr, sizeof(double) * n * k, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(counts, o_cnt.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  if (e != hipSuccess) return hip_fail(e, "top-k copy-out");
+  return CMS_OK;
+}
+
 int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts) {
   if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
   if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
@@ -1049,42 +1098,124 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
   CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
   CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
   CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
-  if (h->multi()) {
-    // one process per GPU: rank r computes shard r of the pairs, then one
-    // all-gather of the partial lists over xGMI and an exact merge (in rounds
-    // of kCandCap / k lists when world * k exceeds a merge workgroup's LDS)
-    const int G = h->world;
-    DevBuf g_ids, g_sc, g_cnt;
-    CMS_HIP(g_ids.ensure(sizeof(int64_t) * n * k * G));
-    CMS_HIP(g_sc.ensure(sizeof(double) * n * k * G));
-    CMS_HIP(g_cnt.ensure(sizeof(int32_t) * n * G));
-    rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>(), h->rank, G);
-    if (rc) return rc;
-    {
-      TimedScope ts(h, "topk_allgather");
-      if ((rc = coll_allgather(h, o_ids.ptr, g_ids.ptr, (int64_t)sizeof(int64_t) * n * k)) ||
-          (rc = coll_allgather(h, o_sc.ptr, g_sc.ptr, (int64_t)sizeof(double) * n * k)) ||
-          (rc = coll_allgather(h, o_cnt.ptr, g_cnt.ptr, (int64_t)sizeof(int32_t) * n)))
-        return rc;
-    }
-    rc = top_k_merge(h, k, G, g_ids.as<int64_t>(), g_sc.as<double>(), g_cnt.as<int32_t>(), o_ids.as<int64_t>(),
-                     o_sc.as<double>(), o_cnt.as<int32_t>());
-    if (rc == CMS_OK) {
-      const hipError_t e = hipStreamSynchronize(h->stream);
-      if (e != hipSuccess) rc = hip_fail(e, "top-k merge");
-    }
-  } else {
-    rc = top_k_all(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
-  }
-  if (rc == CMS_OK) {
-    hipError_t e = hipMemcpyAsync(ids, o_ids.ptr, sizeof(int64_t) * n * k, hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess && scores)
-      e = hipMemcpyAsync(scores, o_sc.ptr, sizeof(double) * n * k, hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(counts, o_cnt.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
-    if (e != hipSuccess) rc = hip_fail(e, "top-k copy-out");
-  }
+  rc = top_k_all_job(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
+  if (rc == CMS_OK) rc = copy_out_lists(h, k, o_ids, o_sc, o_cnt, ids, scores, counts);
   return rc;
+}
+
+// Incremental all-pairs top-k (the periodic refresh of a streaming table):
+// the result of cms_top_k_all on the current table, computed from the lists
+// the previous refresh kept plus the pairs with an owner a COO batch touched
+// since (cms_topk.hip, k_rf_fold, states the exactness argument).
+int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts) {
+  if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  const int64_t n = h->n;
+  DevBuf o_ids, o_sc, o_cnt;
+  CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
+  CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
+  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
+  if (h->per_owner || h->f64) {  // no kept lists for these modes: the whole job
+    rc = top_k_all_job(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
+    if (rc == CMS_OK) rc = copy_out_lists(h, k, o_ids, o_sc, o_cnt, ids, scores, counts);
+    return rc;
+  }
+  // kept lists are twice as deep as the answer, so a few candidates of an
+  // untouched owner may leave before its list must be recomputed
+  const int32_t D = std::min(2 * k, kCandCap / 2);
+  // the job and the redo emit owner ROWS (the kept lists' candidates)
+  struct RowsOut {
+    cms_handle* h;
+    int64_t* saved;
+    ~RowsOut() { h->d_owner_ids = saved; }
+  } rows_out{h, h->d_owner_ids};
+  h->d_owner_ids = nullptr;
+  const bool full = !h->rf_valid || h->rf_k != k || h->rf_depth != D;
+  if (full) {
+    h->rf_valid = false;
+    CMS_HIP(h->rf_ids.ensure(sizeof(int64_t) * (size_t)n * D));
+    CMS_HIP(h->rf_sc.ensure(sizeof(double) * (size_t)n * D));
+    CMS_HIP(h->rf_cnt.ensure(sizeof(int32_t) * (size_t)n));
+    CMS_HIP(h->rf_full.ensure((size_t)n));
+    CMS_HIP(h->rf_touch.ensure((size_t)n));
+    h->rf_depth = D;
+    h->rf_k = k;
+    TimedScope ts(h, "refresh_full");
+    if ((rc = top_k_all_job(h, D, h->rf_ids.as<int64_t>(), h->rf_sc.as<double>(), h->rf_cnt.as<int32_t>())))
+      return rc;
+    if ((rc = refresh_set_full(h))) return rc;
+    h->rf_stat_full += 1;
+    h->rf_stat_touched = n;
+    h->rf_stat_redo = 0;
+  } else {
+    // touched owners since the kept lists were made
+    std::vector<uint8_t> touch(n);
+    CMS_HIP(hipMemcpyAsync(touch.data(), h->rf_touch.ptr, (size_t)n, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    int64_t nt = 0;
+    for (int64_t r = 0; r < n; ++r) nt += touch[r];
+    h->rf_stat_touched = nt;
+    h->rf_stat_redo = 0;
+    if (nt > 0) {
+      CMS_HIP(h->rf_new.ensure((sizeof(int64_t) + sizeof(double)) * (size_t)n * D + sizeof(int32_t) * (size_t)n));
+      int64_t* n_ids = h->rf_new.as<int64_t>();
+      double* n_sc = reinterpret_cast<double*>(n_ids + (size_t)n * D);
+      int32_t* n_cnt = reinterpret_cast<int32_t*>(n_sc + (size_t)n * D);
+      // the operands are re-laid out with the touched owners first
+      h->mfma_ready = false;
+      h->i8blk_ready = false;
+      h->rf_restrict = true;
+      {
+        TimedScope ts(h, "refresh_job");
+        rc = top_k_all_job(h, D, n_ids, n_sc, n_cnt);
+      }
+      h->rf_restrict = false;
+      if (rc) return rc;
+      CMS_HIP(h->rf_redo.ensure(sizeof(uint32_t) * ((size_t)n + 1)));
+      uint32_t* redo = h->rf_redo.as<uint32_t>();
+      {
+        TimedScope ts(h, "refresh_fold");
+        if ((rc = refresh_fold(h, n_ids, n_sc, n_cnt, k, redo))) return rc;
+      }
+      uint32_t nredo = 0;
+      CMS_HIP(hipMemcpyAsync(&nredo, redo, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+      CMS_HIP(hipStreamSynchronize(h->stream));
+      h->rf_stat_redo = nredo;
+      if (nredo > 0) {  // lists an untouched owner could not keep exact: whole-row recompute
+        std::vector<uint32_t> rows(nredo);
+        CMS_HIP(hipMemcpyAsync(rows.data(), redo + 1, sizeof(uint32_t) * nredo, hipMemcpyDeviceToHost, h->stream));
+        CMS_HIP(hipStreamSynchronize(h->stream));
+        std::vector<int64_t> pos(nredo), outp(nredo);
+        for (uint32_t i = 0; i < nredo; ++i) {
+          outp[i] = rows[i];
+          pos[i] = h->h_inv[rows[i]];
+        }
+        TimedScope ts(h, "refresh_redo");
+        if ((rc = slab_top_k_positions(h, pos, outp, D, h->rf_ids.as<int64_t>(), h->rf_sc.as<double>(),
+                                       h->rf_cnt.as<int32_t>())))
+          return rc;
+        // a recomputed list holds every candidate iff it is shorter than D
+        if ((rc = refresh_set_full_list(h, redo, nredo))) return rc;
+      }
+    }
+  }
+  CMS_HIP(hipMemsetAsync(h->rf_touch.ptr, 0, (size_t)n, h->stream));
+  h->rf_valid = true;
+  h->d_owner_ids = rows_out.saved;
+  if ((rc = refresh_emit(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>()))) return rc;
+  return copy_out_lists(h, k, o_ids, o_sc, o_cnt, ids, scores, counts);
+}
+
+int cms_refresh_stats(cms_handle* h, int64_t* touched, int64_t* redone, int64_t* full_jobs) {
+  if (!h || !touched || !redone || !full_jobs) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  *touched = h->rf_stat_touched;
+  *redone = h->rf_stat_redo;
+  *full_jobs = h->rf_stat_full;
+  return CMS_OK;
 }
 
 int cms_top_k_all_partial(cms_handle* h, int32_t k, int32_t shard, int32_t nshards, int64_t* ids, double* scores,

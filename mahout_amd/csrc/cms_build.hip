@@ -409,6 +409,7 @@ int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const fl
 }
 
 int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs) {
+  h->rf_valid = false;  // CSR batches do not mark touched owners: the next refresh is a full job
   return ingest_spans_device(h, d_off, d_off + 1, d_key, d_val, npairs);
 }
 

@@ -66,18 +66,41 @@ __global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int6
 // Stable permutation: owners with 3+ limbs, then 2 limbs, then single-limb
 // owners with a counter above kF4Max, then the fp4 class (every counter
 // <= kF4Max), each class in row order (exclusive scans of the class flags).
+// For an incremental refresh (tpos8/tpos4 non-null) the touched owners of the
+// two single-limb classes come first within their class, so the touched rows
+// are two position ranges and whole symmetric-wave blocks of untouched rows
+// can be skipped.
 __global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, const uint32_t* dpos,
                             const uint32_t* deep_flag, const uint32_t* fpos, const uint32_t* f4_flag,
                             const uint8_t* rowL, int64_t nrows, int64_t n_deep, int64_t n_multi, int64_t n_s8,
-                            int64_t* perm, int64_t* inv, uint8_t* rowLp) {
+                            const uint8_t* touch, const uint32_t* tpos8, const uint32_t* tpos4, int64_t nt8,
+                            int64_t nt4, int64_t* perm, int64_t* inv, uint8_t* rowLp) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p = deep_flag[r]    ? (int64_t)dpos[r]
-                      : multi_flag[r] ? n_deep + ((int64_t)mpos[r] - (int64_t)dpos[r])
-                      : f4_flag[r]    ? n_multi + n_s8 + (int64_t)fpos[r]
-                                      : n_multi + (r - (int64_t)mpos[r] - (int64_t)fpos[r]);
+    int64_t p;
+    if (deep_flag[r]) {
+      p = (int64_t)dpos[r];
+    } else if (multi_flag[r]) {
+      p = n_deep + ((int64_t)mpos[r] - (int64_t)dpos[r]);
+    } else if (f4_flag[r]) {
+      const int64_t q = (int64_t)fpos[r];  // rank in the fp4 class
+      p = n_multi + n_s8 + (!tpos4 ? q : touch[r] ? (int64_t)tpos4[r] : nt4 + q - (int64_t)tpos4[r]);
+    } else {
+      const int64_t q = r - (int64_t)mpos[r] - (int64_t)fpos[r];  // rank in the int8 class
+      p = n_multi + (!tpos8 ? q : touch[r] ? (int64_t)tpos8[r] : nt8 + q - (int64_t)tpos8[r]);
+    }
     perm[p] = r;
     inv[r] = p;
     rowLp[p] = rowL[r];
+  }
+}
+
+// refresh: touched flags of the int8 and fp4 single-limb classes
+__global__ void k_touch_class(const uint8_t* touch, const uint32_t* multi_flag, const uint32_t* f4_flag, int64_t n,
+                              uint32_t* t8, uint32_t* t4) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const bool t = touch[r] != 0 && multi_flag[r] == 0;
+    t8[r] = (t && f4_flag[r] == 0) ? 1u : 0u;
+    t4[r] = (t && f4_flag[r] != 0) ? 1u : 0u;
   }
 }
 
@@ -974,11 +997,41 @@ int cosine_prepare(cms_handle* h) {
   h->n_inexact_rows = host[2];
   const uint32_t n_five = host[3];
   CMS_HIP(h->ws_limbhot.ensure((size_t)std::max<int64_t>(1, n_multi) * (kMaxLimbs - 1) * (size_t)dw));
+  // incremental refresh: touched single-limb owners first within their class
+  const uint8_t* touch = nullptr;
+  uint32_t *t8 = nullptr, *t4 = nullptr, *tpos8 = nullptr, *tpos4 = nullptr;
+  int64_t nt8 = 0, nt4 = 0;
+  if (h->rf_restrict) {
+    CMS_HIP(h->rf_perm.ensure(sizeof(uint32_t) * 4 * (size_t)n));
+    t8 = h->rf_perm.as<uint32_t>();
+    t4 = t8 + n;
+    tpos8 = t4 + n;
+    tpos4 = tpos8 + n;
+    touch = h->rf_touch.as<uint8_t>();
+    TimedScope ts(h, "limb_prep");
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_touch_class, dim3(grid), dim3(256), 0, h->stream, touch, mflag, fflag, n, t8, t4);
+    CMS_HIP(hipGetLastError());
+    int rc = scan_exclusive_u32(h, t8, tpos8, n, bsum);
+    if (rc) return rc;
+    CMS_HIP(hipMemcpyAsync(&host[0], tpos8 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[1], t8 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    rc = scan_exclusive_u32(h, t4, tpos4, n, bsum);
+    if (rc) return rc;
+    CMS_HIP(hipMemcpyAsync(&host[2], tpos4 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipMemcpyAsync(&host[3], t4 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    nt8 = (int64_t)host[0] + host[1];
+    nt4 = (int64_t)host[2] + host[3];
+  }
+  h->rf_t8 = nt8;
+  h->rf_t4 = nt4;
+  h->rf_s8 = n_s8;
   {
     TimedScope ts(h, "limb_prep");
     unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, fpos, fflag, rowL,
-                       n, n_deep, n_multi, n_s8, perm, inv, rowLp);
+                       n, n_deep, n_multi, n_s8, touch, tpos8, tpos4, nt8, nt4, perm, inv, rowLp);
     hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->tview(), dw, perm, rowLp, n_multi,
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
@@ -1472,6 +1525,20 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
           g.cval = cb.cval;
           g.cap = cap;
           g.rbits = fp4 ? rb4 : rb8;
+          if (h->rf_restrict) {  // refresh: the touched rows are two position ranges; keep their blocks' pairs
+            auto blocks = [&](int64_t lo, int64_t hi, int32_t* b0, int32_t* b1) {
+              lo = std::max<int64_t>(lo, g.s0);
+              hi = std::min<int64_t>(hi, g.s0 + g.s_rows);
+              *b0 = *b1 = 0;
+              if (hi > lo) {
+                *b0 = (int32_t)((lo - g.s0) / kSymBlk);
+                *b1 = (int32_t)((hi - g.s0 + kSymBlk - 1) / kSymBlk);
+              }
+            };
+            g.tsel = 1;
+            blocks(nm, nm + h->rf_t8, &g.ts0, &g.ts1);
+            blocks(nm + h->rf_s8, nm + h->rf_s8 + h->rf_t4, &g.ts2, &g.ts3);
+          }
           int64_t slots = nbk;
           if (!fp4 && fb0 < nb_s) {
             g.fsel = 1;

@@ -111,6 +111,10 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
   }
   if ((g.nb & 1) == 0 && 2 * wv == g.nb && 2 * I >= g.nb) return;  // {I, I + nb/2} once
   const int J = (I + wv) % g.nb;
+  if (g.tsel) {  // incremental refresh: block pairs holding a touched owner only
+    auto touched = [&](int b) { return (b >= g.ts0 && b < g.ts1) || (b >= g.ts2 && b < g.ts3); };
+    if (!touched(I) && !touched(J)) return;
+  }
   const bool diag = I == J;
   const int pa = sub / kPB, pb = sub - pa * kPB;
   const int64_t a_pos0 = g.s0 + (int64_t)I * kSymBlk + pa * kSA;

@@ -392,6 +392,9 @@ int compute_norms(cms_handle* h) {
 int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs) {
   if (npairs <= 0) return CMS_OK;
   const int64_t n = h->n;
+  if (h->rf_valid) {  // kept refresh lists: the batch's owners are recomputed by the next refresh
+    if (int rc = refresh_mark(h, d_row, npairs)) return rc;
+  }
   // Global atomics for a small batch, and for any batch into a live table
   // unless its atomic traffic (~d sector RMWs per pair) exceeds the
   // accumulate build's full-table read + write.

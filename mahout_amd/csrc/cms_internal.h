@@ -169,6 +169,19 @@ struct cms_handle {
   bool vl_ok = false;           // every multi-limb owner fits 4 limbs (else the legacy 128x128 path)
   int64_t topk_redo = 0;        // top-k rows the sampled threshold missed (radix-select redo)
   std::vector<int64_t> h_perm, h_inv;  // permuted position <-> owner row
+  // incremental all-pairs top-k (cms_top_k_refresh): exact lists of depth
+  // rf_depth >= k per owner row (candidate rows, scores, valid prefix length,
+  // "holds every candidate" flag) for the table as it was, minus the owners
+  // marked touched by COO ingests since (rf_touch).
+  bool rf_valid = false;
+  int32_t rf_k = 0, rf_depth = 0;
+  cms::DevBuf rf_ids, rf_sc, rf_cnt, rf_full, rf_touch, rf_new, rf_redo, rf_perm;
+  // set by cms_top_k_refresh around its job: cosine_prepare orders touched
+  // single-limb owners first within their class, top_k_all's symmetric waves
+  // keep only block pairs holding a touched owner
+  bool rf_restrict = false;
+  int64_t rf_t8 = 0, rf_t4 = 0, rf_s8 = 0;  // touched int8 / fp4 single-limb owners; int8-class size
+  int64_t rf_stat_touched = 0, rf_stat_redo = 0, rf_stat_full = 0;
   int64_t pairs_ingested = 0;
   int32_t exact_norms = 1;
 
@@ -342,6 +355,24 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
 // merge nparts partial top-k lists ([nparts][n][k] ids by owner ID, scores; [nparts][n] counts)
 int top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* d_ids, const double* d_scores,
                 const int32_t* d_counts, int64_t* d_out_ids, double* d_out_scores, int32_t* d_out_counts);
+// ---- incremental refresh (cms_topk.hip) ----
+// mark the owner rows of a COO batch touched (rf_touch) when refresh lists are live
+int refresh_mark(cms_handle* h, const int64_t* d_row, int64_t npairs);
+// fold a refresh job's lists (rows, depth rf_depth) into the kept lists: touched
+// rows take the new list, untouched rows the first rf_depth of new + kept
+// (kept entries of touched candidates dropped), valid up to the kept boundary;
+// rows left with fewer than k valid entries are listed in redo ([0] = count)
+int refresh_fold(cms_handle* h, const int64_t* d_new_ids, const double* d_new_sc, const int32_t* d_new_cnt,
+                 int32_t k, uint32_t* d_redo);
+// first k of the kept lists -> outputs (owner IDs through d_owner_ids)
+int refresh_emit(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
+// kept lists' "holds every candidate" flags from their counts (after a full job)
+int refresh_set_full(cms_handle* h);
+// the same for the rows of d_list ([0] = count, rows from [1])
+int refresh_set_full_list(cms_handle* h, const uint32_t* d_list, int64_t m);
+// the whole-table job of cms_top_k_all on device outputs (multi-rank: shard,
+// all-gather, merge)
+int top_k_all_job(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
 // ---- cms_profiles.hip (per-owner shapes) ----
 struct PoShape {
   int64_t soff;      // first counter of the owner's own sketch
@@ -410,6 +441,7 @@ struct SymArgs {
   int64_t s0, s_rows;   // the region's positions; blocks of kSymBlk rows from s0
   int32_t nb, wave, band, nblk;
   int32_t fsel, fblk0;              // only block pairs with a block below fblk0
+  int32_t tsel, ts0, ts1, ts2, ts3;  // refresh: only block pairs with a block in [ts0, ts1) or [ts2, ts3)
   int32_t rect, si, sj, njc;        // band enumerated by si x sj block rectangles
   const double* thr;                // candidate lists (CandBufs)
   uint32_t* ccnt;

@@ -725,6 +725,193 @@ int slab_top_k_positions(cms_handle* h, const std::vector<int64_t>& pos, const s
   return CMS_OK;
 }
 
+// ---- incremental refresh of the all-pairs top-k (cms_top_k_refresh) ----
+// A refresh recomputes only the pairs with a touched owner; every other pair's
+// similarity is unchanged (cos(u, v) reads only u's and v's sketches and
+// norms).  An untouched owner u keeps an exact list of depth D >= k from the
+// last job.  Its new list is the first D of (the new job's list of u, which
+// holds every touched candidate that can matter) + (the kept entries whose
+// candidate is untouched).  Every untouched candidate missing from both is
+// ordered after the kept list's last entry B (it was not in the kept list),
+// so the merged entries ordered at or before B are exact; a list left with
+// fewer than k such entries is recomputed whole.  A kept list that held every
+// candidate (fewer than D) has no B: the merge is exact throughout.
+
+__global__ void k_rf_mark(const int64_t* row, int64_t np, int64_t n, uint8_t* touch) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = row[i];
+    if (r >= 0 && r < n) touch[r] = 1;
+  }
+}
+
+int refresh_mark(cms_handle* h, const int64_t* d_row, int64_t npairs) {
+  const unsigned g = (unsigned)std::min<int64_t>((npairs + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_rf_mark, dim3(g), dim3(256), 0, h->stream, d_row, npairs, h->n, h->rf_touch.as<uint8_t>());
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+constexpr int kRfMax = 2 * (kCandCap / 2);  // new + kept entries of one row (depth <= kCandCap / 2)
+
+__global__ __launch_bounds__(kCandThreads) void k_rf_fold(int64_t n, int32_t D, int32_t k, const uint8_t* touch,
+                                                          const int64_t* nid, const double* nsc, const int32_t* ncnt,
+                                                          int64_t* kid, double* ksc, int32_t* kcnt, uint8_t* kfull,
+                                                          uint32_t* redo) {
+  __shared__ uint64_t key[kRfMax];
+  __shared__ int64_t rid[kRfMax];
+  __shared__ double val[kRfMax];
+  __shared__ uint32_t s_m;
+  const int tid = threadIdx.x;
+  for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const int32_t cn = min(ncnt[r], D);
+    const int64_t base = r * D;
+    if (touch[r]) {  // every pair of a touched owner was recomputed: its new list is exact
+      for (int32_t i = tid; i < cn; i += kCandThreads) {
+        kid[base + i] = nid[base + i];
+        ksc[base + i] = nsc[base + i];
+      }
+      if (tid == 0) {
+        kcnt[r] = cn;
+        kfull[r] = cn < D ? 1 : 0;
+      }
+      continue;
+    }
+    const int32_t co = kcnt[r];
+    const bool full = kfull[r] != 0;
+    uint64_t bkey = 0;
+    int64_t brow = -1;
+    if (co > 0) {
+      bkey = score_key(ksc[base + co - 1]);
+      brow = kid[base + co - 1];
+    }
+    if (tid == 0) s_m = 0;
+    __syncthreads();
+    for (int32_t i = tid; i < cn; i += kCandThreads) {
+      const uint32_t p = atomicAdd(&s_m, 1u);
+      key[p] = score_key(nsc[base + i]);
+      rid[p] = nid[base + i];
+      val[p] = nsc[base + i];
+    }
+    for (int32_t i = tid; i < co; i += kCandThreads) {
+      const int64_t c = kid[base + i];
+      if (touch[c]) continue;  // stale: the new list carries its current score
+      const uint32_t p = atomicAdd(&s_m, 1u);
+      key[p] = score_key(ksc[base + i]);
+      rid[p] = c;
+      val[p] = ksc[base + i];
+    }
+    __syncthreads();
+    const uint32_t m = s_m;
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    for (uint32_t i = m + tid; i < P; i += kCandThreads) {
+      key[i] = 0;
+      rid[i] = INT64_MAX;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= P; size <<= 1) {
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = tid; i < P; i += kCandThreads) {
+          const uint32_t jx = i ^ stride;
+          if (jx > i) {
+            const bool up = (i & size) == 0;
+            const bool i_first = key[i] > key[jx] || (key[i] == key[jx] && rid[i] < rid[jx]);
+            if (up != i_first) {
+              const uint64_t tk = key[i];
+              key[i] = key[jx];
+              key[jx] = tk;
+              const int64_t tr = rid[i];
+              rid[i] = rid[jx];
+              rid[jx] = tr;
+              const double tv = val[i];
+              val[i] = val[jx];
+              val[jx] = tv;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (tid == 0) {  // sequential: drop duplicates (an untouched pair both lists hold), keep the first D
+      int32_t c = 0, valid = 0;
+      for (uint32_t i = 0; i < m && c < D; ++i) {
+        if (i > 0 && rid[i] == rid[i - 1] && key[i] == key[i - 1]) continue;
+        kid[base + c] = rid[i];
+        ksc[base + c] = val[i];
+        ++c;
+        if (full || key[i] > bkey || (key[i] == bkey && rid[i] <= brow)) valid = c;
+      }
+      kcnt[r] = full ? c : valid;
+      kfull[r] = (full && c < D) ? 1 : 0;
+      if (!full && valid < k) redo[1 + atomicAdd(redo, 1u)] = (uint32_t)r;
+    }
+    __syncthreads();
+  }
+}
+
+int refresh_fold(cms_handle* h, const int64_t* d_new_ids, const double* d_new_sc, const int32_t* d_new_cnt, int32_t k,
+                 uint32_t* d_redo) {
+  if (h->rf_depth > kCandCap / 2) return set_error(CMS_E_PARAM, "refresh depth %d", h->rf_depth);
+  CMS_HIP(hipMemsetAsync(d_redo, 0, sizeof(uint32_t), h->stream));
+  const unsigned grid = (unsigned)std::min<int64_t>(h->n, 8192);
+  hipLaunchKernelGGL(k_rf_fold, dim3(grid), dim3(kCandThreads), 0, h->stream, h->n, h->rf_depth, k,
+                     h->rf_touch.as<uint8_t>(), d_new_ids, d_new_sc, d_new_cnt, h->rf_ids.as<int64_t>(),
+                     h->rf_sc.as<double>(), h->rf_cnt.as<int32_t>(), h->rf_full.as<uint8_t>(), d_redo);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+__global__ void k_rf_set_full(const int32_t* cnt, int64_t n, int32_t D, uint8_t* full) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    full[r] = cnt[r] < D ? 1 : 0;
+}
+
+__global__ void k_rf_set_full_list(const int32_t* cnt, const uint32_t* list, int32_t D, uint8_t* full) {
+  const uint32_t m = list[0];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    const uint32_t r = list[1 + i];
+    full[r] = cnt[r] < D ? 1 : 0;
+  }
+}
+
+int refresh_set_full_list(cms_handle* h, const uint32_t* d_list, int64_t m) {
+  if (m <= 0) return CMS_OK;
+  const unsigned g = (unsigned)std::min<int64_t>((m + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_rf_set_full_list, dim3(g), dim3(256), 0, h->stream, h->rf_cnt.as<int32_t>(), d_list,
+                     h->rf_depth, h->rf_full.as<uint8_t>());
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+int refresh_set_full(cms_handle* h) {
+  const unsigned g = (unsigned)std::min<int64_t>((h->n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_rf_set_full, dim3(g), dim3(256), 0, h->stream, h->rf_cnt.as<int32_t>(), h->n, h->rf_depth,
+                     h->rf_full.as<uint8_t>());
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+__global__ void k_rf_emit(int64_t n, int32_t D, int32_t k, const int64_t* kid, const double* ksc, const int32_t* kcnt,
+                          const int64_t* owner_ids, int64_t* ids, double* scores, int32_t* counts) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = min(kcnt[r], k);
+    counts[r] = c;
+    for (int32_t t = 0; t < c; ++t) {
+      const int64_t o = kid[r * D + t];
+      ids[r * k + t] = owner_ids ? owner_ids[o] : o;
+      scores[r * k + t] = ksc[r * D + t];
+    }
+  }
+}
+
+int refresh_emit(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  const unsigned g = (unsigned)std::min<int64_t>((h->n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_rf_emit, dim3(g), dim3(256), 0, h->stream, h->n, h->rf_depth, k, h->rf_ids.as<int64_t>(),
+                     h->rf_sc.as<double>(), h->rf_cnt.as<int32_t>(), h->d_owner_ids, d_ids, d_scores, d_counts);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
 int top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k, int64_t* d_ids, double* d_scores,
                int32_t* d_counts) {
   if (k < 1 || k > kTopMax) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kTopMax);

@@ -324,6 +324,23 @@ class SketchTable:
         check(self._lib.cms_top_k_all(self._h, int(k), _ptr(ids), _ptr(sc), _ptr(cnt)))
         return ids, sc, cnt
 
+    def top_k_refresh(self, k):
+        """The same lists as top_k_all(k), recomputing only the pairs with an
+        owner touched by COO ingests since the previous refresh (the first
+        call runs the whole job and keeps 2k-deep lists on the device)."""
+        n = self.num_owners
+        ids = np.zeros((n, k), np.int64)
+        sc = np.zeros((n, k), np.float64)
+        cnt = np.zeros(n, np.int32)
+        check(self._lib.cms_top_k_refresh(self._h, int(k), _ptr(ids), _ptr(sc), _ptr(cnt)))
+        return ids, sc, cnt
+
+    def refresh_stats(self):
+        """(owners touched, lists recomputed whole, whole jobs) of the last refresh."""
+        v = [ctypes.c_int64(0) for _ in range(3)]
+        check(self._lib.cms_refresh_stats(self._h, *[ctypes.byref(x) for x in v]))
+        return tuple(int(x.value) for x in v)
+
     # -- per-owner shapes (CountMinSketchConfig) --
     @classmethod
     def per_owner_shapes(cls, num_owners, seed=42, weighted=False, device=-1, owner_ids=None, frac_bits=0):

@@ -1,0 +1,116 @@
+"""GPU: the incremental all-pairs top-k refresh (cms_top_k_refresh, config 5's
+periodic refresh) equals the whole job (cms_top_k_all) on the same table, bit
+for bit, after every batch.
+
+The reference recomputes nothing incrementally: a Refreshable
+(`T/common/Refreshable.java:51`) re-reads its DataModel and the precomputed
+similarities are rebuilt whole (`ItemSimilarityJob.java:101`, one
+`TopItems.getTopUsers` per owner, `TopItems.java:91-136`).  The refresh must
+therefore give exactly that whole result; cms_top_k_all is itself checked
+against the oracle's TopItems restatement in test_gpu_parity.py.
+"""
+import numpy as np
+import pytest
+
+from mahout_amd import SketchTable
+from mahout_amd.synth import zipf_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _same_lists(a, b):
+    ids, sc, cnt = a
+    rids, rsc, rcnt = b
+    if not np.array_equal(cnt, rcnt):
+        return "counts differ at rows %s" % np.nonzero(cnt != rcnt)[0][:10].tolist()
+    n, k = ids.shape
+    mask = np.arange(k)[None, :] < cnt[:, None]
+    if not np.array_equal(np.where(mask, ids, -1), np.where(mask, rids, -1)):
+        return "ids differ at rows %s" % np.nonzero((np.where(mask, ids, -1) != np.where(mask, rids, -1)).any(1))[0][:10].tolist()
+    a_ = np.where(mask, sc, 0.0)
+    b_ = np.where(mask, rsc, 0.0)
+    eq = (a_ == b_) | (np.isnan(a_) & np.isnan(b_))
+    if not eq.all():
+        return "scores differ at rows %s" % np.nonzero(~eq.all(1))[0][:10].tolist()
+    return None
+
+
+def _batch(rng, n, frac, size, vmax, n_keys):
+    """A COO batch whose owners are a random `frac` of all owners (Zipf-weighted
+    inside that subset) -- the touched set of one streaming interval."""
+    touched = rng.choice(n, size=max(1, int(frac * n)), replace=False)
+    p = 1.0 / np.arange(1, touched.size + 1) ** 1.1
+    rows = touched[rng.choice(touched.size, size=size, p=p / p.sum())].astype(np.int64)
+    keys = rng.integers(0, n_keys, size=size).astype(np.int64)
+    vals = rng.integers(1, vmax + 1, size=size).astype(np.float32)
+    return rows, keys, vals
+
+
+@pytest.mark.parametrize("n,d,w,vmax,k,weighted,seed", [
+    (12000, 4, 256, 2, 25, False, 56),    # fp4 blocks beside int8 blocks, multi-wave bands
+    (11776, 3, 128, 2, 20, False, 55),    # no fp4 image (w % 256): int8 waves only
+    (3000, 5, 8192, 3, 100, False, 58),   # the config-4 shape: fp4, int8 and multi-limb owners
+    (1800, 3, 256, 1, 64, True, 53),      # weighted: not on the symmetric kernel (all pairs recomputed)
+    (700, 5, 512, 2, 5, False, 54),       # fewer than one block pair per wave
+])
+def test_refresh_equals_whole_job(n, d, w, vmax, k, weighted, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    items, users = zipf_stream(4000, n, 400_000, seed=seed)
+    vals = rng.integers(1, vmax + 1, size=items.size).astype(np.float32)
+    with SketchTable(n, depth=d, width=w, seed=42, weighted=weighted) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        first = t.top_k_refresh(k)
+        assert t.refresh_stats()[2] == 1
+        err = _same_lists(first, t.top_k_all(k))
+        assert err is None, err
+        # batches touching 1% .. 30% of the owners; sizes through both the
+        # plain-atomic and the owner-grouped incremental paths
+        for step, (frac, size) in enumerate([(0.01, 2000), (0.05, 40_000), (0.15, 20_000), (0.3, 60_000),
+                                             (0.002, 50)]):
+            rows, keys, v = _batch(rng, n, frac, size, vmax, 4000)
+            t.ingest(rows, keys, v)
+            t.finalize()
+            got = t.top_k_refresh(k)
+            touched, redone, full = t.refresh_stats()
+            assert full == 1, "an incremental refresh fell back to a whole job"
+            assert touched == np.unique(rows).size
+            exp = t.top_k_all(k)
+            err = _same_lists(got, exp)
+            assert err is None, (step, frac, err, (touched, redone))
+        # no batch since: the kept lists are returned as they are
+        again = t.top_k_refresh(k)
+        assert t.refresh_stats()[0] == 0
+        assert _same_lists(again, exp) is None
+
+
+def test_refresh_owner_ids_and_invalidation():
+    """Owner IDs (not rows) in the output; a CSR ingest invalidates the kept
+    lists (the next refresh is a whole job) and a different k starts over."""
+    n, d, w, k = 4000, 4, 256, 30
+    ids_of = np.arange(n, dtype=np.int64) * 7 + 1000
+    items, users = zipf_stream(3000, n, 200_000, seed=9)
+    with SketchTable(n, depth=d, width=w, seed=42, owner_ids=ids_of) as t:
+        t.ingest(ids_of[items], users)
+        t.finalize()
+        t.top_k_refresh(k)
+        rng = np.random.Generator(np.random.PCG64(3))
+        rows, keys, v = _batch(rng, n, 0.1, 30_000, 1, 3000)
+        t.ingest(ids_of[rows], keys, v)
+        t.finalize()
+        got = t.top_k_refresh(k)
+        assert t.refresh_stats()[2] == 1
+        assert _same_lists(got, t.top_k_all(k)) is None
+        assert set(np.unique(got[0][got[0] >= 0])) <= set(ids_of.tolist()) | {0}
+        # another k: whole job again
+        got = t.top_k_refresh(k + 5)
+        assert t.refresh_stats()[2] == 2
+        assert _same_lists(got, t.top_k_all(k + 5)) is None
+        # a CSR batch does not mark owners: the next refresh is a whole job
+        off = np.zeros(n + 1, np.int64)
+        off[11:] = 3  # owner row 10 gets three keys
+        t.ingest_csr(off, np.array([5, 6, 7], np.int64))
+        t.finalize()
+        got = t.top_k_refresh(k + 5)
+        assert t.refresh_stats()[2] == 3
+        assert _same_lists(got, t.top_k_all(k + 5)) is None

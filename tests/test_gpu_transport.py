@@ -11,7 +11,9 @@ Every rank must end with the unsharded result bit for bit:
   counters   == oracle DoubleCountMinSketch.update over the whole stream
                (`T/impl/common/DoubleCountMinSketch.java:72-80`)
   top-k      == a single-rank handle's cms_top_k_all, and the oracle's
-               TopItems.getTopUsers on sampled rows (`TopItems.java:91-136`).
+               TopItems.getTopUsers on sampled rows (`TopItems.java:91-136`);
+  refresh    == cms_top_k_all on the same table (cms_top_k_refresh after the
+               delta exchange: kept lists + the touched owners' pairs).
 """
 import os
 import socket
@@ -65,6 +67,7 @@ def _worker(rank, world, port, q, case):
             t.ingest(items[sel], users[sel], vals[sel])
             t.finalize()  # packed all-reduce through the transport
             res["merge_bytes"] = tr.bytes_moved
+            t.top_k_refresh(k)  # collective whole job; every rank keeps the 2k-deep lists
             for lo, hi in zip(cuts[:-1], cuts[1:]):
                 m = np.zeros(npairs, bool)
                 m[lo:hi] = mine[lo:hi]
@@ -74,6 +77,12 @@ def _worker(rank, world, port, q, case):
             res["delta_bytes"] = tr.bytes_moved - before
             got = t.read_counters()
             ids, sc, cnt = t.top_k_all(k)  # collective: partial lists gathered and merged
+            # collective incremental refresh: only pairs with an owner any rank's batches touched
+            fids, fsc, fcnt = t.top_k_refresh(k)
+            res["refresh_stats"] = t.refresh_stats()
+        res["refresh_vs_all"] = bool(np.array_equal(fcnt, cnt)) and all(
+            fids[r, :cnt[r]].tolist() == ids[r, :cnt[r]].tolist() and _same(fsc[r, :cnt[r]], sc[r, :cnt[r]])
+            for r in range(n))
         a, b = O.hash_params(42, d)
         full = O.build_table(n, d, w, a, b, items, users, vals)
         res["counters"] = bool(np.array_equal(got, full))
@@ -119,6 +128,8 @@ def test_transport_merge_delta_exchange_collective_top_k(world, case):
         assert r["counters"], (rank, r)
         assert r["topk_vs_single_rank"], (rank, r)
         assert r["topk_vs_oracle"], (rank, r)
+        assert r["refresh_vs_all"], (rank, r)
+        assert r["refresh_stats"][2] == 1, (rank, r)  # one whole job, then an incremental refresh
         n, d, w = case[:3]
         assert 0 < r["merge_bytes"] < n * d * w * 4  # the packed merge moved less than the u32 table
         assert 0 < r["delta_bytes"] < n * d * w * 4  # the exchange moved the logs (20 B/pair), not a table
