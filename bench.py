@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the CSR and cosine side measurements")
     ap.add_argument("--no-cosine-1m", action="store_true", help="skip the 1M-item all-pairs measurement")
-    ap.add_argument("--stream-batches", type=int, default=16, help="config-5 incremental batches per rank")
+    ap.add_argument("--stream-batches", type=int, default=8, help="config-5 incremental batches per rank")
+    ap.add_argument("--refresh-every", type=int, default=1,
+                    help="config 5: batches between periodic top-k refreshes (cms_top_k_refresh)")
     ap.add_argument("--stream-refresh-multi", action="store_true",
                     help="also run the config-5 streaming phase with a communicator (delta all-gather)")
     return ap.parse_args()
@@ -608,35 +610,49 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
             it_, us = it_[keep], us[keep]
         batches.append((it_.contiguous(), us.contiguous()))
     local = sum(int(b[0].numel()) for b in batches)
-    # owners the batches touch: an exact incremental refresh must recompute
-    # every pair with a touched owner (its score may fall, so the untouched
-    # side's list needs its (k+1)-th candidate), i.e. 1 - (1 - f)^2 of the pairs
+    # owners the batches touch: the refresh recomputes every pair with a
+    # touched owner, i.e. 1 - (1 - f)^2 of the pairs for a touched fraction f
     touched_all = torch.unique(torch.cat([b[0] for b in batches])).numel() / n
     touched_one = sum(torch.unique(b[0]).numel() for b in batches) / (n * nb)
+    every = max(1, args.refresh_every)
+    # the periodic refresh keeps 2k-deep lists: one whole job builds them
     t.set_timing(True)
+    bar()
+    t0 = time.perf_counter()
+    t.top_k_refresh(k)
+    bar()
+    keep_s = max_over_ranks(time.perf_counter() - t0)
     t.reset_timing()
-    bar()
-    t0 = time.perf_counter()
-    for it_, us in batches:
+    ingest_s = 0.0
+    periods = []
+    cnt = None
+    for bi, (it_, us) in enumerate(batches):
+        bar()
+        t0 = time.perf_counter()
         t.ingest_device_rows(it_, us, None, int(it_.numel()))
-    bar()
-    ingest_s = max_over_ranks(time.perf_counter() - t0)
+        bar()
+        ingest_s += max_over_ranks(time.perf_counter() - t0)
+        if (bi + 1) % every == 0 or bi == nb - 1:
+            t0 = time.perf_counter()
+            t.finalize()  # with G ranks: the delta logs all-gathered and applied
+            bar()
+            fin_s = max_over_ranks(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            _, _, cnt = t.top_k_refresh(k)
+            bar()
+            rs = max_over_ranks(time.perf_counter() - t0)
+            touched, redone, full = t.refresh_stats()
+            periods.append({"after_batch": bi + 1, "finalize_s": round(fin_s, 5), "refresh_s": round(rs, 4),
+                            "touched_owner_frac": touched / n, "lists_redone": redone, "whole_jobs": full})
     atomic_ms, atomic_n = t.timing("ingest_atomic")
-    total = nb * per_batch * world
-    t0 = time.perf_counter()
-    t.finalize()
-    bar()
-    fin_s = max_over_ranks(time.perf_counter() - t0)
-    t0 = time.perf_counter()
-    _, _, cnt = t.top_k_all(k)
-    bar()
-    topk_s = max_over_ranks(time.perf_counter() - t0)
     t.set_timing(False)
+    total = nb * per_batch * world
     del batches
     alg = local * (16 + 2 * 5 * 4)
+    lat = [p["finalize_s"] + p["refresh_s"] for p in periods]
     return {
-        "workload": f"config 5: {nb} batches x {per_batch} pairs per GPU into the resident {n}-item table, "
-                    f"then finalize + top-{k} for every item",
+        "workload": f"config 5: {nb} batches x {per_batch} pairs per GPU into the resident {n}-item table; every "
+                    f"{every} batches finalize + incremental top-{k} refresh of every item (cms_top_k_refresh)",
         "path": "k_ingest_atomic (exact global atomics; norms/row maxima updated incrementally)",
         "batches": nb, "pairs_per_batch_per_gpu": per_batch,
         "sustained_updates_per_s": total / ingest_s,
@@ -647,9 +663,11 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": alg / (atomic_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if atomic_n else None,
                      "avg_launch_ms": atomic_ms / atomic_n if atomic_n else None},
-        "refresh_finalize_s": fin_s,
-        "refresh_topk_all_s": topk_s,
-        "refresh_latency_s": fin_s + topk_s,
+        "refresh_every_batches": every,
+        "keep_lists_whole_job_s": keep_s,
+        "refresh_latency_s": sum(lat) / len(lat),
+        "refresh_latency_max_s": max(lat),
+        "refresh_periods": periods,
         "full_lists": int((cnt == k).sum()),
         "touched_owner_frac": {"all_batches": touched_all, "per_batch": touched_one,
                                "pairs_to_recompute_all_batches": 1 - (1 - touched_all) ** 2,

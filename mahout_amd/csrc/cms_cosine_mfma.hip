@@ -1538,12 +1538,41 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
             g.tsel = 1;
             blocks(nm, nm + h->rf_t8, &g.ts0, &g.ts1);
             blocks(nm + h->rf_s8, nm + h->rf_s8 + h->rf_t4, &g.ts2, &g.ts3);
+            if (getenv("CMS_RF_DEBUG") && wv == 0)
+              fprintf(stderr, "refresh pass %d: nb %d blocks [%d,%d) [%d,%d) (t8 %ld t4 %ld s8 %ld nm %ld)\n", pass,
+                      g.nb, g.ts0, g.ts1, g.ts2, g.ts3, (long)h->rf_t8, (long)h->rf_t4, (long)h->rf_s8, (long)nm);
           }
           int64_t slots = nbk;
           if (!fp4 && fb0 < nb_s) {
             g.fsel = 1;
             g.fblk0 = (int32_t)fb0;
             slots = 2 * fb0;
+          }
+          if (g.tsel) {
+            int32_t a0 = g.ts0, a1 = g.ts1, b0 = g.ts2, b1 = g.ts3;
+            if (a0 == a1) {
+              a0 = b0;
+              a1 = b1;
+              b0 = b1 = 0;
+            }
+            if (a0 == a1) continue;  // no touched owner in this pass's region: no pair to recompute
+            // touched blocks [0, P): enumerate only the pairs with a block
+            // below P (dense, as the fsel waves); otherwise every pair of the
+            // pass is enumerated and the untouched ones leave at once, with the
+            // workgroups spread round-robin over the XCDs (identity map) so the
+            // ones that stay are not all on one XCD
+            if (a0 == 0 && (b0 == b1 || b0 <= a1) && !g.fsel) {
+              const int32_t P = std::max(a1, b0 == b1 ? a1 : b1);
+              if (2 * (int64_t)P < nbk) {
+                g.tsel = 0;
+                g.fsel = 1;
+                g.fblk0 = P;
+                slots = 2 * (int64_t)P;
+              }
+              g.rect = 0;
+            } else {
+              g.rect = 0;
+            }
           }
           if ((rc = launch_sym(h, g, fp4 ? 1 : 0, slots))) return rc;
           continue;

@@ -82,7 +82,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
   __half* s_tb = s_ta + kSA;
 
   // ---- which tile: band of waves, block pair {I, J}, A panel, B panel ----
-  const int lin = (int)block_map(blockIdx.x, g.nblk);
+  // a refresh's sparse pair set (tsel) is spread over the XCDs round-robin
+  const int lin = g.tsel ? (int)blockIdx.x : (int)block_map(blockIdx.x, g.nblk);
   int c, sub, wv;
   if (g.rect) {
     const int per = kSub * g.si * g.sj;
