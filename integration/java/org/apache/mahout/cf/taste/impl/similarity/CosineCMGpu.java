@@ -287,6 +287,16 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     return nativeTopKAll(handle, howMany);
   }
 
+  /**
+   * The same lists after streaming COO batches (cms_top_k_refresh): only the
+   * pairs of owners touched since the previous call are recomputed. This
+   * class re-ingests its DataModel as CSR on refresh(), which makes the next
+   * call a whole job; the incremental path serves streaming callers.
+   */
+  public long[][] allMostSimilarIDsRefreshed(int howMany) throws TasteException {
+    return nativeTopKRefresh(handle, howMany);
+  }
+
   @Override
   public void refresh(Collection<Refreshable> alreadyRefreshed) {
     super.refresh(alreadyRefreshed);
@@ -328,5 +338,6 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private static native float[] nativeEstimatePreferences(long h, long user, long[] neighbors, long[] items,
                                                           float capMin, float capMax) throws TasteException;
   private static native long[][] nativeTopKAll(long h, int k) throws TasteException;
+  private static native long[][] nativeTopKRefresh(long h, int k) throws TasteException;
   private static native void nativeDestroy(long h);
 }

@@ -223,15 +223,16 @@ JNIEXPORT jfloatArray JNICALL JFN(nativeEstimatePreferences)(JNIEnv* env, jclass
   return fail(env, rc, 0) ? NULL : res;
 }
 
-JNIEXPORT jobjectArray JNICALL JFN(nativeTopKAll)(JNIEnv* env, jclass c, jlong h, jint k) {
-  (void)c;
+typedef int (*top_k_fn)(cms_handle*, int32_t, int64_t*, double*, int32_t*);
+
+static jobjectArray top_k_lists(JNIEnv* env, jlong h, jint k, top_k_fn fn) {
   cms_stats st;
   st.pairs_ingested = 0;
   if (fail(env, cms_get_stats(H(h), &st), 0)) return NULL;
   const int64_t n = st.num_owners;
   int64_t* ids = (int64_t*)malloc(sizeof(int64_t) * (size_t)n * (k > 0 ? k : 1));
   int32_t* cnt = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
-  int rc = cms_top_k_all(H(h), k, ids, NULL, cnt);
+  int rc = fn(H(h), k, ids, NULL, cnt);
   jobjectArray res = NULL;
   if (rc == CMS_OK) {
     jclass longArr = (*env)->FindClass(env, "[J");
@@ -247,6 +248,18 @@ JNIEXPORT jobjectArray JNICALL JFN(nativeTopKAll)(JNIEnv* env, jclass c, jlong h
   free(ids);
   free(cnt);
   return fail(env, rc, 0) ? NULL : res;
+}
+
+JNIEXPORT jobjectArray JNICALL JFN(nativeTopKAll)(JNIEnv* env, jclass c, jlong h, jint k) {
+  (void)c;
+  return top_k_lists(env, h, k, cms_top_k_all);
+}
+
+/* The periodic refresh of a streaming table (cms_top_k_refresh): the same
+ * lists, recomputing only the pairs of owners touched since the last call. */
+JNIEXPORT jobjectArray JNICALL JFN(nativeTopKRefresh)(JNIEnv* env, jclass c, jlong h, jint k) {
+  (void)c;
+  return top_k_lists(env, h, k, cms_top_k_refresh);
 }
 
 JNIEXPORT void JNICALL JFN(nativeDestroy)(JNIEnv* env, jclass c, jlong h) {
