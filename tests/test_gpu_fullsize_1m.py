@@ -18,7 +18,9 @@ the domain allows:
     list equals the oracle's TopItems loop over that row's similarities to ALL
     1M owners (computed by the exact pair kernel), and those similarities are
     checked against the oracle's CosineCM on the read-back sketches for the
-    listed owners plus random partners.
+    listed owners plus random partners;
+  * config 5: one streaming batch, then cms_top_k_refresh equals cms_top_k_all
+    on the updated table for all 1M lists.
 """
 import numpy as np
 import pytest
@@ -117,6 +119,25 @@ def test_config34_full_size(oracle):
                     continue
                 want = oracle.cosine_cm(sa, t.read_counters(p, 1)[0])
                 assert _same(np.array([sims[p]]), np.array([want])), (row, p)
+
+        # 5. config 5 at this size: the incremental refresh after one 1.25M-pair
+        # Zipf batch equals the whole job on the updated table, every list
+        def same_lists(a_, b_):
+            i1, s1, c1 = a_
+            i2, s2, c2 = b_
+            if not np.array_equal(c1, c2):
+                return False
+            m = np.arange(K)[None, :] < c1[:, None]
+            return bool(np.array_equal(i1[m], i2[m])) and _same(s1[m], s2[m])
+
+        assert same_lists(t.top_k_refresh(K), (ids, sc, cnt))  # whole job; keeps the 2k-deep lists
+        bi, bu = zipf_stream_torch(N_USERS, N_ITEMS, 1_250_000, seed=777_000, device="cuda")
+        t.ingest_device_rows(bi.contiguous(), bu.contiguous(), None, int(bi.numel()))
+        t.finalize()
+        got = t.top_k_refresh(K)
+        touched, redone, full = t.refresh_stats()
+        assert full == 1 and 0 < touched < N_ITEMS // 2
+        assert same_lists(got, t.top_k_all(K))
     finally:
         t.close()
         torch.cuda.empty_cache()
