@@ -422,14 +422,27 @@ constexpr int kCandThreads = 256;
 // row asc) -- the SimilarUser order -- and raise its admission threshold to
 // the k-th score.  A list that overflowed its capacity is flagged (its row is
 // recomputed exactly afterwards); the threshold stays a valid lower bound.
+__device__ __forceinline__ double key_score(uint64_t key) {  // inverse of score_key
+  return __longlong_as_double((long long)((key >> 63) ? (key & ~(1ULL << 63)) : ~key));
+}
+
+// sorted == 0 (a pass's compaction): the first k are SELECTED (radix select
+// of the k-th key, then of the owner row among its ties -- the same total
+// order) and kept unordered; only the final compaction (sorted == 1) sorts
+// them for the emit.  A full bitonic sort of a 2048-entry list per owner was
+// 0.3 s of the config-4 job at the first compactions after the multi-limb rows.
 __global__ __launch_bounds__(kCandThreads) void k_cand_compact(const uint32_t* list, const uint32_t* list_n,
                                                                uint32_t* ccnt, uint32_t* cidx, double* cval,
                                                                int32_t cap, int32_t k, const int64_t* perm,
-                                                               double* thr, uint32_t* ovf) {
+                                                               double* thr, uint32_t* ovf, int sorted) {
+  static_assert(kCandThreads == 256, "one histogram bin per thread");
   __shared__ uint64_t key[kCandCapSym];
   __shared__ uint32_t row[kCandCapSym];
   __shared__ uint32_t pid[kCandCapSym];
   __shared__ double val[kCandCapSym];
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_need, s_tied, s_rprefix, s_out;
   const uint32_t nl = *list_n;
   const int tid = threadIdx.x;
   for (uint32_t e = blockIdx.x; e < nl; e += gridDim.x) {
@@ -453,6 +466,78 @@ __global__ __launch_bounds__(kCandThreads) void k_cand_compact(const uint32_t* l
       }
     }
     __syncthreads();
+    if (!sorted) {
+      if (m >= (uint32_t)k) {
+        if (tid == 0) {
+          s_prefix = 0;
+          s_need = (uint32_t)k;
+        }
+        __syncthreads();
+        for (int shift = 56; shift >= 0; shift -= 8) {  // the k-th largest key T
+          hist[tid] = 0;
+          __syncthreads();
+          const uint64_t pre = s_prefix;
+          const uint64_t hmask = shift == 56 ? 0ULL : (~0ULL << (shift + 8));
+          for (uint32_t i = tid; i < m; i += kCandThreads)
+            if ((key[i] & hmask) == pre) atomicAdd(&hist[(key[i] >> shift) & 255u], 1u);
+          __syncthreads();
+          if (tid == 0) {
+            uint32_t need = s_need;
+            int digit = 255;
+            for (; digit > 0; --digit) {
+              if (hist[digit] >= need) break;
+              need -= hist[digit];
+            }
+            s_need = need;
+            s_prefix = pre | ((uint64_t)digit << shift);
+            if (shift == 0) s_tied = hist[digit];
+          }
+          __syncthreads();
+        }
+        const uint64_t T = s_prefix;
+        uint32_t R = 0xFFFFFFFFu;
+        if (s_need < s_tied) {  // among keys == T, the s_need-th smallest owner row R
+          if (tid == 0) s_rprefix = 0;
+          __syncthreads();
+          for (int shift = 24; shift >= 0; shift -= 8) {
+            hist[tid] = 0;
+            __syncthreads();
+            const uint32_t pre = s_rprefix;
+            const uint32_t hmask = shift == 24 ? 0u : (~0u << (shift + 8));
+            for (uint32_t i = tid; i < m; i += kCandThreads)
+              if (key[i] == T && (row[i] & hmask) == pre) atomicAdd(&hist[(row[i] >> shift) & 255u], 1u);
+            __syncthreads();
+            if (tid == 0) {
+              uint32_t need = s_need;
+              int digit = 0;
+              for (; digit < 255; ++digit) {
+                if (hist[digit] >= need) break;
+                need -= hist[digit];
+              }
+              s_need = need;
+              s_rprefix = pre | ((uint32_t)digit << shift);
+            }
+            __syncthreads();
+          }
+          R = s_rprefix;
+        }
+        if (tid == 0) s_out = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < m; i += kCandThreads) {
+          if (key[i] > T || (key[i] == T && row[i] <= R)) {
+            const uint32_t o = atomicAdd(&s_out, 1u);
+            cidx[p * cap + o] = pid[i];
+            cval[p * cap + o] = val[i];
+          }
+        }
+        if (tid == 0) {
+          ccnt[p] = (uint32_t)k;
+          thr[p] = key_score(T);
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     for (uint32_t size = 2; size <= P; size <<= 1) {
       for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
         for (uint32_t i = tid; i < P; i += kCandThreads) {
@@ -628,7 +713,8 @@ int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint
   const unsigned g1 = (unsigned)std::min<int64_t>((np + 255) / 256, 4096);
   hipLaunchKernelGGL(k_cand_select, dim3(g1), dim3(256), 0, h->stream, cb.ccnt, p0, np, limit, cb.list, cb.list_n);
   hipLaunchKernelGGL(k_cand_compact, dim3(4096), dim3(kCandThreads), 0, h->stream, cb.list, cb.list_n, cb.ccnt,
-                     cb.cidx, cb.cval, cb.cap, k, cosine_perm_device(h), cb.thr, cb.ovf);
+                     cb.cidx, cb.cval, cb.cap, k, cosine_perm_device(h), cb.thr, cb.ovf,
+                     limit == 0 || getenv("CMS_SORT_COMPACT") ? 1 : 0);  // only the final compaction sorts
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

@@ -620,14 +620,16 @@ def test_write_similar_items_csv(oracle, tmp_path):
     with SketchTable(n, depth=d, width=w, seed=42, owner_ids=ids_universe) as t:
         t.ingest(ids_universe[items], users)
         t.finalize()
-        ids, sc, cnt = t.top_k_all(k)
         path = tmp_path / "similar.csv"
         t.write_similar_items(str(path), k)
     lines = path.read_text().splitlines()
+    # expected text from the oracle's TopItems lists, not the GPU's own
+    ot = oracle_table(oracle, n, d, w, 42, items, users)
     exp = []
     for r in range(n):
-        for i in range(cnt[r]):
-            exp.append(f"{ids_universe[r]},{ids[r, i]},{java_double_to_string(float(np.float32(sc[r, i])))}")
+        eids, esc = oracle.top_users(np.arange(n), _oracle_row_sims(oracle, ot, r), k)
+        for e, v in zip(eids.tolist(), esc.tolist()):
+            exp.append(f"{ids_universe[r]},{ids_universe[e]},{java_double_to_string(float(np.float32(v)))}")
     assert lines == exp
 
 
@@ -641,20 +643,22 @@ def test_write_similarities_other_driver_formats(oracle, tmp_path):
     with SketchTable(n, depth=d, width=w, seed=42, owner_ids=ids_universe) as t:
         t.ingest(ids_universe[items], users)
         t.finalize()
-        ids, sc, cnt = t.top_k_all(k)
         p1, p2 = tmp_path / "isj.txt", tmp_path / "spark.tsv"
         t.write_similarities(str(p1), k, "item_similarity_job")
         t.write_similarities(str(p2), k, "spark_itemsimilarity")
+    # expected text from the oracle's TopItems lists, not the GPU's own
+    ot = oracle_table(oracle, n, d, w, 42, items, users)
+    lists = [oracle.top_users(np.arange(n), _oracle_row_sims(oracle, ot, r), k) for r in range(n)]
     pairs = {}
-    for r in range(n):
-        for i in range(cnt[r]):
-            a, b = sorted((int(ids_universe[r]), int(ids[r, i])))
-            pairs.setdefault((a, b), float(sc[r, i]))  # lower ID's list first (rows ascend with IDs)
+    for r, (eids, esc) in enumerate(lists):
+        for e, v in zip(eids.tolist(), esc.tolist()):
+            a, b = sorted((int(ids_universe[r]), int(ids_universe[e])))
+            pairs.setdefault((a, b), float(v))  # lower ID's list first (rows ascend with IDs)
     exp1 = [f"{a}\t{b}\t{jd(v)}" for (a, b), v in sorted(pairs.items())]
     assert p1.read_text().splitlines() == exp1
     exp2 = []
-    for r in range(n):
-        el = [f"{ids[r, i]}:{jd(float(sc[r, i]))}" for i in range(cnt[r]) if sc[r, i] != 0.0]
+    for r, (eids, esc) in enumerate(lists):
+        el = [f"{ids_universe[e]}:{jd(float(v))}" for e, v in zip(eids.tolist(), esc.tolist()) if v != 0.0]
         exp2.append(f"{ids_universe[r]}\t" + " ".join(el) if el else f"{ids_universe[r]}")
     assert p2.read_text().splitlines() == exp2
 
