@@ -286,3 +286,182 @@ class GenericUserBasedRecommender:
             return self._sim.table.estimate_preferences(theUserID, theNeighborhood, itemIDs, self._capper)
         except _lib.CmsError as e:
             raise _map_error(e, "user")
+
+
+# ---- the precomputed-similarity consumer ----------------
+# GenericItemSimilarity(Iterable<ItemItemSimilarity>) is how Taste consumes
+# precomputed item-item similarities (T/impl/similarity/GenericItemSimilarity.java:71-95,
+# 172-236); the all-pairs lists of cms_top_k_all / cms_top_k_refresh feed it
+# through ``similarities_from_top_k``.
+
+class ItemItemSimilarity:
+    """GenericItemSimilarity.ItemItemSimilarity (:251-315): value must lie in
+    [-1, 1] (NaN rejected, as Preconditions.checkArgument does, :264-266)."""
+
+    __slots__ = ("itemID1", "itemID2", "value")
+
+    def __init__(self, itemID1, itemID2, value):
+        value = float(value)
+        if not (-1.0 <= value <= 1.0):
+            raise ValueError("Illegal value: %r. Must be: -1.0 <= value <= 1.0" % value)
+        self.itemID1 = int(itemID1)
+        self.itemID2 = int(itemID2)
+        self.value = value
+
+    def getItemID1(self):
+        return self.itemID1
+
+    def getItemID2(self):
+        return self.itemID2
+
+    def getValue(self):
+        return self.value
+
+    def __repr__(self):
+        return "ItemItemSimilarity[%d,%d:%r]" % (self.itemID1, self.itemID2, self.value)
+
+
+def _cmp_item_item(a, b):
+    """ItemItemSimilarity.compareTo (:296-300): highest value first."""
+    return -1 if a.value > b.value else 1 if a.value < b.value else 0
+
+
+class _JavaPriorityQueue:
+    """java.util.PriorityQueue with a comparator: a binary min-heap with the
+    JDK's siftUp / siftDown (offer, poll, peek), so ties leave the queue in
+    the same order the reference's does."""
+
+    def __init__(self, cmp):
+        self.q = []
+        self.cmp = cmp
+
+    def add(self, x):
+        q, cmp = self.q, self.cmp
+        k = len(q)
+        q.append(x)
+        while k > 0:  # siftUpUsingComparator
+            parent = (k - 1) >> 1
+            e = q[parent]
+            if cmp(x, e) >= 0:
+                break
+            q[k] = e
+            k = parent
+        q[k] = x
+
+    def peek(self):
+        return self.q[0]
+
+    def poll(self):
+        q, cmp = self.q, self.cmp
+        result = q[0]
+        x = q.pop()
+        n = len(q)
+        if n:
+            k, half = 0, n >> 1
+            while k < half:  # siftDownUsingComparator
+                child = 2 * k + 1
+                c = q[child]
+                right = child + 1
+                if right < n and cmp(c, q[right]) > 0:
+                    child = right
+                    c = q[child]
+                if cmp(x, c) <= 0:
+                    break
+                q[k] = c
+                k = child
+            q[k] = x
+        return result
+
+    def __len__(self):
+        return len(self.q)
+
+
+def get_top_item_item_similarities(howMany, allSimilarities):
+    """TopItems.getTopItemItemSimilarities (T/impl/recommender/TopItems.java:145-174):
+    a PriorityQueue in reverse compareTo order (lowest value at the head), a
+    strict '>' admission once full, then Collections.sort (stable) of the
+    queue's array order."""
+    import functools
+    pq = _JavaPriorityQueue(lambda a, b: -_cmp_item_item(a, b))  # Collections.reverseOrder()
+    full = False
+    lowest = -math.inf
+    for s in allSimilarities:
+        v = s.value
+        if not math.isnan(v) and (not full or v > lowest):
+            pq.add(s)
+            if full:
+                pq.poll()
+            elif len(pq) > howMany:
+                full = True
+                pq.poll()
+            lowest = pq.peek().value
+    result = list(pq.q)
+    result.sort(key=functools.cmp_to_key(_cmp_item_item))  # stable, as Collections.sort
+    return result
+
+
+class GenericItemSimilarity:
+    """org.apache.mahout.cf.taste.impl.similarity.GenericItemSimilarity over
+    precomputed similarities: ordered (smaller ID first) pair map where a later
+    value wins, a pair of an item with itself skipped (assumed 1.0), and the
+    per-item index of similar items (:172-205)."""
+
+    def __init__(self, similarities, maxToKeep=None):
+        if maxToKeep is not None:
+            similarities = get_top_item_item_similarities(int(maxToKeep), similarities)
+        self._maps = {}
+        self._index = {}
+        for s in similarities:
+            a, b = s.itemID1, s.itemID2
+            if a == b:
+                continue
+            lo, hi = (a, b) if a < b else (b, a)
+            self._maps.setdefault(lo, {})[hi] = s.value
+            self._index.setdefault(lo, set()).add(hi)
+            self._index.setdefault(hi, set()).add(lo)
+
+    @classmethod
+    def from_similarity(cls, otherSimilarity, itemIDs, maxToKeep=None):
+        """GenericItemSimilarity(ItemSimilarity, DataModel[, maxToKeep])
+        (:126-160): every pair i < j of the item IDs in ascending order, NaN
+        pairs skipped, as DataModelSimilaritiesIterator enumerates them
+        (:317-353); one batched itemSimilarities call per item on the GPU."""
+        ids = [int(x) for x in sorted(itemIDs)]
+
+        def pairs():
+            for i, a in enumerate(ids[:-1]):
+                rest = ids[i + 1:]
+                vals = otherSimilarity.itemSimilarities(a, rest)
+                for b, v in zip(rest, vals):
+                    if not math.isnan(v):  # the iterator skips NaN pairs (:341)
+                        yield ItemItemSimilarity(a, b, v)
+        return cls(pairs(), maxToKeep)
+
+    def itemSimilarity(self, itemID1, itemID2):
+        """(:219-236): 1.0 for an item with itself, NaN for a pair never given."""
+        if itemID1 == itemID2:
+            return 1.0
+        lo, hi = (itemID1, itemID2) if itemID1 < itemID2 else (itemID2, itemID1)
+        return self._maps.get(lo, {}).get(hi, math.nan)
+
+    def itemSimilarities(self, itemID1, itemID2s):
+        return np.array([self.itemSimilarity(itemID1, int(b)) for b in itemID2s], np.float64)
+
+    def allSimilarItemIDs(self, itemID):
+        """(:248-251).  The reference returns its FastIDSet's hash order; this
+        returns the same IDs in ascending order (order unpinned)."""
+        return np.array(sorted(self._index.get(int(itemID), ())), np.int64)
+
+    def refresh(self, alreadyRefreshed=None):
+        pass  # (:254-256) does nothing
+
+
+def similarities_from_top_k(ids, scores, counts, owner_ids=None):
+    """ItemItemSimilarity records of the all-pairs lists (cms_top_k_all /
+    cms_top_k_refresh: [n][k] partner IDs and scores, counts[n]) in owner order
+    then list order -- the iterable GenericItemSimilarity(Iterable) takes."""
+    n = len(counts)
+    for r in range(n):
+        a = int(owner_ids[r]) if owner_ids is not None else r
+        for i in range(int(counts[r])):
+            yield ItemItemSimilarity(a, int(ids[r, i]), float(scores[r, i]))

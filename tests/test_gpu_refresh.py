@@ -115,3 +115,33 @@ def test_refresh_owner_ids_and_invalidation():
         got = t.top_k_refresh(k + 5)
         assert t.refresh_stats()[2] == 3
         assert _same_lists(got, t.top_k_all(k + 5)) is None
+
+
+def test_refresh_lists_feed_generic_item_similarity():
+    """The refreshed lists as Taste's precomputed similarities
+    (GenericItemSimilarity(Iterable<ItemItemSimilarity>),
+    GenericItemSimilarity.java:71-95): every listed pair answers with the
+    GPU's own pair similarity, an unlisted pair with NaN."""
+    from mahout_amd.taste import GenericItemSimilarity, similarities_from_top_k
+    n, d, w, k = 600, 4, 256, 8
+    items, users = zipf_stream(2000, n, 60_000, seed=12)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        t.top_k_refresh(k)
+        rng = np.random.Generator(np.random.PCG64(5))
+        rows, keys, v = _batch(rng, n, 0.1, 5000, 1, 2000)
+        t.ingest(rows, keys, v)
+        t.finalize()
+        ids, sc, cnt = t.top_k_refresh(k)
+        g = GenericItemSimilarity(similarities_from_top_k(ids, sc, cnt))
+        listed = set()
+        for r in range(0, n, 37):
+            sims = t.similarities(r, np.arange(n))
+            for i in range(cnt[r]):
+                p = int(ids[r, i])
+                listed.add((min(r, p), max(r, p)))
+                assert g.itemSimilarity(r, p) == sims[p] == g.itemSimilarity(p, r)
+        a, b = next((a, b) for a in range(n) for b in range(a + 1, n) if (a, b) not in listed
+                    and b not in ids[a, :cnt[a]] and a not in ids[b, :cnt[b]])
+        assert np.isnan(g.itemSimilarity(a, b))
