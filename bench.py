@@ -667,6 +667,10 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "keep_lists_whole_job_s": keep_s,
         "refresh_latency_s": sum(lat) / len(lat),
         "refresh_latency_max_s": max(lat),
+        # unique pairs with a touched owner (the ones a refresh recomputes) per second
+        "refresh_recomputed_pairs_per_s": sum((1 - (1 - p["touched_owner_frac"]) ** 2) * n * (n - 1) / 2 / p["refresh_s"]
+                                              for p in periods) / len(periods),
+        "refresh_vs_whole_job": keep_s / (sum(lat) / len(lat)),
         "refresh_periods": periods,
         "full_lists": int((cnt == k).sum()),
         "touched_owner_frac": {"all_batches": touched_all, "per_batch": touched_one,
