@@ -1418,13 +1418,17 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   base.cval = cb.cval;
   base.cap = cap;
   const int8_t* limb0 = h->ws_limb0.as<int8_t>();
-  // 1 + 2. multi-limb rows, kPerPass per chunk: one slab each (M x S as
+  // 1 + 2. multi-limb rows in chunks: one slab each (M x S as
   // virtual limb rows, M x M on the MULTI tiles) gives their exact top-k AND
   // the M candidates of every single-limb row -- each (M, S) pair once
   if (nm > 0) {
     TimedScope ts(h, "topk_all_multi_rows");
-    for (int64_t m0 = (int64_t)shard * kPerPass; m0 < nm; m0 += (int64_t)nshards * kPerPass) {
-      const int64_t qc = std::min<int64_t>(kPerPass, nm - m0);
+    // chunk: a slab of qc rows offers qc similarities to every S list, so a
+    // chunk must leave room in a list compacted to cap - qc entries
+    int64_t chunk = std::min<int64_t>(cap / 2, slab_rows_for(n));
+    if (const char* e = getenv("CMS_M_CHUNK")) chunk = std::max<int64_t>(128, std::min<int64_t>(chunk, atoi(e)));
+    for (int64_t m0 = (int64_t)shard * chunk; m0 < nm; m0 += (int64_t)nshards * chunk) {
+      const int64_t qc = std::min<int64_t>(chunk, nm - m0);
       if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts))) return rc;
     }
   }
