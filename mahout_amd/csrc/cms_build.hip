@@ -254,6 +254,9 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       for (int j = tid; j < w; j += kBuildThreads) {
         uint32_t v = lds[j];
         lds[j] = 0u;
+#ifdef CMS_BUILD_NOSLICEADD  // bound analysis only: the slices' global atomics skipped
+        if (v == 0xFFFFFFFFu)
+#endif
         if (v) atomicAdd(dst + rofs + j, v);
       }
     } else if (two && SV > 0 && (w & 7) == 0) {
