@@ -131,7 +131,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
     int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
-    TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate) {
+    TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate,
+    int slices_done) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w]
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -143,7 +144,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   int64_t row, lo, hi;
   bool atomic_mode;
   if (blockIdx.x < emax) {
-    if (blockIdx.x >= counters[1]) return;
+    if (slices_done || blockIdx.x >= counters[1]) return;  // slices_done: k_build_slices built them
 #ifdef CMS_BUILD_NOSLICES  // bound analysis only: hot rows' extra slices skipped
     return;
 #endif
@@ -451,6 +452,54 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   }
 }
 
+// The extra slices of the hot owners with unit increments (every slice of
+// `slice` keys counts at most slice << frac_bits < 2^16 per bucket): each key
+// is read and reduced mod p ONCE and counted into all d sketch rows at once,
+// two u16 counters per LDS word (d * w / 2 words), then the partial rows are
+// added to the owner's u32 slot row with coalesced atomics.  In k_build_rows
+// a slice walks its 8192+ keys once per sketch row (they do not fit its
+// register cache).  Experiment (CMS_SLICES_KERNEL=1): bit-exact, but slower,
+// since this launch cannot overlap the row build that follows it.
+__global__ __launch_bounds__(256) void k_build_slices(const int64_t* lo_, const int64_t* hi_, const int64_t* keys,
+                                                      HashParams hp, int64_t slice, const HotInfo* hot,
+                                                      const int2* extra_map, const uint32_t* counters, TableView tv,
+                                                      uint64_t* row_mass, uint32_t* flags) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] packed u16 pairs
+  __shared__ unsigned long long s_mass;
+  if (blockIdx.x >= counters[1]) return;
+  const int tid = threadIdx.x;
+  const int w = (int)hp.width;
+  const int64_t dw = (int64_t)hp.depth * w;
+  const int words = (int)(dw >> 1);
+  const int2 m = extra_map[blockIdx.x];
+  const int64_t row = hot[m.x].row;
+  const int64_t lo = lo_[row] + (int64_t)m.y * slice;
+  const int64_t hi = min(hi_[row], lo + slice);
+  for (int j = tid; j < words; j += 256) lds[j] = 0u;
+  if (tid == 0) s_mass = 0ULL;
+  __syncthreads();
+  const uint32_t one = 1u << hp.frac_bits;
+  for (int64_t i = lo + tid; i < hi; i += 256) {
+    const uint64_t kp = reduce_key(keys[i]);
+    for (int r = 0; r < hp.depth; ++r) {
+      const uint32_t c = (uint32_t)r * (uint32_t)w + bucket(hp, r, kp);
+      atomicAdd(&lds[c >> 1], one << ((c & 1u) * 16u));
+    }
+  }
+  __syncthreads();
+  uint32_t* dst = tv.hot + (int64_t)tv.hidx[row] * dw;
+  for (int j = tid; j < words; j += 256) {
+    const uint32_t v = lds[j];
+    if (v & 0xFFFFu) atomicAdd(dst + 2 * j, v & 0xFFFFu);
+    if (v >> 16) atomicAdd(dst + 2 * j + 1, v >> 16);
+  }
+  if (tid == 0) {
+    const uint64_t tm = (uint64_t)(hi - lo) * one;
+    const unsigned long long old = atomicAdd((unsigned long long*)&row_mass[row], (unsigned long long)tm);
+    if (old + tm >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+  }
+}
+
 // Sum of squares of the hot rows after every slice landed; grid (<= 256, depth,
 // chunks of 1024), blocks striding over the hot rows the plan counted (the
 // host's bound on them is loose, and empty blocks still cost launch time).
@@ -559,10 +608,27 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       const char* e = getenv("CMS_BUILD_SV");
       return e ? std::max(0, std::min(2, atoi(e))) : kBuildStoreForm;
     }();
+    // extra slices of unit increments on k_build_slices (one pass over the keys
+    // for all d rows; LDS d*w*2 bytes)
+    const size_t slice_lds = (size_t)h->p.depth * (size_t)h->p.width * 2;
+    // measured SLOWER (config 2 build 1.16 -> 1.33 ms, config 3 18.7 -> 19.8 ms:
+    // the slices then run alone before the rows instead of beside them), so it
+    // is an experiment behind CMS_SLICES_KERNEL=1
+    const int slices_done = !d_val && (h->p.width % 2) == 0 && (kSlice << h->hp.frac_bits) < 65536 &&
+                            slice_lds <= 96 * 1024 && getenv("CMS_SLICES_KERNEL");
+    if (slices_done) {
+      static bool attr = [] {
+        (void)hipFuncSetAttribute((const void*)k_build_slices, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        return true;
+      }();
+      (void)attr;
+      hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(256), slice_lds, h->stream, d_lo, d_hi, d_key,
+                         h->hp, kSlice, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
+    }
     auto kern = sv == 2 ? k_build_rows<2> : sv == 1 ? k_build_rows<1> : k_build_rows<0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                        d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
-                       h->d_norm, h->d_rowmax, h->d_flags, accumulate);
+                       h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done);
     CMS_HIP(hipGetLastError());
   }
   {
