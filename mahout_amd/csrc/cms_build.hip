@@ -124,6 +124,11 @@ __device__ __forceinline__ void store_row(uint4* p, uint4 v, int sv) {
   }
 }
 
+#ifdef CMS_NO_SLICE_PAIRS
+constexpr bool kNoSlicePairs = true;
+#else
+constexpr bool kNoSlicePairs = false;
+#endif
 constexpr int kBuildStoreForm = 2;  // 16-B non-temporal: config-3 build 20.4 -> 19.4 ms, config 2 ~1% (scripts/store_ab.sh)
 
 template <int SV>
@@ -207,7 +212,11 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   // a row is below 2^16 (promote_rows guarantees it), so row d counts in the
   // low and row d+1 in the high half of the same LDS word without a carry
   // between them -- d = 5 takes three update/write-out phases instead of five.
-  const bool pair_rows = !dst && !load_old && !atomic_mode && (w & 3) == 0;
+  // A slice of a split (hot) row with unit increments counts at most
+  // slice << frac_bits < 2^16 per bucket, so it pairs its sketch rows the same
+  // way and walks its (uncached) keys ceil(d/2) times instead of d times.
+  const bool slice_pairs = atomic_mode && !vals && (slice << hp.frac_bits) < 65536 && !kNoSlicePairs;
+  const bool pair_rows = ((!dst && !load_old && !atomic_mode) || slice_pairs) && (w & 3) == 0;
   for (int d = 0; d < hp.depth;) {
     const bool two = pair_rows && d + 1 < hp.depth;
     // ---- updates of sketch row d (and d+1) ----
@@ -251,7 +260,14 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     // ---- write-out of row d, zero/load the slot for row d+1, sum of squares ----
     const int64_t rofs = (int64_t)d * w;
     const bool more = load_old && d + 1 < hp.depth;
-    if (atomic_mode) {  // slices of a split row: always a hot (u32) row
+    if (atomic_mode && two) {  // paired slice rows: low halves row d, high halves row d + 1
+      for (int j = tid; j < w; j += kBuildThreads) {
+        const uint32_t v = lds[j];
+        lds[j] = 0u;
+        if (v & 0xFFFFu) atomicAdd(dst + rofs + j, v & 0xFFFFu);
+        if (v >> 16) atomicAdd(dst + rofs + w + j, v >> 16);
+      }
+    } else if (atomic_mode) {  // slices of a split row: always a hot (u32) row
       for (int j = tid; j < w; j += kBuildThreads) {
         uint32_t v = lds[j];
         lds[j] = 0u;
