@@ -1,13 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark: sketch updates/sec on MI355X (BASELINE.json metric, config 2).
+"""Benchmark: sketch updates/sec + item-pair cosines/sec @1M items on MI355X
+(BASELINE.json metric).
 
-A step = one pass of the sketch-update hot path over one batch resident in
-HBM: the rank's unordered Zipf (item, user) stream -> the finished
-[n_items][d][w] u32 sketch table (partition by owner, LDS row build with the
-zero fill and sum-of-squares fused, hot-row reduce), followed by
-cms_finalize (RCCL all-reduce of the counters when N > 1, norms).  Weak
-scaling: every rank ingests its own 50M-pair shard of the user-hash-sharded
-stream into the shared 100K-item table.
+Headline (`value`): config 3's shape, i.e. the metric's "@1M items" -- a
+500M-pair Zipf stream (10M users x 1M items), d=5, w=8192.  One step = one
+pass of the sketch-update hot path over the stream resident in HBM: reset,
+then the rank's unordered COO (item, user) shard -> the finished
+[1M][5][8192] sketch table (partition by owner, LDS row build with the zero
+fill, norms and row maxima fused), then cms_finalize (with N ranks the packed
+RCCL all-reduce of the counters, then the norms).  With N GPUs the same
+500M-pair stream is user-hash sharded over the ranks (strong scaling: the
+job is fixed, as config 3 states it).
+
+Beside it in the same line: config 4 (all-pairs top-100 of every item on the
+headline's table, cosines/s), config 5 (streaming batches + periodic
+refresh on that table), config 2 (100K items, weak scaling) as a secondary
+ingest line, config 1 (ML-100K shape), and the CPU baselines.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -33,20 +41,48 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-items", type=int, default=100_000)
-    ap.add_argument("--n-users", type=int, default=1_000_000)
-    ap.add_argument("--pairs", type=int, default=50_000_000, help="pairs per rank")
+    # headline: config 3's shape (the metric's "@1M items")
+    ap.add_argument("--n-items", type=int, default=1_000_000)
+    ap.add_argument("--n-users", type=int, default=10_000_000)
+    ap.add_argument("--pairs", type=int, default=500_000_000, help="pairs of the whole stream (sharded over ranks)")
     ap.add_argument("--depth", type=int, default=5)
-    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--width", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the CSR and cosine side measurements")
-    ap.add_argument("--no-cosine-1m", action="store_true", help="skip the 1M-item all-pairs measurement")
+    ap.add_argument("--no-extras", action="store_true", help="skip the CSR, host-buffer and query side measurements")
+    ap.add_argument("--no-config1", action="store_true")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (100K items) secondary ingest line")
+    ap.add_argument("--no-cosine-1m", action="store_true", help="skip configs 4 and 5 on the headline table")
     ap.add_argument("--stream-batches", type=int, default=8, help="config-5 incremental batches per rank")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="config 5: batches between periodic top-k refreshes (cms_top_k_refresh)")
     ap.add_argument("--stream-refresh-multi", action="store_true",
                     help="also run the config-5 streaming phase with a communicator (delta all-gather)")
     return ap.parse_args()
+
+
+def visible_gpu_count(env=None, kfd_nodes="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process may use, WITHOUT initialising HIP (the parent of a
+    self-launched multi-rank run must not touch the GPU before its children
+    do): the KFD topology's GPU nodes (gpu_id != 0), narrowed by
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        for node in os.listdir(kfd_nodes):
+            try:
+                with open(os.path.join(kfd_nodes, node, "gpu_id")) as f:
+                    if int(f.read().strip() or "0") != 0:
+                        n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if v.strip() != "" else 0
+    return n
 
 
 def rank_stream(args, rank, world, device):
@@ -124,7 +160,7 @@ def _timed_blocks(fn, n_rows, block, budget_s):
 
 
 def cpu_baseline(off_d, keys_d, args, budget_s=3.0):
-    """Config-2 ingest on the host cores, two modes x {1 thread, all threads}
+    """Sketch ingest on the host cores, two modes x {1 thread, all threads}
     (oracle/cms_baseline.c):
       faithful  -- the reference cost model: per owner a fresh fp64 sketch
                    (w*d zero fill) and d BigInteger-equivalent (128-bit
@@ -323,28 +359,34 @@ def config1(budget_s=3.0):
     return out
 
 
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")  # this round's committed rocprofv3 summaries
+
+
+def _pmc_file(name):
+    path = os.path.join(PROFILE_DIR, name)
+    return path if os.path.exists(path) else None
+
+
 def pmc_record(kernel, name):
-    """The newest committed PMC summary's record of `kernel` (or {})."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name)))
-    if not files:
+    """This round's committed PMC summary record of `kernel` (or {})."""
+    path = _pmc_file(name)
+    if not path:
         return {}
-    rec = json.load(open(files[-1])).get(kernel) or {}
+    rec = json.load(open(path)).get(kernel) or {}
     return {k: v for k, v in rec.items() if k != "counters_avg_per_dispatch"}
 
 
 def pmc_traffic(kernel, name="pmc_summary.json"):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/<round>/pmc_summary.json, scripts/profile.sh on this bench command:
-    2 * FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name)))
-    if not files:
+    """HBM bytes per launch of `kernel` from this round's committed PMC summary
+    (profiles/r03/<name>, scripts/profile.sh on the same bench command:
+    2 * FETCH_SIZE + WRITE_SIZE, gfx950 FETCH correction); (None, None) when
+    that profile is not committed (a stale round's numbers are never used)."""
+    path = _pmc_file(name)
+    if not path:
         return None, None
-    data = json.load(open(files[-1]))
-    rec = data.get(kernel)
+    rec = json.load(open(path)).get(kernel)
     val = (rec.get("hbm_bytes_per_launch") or rec.get("fetch_bytes_per_dispatch")) if rec else None
-    return val, os.path.relpath(files[-1], ROOT)
+    return val, os.path.relpath(path, ROOT)
 
 
 INT8_MFMA_PEAK_TOPS = 5000.0  # dense int8 MFMA (2x the 2.5 PF bf16 dense peak), MI355X_MICROARCH.md
@@ -411,110 +453,124 @@ def config3_shard(n_items, n_users, total_pairs, rank, world, device, seed=20261
     return torch.cat(out_i), torch.cat(out_u)
 
 
-def cosine_1m(args, local, device, rank=0, world=1):
-    """Configs 3 + 4: the 1M-item table (d=5, w=8192) from a 500M-pair Zipf
-    stream -- user-hash sharded over the ranks and merged by the RCCL
-    all-reduce in cms_finalize -- then mostSimilar top-100 for EVERY item
-    through cms_top_k_all: each unordered pair computed once (int8 limb MFMA,
-    exact fp64 epilogue) and streamed into both items' lists; with G ranks
-    the pairs are split G ways and the partial lists all-gathered and merged
-    (strong scaling: the job is fixed)."""
-    from mahout_amd import SketchTable, comm_unique_id
-    n, d, w, npairs, k = 1_000_000, 5, 8192, 500_000_000, 100
-    t = SketchTable(n, depth=d, width=w, seed=42, device=local)
-    if world > 1:
-        uid = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        t.comm_init(uid[0], rank, world)
-    items, users = config3_shard(n, 10_000_000, npairs, rank, world, device)
-    local_pairs = int(items.numel())
+def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
+    """Roofline of k_build_rows (the ingest's dominant kernel).
 
-    def bar():
-        t.synchronize()
+    Algorithmic bytes per launch = what the row build must move for the table
+    as it is stored: the grouped keys read once (8 B per pair), the owner spans
+    (2 x 8 B per owner) and every counter written once at its stored width
+    (u16 narrow rows, u32 hot rows: cms_stats.stored_bytes).  SURVEY 8(d)
+    prices every counter at 4 B; that figure is reported beside it as
+    `u32_priced_*` -- it exceeds the bytes the kernel has to move, so a
+    fraction of it is not a bandwidth fraction and can pass 1.  `traffic` is
+    the measured HBM bytes per launch of the same kernel (2 x FETCH_SIZE +
+    WRITE_SIZE, gfx950 FETCH correction) from the committed profile."""
+    st = table.stats()
+    n, d, w = table.num_owners, table.depth, table.width
+    stored = int(st["stored_bytes"])
+    alg = local_pairs * 8 + n * 16 + stored
+    u32_alg = local_pairs * 8 + (n + 1) * 8 + n * d * w * 4
+    avg_s = build_ms / build_n * 1e-3 if build_n else None
+    traffic, src = pmc_traffic(pmc_kernel, pmc_file)
+    out = {"bound": "hbm", "kernel": "k_build_rows",
+           "achieved": alg / avg_s / 1e9 if avg_s else None, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+           "frac": alg / avg_s / 1e9 / HBM_PEAK_GBPS if avg_s else None,
+           "traffic": traffic, "traffic_source": src,
+           "frac_traffic": traffic / avg_s / 1e9 / HBM_PEAK_GBPS if traffic and avg_s else None,
+           "algorithmic_bytes_per_launch": alg,
+           "algorithmic_bytes_basis": "keys 8 B/pair + spans 16 B/owner + counters at stored width "
+                                      f"({n - int(st['hot_rows'])} u16 rows, {int(st['hot_rows'])} u32 rows)",
+           "avg_launch_ms": avg_s * 1e3 if avg_s else None,
+           "u32_priced_bytes_per_launch": u32_alg,
+           "u32_priced_GBps": u32_alg / avg_s / 1e9 if avg_s else None}
+    return out
+
+
+def ingest_steps(table, items, users, npairs, steps, warmup, world, breakdown_names):
+    """`warmup` untimed then `steps` timed steps of reset + device COO ingest +
+    finalize, bracketed by barrier + synchronize, max over ranks; HIP events
+    on the library's stream around k_build_rows only (timing level 1); then a
+    separate pass of <= 5 steps with every phase scope timed."""
+    def step():
+        table.reset()
+        table.ingest_device_rows(items, users, None, npairs)
+        table.finalize()
+
+    def barrier():
+        table.synchronize()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    def max_over_ranks(x):
-        if world == 1:
-            return x
-        v = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        return float(v.item())
-
-    # config 3 as a measured step: reset + ingest of this rank's shard + finalize
-    # (with G ranks the packed RCCL all-reduce of the 1M-item table); 1 warm-up
-    # step, then c3_steps timed steps; the last one leaves the table for config 4
-    c3_steps = 5
-
-    def c3_step():
-        t.reset()
-        t.ingest_device_rows(items, users, None, local_pairs)
-        t.finalize()
-
-    c3_step()
-    t.set_timing(True, level=1)
-    t.reset_timing()
-    bar()
+    for _ in range(warmup):
+        step()
+    table.set_timing(True, level=1)
+    table.reset_timing()
+    barrier()
     t0 = time.perf_counter()
-    for _ in range(c3_steps):
-        c3_step()
-    bar()
-    ingest_s = max_over_ranks(time.perf_counter() - t0) / c3_steps
-    b_ms, b_n = t.timing("build_rows")
-    ar_ms, ar_n = t.timing("allreduce")
-    t.set_timing(True, level=2)
-    t.reset_timing()
-    c3_step()
-    t.synchronize()
-    c3_break = {}
-    for name in ["partition", "build_plan", "build_rows", "hot_norms", "norms", "merge_bounds", "merge_pack",
-                 "allreduce", "merge_unpack"]:
-        ms_, n_ = t.timing(name)
+    for _ in range(steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    build_ms, build_n = table.timing("build_rows")
+    ar_ms, ar_n = table.timing("allreduce")
+    table.set_timing(True, level=2)
+    table.reset_timing()
+    bsteps = max(1, min(steps, 5))
+    for _ in range(bsteps):
+        step()
+    table.synchronize()
+    breakdown = {}
+    for name in breakdown_names:
+        ms, n_ = table.timing(name)
         if n_:
-            c3_break[name] = round(ms_, 3)
-    t.set_timing(False)
-    tb = n * d * w * 4  # SURVEY 8(d): the table priced at 4 B per counter (the build stores u16 for all but hot rows)
-    c3_build_bytes = local_pairs * 8 + (n + 1) * 8 + tb  # CSR keys + offsets read, table written once
-    c3_step_bytes = local_pairs * 16 + tb  # per GPU: B_g = N/G * 16 + n*d*w*4
-    config3 = {
-        "workload": f"config 3: {npairs}-pair Zipf stream (10M users x {n} items), d={d} w={w}, user-hash sharded over "
-                    f"{world} GPU(s); one step = reset + ingest of the rank's shard + finalize"
-                    + (" (packed RCCL all-reduce of the table)" if world > 1 else ""),
-        "pairs_per_rank": local_pairs, "steps": c3_steps, "warmup": 1,
-        "ms_per_step": ingest_s * 1e3, "updates_per_s": npairs / ingest_s,
-        "roofline": {"bound": "hbm", "kernel": "k_build_rows",
-                     "achieved": c3_build_bytes / (b_ms / b_n * 1e-3) / 1e9 if b_n else None,
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": c3_build_bytes / (b_ms / b_n * 1e-3) / 1e9 / HBM_PEAK_GBPS if b_n else None,
-                     "algorithmic_bytes_per_launch": c3_build_bytes,
-                     "avg_launch_ms": b_ms / b_n if b_n else None,
-                     "u16_table_write_GBps": (n * d * w * 2) / (b_ms / b_n * 1e-3) / 1e9 if b_n else None},
-        "step_roofline": {"algorithmic_bytes_per_gpu": c3_step_bytes,
-                          "achieved_GBps": c3_step_bytes / ingest_s / 1e9,
-                          "frac": c3_step_bytes / ingest_s / 1e9 / HBM_PEAK_GBPS},
-        "allreduce_ms_per_step": ar_ms / ar_n if ar_n else None,
-        "breakdown_ms_one_step": c3_break,
-    }
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cosine_cpu_baseline(items, users, n, d, w)
-    del items, users
-    torch.cuda.empty_cache()
-    t.release_scratch()
+            breakdown[name] = round(ms / bsteps, 4)
+    table.set_timing(False)
+    barrier()
+    return {"elapsed_s": elapsed, "ms_per_step": elapsed * 1e3 / steps, "build_ms": build_ms, "build_n": build_n,
+            "allreduce_ms_per_step": ar_ms / ar_n if ar_n else None, "breakdown_ms_per_step": breakdown,
+            "breakdown_source": f"{bsteps} extra steps after the timed region with every phase scope event-timed"}
+
+
+BREAKDOWN = ["partition", "build_plan", "build_rows", "hot_norms", "reduce_hot", "norms", "merge_bounds", "merge_pack",
+             "allreduce", "merge_unpack"]
+
+
+def csr_prefix_on_device(items, users, n_owners):
+    """CSR of the owners [0, n_owners) of a COO stream (the CPU baseline's
+    sample), on the GPU (setup only, untimed)."""
+    sel = items < n_owners
+    it, us = items[sel], users[sel]
+    return csr_on_device(it, us, n_owners)
+
+
+def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
+    """Config 4 on the config-3 table the headline just built: mostSimilar
+    top-100 for EVERY one of the 1M items through cms_top_k_all -- each
+    unordered pair computed once (fp4 / int8 MFMA, exact fp64 epilogue) and
+    streamed into both items' lists; with G ranks the pairs are split G ways
+    and the partial lists all-gathered and merged (strong scaling: the job
+    is fixed).  Then config 5 (streaming + periodic refresh) on the same
+    resident table."""
+    n, d, w, k = t.num_owners, t.depth, t.width, 100
     t.set_timing(True)
     t.top_k_rows(0, 128, k)  # limb operands prepared, kernels warm (local work)
     # one untimed job: the blocked operand images and the candidate lists are
     # allocated and written once per table (the timed job is the steady state)
     first_t0 = time.perf_counter()
-    t.top_k_all(k)
+    t.top_k_all_device(k)
     first_job_s = time.perf_counter() - first_t0
     t.reset_timing()
     bar()
     t0 = time.perf_counter()
-    _, _, cnt = t.top_k_all(k)
+    _, _, cnt = t.top_k_all_device(k)  # lists stay in HBM (no 1.6 GB host copy in the timed job)
     bar()
     wall = max_over_ranks(time.perf_counter() - t0)
+    cnt = cnt.cpu().numpy()
     tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves",
                                                "topk_allgather", "topk_merge"]}
     waves_ms, waves_n = t.timing("topk_all_waves")
@@ -543,10 +599,9 @@ def cosine_1m(args, local, device, rank=0, world=1):
     cos_traffic = pmc_traffic("void cms::k_cosine_sym<5, 64, 1>", "cosine_pmc_summary.json")
     cos_pmc = pmc_record("void cms::k_cosine_sym<5, 64, 1>", "cosine_pmc_summary.json")
     cos_pmc8 = pmc_record("void cms::k_cosine_sym<5, 64, 0>", "cosine_pmc_summary.json")
-    t.close()
     return {
-        "workload": f"configs 3+4: {npairs}-pair Zipf stream -> {n}-item table (d={d} w={w}), user-hash sharded over "
-                    f"{world} GPU(s) + RCCL all-reduce; then top-{k} most similar items for every item",
+        "workload": f"config 4: top-{k} most similar items for every one of the {n} items of the config-3 table "
+                    f"(d={d} w={w}; {world} GPU(s), pairs split over the ranks, partial lists all-gathered)",
         "n_gpus": world, "scaling": "strong",
         "unique_item_pair_cosines_per_s": uniq / wall,
         "wall_s": wall,
@@ -580,11 +635,7 @@ def cosine_1m(args, local, device, rank=0, world=1):
         "fp4_owners": nf,
         "timing_ms_rank0": tm,
         "multi_limb_owners": nm, "full_lists": int((cnt == k).sum()), "topk_redo_rows": int(st["topk_redo"]),
-        "config3_ingest_merge_s": ingest_s,
-        "config3_updates_per_s": npairs / ingest_s,
-        "config3": config3,
         "config5_streaming": stream,
-        "cpu_baseline": cpu,
     }
 
 
@@ -619,7 +670,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     t.set_timing(True)
     bar()
     t0 = time.perf_counter()
-    t.top_k_refresh(k)
+    t.top_k_refresh_device(k)
     bar()
     keep_s = max_over_ranks(time.perf_counter() - t0)
     t.reset_timing()
@@ -638,13 +689,18 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
             bar()
             fin_s = max_over_ranks(time.perf_counter() - t0)
             t0 = time.perf_counter()
-            _, _, cnt = t.top_k_refresh(k)
+            _, _, cnt = t.top_k_refresh_device(k)  # lists stay in HBM (Refreshable consumers read them there)
             bar()
             rs = max_over_ranks(time.perf_counter() - t0)
             touched, redone, full = t.refresh_stats()
             periods.append({"after_batch": bi + 1, "finalize_s": round(fin_s, 5), "refresh_s": round(rs, 4),
                             "touched_owner_frac": touched / n, "lists_redone": redone, "whole_jobs": full})
     atomic_ms, atomic_n = t.timing("ingest_atomic")
+    sorted_ms, sorted_n = t.timing("ingest_sorted")
+    kern = "k_ingest_sorted" if sorted_n else "k_ingest_atomic"
+    if sorted_n:
+        atomic_ms, atomic_n = sorted_ms, sorted_n
+    cnt = cnt.cpu().numpy()
     t.set_timing(False)
     total = nb * per_batch * world
     del batches
@@ -653,12 +709,17 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     return {
         "workload": f"config 5: {nb} batches x {per_batch} pairs per GPU into the resident {n}-item table; every "
                     f"{every} batches finalize + incremental top-{k} refresh of every item (cms_top_k_refresh)",
-        "path": "k_ingest_atomic (exact global atomics; norms/row maxima updated incrementally)",
+        "path": f"{kern} (batches of >= 32768 pairs into a live table are grouped by owner first and take "
+                "k_ingest_sorted: exact u32 global atomics, norm / row-max / mass deltas reduced per owner inside the "
+                "wave; smaller batches take k_ingest_atomic)",
         "batches": nb, "pairs_per_batch_per_gpu": per_batch,
         "sustained_updates_per_s": total / ingest_s,
         "batch_latency_ms": ingest_s * 1e3 / nb,
-        "roofline": {"bound": "hbm", "kernel": "k_ingest_atomic",
+        "roofline": {"bound": "hbm", "kernel": kern,
                      "algorithmic_bytes_per_update": 56,
+                     "note": "SURVEY 8(d) prices an incremental update at 56 B of streaming traffic; the kernel's d "
+                             "counter updates per pair are scattered single-dword atomics (one 64-B sector RMW each), "
+                             "whose measured ceiling is far below the streaming rate (DESIGN 4.1)",
                      "achieved": alg / (atomic_ms * 1e-3) / 1e9 if atomic_n else None,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": alg / (atomic_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if atomic_n else None,
@@ -720,11 +781,103 @@ def spawn_ranks(n, child_argv, port=None, timeout=None):
     return 0
 
 
+def config2_line(args, rank, world, local, device):
+    """Config 2 (BASELINE configs[1]): Zipf 1M users x 100K items, 50M pairs
+    per rank (weak scaling), d=5, w=4096 -- the round-1/2 headline, kept as a
+    secondary ingest line with its own roofline; single-GPU extras (CSR and
+    host-buffer ingest, query latency, all-pairs top-100 on this table)."""
+    from mahout_amd import SketchTable, comm_unique_id
+    c2 = argparse.Namespace(n_users=1_000_000, n_items=100_000, pairs=50_000_000)
+    n, d, w = c2.n_items, 5, 4096
+    table = SketchTable(n, depth=d, width=w, seed=42, device=local)
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        table.comm_init(uid[0], rank, world)
+    items, users = rank_stream(c2, rank, world, device)
+    npairs = int(items.numel())
+    torch.cuda.synchronize()
+    steps = max(args.steps, 10)
+    m = ingest_steps(table, items, users, npairs, steps, max(args.warmup, 2), world, BREAKDOWN)
+    value = npairs * world * steps / m["elapsed_s"]
+    roof = build_roofline(table, npairs, m["build_ms"], m["build_n"], "void cms::k_build_rows<2>",
+                          "pmc_summary_config2.json")
+    table_bytes_u32 = n * d * w * 4
+    out = {
+        "workload": f"config 2: Zipf {c2.n_users} users x {n} items, {npairs} pairs per rank, d={d} w={w}; unordered "
+                    "COO (item, user) stream -> finished sketch table + norms (+ packed all-reduce with N ranks)",
+        "scaling": "weak", "steps": steps, "updates_per_s": value, "ms_per_step": m["ms_per_step"],
+        "roofline": roof,
+        "step_roofline": {"algorithmic_bytes": npairs * 16 + table.stats()["stored_bytes"],
+                          "basis": "stream read once (16 B/pair) + counters written once at stored width",
+                          "achieved_GBps": (npairs * 16 + table.stats()["stored_bytes"]) / (m["ms_per_step"] * 1e-3) / 1e9,
+                          "frac": (npairs * 16 + table.stats()["stored_bytes"]) / (m["ms_per_step"] * 1e-3) / 1e9
+                          / HBM_PEAK_GBPS,
+                          "u32_priced_frac": (npairs * 16 + table_bytes_u32) / (m["ms_per_step"] * 1e-3) / 1e9
+                          / HBM_PEAK_GBPS},
+        "breakdown_ms_per_step": m["breakdown_ms_per_step"],
+        "allreduce_ms_per_step": m["allreduce_ms_per_step"],
+    }
+    if world > 1:
+        mw = table.stats()["merge_words"]
+        out["merge"] = {"allreduce_bytes_per_step": mw * 8, "u32_table_bytes": table_bytes_u32,
+                        "payload_ratio": mw * 8 / table_bytes_u32}
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = {}
+        off, ckeys = csr_on_device(items, users, n)
+        # CSR (DataModel layout) ingest of the same stream: no partition pass
+        table.reset()
+        table.ingest_csr_device(off, ckeys)
+        table.finalize()
+        table.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            table.reset()
+            table.ingest_csr_device(off, ckeys)
+            table.finalize()
+        table.synchronize()
+        dt = time.perf_counter() - t0
+        extras["csr_updates_per_s"] = npairs * steps / dt
+        extras["csr_ms_per_step"] = dt * 1e3 / steps
+        del off, ckeys
+        # the same stream handed over in HOST memory (cms_ingest: PCIe copy +
+        # validation + the device path), i.e. the JNI boundary's rate
+        h_items = items.cpu().numpy()
+        h_users = users.cpu().numpy()
+        table.reset()
+        table.ingest(h_items, h_users)
+        table.finalize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            table.reset()
+            table.ingest(h_items, h_users)
+            table.finalize()
+        dt = time.perf_counter() - t0
+        extras["host_buffers_updates_per_s"] = npairs * 3 / dt
+        del h_items, h_users
+        extras["query_latency"] = query_latency(table, n)
+        # all-pairs top-100 over the config-2 table: per-row slab path, then
+        # the symmetric streaming pass (each unordered pair once)
+        extras["allpairs_top100_cfg2"] = allpairs_measure(table, 0, n, 100, n, d, w)
+        t0 = time.perf_counter()
+        _, _, cnt_all = table.top_k_all_device(100)
+        dt = time.perf_counter() - t0
+        extras["allpairs_top100_cfg2_streaming"] = {
+            "wall_s": dt, "unique_item_pair_cosines_per_s": n * (n - 1) / 2 / dt,
+            "full_lists": int((cnt_all == 100).sum().item())}
+        out["extras"] = extras
+    table.close()
+    del items, users
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        # self-launch: one rank per GPU (before any GPU call in this process)
-        have = torch.cuda.device_count()
+        # self-launch: one rank per GPU; this parent never initialises HIP
+        have = visible_gpu_count()
         if have < args.gpus:
             print(f"bench: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
             sys.exit(2)
@@ -742,71 +895,42 @@ def main():
 
     from mahout_amd import SketchTable, comm_unique_id
 
-    table = SketchTable(args.n_items, depth=args.depth, width=args.width, seed=42, device=local)
-    if world > 1:
-        uid = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        table.comm_init(uid[0], rank, world)
-
-    items, users = rank_stream(args, rank, world, device)
-    npairs = int(items.numel())
-    torch.cuda.synchronize()
-
-    def step():
-        table.reset()
-        table.ingest_device_rows(items, users, None, npairs)
-        table.finalize()
-
-    for _ in range(args.warmup):
-        step()
-    # timed steps carry HIP events around the roofline kernel only; the phase
-    # breakdown comes from a separate pass after the timed region
-    table.set_timing(True, level=1)
-    table.reset_timing()
-
-    def barrier():
-        table.synchronize()
+    def bar():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_updates = npairs * world * args.steps
-    value = total_updates / elapsed
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        v = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        return float(v.item())
 
-    build_ms, build_n = table.timing("build_rows")
-    # phase breakdown (every scope timed: slightly slower steps, not the value)
-    table.set_timing(True, level=2)
-    table.reset_timing()
-    bsteps = max(1, min(args.steps, 5))
-    for _ in range(bsteps):
-        step()
-    table.synchronize()
-    breakdown = {}
-    for name in ["partition", "build_plan", "build_rows", "reduce_hot", "norms", "merge_bounds", "merge_pack",
-                 "allreduce", "merge_unpack"]:
-        ms, n = table.timing(name)
-        if n:
-            breakdown[name] = round(ms / bsteps, 4)
+    # secondary lines first (their tables are freed before the 82 GB headline table)
+    config2 = None if args.no_config2 else config2_line(args, rank, world, local, device)
+    cfg1 = None
+    if rank == 0 and world == 1 and not args.no_config1 and not args.no_extras:
+        cfg1 = config1()
+
+    # ---- headline: config 3's shape ----
     n, d, w = args.n_items, args.depth, args.width
-    table_bytes = n * d * w * 4
-    build_alg_bytes = npairs * 8 + (n + 1) * 8 + table_bytes  # CSR keys + offsets read, table written once
-    achieved = build_alg_bytes / (build_ms / build_n * 1e-3) / 1e9 if build_n else None
-    table.set_timing(False)
-    traffic, traffic_src = pmc_traffic("void cms::k_build_rows<2>")  # the 16-B non-temporal store form
-    if traffic is None:
-        traffic, traffic_src = pmc_traffic("cms::k_build_rows")
-
+    table = SketchTable(n, depth=d, width=w, seed=42, device=local)
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        table.comm_init(uid[0], rank, world)
+    items, users = config3_shard(n, args.n_users, args.pairs, rank, world, device)
+    npairs = int(items.numel())
+    torch.cuda.synchronize()
+    m = ingest_steps(table, items, users, npairs, args.steps, args.warmup, world, BREAKDOWN)
+    value = args.pairs * args.steps / m["elapsed_s"]  # the whole stream per step, over all ranks
+    roof = build_roofline(table, npairs, m["build_ms"], m["build_n"], "void cms::k_build_rows<2>",
+                          "pmc_summary.json")
+    st = table.stats()
+    stored = int(st["stored_bytes"])
+    step_bytes = npairs * 16 + stored  # per GPU: its shard read once + its full table written once
+    u32_step_bytes = npairs * 16 + n * d * w * 4  # SURVEY 8(d)'s B_g (4 B per counter)
     result = {
         "metric": METRIC,
         "value": value,
@@ -814,115 +938,70 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": m["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,  # no published number for this path
         "dtype": "u32",
         "data": "synthetic Zipf stream (items ~ rank^-1.1, users ~ rank^-0.9), generated on the GPU, resident in HBM",
         "config": {
-            "workload": f"config 2: Zipf {args.n_users} users x {n} items, {npairs} pairs per rank, d={d} w={w}; "
-                        "unordered COO (item, user) stream -> finished u32 sketch table + norms",
-            "n_items": n, "n_users": args.n_users, "pairs_per_rank": npairs, "depth": d, "width": w,
+            "workload": f"config 3 shape (@1M items): Zipf {args.n_users} users x {n} items, {args.pairs}-pair stream "
+                        f"user-hash sharded over {world} GPU(s) ({npairs} pairs on rank {rank}), d={d} w={w}; one "
+                        "step = reset + unordered COO shard -> finished sketch table + norms"
+                        + (" + packed RCCL all-reduce of the counters" if world > 1 else ""),
+            "n_items": n, "n_users": args.n_users, "pairs": args.pairs, "pairs_per_rank": npairs, "depth": d,
+            "width": w,
             "sharding": "user-hash (splitmix64) across ranks; RCCL all-reduce of the counters, counter-width-adaptive "
                         "packed (bit-identical to a u32 sum)",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "k_build_rows",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            # the measured HBM bytes (PMC) per launch over the same launch time
-            "frac_traffic": (traffic / (build_ms / build_n * 1e-3) / 1e9 / HBM_PEAK_GBPS)
-            if traffic and build_n else None,
-            "algorithmic_bytes_per_launch": build_alg_bytes,
-            "avg_launch_ms": build_ms / build_n if build_n else None,
-        },
-        "step_roofline": {
-            "algorithmic_bytes": npairs * 16 + table_bytes,
-            "achieved_GBps": (npairs * 16 + table_bytes) / (ms_per_step * 1e-3) / 1e9,
-            "frac": (npairs * 16 + table_bytes) / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-        },
-        "breakdown_ms_per_step": breakdown,
-        "breakdown_source": f"{bsteps} extra steps after the timed region with every phase scope event-timed",
+        "roofline": roof,
+        "step_roofline": {"algorithmic_bytes_per_gpu": step_bytes,
+                          "basis": "shard read once (16 B/pair) + every counter written once at stored width",
+                          "achieved_GBps": step_bytes / (m["ms_per_step"] * 1e-3) / 1e9,
+                          "frac": step_bytes / (m["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                          "u32_priced_bytes_per_gpu": u32_step_bytes,
+                          "u32_priced_GBps": u32_step_bytes / (m["ms_per_step"] * 1e-3) / 1e9},
+        "breakdown_ms_per_step": m["breakdown_ms_per_step"],
+        "breakdown_source": m["breakdown_source"],
+        "allreduce_ms_per_step": m["allreduce_ms_per_step"],
+        "table": {"stored_bytes": stored, "hot_rows": int(st["hot_rows"]), "u32_bytes": n * d * w * 4},
     }
     if world > 1:
-        mw = table.stats()["merge_words"]
-        result["merge"] = {"allreduce_bytes_per_step": mw * 8, "u32_table_bytes": table_bytes,
-                           "payload_ratio": mw * 8 / table_bytes}
-
-    off = ckeys = None
-    # extras run on a single GPU only: with a communicator, finalize and the
-    # all-pairs top-k are collectives every rank must join
-    extras_on = rank == 0 and world == 1 and not args.no_extras
-    if rank == 0 and (extras_on or not args.no_cpu_baseline):
-        off, ckeys = csr_on_device(items, users, n)
-    if extras_on:
-        extras = {}
-        # CSR (DataModel layout) ingest of the same stream: no partition pass
-        table.reset()
-        table.ingest_csr_device(off, ckeys)
-        table.finalize()
-        table.synchronize()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            table.reset()
-            table.ingest_csr_device(off, ckeys)
-            table.finalize()
-        table.synchronize()
-        dt = time.perf_counter() - t0
-        extras["csr_updates_per_s"] = npairs * args.steps / dt
-        extras["csr_ms_per_step"] = dt * 1e3 / args.steps
-        # the same stream handed over in HOST memory (cms_ingest: PCIe copy +
-        # validation + the device path), i.e. the JNI boundary's rate
-        h_items = items.cpu().numpy()
-        h_users = users.cpu().numpy()
-        table.reset()
-        table.ingest(h_items, h_users)
-        table.finalize()
-        t0 = time.perf_counter()
-        for _ in range(3):
-            table.reset()
-            table.ingest(h_items, h_users)
-            table.finalize()
-        dt = time.perf_counter() - t0
-        extras["host_buffers_updates_per_s"] = npairs * 3 / dt
-        del h_items, h_users
-        extras["query_latency"] = query_latency(table, n)
-        # all-pairs top-100 over the config-2 table (int8-limb MFMA + exact fp64 epilogue)
-        extras["allpairs_top100_cfg2"] = allpairs_measure(table, 0, n, 100, n, d, w)
-        # the same lists through the symmetric streaming pass (each unordered pair once)
-        t0 = time.perf_counter()
-        _, _, cnt_all = table.top_k_all(100)
-        dt = time.perf_counter() - t0
-        extras["allpairs_top100_cfg2_streaming"] = {
-            "wall_s": dt, "unique_item_pair_cosines_per_s": n * (n - 1) / 2 / dt,
-            "full_lists": int((cnt_all == 100).sum())}
-        result["extras"] = extras
+        mw = st["merge_words"]
+        result["merge"] = {"allreduce_bytes_per_step": mw * 8, "u32_table_bytes": n * d * w * 4,
+                           "payload_ratio": mw * 8 / (n * d * w * 4)}
     if rank == 0 and not args.no_cpu_baseline:
+        # bounded sample of the same workload: the owners [0, 65536) of rank 0's
+        # shard (IDs are a seeded permutation of popularity ranks, so an ID
+        # prefix is a popularity-unbiased sample)
+        off, ckeys = csr_prefix_on_device(items, users, 65536)
         result["cpu_baseline"] = cpu_baseline(off, ckeys, args)
+        result["cpu_baseline"]["sample"] = ("owners [0, 65536) of the config-3-shape stream (rank 0's shard), in ID "
+                                            "order, blocks of 512 / 4096 owners, ~3 s per leg; value = faithful mode "
+                                            "(fp64 sketch per owner, 128-bit BigInteger-equivalent hash) on "
+                                            f"{result['cpu_baseline']['cores']} threads")
         result["vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
-        if world == 1 and not args.no_extras:
-            result["config1"] = config1()
-    del off, ckeys
-    table.close()
+        del off, ckeys
+    cos_cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_cosine_1m:
+        cos_cpu = cosine_cpu_baseline(items, users, n, d, w)
     del items, users
     torch.cuda.empty_cache()
-    if world > 1:
-        dist.barrier()
     if not args.no_cosine_1m:
         try:
-            cos = cosine_1m(args, local, device, rank, world)
+            table.release_scratch()
+            cos = cosine_1m(args, table, local, device, rank, world, bar, max_over_ranks)
+            cos["cpu_baseline"] = cos_cpu
             if rank == 0:
                 result["cosine"] = cos
         except Exception as e:  # the headline line must still be printed
             if rank == 0:
                 result["cosine"] = {"error": f"{type(e).__name__}: {e}"}
+    table.close()
+    if config2 is not None:
+        result["config2"] = config2
+    if cfg1 is not None:
+        result["config1"] = cfg1
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -241,8 +241,14 @@ int cms_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t 
  * scope table): the same lists as cms_top_k_rows(h, 0, num_owners, ...), but
  * each unordered pair's similarity is computed once and streamed into both
  * owners' lists (no n x n slab).  ids/scores are [num_owners][k] by owner
- * row, counts[num_owners]; k <= 512. */
+ * row, counts[num_owners]; k <= 512.  Entries past counts[r] in row r are
+ * padding with a defined value: ID -1 and a NaN score (every byte 0xFF), for
+ * this call and for cms_top_k_refresh and the _device variants below. */
 int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts);
+/* cms_top_k_all with the lists left on the device: d_ids / d_scores
+ * [num_owners][k] and d_counts [num_owners] on the handle's GPU (no host copy
+ * of the 1.6 GB answer at 1M owners, k = 100).  Returns when they are written. */
+int cms_top_k_all_device(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
 /* With a communicator (cms_comm_init, world G > 1) cms_top_k_all is collective:
  * rank r computes shard r of the pairs, the partial lists are all-gathered
  * over RCCL and merged exactly; every rank receives the full result
@@ -265,6 +271,9 @@ int cms_top_k_merge(cms_handle* h, int32_t k, int32_t nparts, const int64_t* ids
  * lists, and recompute whole any list that lost its exactness margin.
  * Collective like cms_top_k_all with a communicator. */
 int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts);
+/* cms_top_k_refresh into device buffers (layout and padding as
+ * cms_top_k_all_device). */
+int cms_top_k_refresh_device(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts);
 /* Statistics of the last cms_top_k_refresh: owners touched (num_owners for a
  * whole job), lists recomputed whole, whole jobs so far. */
 int cms_refresh_stats(cms_handle* h, int64_t* touched, int64_t* redone, int64_t* full_jobs);
@@ -363,6 +372,8 @@ typedef struct cms_stats {
   int64_t deep_limb_owners;  /* of those, owners with a counter >= 2^14 (3+ limbs); -1 before */
   int64_t fp4_owners;        /* single-limb owners with every counter <= 4 (fp4 MFMA operands); -1 before */
   int64_t merge_words;       /* u64 words the last multi-rank merge all-reduced (packed counters) */
+  int64_t hot_rows;          /* owners whose counters are stored as u32 (the others narrow) */
+  int64_t stored_bytes;      /* bytes of counters as stored: what one whole-table build writes */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -42,6 +42,7 @@ EXPORTS = [
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
     "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities", "cms_write_similarities_threshold",
     "cms_comm_init_transport", "cms_read_counters_device", "cms_top_k_refresh", "cms_refresh_stats",
+    "cms_top_k_all_device", "cms_top_k_refresh_device",
 ]
 
 
@@ -75,6 +76,8 @@ class CmsStats(ctypes.Structure):
         ("deep_limb_owners", ctypes.c_int64),
         ("fp4_owners", ctypes.c_int64),
         ("merge_words", ctypes.c_int64),
+        ("hot_rows", ctypes.c_int64),
+        ("stored_bytes", ctypes.c_int64),
     ]
 
 
@@ -124,6 +127,8 @@ _SIGS = {
     "cms_top_k_merge": (_int, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cms_top_k_all": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_top_k_refresh": (_int, [_vp, _i32, _vp, _vp, _vp]),
+    "cms_top_k_all_device": (_int, [_vp, _i32, _vp, _vp, _vp]),
+    "cms_top_k_refresh_device": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_refresh_stats": (_int, [_vp, _vp, _vp, _vp]),
     "cms_read_counters": (_int, [_vp, _i64, _i64, _vp]),
     "cms_get_stats": (_int, [_vp, ctypes.POINTER(CmsStats)]),

@@ -681,6 +681,9 @@ int cms_release_scratch(cms_handle* h) {
                   &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked, &h->rf_ids, &h->rf_sc, &h->rf_cnt,
                   &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};
   for (DevBuf* b : ws) b->release();
+  // the kept refresh lists and touched marks are gone: the next COO ingest must not mark
+  // into rf_touch, and the next cms_top_k_refresh is a whole job
+  h->rf_valid = false;
   return CMS_OK;
 }
 
@@ -827,6 +830,7 @@ int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   };
   int rc = merge_packed(h, ext);
   if (rc) return rc;
+  h->rf_valid = false;  // the table is now the cross-rank sum: kept lists describe the local table
   h->ext_merged = true;
   if ((rc = compute_norms(h))) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
@@ -1075,6 +1079,16 @@ int top_k_all_job(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, in
 }  // namespace cms
 }
 
+// Padding of the [n][k] list outputs: entries past counts[r] hold ID -1 and a
+// NaN score (all-ones bytes), written before the job so the kernels' valid
+// prefixes overwrite it (include/mahout_cms.h, cms_top_k_all).
+static int pad_lists(cms_handle* h, int64_t k, int64_t* d_ids, double* d_sc) {
+  const size_t cells = (size_t)h->n * (size_t)k;
+  CMS_HIP(hipMemsetAsync(d_ids, 0xFF, sizeof(int64_t) * cells, h->stream));
+  if (d_sc) CMS_HIP(hipMemsetAsync(d_sc, 0xFF, sizeof(double) * cells, h->stream));
+  return CMS_OK;
+}
+
 static int copy_out_lists(cms_handle* h, int64_t k, const DevBuf& o_ids, const DevBuf& o_sc, const DevBuf& o_cnt,
                           int64_t* ids, double* scores, int32_t* counts) {
   const int64_t n = h->n;
@@ -1087,9 +1101,14 @@ static int copy_out_lists(cms_handle* h, int64_t k, const DevBuf& o_ids, const D
   return CMS_OK;
 }
 
+static int check_k(int32_t k) {
+  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  return CMS_OK;
+}
+
 int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts) {
   if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
-  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+  if (int rc0 = check_k(k)) return rc0;
   Guard g(h);
   int rc = require_finalized(h);
   if (rc) return rc;
@@ -1098,31 +1117,34 @@ int cms_top_k_all(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_
   CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
   CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
   CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
+  if ((rc = pad_lists(h, k, o_ids.as<int64_t>(), o_sc.as<double>()))) return rc;
   rc = top_k_all_job(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
   if (rc == CMS_OK) rc = copy_out_lists(h, k, o_ids, o_sc, o_cnt, ids, scores, counts);
   return rc;
 }
 
-// Incremental all-pairs top-k (the periodic refresh of a streaming table):
-// the result of cms_top_k_all on the current table, computed from the lists
-// the previous refresh kept plus the pairs with an owner a COO batch touched
-// since (cms_topk.hip, k_rf_fold, states the exactness argument).
-int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts) {
-  if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
-  if (k < 1 || k > kCandCap / 2) return set_error(CMS_E_PARAM, "k must be in [1, %d]", kCandCap / 2);
+int cms_top_k_all_device(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  if (!h || !d_ids || !d_scores || !d_counts) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = check_k(k)) return rc0;
   Guard g(h);
   int rc = require_finalized(h);
   if (rc) return rc;
+  if ((rc = pad_lists(h, k, d_ids, d_scores))) return rc;
+  if ((rc = top_k_all_job(h, k, d_ids, d_scores, d_counts))) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return check_flags(h, false);
+}
+
+// Incremental all-pairs top-k (the periodic refresh of a streaming table):
+// the result of cms_top_k_all on the current table, computed from the lists
+// the previous refresh kept plus the pairs with an owner a COO batch touched
+// since (cms_topk.hip, k_rf_fold, states the exactness argument).  Writes the
+// k-deep answer into the device buffers o_* (already padded).
+static int top_k_refresh_job(cms_handle* h, int32_t k, int64_t* o_ids, double* o_sc, int32_t* o_cnt) {
   const int64_t n = h->n;
-  DevBuf o_ids, o_sc, o_cnt;
-  CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
-  CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
-  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
-  if (h->per_owner || h->f64) {  // no kept lists for these modes: the whole job
-    rc = top_k_all_job(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>());
-    if (rc == CMS_OK) rc = copy_out_lists(h, k, o_ids, o_sc, o_cnt, ids, scores, counts);
-    return rc;
-  }
+  int rc = CMS_OK;
+  if (h->per_owner || h->f64)  // no kept lists for these modes: the whole job
+    return top_k_all_job(h, k, o_ids, o_sc, o_cnt);
   // kept lists are twice as deep as the answer, so a few candidates of an
   // untouched owner may leave before its list must be recomputed
   const int32_t D = std::min(2 * k, kCandCap / 2);
@@ -1134,8 +1156,12 @@ int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, in
   } rows_out{h, h->d_owner_ids};
   h->d_owner_ids = nullptr;
   const bool full = !h->rf_valid || h->rf_k != k || h->rf_depth != D;
+  // Until this call completes the kept lists are not trusted: a failure at any
+  // step below (after the fold has rewritten some lists, say) leaves rf_valid
+  // false, so the next refresh is a whole job and no COO ingest marks into
+  // the touched-owner array meanwhile.
+  h->rf_valid = false;
   if (full) {
-    h->rf_valid = false;
     CMS_HIP(h->rf_ids.ensure(sizeof(int64_t) * (size_t)n * D));
     CMS_HIP(h->rf_sc.ensure(sizeof(double) * (size_t)n * D));
     CMS_HIP(h->rf_cnt.ensure(sizeof(int32_t) * (size_t)n));
@@ -1205,8 +1231,35 @@ int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, in
   CMS_HIP(hipMemsetAsync(h->rf_touch.ptr, 0, (size_t)n, h->stream));
   h->rf_valid = true;
   h->d_owner_ids = rows_out.saved;
-  if ((rc = refresh_emit(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>()))) return rc;
+  return refresh_emit(h, k, o_ids, o_sc, o_cnt);
+}
+
+int cms_top_k_refresh(cms_handle* h, int32_t k, int64_t* ids, double* scores, int32_t* counts) {
+  if (!h || !ids || !counts) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = check_k(k)) return rc0;
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  const int64_t n = h->n;
+  DevBuf o_ids, o_sc, o_cnt;
+  CMS_HIP(o_ids.ensure(sizeof(int64_t) * n * k));
+  CMS_HIP(o_sc.ensure(sizeof(double) * n * k));
+  CMS_HIP(o_cnt.ensure(sizeof(int32_t) * n));
+  if ((rc = pad_lists(h, k, o_ids.as<int64_t>(), o_sc.as<double>()))) return rc;
+  if ((rc = top_k_refresh_job(h, k, o_ids.as<int64_t>(), o_sc.as<double>(), o_cnt.as<int32_t>()))) return rc;
   return copy_out_lists(h, k, o_ids, o_sc, o_cnt, ids, scores, counts);
+}
+
+int cms_top_k_refresh_device(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+  if (!h || !d_ids || !d_scores || !d_counts) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = check_k(k)) return rc0;
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  if ((rc = pad_lists(h, k, d_ids, d_scores))) return rc;
+  if ((rc = top_k_refresh_job(h, k, d_ids, d_scores, d_counts))) return rc;
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return check_flags(h, false);
 }
 
 int cms_refresh_stats(cms_handle* h, int64_t* touched, int64_t* redone, int64_t* full_jobs) {
@@ -1394,6 +1447,11 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;
   out->fp4_owners = h->mfma_ready ? h->n_f4 : -1;
   out->merge_words = h->merge_words;
+  out->hot_rows = hot_rows;
+  out->stored_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
+                     : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
+                                   : (int64_t)sizeof(uint16_t) * (h->n - hot_rows) * h->dw +
+                                    (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
   return CMS_OK;
 }
 

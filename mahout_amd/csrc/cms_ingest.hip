@@ -428,7 +428,7 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
           return rc;
         if ((rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true))) return rc;
       }
-      TimedScope ts(h, "ingest_atomic");
+      TimedScope ts(h, "ingest_sorted");
       h->stale_possible = true;
       unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
       hipLaunchKernelGGL(k_ingest_sorted, dim3(grid), dim3(256), 0, h->stream, h->ws_srow.as<int32_t>(), ckey, cval,

@@ -91,6 +91,10 @@ class SketchTable:
         check(create(ctypes.byref(p), ctypes.byref(h)))
         self.per_owner = per_owner
         self.counters = counters
+        if device < 0:  # the handle took the current HIP device at creation
+            import torch
+            device = torch.cuda.current_device()
+        self.device = int(device)
         self._lib = lib
         self._h = h
         self.num_owners = num_owners
@@ -318,20 +322,42 @@ class SketchTable:
         """mostSimilar lists of every owner, [num_owners][k] by owner row
         (symmetric streaming all-pairs pass)."""
         n = self.num_owners
-        ids = np.zeros((n, k), np.int64)
-        sc = np.zeros((n, k), np.float64)
-        cnt = np.zeros(n, np.int32)
+        # uninitialised on purpose: the library defines every cell (ID -1 and a
+        # NaN score past a row's count)
+        ids = np.empty((n, k), np.int64)
+        sc = np.empty((n, k), np.float64)
+        cnt = np.empty(n, np.int32)
         check(self._lib.cms_top_k_all(self._h, int(k), _ptr(ids), _ptr(sc), _ptr(cnt)))
         return ids, sc, cnt
+
+    def _device_lists(self, k):
+        import torch
+        dev = torch.device("cuda", self.device)
+        n = self.num_owners
+        return (torch.empty((n, k), dtype=torch.int64, device=dev), torch.empty((n, k), dtype=torch.float64, device=dev),
+                torch.empty(n, dtype=torch.int32, device=dev))
+
+    def top_k_all_device(self, k):
+        """top_k_all(k) with the lists left on the handle's GPU as torch
+        tensors (cms_top_k_all_device): (ids [n][k], scores [n][k], counts [n])."""
+        out = self._device_lists(k)
+        check(self._lib.cms_top_k_all_device(self._h, int(k), *[ctypes.c_void_p(x.data_ptr()) for x in out]))
+        return out
+
+    def top_k_refresh_device(self, k):
+        """top_k_refresh(k) into device tensors (cms_top_k_refresh_device)."""
+        out = self._device_lists(k)
+        check(self._lib.cms_top_k_refresh_device(self._h, int(k), *[ctypes.c_void_p(x.data_ptr()) for x in out]))
+        return out
 
     def top_k_refresh(self, k):
         """The same lists as top_k_all(k), recomputing only the pairs with an
         owner touched by COO ingests since the previous refresh (the first
         call runs the whole job and keeps 2k-deep lists on the device)."""
         n = self.num_owners
-        ids = np.zeros((n, k), np.int64)
-        sc = np.zeros((n, k), np.float64)
-        cnt = np.zeros(n, np.int32)
+        ids = np.empty((n, k), np.int64)
+        sc = np.empty((n, k), np.float64)
+        cnt = np.empty(n, np.int32)
         check(self._lib.cms_top_k_refresh(self._h, int(k), _ptr(ids), _ptr(sc), _ptr(cnt)))
         return ids, sc, cnt
 
@@ -386,18 +412,31 @@ class SketchTable:
         return out
 
     def read_counters_device(self, row_begin=0, row_count=None, out=None):
-        """Counters as a u32 torch tensor [row_count][d][w] on the handle's
-        device, in counter units (cms_read_counters_device)."""
+        """Counters [row_count][d][w] on the handle's device, in counter units
+        (cms_read_counters_device).  The tensor is torch.int32 holding the u32
+        bits (torch's integer reductions work on it); a counter at or above
+        2^31 reads negative -- use .view(torch.uint32) or mask with 0xFFFFFFFF
+        in int64 where such counters can occur."""
         import torch
         if row_count is None:
             row_count = self.num_owners - row_begin
         if out is None:
-            out = torch.empty((row_count, self.depth, self.width), dtype=torch.int32, device="cuda")
+            out = torch.empty((row_count, self.depth, self.width), dtype=torch.int32,
+                              device=torch.device("cuda", self.device))
+        if out.device != torch.device("cuda", self.device) or out.element_size() != 4 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous 4-byte tensor on cuda:%d" % self.device)
+        if out.numel() < row_count * self.depth * self.width:
+            raise ValueError("out holds fewer than row_count * depth * width counters")
         check(self._lib.cms_read_counters_device(self._h, int(row_begin), int(row_count), ctypes.c_void_p(out.data_ptr())))
         s = torch.cuda.current_stream(out.device).cuda_stream
         if s:  # later torch work on this stream waits for the copy
             check(self._lib.cms_release_to_stream(self._h, ctypes.c_void_p(s)))
         return out
+
+    def release_scratch(self):
+        """cms_release_scratch: ingest/query scratch and the kept refresh lists
+        go back to the allocator (the next refresh is a whole job)."""
+        check(self._lib.cms_release_scratch(self._h))
 
     # -- instrumentation --
     def stats(self):
@@ -433,13 +472,6 @@ def shard_of_keys(keys, world):
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
     return (z % np.uint64(world)).astype(np.int32)
-
-
-def _release_scratch(self):
-    check(self._lib.cms_release_scratch(self._h))
-
-
-SketchTable.release_scratch = _release_scratch
 
 
 def java_double_to_string(v):

@@ -127,8 +127,10 @@ def test_config34_full_size(oracle):
             i2, s2, c2 = b_
             if not np.array_equal(c1, c2):
                 return False
-            m = np.arange(K)[None, :] < c1[:, None]
-            return bool(np.array_equal(i1[m], i2[m])) and _same(s1[m], s2[m])
+            pad = np.arange(K)[None, :] >= c1[:, None]
+            if not ((i1[pad] == -1).all() and np.isnan(s1[pad]).all()):  # defined padding
+                return False
+            return bool(np.array_equal(i1, i2)) and _same(s1, s2)
 
         assert same_lists(t.top_k_refresh(K), (ids, sc, cnt))  # whole job; keeps the 2k-deep lists
         bi, bu = zipf_stream_torch(N_USERS, N_ITEMS, 1_250_000, seed=777_000, device="cuda")
@@ -138,6 +140,21 @@ def test_config34_full_size(oracle):
         touched, redone, full = t.refresh_stats()
         assert full == 1 and 0 < touched < N_ITEMS // 2
         assert same_lists(got, t.top_k_all(K))
+        # refreshed lists of 2 touched and 2 untouched owners against the
+        # oracle's TopItems loop over the updated table's exact similarities
+        tb = np.unique(bi.cpu().numpy())
+        untouched = np.setdiff1d(np.flatnonzero(counts), tb)
+        gi, gs, gc = got
+        for row in np.concatenate([rng.choice(tb, 2, replace=False), rng.choice(untouched, 2, replace=False)]).tolist():
+            sims = t.similarities(row, all_ids)
+            sims[row] = np.nan
+            eids, esc = oracle.top_users(all_ids, sims, K)
+            assert gi[row, :gc[row]].tolist() == eids.tolist(), row
+            assert _same(gs[row, :gc[row]], esc), row
+            sa = t.read_counters(row, 1)[0]
+            for p in np.concatenate([gi[row, :gc[row]][:20], rng.choice(N_ITEMS, 20, replace=False)]).tolist():
+                if p != row:
+                    assert _same(np.array([sims[p]]), np.array([oracle.cosine_cm(sa, t.read_counters(p, 1)[0])])), (row, p)
     finally:
         t.close()
         torch.cuda.empty_cache()

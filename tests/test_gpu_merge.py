@@ -52,7 +52,8 @@ def _worker(rank, world, port, q, case):
         from mahout_amd import SketchTable
         from mahout_amd.sketch import shard_of_keys
         from mahout_amd.synth import zipf_stream
-        n, d, w, npairs, vmax = case
+        n, d, w, npairs, vmax = case[:5]
+        refresh_k = case[5] if len(case) > 5 else 0
         items, users = zipf_stream(30000, n, npairs, seed=n)
         vals = None
         if vmax > 1:
@@ -72,15 +73,33 @@ def _worker(rank, world, port, q, case):
 
         with SketchTable(n, depth=d, width=w, seed=42, device=0) as t:
             t.ingest(items[mine], users[mine], None if vals is None else vals[mine])
+            if refresh_k:
+                # kept refresh lists of the LOCAL (shard) table; the merge below
+                # replaces the table, so the next refresh must be a whole job
+                t.finalize()
+                t.top_k_refresh(refresh_k)
             t.finalize_with(allreduce)
             got = t.read_counters()
             sims = t.similarities(1, np.arange(n))
+            if refresh_k:
+                lists = t.top_k_refresh(refresh_k)
+                full_jobs = t.refresh_stats()[2]
+                whole = t.top_k_all(refresh_k)
         a, b = O.hash_params(42, d)
         full = O.build_table(n, d, w, a, b, items, users, vals)
         exp = O.similarities_row(full, 1)
         exp[1] = O.cosine_cm(full[1], full[1])
         ok_t = bool(np.array_equal(got, full))
         ok_s = bool(np.all((sims == exp) | (np.isnan(sims) & np.isnan(exp))))
+        if refresh_k:
+            ids, sc, cnt = lists
+            ok_s = ok_s and full_jobs == 2
+            ok_s = ok_s and all(np.array_equal(x, y, equal_nan=True) for x, y in zip(lists, whole))
+            for row in (0, 1, n // 2, n - 1):  # TopItems.getTopUsers over the merged table
+                er = O.similarities_row(full, row)
+                eids, esc = O.top_users(np.arange(n, dtype=np.int64), er, refresh_k)
+                ok_s = ok_s and ids[row, :cnt[row]].tolist() == eids.tolist()
+                ok_s = ok_s and np.array_equal(sc[row, :cnt[row]], esc, equal_nan=True)
         q.put((rank, ok_t, ok_s, moved))
     except Exception as e:  # noqa: BLE001
         import traceback
@@ -90,7 +109,8 @@ def _worker(rank, world, port, q, case):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", [(800, 4, 512, 200_000, 1), (300, 5, 1000, 150_000, 5), (64, 3, 128, 400_000, 1)])
+@pytest.mark.parametrize("case", [(800, 4, 512, 200_000, 1), (300, 5, 1000, 150_000, 5), (64, 3, 128, 400_000, 1),
+                                  (800, 4, 512, 200_000, 2, 20)])  # + refresh lists across the merge
 def test_packed_merge_two_ranks_bit_exact(case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -19,19 +19,39 @@ pytestmark = pytest.mark.gpu
 
 
 def _same_lists(a, b):
+    """Bit equality of two (ids, scores, counts) answers, padding included:
+    past counts[r] every ID is -1 and every score NaN (include/mahout_cms.h,
+    cms_top_k_all)."""
     ids, sc, cnt = a
     rids, rsc, rcnt = b
     if not np.array_equal(cnt, rcnt):
         return "counts differ at rows %s" % np.nonzero(cnt != rcnt)[0][:10].tolist()
     n, k = ids.shape
-    mask = np.arange(k)[None, :] < cnt[:, None]
-    if not np.array_equal(np.where(mask, ids, -1), np.where(mask, rids, -1)):
-        return "ids differ at rows %s" % np.nonzero((np.where(mask, ids, -1) != np.where(mask, rids, -1)).any(1))[0][:10].tolist()
-    a_ = np.where(mask, sc, 0.0)
-    b_ = np.where(mask, rsc, 0.0)
-    eq = (a_ == b_) | (np.isnan(a_) & np.isnan(b_))
+    pad = np.arange(k)[None, :] >= cnt[:, None]
+    for x_ids, x_sc in ((ids, sc), (rids, rsc)):
+        if not (x_ids[pad] == -1).all() or not np.isnan(x_sc[pad]).all():
+            return "padding past a row's count is not (-1, NaN)"
+    if not np.array_equal(ids, rids):
+        return "ids differ at rows %s" % np.nonzero((ids != rids).any(1))[0][:10].tolist()
+    eq = (sc == rsc) | (np.isnan(sc) & np.isnan(rsc))
     if not eq.all():
         return "scores differ at rows %s" % np.nonzero(~eq.all(1))[0][:10].tolist()
+    return None
+
+
+def _oracle_rows(O, table, lists, rows, k, weighted=False):
+    """The refreshed lists of `rows` against the oracle's TopItems.getTopUsers
+    loop (TopItems.java:91-136) over that row's exact similarities
+    (DoubleCountMinSketch.cosine via CosineCM, oracle/cms_oracle.c)."""
+    ids, sc, cnt = lists
+    n = table.shape[0]
+    for row in rows:
+        exp = O.similarities_row(table, int(row), weighted)
+        eids, esc = O.top_users(np.arange(n, dtype=np.int64), exp, k)
+        if ids[row, :cnt[row]].tolist() != eids.tolist():
+            return "row %d: ids differ from the oracle" % row
+        if not np.array_equal(sc[row, :cnt[row]], esc, equal_nan=True):
+            return "row %d: scores differ from the oracle" % row
     return None
 
 
@@ -53,10 +73,15 @@ def _batch(rng, n, frac, size, vmax, n_keys):
     (1800, 3, 256, 1, 64, True, 53),      # weighted: not on the symmetric kernel (all pairs recomputed)
     (700, 5, 512, 2, 5, False, 54),       # fewer than one block pair per wave
 ])
-def test_refresh_equals_whole_job(n, d, w, vmax, k, weighted, seed):
+def test_refresh_equals_whole_job(n, d, w, vmax, k, weighted, seed, oracle):
     rng = np.random.Generator(np.random.PCG64(seed))
     items, users = zipf_stream(4000, n, 400_000, seed=seed)
     vals = rng.integers(1, vmax + 1, size=items.size).astype(np.float32)
+    # at the config-4 shape the refreshed lists are also checked against the
+    # oracle after every batch: touched and untouched sampled rows
+    check_oracle = w == 8192
+    stream = [(items.astype(np.int64), users.astype(np.int64), vals)]
+    a, b = oracle.hash_params(42, d)
     with SketchTable(n, depth=d, width=w, seed=42, weighted=weighted) as t:
         t.ingest(items, users, vals)
         t.finalize()
@@ -70,6 +95,7 @@ def test_refresh_equals_whole_job(n, d, w, vmax, k, weighted, seed):
                                              (0.002, 50)]):
             rows, keys, v = _batch(rng, n, frac, size, vmax, 4000)
             t.ingest(rows, keys, v)
+            stream.append((rows, keys, v))
             t.finalize()
             got = t.top_k_refresh(k)
             touched, redone, full = t.refresh_stats()
@@ -78,6 +104,15 @@ def test_refresh_equals_whole_job(n, d, w, vmax, k, weighted, seed):
             exp = t.top_k_all(k)
             err = _same_lists(got, exp)
             assert err is None, (step, frac, err, (touched, redone))
+            if check_oracle:
+                table = oracle.build_table(n, d, w, a, b, *[np.concatenate(c) for c in zip(*stream)])
+                tr = np.unique(rows)
+                untouched = np.setdiff1d(np.arange(n), tr)
+                sample = np.concatenate([rng.choice(tr, min(3, tr.size), replace=False),
+                                         rng.choice(untouched, 3, replace=False)])
+                err = _oracle_rows(oracle, table, got, sample, k, weighted)
+                assert err is None, (step, frac, err)
+                del table
         # no batch since: the kept lists are returned as they are
         again = t.top_k_refresh(k)
         assert t.refresh_stats()[0] == 0
@@ -101,8 +136,10 @@ def test_refresh_owner_ids_and_invalidation():
         got = t.top_k_refresh(k)
         assert t.refresh_stats()[2] == 1
         assert _same_lists(got, t.top_k_all(k)) is None
-        listed = got[0][np.arange(k)[None, :] < got[2][:, None]]  # entries past a row's count are not written
+        valid = np.arange(k)[None, :] < got[2][:, None]
+        listed = got[0][valid]
         assert listed.size > 0 and set(np.unique(listed).tolist()) <= set(ids_of.tolist())
+        assert (got[0][~valid] == -1).all() and np.isnan(got[1][~valid]).all()  # defined padding
         # another k: whole job again
         got = t.top_k_refresh(k + 5)
         assert t.refresh_stats()[2] == 2
@@ -145,3 +182,56 @@ def test_refresh_lists_feed_generic_item_similarity():
         a, b = next((a, b) for a in range(n) for b in range(a + 1, n) if (a, b) not in listed
                     and b not in ids[a, :cnt[a]] and a not in ids[b, :cnt[b]])
         assert np.isnan(g.itemSimilarity(a, b))
+
+
+def test_refresh_after_release_scratch(oracle):
+    """cms_release_scratch frees the kept lists: a COO ingest after it must not
+    mark into them, and the next refresh is a whole job equal to the whole
+    all-pairs answer (and to the oracle's TopItems lists)."""
+    n, d, w, k = 3000, 4, 256, 16
+    items, users = zipf_stream(3000, n, 200_000, seed=21)
+    rng = np.random.Generator(np.random.PCG64(21))
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        t.top_k_refresh(k)
+        t.release_scratch()
+        rows, keys, v = _batch(rng, n, 0.1, 20_000, 1, 3000)
+        t.ingest(rows, keys, v)
+        t.finalize()
+        got = t.top_k_refresh(k)
+        assert t.refresh_stats()[2] == 2  # whole job: the kept lists were released
+        assert _same_lists(got, t.top_k_all(k)) is None
+        a, b = oracle.hash_params(42, d)
+        table = oracle.build_table(n, d, w, a, b, np.concatenate([items, rows]), np.concatenate([users, keys]),
+                                   np.concatenate([np.ones(items.size, np.float32), v]))
+        assert _oracle_rows(oracle, table, got, [0, int(rows[0]), n // 3, n - 1], k) is None
+        # and the incremental path works again from the new kept lists
+        rows, keys, v = _batch(rng, n, 0.05, 5_000, 1, 3000)
+        t.ingest(rows, keys, v)
+        t.finalize()
+        got = t.top_k_refresh(k)
+        assert t.refresh_stats()[2] == 2
+        assert _same_lists(got, t.top_k_all(k)) is None
+
+
+def test_device_outputs_equal_host_outputs():
+    """cms_top_k_all_device / cms_top_k_refresh_device write the same lists,
+    padding included, into caller device buffers."""
+    import torch
+    n, d, w, k = 2500, 4, 256, 12
+    items, users = zipf_stream(3000, n, 150_000, seed=31)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        host = t.top_k_all(k)
+        dev = t.top_k_all_device(k)
+        assert all(isinstance(x, torch.Tensor) and x.is_cuda for x in dev)
+        assert _same_lists(tuple(x.cpu().numpy() for x in dev), host) is None
+        t.top_k_refresh(k)
+        rng = np.random.Generator(np.random.PCG64(31))
+        rows, keys, v = _batch(rng, n, 0.1, 10_000, 1, 3000)
+        t.ingest(rows, keys, v)
+        t.finalize()
+        dev = t.top_k_refresh_device(k)
+        assert _same_lists(tuple(x.cpu().numpy() for x in dev), t.top_k_all(k)) is None
