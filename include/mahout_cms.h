@@ -109,6 +109,14 @@ int cms_set_owner_ids(cms_handle* h, const int64_t* ids, int64_t n);
 /* The d hash parameters (a_i, b_i) of HashFunctionBuilder(seed)
  * (HashFunctionBuilder.java:40-61). */
 int cms_hash_params(cms_handle* h, int64_t* a, int64_t* b);
+/* Install a caller's HashFunctionBuilder parameters instead of the ones
+ * drawn from p->seed: (a_i, b_i) = (randomParamA[i], randomParamB[i]) as the
+ * builder drew them (HashFunctionBuilder.java:40-61) -- for a builder whose
+ * seed is unknown (new HashFunctionBuilder() seeds from the clock).  count
+ * must be the handle's depth (CMS_MAX_DEPTH = 32 for a per-owner handle: the
+ * rows any owner's shape may use).  Before the first ingest only
+ * (CMS_E_STATE otherwise; cms_reset allows it again). */
+int cms_set_hash_params(cms_handle* h, const int64_t* a, const int64_t* b, int32_t count);
 
 /* HashFunction.hash(key) for every row i < d, computed on the GPU
  * (HashFunction.java:31-34): out[k*d + i] = h_i(keys[k]). */

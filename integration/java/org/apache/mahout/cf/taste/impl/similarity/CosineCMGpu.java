@@ -47,7 +47,12 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private final long seed;
   private final boolean weighted;
   private final int device;
+  private final long[] hashA;  // a HashFunctionBuilder's drawn (a_i, b_i), or null: drawn from seed
+  private final long[] hashB;
   private long handle;  // cms_handle*
+
+  /** Hash rows a per-owner handle carries (CMS_MAX_DEPTH of include/mahout_cms.h). */
+  static final int MAX_DEPTH = 32;
 
   /**
    * @param hfBuilderSeed the seed a HashFunctionBuilder(seed) would be built with
@@ -66,6 +71,8 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     this.seed = hfBuilderSeed;
     this.weighted = weighting == Weighting.WEIGHTED;
     this.device = device;
+    this.hashA = null;
+    this.hashB = null;
     build();
   }
 
@@ -87,6 +94,8 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     this.seed = hfBuilderSeed;
     this.weighted = weighting == Weighting.WEIGHTED;
     this.device = device;
+    this.hashA = null;
+    this.hashB = null;
     build();
   }
 
@@ -107,6 +116,35 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     this.seed = hfBuilderSeed;
     this.weighted = weighting == Weighting.WEIGHTED;
     this.device = device;
+    this.hashA = null;
+    this.hashB = null;
+    build();
+  }
+
+  /**
+   * Per-owner shapes from the caller's config, hashing with parameters a
+   * HashFunctionBuilder has drawn (HashFunctionParams.draw(builder, MAX_DEPTH)):
+   * the backing of the same-package CosineCM replacement, whose constructors
+   * take the builder itself (CosineCM.java:26-39).
+   */
+  CosineCMGpu(DataModel dataModel, Weighting weighting, CountMinSketchConfig conf, long[] hashA, long[] hashB,
+              int device) throws TasteException {
+    super(dataModel);
+    if (!dataModel.hasPreferenceValues()) {  // CosineCM.java:38
+      throw new IllegalArgumentException("DataModel doesn't have preference values");
+    }
+    if (hashA.length != MAX_DEPTH || hashB.length != MAX_DEPTH) {
+      throw new IllegalArgumentException("one (a, b) pair per hash row: " + MAX_DEPTH);
+    }
+    this.depth = 0;
+    this.width = 0;
+    this.config = conf;
+    this.q = Double.NaN;
+    this.seed = 0L;
+    this.weighted = weighting == Weighting.WEIGHTED;
+    this.device = device;
+    this.hashA = hashA.clone();
+    this.hashB = hashB.clone();
     build();
   }
 
@@ -147,6 +185,9 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     long h = perOwner() ? nativeCreatePerOwner(seed, n, weighted, device, fracBits)
                         : nativeCreate(depth, width, seed, n, weighted, device, fracBits);
     try {
+      if (hashA != null) {
+        nativeSetHashParams(h, hashA, hashB);
+      }
       nativeSetOwnerIds(h, ids);
       nativeIngestCsr(h, offsets, keys, vals);
       if (config != null) {
@@ -269,6 +310,16 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     return nativePointQuery(handle, ownerID, key);
   }
 
+  /** {width, depth} of the owner's own sketch (per-owner shapes). */
+  int[] ownerShape(long ownerID) throws TasteException {
+    return nativeOwnerShape(handle, ownerID);
+  }
+
+  /** The owner's own sketch, [depth][width] row-major as DoubleCountMinSketch stores it. */
+  double[] readOwnerSketch(long ownerID) throws TasteException {
+    return nativeReadOwnerSketch(handle, ownerID);
+  }
+
   /**
    * GenericUserBasedRecommender.doEstimatePreference(user, neighborhood, item)
    * with the CosineCM point query, for many items in one call; NaN where fewer
@@ -329,6 +380,9 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private static native void nativeSetOwnerDeltaEpsilon(long h, double[] delta, double[] epsilon)
       throws TasteException;
   private static native void nativeSetOwnerIds(long h, long[] ids) throws TasteException;
+  private static native void nativeSetHashParams(long h, long[] a, long[] b) throws TasteException;
+  private static native int[] nativeOwnerShape(long h, long id) throws TasteException;
+  private static native double[] nativeReadOwnerSketch(long h, long id) throws TasteException;
   private static native void nativeIngestCsr(long h, long[] offsets, long[] keys, float[] vals) throws TasteException;
   private static native void nativeFinalize(long h) throws TasteException;
   private static native double nativeSimilarity(long h, long id1, long id2, boolean itemIds) throws TasteException;

@@ -262,6 +262,67 @@ JNIEXPORT jobjectArray JNICALL JFN(nativeTopKRefresh)(JNIEnv* env, jclass c, jlo
   return top_k_lists(env, h, k, cms_top_k_refresh);
 }
 
+/* HashFunctionBuilder's drawn parameters (HashFunctionParams.draw) installed
+   before the first ingest: the GPU hashes with the caller's own builder. */
+JNIEXPORT void JNICALL JFN(nativeSetHashParams)(JNIEnv* env, jclass c, jlong h, jlongArray a, jlongArray b) {
+  (void)c;
+  const jsize n = (*env)->GetArrayLength(env, a);
+  if ((*env)->GetArrayLength(env, b) != n) {
+    throw_named(env, "java/lang/IllegalArgumentException", "a and b differ in length");
+    return;
+  }
+  int64_t* pa = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int64_t* pb = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  if (!pa || !pb) {
+    free(pa);
+    free(pb);
+    throw_named(env, "java/lang/OutOfMemoryError", "hash parameters");
+    return;
+  }
+  (*env)->GetLongArrayRegion(env, a, 0, n, (jlong*)pa);
+  (*env)->GetLongArrayRegion(env, b, 0, n, (jlong*)pb);
+  int rc = cms_set_hash_params(H(h), pa, pb, (int32_t)n);
+  free(pa);
+  free(pb);
+  fail(env, rc, 0);
+}
+
+/* {width, depth} of an owner's own sketch (per-owner handle; cms_read_owner_sketch
+   with out = NULL): the shape new DoubleCountMinSketch(delta, epsilon, ...) gives it. */
+JNIEXPORT jintArray JNICALL JFN(nativeOwnerShape)(JNIEnv* env, jclass c, jlong h, jlong id) {
+  (void)c;
+  int32_t w = 0, d = 0;
+  if (fail(env, cms_read_owner_sketch(H(h), id, NULL, 0, &w, &d), 0)) return NULL;
+  jintArray out = (*env)->NewIntArray(env, 2);
+  if (!out) return NULL;
+  jint v[2] = {w, d};
+  (*env)->SetIntArrayRegion(env, out, 0, 2, v);
+  return out;
+}
+
+/* getExportedCMProfile(id)'s counters, [depth][width] row-major as
+   DoubleCountMinSketch.count holds them (DoubleCountMinSketch.java:62-64). */
+JNIEXPORT jdoubleArray JNICALL JFN(nativeReadOwnerSketch)(JNIEnv* env, jclass c, jlong h, jlong id) {
+  (void)c;
+  int32_t w = 0, d = 0;
+  if (fail(env, cms_read_owner_sketch(H(h), id, NULL, 0, &w, &d), 0)) return NULL;
+  const int64_t cells = (int64_t)w * d;
+  double* buf = (double*)malloc(sizeof(double) * (size_t)(cells > 0 ? cells : 1));
+  if (!buf) {
+    throw_named(env, "java/lang/OutOfMemoryError", "owner sketch");
+    return NULL;
+  }
+  int rc = cms_read_owner_sketch(H(h), id, buf, cells, &w, &d);
+  if (fail(env, rc, 0)) {
+    free(buf);
+    return NULL;
+  }
+  jdoubleArray out = (*env)->NewDoubleArray(env, (jsize)cells);
+  if (out) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)cells, buf);
+  free(buf);
+  return out;
+}
+
 JNIEXPORT void JNICALL JFN(nativeDestroy)(JNIEnv* env, jclass c, jlong h) {
   (void)env;
   (void)c;

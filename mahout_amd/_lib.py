@@ -42,7 +42,7 @@ EXPORTS = [
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
     "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities", "cms_write_similarities_threshold",
     "cms_comm_init_transport", "cms_read_counters_device", "cms_top_k_refresh", "cms_refresh_stats",
-    "cms_top_k_all_device", "cms_top_k_refresh_device",
+    "cms_top_k_all_device", "cms_top_k_refresh_device", "cms_set_hash_params",
 ]
 
 
@@ -128,6 +128,7 @@ _SIGS = {
     "cms_top_k_all": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_top_k_refresh": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_top_k_all_device": (_int, [_vp, _i32, _vp, _vp, _vp]),
+    "cms_set_hash_params": (_int, [_vp, _vp, _vp, _i32]),
     "cms_top_k_refresh_device": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_refresh_stats": (_int, [_vp, _vp, _vp, _vp]),
     "cms_read_counters": (_int, [_vp, _i64, _i64, _vp]),

@@ -411,6 +411,22 @@ int cms_hash_params(cms_handle* h, int64_t* a, int64_t* b) {
   return CMS_OK;
 }
 
+int cms_set_hash_params(cms_handle* h, const int64_t* a, const int64_t* b, int32_t count) {
+  if (!h || !a || !b) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  if (count != h->p.depth)
+    return set_error(CMS_E_PARAM, "expected %d (a, b) pairs, got %d", (int)h->p.depth, (int)count);
+  if (!h->empty || h->pairs_ingested != 0 || h->po_loaded)
+    return set_error(CMS_E_STATE, "hash parameters must be set before the first ingest (or after cms_reset)");
+  for (int i = 0; i < count; ++i) {
+    h->a[i] = a[i];
+    h->b[i] = b[i];
+    h->hp.ap[i] = reduce_key(a[i]);  // any int64, as BigInteger.valueOf(a).mod(p) takes it
+    h->hp.bp[i] = reduce_key(b[i]);
+  }
+  return CMS_OK;
+}
+
 int cms_hash_keys(cms_handle* h, const int64_t* keys, int64_t n, int32_t* out) {
   if (!h || (n > 0 && (!keys || !out))) return set_error(CMS_E_PARAM, "null argument");
   if (int rc0 = refuse_per_owner(h, "cms_hash_keys")) return rc0;

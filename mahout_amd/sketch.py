@@ -101,6 +101,7 @@ class SketchTable:
         self.depth = depth
         self.width = width
         self.seed = seed
+        self.hash_rows = 32 if per_owner else depth  # CMS_MAX_DEPTH rows for per-owner handles
         if owner_ids is not None:
             self.set_owner_ids(owner_ids)
 
@@ -128,10 +129,21 @@ class SketchTable:
         check(self._lib.cms_set_owner_ids(self._h, _ptr(ids), ids.size))
 
     def hash_params(self):
-        a = np.zeros(self.depth, np.int64)
-        b = np.zeros(self.depth, np.int64)
+        """(a_i, b_i) of every hash row: depth rows, or all CMS_MAX_DEPTH (32)
+        rows of a per-owner handle (any owner's shape may use them)."""
+        a = np.zeros(self.hash_rows, np.int64)
+        b = np.zeros(self.hash_rows, np.int64)
         check(self._lib.cms_hash_params(self._h, _ptr(a), _ptr(b)))
         return a, b
+
+    def set_hash_params(self, a, b):
+        """Install a HashFunctionBuilder's drawn (a_i, b_i) (cms_set_hash_params);
+        one pair per sketch row of the handle (32 for per-owner handles)."""
+        a = np.ascontiguousarray(a, np.int64)
+        b = np.ascontiguousarray(b, np.int64)
+        if a.shape != b.shape:
+            raise ValueError("a and b differ in length")
+        check(self._lib.cms_set_hash_params(self._h, _ptr(a), _ptr(b), int(a.size)))
 
     def hash_keys(self, keys):
         keys = np.ascontiguousarray(keys, np.int64)
