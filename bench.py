@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-config1", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (100K items) secondary ingest line")
     ap.add_argument("--no-cosine-1m", action="store_true", help="skip configs 4 and 5 on the headline table")
+    ap.add_argument("--no-headline", action="store_true",
+                    help="profiling aid: run the secondary lines only (no headline value is printed)")
     ap.add_argument("--stream-batches", type=int, default=8, help="config-5 incremental batches per rank")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="config 5: batches between periodic top-k refreshes (cms_top_k_refresh)")
@@ -912,6 +914,15 @@ def main():
     cfg1 = None
     if rank == 0 and world == 1 and not args.no_config1 and not args.no_extras:
         cfg1 = config1()
+
+    if args.no_headline:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "note": "--no-headline (profiling aid)",
+                              "config2": config2, "config1": cfg1}))
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     # ---- headline: config 3's shape ----
     n, d, w = args.n_items, args.depth, args.width

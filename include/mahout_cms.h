@@ -382,6 +382,8 @@ typedef struct cms_stats {
   int64_t merge_words;       /* u64 words the last multi-rank merge all-reduced (packed counters) */
   int64_t hot_rows;          /* owners whose counters are stored as u32 (the others narrow) */
   int64_t stored_bytes;      /* bytes of counters as stored: what one whole-table build writes */
+  int64_t u8_rows;           /* narrow owners stored as u8 (every counter < 2^8) */
+  int64_t nibble_rows;       /* narrow owners stored as 4-bit counters (every counter < 2^4) */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -78,6 +78,8 @@ class CmsStats(ctypes.Structure):
         ("merge_words", ctypes.c_int64),
         ("hot_rows", ctypes.c_int64),
         ("stored_bytes", ctypes.c_int64),
+        ("u8_rows", ctypes.c_int64),
+        ("nibble_rows", ctypes.c_int64),
     ]
 
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -338,6 +339,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
       (f64 && (e = hipMalloc(&h->d_t64, 4 * tbytes)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||
       (!per_owner && (e = hipMemset(h->d_hidx, 0xff, sizeof(int32_t) * h->n)) != hipSuccess) ||
+      (!per_owner && !f64 && (e = hipMalloc(&h->d_cbound, sizeof(uint32_t) * h->n)) != hipSuccess) ||
       (e = hipMalloc(&h->d_row_mass, sizeof(uint64_t) * h->n)) != hipSuccess ||
       (!per_owner && (e = hipMalloc(&h->d_norm, sizeof(uint64_t) * h->n * p->depth)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_norm_sqrt, sizeof(double) * h->n * p->depth)) != hipSuccess) ||
@@ -352,6 +354,8 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   }
   h->empty = true;
   h->norms_valid = false;
+  // u8 / nibble row forms need 64-B aligned slots and 16-B nibble rows
+  h->forms_ok = !per_owner && !f64 && h->dw % 32 == 0 && !getenv("CMS_NO_FORMS");
   *out = h;
   return CMS_OK;
 }
@@ -372,7 +376,7 @@ void cms_destroy(cms_handle* h) {
   if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   free_query_pool(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
+  void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -1383,24 +1387,24 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
     if (cnt) CMS_HIP(hipMemcpy(out, h->d_t64 + row_begin * h->dw, sizeof(double) * cnt, hipMemcpyDeviceToHost));
     return CMS_OK;
   }
-  // narrow rows straight from the u16 table, hot rows from their slots
-  std::vector<uint16_t> t16(cnt);
-  std::vector<int32_t> hidx(std::max<int64_t>(row_count, 1));
-  std::vector<uint32_t> hot((size_t)h->dw);
+  // every storage form (u32 slots, u16 / u8 / nibble rows) through the
+  // device read, in chunks of at most 256 MB of u32 counters
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(row_count, (int64_t(1) << 26) / std::max<int64_t>(h->dw, 1)));
+  DevBuf tmp;
+  std::vector<uint32_t> host;
   if (row_count > 0) {
-    CMS_HIP(hipMemcpy(t16.data(), h->d_t16 + row_begin * h->dw, sizeof(uint16_t) * cnt, hipMemcpyDeviceToHost));
-    CMS_HIP(hipMemcpy(hidx.data(), h->d_hidx + row_begin, sizeof(int32_t) * row_count, hipMemcpyDeviceToHost));
+    CMS_HIP(tmp.ensure(sizeof(uint32_t) * (size_t)(chunk * h->dw)));
+    host.resize((size_t)(chunk * h->dw));
   }
-  for (int64_t r = 0; r < row_count; ++r) {
-    double* o = out + r * h->dw;
-    if (hidx[r] >= 0) {
-      CMS_HIP(hipMemcpy(hot.data(), h->hot_tab.as<uint32_t>() + (int64_t)hidx[r] * h->dw, sizeof(uint32_t) * h->dw,
-                        hipMemcpyDeviceToHost));
-      for (int64_t j = 0; j < h->dw; ++j) o[j] = std::ldexp((double)hot[j], -h->p.frac_bits);
-    } else {
-      const uint16_t* s16 = t16.data() + r * h->dw;
-      for (int64_t j = 0; j < h->dw; ++j) o[j] = std::ldexp((double)s16[j], -h->p.frac_bits);
-    }
+  for (int64_t r0 = 0; r0 < row_count; r0 += chunk) {
+    const int64_t rc = std::min(chunk, row_count - r0);
+    int rc1 = read_counters_device(h, row_begin + r0, rc, tmp.as<uint32_t>());
+    if (rc1) return rc1;
+    CMS_HIP(hipMemcpyAsync(host.data(), tmp.ptr, sizeof(uint32_t) * (size_t)(rc * h->dw), hipMemcpyDeviceToHost,
+                           h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    double* o = out + r0 * h->dw;
+    for (int64_t j = 0; j < rc * h->dw; ++j) o[j] = std::ldexp((double)host[j], -h->p.frac_bits);
   }
   return CMS_OK;
 }
@@ -1450,11 +1454,12 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
-  int64_t hot_rows = 0;
+  int64_t forms[4] = {0, 0, 0, 0};  // hot, u16, u8, nibble rows
   if (!h->per_owner && !h->f64 && h->d_hidx) {
-    int rc = count_hot_rows(h, &hot_rows);
+    int rc = count_forms(h, forms);
     if (rc) return rc;
   }
+  const int64_t hot_rows = forms[0];
   out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                     : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
                                   : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
@@ -1466,8 +1471,10 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->hot_rows = hot_rows;
   out->stored_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                      : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
-                                   : (int64_t)sizeof(uint16_t) * (h->n - hot_rows) * h->dw +
-                                    (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
+                                   : 4 * forms[0] * h->dw + 2 * forms[1] * h->dw + forms[2] * h->dw +
+                                    forms[3] * (h->dw / 2);
+  out->u8_rows = forms[2];
+  out->nibble_rows = forms[3];
   return CMS_OK;
 }
 

@@ -41,6 +41,13 @@ struct HotInfo {
 constexpr int kKeyRegs = CMS_KEY_REGS;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // keys cached per thread: owners up to 1024 keys are read once
+typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
+
+// 8 byte counters (each < 16) of two words -> 8 nibbles, counter k in bits 4k
+__device__ __forceinline__ uint32_t nibbles4(uint32_t x) {
+  return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u);
+}
+__device__ __forceinline__ uint32_t nibbles8(uint32_t lo, uint32_t hi) { return nibbles4(lo) | (nibbles4(hi) << 16); }
 
 __global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
                              int2* extra_map, uint32_t* counters /* [0]=hot rows [1]=extra slices */,
@@ -129,7 +136,8 @@ constexpr bool kNoSlicePairs = true;
 #else
 constexpr bool kNoSlicePairs = false;
 #endif
-constexpr int kBuildStoreForm = 2;  // 16-B non-temporal: config-3 build 20.4 -> 19.4 ms, config 2 ~1% (scripts/store_ab.sh)
+constexpr int kBuildStoreForm = 2;
+constexpr size_t kFormLdsMax = 64 * 1024;  // byte-form owners: [d][w] bytes of LDS per workgroup  // 16-B non-temporal: config-3 build 20.4 -> 19.4 ms, config 2 ~1% (scripts/store_ab.sh)
 
 template <int SV>
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_rows(
@@ -137,8 +145,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
     TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate,
-    int slices_done) {
-  extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w]
+    int slices_done, const uint64_t* bound, int forms, int skip_untouched, int32_t* hidx_w, uint32_t* cbound) {
+  extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w] u32, or a byte-form owner's [d][w] u8
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
   __shared__ uint32_t s_max;  // largest counter of the row (limb count of the all-pairs operands)
@@ -163,6 +171,10 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     lo = lo_[row];
     atomic_mode = row_hot[row] >= 0;
     hi = atomic_mode ? lo + slice : hi_[row];
+    // accumulating into a live table with current norms: a row without keys
+    // keeps its counters, norms and form (a form row may only be touched
+    // after widen_rows made it u16)
+    if (skip_untouched && hi_[row] == lo) return;
   }
 #ifdef CMS_BUILD_NOKEYS  // bound analysis only: the write path alone
   hi = lo;
@@ -204,6 +216,65 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       }
     }
   }
+  // Byte forms: a fresh narrow owner whose mass (so every counter) stays
+  // below 2^8 is built whole in LDS as bytes -- all d sketch rows in one pass
+  // over its cached keys -- and leaves as u8, or as nibbles when its largest
+  // counter is below 2^4 (the row's form is chosen here, hidx_w / cbound).
+  const bool byte_form = forms && cached && !atomic_mode && !load_old && !dst && bound[row] < 256;
+  if (byte_form) {
+    const int nq = (int)(dw >> 4);  // uint4 words of the [d][w] byte image (dw % 32 == 0)
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kKeyRegs; ++k)
+      if (ik[k])
+        for (int d = 0; d < hp.depth; ++d) {
+          const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kp[k]);
+          atomicAdd(&lds[c >> 2], ik[k] << ((c & 3u) << 3));  // < 2^8 per byte: no carry
+        }
+    __syncthreads();
+    // sums of squares per sketch row (v_dot4_u32_u8: <= mass * 255 < 2^16),
+    // largest counter, and the OR of every byte (all < 16: nibbles)
+    u8x4 pm = {0, 0, 0, 0};
+    const int qr = w >> 4;  // uint4 per sketch row
+    for (int d = 0; d < hp.depth; ++d) {
+      uint32_t sq = 0;
+      for (int j = tid; j < qr; j += kBuildThreads) {
+        const uint4 v = l4[d * qr + j];
+        sq = __builtin_amdgcn_udot4(v.x, v.x, sq, false);
+        sq = __builtin_amdgcn_udot4(v.y, v.y, sq, false);
+        sq = __builtin_amdgcn_udot4(v.z, v.z, sq, false);
+        sq = __builtin_amdgcn_udot4(v.w, v.w, sq, false);
+        const u8x4 a = __builtin_bit_cast(u8x4, v.x), b = __builtin_bit_cast(u8x4, v.y);
+        const u8x4 c = __builtin_bit_cast(u8x4, v.z), e = __builtin_bit_cast(u8x4, v.w);
+        pm = __builtin_elementwise_max(pm, __builtin_elementwise_max(__builtin_elementwise_max(a, b),
+                                                                     __builtin_elementwise_max(c, e)));
+      }
+      sq = wave_sum_u32(sq);
+      if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+    }
+    vmax = max(max((uint32_t)pm.x, (uint32_t)pm.y), max((uint32_t)pm.z, (uint32_t)pm.w));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
+    __syncthreads();
+    const bool nib = s_max < 16u;
+    uint4* d4 = reinterpret_cast<uint4*>(dst16);  // the row's u16 slot (64-B aligned)
+    if (nib) {  // 32 counters per 16-B store
+      for (int j = tid; j < (nq >> 1); j += kBuildThreads) {
+        const uint4 a = l4[2 * j], b = l4[2 * j + 1];
+        store_row(d4 + j, make_uint4(nibbles8(a.x, a.y), nibbles8(a.z, a.w), nibbles8(b.x, b.y), nibbles8(b.z, b.w)),
+                  SV);
+      }
+    } else {  // 16 counters per 16-B store
+      for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
+    }
+    if (tid == 0) {
+      hidx_w[row] = nib ? kFormU4 : kFormU8;
+      cbound[row] = s_max;
+    }
+  } else {
   // LDS slot for sketch row 0 (the old counters when accumulating)
   for (int j = tid; j < w; j += kBuildThreads) lds[j] = load_old ? (dst ? dst[j] : (uint32_t)dst16[j]) : 0u;
   __syncthreads();
@@ -445,6 +516,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     lds_barrier();  // LDS order only: the write-out stores stay in flight
     d += two ? 2 : 1;
   }
+  }  // sketch-row loop (not byte_form)
 
   if (badv) atomicOr(flags, kFlagBadValue);
   mass = wave_sum_u64_sat(mass);
@@ -609,6 +681,11 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       if ((double)slots * (double)h->dw * 4.0 <= 2.0e9) max_new = slots;
     }
     if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0, max_new))) return rc0;
+    // accumulating: every touched u8 / nibble row becomes u16 first (the build
+    // adds into u16 or u32 rows); untouched rows are skipped by the build when
+    // their norms are current, otherwise every form row is widened
+    if (accumulate && (rc0 = widen_rows(h, h->norms_valid ? bound.as<uint64_t>() : nullptr, h->d_row_mass, true)))
+      return rc0;
   }
   {
     TimedScope ts(h, "build_plan");
@@ -617,7 +694,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                        counters, h->d_norm, h->d_rowmax, h->p.depth);
     CMS_HIP(hipGetLastError());
   }
-  const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
+  // fresh builds may store byte forms: the whole [d][w] byte image in LDS
+  const int forms = h->forms_ok && !accumulate && (size_t)h->dw <= kFormLdsMax ? 1 : 0;
+  const int skip_untouched = accumulate && h->norms_valid ? 1 : 0;
+  const size_t lds = std::max(sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3), forms ? (size_t)h->dw : (size_t)0);
   {
     TimedScope ts(h, "build_rows");
     static const int sv = [] {
@@ -644,7 +724,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     auto kern = sv == 2 ? k_build_rows<2> : sv == 1 ? k_build_rows<1> : k_build_rows<0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                        d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
-                       h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done);
+                       h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
+                       skip_untouched, h->d_hidx, h->d_cbound);
     CMS_HIP(hipGetLastError());
   }
   {

@@ -175,13 +175,24 @@ int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_row
 // counter c of row r += inc; returns the old value.  Narrow rows add into
 // their half of the aligned 32-bit word: promote_rows guarantees the row's
 // bound stays < 2^16, so no carry reaches the neighbouring half.
+// u8 / nibble rows add into their byte / nibble of the aligned word the same
+// way: widen_rows ran first, so the row's counter bound stays within its form.
 __device__ __forceinline__ uint32_t table_add(const TableView& tv, int64_t r, int64_t c, uint32_t inc) {
   const int32_t s = tv.hidx[r];
   if (s >= 0) return atomicAdd(tv.hot + (int64_t)s * tv.dw + c, inc);
-  const int64_t g = r * tv.dw + c;
-  const uint32_t sh = (uint32_t)(g & 1) << 4;
-  const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(tv.t16) + (g >> 1), inc << sh);
-  return (old >> sh) & 0xffffu;
+  if (s == kFormU16) {
+    const int64_t g = r * tv.dw + c;
+    const uint32_t sh = (uint32_t)(g & 1) << 4;
+    const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(tv.t16) + (g >> 1), inc << sh);
+    return (old >> sh) & 0xffffu;
+  }
+  uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * tv.dw);  // slot start: 64-B aligned with forms
+  if (s == kFormU8) {
+    const uint32_t sh = (uint32_t)(c & 3) << 3;
+    return (atomicAdd(w32 + (c >> 2), inc << sh) >> sh) & 0xffu;
+  }
+  const uint32_t sh = (uint32_t)(c & 7) << 2;
+  return (atomicAdd(w32 + (c >> 3), inc << sh) >> sh) & 0xfu;
 }
 
 // batch mass per row (counter units) for the promotion check of unsorted batches
@@ -427,6 +438,8 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
                              force.as<uint8_t>())))
           return rc;
         if ((rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true))) return rc;
+        // u8 / nibble rows the batch could push past their form become u16
+        if ((rc = widen_rows(h, bound.as<uint64_t>(), h->d_row_mass, false))) return rc;
       }
       TimedScope ts(h, "ingest_sorted");
       h->stale_possible = true;
@@ -461,6 +474,7 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
       CMS_HIP(hipGetLastError());
       int rc = promote_rows(h, bound.as<uint64_t>(), nullptr, true);
       if (rc) return rc;
+      if ((rc = widen_rows(h, bound.as<uint64_t>(), h->d_row_mass, false))) return rc;
     }
     const int track = h->norms_valid ? 1 : 0;
     h->stale_possible = true;

@@ -67,23 +67,49 @@ struct PendingEvent {
 // workgroups) get a u32 row in the slot table -- at config 2 that halves the
 // bytes the row build writes.  Writers promote a row to a slot before its
 // bound can reach 2^16 (promote_rows), so a u16 counter never overflows.
+//
+// Narrow FORMS: every non-hot row owns a u16-sized slot ([dw] u16 at
+// t16 + row * dw), but a fresh build stores a row whose counters are all
+// below 2^8 as u8 in the first dw bytes of its slot, and one whose counters
+// are all below 2^4 as packed nibbles (counter j in bits 4*(j&1) of byte j/2)
+// in the first dw/2 bytes -- at config 3 most of the 1M owners, so the build
+// writes a fraction of the u16 bytes.  hidx[row] names the form (< 0) or the
+// hot slot (>= 0).  cbound[row] (u32) bounds a form row's counters; a writer
+// widens a form row to u16 in place (widen_rows) before its bound could pass
+// the form's capacity.  Forms exist only when dw % 32 == 0 (every slot and
+// every nibble row then starts 64-byte aligned).
 constexpr uint64_t kNarrowLimit = 1ULL << 16;
+constexpr int32_t kFormU16 = -1, kFormU8 = -2, kFormU4 = -3;
+constexpr uint32_t form_cap(int32_t form) { return form == kFormU4 ? 15u : form == kFormU8 ? 255u : 65535u; }
 
 struct TableView {
-  uint16_t* t16;        // [n][dw] narrow rows
+  uint16_t* t16;        // [n][dw] narrow slots
   uint32_t* hot;        // [hot_cap][dw] u32 rows
-  const int32_t* hidx;  // [n] slot of a hot row, -1 for a narrow one
+  const int32_t* hidx;  // [n] slot of a hot row, or the narrow form (kForm*)
   int64_t dw;
   __device__ __forceinline__ uint32_t get(int64_t row, int64_t j) const {
     const int32_t s = hidx[row];
-    return s >= 0 ? hot[(int64_t)s * dw + j] : (uint32_t)t16[row * dw + j];
+    if (s >= 0) return hot[(int64_t)s * dw + j];
+    if (s == kFormU16) return (uint32_t)t16[row * dw + j];
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
+    if (s == kFormU8) return p[j];
+    return (uint32_t)(p[j >> 1] >> ((j & 1) << 2)) & 15u;
   }
   // counters j..j+3 of a row (j % 4 == 0 and dw % 4 == 0: aligned vector loads)
   __device__ __forceinline__ uint4 get4(int64_t row, int64_t j) const {
     const int32_t s = hidx[row];
     if (s >= 0) return *reinterpret_cast<const uint4*>(hot + (int64_t)s * dw + j);
-    const ushort4 v = *reinterpret_cast<const ushort4*>(t16 + row * dw + j);
-    return make_uint4(v.x, v.y, v.z, v.w);
+    if (s == kFormU16) {
+      const ushort4 v = *reinterpret_cast<const ushort4*>(t16 + row * dw + j);
+      return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
+    if (s == kFormU8) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(p + j);
+      return make_uint4(v & 255u, (v >> 8) & 255u, (v >> 16) & 255u, v >> 24);
+    }
+    const uint32_t v = *reinterpret_cast<const uint16_t*>(p + (j >> 1));
+    return make_uint4(v & 15u, (v >> 4) & 15u, (v >> 8) & 15u, v >> 12);
   }
 };
 
@@ -128,7 +154,9 @@ struct cms_handle {
   uint16_t* d_t16 = nullptr;        // [n][d][w] narrow counters
   bool f64 = false;                 // CMS_COUNTER_F64: fp64 counters in d_t64 (cms_f64.hip), no u16/u32 table
   double* d_t64 = nullptr;          // [n][d][w] fp64 counters
-  int32_t* d_hidx = nullptr;        // [n] hot slot or -1
+  int32_t* d_hidx = nullptr;        // [n] hot slot, or the narrow form (kFormU16 / kFormU8 / kFormU4)
+  uint32_t* d_cbound = nullptr;     // [n] bound of a form row's counters (maintained for form rows only)
+  bool forms_ok = false;            // dw % 32 == 0: fresh builds may store u8 / nibble forms
   cms::DevBuf hot_tab;              // [hot_cap][d][w] u32 counters of the hot rows
   cms::DevBuf ws_bound, ws_force, ws_plist;  // promotion scratch: u64 [n], u8 [n], i32 [n] + count
   int64_t hot_cap = 0, hot_used = 0;
@@ -279,6 +307,15 @@ int local_norms(cms_handle* h);
 int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new = -1);
 // rows holding a u32 slot (synchronises the stream)
 int count_hot_rows(cms_handle* h, int64_t* out);
+// rows per storage form: [0] hot, [1] u16, [2] u8, [3] nibble (synchronises)
+int count_forms(cms_handle* h, int64_t out[4]);
+// Form rows that a coming write could push past their capacity become u16 in
+// place: with d_bound (a u64 upper bound of each row's mass after the write)
+// and old_mass, a touched form row (bound > old mass) is widened when
+// cbound + (bound - old_mass) exceeds its form's capacity, and its cbound grows
+// by the batch's mass; all_touched widens every touched form row; d_bound null
+// widens every form row.
+int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched);
 // per-row counter bounds after a CSR batch (mass in counter units + old_mass)
 // and the rows split over more than `slice` keys (cms_build.hip)
 int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,

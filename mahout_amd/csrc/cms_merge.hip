@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
     const int32_t slot = tv.hidx[o];
     const uint32_t* s32 = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
     const uint16_t* s16 = tv.t16 + o * dw;
-    if (use_img && !s32) {
+    if (use_img && slot == kFormU16) {
       const uint4* g4 = reinterpret_cast<const uint4*>(s16);
       uint4* l4 = reinterpret_cast<uint4*>(img);
       for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) l4[j] = g4[j];
@@ -83,7 +83,8 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
       uint64_t wv = 0;
       for (int f = 0; f < F; ++f) {
         const int64_t idx = (int64_t)f * nw + i;
-        if (idx < dw) wv |= (uint64_t)(s32 ? s32[idx] : (uint32_t)s16[idx]) << (f * b);
+        if (idx < dw)  // u8 / nibble rows through the view
+          wv |= (uint64_t)(s32 ? s32[idx] : slot == kFormU16 ? (uint32_t)s16[idx] : tv.get(o, idx)) << (f * b);
       }
       words[w0 + i] = wv;
     }
@@ -96,7 +97,8 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
 // counters (one word read per F counters, no per-counter division), which
 // then leaves as 16-byte row-major stores while the norms are summed.
 __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int64_t n, HashParams hp, PackLayout L,
-                                                      TableView tv, uint64_t* norm, uint32_t* rowmax, int use_img) {
+                                                      TableView tv, uint64_t* norm, uint32_t* rowmax, int use_img,
+                                                      int32_t* hidx_w) {
   extern __shared__ __align__(16) uint16_t img[];  // [dw] (use_img)
   __shared__ uint64_t red[4];
   __shared__ uint32_t smax[4];
@@ -114,7 +116,11 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
         else dst16[i] = 0;
       }
       if (threadIdx.x < hp.depth) norm[o * hp.depth + threadIdx.x] = 0;
-      if (threadIdx.x == 0) rowmax[o] = 0;
+      if (threadIdx.x == 0) {
+        rowmax[o] = 0;
+        if (slot < 0) hidx_w[o] = kFormU16;
+      }
+      __syncthreads();
       continue;
     }
     const uint32_t nw = (uint32_t)(L.woff[o + 1] - L.woff[o]);
@@ -186,7 +192,10 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
     for (int s = 32; s > 0; s >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, s, 64));
     if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = vmax;
     __syncthreads();
-    if (threadIdx.x == 0) rowmax[o] = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+    if (threadIdx.x == 0) {
+      rowmax[o] = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+      if (slot < 0) hidx_w[o] = kFormU16;  // a u8 / nibble row now holds u16 merged counters
+    }
     __syncthreads();
   }
 }
@@ -261,7 +270,7 @@ int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
   {
     TimedScope ts(h, "merge_unpack");
     hipLaunchKernelGGL(k_merge_unpack, dim3(go), dim3(256), use_img ? img : 0, h->stream, packed.as<uint64_t>(), n,
-                       h->hp, L, h->tview(), h->d_norm, h->d_rowmax, use_img);
+                       h->hp, L, h->tview(), h->d_norm, h->d_rowmax, use_img, h->d_hidx);
     CMS_HIP(hipGetLastError());
   }
   h->norms_valid = true;  // the unpack wrote the merged norms

@@ -1,4 +1,5 @@
-// cms_table.hip -- layout of the sketch table: u16 narrow rows + u32 hot slots.
+// cms_table.hip -- layout of the sketch table: u16 narrow slots (holding u16,
+// u8 or nibble rows) + u32 hot slots.
 //
 // DoubleCountMinSketch keeps fp64 counters (T/impl/common/DoubleCountMinSketch.java:21);
 // with integer increments every counter is an integer no larger than its
@@ -44,8 +45,8 @@ __global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64
     const int64_t r = list[i];
     const int64_t slot = base + i;
     uint32_t* dst = tv.hot + slot * tv.dw;
-    const uint16_t* src = tv.t16 + r * tv.dw;
-    for (int64_t j = threadIdx.x; j < tv.dw; j += 256) dst[j] = copy_old ? (uint32_t)src[j] : 0u;
+    for (int64_t j = threadIdx.x; j < tv.dw; j += 256) dst[j] = copy_old ? tv.get(r, j) : 0u;  // any narrow form
+    __syncthreads();  // every lane has read the row through its old form before the form changes
     if (threadIdx.x == 0) hidx[r] = (int32_t)slot;
   }
 }
@@ -107,6 +108,111 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
                      (int64_t)c, (const uint32_t*)nullptr, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
   CMS_HIP(hipGetLastError());
   h->hot_used = need;
+  return CMS_OK;
+}
+
+// ---- narrow forms (u8 / nibble rows inside their u16 slots) ----
+
+// Rows to widen to u16 before a write (see widen_rows in cms_internal.h).
+__global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int32_t* hidx, uint32_t* cbound,
+                             int64_t n, int all_touched, int32_t* list, uint32_t* cnt) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t f = hidx[r];
+    if (f >= 0 || f == kFormU16) continue;
+    bool need = true;
+    if (bound) {
+      const uint64_t b = bound[r], m = old_mass ? old_mass[r] : 0ULL;
+      if (b <= m) continue;  // no increment lands on this row
+      const uint64_t nb = (uint64_t)cbound[r] + (b - m);
+      need = all_touched || nb > (uint64_t)form_cap(f);
+      if (!need) cbound[r] = (uint32_t)nb;  // <= the form's capacity
+    }
+    if (need) list[atomicAdd(cnt, 1u)] = (int32_t)r;
+  }
+}
+
+// One workgroup per listed row: its u8 / nibble counters rewritten as u16 in
+// the same slot.  The u16 image of counters [c0, c1) covers bytes
+// [2 c0, 2 c1), which holds only old bytes of counters >= c0; so chunks of
+// 4096 counters are processed from the top down, each read completely (16
+// counters per lane) before any lane writes it.
+__global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const uint32_t* dcount, TableView tv,
+                                                    int32_t* hidx) {
+  const int64_t count = *dcount;
+  const int64_t dw = tv.dw;
+  constexpr int64_t kChunk = 256 * 16;
+  for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const int64_t r = list[i];
+    const int32_t f = hidx[r];
+    uint8_t* p8 = reinterpret_cast<uint8_t*>(tv.t16 + r * dw);
+    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + r * dw);
+    for (int64_t c0 = ((dw - 1) / kChunk) * kChunk; c0 >= 0; c0 -= kChunk) {
+      const int64_t j = c0 + (int64_t)threadIdx.x * 16;  // this lane's 16 counters
+      uint32_t v[16];
+      if (j < dw) {
+        if (f == kFormU8) {
+          const uint4 x = *reinterpret_cast<const uint4*>(p8 + j);
+          const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 2] >> ((q & 3) * 8)) & 255u;
+        } else {
+          const uint2 x = *reinterpret_cast<const uint2*>(p8 + (j >> 1));
+          const uint32_t wv[2] = {x.x, x.y};
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 3] >> ((q & 7) * 4)) & 15u;
+        }
+      }
+      __syncthreads();  // the whole chunk is read before any lane overwrites it
+      if (j < dw) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+          d4[(j >> 3) + h2] = make_uint4(v[8 * h2] | (v[8 * h2 + 1] << 16), v[8 * h2 + 2] | (v[8 * h2 + 3] << 16),
+                                         v[8 * h2 + 4] | (v[8 * h2 + 5] << 16), v[8 * h2 + 6] | (v[8 * h2 + 7] << 16));
+      }
+      __syncthreads();  // the next (lower) chunk's old bytes are read after these stores
+    }
+    if (threadIdx.x == 0) hidx[r] = kFormU16;
+  }
+}
+
+int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched) {
+  if (!h->forms_ok) return CMS_OK;
+  const int64_t n = h->n;
+  CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
+  int32_t* list = h->ws_plist.as<int32_t>();
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(list + n);
+  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, h->d_hidx, h->d_cbound, n,
+                     all_touched ? 1 : 0, list, cnt);
+  // one workgroup per row, looping: the count stays on the device
+  hipLaunchKernelGGL(k_widen_rows, dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(256), 0, h->stream, list, cnt,
+                     h->tview(), h->d_hidx);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+__global__ void k_count_forms(const int32_t* hidx, int64_t n, unsigned long long* out) {
+  uint32_t c[4] = {0, 0, 0, 0};
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t f = hidx[r];
+    c[f >= 0 ? 0 : f == kFormU16 ? 1 : f == kFormU8 ? 2 : 3] += 1;
+  }
+  for (int q = 0; q < 4; ++q)
+    if (c[q]) atomicAdd(out + q, (unsigned long long)c[q]);
+}
+
+int count_forms(cms_handle* h, int64_t out[4]) {
+  DevBuf tmp;
+  CMS_HIP(tmp.ensure(4 * sizeof(unsigned long long)));
+  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 4 * sizeof(unsigned long long), h->stream));
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 4096));
+  hipLaunchKernelGGL(k_count_forms, dim3(g), dim3(256), 0, h->stream, h->d_hidx, h->n, tmp.as<unsigned long long>());
+  CMS_HIP(hipGetLastError());
+  unsigned long long c[4];
+  CMS_HIP(hipMemcpyAsync(c, tmp.ptr, sizeof(c), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  for (int q = 0; q < 4; ++q) out[q] = (int64_t)c[q];
   return CMS_OK;
 }
 

@@ -1,0 +1,133 @@
+"""GPU: narrow storage forms of the sketch table (u8 and 4-bit rows inside
+their u16 slots; cms_internal.h TableView, cms_build.hip byte-form path,
+cms_table.hip widen_rows).
+
+The form a row is stored in is an implementation detail: every counter must
+read back as DoubleCountMinSketch's value (`T/impl/common/DoubleCountMinSketch.java:72-80`)
+whatever path wrote it, and every similarity / top-k must be bit-identical to
+the oracle and to a handle that never uses forms (CMS_NO_FORMS=1).  The cases:
+a fresh build with owners in every class (nibble, u8, u16, u32 hot), then
+incremental batches that push nibble rows past 15 and u8 rows past 255
+(widening in place), and a large batch into the live table (the accumulate
+build, which widens every touched form row first).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from mahout_amd import SketchTable
+from mahout_amd.synth import zipf_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b):
+    return bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+def _stream(n, n_keys, pairs, seed):
+    items, users = zipf_stream(n_keys, n, pairs, seed=seed)
+    return items.astype(np.int64), users.astype(np.int64)
+
+
+def _handle(n, d, w, forms):
+    old = os.environ.pop("CMS_NO_FORMS", None)
+    if not forms:
+        os.environ["CMS_NO_FORMS"] = "1"
+    try:
+        return SketchTable(n, depth=d, width=w, seed=42)
+    finally:
+        os.environ.pop("CMS_NO_FORMS", None)
+        if old is not None:
+            os.environ["CMS_NO_FORMS"] = old
+
+
+@pytest.mark.parametrize("n,d,w", [(3000, 5, 1024), (1500, 4, 256)])
+def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
+    rng = np.random.Generator(np.random.PCG64(n))
+    # Zipf: a few hot owners (u32), a band of u16 owners, many u8 / nibble owners
+    items, users = _stream(n, 20000, 600_000, seed=n)
+    a, b = oracle.hash_params(42, d)
+    stream = [(items, users, np.ones(items.size, np.float32))]
+    with _handle(n, d, w, True) as t, _handle(n, d, w, False) as plain:
+        for x in (t, plain):
+            x.ingest(items, users)
+            x.finalize()
+        st = t.stats()
+        assert st["nibble_rows"] > 0 and st["u8_rows"] > 0 and st["hot_rows"] > 0, st
+        assert st["nibble_rows"] + st["u8_rows"] + st["hot_rows"] < n  # and some u16 rows
+        assert plain.stats()["nibble_rows"] == 0 and plain.stats()["u8_rows"] == 0
+        assert st["stored_bytes"] < plain.stats()["stored_bytes"]
+        exp = oracle.build_table(n, d, w, a, b, *[np.concatenate(c) for c in zip(*stream)])
+        assert np.array_equal(t.read_counters(), exp)
+        # batches: (1) small values onto nibble rows (some stay nibble, some pass 15),
+        # (2) weights pushing u8 rows past 255, (3) the owner-grouped atomic path,
+        # (4) a large batch -> accumulate build
+        nib_rows = np.flatnonzero(np.abs(exp).max(axis=(1, 2)) < 16)
+        u8_rows = np.flatnonzero((exp.max(axis=(1, 2)) >= 16) & (exp.max(axis=(1, 2)) < 256))
+        batches = [
+            (rng.choice(nib_rows, 3000), rng.integers(0, 20000, 3000), rng.integers(1, 3, 3000)),
+            # half of the u8 rows get weights that push them past 255 (the other half stays u8)
+            (rng.choice(u8_rows[: max(1, u8_rows.size // 2)], 2000), rng.integers(0, 50, 2000),
+             rng.integers(1, 200, 2000)),
+            # >= 32768 pairs into the live table: grouped by owner, k_ingest_sorted
+            (rng.choice(nib_rows, 40000), rng.integers(0, 20000, 40000), np.ones(40000, np.int64)),
+        ]
+        bi, bu = _stream(n, 20000, 300_000, seed=n + 1)
+        batches.append((bi, bu, np.ones(bi.size, np.int64)))
+        seen = []
+        for step, (r, k, v) in enumerate(batches):
+            r = r.astype(np.int64)
+            k = k.astype(np.int64)
+            v = v.astype(np.float32)
+            for x in (t, plain):
+                x.ingest(r, k, v)
+                x.finalize()
+            stream.append((r, k, v))
+            exp = oracle.build_table(n, d, w, a, b, *[np.concatenate(c) for c in zip(*stream)])
+            got = t.read_counters()
+            assert np.array_equal(got, exp), step
+            assert np.array_equal(plain.read_counters(), exp), step
+            for q in (0, int(r[0]), n - 1):
+                s1 = t.similarities(q, np.arange(n))
+                assert _same(s1, plain.similarities(q, np.arange(n))), (step, q)
+                ref = oracle.similarities_row(exp, q)
+                ref[q] = oracle.cosine_cm(exp[q], exp[q])
+                assert _same(s1, ref), (step, q)
+            seen.append(t.stats())
+        # the atomic batches widen only the rows they could push past their form
+        assert 0 < seen[0]["nibble_rows"] < st["nibble_rows"]
+        assert u8_rows.size < 2 or 0 < seen[1]["u8_rows"] < seen[0]["u8_rows"]
+        assert seen[1]["hot_rows"] >= st["hot_rows"]
+        assert seen[2]["nibble_rows"] <= seen[1]["nibble_rows"]
+        # the accumulate build widens every touched form row (u16 or hot)
+        assert seen[3]["nibble_rows"] <= seen[2]["nibble_rows"]
+        # the all-pairs job over form rows equals the form-free handle's
+        k = 20
+        got = t.top_k_all(k)
+        want = plain.top_k_all(k)
+        assert all(np.array_equal(x, y, equal_nan=True) for x, y in zip(got, want))
+
+
+def test_forms_point_queries_and_device_read(oracle):
+    """Point queries (DoubleCountMinSketch.get, :94-103) and the device
+    counter read on nibble and u8 rows."""
+    import torch
+    n, d, w = 2000, 4, 512
+    items, users = _stream(n, 5000, 300_000, seed=3)  # > 262143 pairs: the row build (smaller batches: atomics)
+    a, b = oracle.hash_params(42, d)
+    exp = oracle.build_table(n, d, w, a, b, items, users)
+    with _handle(n, d, w, True) as t:
+        t.ingest(items, users)
+        t.finalize()
+        assert t.stats()["nibble_rows"] > 0
+        dev = t.read_counters_device(0, n).cpu().numpy()
+        assert np.array_equal(dev.astype(np.float64), exp)
+        for r in (0, 5, 400, n - 1):
+            for key in (0, 1, 17, 4999, -3):
+                assert t.point_query(r, key) == oracle.sketch_get(exp[r], a, b, key)
+        t.ingest_csr(np.zeros(n + 1, np.int64), np.zeros(0, np.int64))  # an empty CSR batch changes nothing
+        t.finalize()
+        assert np.array_equal(t.read_counters(), exp)
+        torch.cuda.synchronize()
