@@ -316,6 +316,11 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     delete h;
     return hip_fail(e, "hipSetDevice");
   }
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+      h->num_cus = cus;
+  }
   h->n = p->num_owners;
   h->dw = (int64_t)p->depth * p->width;
   java_hash_params(p->seed, h->p.depth, h->a, h->b);

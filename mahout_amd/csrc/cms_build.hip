@@ -261,6 +261,9 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     __syncthreads();
     const bool nib = s_max < 16u;
     uint4* d4 = reinterpret_cast<uint4*>(dst16);  // the row's u16 slot (64-B aligned)
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+    if (false)
+#endif
     if (nib) {  // 32 counters per 16-B store
       for (int j = tid; j < (nq >> 1); j += kBuildThreads) {
         const uint4 a = l4[2 * j], b = l4[2 * j + 1];

@@ -137,6 +137,7 @@ struct QueryCtx {
 struct cms_handle {
   cms_params p{};
   int device = 0;
+  int num_cus = 256;  // compute units of the device (persistent grids)
   hipStream_t stream = nullptr;
   // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
   // the point queries after cms_finalize hold it shared and run concurrently,
