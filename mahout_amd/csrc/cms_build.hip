@@ -41,13 +41,13 @@ struct HotInfo {
 constexpr int kKeyRegs = CMS_KEY_REGS;
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));  // keys cached per thread: owners up to 1024 keys are read once
-typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
 
-// 8 byte counters (each < 16) of two words -> 8 nibbles, counter k in bits 4k
-__device__ __forceinline__ uint32_t nibbles4(uint32_t x) {
-  return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u);
+// 8 byte counters (each < 16) of two words -> 8 nibbles, counter k in bits 4k:
+// x | x >> 4 puts counters 0|1 in byte 0 and 2|3 in byte 2; one v_perm_b32
+// gathers bytes 0 and 2 of both words.
+__device__ __forceinline__ uint32_t nibbles8(uint32_t lo, uint32_t hi) {
+  return __builtin_amdgcn_perm(hi | (hi >> 4), lo | (lo >> 4), 0x06040200u);
 }
-__device__ __forceinline__ uint32_t nibbles8(uint32_t lo, uint32_t hi) { return nibbles4(lo) | (nibbles4(hi) << 16); }
 
 __global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
                              int2* extra_map, uint32_t* counters /* [0]=hot rows [1]=extra slices */,
@@ -115,6 +115,13 @@ __global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* lo_, co
       force[r] = (hi_[r] - lo_[r]) > slice ? 1 : 0;
     }
   }
+}
+
+// An owner of a fresh build whose every counter is provably below 2^8 (its
+// mass bound) and whose keys fit the register cache: built whole in LDS by
+// k_build_nibbles / k_build_bytes (not by k_build_rows).
+__device__ __forceinline__ bool byte_class(int32_t slot, bool cached, uint64_t bound) {
+  return slot < 0 && cached && bound < 256;
 }
 
 // grid = emax + nrows: blocks [0, emax) build extra slices of hot owners (heavy
@@ -193,6 +200,10 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
 
   // keys of small owners: read and reduced once for all d sketch rows
   const bool cached = (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs;
+  // Byte forms: a fresh narrow owner whose mass (so every counter) stays
+  // below 2^8 is built by k_build_nibbles (4-bit rows) or, when a counter
+  // reaches 16, by k_build_bytes (u8 rows) -- both launched after this kernel.
+  if (forms && !atomic_mode && !load_old && byte_class(slot, cached, bound[row])) return;
   uint64_t kp[kKeyRegs];
   uint32_t ik[kKeyRegs];
   uint64_t mass = 0;
@@ -216,68 +227,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       }
     }
   }
-  // Byte forms: a fresh narrow owner whose mass (so every counter) stays
-  // below 2^8 is built whole in LDS as bytes -- all d sketch rows in one pass
-  // over its cached keys -- and leaves as u8, or as nibbles when its largest
-  // counter is below 2^4 (the row's form is chosen here, hidx_w / cbound).
-  const bool byte_form = forms && cached && !atomic_mode && !load_old && !dst && bound[row] < 256;
-  if (byte_form) {
-    const int nq = (int)(dw >> 4);  // uint4 words of the [d][w] byte image (dw % 32 == 0)
-    uint4* l4 = reinterpret_cast<uint4*>(lds);
-    for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kKeyRegs; ++k)
-      if (ik[k])
-        for (int d = 0; d < hp.depth; ++d) {
-          const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kp[k]);
-          atomicAdd(&lds[c >> 2], ik[k] << ((c & 3u) << 3));  // < 2^8 per byte: no carry
-        }
-    __syncthreads();
-    // sums of squares per sketch row (v_dot4_u32_u8: <= mass * 255 < 2^16),
-    // largest counter, and the OR of every byte (all < 16: nibbles)
-    u8x4 pm = {0, 0, 0, 0};
-    const int qr = w >> 4;  // uint4 per sketch row
-    for (int d = 0; d < hp.depth; ++d) {
-      uint32_t sq = 0;
-      for (int j = tid; j < qr; j += kBuildThreads) {
-        const uint4 v = l4[d * qr + j];
-        sq = __builtin_amdgcn_udot4(v.x, v.x, sq, false);
-        sq = __builtin_amdgcn_udot4(v.y, v.y, sq, false);
-        sq = __builtin_amdgcn_udot4(v.z, v.z, sq, false);
-        sq = __builtin_amdgcn_udot4(v.w, v.w, sq, false);
-        const u8x4 a = __builtin_bit_cast(u8x4, v.x), b = __builtin_bit_cast(u8x4, v.y);
-        const u8x4 c = __builtin_bit_cast(u8x4, v.z), e = __builtin_bit_cast(u8x4, v.w);
-        pm = __builtin_elementwise_max(pm, __builtin_elementwise_max(__builtin_elementwise_max(a, b),
-                                                                     __builtin_elementwise_max(c, e)));
-      }
-      sq = wave_sum_u32(sq);
-      if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
-    }
-    vmax = max(max((uint32_t)pm.x, (uint32_t)pm.y), max((uint32_t)pm.z, (uint32_t)pm.w));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-    if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
-    __syncthreads();
-    const bool nib = s_max < 16u;
-    uint4* d4 = reinterpret_cast<uint4*>(dst16);  // the row's u16 slot (64-B aligned)
-#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
-    if (false)
-#endif
-    if (nib) {  // 32 counters per 16-B store
-      for (int j = tid; j < (nq >> 1); j += kBuildThreads) {
-        const uint4 a = l4[2 * j], b = l4[2 * j + 1];
-        store_row(d4 + j, make_uint4(nibbles8(a.x, a.y), nibbles8(a.z, a.w), nibbles8(b.x, b.y), nibbles8(b.z, b.w)),
-                  SV);
-      }
-    } else {  // 16 counters per 16-B store
-      for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
-    }
-    if (tid == 0) {
-      hidx_w[row] = nib ? kFormU4 : kFormU8;
-      cbound[row] = s_max;
-    }
-  } else {
+  {
   // LDS slot for sketch row 0 (the old counters when accumulating)
   for (int j = tid; j < w; j += kBuildThreads) lds[j] = load_old ? (dst ? dst[j] : (uint32_t)dst16[j]) : 0u;
   __syncthreads();
@@ -519,7 +469,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     lds_barrier();  // LDS order only: the write-out stores stay in flight
     d += two ? 2 : 1;
   }
-  }  // sketch-row loop (not byte_form)
+  }  // sketch-row loop
 
   if (badv) atomicOr(flags, kFlagBadValue);
   mass = wave_sum_u64_sat(mass);
@@ -540,6 +490,190 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       unsigned long long old = atomicAdd((unsigned long long*)&row_mass[row], (unsigned long long)tm);
       if (old + tm >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
     }
+  }
+}
+
+// Byte-class owners (byte_class): the whole [d][w] sketch in LDS as 4-bit
+// counters (dw / 2 bytes: 20 KB at d=5, w=8192, so twice the workgroups of a
+// byte image fit a CU), built in one pass over the owner's cached keys.  The
+// LDS adds return the old counter, so each sketch row's sum of squares
+// (2 c inc + inc^2 per update, telescoping to the exact sum) and the row
+// maximum come out of the update pass, and the finished image IS the stored
+// nibble row: it leaves LDS as 16-B non-temporal stores with no packing.  A
+// counter that would pass 15 (a repeated key, a collision, an increment >= 16)
+// is detected by its add and the owner is queued for k_build_bytes (u8 rows);
+// its partial image is discarded.  One workgroup per owner row; rows of other
+// classes leave at once.
+template <int SV>
+__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
+    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
+    const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
+    uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [d][w] nibbles
+  __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
+  __shared__ uint32_t s_max, s_ovf, s_mass;
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t lo = lo_[row], hi = hi_[row];
+  if (row_hot[row] >= 0 || !byte_class(tv.hidx[row], (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs, bound[row])) return;
+  const int w = (int)hp.width;
+  const int64_t dw = (int64_t)hp.depth * w;
+  if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+  if (tid == 0) {
+    s_max = 0u;
+    s_ovf = 0u;
+    s_mass = 0u;
+  }
+  uint64_t kp[kKeyRegs];
+  uint32_t ik[kKeyRegs];
+  uint32_t mass = 0;
+  bool badv = false;
+#pragma unroll
+  for (int k = 0; k < kKeyRegs; ++k) {
+    const int64_t i = lo + tid + (int64_t)k * kBuildThreads;
+    kp[k] = 0;
+    ik[k] = 0;
+    if (i < hi) {
+      uint32_t inc;
+      if (!load_inc(vals, i, inc, hp.frac_bits)) {
+        badv = true;
+        inc = 0;
+      }
+      kp[k] = reduce_key(keys[i]);
+      ik[k] = inc;
+      mass += inc;
+    }
+  }
+  const int nq = (int)(dw >> 5);  // uint4 words of the nibble image (dw % 32 == 0)
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+  for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  uint32_t vmax = 0;
+  bool ovf = false;
+  for (int d = 0; d < hp.depth; ++d) {
+    uint32_t sq = 0;
+#pragma unroll
+    for (int k = 0; k < kKeyRegs; ++k)
+      if (ik[k]) {
+        const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kp[k]);
+        const uint32_t sh = (c & 7u) << 2;
+        const uint32_t old = (atomicAdd(&lds[c >> 3], ik[k] << sh) >> sh) & 15u;
+        const uint32_t nv = old + ik[k];
+        ovf |= nv > 15u || ik[k] > 15u;  // the add carried into the next counter: rebuild as u8
+        sq += (2u * old + ik[k]) * ik[k];
+        vmax = max(vmax, nv);
+      }
+    sq = wave_sum_u32(sq);
+    if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+  }
+  if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+  if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
+  mass = wave_sum_u32(mass);  // < 2^8 (byte class)
+  if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, mass);
+  __syncthreads();
+  if (s_ovf) {
+    if (tid == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
+    return;
+  }
+  uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * dw);  // the row's u16 slot (64-B aligned)
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+  if (false)
+#endif
+  for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
+  if (badv) atomicOr(flags, kFlagBadValue);
+  if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+  if (tid == 0) {
+    rowmax[row] = s_max;
+    row_mass[row] = s_mass;
+    hidx_w[row] = kFormU4;
+    cbound[row] = s_max;
+  }
+}
+
+// The byte-class owners a counter >= 16 sent back from k_build_nibbles: the
+// same one-pass build on a [d][w] u8 image (dw bytes of LDS), stored as u8
+// rows.  A persistent grid walks the device-side list (no host count).
+template <int SV>
+__global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
+    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
+    const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
+    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [d][w] bytes
+  __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
+  __shared__ uint32_t s_max, s_mass;
+  const int tid = threadIdx.x;
+  const int w = (int)hp.width;
+  const int64_t dw = (int64_t)hp.depth * w;
+  const uint32_t count = *list_cnt;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const int64_t row = list[li];
+    const int64_t lo = lo_[row], hi = hi_[row];
+    if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+    if (tid == 0) {
+      s_max = 0u;
+      s_mass = 0u;
+    }
+    uint64_t kp[kKeyRegs];
+    uint32_t ik[kKeyRegs];
+    uint32_t mass = 0;
+    bool badv = false;
+#pragma unroll
+    for (int k = 0; k < kKeyRegs; ++k) {
+      const int64_t i = lo + tid + (int64_t)k * kBuildThreads;
+      kp[k] = 0;
+      ik[k] = 0;
+      if (i < hi) {
+        uint32_t inc;
+        if (!load_inc(vals, i, inc, hp.frac_bits)) {
+          badv = true;
+          inc = 0;
+        }
+        kp[k] = reduce_key(keys[i]);
+        ik[k] = inc;
+        mass += inc;
+      }
+    }
+    const int nq = (int)(dw >> 4);  // uint4 words of the byte image
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    uint32_t vmax = 0;
+    for (int d = 0; d < hp.depth; ++d) {
+      uint32_t sq = 0;
+#pragma unroll
+      for (int k = 0; k < kKeyRegs; ++k)
+        if (ik[k]) {
+          const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kp[k]);
+          const uint32_t sh = (c & 3u) << 3;
+          const uint32_t old = (atomicAdd(&lds[c >> 2], ik[k] << sh) >> sh) & 255u;  // < 2^8: no carry
+          sq += (2u * old + ik[k]) * ik[k];
+          vmax = max(vmax, old + ik[k]);
+        }
+      sq = wave_sum_u32(sq);  // <= mass * 255 < 2^16
+      if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
+    mass = wave_sum_u32(mass);
+    if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, mass);
+    __syncthreads();
+    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * dw);
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+    if (false)
+#endif
+    for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
+    if (badv) atomicOr(flags, kFlagBadValue);
+    if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+    if (tid == 0) {
+      rowmax[row] = s_max;
+      row_mass[row] = s_mass;
+      hidx_w[row] = kFormU8;
+      cbound[row] = s_max;
+    }
+    __syncthreads();  // the image and the shared sums are consumed before the next owner
   }
 }
 
@@ -700,7 +834,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   // fresh builds may store byte forms: the whole [d][w] byte image in LDS
   const int forms = h->forms_ok && !accumulate && (size_t)h->dw <= kFormLdsMax ? 1 : 0;
   const int skip_untouched = accumulate && h->norms_valid ? 1 : 0;
-  const size_t lds = std::max(sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3), forms ? (size_t)h->dw : (size_t)0);
+  const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
   {
     TimedScope ts(h, "build_rows");
     static const int sv = [] {
@@ -730,6 +864,21 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                        h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
                        skip_untouched, h->d_hidx, h->d_cbound);
     CMS_HIP(hipGetLastError());
+    if (forms) {  // the byte-class owners: 4-bit rows, u8 rows for those a counter >= 16 sent back
+      CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
+      int32_t* redo = h->ws_plist.as<int32_t>();
+      uint32_t* redo_cnt = reinterpret_cast<uint32_t*>(redo + n);
+      CMS_HIP(hipMemsetAsync(redo_cnt, 0, sizeof(uint32_t), h->stream));
+      auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
+      hipLaunchKernelGGL(nk, dim3((unsigned)n), dim3(kBuildThreads), (size_t)h->dw / 2, h->stream, d_lo, d_hi, d_key,
+                         d_val, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
+                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt);
+      auto bk = sv == 2 ? k_build_bytes<2> : sv == 1 ? k_build_bytes<1> : k_build_bytes<0>;
+      hipLaunchKernelGGL(bk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
+                         (size_t)h->dw, h->stream, d_lo, d_hi, d_key, d_val, h->hp, redo, redo_cnt, h->tview(),
+                         h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+      CMS_HIP(hipGetLastError());
+    }
   }
   {
     TimedScope ts(h, "hot_norms");
