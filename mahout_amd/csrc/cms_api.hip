@@ -340,6 +340,9 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
 
   size_t tbytes = sizeof(uint16_t) * (size_t)h->n * (size_t)h->dw;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess ||
       (!per_owner && !f64 && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
       (f64 && (e = hipMalloc(&h->d_t64, 4 * tbytes)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||
@@ -379,6 +382,9 @@ void cms_destroy(cms_handle* h) {
   }
   for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
   if (h->order_ev) (void)hipEventDestroy(h->order_ev);
+  if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   free_query_pool(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
@@ -396,6 +402,7 @@ void cms_destroy(cms_handle* h) {
                   &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
   delete h;
 }
 

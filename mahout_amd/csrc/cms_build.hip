@@ -120,8 +120,9 @@ __global__ __launch_bounds__(256) void k_row_bound_values(const int64_t* lo_, co
 // An owner of a fresh build whose every counter is provably below 2^8 (its
 // mass bound) and whose keys fit the register cache: built whole in LDS by
 // k_build_nibbles / k_build_bytes (not by k_build_rows).
-__device__ __forceinline__ bool byte_class(int32_t slot, bool cached, uint64_t bound) {
-  return slot < 0 && cached && bound < 256;
+constexpr int64_t kByteKeys = 64 * kKeyRegs;  // one wave's register cache (k_build_nibbles)
+__device__ __forceinline__ bool byte_class(int32_t slot, int64_t nkeys, uint64_t bound) {
+  return slot < 0 && nkeys <= kByteKeys && bound < 256;
 }
 
 // grid = emax + nrows: blocks [0, emax) build extra slices of hot owners (heavy
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   // Byte forms: a fresh narrow owner whose mass (so every counter) stays
   // below 2^8 is built by k_build_nibbles (4-bit rows) or, when a counter
   // reaches 16, by k_build_bytes (u8 rows) -- both launched after this kernel.
-  if (forms && !atomic_mode && !load_old && byte_class(slot, cached, bound[row])) return;
+  if (forms && !atomic_mode && !load_old && byte_class(slot, hi - lo, bound[row])) return;
   uint64_t kp[kKeyRegs];
   uint32_t ik[kKeyRegs];
   uint64_t mass = 0;
@@ -493,44 +494,41 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   }
 }
 
-// Byte-class owners (byte_class): the whole [d][w] sketch in LDS as 4-bit
-// counters (dw / 2 bytes: 20 KB at d=5, w=8192, so twice the workgroups of a
-// byte image fit a CU), built in one pass over the owner's cached keys.  The
-// LDS adds return the old counter, so each sketch row's sum of squares
-// (2 c inc + inc^2 per update, telescoping to the exact sum) and the row
-// maximum come out of the update pass, and the finished image IS the stored
-// nibble row: it leaves LDS as 16-B non-temporal stores with no packing.  A
-// counter that would pass 15 (a repeated key, a collision, an increment >= 16)
-// is detected by its add and the owner is queued for k_build_bytes (u8 rows);
-// its partial image is discarded.  One workgroup per owner row; rows of other
-// classes leave at once.
+// Byte-class owners (byte_class): ONE WAVE per owner, four owners per
+// workgroup, each wave with its own w/2-byte LDS slot (4 KB at w = 8192).  The
+// owner's keys are read once into registers; each sketch row in turn is
+// counted in the slot as 4-bit counters and leaves as 16-B non-temporal
+// stores of the slot itself (a nibble row needs no packing).  The LDS adds
+// return the old counter, so each sketch row's sum of squares (2 c inc +
+// inc^2 per update, telescoping to the exact sum) and the row maximum come out
+// of the update pass.  With 4 KB per owner 32 owners are in flight per CU
+// (the wave limit), against 8 with a whole-sketch 20 KB image per workgroup
+// (config 3: 5.1 ms for this kernel).  A counter that would pass 15 (a
+// repeated key, a collision, an increment >= 16) is detected by its add; the
+// owner is queued for k_build_bytes, which rewrites its whole slot, norms and
+// maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
+// one wave's LDS operations execute in program order.
+constexpr int kNibWaves = 4;
 template <int SV>
-__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
-    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
+__global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
+    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
     const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
     uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt) {
-  extern __shared__ __align__(16) uint32_t lds[];  // [d][w] nibbles
-  __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
-  __shared__ uint32_t s_max, s_ovf, s_mass;
-  const int64_t row = blockIdx.x;
-  const int tid = threadIdx.x;
+  extern __shared__ __align__(16) uint32_t lds[];  // [kNibWaves][w / 8] words: one sketch row of nibbles per wave
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * kNibWaves + wv;
+  if (row >= nrows) return;
   const int64_t lo = lo_[row], hi = hi_[row];
-  if (row_hot[row] >= 0 || !byte_class(tv.hidx[row], (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs, bound[row])) return;
+  if (row_hot[row] >= 0 || !byte_class(tv.hidx[row], hi - lo, bound[row])) return;
   const int w = (int)hp.width;
-  const int64_t dw = (int64_t)hp.depth * w;
-  if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
-  if (tid == 0) {
-    s_max = 0u;
-    s_ovf = 0u;
-    s_mass = 0u;
-  }
   uint64_t kp[kKeyRegs];
   uint32_t ik[kKeyRegs];
   uint32_t mass = 0;
   bool badv = false;
 #pragma unroll
   for (int k = 0; k < kKeyRegs; ++k) {
-    const int64_t i = lo + tid + (int64_t)k * kBuildThreads;
+    const int64_t i = lo + lane + (int64_t)k * 64;
     kp[k] = 0;
     ik[k] = 0;
     if (i < hi) {
@@ -544,51 +542,46 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       mass += inc;
     }
   }
-  const int nq = (int)(dw >> 5);  // uint4 words of the nibble image (dw % 32 == 0)
-  uint4* l4 = reinterpret_cast<uint4*>(lds);
-  for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
-  __syncthreads();
+  const int nq = w >> 5;  // uint4 per sketch row of nibbles (w % 32 == 0 with forms)
+  uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * nq;
+  uint32_t* slot = lds + wv * (w >> 3);
+  uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's u16 slot (64-B aligned)
   uint32_t vmax = 0;
   bool ovf = false;
   for (int d = 0; d < hp.depth; ++d) {
+    for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
     uint32_t sq = 0;
 #pragma unroll
     for (int k = 0; k < kKeyRegs; ++k)
       if (ik[k]) {
-        const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kp[k]);
+        const uint32_t c = bucket(hp, d, kp[k]);
         const uint32_t sh = (c & 7u) << 2;
-        const uint32_t old = (atomicAdd(&lds[c >> 3], ik[k] << sh) >> sh) & 15u;
+        const uint32_t old = (atomicAdd(&slot[c >> 3], ik[k] << sh) >> sh) & 15u;
         const uint32_t nv = old + ik[k];
         ovf |= nv > 15u || ik[k] > 15u;  // the add carried into the next counter: rebuild as u8
         sq += (2u * old + ik[k]) * ik[k];
         vmax = max(vmax, nv);
       }
-    sq = wave_sum_u32(sq);
-    if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+    sq = wave_sum_u32(sq);  // <= mass * 15 (exact unless ovf)
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+    if (false)
+#endif
+    for (int j = lane; j < nq; j += 64) store_row(d4 + d * nq + j, slot4[j], SV);
+    if (lane == 0) norm[row * hp.depth + d] = sq;
   }
-  if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-  if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
-  mass = wave_sum_u32(mass);  // < 2^8 (byte class)
-  if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, mass);
-  __syncthreads();
-  if (s_ovf) {
-    if (tid == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
+  if (badv) atomicOr(flags, kFlagBadValue);
+  if (__ballot(ovf)) {
+    if (lane == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
     return;
   }
-  uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * dw);  // the row's u16 slot (64-B aligned)
-#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
-  if (false)
-#endif
-  for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
-  if (badv) atomicOr(flags, kFlagBadValue);
-  if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
-  if (tid == 0) {
-    rowmax[row] = s_max;
-    row_mass[row] = s_mass;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+  mass = wave_sum_u32(mass);  // < 2^8 (byte class)
+  if (lane == 0) {
+    rowmax[row] = vmax;
+    row_mass[row] = mass;
     hidx_w[row] = kFormU4;
-    cbound[row] = s_max;
+    cbound[row] = vmax;
   }
 }
 
@@ -841,22 +834,26 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       const char* e = getenv("CMS_BUILD_SV");
       return e ? std::max(0, std::min(2, atoi(e))) : kBuildStoreForm;
     }();
-    // extra slices of unit increments on k_build_slices (one pass over the keys
-    // for all d rows; LDS d*w*2 bytes)
+    // EXPERIMENT (CMS_SLICES_SIDE=1): the extra slices of the hot owners with
+    // unit increments on k_build_slices (each key read and reduced once for
+    // all d rows; LDS d*w*2 bytes) on a side stream, beside the row builds.
+    // Measured no faster (config 3 build 11.9 -> 12.5 ms, config 2 equal), so
+    // the slices stay in k_build_rows (d/2 passes over their keys).
     const size_t slice_lds = (size_t)h->p.depth * (size_t)h->p.width * 2;
-    // measured SLOWER (config 2 build 1.16 -> 1.33 ms, config 3 18.7 -> 19.8 ms:
-    // the slices then run alone before the rows instead of beside them), so it
-    // is an experiment behind CMS_SLICES_KERNEL=1
     const int slices_done = !d_val && (h->p.width % 2) == 0 && (kSlice << h->hp.frac_bits) < 65536 &&
-                            slice_lds <= 96 * 1024 && getenv("CMS_SLICES_KERNEL");
+                            slice_lds <= 96 * 1024 && h->side_stream && getenv("CMS_SLICES_SIDE");
     if (slices_done) {
       static bool attr = [] {
         (void)hipFuncSetAttribute((const void*)k_build_slices, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
         return true;
       }();
       (void)attr;
-      hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(256), slice_lds, h->stream, d_lo, d_hi, d_key,
+      CMS_HIP(hipEventRecord(h->ev_fork, h->stream));  // plan, promotion (slot rows zeroed) are done
+      CMS_HIP(hipStreamWaitEvent(h->side_stream, h->ev_fork, 0));
+      hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(256), slice_lds, h->side_stream, d_lo, d_hi, d_key,
                          h->hp, kSlice, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
+      CMS_HIP(hipGetLastError());
+      CMS_HIP(hipEventRecord(h->ev_join, h->side_stream));
     }
     auto kern = sv == 2 ? k_build_rows<2> : sv == 1 ? k_build_rows<1> : k_build_rows<0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
@@ -870,15 +867,17 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       uint32_t* redo_cnt = reinterpret_cast<uint32_t*>(redo + n);
       CMS_HIP(hipMemsetAsync(redo_cnt, 0, sizeof(uint32_t), h->stream));
       auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
-      hipLaunchKernelGGL(nk, dim3((unsigned)n), dim3(kBuildThreads), (size_t)h->dw / 2, h->stream, d_lo, d_hi, d_key,
-                         d_val, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
-                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt);
+      hipLaunchKernelGGL(nk, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)), dim3(64 * kNibWaves),
+                         (size_t)kNibWaves * (size_t)h->p.width / 2, h->stream, d_lo, d_hi, d_key, d_val, n, h->hp,
+                         row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass,
+                         h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt);
       auto bk = sv == 2 ? k_build_bytes<2> : sv == 1 ? k_build_bytes<1> : k_build_bytes<0>;
       hipLaunchKernelGGL(bk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
                          (size_t)h->dw, h->stream, d_lo, d_hi, d_key, d_val, h->hp, redo, redo_cnt, h->tview(),
                          h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       CMS_HIP(hipGetLastError());
     }
+    if (slices_done) CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join, 0));  // the slices have landed
   }
   {
     TimedScope ts(h, "hot_norms");

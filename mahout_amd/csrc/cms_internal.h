@@ -139,6 +139,10 @@ struct cms_handle {
   int device = 0;
   int num_cus = 256;  // compute units of the device (persistent grids)
   hipStream_t stream = nullptr;
+  // side stream of the row build: the hot owners' slices run beside the row
+  // kernels (ordered by ev_fork / ev_join on the handle's stream)
+  hipStream_t side_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
   // the point queries after cms_finalize hold it shared and run concurrently,
   // each on a QueryCtx of its own (the table and norms are read-only then).
