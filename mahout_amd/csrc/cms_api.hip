@@ -397,7 +397,7 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
                   &h->ws_f4, &h->ws_i8blk, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
-                  &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist,
+                  &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist, &h->ws_blist,
                   &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked, &h->rf_ids, &h->rf_sc, &h->rf_cnt,
                   &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};
   for (DevBuf* b : ws) b->release();

@@ -153,7 +153,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
     TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate,
-    int slices_done, const uint64_t* bound, int forms, int skip_untouched, int32_t* hidx_w, uint32_t* cbound) {
+    int slices_done, const uint64_t* bound, int forms, int skip_untouched, int32_t* hidx_w, uint32_t* cbound,
+    const int32_t* rows_list, const uint32_t* rows_cnt) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w] u32, or a byte-form owner's [d][w] u8
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -176,6 +177,10 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     atomic_mode = true;
   } else {
     row = (int64_t)blockIdx.x - emax;
+    if (rows_list) {  // only the listed rows (the slot rows; the others have kernels of their own)
+      if (row >= (int64_t)*rows_cnt) return;
+      row = rows_list[row];
+    }
     lo = lo_[row];
     atomic_mode = row_hot[row] >= 0;
     hi = atomic_mode ? lo + slice : hi_[row];
@@ -491,6 +496,177 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
       unsigned long long old = atomicAdd((unsigned long long*)&row_mass[row], (unsigned long long)tm);
       if (old + tm >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
     }
+  }
+}
+
+// Owner classes of a fresh build with forms: rows holding a u32 slot (split
+// owners and masses >= 2^16: k_build_rows), byte-class rows (k_build_nibbles
+// finds them itself) and the rest, the mid class (k_build_mid).  Each wave
+// appends its rows with one atomic per list.
+__global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const int64_t* hi_, int64_t nrows,
+                                                       const int32_t* hidx, const uint64_t* bound, int32_t* slot_list,
+                                                       int32_t* mid_list, uint32_t* cnt /* [0] slot, [1] mid */) {
+  const int lane = (int)__lane_id();
+  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nrows; base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = base + threadIdx.x;
+    bool is_slot = false, is_mid = false;
+    if (r < nrows) {
+      const int32_t sl = hidx[r];
+      is_slot = sl >= 0;
+      is_mid = !is_slot && !byte_class(sl, hi_[r] - lo_[r], bound[r]);
+    }
+    const unsigned long long ms = __ballot(is_slot), mm = __ballot(is_mid);
+    const unsigned long long below = (1ULL << lane) - 1ULL;
+    uint32_t b0 = 0, b1 = 0;
+    if (lane == 0) {
+      if (ms) b0 = atomicAdd(&cnt[0], (uint32_t)__popcll(ms));
+      if (mm) b1 = atomicAdd(&cnt[1], (uint32_t)__popcll(mm));
+    }
+    b0 = (uint32_t)__shfl((int)b0, 0, 64);
+    b1 = (uint32_t)__shfl((int)b1, 0, 64);
+    if (is_slot) slot_list[b0 + __popcll(ms & below)] = (int32_t)r;
+    if (is_mid) mid_list[b1 + __popcll(mm & below)] = (int32_t)r;
+  }
+}
+
+// Mid-class owners (narrow, more than 256 keys or a mass >= 256): one
+// workgroup per owner, one sketch row at a time in a 2w-byte LDS image, in
+// the narrowest form that holds it -- 4-bit first, u8 when a counter reaches
+// 16, u16 when one reaches 256 (each escalation restarts the owner; the wider
+// layout overwrites every byte the narrower one wrote).  As in
+// k_build_nibbles the returning LDS adds give each sketch row's sum of squares
+// and the row maximum, and each finished sketch row leaves LDS as is.  The
+// 16 KB image (config 3) keeps 8 workgroups per CU against 5 with the 32 KB
+// paired-u16 row image of k_build_rows; the stored rows shrink 2-4x.  A
+// persistent grid walks the device-side list.
+template <int SV>
+__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_mid(
+    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
+    const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
+    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
+  extern __shared__ __align__(16) uint32_t lds[];  // one sketch row, up to w u16 counters
+  __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
+  __shared__ unsigned long long s_mass;
+  __shared__ uint32_t s_max, s_ovf;
+  const int tid = threadIdx.x;
+  const int w = (int)hp.width;
+  const uint32_t count = *list_cnt;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const int64_t row = list[li];
+    const int64_t lo = lo_[row], hi = hi_[row];
+    const bool cached = (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs;
+    uint64_t kp[kKeyRegs];
+    uint32_t ik[kKeyRegs];
+    uint64_t mass = 0;
+    bool badv = false;
+    if (cached) {
+#pragma unroll
+      for (int k = 0; k < kKeyRegs; ++k) {
+        const int64_t i = lo + tid + (int64_t)k * kBuildThreads;
+        kp[k] = 0;
+        ik[k] = 0;
+        if (i < hi) {
+          uint32_t inc;
+          if (!load_inc(vals, i, inc, hp.frac_bits)) {
+            badv = true;
+            inc = 0;
+          }
+          kp[k] = reduce_key(keys[i]);
+          ik[k] = inc;
+          mass += inc;
+        }
+      }
+    }
+    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's slot (64-B aligned)
+    int level = 0;  // 0: 4-bit, 1: u8, 2: u16 (the class bound keeps every counter < 2^16)
+    uint32_t vmax = 0;
+    for (;;) {
+      const int bits = 4 << level;
+      const int lg = 3 - level;          // log2(counters per word)
+      const uint32_t cap = (1u << bits) - 1u;
+      const int nq = (w * bits) >> 7;    // uint4 per sketch row (w % 32 == 0)
+      uint4* l4 = reinterpret_cast<uint4*>(lds);
+      if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+      if (tid == 0) {
+        s_max = 0u;
+        s_ovf = 0u;
+        s_mass = 0ULL;
+      }
+      vmax = 0;
+      for (int d = 0; d < hp.depth; ++d) {
+        for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        uint64_t sq = 0;
+        bool ovf = false;
+        auto add = [&](uint64_t kr, uint32_t inc) {
+          const uint32_t c = bucket(hp, d, kr);
+          const uint32_t sh = (c & ((1u << lg) - 1u)) * (uint32_t)bits;
+          const uint32_t old = (atomicAdd(&lds[c >> lg], inc << sh) >> sh) & cap;
+          const uint32_t nv = old + inc;
+          ovf |= nv > cap || inc > cap;  // carried into the next counter: a wider form
+          sq += (uint64_t)(2u * old + inc) * inc;
+          vmax = max(vmax, nv);
+        };
+        if (cached) {
+#pragma unroll
+          for (int k = 0; k < kKeyRegs; ++k)
+            if (ik[k]) add(kp[k], ik[k]);
+        } else {
+          for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
+            int64_t kk[4];
+            uint32_t inc4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+              kk[u] = i < hi ? keys[i] : 0;
+              inc4[u] = 0;
+              if (i < hi) {
+                uint32_t inc;
+                if (!load_inc(vals, i, inc, hp.frac_bits)) {
+                  badv = true;
+                  inc = 0;
+                }
+                inc4[u] = inc;
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (inc4[u]) add(reduce_key(kk[u]), inc4[u]);
+              if (d == 0 && level == 0) mass += inc4[u];
+            }
+          }
+        }
+        sq = wave_sum_u64_sat(sq);
+        if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+        if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
+        __syncthreads();
+        if (s_ovf) break;  // uniform: escalate
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+        if (false)
+#endif
+        for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + d * nq + j, l4[j], SV);
+        __syncthreads();  // the image is read out before the next sketch row zeroes it
+      }
+      if (!s_ovf || level == 2) break;
+      __syncthreads();
+      ++level;
+    }
+    if (badv) atomicOr(flags, kFlagBadValue);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
+    mass = wave_sum_u64_sat(mass);
+    if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, (unsigned long long)mass);
+    __syncthreads();
+    if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+    if (tid == 0) {
+      rowmax[row] = s_max;
+      row_mass[row] = s_mass;
+      if (s_mass >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+      hidx_w[row] = level == 0 ? kFormU4 : level == 1 ? kFormU8 : kFormU16;
+      cbound[row] = s_max;
+    }
+    __syncthreads();  // shared sums consumed before the next owner
   }
 }
 
@@ -856,10 +1032,34 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       CMS_HIP(hipEventRecord(h->ev_join, h->side_stream));
     }
     auto kern = sv == 2 ? k_build_rows<2> : sv == 1 ? k_build_rows<1> : k_build_rows<0>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
-                       d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
-                       h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
-                       skip_untouched, h->d_hidx, h->d_cbound);
+    if (forms) {
+      // owner classes: slot rows -> k_build_rows, mid rows -> k_build_mid, the
+      // byte class -> k_build_nibbles (below)
+      CMS_HIP(h->ws_blist.ensure(sizeof(int32_t) * (size_t)(2 * n + 4)));
+      int32_t* slot_list = h->ws_blist.as<int32_t>();
+      int32_t* mid_list = slot_list + n;
+      uint32_t* lcnt = reinterpret_cast<uint32_t*>(mid_list + n);
+      CMS_HIP(hipMemsetAsync(lcnt, 0, 2 * sizeof(uint32_t), h->stream));
+      hipLaunchKernelGGL(k_build_classes, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))),
+                         dim3(256), 0, h->stream, d_lo, d_hi, n, h->d_hidx, h->ws_bound.as<uint64_t>(), slot_list,
+                         mid_list, lcnt);
+      // slot rows: at most the slots in use (host-known), plus the extra slices
+      const int64_t nslot = std::min<int64_t>(n, h->hot_used);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(emax + nslot)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
+                         d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
+                         h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
+                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)slot_list, (const uint32_t*)lcnt);
+      auto mk = sv == 2 ? k_build_mid<2> : sv == 1 ? k_build_mid<1> : k_build_mid<0>;
+      hipLaunchKernelGGL(mk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)), dim3(kBuildThreads),
+                         (size_t)h->p.width * 2, h->stream, d_lo, d_hi, d_key, d_val, h->hp, (const int32_t*)mid_list,
+                         (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
+                         h->d_rowmax, h->d_flags);
+    } else {
+      hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
+                         d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
+                         h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
+                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)nullptr, (const uint32_t*)nullptr);
+    }
     CMS_HIP(hipGetLastError());
     if (forms) {  // the byte-class owners: 4-bit rows, u8 rows for those a counter >= 16 sent back
       CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));

@@ -164,6 +164,7 @@ struct cms_handle {
   bool forms_ok = false;            // dw % 32 == 0: fresh builds may store u8 / nibble forms
   cms::DevBuf hot_tab;              // [hot_cap][d][w] u32 counters of the hot rows
   cms::DevBuf ws_bound, ws_force, ws_plist;  // promotion scratch: u64 [n], u8 [n], i32 [n] + count
+  cms::DevBuf ws_blist;                      // row build: slot-row and mid-class row lists + counts
   int64_t hot_cap = 0, hot_used = 0;
   cms::TableView tview() const {
     return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw};
