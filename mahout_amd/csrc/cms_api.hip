@@ -343,6 +343,8 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
       (e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_fork2, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_join2, hipEventDisableTiming)) != hipSuccess ||
       (!per_owner && !f64 && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
       (f64 && (e = hipMalloc(&h->d_t64, 4 * tbytes)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||
@@ -385,6 +387,8 @@ void cms_destroy(cms_handle* h) {
   if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ev_fork2) (void)hipEventDestroy(h->ev_fork2);
+  if (h->ev_join2) (void)hipEventDestroy(h->ev_join2);
   free_query_pool(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
   void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};

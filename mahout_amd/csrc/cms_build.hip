@@ -1033,48 +1033,59 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     }
     auto kern = sv == 2 ? k_build_rows<2> : sv == 1 ? k_build_rows<1> : k_build_rows<0>;
     if (forms) {
-      // owner classes: slot rows -> k_build_rows, mid rows -> k_build_mid, the
-      // byte class -> k_build_nibbles (below)
+      // owner classes: slot rows -> k_build_rows (the handle's stream), byte
+      // rows -> k_build_nibbles (+ k_build_bytes for the ones a counter >= 16
+      // sends back) and mid rows -> k_build_mid on the side stream, so the
+      // three classes' kernels overlap (their tails no longer leave CUs idle)
       CMS_HIP(h->ws_blist.ensure(sizeof(int32_t) * (size_t)(2 * n + 4)));
       int32_t* slot_list = h->ws_blist.as<int32_t>();
       int32_t* mid_list = slot_list + n;
       uint32_t* lcnt = reinterpret_cast<uint32_t*>(mid_list + n);
+      CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
+      int32_t* redo = h->ws_plist.as<int32_t>();
+      uint32_t* redo_cnt = reinterpret_cast<uint32_t*>(redo + n);
       CMS_HIP(hipMemsetAsync(lcnt, 0, 2 * sizeof(uint32_t), h->stream));
+      CMS_HIP(hipMemsetAsync(redo_cnt, 0, sizeof(uint32_t), h->stream));
       hipLaunchKernelGGL(k_build_classes, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))),
                          dim3(256), 0, h->stream, d_lo, d_hi, n, h->d_hidx, h->ws_bound.as<uint64_t>(), slot_list,
                          mid_list, lcnt);
+      CMS_HIP(hipGetLastError());
+      hipStream_t side = h->side_stream ? h->side_stream : h->stream;
+      if (side != h->stream) {
+        CMS_HIP(hipEventRecord(h->ev_fork2, h->stream));
+        CMS_HIP(hipStreamWaitEvent(side, h->ev_fork2, 0));
+      }
+      auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
+      hipLaunchKernelGGL(nk, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)), dim3(64 * kNibWaves),
+                         (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, d_key, d_val, n, h->hp,
+                         row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass,
+                         h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt);
+      auto mk = sv == 2 ? k_build_mid<2> : sv == 1 ? k_build_mid<1> : k_build_mid<0>;
+      hipLaunchKernelGGL(mk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)), dim3(kBuildThreads),
+                         (size_t)h->p.width * 2, side, d_lo, d_hi, d_key, d_val, h->hp, (const int32_t*)mid_list,
+                         (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
+                         h->d_rowmax, h->d_flags);
+      auto bk = sv == 2 ? k_build_bytes<2> : sv == 1 ? k_build_bytes<1> : k_build_bytes<0>;
+      hipLaunchKernelGGL(bk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
+                         (size_t)h->dw, side, d_lo, d_hi, d_key, d_val, h->hp, redo, redo_cnt, h->tview(),
+                         h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+      CMS_HIP(hipGetLastError());
       // slot rows: at most the slots in use (host-known), plus the extra slices
       const int64_t nslot = std::min<int64_t>(n, h->hot_used);
       hipLaunchKernelGGL(kern, dim3((unsigned)(emax + nslot)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                          d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
                          h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
                          skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)slot_list, (const uint32_t*)lcnt);
-      auto mk = sv == 2 ? k_build_mid<2> : sv == 1 ? k_build_mid<1> : k_build_mid<0>;
-      hipLaunchKernelGGL(mk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)), dim3(kBuildThreads),
-                         (size_t)h->p.width * 2, h->stream, d_lo, d_hi, d_key, d_val, h->hp, (const int32_t*)mid_list,
-                         (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
-                         h->d_rowmax, h->d_flags);
+      CMS_HIP(hipGetLastError());
+      if (side != h->stream) {
+        CMS_HIP(hipEventRecord(h->ev_join2, side));
+        CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join2, 0));
+      }
     } else {
       hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                          d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
                          h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
                          skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)nullptr, (const uint32_t*)nullptr);
-    }
-    CMS_HIP(hipGetLastError());
-    if (forms) {  // the byte-class owners: 4-bit rows, u8 rows for those a counter >= 16 sent back
-      CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
-      int32_t* redo = h->ws_plist.as<int32_t>();
-      uint32_t* redo_cnt = reinterpret_cast<uint32_t*>(redo + n);
-      CMS_HIP(hipMemsetAsync(redo_cnt, 0, sizeof(uint32_t), h->stream));
-      auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
-      hipLaunchKernelGGL(nk, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)), dim3(64 * kNibWaves),
-                         (size_t)kNibWaves * (size_t)h->p.width / 2, h->stream, d_lo, d_hi, d_key, d_val, n, h->hp,
-                         row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass,
-                         h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt);
-      auto bk = sv == 2 ? k_build_bytes<2> : sv == 1 ? k_build_bytes<1> : k_build_bytes<0>;
-      hipLaunchKernelGGL(bk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
-                         (size_t)h->dw, h->stream, d_lo, d_hi, d_key, d_val, h->hp, redo, redo_cnt, h->tview(),
-                         h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       CMS_HIP(hipGetLastError());
     }
     if (slices_done) CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join, 0));  // the slices have landed

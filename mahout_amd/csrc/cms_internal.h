@@ -142,7 +142,8 @@ struct cms_handle {
   // side stream of the row build: the hot owners' slices run beside the row
   // kernels (ordered by ev_fork / ev_join on the handle's stream)
   hipStream_t side_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;    // slices experiment (CMS_SLICES_SIDE)
+  hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // byte / mid class kernels beside the slot rows
   // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
   // the point queries after cms_finalize hold it shared and run concurrently,
   // each on a QueryCtx of its own (the table and norms are read-only then).
