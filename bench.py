@@ -456,12 +456,14 @@ def config3_shard(n_items, n_users, total_pairs, rank, world, device, seed=20261
 
 
 def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
-    """Roofline of k_build_rows (the ingest's dominant kernel).
+    """Roofline of the row build (the "build_rows" scope: k_build_rows for the
+    slot rows and slices, k_build_mid, k_build_nibbles, k_build_bytes -- the
+    ingest's dominant phase).
 
     Algorithmic bytes per launch = what the row build must move for the table
     as it is stored: the grouped keys read once (8 B per pair), the owner spans
     (2 x 8 B per owner) and every counter written once at its stored width
-    (u16 narrow rows, u32 hot rows: cms_stats.stored_bytes).  SURVEY 8(d)
+    (4-bit / u8 / u16 narrow rows, u32 hot rows: cms_stats.stored_bytes).  SURVEY 8(d)
     prices every counter at 4 B; that figure is reported beside it as
     `u32_priced_*` -- it exceeds the bytes the kernel has to move, so a
     fraction of it is not a bandwidth fraction and can pass 1.  `traffic` is
@@ -481,7 +483,9 @@ def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
            "frac_traffic": traffic / avg_s / 1e9 / HBM_PEAK_GBPS if traffic and avg_s else None,
            "algorithmic_bytes_per_launch": alg,
            "algorithmic_bytes_basis": "keys 8 B/pair + spans 16 B/owner + counters at stored width "
-                                      f"({n - int(st['hot_rows'])} u16 rows, {int(st['hot_rows'])} u32 rows)",
+                                      f"({int(st['nibble_rows'])} 4-bit rows, {int(st['u8_rows'])} u8 rows, "
+                                      f"{n - int(st['hot_rows']) - int(st['nibble_rows']) - int(st['u8_rows'])} u16 rows, "
+                                      f"{int(st['hot_rows'])} u32 rows)",
            "avg_launch_ms": avg_s * 1e3 if avg_s else None,
            "u32_priced_bytes_per_launch": u32_alg,
            "u32_priced_GBps": u32_alg / avg_s / 1e9 if avg_s else None}
