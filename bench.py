@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--no-cosine-1m", action="store_true", help="skip configs 4 and 5 on the headline table")
     ap.add_argument("--no-headline", action="store_true",
                     help="profiling aid: run the secondary lines only (no headline value is printed)")
-    ap.add_argument("--stream-batches", type=int, default=8, help="config-5 incremental batches per rank")
+    ap.add_argument("--stream-batches", type=int, default=4, help="config 5: refresh-phase batches (1.25M pairs per rank)")
+    ap.add_argument("--stream-pairs", type=float, default=1e9, help="config 5: pairs of the sustained stream (per node)")
+    ap.add_argument("--stream-batch", type=float, default=1e7, help="config 5: pairs per sustained-stream batch")
     ap.add_argument("--refresh-every", type=int, default=1,
                     help="config 5: batches between periodic top-k refreshes (cms_top_k_refresh)")
     ap.add_argument("--stream-refresh-multi", action="store_true",
@@ -646,90 +648,122 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
 
 
 def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
-    """Config 5 on the resident 1M-item table: incremental batches of 1.25M
-    pairs per GPU (the config's per-second share) through the atomic update
-    path, which keeps norms and row maxima current, then one refresh =
-    cms_finalize (with G ranks: the batches' delta logs all-gathered and
-    applied) + the all-pairs top-k.  Reports the sustained incremental rate
-    (B = N*(R + 2*d*C) = 56 B/update) and the refresh latency."""
+    """Config 5 on the resident 1M-item table (BASELINE configs[4]: a 1B-pair
+    stream at 10M pairs/s, incremental sketch + periodic top-k refresh).
+
+    Sustained ingest: the whole 1B-pair stream (per node; user-hash sharded
+    over the ranks) in batches of 10M pairs -- one second of the stream each --
+    through the incremental path (grouped by owner, k_ingest_sorted: exact
+    atomics that keep norms and row maxima current), each batch generated
+    outside the timed region; one finalize at the end (with G ranks: the delta
+    logs all-gathered and applied).  Periodic refresh: after the stream, short
+    batches of 1.25M pairs (an eighth of a second of the stream) each followed
+    by finalize + cms_top_k_refresh_device, against the whole job that builds
+    the kept lists."""
     from mahout_amd.sketch import shard_of_keys
     from mahout_amd.synth import zipf_stream_torch
-    per_batch = 1_250_000
-    nb = max(1, args.stream_batches)
     shard_tbl = None
     if world > 1:
         shard_tbl = torch.from_numpy(shard_of_keys(np.arange(10_000_000, dtype=np.int64), world)).to(device)
-    batches = []
-    for b in range(nb):
-        it_, us = zipf_stream_torch(10_000_000, n, per_batch * world, seed=777_000 + b, device=device)
+
+    def batch(seed, size):
+        it_, us = zipf_stream_torch(10_000_000, n, size, seed=seed, device=device)
         if shard_tbl is not None:
             keep = shard_tbl[us] == rank
             it_, us = it_[keep], us[keep]
-        batches.append((it_.contiguous(), us.contiguous()))
-    local = sum(int(b[0].numel()) for b in batches)
+        return it_.contiguous(), us.contiguous()
+
+    # ---- sustained ingest of the 1B-pair stream ----
+    t.set_timing(True)
+    t.reset_timing()
+    total = int(args.stream_pairs)
+    bsize = int(args.stream_batch)
+    nbatch = (total + bsize - 1) // bsize
+    ingest_s, local, worst = 0.0, 0, 0.0
+    for b in range(nbatch):
+        it_, us = batch(555_000 + b, min(bsize, total - b * bsize))
+        bar()
+        t0 = time.perf_counter()
+        t.ingest_device_rows(it_, us, None, int(it_.numel()))
+        bar()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        ingest_s += dt
+        worst = max(worst, dt)
+        local += int(it_.numel())
+        del it_, us
+    t0 = time.perf_counter()
+    t.finalize()
+    bar()
+    fin_s = max_over_ranks(time.perf_counter() - t0)
+    sorted_ms, sorted_n = t.timing("ingest_sorted")
+    atomic_ms, atomic_n = t.timing("ingest_atomic")
+    kern = "k_ingest_sorted" if sorted_n else "k_ingest_atomic"
+    kern_ms, kern_n = (sorted_ms, sorted_n) if sorted_n else (atomic_ms, atomic_n)
+    alg = local * (16 + 2 * 5 * 4)
+    sustained = {
+        "stream_pairs": total, "batch_pairs": bsize, "batches": nbatch,
+        "ingest_s": ingest_s, "finalize_s": fin_s,
+        "sustained_updates_per_s": total / ingest_s,
+        "x_realtime": (total / ingest_s) / 10e6,  # the stream arrives at 10M pairs/s
+        "batch_latency_ms": ingest_s * 1e3 / nbatch, "batch_latency_max_ms": worst * 1e3,
+        "path": f"{kern} (batches of >= 32768 pairs into a live table are grouped by owner first and take "
+                "k_ingest_sorted: exact u32 global atomics, norm / row-max / mass deltas reduced per owner inside the "
+                "wave; smaller batches take k_ingest_atomic)",
+        "roofline": {"bound": "hbm", "kernel": kern, "algorithmic_bytes_per_update": 56,
+                     "note": "SURVEY 8(d) prices an incremental update at 56 B of streaming traffic; the kernel's d "
+                             "counter updates per pair are scattered single-dword atomics (one 64-B sector RMW each), "
+                             "whose measured ceiling is far below the streaming rate (DESIGN 4.1)",
+                     "achieved": alg / (kern_ms * 1e-3) / 1e9 if kern_n else None, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": alg / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if kern_n else None,
+                     "avg_launch_ms": kern_ms / kern_n if kern_n else None},
+    }
+
+    # ---- periodic refresh ----
+    per_batch = 1_250_000
+    nb = max(1, args.stream_batches)
+    batches = [batch(777_000 + b, per_batch * world) for b in range(nb)]
     # owners the batches touch: the refresh recomputes every pair with a
     # touched owner, i.e. 1 - (1 - f)^2 of the pairs for a touched fraction f
     touched_all = torch.unique(torch.cat([b[0] for b in batches])).numel() / n
     touched_one = sum(torch.unique(b[0]).numel() for b in batches) / (n * nb)
     every = max(1, args.refresh_every)
     # the periodic refresh keeps 2k-deep lists: one whole job builds them
-    t.set_timing(True)
     bar()
     t0 = time.perf_counter()
     t.top_k_refresh_device(k)
     bar()
     keep_s = max_over_ranks(time.perf_counter() - t0)
-    t.reset_timing()
-    ingest_s = 0.0
     periods = []
     cnt = None
     for bi, (it_, us) in enumerate(batches):
         bar()
-        t0 = time.perf_counter()
         t.ingest_device_rows(it_, us, None, int(it_.numel()))
         bar()
-        ingest_s += max_over_ranks(time.perf_counter() - t0)
         if (bi + 1) % every == 0 or bi == nb - 1:
             t0 = time.perf_counter()
             t.finalize()  # with G ranks: the delta logs all-gathered and applied
             bar()
-            fin_s = max_over_ranks(time.perf_counter() - t0)
+            fs = max_over_ranks(time.perf_counter() - t0)
             t0 = time.perf_counter()
             _, _, cnt = t.top_k_refresh_device(k)  # lists stay in HBM (Refreshable consumers read them there)
             bar()
             rs = max_over_ranks(time.perf_counter() - t0)
             touched, redone, full = t.refresh_stats()
-            periods.append({"after_batch": bi + 1, "finalize_s": round(fin_s, 5), "refresh_s": round(rs, 4),
+            periods.append({"after_batch": bi + 1, "finalize_s": round(fs, 5), "refresh_s": round(rs, 4),
                             "touched_owner_frac": touched / n, "lists_redone": redone, "whole_jobs": full})
-    atomic_ms, atomic_n = t.timing("ingest_atomic")
-    sorted_ms, sorted_n = t.timing("ingest_sorted")
-    kern = "k_ingest_sorted" if sorted_n else "k_ingest_atomic"
-    if sorted_n:
-        atomic_ms, atomic_n = sorted_ms, sorted_n
     cnt = cnt.cpu().numpy()
     t.set_timing(False)
-    total = nb * per_batch * world
     del batches
-    alg = local * (16 + 2 * 5 * 4)
     lat = [p["finalize_s"] + p["refresh_s"] for p in periods]
     return {
-        "workload": f"config 5: {nb} batches x {per_batch} pairs per GPU into the resident {n}-item table; every "
-                    f"{every} batches finalize + incremental top-{k} refresh of every item (cms_top_k_refresh)",
-        "path": f"{kern} (batches of >= 32768 pairs into a live table are grouped by owner first and take "
-                "k_ingest_sorted: exact u32 global atomics, norm / row-max / mass deltas reduced per owner inside the "
-                "wave; smaller batches take k_ingest_atomic)",
-        "batches": nb, "pairs_per_batch_per_gpu": per_batch,
-        "sustained_updates_per_s": total / ingest_s,
-        "batch_latency_ms": ingest_s * 1e3 / nb,
-        "roofline": {"bound": "hbm", "kernel": kern,
-                     "algorithmic_bytes_per_update": 56,
-                     "note": "SURVEY 8(d) prices an incremental update at 56 B of streaming traffic; the kernel's d "
-                             "counter updates per pair are scattered single-dword atomics (one 64-B sector RMW each), "
-                             "whose measured ceiling is far below the streaming rate (DESIGN 4.1)",
-                     "achieved": alg / (atomic_ms * 1e-3) / 1e9 if atomic_n else None,
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": alg / (atomic_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS if atomic_n else None,
-                     "avg_launch_ms": atomic_ms / atomic_n if atomic_n else None},
+        "workload": f"config 5: a {total}-pair Zipf stream (10M pairs/s) into the resident {n}-item table in "
+                    f"{bsize}-pair batches; then {nb} batches of {per_batch} pairs per GPU, every {every} batch(es) "
+                    f"finalize + incremental top-{k} refresh of every item (cms_top_k_refresh)",
+        "sustained": sustained,
+        "sustained_updates_per_s": sustained["sustained_updates_per_s"],
+        "path": sustained["path"],
+        "roofline": sustained["roofline"],
+        "refresh_batches": nb, "pairs_per_batch_per_gpu": per_batch,
         "refresh_every_batches": every,
         "keep_lists_whole_job_s": keep_s,
         "refresh_latency_s": sum(lat) / len(lat),

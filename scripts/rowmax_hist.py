@@ -1,16 +1,16 @@
-"""EXPERIMENT: distribution of the largest counter per owner at config 4
-(1M items, d=5, w=8192, the 500M-pair config-3 stream) -- which operand
-formats could carry each owner class exactly (fp4 e2m1: <= 4, fp6 e2m3:
-<= 7, fp8 e4m3: <= 16, int8 limb: <= 127)."""
+"""Histogram of the owners' largest counter after the config-3 ingest (which
+operand class the all-pairs job can give them: fp4 <= 4, fp6 e2m3 <= 7,
+int8 single limb < 128, multi-limb)."""
 import json
 import sys
 
 sys.path.insert(0, ".")
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from mahout_amd import SketchTable  # noqa: E402
 from mahout_amd.synth import zipf_stream_torch  # noqa: E402
 
-n, pairs, w, d = 1_000_000, 500_000_000, 8192, 5
+n, d, w, pairs = 1_000_000, 5, 8192, 500_000_000
 chunks, done, it = [], 0, 0
 while done < pairs:
     m = min(1 << 26, pairs - done)
@@ -23,28 +23,16 @@ del chunks
 t = SketchTable(n, depth=d, width=w, seed=42, device=0)
 t.ingest_device_rows(items, users, None, pairs)
 t.finalize()
-counts = torch.bincount(items, minlength=n)
+t.synchronize()
 del items, users
 torch.cuda.empty_cache()
-t.release_scratch()
-mx = torch.empty(n, dtype=torch.int64, device="cuda")
-step = 16384
-buf = None
-for r0 in range(0, n, step):
-    rc = min(step, n - r0)
-    buf = t.read_counters_device(r0, rc, out=None)
-    mx[r0:r0 + rc] = buf.view(rc, -1).to(torch.int64).amax(dim=1)
-edges = [0, 4, 7, 8, 15, 16, 31, 63, 127, 1 << 40]
-hist = {}
-lo = -1
-for e in edges:
-    hist[f"({lo},{e}]"] = int(((mx > lo) & (mx <= e)).sum())
-    lo = e
-# pairs per owner by class
-cls = {"<=4": mx <= 4, "5..7": (mx > 4) & (mx <= 7), "8..16": (mx > 7) & (mx <= 16), "17..127": (mx > 16) & (mx <= 127),
-       ">=128": mx > 127}
-out = {"hist_rowmax": hist,
-       "owners": {k: int(v.sum()) for k, v in cls.items()},
-       "pairs": {k: int(counts[v].sum()) for k, v in cls.items()},
-       "median_pairs": {k: float(counts[v].float().median()) if int(v.sum()) else None for k, v in cls.items()}}
-print(json.dumps(out), flush=True)
+C = 8192
+buf = torch.empty((C, d, w), dtype=torch.int32, device="cuda")
+mx = np.zeros(n, np.int64)
+for o in range(0, n, C):
+    c = min(C, n - o)
+    v = t.read_counters_device(o, c, buf[:c])
+    mx[o:o + c] = v.view(c, -1).amax(dim=1).cpu().numpy()
+edges = [0, 1, 5, 8, 16, 128, 1 << 14, 1 << 40]
+h = {f"[{a},{b})": int(((mx >= a) & (mx < b)).sum()) for a, b in zip(edges[:-1], edges[1:])}
+print(json.dumps({"rowmax_hist": h, "le7": int((mx <= 7).sum()), "le4": int((mx <= 4).sum())}))
