@@ -1425,7 +1425,8 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     TimedScope ts(h, "topk_all_multi_rows");
     // chunk: a slab of qc rows offers qc similarities to every S list, so a
     // chunk must leave room in a list compacted to cap - qc entries
-    int64_t chunk = std::min<int64_t>(cap / 2, slab_rows_for(n));
+    // (the lists are offered the slab cap/2 rows at a time: multi_rows_slab_offer)
+    int64_t chunk = getenv("CMS_M_SMALL") ? std::min<int64_t>(cap / 2, slab_rows_for(n)) : multi_slab_rows(h, n);
     if (const char* e = getenv("CMS_M_CHUNK")) chunk = std::max<int64_t>(128, std::min<int64_t>(chunk, atoi(e)));
     for (int64_t m0 = (int64_t)shard * chunk; m0 < nm; m0 += (int64_t)nshards * chunk) {
       const int64_t qc = std::min<int64_t>(chunk, nm - m0);

@@ -450,6 +450,8 @@ struct TopQuery {
 int launch_top_k(cms_handle* h, const double* slab, const std::vector<TopQuery>& qs, int32_t k, const int64_t* d_perm,
                  int64_t* d_ids, double* d_scores, int32_t* d_counts);
 int64_t slab_rows_for(int64_t n);
+// slab rows of one multi-limb chunk of the all-pairs job (memory permitting, up to 4096 at 1M)
+int64_t multi_slab_rows(cms_handle* h, int64_t n);
 // ---- cms_f64.hip (CMS_COUNTER_F64) ----
 int f64_ingest_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val);
 int f64_ingest_coo_host(cms_handle* h, const int64_t* owner, const int64_t* key, const float* val, int64_t np);

@@ -761,15 +761,36 @@ int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t
   std::vector<TopQuery> qs;
   for (int64_t p = m0; p < m0 + qc; ++p) qs.push_back(TopQuery{p - m0, p, h->h_perm[p]});
   if ((rc = launch_top_k(h, slab, qs, k, cosine_perm_device(h), d_ids, d_scores, d_counts))) return rc;
-  // and the same similarities for the columns' lists
+  // and the same similarities for the columns' lists, cap/2 slab rows at a
+  // time: each part offers at most that many entries to a list compacted to
+  // cap - part first (a slab may hold more rows than a list has room for)
   if (c1 > c0) {
-    if ((rc = cand_compact(h, cb, c0, c1 - c0, (uint32_t)(cb.cap - qc), k))) return rc;
-    const unsigned g1 = (unsigned)std::min<int64_t>((c1 - c0 + 255) / 256, 8192);
-    hipLaunchKernelGGL(k_slab_offer, dim3(g1), dim3(256), 0, h->stream, slab, n, m0, qc, c0, c1, cb.thr, cb.ccnt,
-                       cb.cidx, cb.cval, cb.cap);
-    CMS_HIP(hipGetLastError());
+    const int64_t part = std::max<int64_t>(1, cb.cap / 2);
+    for (int64_t s0 = 0; s0 < qc; s0 += part) {
+      const int64_t pc = std::min(part, qc - s0);
+      if ((rc = cand_compact(h, cb, c0, c1 - c0, (uint32_t)(cb.cap - pc), k))) return rc;
+      const unsigned g1 = (unsigned)std::min<int64_t>((c1 - c0 + 255) / 256, 8192);
+      hipLaunchKernelGGL(k_slab_offer, dim3(g1), dim3(256), 0, h->stream, slab + s0 * n, n, m0 + s0, pc, c0, c1,
+                         cb.thr, cb.ccnt, cb.cidx, cb.cval, cb.cap);
+      CMS_HIP(hipGetLastError());
+    }
   }
   return CMS_OK;
+}
+
+// Slab rows for the multi-limb rows of the all-pairs job: each chunk streams
+// the whole single-limb image once, so as many rows as memory allows -- up to
+// 4096 at 1M owners (32 GiB), never fewer than the general slab budget, and
+// leaving 6 GiB of the device free.
+int64_t multi_slab_rows(cms_handle* h, int64_t n) {
+  const int64_t base = slab_rows_for(n);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return base;
+  const double have = (double)free_b + (double)h->ws_slab.bytes - 6.0 * (double)(1ULL << 30);
+  int64_t rows = (int64_t)(have / (8.0 * (double)std::max<int64_t>(1, n)));
+  rows = std::min<int64_t>(rows, ((int64_t(1) << 32) / std::max<int64_t>(1, n)));
+  rows = rows / 128 * 128;
+  return std::max(base, rows);
 }
 
 // slab budget: 2^30 fp64 similarities (8 GiB) -- 1,024 query rows at 1M owners
