@@ -1524,6 +1524,8 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
           g.si = 4;
           g.sj = 4;
           if (const char* e = getenv("CMS_SYM_RECT")) sscanf(e, "%d,%d", &g.si, &g.sj);
+          g.xchunk = 32;  // the XCDs side by side (xcd_chunk_map): int8 waves -7%, fp4 waves unchanged
+          if (const char* e = getenv("CMS_SYM_XCHUNK")) g.xchunk = std::max(0, atoi(e));
           g.thr = cb.thr;
           g.ccnt = cb.ccnt;
           g.cidx = cb.cidx;

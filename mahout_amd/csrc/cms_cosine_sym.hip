@@ -61,8 +61,18 @@ __device__ __forceinline__ uint32_t block_map(int bx, int nblk) {
   return (uint32_t)((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3));
 }
 
+// the XCDs side by side: the q-th workgroup of XCD x takes tile
+// (q / C) * 8C + x C + q % C, so at any time the 8 XCDs work on neighbouring
+// runs of C tiles (one rectangle of block pairs) -- each XCD's run shares its
+// panels in its own L2, the 8 runs share theirs in the Infinity Cache.  The
+// grid is rounded up to 8C; tiles past the end leave at once.
+__device__ __forceinline__ uint32_t xcd_chunk_map(int bx, int C) {
+  const int q = bx >> 3;
+  return (uint32_t)((q / C) * 8 * C + (bx & 7) * C + q % C);
+}
+
 template <int NSTAGE, int BK, int FMT, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
+__device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   using AccT = typename AccOf<FMT>::type;
   // NW waves in (NW/2) x 2; a wave holds TI x 3 MFMA tiles (TI = 2 at 8 waves;
   // 3 at 4 waves: one wave per SIMD with 512 registers, 6 fragments per 9 MFMAs)
@@ -83,7 +93,8 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
 
   // ---- which tile: band of waves, block pair {I, J}, A panel, B panel ----
   // a refresh's sparse pair set (tsel) is spread over the XCDs round-robin
-  const int lin = g.tsel ? (int)blockIdx.x : (int)block_map(blockIdx.x, g.nblk);
+  const int lin = g.tsel ? bx : (g.xchunk ? (int)xcd_chunk_map(bx, g.xchunk) : (int)block_map(bx, g.nblk));
+  if (lin >= g.nblk) return;
   int c, sub, wv;
   if (g.rect) {
     const int per = kSub * g.si * g.sj;
@@ -401,6 +412,11 @@ __global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
   }
 }
 
+template <int NSTAGE, int BK, int FMT, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void k_cosine_sym(SymArgs g) {
+  sym_tile<NSTAGE, BK, FMT, NW>(g, (int)blockIdx.x);
+}
+
 #ifndef CMS_SYM_NS
 #define CMS_SYM_NS 5
 #endif
@@ -434,6 +450,8 @@ int launch_sym(cms_handle* h, SymArgs g, int fmt, int64_t pair_slots) {
     g.nblk = (int32_t)(((pair_slots + g.si - 1) / g.si) * g.njc * g.si * g.sj * kSub);
   }
   if (g.nblk <= 0) return CMS_OK;
+  if (g.tsel) g.xchunk = 0;
+  int64_t grid = g.xchunk ? (g.nblk + 8LL * g.xchunk - 1) / (8LL * g.xchunk) * 8LL * g.xchunk : g.nblk;
   const size_t bytes = sym_lds_bytes(g.depth);
   static bool attr = [] {
     (void)hipFuncSetAttribute((const void*)k_cosine_sym<kSymNS, kSymBK, 0, kSymNW>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -443,8 +461,8 @@ int launch_sym(cms_handle* h, SymArgs g, int fmt, int64_t pair_slots) {
     return true;
   }();
   (void)attr;
-  if (fmt == 1) hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 1, kSymNW>), dim3(g.nblk), dim3(64 * kSymNW), bytes, h->stream, g);
-  else hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 0, kSymNW>), dim3(g.nblk), dim3(64 * kSymNW), bytes, h->stream, g);
+  if (fmt == 1) hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 1, kSymNW>), dim3((unsigned)grid), dim3(64 * kSymNW), bytes, h->stream, g);
+  else hipLaunchKernelGGL((k_cosine_sym<kSymNS, kSymBK, 0, kSymNW>), dim3((unsigned)grid), dim3(64 * kSymNW), bytes, h->stream, g);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

@@ -495,6 +495,7 @@ struct SymArgs {
   double* cval;
   int32_t cap;
   int32_t rbits;  // bits of the sketch-row index in the packed running-min state
+  int32_t xchunk; // > 0: runs of xchunk consecutive tiles per XCD, the 8 XCDs side by side (0: one contiguous range per XCD)
 };
 // the kernel can run this table's waves (unweighted, its exact dot fits the
 // packed state, LDS budget); fmt 0 int8, 1 fp4
