@@ -1069,6 +1069,7 @@ int cosine_prepare(cms_handle* h) {
     G.ls = slots[gi];
     const int per = 32 / G.ls;  // owners per 32-row block
     G.rows = (G.o1 - G.o0 + per - 1) / per * 32;
+    G.bready = false;
     if (!h->vl_ok || G.rows == 0) continue;
     CMS_HIP(G.buf.ensure((size_t)G.rows * (size_t)dw));
     TimedScope ts(h, "limb_prep");
@@ -1201,6 +1202,28 @@ static BigArgs big_base(cms_handle* h) {
   return b;
 }
 
+// The K-blocked copy of the single-limb int8 image (positions [n_multi, n))
+// that the int8 symmetric waves and k_cosine_mls read, when the device has
+// room for it next to everything else.
+static bool ensure_i8blk(cms_handle* h) {
+  if (h->i8blk_ready) return true;
+  if (getenv("CMS_NO_I8BLK")) return false;
+  const int64_t nm = h->n_hot_limb, ns = h->n - nm;
+  if (ns <= 0) return false;
+  const int64_t blocks = (ns + kImgBlk - 1) / kImgBlk;
+  const size_t bytes = (size_t)blocks * kImgBlk * (size_t)h->dw;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || free_b <= bytes + ((size_t)4 << 30) ||
+      h->ws_i8blk.ensure(bytes) != hipSuccess)
+    return false;
+  TimedScope ts(h, "limb_prep");
+  hipLaunchKernelGGL(k_i8blk_write, dim3((unsigned)(blocks * kImgBlk)), dim3(256), 0, h->stream, h->ws_limb0.as<int8_t>(),
+                     h->dw, nm, ns, h->ws_i8blk.as<int8_t>(), h->sym_sw);
+  if (hipGetLastError() != hipSuccess) return false;
+  h->i8blk_ready = true;
+  return true;
+}
+
 int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   int rc = cosine_prepare(h);
   if (rc) return rc;
@@ -1258,7 +1281,32 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
       const int ls = G.ls, per = 32 / ls;
       const int8_t* vl = G.buf.as<int8_t>();
       TimedScope ts(h, "cosine_mfma_limbs");
-      if (q0 < G.o1 && qend > G.o0 && nm < n) {  // M x S: multi-limb queries against single-limb candidates
+      if (q0 < G.o1 && qend > G.o0 && nm < n && h->i8blk_ready && mls_eligible(h) && !getenv("CMS_NO_MLS")) {
+        // M x S on k_cosine_mls (256 x 192 tiles from the K-blocked images):
+        // from the 64-row image block holding the slab's first owner of the group
+        if ((rc = vl_blk_prepare(h, gi))) return rc;
+        const int64_t oa0 = G.o0 + (std::max(q0, G.o0) - G.o0) / (2 * per) * (2 * per);
+        const int64_t vrow0 = (oa0 - G.o0) / per * 32;
+        MlsArgs m{};
+        m.A = G.bbuf.as<int8_t>() + vrow0 * dw;
+        m.a_vrows = G.rows - vrow0;
+        m.a_pos0 = oa0;
+        m.a_owners = std::min(qend, G.o1) - oa0;
+        m.B = h->ws_i8blk.as<int8_t>();
+        m.b_img0 = m.b_pos0 = nm;
+        m.b_rows = n - nm;
+        m.rs = dw;
+        m.kw = h->p.width;
+        m.depth = h->p.depth;
+        m.nsq_t = h->ws_nsq.as<double>();
+        m.n = n;
+        m.out = d_out;
+        m.ldo = n;
+        m.q0 = q0;
+        m.qcount = qc;
+        m.weighted = h->p.weighting == CMS_WEIGHTED;
+        if ((rc = launch_mls(h, m, ls))) return rc;
+      } else if (q0 < G.o1 && qend > G.o0 && nm < n) {  // M x S: multi-limb queries against single-limb candidates
         const int64_t oa0 = G.o0 + (std::max(q0, G.o0) - G.o0) / per * per;
         const int64_t blk = (oa0 - G.o0) / per;
         BigArgs g = base;
@@ -1383,7 +1431,6 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   const bool sym8 = sym_img && sym_eligible(h, 0, &rb8);
   const bool sym4 = sym_img && sym_eligible(h, 1, &rb4);
   const int32_t cap = (sym8 || sym4) ? kCandCapSym : kCandCap;
-  constexpr uint32_t kPerPass = 512;  // most offers one row takes in one pass
   DevBuf& ws = h->ws_cand;
   const size_t off_cidx = (sizeof(uint32_t) * (size_t)n + 255) & ~size_t(255);
   const size_t off_cval = off_cidx + ((sizeof(uint32_t) * (size_t)n * cap + 255) & ~size_t(255));
@@ -1422,6 +1469,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   // virtual limb rows, M x M on the MULTI tiles) gives their exact top-k AND
   // the M candidates of every single-limb row -- each (M, S) pair once
   if (nm > 0) {
+    if (ns > 0) (void)ensure_i8blk(h);  // k_cosine_mls's candidate operand (and the int8 waves')
     TimedScope ts(h, "topk_all_multi_rows");
     // chunk: a slab of qc rows offers qc similarities to every S list, so a
     // chunk must leave room in a list compacted to cap - qc entries
@@ -1467,22 +1515,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // The int8 waves read their operands from a K-blocked copy of the
     // single-limb image (a stage of a block is one contiguous run) when the
     // device has room for it next to everything else
-    bool i8blk = false;
-    if (fblk0 > 0 && !getenv("CMS_NO_I8BLK")) {
-      const int64_t blocks = (ns + kImgBlk - 1) / kImgBlk;
-      const size_t bytes = (size_t)blocks * kImgBlk * (size_t)h->dw;
-      size_t free_b = 0, total_b = 0;
-      if (h->i8blk_ready) {
-        i8blk = true;
-      } else if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > bytes + ((size_t)4 << 30) &&
-                 h->ws_i8blk.ensure(bytes) == hipSuccess) {
-        TimedScope ts(h, "limb_prep");
-        hipLaunchKernelGGL(k_i8blk_write, dim3((unsigned)(blocks * kImgBlk)), dim3(256), 0, h->stream, limb0, h->dw,
-                           nm, ns, h->ws_i8blk.as<int8_t>(), h->sym_sw);
-        CMS_HIP(hipGetLastError());
-        h->i8blk_ready = i8blk = true;
-      }
-    }
+    const bool i8blk = fblk0 > 0 && ensure_i8blk(h);
     const BigCfg scfg = big_config(h, h->sym_sw);  // the blocked images' stage depth
     // pass 0: fp4 x fp4 block pairs; pass 1: the rest (all S when no fp4 region).
     // Each pass picks its kernel: k_cosine_sym (768-row blocks) or

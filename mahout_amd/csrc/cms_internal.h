@@ -196,6 +196,8 @@ struct cms_handle {
     int32_t ls = 0;          // limb slots
     int64_t rows = 0;        // virtual rows in buf
     cms::DevBuf buf;
+    cms::DevBuf bbuf;        // the same rows K-blocked (k_cosine_mls operands), valid when bready
+    bool bready = false;
   } vl[2];
   int64_t n_f4 = 0;     // single-limb owners whose counters are all <= 4 (fp4-exact)
   int64_t f4_pos0 = 0;  // first permuted position of the fp4 image (ws_f4); n if none
@@ -500,6 +502,26 @@ struct SymArgs {
 // the kernel can run this table's waves (unweighted, its exact dot fits the
 // packed state, LDS budget); fmt 0 int8, 1 fp4
 bool sym_eligible(cms_handle* h, int fmt, int32_t* rbits);
+// ---- cms_cosine_mls.hip: multi-limb x single-limb slab block on 256 x 192 tiles ----
+struct MlsArgs {
+  const int8_t* A;      // K-blocked virtual limb rows, row 0 = the launch's first (a multiple of kImgBlk in the group)
+  int64_t a_vrows;      // rows available from A
+  int64_t a_pos0;       // permuted position of the owner of A's row 0
+  int64_t a_owners;     // owners from a_pos0 (the group's, up to the slab's end)
+  const int8_t* B;      // K-blocked int8 image of the single-limb owners, row 0 = position b_img0
+  int64_t b_img0, b_pos0, b_rows;  // candidates: positions [b_pos0, b_pos0 + b_rows), b_pos0 - b_img0 a multiple of kImgBlk
+  int64_t rs;           // bytes per image row
+  int32_t kw, depth;    // bytes per sketch row, sketch rows
+  const double* nsq_t;  // [d][n] sqrt norms by permuted position
+  int64_t n;
+  double* out;          // slab [qcount][ldo], row = position - q0, column = position
+  int64_t ldo, q0, qcount;
+  int32_t weighted;
+  int32_t tilesA, tilesB, ga, gb, nblk;  // set by launch_mls
+};
+bool mls_eligible(cms_handle* h);
+int vl_blk_prepare(cms_handle* h, int gi);
+int launch_mls(cms_handle* h, MlsArgs g, int ls);
 int launch_sym(cms_handle* h, SymArgs g, int fmt, int64_t pair_slots);
 int sym_stage_bytes();  // k_cosine_sym's K slice per stage = the images' slice width
 // ---- cms_cosine_mfma.hip ----

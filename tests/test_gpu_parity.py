@@ -718,3 +718,37 @@ def test_streaming_refresh_incremental_norms(oracle):
             assert ids[q, :cnt[q]].tolist() == rids[q, :rcnt[q]].tolist(), q
             assert same(sc[q, :cnt[q]], rsc[q, :rcnt[q]]), q
         assert t.stats()["multi_limb_owners"] > 0
+
+
+def test_multi_limb_slab_kernel_equals_reference_path(oracle):
+    """The multi-limb x single-limb slab block on k_cosine_mls (256 x 192
+    tiles, 2- and 4-limb owners) gives the same all-pairs lists as the
+    k_cosine_big path (CMS_NO_MLS=1), and the hottest owners' lists equal the
+    oracle's TopItems restatement (DoubleCountMinSketch.cosine over the
+    sketches, TopItems.getTopUsers)."""
+    import os
+    n, d, w, k = 3000, 5, 512, 50
+    items, users = zipf_stream(5000, n, 500_000, seed=17)
+    vals = np.random.Generator(np.random.PCG64(17)).integers(1, 300, size=items.size).astype(np.float32)
+    ot = oracle_table(oracle, n, d, w, 42, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        ids, sc, cnt = t.top_k_all(k)
+        st = t.stats()
+        assert st["deep_limb_owners"] > 0 and st["multi_limb_owners"] > st["deep_limb_owners"], st
+        os.environ["CMS_NO_MLS"] = "1"
+        try:
+            ids2, sc2, cnt2 = t.top_k_all(k)
+        finally:
+            del os.environ["CMS_NO_MLS"]
+        assert np.array_equal(cnt, cnt2)
+        for q in range(n):
+            assert ids[q, :cnt[q]].tolist() == ids2[q, :cnt2[q]].tolist(), q
+            assert same(sc[q, :cnt[q]], sc2[q, :cnt2[q]]), q
+        hottest = np.argsort(-ot.max(axis=(1, 2)), kind="stable")[:6]
+        for q in hottest.tolist() + [int(np.argsort(-ot.max(axis=(1, 2)))[st["multi_limb_owners"] - 1])]:
+            sims = _oracle_row_sims(oracle, ot, q)
+            eids, esc = oracle.top_users(np.arange(n), sims, k)
+            assert ids[q, :cnt[q]].tolist() == eids.tolist(), q
+            assert same(sc[q, :cnt[q]], esc), q
