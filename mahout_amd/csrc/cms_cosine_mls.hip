@@ -152,52 +152,64 @@ __global__ __launch_bounds__(512, 1) void k_cosine_mls(MlsArgs g) {
       for (int e = 0; e < 4 * OG; ++e) mn[i][j][e] = ~0ULL;
     }
 
+  // the five fragments of k-step ks of a stage
+  auto frags = [&](const unsigned char* A, int ks, i8x16* fa, i8x16* fb) {
+    const int ch = 2 * ks + (lane >> 5);
 #pragma unroll
-  for (int s = 0; s < NSTAGE - 1; ++s) issue(min(s, total - 1), s, 3);  // every iteration issues: one vmcnt count
+    for (int j = 0; j < 3; ++j)
+      fb[j] = *reinterpret_cast<const i8x16*>(A + kStageA + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
+  };
+  // k_cosine_sym's schedule (CMS_SYM_SCHED 3): the barrier between a stage's
+  // two k-steps, the next stage's first fragments read behind the second
+  // k-step's MFMAs, the slot just finished refilled at once
+  constexpr int NVB = OPA + OPB_LO;
+#pragma unroll
+  for (int s = 0; s < NSTAGE; ++s) issue(min(s, total - 1), s, 3);  // every iteration issues: one vmcnt count
+  if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 1)>();
+  else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 1)>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  i8x16 fa0[2], fb0[3];
+  frags(lds, 0, fa0, fb0);
 
   for (int s = 0; s < total; ++s) {
-    asm volatile("" ::: "memory");
-    if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 2)>();
-    else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 2)>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const unsigned char* A = lds + (s % NSTAGE) * kStage;
-    const unsigned char* B = A + kStageA;
     {
-      const int sn = min(s + NSTAGE - 1, total - 1);
+      const unsigned char* A = lds + (s % NSTAGE) * kStage;
+      i8x16 fa1[2], fb1[3];
+      frags(A, 1, fa1, fb1);
 #pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        const int ch = 2 * ks + (lane >> 5);
-        i8x16 fb[3], fa[2];
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          fb[j] = *reinterpret_cast<const i8x16*>(B + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
+        for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[i], fb0[j], acc[i][j], 0, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * 64 + i * 32 + (lane & 31), ch));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        if (ks == 0) issue(sn, s + NSTAGE - 1, 1);
+      for (int m = 0; m < 6; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (m < 5) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      constexpr int NV = OPA + OPB_LO, NF = 5, NM = 6, KS = BK / 32;
-      static_assert(NV <= NM * KS, "schedule shape");
-      __builtin_amdgcn_sched_group_barrier(0x100, NF, 0);
+      asm volatile("" ::: "memory");
+      if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 2)>();
+      else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 2)>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int sn = min(s + NSTAGE, total - 1);
+      issue(sn, s, 1);
+      frags(lds + ((s + 1) % NSTAGE) * kStage, 0, fa0, fb0);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if (ks * NM + m < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          if (ks + 1 < KS && m >= NM - 4) {
-            if (m == NM - 1) __builtin_amdgcn_sched_group_barrier(0x100, NF - 3, 0);
-            else __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-        }
+        for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[i], fb1[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (m < NVB) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (m >= 1 && m < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      issue(sn, s + NSTAGE - 1, 2);
+      issue(sn, s, 2);
     }
     const int r = s / cstages;
     if (s - r * cstages != cstages - 1) continue;

@@ -38,7 +38,9 @@
 #include "cms_mfma.h"
 
 #ifndef CMS_SYM_SCHED
-#define CMS_SYM_SCHED 2  // 0: refill loads before the MFMAs, 1: interleaved with them, 2: also the next k-step's fragments
+// 0: refill loads before the MFMAs, 1: interleaved with them, 2: also the next
+// k-step's fragments, 3: the barrier between the two k-steps (f4 -4 %, i8 -6 % over 2)
+#define CMS_SYM_SCHED 3
 #endif
 
 namespace cms {
@@ -222,6 +224,34 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
       }
   const uint32_t rbits = (uint32_t)g.rbits, rmask = (1u << rbits) - 1u;
 
+  // the five fragments of k-step ks of a stage
+  auto frags = [&](const unsigned char* A, int ks, i8x16* fa, i8x16* fb) {
+    const int ch = 2 * ks + (lane >> 5);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      fb[j] = *reinterpret_cast<const i8x16*>(A + kStageA + lds_off_bk<BK>(wc * 96 + j * 32 + (lane & 31), ch));
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+      fa[i] = *reinterpret_cast<const i8x16*>(A + lds_off_bk<BK>(wr * WROWS + i * 32 + (lane & 31), ch));
+  };
+#if CMS_SYM_SCHED == 3
+  // Barrier between a stage's two k-steps: the first k-step's MFMAs run
+  // through the wait for the NEXT stage, whose first fragments are then read
+  // behind the second k-step's MFMAs -- no fragment-read bubble after the
+  // barrier, and the slot just finished is refilled at once (every slot of
+  // the ring is in flight or being read).
+  static_assert(BK == 64, "two k-steps per stage");
+  constexpr int NVB = OPA + OPB_LO;
+#pragma unroll
+  for (int s = 0; s < NSTAGE; ++s) issue(min(s, total - 1), s, 3);  // every iteration issues: one vmcnt count
+  if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 1)>();
+  else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 1)>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  i8x16 fa0[TI], fb0[3];
+  frags(lds, 0, fa0, fb0);
+#else
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
 #if CMS_SYM_SCHED
@@ -229,8 +259,47 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #else
     if (s < total) issue(s, s, 3);
 #endif
+#endif
 
   for (int s = 0; s < total; ++s) {
+#if CMS_SYM_SCHED == 3
+    {
+      const unsigned char* A = lds + (s % NSTAGE) * kStage;
+      i8x16 fa1[TI], fb1[3];
+      frags(A, 1, fa1, fb1);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa0[i], fb0[j], acc[i][j]);
+#pragma unroll
+      for (int m = 0; m < TI * 3; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (m < TI + 3) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      // stage s+1 landed (the NSTAGE-2 younger stages stay in flight); every
+      // wave's reads of slot s are done past the barrier
+      asm volatile("" ::: "memory");
+      if (opb == OPB_HI) wait_vmcnt<(OPA + OPB_HI) * (NSTAGE - 2)>();
+      else wait_vmcnt<(OPA + OPB_LO) * (NSTAGE - 2)>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int sn = min(s + NSTAGE, total - 1);
+      issue(sn, s, 1);
+      frags(lds + ((s + 1) % NSTAGE) * kStage, 0, fa0, fb0);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa1[i], fb1[j], acc[i][j]);
+#pragma unroll
+      for (int m = 0; m < TI * 3; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (m < NVB) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        if (m >= 1 && m < TI + 4) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      issue(sn, s, 2);
+    }
+#else
     // stage s landed: at most the (NSTAGE-2) younger stages stay in flight
     asm volatile("" ::: "memory");
 #if CMS_SYM_SCHED
@@ -311,6 +380,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
     }
 #endif
+#endif  // CMS_SYM_SCHED == 3
     const int r = s / cstages;
     if (s - r * cstages != cstages - 1) continue;
     // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
