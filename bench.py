@@ -556,6 +556,11 @@ def csr_prefix_on_device(items, users, n_owners):
     return csr_on_device(it, us, n_owners)
 
 
+def hbm_used_gb(device):
+    free, total = torch.cuda.mem_get_info(device)
+    return (total - free) / 1e9
+
+
 def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
     """Config 4 on the config-3 table the headline just built: mostSimilar
     top-100 for EVERY one of the 1M items through cms_top_k_all -- each
@@ -578,18 +583,22 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
     _, _, cnt = t.top_k_all_device(k)  # lists stay in HBM (no 1.6 GB host copy in the timed job)
     bar()
     wall = max_over_ranks(time.perf_counter() - t0)
+    used_gb = max_over_ranks(hbm_used_gb(device))  # operand images, slab, candidate lists still held
     cnt = cnt.cpu().numpy()
     tm = {name: t.timing(name)[0] for name in ["topk_all_multi_rows", "topk_all_limbs", "topk_all_waves",
                                                "topk_allgather", "topk_merge"]}
     waves_ms, waves_n = t.timing("topk_all_waves")
     f4_ms, f4_n = t.timing("topk_all_waves_f4")
     i8_ms, i8_n = t.timing("topk_all_waves_i8")
+    ml_ms, ml_n = t.timing("cosine_mfma_limbs")  # k_cosine_mls: the multi-limb x single-limb slab blocks
     t.set_timing(False)
     st = t.stats()
     stream = None
     if world == 1 or args.stream_refresh_multi:
         stream = streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks)
     nm = max(0, int(st["multi_limb_owners"]))
+    ndeep = max(0, int(st["deep_limb_owners"]))
+    ml_hw_ops = (4 * ndeep + 2 * (nm - ndeep)) * (n - nm) * 2 * d * w / world
     uniq = n * (n - 1) / 2
     alg_ops = uniq * 2 * d * w  # F = n(n-1)/2 * 2dw
     ns = n - nm
@@ -604,9 +613,10 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
     job_f4 = nf * (nf - 1) / 2 * 2 * d * w
     job_peak = alg_ops / (job_f4 / FP4_MFMA_PEAK_TOPS + (alg_ops - job_f4) / INT8_MFMA_PEAK_TOPS)
     wave_ach = wave_ops / (waves_ms * 1e-3) / 1e12 if waves_ms else None
-    cos_traffic = pmc_traffic("void cms::k_cosine_sym<5, 64, 1>", "cosine_pmc_summary.json")
-    cos_pmc = pmc_record("void cms::k_cosine_sym<5, 64, 1>", "cosine_pmc_summary.json")
-    cos_pmc8 = pmc_record("void cms::k_cosine_sym<5, 64, 0>", "cosine_pmc_summary.json")
+    cos_traffic = pmc_traffic("void cms::k_cosine_sym<5, 64, 1, 8>", "cosine_pmc_summary.json")
+    cos_pmc = pmc_record("void cms::k_cosine_sym<5, 64, 1, 8>", "cosine_pmc_summary.json")
+    cos_pmc8 = pmc_record("void cms::k_cosine_sym<5, 64, 0, 8>", "cosine_pmc_summary.json")
+    cos_pmcm = pmc_record("void cms::k_cosine_mls<2>", "cosine_pmc_summary.json")
     return {
         "workload": f"config 4: top-{k} most similar items for every one of the {n} items of the config-3 table "
                     f"(d={d} w={w}; {world} GPU(s), pairs split over the ranks, partial lists all-gathered)",
@@ -614,6 +624,7 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
         "unique_item_pair_cosines_per_s": uniq / wall,
         "wall_s": wall,
         "first_job_s": first_job_s,
+        "hbm_used_gb": used_gb,
         "algorithmic_TOPS": alg_ops / wall / 1e12,
         "frac_int8_peak_per_gpu": alg_ops / wall / 1e12 / INT8_MFMA_PEAK_TOPS / world,
         "mixed_peak_TOPS": job_peak,
@@ -640,6 +651,12 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
                                              f"{INT8_MFMA_PEAK_TOPS:.0f} TOP/s for the rest, weighted by their ops",
                                "frac": wave_ach / wave_peak if wave_ach and wave_peak else None,
                                "ms": waves_ms, "launches": waves_n},
+        "multi_limb_block": {"kernel": "k_cosine_mls<LS> (multi-limb x single-limb slab blocks, 256 x 192 tiles)",
+                             "ms": ml_ms, "launches": ml_n,
+                             "hw_int8_ops": ml_hw_ops,
+                             "hw_frac_int8_peak": ml_hw_ops / (ml_ms * 1e-3) / 1e12 / INT8_MFMA_PEAK_TOPS if ml_ms else None,
+                             "hw_ops_basis": "limb slots x single-limb owners x 2dw (each limb is an int8 pass)",
+                             "pmc_mfma_busy_frac": cos_pmcm.get("mfma_busy_frac"), "pmc_l2_hit": cos_pmcm.get("l2_hit")},
         "fp4_owners": nf,
         "timing_ms_rank0": tm,
         "multi_limb_owners": nm, "full_lists": int((cnt == k).sum()), "topk_redo_rows": int(st["topk_redo"]),
@@ -1031,6 +1048,11 @@ def main():
                                             f"{result['cpu_baseline']['cores']} threads")
         result["vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
         del off, ckeys
+    # device memory in use on the busiest rank (hipMemGetInfo: the library's
+    # allocations and torch's), with this rank's input stream still resident
+    result["memory"] = {"total_gb": torch.cuda.mem_get_info(device)[1] / 1e9,
+                        "used_after_ingest_gb": max_over_ranks(hbm_used_gb(device)),
+                        "basis": "max over ranks of (total - free) from hipMemGetInfo"}
     cos_cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_cosine_1m:
         cos_cpu = cosine_cpu_baseline(items, users, n, d, w)
@@ -1043,6 +1065,7 @@ def main():
             cos["cpu_baseline"] = cos_cpu
             if rank == 0:
                 result["cosine"] = cos
+                result["memory"]["used_during_cosine_gb"] = cos.get("hbm_used_gb")
         except Exception as e:  # the headline line must still be printed
             if rank == 0:
                 result["cosine"] = {"error": f"{type(e).__name__}: {e}"}

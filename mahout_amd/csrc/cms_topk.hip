@@ -732,20 +732,29 @@ int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t
 // Offer the similarities of slab rows (positions [m0, m0+qc)) to the lists
 // of the columns [c0, c1): one thread per column walks the slab rows in order
 // (no contention: a list has one writer here).
-__global__ void k_slab_offer(const double* slab, int64_t ld, int64_t m0, int64_t qc, int64_t c0, int64_t c1,
-                             const double* thr, uint32_t* ccnt, uint32_t* cidx, double* cval, int32_t cap) {
+__global__ void k_slab_offer(const double* __restrict__ slab, int64_t ld, int64_t m0, int64_t qc, int64_t c0, int64_t c1,
+                             const double* __restrict__ thr, uint32_t* __restrict__ ccnt, uint32_t* __restrict__ cidx,
+                             double* __restrict__ cval, int32_t cap) {
   for (int64_t c = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < c1; c += (int64_t)gridDim.x * blockDim.x) {
     const double t = thr[c];
     uint32_t cnt = ccnt[c];
-    for (int64_t m = 0; m < qc; ++m) {
-      const double v = slab[m * ld + c];
-      if (v != v || v < t || m0 + m == c) continue;
+    auto offer = [&](int64_t m, double v) {
+      if (v != v || v < t || m0 + m == c) return;
       if (cnt < (uint32_t)cap) {
         cidx[c * cap + cnt] = (uint32_t)(m0 + m);
         cval[c * cap + cnt] = v;
       }
       ++cnt;
+    };
+    int64_t m = 0;
+    for (; m + 8 <= qc; m += 8) {  // eight rows' loads in flight per thread
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(m + u) * ld + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) offer(m + u, v[u]);
     }
+    for (; m < qc; ++m) offer(m, slab[m * ld + c]);
     ccnt[c] = cnt;
   }
 }
@@ -766,13 +775,14 @@ int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t
   // cap - part first (a slab may hold more rows than a list has room for)
   if (c1 > c0) {
     const int64_t part = std::max<int64_t>(1, cb.cap / 2);
-    for (int64_t s0 = 0; s0 < qc; s0 += part) {
+    for (int64_t s0 = 0; s0 < qc;) {
       const int64_t pc = std::min(part, qc - s0);
       if ((rc = cand_compact(h, cb, c0, c1 - c0, (uint32_t)(cb.cap - pc), k))) return rc;
       const unsigned g1 = (unsigned)std::min<int64_t>((c1 - c0 + 255) / 256, 8192);
       hipLaunchKernelGGL(k_slab_offer, dim3(g1), dim3(256), 0, h->stream, slab + s0 * n, n, m0 + s0, pc, c0, c1,
                          cb.thr, cb.ccnt, cb.cidx, cb.cval, cb.cap);
       CMS_HIP(hipGetLastError());
+      s0 += pc;
     }
   }
   return CMS_OK;
