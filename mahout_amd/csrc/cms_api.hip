@@ -396,7 +396,7 @@ void cms_destroy(cms_handle* h) {
     if (b) (void)hipFree(b);
   if (h->h_pin) (void)hipHostFree(h->h_pin);
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
-                  &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_csr_hi, &h->ws_hotpart, &h->ws_hist, &h->ws_small, &h->ws_partials,
+                  &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_csr_hi, &h->ws_hotpart, &h->ws_hist, &h->ws_small, &h->ws_partials, &h->ws_slicepart,
                   &h->ws_hot, &h->ws_query, &h->ws_out, &h->ws_limb0, &h->ws_limbmeta, &h->ws_limbhot,
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
@@ -712,7 +712,7 @@ int cms_release_scratch(cms_handle* h) {
   Guard g(h);
   CMS_HIP(hipStreamSynchronize(h->stream));
   DevBuf* ws[] = {&h->ws_in_row, &h->ws_in_key, &h->ws_in_val, &h->ws_p1_row, &h->ws_p1_key, &h->ws_p1_val,
-                  &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_csr_hi, &h->ws_hotpart, &h->ws_hist, &h->ws_hot, &h->ws_query,
+                  &h->ws_csr_key, &h->ws_csr_val, &h->ws_csr_off, &h->ws_csr_hi, &h->ws_hotpart, &h->ws_hist, &h->ws_hot, &h->ws_slicepart, &h->ws_query,
                   &h->ws_out, &h->ws_slab, &h->ws_topq, &h->ws_tiles, &h->ws_cand, &h->ws_srow,
                   &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked, &h->rf_ids, &h->rf_sc, &h->rf_cnt,
                   &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};

@@ -32,7 +32,7 @@ namespace cms {
 struct HotInfo {
   int64_t row;
   int32_t nslices;
-  int32_t pad;
+  int32_t e0;  // first extra slice (extra_map index) of the row
 };
 
 #ifndef CMS_KEY_REGS
@@ -67,7 +67,7 @@ __global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nro
           atomicAdd(reinterpret_cast<unsigned long long*>(counters), ((unsigned long long)(ns - 1) << 32) | 1ULL);
       hidx = (uint32_t)old;
       e0 = (uint32_t)(old >> 32);
-      hot[hidx] = HotInfo{r, ns, 0};
+      hot[hidx] = HotInfo{r, ns, (int32_t)e0};
       row_hot[r] = (int32_t)hidx;
       for (int d = 0; d < depth; ++d) norm[r * depth + d] = 0;
       rowmax[r] = 0;
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
     TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate,
     int slices_done, const uint64_t* bound, int forms, int skip_untouched, int32_t* hidx_w, uint32_t* cbound,
-    const int32_t* rows_list, const uint32_t* rows_cnt) {
+    const int32_t* rows_list, const uint32_t* rows_cnt, uint16_t* part, int64_t hcap) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w] u32, or a byte-form owner's [d][w] u8
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -197,6 +197,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
   uint32_t* dst = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
   uint16_t* dst16 = tv.t16 + row * dw;
   const bool load_old = accumulate && !atomic_mode;
+  // slices with partial rows (part: unit increments, slice << frac_bits <
+  // 2^16): a slice writes its d x w counts as a u16 partial row with plain
+  // 16-B stores (slice 0 at the row's hot index, extra slice e at hcap + e);
+  // k_hot_reduce sums them into the slot row -- no global atomics here
+  const bool to_part = atomic_mode && part != nullptr;
+  if (to_part) {
+    dst16 = part + (blockIdx.x < emax ? hcap + (int64_t)blockIdx.x : (int64_t)row_hot[row]) * dw;
+    dst = nullptr;
+  }
   if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
   if (tid == 0) {
     s_mass = 0ULL;
@@ -290,14 +299,14 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
     // ---- write-out of row d, zero/load the slot for row d+1, sum of squares ----
     const int64_t rofs = (int64_t)d * w;
     const bool more = load_old && d + 1 < hp.depth;
-    if (atomic_mode && two) {  // paired slice rows: low halves row d, high halves row d + 1
+    if (atomic_mode && two && !to_part) {  // paired slice rows: low halves row d, high halves row d + 1
       for (int j = tid; j < w; j += kBuildThreads) {
         const uint32_t v = lds[j];
         lds[j] = 0u;
         if (v & 0xFFFFu) atomicAdd(dst + rofs + j, v & 0xFFFFu);
         if (v >> 16) atomicAdd(dst + rofs + w + j, v >> 16);
       }
-    } else if (atomic_mode) {  // slices of a split row: always a hot (u32) row
+    } else if (atomic_mode && !to_part) {  // slices of a split row: always a hot (u32) row
       for (int j = tid; j < w; j += kBuildThreads) {
         uint32_t v = lds[j];
         lds[j] = 0u;
@@ -921,6 +930,95 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
   }
 }
 
+// The split rows' slot counters from their slices' u16 partial rows (slice 0
+// at part[h], slice s >= 1 at part[hcap + e0 + s - 1]), plus the old counters
+// when accumulating; the same pass derives the rows' sums of squares and
+// largest counter (k_hot_norms' job).  Block (h, sketch row, 512-counter
+// chunk): thread t sums 8 counters (one 16-B load per slice) over the slices
+// s = t / 64 mod 4, the four waves' sums meet in LDS.  Counter sums are
+// bounded by the row mass (< 2^32, checked by the build).
+constexpr int kRedChunk = 512;
+__global__ __launch_bounds__(256) void k_hot_reduce(const HotInfo* hot, const uint32_t* counters, HashParams hp,
+                                                    const uint16_t* part, int64_t hcap, TableView tv, int accumulate,
+                                                    uint64_t* norm, uint32_t* rowmax) {
+  __shared__ uint4 red[3][64][2];
+  __shared__ uint64_t sred[4];
+  const uint32_t nhot = counters[0];
+  const int w = (int)hp.width;
+  const int64_t dw = tv.dw;
+  const int d = blockIdx.y;
+  const int j0 = blockIdx.z * kRedChunk + (threadIdx.x & 63) * 8;  // this thread's 8 counters
+  const int q = threadIdx.x >> 6;
+  for (uint32_t hb = blockIdx.x; hb < nhot; hb += gridDim.x) {
+    const HotInfo hi = hot[hb];
+    const int64_t off = (int64_t)d * w + j0;
+    uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (j0 < w) {
+      auto add = [&](const u32x4_t v) {
+        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          s[2 * c] += x[c] & 0xFFFFu;
+          s[2 * c + 1] += x[c] >> 16;
+        }
+      };
+      auto src = [&](int sl) {
+        const int64_t pi = sl == 0 ? (int64_t)hb : hcap + hi.e0 + sl - 1;
+        return reinterpret_cast<const u32x4_t*>(part + pi * dw + off);
+      };
+      int sl = q;
+      for (; sl + 12 < hi.nslices; sl += 16) {  // four loads in flight
+        const u32x4_t a = __builtin_nontemporal_load(src(sl)), b = __builtin_nontemporal_load(src(sl + 4));
+        const u32x4_t c = __builtin_nontemporal_load(src(sl + 8)), e = __builtin_nontemporal_load(src(sl + 12));
+        add(a);
+        add(b);
+        add(c);
+        add(e);
+      }
+      for (; sl < hi.nslices; sl += 4) add(__builtin_nontemporal_load(src(sl)));
+    }
+    if (q > 0) {
+      red[q - 1][threadIdx.x & 63][0] = make_uint4(s[0], s[1], s[2], s[3]);
+      red[q - 1][threadIdx.x & 63][1] = make_uint4(s[4], s[5], s[6], s[7]);
+    }
+    __syncthreads();
+    uint64_t sq = 0;
+    uint32_t vmax = 0;
+    if (q == 0 && j0 < w) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const uint4 a = red[p][threadIdx.x][0], b = red[p][threadIdx.x][1];
+        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+        s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+      }
+      uint4* dst = reinterpret_cast<uint4*>(tv.hot + (int64_t)tv.hidx[hi.row] * dw + off);
+      if (accumulate) {
+        const uint4 a = dst[0], b = dst[1];
+        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+        s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+      }
+      dst[0] = make_uint4(s[0], s[1], s[2], s[3]);
+      dst[1] = make_uint4(s[4], s[5], s[6], s[7]);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        sq = sat_add(sq, (uint64_t)s[c] * s[c]);
+        vmax = max(vmax, s[c]);
+      }
+    }
+    if (q == 0) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+      sq = wave_sum_u64_sat(sq);
+      if (threadIdx.x == 0) {
+        if (vmax) atomicMax(&rowmax[hi.row], vmax);
+        if (sq > (1ULL << 60)) sq = 1ULL << 60;
+        if (sq) atomicAdd((unsigned long long*)&norm[hi.row * hp.depth + d], (unsigned long long)sq);
+      }
+    }
+    __syncthreads();  // red[] is rewritten by the next row
+  }
+}
+
 int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,
                int64_t slice, uint64_t* bound, uint8_t* force) {
   const int64_t n = h->n;
@@ -1000,6 +1098,21 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                        counters, h->d_norm, h->d_rowmax, h->p.depth);
     CMS_HIP(hipGetLastError());
   }
+  // EXPERIMENT (CMS_SLICE_PARTIALS=1, read per call): split rows' slices
+  // write u16 partial rows (plain 16-B stores; unit increments, so a slice
+  // counts at most kSlice << frac_bits < 2^16 per bucket) that k_hot_reduce
+  // sums into the slot rows, instead of adding into them with global atomics.
+  // Measured at config 3 (scripts/ab_env.sh): k_build_rows 8.40 -> 8.18 ms,
+  // but the reduction pass costs 0.53 ms against k_hot_norms' 0.18 ms (it
+  // re-reads 1.9 GB of partials), so the step is 0.13 ms slower; bit-exact
+  // (tests/test_gpu_parity.py runs both).
+  const bool use_part = getenv("CMS_SLICE_PARTIALS") != nullptr && !d_val && (h->p.width % 8) == 0 &&
+                        (kSlice << h->hp.frac_bits) < 65536;
+  uint16_t* part = nullptr;
+  if (use_part) {
+    CMS_HIP(h->ws_slicepart.ensure(sizeof(uint16_t) * (size_t)(max_hot + emax) * (size_t)h->dw));
+    part = h->ws_slicepart.as<uint16_t>();
+  }
   // fresh builds may store byte forms: the whole [d][w] byte image in LDS
   const int forms = h->forms_ok && !accumulate && (size_t)h->dw <= kFormLdsMax ? 1 : 0;
   const int skip_untouched = accumulate && h->norms_valid ? 1 : 0;
@@ -1016,7 +1129,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     // Measured no faster (config 3 build 11.9 -> 12.5 ms, config 2 equal), so
     // the slices stay in k_build_rows (d/2 passes over their keys).
     const size_t slice_lds = (size_t)h->p.depth * (size_t)h->p.width * 2;
-    const int slices_done = !d_val && (h->p.width % 2) == 0 && (kSlice << h->hp.frac_bits) < 65536 &&
+    const int slices_done = !use_part && !d_val && (h->p.width % 2) == 0 && (kSlice << h->hp.frac_bits) < 65536 &&
                             slice_lds <= 96 * 1024 && h->side_stream && getenv("CMS_SLICES_SIDE");
     if (slices_done) {
       static bool attr = [] {
@@ -1075,7 +1188,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       hipLaunchKernelGGL(kern, dim3((unsigned)(emax + nslot)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                          d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
                          h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
-                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)slot_list, (const uint32_t*)lcnt);
+                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)slot_list, (const uint32_t*)lcnt, part,
+                         max_hot);
       CMS_HIP(hipGetLastError());
       if (side != h->stream) {
         CMS_HIP(hipEventRecord(h->ev_join2, side));
@@ -1085,16 +1199,24 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
                          d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
                          h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
-                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)nullptr, (const uint32_t*)nullptr);
+                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)nullptr, (const uint32_t*)nullptr, part,
+                         max_hot);
       CMS_HIP(hipGetLastError());
     }
     if (slices_done) CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join, 0));  // the slices have landed
   }
   {
     TimedScope ts(h, "hot_norms");
-    dim3 grid((unsigned)std::min<int64_t>(max_hot, 256), (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
-    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
-                       h->d_rowmax);
+    if (use_part) {
+      dim3 grid((unsigned)std::min<int64_t>(max_hot, 1024), (unsigned)h->p.depth,
+                (unsigned)((h->p.width + kRedChunk - 1) / kRedChunk));
+      hipLaunchKernelGGL(k_hot_reduce, grid, dim3(256), 0, h->stream, hot, counters, h->hp, part, max_hot, h->tview(),
+                         accumulate, h->d_norm, h->d_rowmax);
+    } else {
+      dim3 grid((unsigned)std::min<int64_t>(max_hot, 256), (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
+      hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
+                         h->d_rowmax);
+    }
     CMS_HIP(hipGetLastError());
   }
   h->empty = false;

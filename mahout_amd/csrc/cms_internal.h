@@ -229,6 +229,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off, ws_csr_hi;
   cms::DevBuf ws_hotpart;  // hot-owner routing of the partition: slot keys [1024] u64, sample counts [n] u32
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
+  cms::DevBuf ws_slicepart;  // row build: u16 [hot + extra slices][d*w] partial rows of split owners (k_hot_reduce)
   cms::DevBuf ws_query, ws_out, ws_srow, ws_f4, ws_i8blk;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 

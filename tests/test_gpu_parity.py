@@ -299,7 +299,13 @@ def test_owner_ids_and_errors(oracle):
         assert abs(t.similarity(3, 3) - 1.0) < 1e-15
 
 
-def test_accumulate_equals_single_batch(oracle):
+@pytest.mark.parametrize("partials", [False, True])
+def test_accumulate_equals_single_batch(oracle, monkeypatch, partials):
+    """Split rows' slices add into their slot rows with global atomics, or
+    (CMS_SLICE_PARTIALS, the experiment) write partial rows that k_hot_reduce
+    sums; both bit-exact, fresh and accumulating."""
+    if partials:
+        monkeypatch.setenv("CMS_SLICE_PARTIALS", "1")
     n, d, w = 1500, 4, 512
     items, users = zipf_stream(30000, n, 800_000, seed=21)
     with SketchTable(n, depth=d, width=w, seed=42) as t:
@@ -308,7 +314,17 @@ def test_accumulate_equals_single_batch(oracle):
         t.ingest(items[700_000:], users[700_000:])       # atomic path (small batch)
         t.finalize()
         got = t.read_counters()
-    assert same(got, oracle_table(oracle, n, d, w, 42, items, users))
+        exp = oracle_table(oracle, n, d, w, 42, items, users)
+        assert same(got, exp)
+        # the hottest owners were split into slices in both builds (their slot
+        # rows summed from slice partial rows, old counters included the second
+        # time): their norms show in every similarity of their rows
+        cnt = np.bincount(items[:400_000], minlength=n)
+        assert cnt.max() > 2 * 8192
+        for q in np.argsort(cnt)[-3:]:
+            e = oracle.similarities_row(exp, int(q))
+            e[q] = oracle.cosine_cm(exp[q], exp[q])
+            assert same(t.similarities(int(q), np.arange(n)), e), q
 
 
 def _oracle_row_sims(oracle, table, q, weighted=False):
