@@ -343,8 +343,12 @@ int cms_read_counters_device(cms_handle* h, int64_t row_begin, int64_t row_count
  * p->depth / p->width are ignored.  cms_similarity(ies), cms_point_query,
  * cms_estimate_preferences, cms_most_similar, cms_top_k_rows, cms_top_k_all
  * and cms_write_similar_items work as for fixed shapes; the COO ingests,
- * cms_read_counters, cms_hash_keys, cms_top_k_all_partial and cms_comm_init
- * return CMS_E_STATE (per-owner mode is single-GPU). */
+ * cms_read_counters, cms_hash_keys and cms_top_k_all_partial return
+ * CMS_E_STATE.  Several GPUs: every rank ingests the whole DataModel (u1's
+ * preferences are hashed at each candidate's shape) and, after
+ * cms_comm_init / cms_comm_init_transport, cms_top_k_all splits the QUERY
+ * rows over the ranks (256-row chunks round-robin) and all-gathers the lists,
+ * so every rank returns the single-GPU answer. */
 int cms_create_per_owner(const cms_params* p, cms_handle** out);
 /* CountMinSketchConfig(q).configure(dataModel) -> computeConfig on the GPU:
  * per owner n = its CSR row length (PreferenceArray.length()), u = num_keys

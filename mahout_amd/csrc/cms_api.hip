@@ -736,7 +736,6 @@ int cms_comm_unique_id(void* out) {
 int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t world) {
   if (!h || !unique_id) return set_error(CMS_E_PARAM, "null argument");
   if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
-  if (int rc0 = refuse_per_owner(h, "cms_comm_init")) return rc0;
   if (h->f64 && world > 1)
     return set_error(CMS_E_STATE, "fp64 counters are single-GPU: shard sums would not round in the reference's order");
   Guard g(h);
@@ -760,7 +759,6 @@ int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allr
   if (!h) return set_error(CMS_E_PARAM, "null handle");
   if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
   if (world > 1 && (!allreduce || !allgather)) return set_error(CMS_E_PARAM, "null transport function");
-  if (int rc0 = refuse_per_owner(h, "cms_comm_init_transport")) return rc0;
   if (h->f64 && world > 1)
     return set_error(CMS_E_STATE, "fp64 counters are single-GPU: shard sums would not round in the reference's order");
   Guard g(h);

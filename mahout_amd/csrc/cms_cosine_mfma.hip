@@ -1398,8 +1398,20 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
 int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts, int32_t shard,
               int32_t nshards) {
   if (h->per_owner) {  // asymmetric similarities: every row scans every candidate
-    if (nshards != 1) return set_error(CMS_E_STATE, "per-owner shapes: all-pairs top-k is single-GPU");
-    return top_k_rows(h, 0, h->n, k, d_ids, d_scores, d_counts);
+    if (nshards == 1) return top_k_rows(h, 0, h->n, k, d_ids, d_scores, d_counts);
+    // G ranks: every rank holds the whole DataModel (u1's preferences are
+    // hashed at each candidate's shape), so the job shards by QUERY rows --
+    // chunks of kPoShardRows rows round-robin (a Zipf model's costly rows
+    // spread over the ranks); the other rows' lists stay empty (count 0) and
+    // the collective merge (top_k_all_job) takes each row's list from the
+    // rank that computed it
+    constexpr int64_t kPoShardRows = 256;
+    CMS_HIP(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * h->n, h->stream));
+    for (int64_t r0 = (int64_t)shard * kPoShardRows; r0 < h->n; r0 += (int64_t)nshards * kPoShardRows) {
+      const int64_t rc0 = std::min<int64_t>(kPoShardRows, h->n - r0);
+      if (int rc = top_k_rows(h, r0, rc0, k, d_ids + r0 * k, d_scores + r0 * k, d_counts + r0)) return rc;
+    }
+    return CMS_OK;
   }
   if (h->f64) {  // fp64 counters: the exact sequential kernels, one slab of query rows at a time
     if (nshards == 1) return top_k_rows(h, 0, h->n, k, d_ids, d_scores, d_counts);

@@ -1,0 +1,22 @@
+"""Per-owner shapes (CosineCM + CountMinSketchConfig) beyond config 1: the
+config-2 stream (1M users x 100K items, 50M pairs) as the transposed
+DataModel, CountMinSketchConfig(q=1) for all 100K items, then mostSimilar
+top-100 for blocks of query rows over all 100K candidates.
+
+usage: python scripts/po_scale_probe.py [rows_per_block]"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import csr_on_device, per_owner_scale  # noqa: E402
+from mahout_amd.synth import zipf_stream_torch  # noqa: E402
+
+rows = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+items, users = zipf_stream_torch(1_000_000, 100_000, 50_000_000, seed=20261016, device="cuda")
+t0 = time.perf_counter()
+print(json.dumps(per_owner_scale(items, users, 100_000, 1_000_000, rows)), flush=True)
+print(f"total {time.perf_counter() - t0:.1f} s", file=sys.stderr)

@@ -133,3 +133,74 @@ def test_transport_merge_delta_exchange_collective_top_k(world, case):
         n, d, w = case[:3]
         assert 0 < r["merge_bytes"] < n * d * w * 4  # the packed merge moved less than the u32 table
         assert 0 < r["delta_bytes"] < n * d * w * 4  # the exchange moved the logs (20 B/pair), not a table
+
+
+def _po_worker(rank, world, port, q):
+    import torch
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from mahout_amd import SketchTable
+        from mahout_amd.synth import movielens_like, to_csr
+        from mahout_amd.transport import TorchDistTransport
+        torch.cuda.init()
+        users, items, ratings = movielens_like(700, 900, 30_000, seed=11, min_per_user=5)
+        uid = np.unique(users)
+        rows = np.searchsorted(uid, users)
+        order = np.lexsort((items, rows))
+        off, keys, vals = to_csr(rows[order], items[order], uid.size, ratings[order])
+        k, n = 20, uid.size
+        res = {}
+        tr = TorchDistTransport()
+
+        def job(collective):
+            with SketchTable.per_owner_shapes(n, seed=42, owner_ids=uid, device=0) as t:
+                t.ingest_csr(off, keys, vals)  # every rank holds the whole DataModel
+                t.configure_owner_shapes(1.0, 900)
+                if collective:
+                    tr.attach(t)
+                t.finalize()
+                shapes = t.owner_shapes()[2:]
+                return t.top_k_all(k), shapes
+        (ids, sc, cnt), shapes = job(True)
+        (rids, rsc, rcnt), _ = job(False)
+        res["vs_single_rank"] = bool(np.array_equal(cnt, rcnt) and np.array_equal(ids, rids) and _same(sc, rsc))
+        a, b = O.hash_params(42, 32)
+        ok = True
+        for r in [0, 1, 255, 256, 257, 511, 512, n // 2, n - 1]:
+            sims = np.array([O.per_owner_similarity(off, keys, vals, shapes, a, b, r, c) for c in range(n)])
+            sims[r] = np.nan  # TopItems skips the query owner itself
+            eids, esc = O.top_users(uid, sims, k)
+            ok &= ids[r, :cnt[r]].tolist() == eids.tolist() and _same(sc[r, :cnt[r]], esc)
+        res["vs_oracle"] = bool(ok)
+        q.put((rank, res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_transport_per_owner_shapes_collective_top_k():
+    """Per-owner shapes (CosineCM with CountMinSketchConfig, asymmetric
+    userSimilarity(u1, u2), `T/impl/similarity/CosineCM.java:83-96`) on 2
+    ranks: the all-pairs top-k sharded by query rows and gathered equals the
+    single-rank job and the oracle's TopItems loop on rows of both shards."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_po_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=500) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, r in res:
+        assert "error" not in r, (rank, r)
+        assert r["vs_single_rank"], (rank, r)
+        assert r["vs_oracle"], (rank, r)
