@@ -388,6 +388,7 @@ typedef struct cms_stats {
   int64_t stored_bytes;      /* bytes of counters as stored: what one whole-table build writes */
   int64_t u8_rows;           /* narrow owners stored as u8 (every counter < 2^8) */
   int64_t nibble_rows;       /* narrow owners stored as 4-bit counters (every counter < 2^4) */
+  int64_t crumb_rows;        /* narrow owners stored as 2-bit counters (every counter < 2^2) */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -80,6 +80,7 @@ class CmsStats(ctypes.Structure):
         ("stored_bytes", ctypes.c_int64),
         ("u8_rows", ctypes.c_int64),
         ("nibble_rows", ctypes.c_int64),
+        ("crumb_rows", ctypes.c_int64),
     ]
 
 

@@ -694,6 +694,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
 // maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
 // one wave's LDS operations execute in program order.
 constexpr int kNibWaves = 4;
+constexpr int64_t kCrumbKeys = 128;  // owners with at most this many keys try 2-bit rows first
 template <int SV>
 __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
     const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
@@ -727,32 +728,46 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
       mass += inc;
     }
   }
-  const int nq = w >> 5;  // uint4 per sketch row of nibbles (w % 32 == 0 with forms)
-  uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * nq;
+  // 2-bit counters first for owners of <= kCrumbKeys keys (most byte-class
+  // owners: no counter reaches 4), 4-bit for the rest or when a 2-bit add
+  // overflows (the wave restarts the owner; the 4-bit rows overwrite every
+  // byte the 2-bit ones wrote), u8 (k_build_bytes) past 15
+  int bits = ((hi - lo) <= kCrumbKeys && (w & 63) == 0) ? 2 : 4;
+  uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * (w >> 5);  // w/2 bytes per wave (the 4-bit row)
   uint32_t* slot = lds + wv * (w >> 3);
   uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's u16 slot (64-B aligned)
   uint32_t vmax = 0;
   bool ovf = false;
-  for (int d = 0; d < hp.depth; ++d) {
-    for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
-    uint32_t sq = 0;
+  for (;;) {
+    const int lg = bits == 2 ? 4 : 3;  // log2(counters per 32-bit word)
+    const uint32_t cap = (1u << bits) - 1u;
+    const int nq = (w * bits) >> 7;   // uint4 per sketch row
+    vmax = 0;
+    ovf = false;
+    for (int d = 0; d < hp.depth; ++d) {
+      for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
+      uint32_t sq = 0;
 #pragma unroll
-    for (int k = 0; k < kKeyRegs; ++k)
-      if (ik[k]) {
-        const uint32_t c = bucket(hp, d, kp[k]);
-        const uint32_t sh = (c & 7u) << 2;
-        const uint32_t old = (atomicAdd(&slot[c >> 3], ik[k] << sh) >> sh) & 15u;
-        const uint32_t nv = old + ik[k];
-        ovf |= nv > 15u || ik[k] > 15u;  // the add carried into the next counter: rebuild as u8
-        sq += (2u * old + ik[k]) * ik[k];
-        vmax = max(vmax, nv);
-      }
-    sq = wave_sum_u32(sq);  // <= mass * 15 (exact unless ovf)
+      for (int k = 0; k < kKeyRegs; ++k)
+        if (ik[k]) {
+          const uint32_t c = bucket(hp, d, kp[k]);
+          const uint32_t sh = (c & ((1u << lg) - 1u)) * (uint32_t)bits;
+          const uint32_t old = (atomicAdd(&slot[c >> lg], ik[k] << sh) >> sh) & cap;
+          const uint32_t nv = old + ik[k];
+          ovf |= nv > cap || ik[k] > cap;  // the add carried into the next counter: a wider form
+          sq += (2u * old + ik[k]) * ik[k];
+          vmax = max(vmax, nv);
+        }
+      if (__ballot(ovf)) break;  // uniform: escalate
+      sq = wave_sum_u32(sq);  // <= mass * 15
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
-    if (false)
+      if (false)
 #endif
-    for (int j = lane; j < nq; j += 64) store_row(d4 + d * nq + j, slot4[j], SV);
-    if (lane == 0) norm[row * hp.depth + d] = sq;
+      for (int j = lane; j < nq; j += 64) store_row(d4 + d * nq + j, slot4[j], SV);
+      if (lane == 0) norm[row * hp.depth + d] = sq;
+    }
+    if (!__ballot(ovf) || bits == 4) break;
+    bits = 4;
   }
   if (badv) atomicOr(flags, kFlagBadValue);
   if (__ballot(ovf)) {
@@ -765,7 +780,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
   if (lane == 0) {
     rowmax[row] = vmax;
     row_mass[row] = mass;
-    hidx_w[row] = kFormU4;
+    hidx_w[row] = bits == 2 ? kFormU2 : kFormU4;
     cbound[row] = vmax;
   }
 }

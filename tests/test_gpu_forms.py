@@ -1,13 +1,14 @@
-"""GPU: narrow storage forms of the sketch table (u8 and 4-bit rows inside
-their u16 slots; cms_internal.h TableView, cms_build.hip byte-form path,
+"""GPU: narrow storage forms of the sketch table (u8, 4-bit and 2-bit rows
+inside their u16 slots; cms_internal.h TableView, cms_build.hip byte-form path,
 cms_table.hip widen_rows).
 
 The form a row is stored in is an implementation detail: every counter must
 read back as DoubleCountMinSketch's value (`T/impl/common/DoubleCountMinSketch.java:72-80`)
 whatever path wrote it, and every similarity / top-k must be bit-identical to
 the oracle and to a handle that never uses forms (CMS_NO_FORMS=1).  The cases:
-a fresh build with owners in every class (nibble, u8, u16, u32 hot), then
-incremental batches that push nibble rows past 15 and u8 rows past 255
+a fresh build with owners in every class (2-bit, 4-bit, u8, u16, u32 hot),
+then incremental batches that push 2-bit rows past 3, 4-bit rows past 15 and
+u8 rows past 255
 (widening in place), and a large batch into the live table (the accumulate
 build, which widens every touched form row first).
 """
@@ -55,9 +56,10 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
             x.ingest(items, users)
             x.finalize()
         st = t.stats()
-        assert st["nibble_rows"] > 0 and st["u8_rows"] > 0 and st["hot_rows"] > 0, st
-        assert st["nibble_rows"] + st["u8_rows"] + st["hot_rows"] < n  # and some u16 rows
-        assert plain.stats()["nibble_rows"] == 0 and plain.stats()["u8_rows"] == 0
+        assert st["crumb_rows"] > 0 and st["nibble_rows"] > 0 and st["u8_rows"] > 0 and st["hot_rows"] > 0, st
+        assert st["crumb_rows"] + st["nibble_rows"] + st["u8_rows"] + st["hot_rows"] < n  # and some u16 rows
+        ps = plain.stats()
+        assert ps["crumb_rows"] == 0 and ps["nibble_rows"] == 0 and ps["u8_rows"] == 0
         assert st["stored_bytes"] < plain.stats()["stored_bytes"]
         exp = oracle.build_table(n, d, w, a, b, *[np.concatenate(c) for c in zip(*stream)])
         assert np.array_equal(t.read_counters(), exp)
@@ -97,12 +99,14 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
                 assert _same(s1, ref), (step, q)
             seen.append(t.stats())
         # the atomic batches widen only the rows they could push past their form
-        assert 0 < seen[0]["nibble_rows"] < st["nibble_rows"]
+        small = [x["nibble_rows"] + x["crumb_rows"] for x in seen]
+        assert 0 < small[0] < st["nibble_rows"] + st["crumb_rows"]
+        assert seen[0]["crumb_rows"] < st["crumb_rows"]  # 2-bit rows pushed past 3 were widened
         assert u8_rows.size < 2 or 0 < seen[1]["u8_rows"] < seen[0]["u8_rows"]
         assert seen[1]["hot_rows"] >= st["hot_rows"]
-        assert seen[2]["nibble_rows"] <= seen[1]["nibble_rows"]
+        assert small[2] <= small[1]
         # the accumulate build widens every touched form row (u16 or hot)
-        assert seen[3]["nibble_rows"] <= seen[2]["nibble_rows"]
+        assert small[3] <= small[2]
         # the all-pairs job over form rows equals the form-free handle's
         k = 20
         got = t.top_k_all(k)
@@ -121,7 +125,7 @@ def test_forms_point_queries_and_device_read(oracle):
     with _handle(n, d, w, True) as t:
         t.ingest(items, users)
         t.finalize()
-        assert t.stats()["nibble_rows"] > 0
+        assert t.stats()["nibble_rows"] > 0 and t.stats()["crumb_rows"] > 0
         dev = t.read_counters_device(0, n).cpu().numpy()
         assert np.array_equal(dev.astype(np.float64), exp)
         for r in (0, 5, 400, n - 1):
