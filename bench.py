@@ -528,9 +528,9 @@ def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
            "frac_traffic": traffic / avg_s / 1e9 / HBM_PEAK_GBPS if traffic and avg_s else None,
            "algorithmic_bytes_per_launch": alg,
            "algorithmic_bytes_basis": "keys 8 B/pair + spans 16 B/owner + counters at stored width "
-                                      f"({int(st['crumb_rows'])} 2-bit rows, {int(st['nibble_rows'])} 4-bit rows, "
-                                      f"{int(st['u8_rows'])} u8 rows, "
-                                      f"{n - int(st['hot_rows']) - int(st['crumb_rows']) - int(st['nibble_rows']) - int(st['u8_rows'])} u16 rows, "
+                                      f"({int(st['bit_rows'])} 1-bit rows, {int(st['crumb_rows'])} 2-bit rows, "
+                                      f"{int(st['nibble_rows'])} 4-bit rows, {int(st['u8_rows'])} u8 rows, "
+                                      f"{n - int(st['hot_rows']) - int(st['bit_rows']) - int(st['crumb_rows']) - int(st['nibble_rows']) - int(st['u8_rows'])} u16 rows, "
                                       f"{int(st['hot_rows'])} u32 rows)",
            "avg_launch_ms": avg_s * 1e3 if avg_s else None,
            "u32_priced_bytes_per_launch": u32_alg,

@@ -389,6 +389,7 @@ typedef struct cms_stats {
   int64_t u8_rows;           /* narrow owners stored as u8 (every counter < 2^8) */
   int64_t nibble_rows;       /* narrow owners stored as 4-bit counters (every counter < 2^4) */
   int64_t crumb_rows;        /* narrow owners stored as 2-bit counters (every counter < 2^2) */
+  int64_t bit_rows;          /* narrow owners stored as 1-bit counters (every counter 0 or 1) */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -81,6 +81,7 @@ class CmsStats(ctypes.Structure):
         ("u8_rows", ctypes.c_int64),
         ("nibble_rows", ctypes.c_int64),
         ("crumb_rows", ctypes.c_int64),
+        ("bit_rows", ctypes.c_int64),
     ]
 
 

@@ -1468,7 +1468,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
-  int64_t forms[5] = {0, 0, 0, 0, 0};  // hot, u16, u8, 4-bit, 2-bit rows
+  int64_t forms[6] = {0, 0, 0, 0, 0, 0};  // hot, u16, u8, 4-bit, 2-bit, 1-bit rows
   if (!h->per_owner && !h->f64 && h->d_hidx) {
     int rc = count_forms(h, forms);
     if (rc) return rc;
@@ -1486,10 +1486,11 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->stored_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                      : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
                                    : 4 * forms[0] * h->dw + 2 * forms[1] * h->dw + forms[2] * h->dw +
-                                    forms[3] * (h->dw / 2) + forms[4] * (h->dw / 4);
+                                    forms[3] * (h->dw / 2) + forms[4] * (h->dw / 4) + forms[5] * (h->dw / 8);
   out->u8_rows = forms[2];
   out->nibble_rows = forms[3];
   out->crumb_rows = forms[4];
+  out->bit_rows = forms[5];
   return CMS_OK;
 }
 

@@ -694,12 +694,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
 // maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
 // one wave's LDS operations execute in program order.
 constexpr int kNibWaves = 4;
-constexpr int64_t kCrumbKeys = 128;  // owners with at most this many keys try 2-bit rows first
+// owners with at most kBitKeys keys try 1-bit rows first, with at most
+// kCrumbKeys 2-bit rows (CMS_BIT_KEYS / CMS_CRUMB_KEYS override)
+constexpr int kBitKeys = 64, kCrumbKeys = 256;
 template <int SV>
 __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
     const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
     const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
-    uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt) {
+    uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt, int bit_keys,
+    int crumb_keys) {
   extern __shared__ __align__(16) uint32_t lds[];  // [kNibWaves][w / 8] words: one sketch row of nibbles per wave
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -728,18 +731,20 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
       mass += inc;
     }
   }
-  // 2-bit counters first for owners of <= kCrumbKeys keys (most byte-class
-  // owners: no counter reaches 4), 4-bit for the rest or when a 2-bit add
-  // overflows (the wave restarts the owner; the 4-bit rows overwrite every
-  // byte the 2-bit ones wrote), u8 (k_build_bytes) past 15
-  int bits = ((hi - lo) <= kCrumbKeys && (w & 63) == 0) ? 2 : 4;
+  // 1-bit counters first for owners of <= bit_keys keys, 2-bit for <=
+  // crumb_keys (most byte-class owners: no counter reaches 4), 4-bit for the
+  // rest; an add that overflows the form restarts the owner one form wider
+  // (the wider rows overwrite every byte the narrower ones wrote), and past 15
+  // the owner goes to k_build_bytes (u8)
+  const int64_t m = hi - lo;
+  int bits = (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
   uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * (w >> 5);  // w/2 bytes per wave (the 4-bit row)
   uint32_t* slot = lds + wv * (w >> 3);
   uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's u16 slot (64-B aligned)
   uint32_t vmax = 0;
   bool ovf = false;
   for (;;) {
-    const int lg = bits == 2 ? 4 : 3;  // log2(counters per 32-bit word)
+    const int lg = bits == 1 ? 5 : bits == 2 ? 4 : 3;  // log2(counters per 32-bit word)
     const uint32_t cap = (1u << bits) - 1u;
     const int nq = (w * bits) >> 7;   // uint4 per sketch row
     vmax = 0;
@@ -767,7 +772,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
       if (lane == 0) norm[row * hp.depth + d] = sq;
     }
     if (!__ballot(ovf) || bits == 4) break;
-    bits = 4;
+    bits *= 2;
   }
   if (badv) atomicOr(flags, kFlagBadValue);
   if (__ballot(ovf)) {
@@ -780,7 +785,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
   if (lane == 0) {
     rowmax[row] = vmax;
     row_mass[row] = mass;
-    hidx_w[row] = bits == 2 ? kFormU2 : kFormU4;
+    hidx_w[row] = bits == 1 ? kFormU1 : bits == 2 ? kFormU2 : kFormU4;
     cbound[row] = vmax;
   }
 }
@@ -1184,10 +1189,12 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
         CMS_HIP(hipStreamWaitEvent(side, h->ev_fork2, 0));
       }
       auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
+      const int bit_keys = getenv("CMS_BIT_KEYS") ? atoi(getenv("CMS_BIT_KEYS")) : kBitKeys;  // read per build (tests)
+      const int crumb_keys = getenv("CMS_CRUMB_KEYS") ? atoi(getenv("CMS_CRUMB_KEYS")) : kCrumbKeys;
       hipLaunchKernelGGL(nk, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)), dim3(64 * kNibWaves),
                          (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, d_key, d_val, n, h->hp,
                          row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass,
-                         h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt);
+                         h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, bit_keys, crumb_keys);
       auto mk = sv == 2 ? k_build_mid<2> : sv == 1 ? k_build_mid<1> : k_build_mid<0>;
       hipLaunchKernelGGL(mk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)), dim3(kBuildThreads),
                          (size_t)h->p.width * 2, side, d_lo, d_hi, d_key, d_val, h->hp, (const int32_t*)mid_list,

@@ -175,7 +175,7 @@ int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_row
 // counter c of row r += inc; returns the old value.  Narrow rows add into
 // their half of the aligned 32-bit word: promote_rows guarantees the row's
 // bound stays < 2^16, so no carry reaches the neighbouring half.
-// u8 / 4-bit / 2-bit rows add into their byte / nibble / 2 bits of the aligned word the same
+// u8 / 4-bit / 2-bit / 1-bit rows add into their byte / nibble / bits of the aligned word the same
 // way: widen_rows ran first, so the row's counter bound stays within its form.
 __device__ __forceinline__ uint32_t table_add(const TableView& tv, int64_t r, int64_t c, uint32_t inc) {
   const int32_t s = tv.hidx[r];
@@ -194,6 +194,10 @@ __device__ __forceinline__ uint32_t table_add(const TableView& tv, int64_t r, in
   if (s == kFormU2) {
     const uint32_t sh = (uint32_t)(c & 15) << 1;
     return (atomicAdd(w32 + (c >> 4), inc << sh) >> sh) & 0x3u;
+  }
+  if (s == kFormU1) {
+    const uint32_t sh = (uint32_t)(c & 31);
+    return (atomicAdd(w32 + (c >> 5), inc << sh) >> sh) & 0x1u;
   }
   const uint32_t sh = (uint32_t)(c & 7) << 2;
   return (atomicAdd(w32 + (c >> 3), inc << sh) >> sh) & 0xfu;

@@ -73,17 +73,18 @@ struct PendingEvent {
 // below 2^8 as u8 in the first dw bytes of its slot, and one whose counters
 // are all below 2^4 as packed nibbles (counter j in bits 4*(j&1) of byte j/2)
 // in the first dw/2 bytes, and one whose counters are all below 2^2 as 2-bit
-// counters (counter j in bits 2*(j&3) of byte j/4) in the first dw/4 bytes
-// -- at config 3 most of the 1M owners, so the build
+// counters (counter j in bits 2*(j&3) of byte j/4) in the first dw/4 bytes,
+// and one whose counters are all 0 or 1 as bits (counter j in bit j&7 of
+// byte j/8) in the first dw/8 bytes -- at config 3 most of the 1M owners, so the build
 // writes a fraction of the u16 bytes.  hidx[row] names the form (< 0) or the
 // hot slot (>= 0).  cbound[row] (u32) bounds a form row's counters; a writer
 // widens a form row to u16 in place (widen_rows) before its bound could pass
 // the form's capacity.  Forms exist only when dw % 32 == 0 (every slot and
 // every nibble row then starts 64-byte aligned).
 constexpr uint64_t kNarrowLimit = 1ULL << 16;
-constexpr int32_t kFormU16 = -1, kFormU8 = -2, kFormU4 = -3, kFormU2 = -4;
+constexpr int32_t kFormU16 = -1, kFormU8 = -2, kFormU4 = -3, kFormU2 = -4, kFormU1 = -5;
 constexpr uint32_t form_cap(int32_t form) {
-  return form == kFormU2 ? 3u : form == kFormU4 ? 15u : form == kFormU8 ? 255u : 65535u;
+  return form == kFormU1 ? 1u : form == kFormU2 ? 3u : form == kFormU4 ? 15u : form == kFormU8 ? 255u : 65535u;
 }
 
 struct TableView {
@@ -98,6 +99,7 @@ struct TableView {
     const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
     if (s == kFormU8) return p[j];
     if (s == kFormU2) return (uint32_t)(p[j >> 2] >> ((j & 3) << 1)) & 3u;
+    if (s == kFormU1) return (uint32_t)(p[j >> 3] >> (j & 7)) & 1u;
     return (uint32_t)(p[j >> 1] >> ((j & 1) << 2)) & 15u;
   }
   // counters j..j+3 of a row (j % 4 == 0 and dw % 4 == 0: aligned vector loads)
@@ -116,6 +118,10 @@ struct TableView {
     if (s == kFormU2) {
       const uint32_t v = p[j >> 2];
       return make_uint4(v & 3u, (v >> 2) & 3u, (v >> 4) & 3u, v >> 6);
+    }
+    if (s == kFormU1) {
+      const uint32_t v = (uint32_t)p[j >> 3] >> (j & 4);
+      return make_uint4(v & 1u, (v >> 1) & 1u, (v >> 2) & 1u, (v >> 3) & 1u);
     }
     const uint32_t v = *reinterpret_cast<const uint16_t*>(p + (j >> 1));
     return make_uint4(v & 15u, (v >> 4) & 15u, (v >> 8) & 15u, v >> 12);
@@ -169,7 +175,7 @@ struct cms_handle {
   uint16_t* d_t16 = nullptr;        // [n][d][w] narrow counters
   bool f64 = false;                 // CMS_COUNTER_F64: fp64 counters in d_t64 (cms_f64.hip), no u16/u32 table
   double* d_t64 = nullptr;          // [n][d][w] fp64 counters
-  int32_t* d_hidx = nullptr;        // [n] hot slot, or the narrow form (kFormU16 / kFormU8 / kFormU4 / kFormU2)
+  int32_t* d_hidx = nullptr;        // [n] hot slot, or the narrow form (kFormU16 / kFormU8 / kFormU4 / kFormU2 / kFormU1)
   uint32_t* d_cbound = nullptr;     // [n] bound of a form row's counters (maintained for form rows only)
   bool forms_ok = false;            // dw % 32 == 0: fresh builds may store u8 / nibble forms
   cms::DevBuf hot_tab;              // [hot_cap][d][w] u32 counters of the hot rows
@@ -327,7 +333,7 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 // rows holding a u32 slot (synchronises the stream)
 int count_hot_rows(cms_handle* h, int64_t* out);
 // rows per storage form: [0] hot, [1] u16, [2] u8, [3] nibble (synchronises)
-int count_forms(cms_handle* h, int64_t out[5]);  // hot, u16, u8, 4-bit, 2-bit rows
+int count_forms(cms_handle* h, int64_t out[6]);  // hot, u16, u8, 4-bit, 2-bit, 1-bit rows
 // Form rows that a coming write could push past their capacity become u16 in
 // place: with d_bound (a u64 upper bound of each row's mass after the write)
 // and old_mass, a touched form row (bound > old mass) is widened when

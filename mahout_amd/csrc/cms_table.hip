@@ -111,7 +111,7 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
   return CMS_OK;
 }
 
-// ---- narrow forms (u8 / 4-bit / 2-bit rows inside their u16 slots) ----
+// ---- narrow forms (u8 / 4-bit / 2-bit / 1-bit rows inside their u16 slots) ----
 
 // Rows to widen to u16 before a write (see widen_rows in cms_internal.h).
 __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int32_t* hidx, uint32_t* cbound,
@@ -131,7 +131,7 @@ __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, co
   }
 }
 
-// One workgroup per listed row: its u8 / 4-bit / 2-bit counters rewritten as u16 in
+// One workgroup per listed row: its u8 / 4-bit / 2-bit / 1-bit counters rewritten as u16 in
 // the same slot.  The u16 image of counters [c0, c1) covers bytes
 // [2 c0, 2 c1), which holds only old bytes of counters >= c0; so chunks of
 // 4096 counters are processed from the top down, each read completely (16
@@ -159,6 +159,10 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
           const uint32_t x = *reinterpret_cast<const uint32_t*>(p8 + (j >> 2));
 #pragma unroll
           for (int q = 0; q < 16; ++q) v[q] = (x >> (q * 2)) & 3u;
+        } else if (f == kFormU1) {
+          const uint32_t x = *reinterpret_cast<const uint16_t*>(p8 + (j >> 3));
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = (x >> q) & 1u;
         } else {
           const uint2 x = *reinterpret_cast<const uint2*>(p8 + (j >> 1));
           const uint32_t wv[2] = {x.x, x.y};
@@ -197,26 +201,26 @@ int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass,
 }
 
 __global__ void k_count_forms(const int32_t* hidx, int64_t n, unsigned long long* out) {
-  uint32_t c[5] = {0, 0, 0, 0, 0};
+  uint32_t c[6] = {0, 0, 0, 0, 0, 0};
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = hidx[r];
-    c[f >= 0 ? 0 : f == kFormU16 ? 1 : f == kFormU8 ? 2 : f == kFormU4 ? 3 : 4] += 1;
+    c[f >= 0 ? 0 : f == kFormU16 ? 1 : f == kFormU8 ? 2 : f == kFormU4 ? 3 : f == kFormU2 ? 4 : 5] += 1;
   }
-  for (int q = 0; q < 5; ++q)
+  for (int q = 0; q < 6; ++q)
     if (c[q]) atomicAdd(out + q, (unsigned long long)c[q]);
 }
 
-int count_forms(cms_handle* h, int64_t out[5]) {
+int count_forms(cms_handle* h, int64_t out[6]) {
   DevBuf tmp;
-  CMS_HIP(tmp.ensure(5 * sizeof(unsigned long long)));
-  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 5 * sizeof(unsigned long long), h->stream));
+  CMS_HIP(tmp.ensure(6 * sizeof(unsigned long long)));
+  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 6 * sizeof(unsigned long long), h->stream));
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 4096));
   hipLaunchKernelGGL(k_count_forms, dim3(g), dim3(256), 0, h->stream, h->d_hidx, h->n, tmp.as<unsigned long long>());
   CMS_HIP(hipGetLastError());
-  unsigned long long c[5];
+  unsigned long long c[6];
   CMS_HIP(hipMemcpyAsync(c, tmp.ptr, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
-  for (int q = 0; q < 5; ++q) out[q] = (int64_t)c[q];
+  for (int q = 0; q < 6; ++q) out[q] = (int64_t)c[q];
   return CMS_OK;
 }
 

@@ -57,9 +57,9 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
             x.finalize()
         st = t.stats()
         assert st["crumb_rows"] > 0 and st["nibble_rows"] > 0 and st["u8_rows"] > 0 and st["hot_rows"] > 0, st
-        assert st["crumb_rows"] + st["nibble_rows"] + st["u8_rows"] + st["hot_rows"] < n  # and some u16 rows
+        assert st["bit_rows"] + st["crumb_rows"] + st["nibble_rows"] + st["u8_rows"] + st["hot_rows"] < n  # and u16 rows
         ps = plain.stats()
-        assert ps["crumb_rows"] == 0 and ps["nibble_rows"] == 0 and ps["u8_rows"] == 0
+        assert ps["bit_rows"] == 0 and ps["crumb_rows"] == 0 and ps["nibble_rows"] == 0 and ps["u8_rows"] == 0
         assert st["stored_bytes"] < plain.stats()["stored_bytes"]
         exp = oracle.build_table(n, d, w, a, b, *[np.concatenate(c) for c in zip(*stream)])
         assert np.array_equal(t.read_counters(), exp)
@@ -99,8 +99,8 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
                 assert _same(s1, ref), (step, q)
             seen.append(t.stats())
         # the atomic batches widen only the rows they could push past their form
-        small = [x["nibble_rows"] + x["crumb_rows"] for x in seen]
-        assert 0 < small[0] < st["nibble_rows"] + st["crumb_rows"]
+        small = [x["nibble_rows"] + x["crumb_rows"] + x["bit_rows"] for x in seen]
+        assert 0 < small[0] < st["nibble_rows"] + st["crumb_rows"] + st["bit_rows"]
         assert seen[0]["crumb_rows"] < st["crumb_rows"]  # 2-bit rows pushed past 3 were widened
         assert u8_rows.size < 2 or 0 < seen[1]["u8_rows"] < seen[0]["u8_rows"]
         assert seen[1]["hot_rows"] >= st["hot_rows"]
@@ -114,10 +114,15 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
         assert all(np.array_equal(x, y, equal_nan=True) for x, y in zip(got, want))
 
 
-def test_forms_point_queries_and_device_read(oracle):
+@pytest.mark.parametrize("bit_keys", ["0", None])
+def test_forms_point_queries_and_device_read(oracle, monkeypatch, bit_keys):
     """Point queries (DoubleCountMinSketch.get, :94-103) and the device
-    counter read on nibble and u8 rows."""
+    counter read on 2-bit, 4-bit and u8 rows, with and without 1-bit rows
+    (owners of <= 64 keys try them first unless CMS_BIT_KEYS=0), then a batch
+    that widens some of every form."""
     import torch
+    if bit_keys:
+        monkeypatch.setenv("CMS_BIT_KEYS", bit_keys)
     n, d, w = 2000, 4, 512
     items, users = _stream(n, 5000, 300_000, seed=3)  # > 262143 pairs: the row build (smaller batches: atomics)
     a, b = oracle.hash_params(42, d)
@@ -125,7 +130,8 @@ def test_forms_point_queries_and_device_read(oracle):
     with _handle(n, d, w, True) as t:
         t.ingest(items, users)
         t.finalize()
-        assert t.stats()["nibble_rows"] > 0 and t.stats()["crumb_rows"] > 0
+        st = t.stats()
+        assert st["nibble_rows"] > 0 and st["crumb_rows"] > 0 and (st["bit_rows"] > 0) == (bit_keys is None), st
         dev = t.read_counters_device(0, n).cpu().numpy()
         assert np.array_equal(dev.astype(np.float64), exp)
         for r in (0, 5, 400, n - 1):
@@ -134,4 +140,18 @@ def test_forms_point_queries_and_device_read(oracle):
         t.ingest_csr(np.zeros(n + 1, np.int64), np.zeros(0, np.int64))  # an empty CSR batch changes nothing
         t.finalize()
         assert np.array_equal(t.read_counters(), exp)
+        # a small batch (atomics) onto every row: rows it could push past their
+        # form are widened in place, the others keep it; all stay exact
+        rng = np.random.Generator(np.random.PCG64(9))
+        br = rng.integers(0, n, 3000).astype(np.int64)
+        bk = rng.integers(0, 5000, 3000).astype(np.int64)
+        t.ingest(br, bk)
+        t.finalize()
+        exp2 = oracle.build_table(n, d, w, a, b, np.concatenate([items, br]), np.concatenate([users, bk]))
+        assert np.array_equal(t.read_counters(), exp2)
+        for r in (0, 5, 400, n - 1):
+            s1 = t.similarities(r, np.arange(n))
+            ref = oracle.similarities_row(exp2, r)
+            ref[r] = oracle.cosine_cm(exp2[r], exp2[r])
+            assert _same(s1, ref), r
         torch.cuda.synchronize()
