@@ -107,9 +107,12 @@ __device__ __forceinline__ uint32_t lds_bin_add(uint32_t* hist, uint32_t bin, bo
 // table, the one with the most hits wins (ties: larger owner; an owner that
 // loses its slot simply stays on the two-pass path -- correctness never
 // depends on who is hot).
-constexpr int kHotBins = 1024;
+#ifndef CMS_HOT_LOG
+#define CMS_HOT_LOG 10
+#endif
+constexpr int kHotLog = CMS_HOT_LOG, kHotBins = 1 << kHotLog;
 __device__ __forceinline__ uint32_t hslot(int64_t o) {
-  return (uint32_t)(((uint64_t)o * 0x9E3779B97F4A7C15ULL) >> 54);  // top 10 bits
+  return (uint32_t)(((uint64_t)o * 0x9E3779B97F4A7C15ULL) >> (64 - kHotLog));  // top kHotLog bits
 }
 
 // Sample counts: each block counts its share of the strided sample in an LDS
