@@ -169,6 +169,16 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t r, int s2, int P1, const uin
   return r >> s2;
 }
 
+// scatter stores: plain, or non-temporal with CMS_PART_NT (experiment)
+template <class T>
+__device__ __forceinline__ void pstore(T* p, T v) {
+#ifdef CMS_PART_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // Pass-1 work is cut into tiles of kPartTile pairs, and block b takes tiles
 // b, b + NB, b + 2 NB, ... (the same assignment in k_p1_hist and
 // k_p1_scatter): at any moment the blocks stream one contiguous window of the
@@ -349,12 +359,12 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
       if (g != 0xFFFFFFFFu) continue;
 #endif
       if ((int)bin >= P1) {  // hot owner: final place
-        okey_hot[g] = L.key[i];
+        pstore(okey_hot + g, L.key[i]);
         if (oval) oval_hot[g] = L.val[i];
         continue;
       }
-      okey[g] = L.key[i];
-      ofine[g] = L.fine[i];
+      pstore(okey + g, L.key[i]);
+      pstore(ofine + g, L.fine[i]);
       if (oval) oval[g] = L.val[i];
     }
     lds_barrier();
@@ -640,7 +650,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
 #ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
       if (g != 0xFFFFFFFFu) continue;
 #endif
-      okey[g] = L.key[i];
+      pstore(okey + g, L.key[i]);
       if (oval) oval[g] = L.val[i];
       if (orow) orow[g] = b * P2 + (int32_t)f;
     }
