@@ -682,13 +682,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8
 // Byte-class owners (byte_class): ONE WAVE per owner, four owners per
 // workgroup, each wave with its own w/2-byte LDS slot (4 KB at w = 8192).  The
 // owner's keys are read once into registers; each sketch row in turn is
-// counted in the slot as 4-bit counters and leaves as 16-B non-temporal
-// stores of the slot itself (a nibble row needs no packing).  The LDS adds
+// counted in the slot as 1-, 2- or 4-bit counters (the narrowest form the
+// owner's key count suggests, widened on overflow) and leaves as 16-B
+// non-temporal stores of the slot itself (no packing).  The LDS adds
 // return the old counter, so each sketch row's sum of squares (2 c inc +
 // inc^2 per update, telescoping to the exact sum) and the row maximum come out
 // of the update pass.  With 4 KB per owner 32 owners are in flight per CU
 // (the wave limit), against 8 with a whole-sketch 20 KB image per workgroup
-// (config 3: 5.1 ms for this kernel).  A counter that would pass 15 (a
+// (config 3: 5.1 ms for this kernel with 4-bit rows only, 3.1 ms with 1- and
+// 2-bit rows, which halve and quarter the row bytes).  A counter that would pass 15 (a
 // repeated key, a collision, an increment >= 16) is detected by its add; the
 // owner is queued for k_build_bytes, which rewrites its whole slot, norms and
 // maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
