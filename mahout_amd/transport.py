@@ -47,13 +47,22 @@ def _h2d(ptr, host, nbytes):
         raise RuntimeError("hipMemcpy host->device failed")
 
 
-class TorchDistTransport:
-    """allreduce / allgather callables for SketchTable.comm_init_transport."""
+def _host_copy(dst, src, nbytes):
+    ctypes.memmove(dst, src, nbytes)
 
-    def __init__(self, group=None):
+
+class TorchDistTransport:
+    """allreduce / allgather callables for SketchTable.comm_init_transport.
+
+    The library hands device pointers (staged through host memory with
+    hipMemcpy); host=True takes host pointers instead (the same collective
+    logic without a GPU: tests/test_dist_gloo.py)."""
+
+    def __init__(self, group=None, host=False):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
+        self.host = host
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.bytes_moved = 0
@@ -62,23 +71,35 @@ class TorchDistTransport:
     def allreduce(self, ptr, count):
         import torch
         host = np.empty(count, np.int64)
-        _d2h(host, ptr, count * 8)
+        self._in(host, ptr, count * 8)
         t = torch.from_numpy(host)
         self.dist.all_reduce(t, group=self.group)  # u64 sums: two's complement gives the same bits
-        _h2d(ptr, host, count * 8)
+        self._out(ptr, host, count * 8)
         self.bytes_moved += count * 8
         self.calls.append(("allreduce", count * 8))
 
     def allgather(self, send, recv, nbytes):
         import torch
         host = np.empty(nbytes, np.uint8)
-        _d2h(host, send, nbytes)
+        self._in(host, send, nbytes)
         out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
         self.dist.all_gather(out, torch.from_numpy(host), group=self.group)
         allh = np.ascontiguousarray(torch.cat(out).numpy())
-        _h2d(recv, allh, nbytes * self.world)
+        self._out(recv, allh, nbytes * self.world)
         self.bytes_moved += nbytes * self.world
         self.calls.append(("allgather", nbytes))
+
+    def _in(self, host, ptr, nbytes):
+        if self.host:
+            _host_copy(host.ctypes.data, ptr, nbytes)
+        else:
+            _d2h(host, ptr, nbytes)
+
+    def _out(self, ptr, host, nbytes):
+        if self.host:
+            _host_copy(ptr, host.ctypes.data, nbytes)
+        else:
+            _h2d(ptr, host, nbytes)
 
     def attach(self, table):
         table.comm_init_transport(self.rank, self.world, self.allreduce, self.allgather)
