@@ -147,8 +147,14 @@ constexpr bool kNoSlicePairs = false;
 constexpr int kBuildStoreForm = 2;
 constexpr size_t kFormLdsMax = 64 * 1024;  // byte-form owners: [d][w] bytes of LDS per workgroup  // 16-B non-temporal: config-3 build 20.4 -> 19.4 ms, config 2 ~1% (scripts/store_ab.sh)
 
+// waves per SIMD the row and mid builds are compiled for: 6 (up to 80 VGPRs,
+// no spills) -- at 8 (64 VGPRs) both spilled a few registers and the config-3
+// build scope took 7.21-7.25 ms against 6.80-6.82 ms at 6 (6.88-6.94 at 7)
+#ifndef CMS_BUILD_WAVES
+#define CMS_BUILD_WAVES 6
+#endif
 template <int SV>
-__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_rows(
+__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(CMS_BUILD_WAVES, 8))) void k_build_rows(
     const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
     int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
@@ -549,7 +555,7 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 // paired-u16 row image of k_build_rows; the stored rows shrink 2-4x.  A
 // persistent grid walks the device-side list.
 template <int SV>
-__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_mid(
+__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(CMS_BUILD_WAVES, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
     uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
