@@ -896,7 +896,6 @@ __global__ __launch_bounds__(256) void k_build_slices(const int64_t* lo_, const 
                                                       const int2* extra_map, const uint32_t* counters, TableView tv,
                                                       uint64_t* row_mass, uint32_t* flags) {
   extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] packed u16 pairs
-  __shared__ unsigned long long s_mass;
   if (blockIdx.x >= counters[1]) return;
   const int tid = threadIdx.x;
   const int w = (int)hp.width;
@@ -907,7 +906,6 @@ __global__ __launch_bounds__(256) void k_build_slices(const int64_t* lo_, const 
   const int64_t lo = lo_[row] + (int64_t)m.y * slice;
   const int64_t hi = min(hi_[row], lo + slice);
   for (int j = tid; j < words; j += 256) lds[j] = 0u;
-  if (tid == 0) s_mass = 0ULL;
   __syncthreads();
   const uint32_t one = 1u << hp.frac_bits;
   for (int64_t i = lo + tid; i < hi; i += 256) {
@@ -970,7 +968,6 @@ __global__ __launch_bounds__(256) void k_hot_reduce(const HotInfo* hot, const ui
                                                     const uint16_t* part, int64_t hcap, TableView tv, int accumulate,
                                                     uint64_t* norm, uint32_t* rowmax) {
   __shared__ uint4 red[3][64][2];
-  __shared__ uint64_t sred[4];
   const uint32_t nhot = counters[0];
   const int w = (int)hp.width;
   const int64_t dw = tv.dw;
