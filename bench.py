@@ -397,7 +397,7 @@ def config1(budget_s=3.0):
     return out
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")  # this round's committed rocprofv3 summaries
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")  # this round's committed rocprofv3 summaries
 
 
 def _pmc_file(name):
@@ -816,6 +816,10 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     t.set_timing(False)
     del batches
     lat = [p["finalize_s"] + p["refresh_s"] for p in periods]
+    all_pairs = n * (n - 1) / 2
+    recomputed_rate = sum((1 - (1 - p["touched_owner_frac"]) ** 2) * all_pairs / p["refresh_s"]
+                          for p in periods) / len(periods)
+    whole_rate = all_pairs / keep_s
     return {
         "workload": f"config 5: a {total}-pair Zipf stream (10M pairs/s) into the resident {n}-item table in "
                     f"{bsize}-pair batches; then {nb} batches of {per_batch} pairs per GPU, every {every} batch(es) "
@@ -830,9 +834,14 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "refresh_latency_s": sum(lat) / len(lat),
         "refresh_latency_max_s": max(lat),
         # unique pairs with a touched owner (the ones a refresh recomputes) per second
-        "refresh_recomputed_pairs_per_s": sum((1 - (1 - p["touched_owner_frac"]) ** 2) * n * (n - 1) / 2 / p["refresh_s"]
-                                              for p in periods) / len(periods),
+        "refresh_recomputed_pairs_per_s": recomputed_rate,
+        # ... against the whole job's unique pairs per second (1.0: a refresh is as efficient per pair)
+        "refresh_pair_rate_vs_whole_job": recomputed_rate / whole_rate,
         "refresh_vs_whole_job": keep_s / (sum(lat) / len(lat)),
+        # the refresh latency in arrival intervals: one interval = the time one refresh batch (all ranks)
+        # takes to arrive at 10M pairs/s (0.125 s per 1.25M-pair batch on one GPU, 1 s on eight)
+        "batch_interval_s": per_batch * world / 10e6,
+        "refresh_latency_in_batch_intervals": (sum(lat) / len(lat)) / (per_batch * world / 10e6),
         "refresh_periods": periods,
         "full_lists": int((cnt == k).sum()),
         "touched_owner_frac": {"all_batches": touched_all, "per_batch": touched_one,
@@ -1120,10 +1129,66 @@ def main():
     if cfg1 is not None:
         result["config1"] = cfg1
     if rank == 0:
+        cos = result.get("cosine") or {}
+        if "unique_item_pair_cosines_per_s" in cos:  # the metric's cosine half as top-level keys
+            result["cosines_per_s"] = cos["unique_item_pair_cosines_per_s"]
+            result["cosine_wall_s"] = cos["wall_s"]
+            result["cosine_first_job_s"] = cos["first_job_s"]
+            result["cosine_roofline"] = {k: cos["roofline"].get(k) for k in
+                                         ("bound", "achieved", "peak", "unit", "frac", "avg_launch_ms",
+                                          "pmc_mfma_busy_frac", "pmc_l2_hit")}
+            result["cosine_roofline"]["kernel"] = "k_cosine_sym fp4"
+        # last key: a compact record of every line, so the stdout tail carries it
+        result["summary"] = summary(result)
         print(json.dumps(result))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _r(x, nd=4):
+    return None if x is None else float(f"{x:.{nd}g}")
+
+
+def summary(res):
+    """Compact figures of the whole line (configs 3, 4, 5, 2, 1, CPU
+    baselines), printed last so a truncated stdout tail still holds them."""
+    out = {"cfg3_updates_per_s": _r(res.get("value")), "cfg3_ms_per_step": _r(res.get("ms_per_step")),
+           "cfg3_build_frac": _r((res.get("roofline") or {}).get("frac"), 3),
+           "cfg3_step_frac": _r((res.get("step_roofline") or {}).get("frac"), 3),
+           "cfg3_breakdown_ms": {k: _r(v, 3) for k, v in (res.get("breakdown_ms_per_step") or {}).items()}}
+    cos = res.get("cosine") or {}
+    if "wall_s" in cos:
+        rf = cos.get("roofline") or {}
+        out.update({"cfg4_cosines_per_s": _r(cos.get("unique_item_pair_cosines_per_s")),
+                    "cfg4_wall_s": _r(cos.get("wall_s")), "cfg4_first_job_s": _r(cos.get("first_job_s")),
+                    "cfg4_fp4_frac": _r(rf.get("frac"), 3), "cfg4_fp4_avg_launch_ms": _r(rf.get("avg_launch_ms")),
+                    "cfg4_int8_frac": _r((cos.get("roofline_int8_waves") or {}).get("frac"), 3),
+                    "cfg4_mixed_peak_frac": _r(cos.get("frac_mixed_peak_per_gpu"), 3),
+                    "cfg4_full_lists": cos.get("full_lists")})
+        st = cos.get("config5_streaming") or {}
+        if st:
+            out.update({"cfg5_sustained_updates_per_s": _r(st.get("sustained_updates_per_s")),
+                        "cfg5_refresh_latency_s": _r(st.get("refresh_latency_s")),
+                        "cfg5_refresh_pair_rate_vs_whole_job": _r(st.get("refresh_pair_rate_vs_whole_job"), 3),
+                        "cfg5_whole_job_s": _r(st.get("keep_lists_whole_job_s"))})
+        if cos.get("cpu_baseline"):
+            out["cfg4_cpu_pairs_per_s"] = _r(cos["cpu_baseline"].get("value"))
+    elif cos:
+        out["cfg4_error"] = str(cos.get("error"))[:200]
+    c2 = res.get("config2") or {}
+    if c2:
+        out["cfg2_updates_per_s"] = _r(c2.get("updates_per_s"))
+        po = ((c2.get("extras") or {}).get("per_owner_shapes_cfg2") or {})
+        if po.get("all_pairs"):
+            out["cfg2_per_owner_all_pairs_s"] = _r(po["all_pairs"].get("s"))
+            out["cfg2_per_owner_ordered_pairs_per_s"] = _r(po["all_pairs"].get("ordered_pairs_per_s"))
+    if res.get("cpu_baseline"):
+        out["cfg3_cpu_updates_per_s"] = _r(res["cpu_baseline"].get("value"))
+    if res.get("merge"):
+        out["merge_payload_ratio"] = _r(res["merge"].get("payload_ratio"), 3)
+        out["allreduce_ms_per_step"] = _r(res.get("allreduce_ms_per_step"))
+    return out
 
 
 if __name__ == "__main__":

@@ -80,8 +80,20 @@ typedef struct cms_params {
                            ratings); counters hold pref * 2^frac_bits.  Similarities are
                            scale-invariant bit for bit; point queries / counters read back
                            in preference units.  0 = integer preferences. */
-  int32_t reserved;
+  int32_t flags;        /* CMS_FLAG_* bits (0 = defaults) */
 } cms_params;
+
+/* cms_params.flags:
+ * CMS_FLAG_COLLECTIVE_SINGLE_RANK -- a one-rank job still takes the multi-rank
+ *   data path: cms_comm_init(h, uid, 0, 1) creates a real one-rank RCCL
+ *   communicator (and cms_comm_init_transport(h, 0, 1, ...) attaches the
+ *   caller's transport), so cms_finalize merges through the packed all-reduce,
+ *   later COO batches go through the delta log and its all-gather, and
+ *   cms_top_k_all through the collective merge -- each with one participant,
+ *   so the results equal the plain single-GPU path bit for bit.  Without the
+ *   flag a world of 1 detaches any communicator (the fast single-GPU path).
+ *   Not with CMS_COUNTER_F64 (CMS_E_PARAM). */
+#define CMS_FLAG_COLLECTIVE_SINGLE_RANK 0x1
 
 typedef struct cms_handle cms_handle;
 
@@ -390,6 +402,9 @@ typedef struct cms_stats {
   int64_t nibble_rows;       /* narrow owners stored as 4-bit counters (every counter < 2^4) */
   int64_t crumb_rows;        /* narrow owners stored as 2-bit counters (every counter < 2^2) */
   int64_t bit_rows;          /* narrow owners stored as 1-bit counters (every counter 0 or 1) */
+  int64_t collective_calls;  /* all-reduce / all-gather calls made through the communicator so far */
+  int32_t comm_kind;         /* 0 none (single-GPU path), 1 RCCL (cms_comm_init), 2 caller transport */
+  int32_t device;            /* HIP device ordinal of the handle */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

@@ -26,7 +26,21 @@
  *    its get(key) -- the recommender's point query -- is answered by the GPU
  *    (cms_point_query, the same fp64 value);
  *  - everything else (itemSimilarity as AbstractSimilarity's exact co-rated
- *    cosine, computeResult, refresh) is inherited exactly as before.
+ *    cosine, computeResult) is as before; refresh(Collection) and toString()
+ *    are AbstractSimilarity's own: both are final there
+ *    (AbstractSimilarity.java:333,339), so this class cannot override them.
+ *
+ * Refresh semantics.  AbstractSimilarity.refresh refreshes the DataModel and
+ * re-reads its getNumUsers()/getNumItems() (AbstractSimilarity.java:53-62).
+ * The reference's CosineCM keeps its `sketches` cache across a refresh (it is
+ * never cleared, CosineCM.java:60-67) and rebuilds u1's sketch on every
+ * userSimilarity call.  Here both sketches live on the device, so every entry
+ * point first compares the DataModel's user and item counts with the ones the
+ * device table was built from and, when they differ (a refreshed model that
+ * gained or lost users or items), rebuilds the table and drops the cached
+ * profiles.  A refresh that only changes preference values keeps the counts:
+ * call rebuild() after it (the reference would serve such a change for u1
+ * but not for its cached u2 sketches).
  * The hash functions are the caller's own HashFunctionBuilder: its drawn
  * (a_i, b_i) are installed on the device (HashFunctionParams.draw,
  * cms_set_hash_params), so even a clock-seeded builder hashes identically.
@@ -36,11 +50,9 @@
  */
 package org.apache.mahout.cf.taste.impl.similarity;
 
-import java.util.Collection;
 import java.util.concurrent.ConcurrentHashMap;
 import java.lang.reflect.Field;
 
-import org.apache.mahout.cf.taste.common.Refreshable;
 import org.apache.mahout.cf.taste.common.TasteException;
 import org.apache.mahout.cf.taste.common.Weighting;
 import org.apache.mahout.cf.taste.impl.common.AbstractCountMinSketch;
@@ -88,6 +100,7 @@ public final class CosineCM extends AbstractSimilarity {
    * (delta, epsilon), counters read from the device once and cached.
    */
   public DoubleCountMinSketch getExportedCMProfile(long userID) throws TasteException {
+    ensureCurrent();
     DoubleCountMinSketch cm = sketches.get(userID);
     if (cm == null) {
       int[] shape = gpu.ownerShape(userID);  // NoSuchUserException / TasteException as exportProfile
@@ -120,19 +133,32 @@ public final class CosineCM extends AbstractSimilarity {
   /** CosineCM.userSimilarity (CosineCM.java:83-96) as one cms_similarity call. */
   @Override
   public double userSimilarity(long userID1, long userID2) throws TasteException {
+    ensureCurrent();
     return gpu.userSimilarity(userID1, userID2);
   }
 
-  @Override
-  public void refresh(Collection<Refreshable> alreadyRefreshed) {
-    super.refresh(alreadyRefreshed);
-    sketches.clear();
-    gpu.refresh(alreadyRefreshed);
+  /**
+   * Rebuild the device table from the DataModel as it is now and drop the
+   * cached profiles (after a refresh that changed preference values but not
+   * the user or item counts).
+   */
+  public void rebuild() throws TasteException {
+    synchronized (gpu) {
+      gpu.rebuild();
+      sketches.clear();
+    }
   }
 
-  @Override
-  public String toString() {
-    return "CosineCM[dataModel:" + getDataModel() + ",GPU sketches]";
+  /** Lazy refresh: the DataModel gained or lost users or items since the build. */
+  private void ensureCurrent() throws TasteException {
+    if (gpu.isStale()) {
+      synchronized (gpu) {
+        if (gpu.isStale()) {
+          gpu.rebuild();
+          sketches.clear();
+        }
+      }
+    }
   }
 
   /**

@@ -49,7 +49,9 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private final int device;
   private final long[] hashA;  // a HashFunctionBuilder's drawn (a_i, b_i), or null: drawn from seed
   private final long[] hashB;
-  private long handle;  // cms_handle*
+  private volatile long handle;  // cms_handle*
+  private volatile int builtUsers = -1;  // DataModel.getNumUsers() / getNumItems() the table was built from
+  private volatile int builtItems = -1;
 
   /** Hash rows a per-owner handle carries (CMS_MAX_DEPTH of include/mahout_cms.h). */
   static final int MAX_DEPTH = 32;
@@ -160,6 +162,7 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private void build() throws TasteException {
     DataModel model = getDataModel();
     int n = model.getNumUsers();
+    int numItems = model.getNumItems();
     long[] ids = new long[n];
     long[] offsets = new long[n + 1];
     int r = 0;
@@ -208,9 +211,22 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     }
     long old = handle;
     handle = h;
+    builtUsers = n;
+    builtItems = numItems;
     if (old != 0) {
       nativeDestroy(old);
     }
+  }
+
+  /** The DataModel's user or item count differs from the one the table was built from. */
+  boolean isStale() throws TasteException {
+    DataModel model = getDataModel();
+    return model.getNumUsers() != builtUsers || model.getNumItems() != builtItems;
+  }
+
+  /** Rebuild the device table from the DataModel as it is now. */
+  void rebuild() throws TasteException {
+    build();
   }
 
   /**

@@ -29,6 +29,7 @@ CMS_FORMAT_ITEM_SIMILARITY_JOB = 1
 CMS_FORMAT_SPARK_ITEMSIMILARITY = 2
 CMS_UNWEIGHTED = 0
 CMS_WEIGHTED = 1
+CMS_FLAG_COLLECTIVE_SINGLE_RANK = 0x1
 
 # Every symbol the header declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -57,7 +58,7 @@ class CmsParams(ctypes.Structure):
         ("weighting", ctypes.c_int32),
         ("device", ctypes.c_int32),
         ("frac_bits", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
     ]
 
 
@@ -82,6 +83,9 @@ class CmsStats(ctypes.Structure):
         ("nibble_rows", ctypes.c_int64),
         ("crumb_rows", ctypes.c_int64),
         ("bit_rows", ctypes.c_int64),
+        ("collective_calls", ctypes.c_int64),
+        ("comm_kind", ctypes.c_int32),
+        ("device", ctypes.c_int32),
     ]
 
 

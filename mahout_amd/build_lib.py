@@ -12,9 +12,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp
          "-mcode-object-version=5", "-Wall", "-Wno-unused-function", "-I/opt/rocm/include"]
 
 
-def build(verbose=False, force=False):
+def build(verbose=False, force=False, jobs=None):
     """CMS_BOUND_ANALYSIS=1 in the environment builds the bound-analysis
-    variant (kernel parts switchable by CMS_COS_MODE; scripts/cos_modes.sh)."""
+    variant (kernel parts switchable by CMS_COS_MODE; scripts/cos_modes.sh).
+    Translation units compile in parallel (objects under mahout_amd/build/),
+    then link into the one in-tree shared object."""
+    from concurrent.futures import ThreadPoolExecutor
     analysis = os.environ.get("CMS_BOUND_ANALYSIS") == "1"
     force = force or analysis
     srcs = [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
@@ -22,9 +25,24 @@ def build(verbose=False, force=False):
     deps.append(os.path.join(HERE, "..", "include", "mahout_cms.h"))
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
         return OUT
-    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + (["-DCMS_BOUND_ANALYSIS"] if analysis else []) + srcs + ["-o", OUT,
-                                                                                            "-L/opt/rocm/lib", "-lrccl",
-                                                   "-Wl,-rpath,/opt/rocm/lib"]
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    extra = ["-DCMS_BOUND_ANALYSIS"] if analysis else []
+    cflags = [f for f in FLAGS if f != "-shared"]
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        cmd = ["/opt/rocm/bin/hipcc"] + cflags + extra + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        return obj
+
+    jobs = jobs or min(len(srcs), max(1, min(16, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + [
+        "-o", OUT, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -221,6 +221,7 @@ static int require_finalized(cms_handle* h) {
 
 int coll_allreduce_u64(cms_handle* h, uint64_t* d_buf, int64_t count) {
   if (count <= 0) return CMS_OK;
+  ++h->coll_calls;
   if (h->ext_comm) {
     CMS_HIP(hipStreamSynchronize(h->stream));
     const int r = h->x_allreduce(d_buf, count, h->x_user);
@@ -234,6 +235,7 @@ int coll_allreduce_u64(cms_handle* h, uint64_t* d_buf, int64_t count) {
 
 int coll_allgather(cms_handle* h, const void* d_send, void* d_recv, int64_t bytes) {
   if (bytes <= 0) return CMS_OK;
+  ++h->coll_calls;
   if (h->ext_comm) {
     CMS_HIP(hipStreamSynchronize(h->stream));
     const int r = h->x_allgather(d_send, d_recv, bytes, h->x_user);
@@ -296,6 +298,9 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   const bool f64 = p->counter_type == CMS_COUNTER_F64;
   if (f64 && !per_owner && p->width > 16384) return set_error(CMS_E_PARAM, "fp64 counters: width must be <= 16384 (LDS sketch row)");
   if (p->frac_bits < 0 || p->frac_bits > 31) return set_error(CMS_E_PARAM, "frac_bits must be in [0, 31]");
+  if (p->flags & ~CMS_FLAG_COLLECTIVE_SINGLE_RANK) return set_error(CMS_E_PARAM, "unknown flags 0x%x", p->flags);
+  if (f64 && (p->flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK))
+    return set_error(CMS_E_PARAM, "fp64 counters are single-GPU: no collective path");
   cms_handle* h = new (std::nothrow) cms_handle();
   if (!h) return set_error(CMS_E_OOM, "host allocation failed");
   h->p = *p;
@@ -746,7 +751,7 @@ int cms_comm_init(cms_handle* h, const void* unique_id, int32_t rank, int32_t wo
   h->ext_comm = false;
   h->rank = rank;
   h->world = world;
-  if (world == 1) return CMS_OK;
+  if (world == 1 && !(h->p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK)) return CMS_OK;  // detached: single-GPU path
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
   ncclResult_t r = ncclCommInitRank(&h->comm, world, id, rank);
@@ -766,9 +771,11 @@ int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allr
     (void)ncclCommDestroy(h->comm);
     h->comm = nullptr;
   }
+  if (world == 1 && (h->p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK) && (!allreduce || !allgather))
+    return set_error(CMS_E_PARAM, "null transport function");
   h->rank = world > 1 ? rank : 0;
   h->world = world;
-  h->ext_comm = world > 1;
+  h->ext_comm = world > 1 || (h->p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK);
   h->x_allreduce = allreduce;
   h->x_allgather = allgather;
   h->x_user = user;
@@ -1491,6 +1498,9 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->nibble_rows = forms[3];
   out->crumb_rows = forms[4];
   out->bit_rows = forms[5];
+  out->collective_calls = h->coll_calls;
+  out->comm_kind = h->comm ? 1 : h->ext_comm ? 2 : 0;
+  out->device = h->device;
   return CMS_OK;
 }
 

@@ -1113,7 +1113,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     // accumulating: every touched u8 / nibble row becomes u16 first (the build
     // adds into u16 or u32 rows); untouched rows are skipped by the build when
     // their norms are current, otherwise every form row is widened
-    if (accumulate && (rc0 = widen_rows(h, h->norms_valid ? bound.as<uint64_t>() : nullptr, h->d_row_mass, true)))
+    if (accumulate &&
+        (rc0 = widen_rows(h, h->norms_valid ? bound.as<uint64_t>() : nullptr, h->d_row_mass, true, d_lo, d_hi)))
       return rc0;
   }
   {
@@ -1189,9 +1190,22 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          mid_list, lcnt);
       CMS_HIP(hipGetLastError());
       hipStream_t side = h->side_stream ? h->side_stream : h->stream;
+      // once the side stream has forked, every exit (error returns included)
+      // joins it back: the caller's next work on h->stream may reuse or free
+      // the buffers the side kernels are still writing
+      struct SideJoin {
+        cms_handle* h;
+        hipStream_t side;
+        bool armed = false;
+        ~SideJoin() {
+          if (armed && hipEventRecord(h->ev_join2, side) == hipSuccess)
+            (void)hipStreamWaitEvent(h->stream, h->ev_join2, 0);
+        }
+      } join{h, side};
       if (side != h->stream) {
         CMS_HIP(hipEventRecord(h->ev_fork2, h->stream));
         CMS_HIP(hipStreamWaitEvent(side, h->ev_fork2, 0));
+        join.armed = true;
       }
       auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
       const int bit_keys = getenv("CMS_BIT_KEYS") ? atoi(getenv("CMS_BIT_KEYS")) : kBitKeys;  // read per build (tests)
@@ -1218,7 +1232,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)slot_list, (const uint32_t*)lcnt, part,
                          max_hot);
       CMS_HIP(hipGetLastError());
-      if (side != h->stream) {
+      if (join.armed) {
+        join.armed = false;
         CMS_HIP(hipEventRecord(h->ev_join2, side));
         CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join2, 0));
       }

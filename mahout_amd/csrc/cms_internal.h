@@ -255,7 +255,12 @@ struct cms_handle {
   cms_allgather_fn x_allgather = nullptr;
   void* x_user = nullptr;
   bool ext_comm = false;
-  bool multi() const { return world > 1 && (comm != nullptr || ext_comm); }
+  int64_t coll_calls = 0;  // collectives issued through the communicator (cms_stats.collective_calls)
+  // the multi-rank data path: a communicator is attached and either there are
+  // several ranks or the handle asked for the collective path at one rank
+  bool multi() const {
+    return (world > 1 || (p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK)) && (comm != nullptr || ext_comm);
+  }
   // After the first multi-rank finalize every rank holds the summed table; later
   // COO batches are logged here and only the logs are exchanged at the next
   // finalize (each rank applies the other ranks' batches).
@@ -338,9 +343,11 @@ int count_forms(cms_handle* h, int64_t out[6]);  // hot, u16, u8, 4-bit, 2-bit, 
 // place: with d_bound (a u64 upper bound of each row's mass after the write)
 // and old_mass, a touched form row (bound > old mass) is widened when
 // cbound + (bound - old_mass) exceeds its form's capacity, and its cbound grows
-// by the batch's mass; all_touched widens every touched form row; d_bound null
-// widens every form row.
-int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched);
+// by the batch's mass; all_touched widens every touched form row (with d_lo /
+// d_hi, the build's owner spans, a row with keys counts as touched even when
+// its increments add no mass); d_bound null widens every form row.
+int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched,
+               const int64_t* d_lo = nullptr, const int64_t* d_hi = nullptr);
 // per-row counter bounds after a CSR batch (mass in counter units + old_mass)
 // and the rows split over more than `slice` keys (cms_build.hip)
 int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,

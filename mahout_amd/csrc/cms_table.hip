@@ -114,15 +114,20 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 // ---- narrow forms (u8 / 4-bit / 2-bit / 1-bit rows inside their u16 slots) ----
 
 // Rows to widen to u16 before a write (see widen_rows in cms_internal.h).
-__global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int32_t* hidx, uint32_t* cbound,
-                             int64_t n, int all_touched, int32_t* list, uint32_t* cnt) {
+// With span bounds (lo, hi: the accumulate build's owner spans) a row is
+// touched when it has keys -- the build rewrites every such row through its
+// u16 / u32 image even when all its increments are 0 (no mass added).
+__global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int64_t* lo, const int64_t* hi,
+                             const int32_t* hidx, uint32_t* cbound, int64_t n, int all_touched, int32_t* list,
+                             uint32_t* cnt) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = hidx[r];
     if (f >= 0 || f == kFormU16) continue;
     bool need = true;
     if (bound) {
       const uint64_t b = bound[r], m = old_mass ? old_mass[r] : 0ULL;
-      if (b <= m) continue;  // no increment lands on this row
+      const bool has_keys = lo && hi[r] > lo[r];
+      if (b <= m && !has_keys) continue;  // no update lands on this row
       const uint64_t nb = (uint64_t)cbound[r] + (b - m);
       need = all_touched || nb > (uint64_t)form_cap(f);
       if (!need) cbound[r] = (uint32_t)nb;  // <= the form's capacity
@@ -183,7 +188,8 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
   }
 }
 
-int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched) {
+int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched, const int64_t* d_lo,
+               const int64_t* d_hi) {
   if (!h->forms_ok) return CMS_OK;
   const int64_t n = h->n;
   CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
@@ -191,8 +197,8 @@ int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass,
   uint32_t* cnt = reinterpret_cast<uint32_t*>(list + n);
   CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-  hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, h->d_hidx, h->d_cbound, n,
-                     all_touched ? 1 : 0, list, cnt);
+  hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, d_lo, d_hi, h->d_hidx,
+                     h->d_cbound, n, all_touched ? 1 : 0, list, cnt);
   // one workgroup per row, looping: the count stays on the device
   hipLaunchKernelGGL(k_widen_rows, dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(256), 0, h->stream, list, cnt,
                      h->tview(), h->d_hidx);

@@ -72,9 +72,11 @@ def comm_unique_id():
 
 class SketchTable:
     def __init__(self, num_owners, depth=5, width=4096, seed=42, weighted=False, device=-1, owner_ids=None,
-                 per_owner=False, frac_bits=0, counters="u32"):
+                 per_owner=False, frac_bits=0, counters="u32", collective_single_rank=False):
         """counters: "u32" (exact integer counters in units of 2^-frac_bits) or
-        "f64" (DoubleCountMinSketch's fp64 counters for any float preference)."""
+        "f64" (DoubleCountMinSketch's fp64 counters for any float preference).
+        collective_single_rank: CMS_FLAG_COLLECTIVE_SINGLE_RANK (a one-rank
+        comm_init still takes the multi-rank data path)."""
         lib = _lib.load()
         p = _lib.CmsParams()
         check(lib.cms_params_init(ctypes.byref(p)))
@@ -86,17 +88,17 @@ class SketchTable:
         p.weighting = _lib.CMS_WEIGHTED if weighted else _lib.CMS_UNWEIGHTED
         p.device = device
         p.frac_bits = frac_bits
+        p.flags = _lib.CMS_FLAG_COLLECTIVE_SINGLE_RANK if collective_single_rank else 0
         h = ctypes.c_void_p()
         create = lib.cms_create_per_owner if per_owner else lib.cms_create
         check(create(ctypes.byref(p), ctypes.byref(h)))
         self.per_owner = per_owner
         self.counters = counters
-        if device < 0:  # the handle took the current HIP device at creation
-            import torch
-            device = torch.cuda.current_device()
-        self.device = int(device)
         self._lib = lib
         self._h = h
+        if device < 0:  # the device the library chose (hipGetDevice at creation), not torch's guess
+            device = self.stats()["device"]
+        self.device = int(device)
         self.num_owners = num_owners
         self.depth = depth
         self.width = width

@@ -155,3 +155,53 @@ def test_forms_point_queries_and_device_read(oracle, monkeypatch, bit_keys):
             ref[r] = oracle.cosine_cm(exp2[r], exp2[r])
             assert _same(s1, ref), r
         torch.cuda.synchronize()
+
+
+def test_accumulate_build_zero_valued_form_rows(oracle):
+    """A CSR batch into a live table with forms (the accumulate build) where
+    narrow owners' keys all carry 0.0: the build rewrites every owner that has
+    keys through its u16 image, so those rows must be widened first even though
+    the batch adds no mass to them (update(key, 0.0) leaves the counters as
+    they were, DoubleCountMinSketch.java:72-80)."""
+    n, d, w = 1500, 4, 256
+    items, users = _stream(n, 5000, 300_000, seed=11)
+    a, b = oracle.hash_params(42, d)
+    exp = oracle.build_table(n, d, w, a, b, items, users)
+    with _handle(n, d, w, True) as t:
+        t.ingest(items, users)
+        t.finalize()
+        st = t.stats()
+        assert st["bit_rows"] > 0 and st["crumb_rows"] > 0 and st["nibble_rows"] > 0, st
+        mx = exp.max(axis=(1, 2))
+        # owners in the 1-/2-bit, 4-bit and u8 forms
+        picks = [np.flatnonzero(mx == 1)[:2], np.flatnonzero((mx >= 2) & (mx <= 3))[:2],
+                 np.flatnonzero((mx >= 4) & (mx <= 15))[:2], np.flatnonzero((mx >= 16) & (mx <= 255))[:2]]
+        zero_rows = np.concatenate(picks).astype(np.int64)
+        assert zero_rows.size >= 6
+        rng = np.random.Generator(np.random.PCG64(5))
+        rows, keys, vals = [], [], []
+        for r in range(n):
+            if r in set(zero_rows.tolist()):
+                k = rng.integers(0, 5000, 7)
+                rows.append(np.full(k.size, r)), keys.append(k), vals.append(np.zeros(k.size))
+            elif r % 5 == 0:
+                k = rng.integers(0, 5000, 3)
+                rows.append(np.full(k.size, r)), keys.append(k), vals.append(np.ones(k.size))
+        br = np.concatenate(rows).astype(np.int64)
+        bk = np.concatenate(keys).astype(np.int64)
+        bv = np.concatenate(vals).astype(np.float32)
+        off = np.zeros(n + 1, np.int64)
+        np.add.at(off, br + 1, 1)
+        off = np.cumsum(off)
+        t.ingest_csr(off, bk, bv)  # rows ascending already: the CSR order
+        t.finalize()
+        exp2 = oracle.build_table(n, d, w, a, b, np.concatenate([items, br]), np.concatenate([users, bk]),
+                                  np.concatenate([np.ones(items.size, np.float32), bv]))
+        got = t.read_counters()
+        assert np.array_equal(got[zero_rows], exp2[zero_rows])
+        assert np.array_equal(got, exp2)
+        for r in zero_rows[::2]:
+            s1 = t.similarities(int(r), np.arange(n))
+            ref = oracle.similarities_row(exp2, int(r))
+            ref[r] = oracle.cosine_cm(exp2[r], exp2[r])
+            assert _same(s1, ref), r
