@@ -304,6 +304,16 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   cms_handle* h = new (std::nothrow) cms_handle();
   if (!h) return set_error(CMS_E_OOM, "host allocation failed");
   h->p = *p;
+  {  // tunables: the environment is read here and nowhere else
+    auto flag = [](const char* name) { const char* e = getenv(name); return e && *e && std::strcmp(e, "0") != 0; };
+    auto num = [](const char* name, int dflt) { const char* e = getenv(name); return e && *e ? atoi(e) : dflt; };
+    h->tune.bit_keys = num("CMS_BIT_KEYS", h->tune.bit_keys);
+    h->tune.crumb_keys = num("CMS_CRUMB_KEYS", h->tune.crumb_keys);
+    h->tune.forms = !flag("CMS_NO_FORMS");
+    h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
+    h->tune.fp4 = !flag("CMS_NO_FP4");
+    h->tune.mls = !flag("CMS_NO_MLS");
+  }
   h->per_owner = per_owner;
   h->f64 = f64;
   if (f64) h->p.frac_bits = 0;  // raw (double) float preferences
@@ -370,7 +380,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   h->empty = true;
   h->norms_valid = false;
   // u8 / nibble row forms need 64-B aligned slots and 16-B nibble rows
-  h->forms_ok = !per_owner && !f64 && h->dw % 32 == 0 && !getenv("CMS_NO_FORMS");
+  h->forms_ok = !per_owner && !f64 && h->dw % 32 == 0 && h->tune.forms;
   *out = h;
   return CMS_OK;
 }

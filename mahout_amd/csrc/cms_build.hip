@@ -49,22 +49,27 @@ __device__ __forceinline__ uint32_t nibbles8(uint32_t lo, uint32_t hi) {
   return __builtin_amdgcn_perm(hi | (hi >> 4), lo | (lo >> 4), 0x06040200u);
 }
 
-__global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int64_t slice, int32_t* row_hot, HotInfo* hot,
-                             int2* extra_map, uint32_t* counters /* [0]=hot rows [1]=extra slices */,
-                             uint64_t* norm, uint32_t* rowmax, int depth) {
+// Rows with more than `split` keys are hot (u32 slot, built in slices of
+// `slice` keys); slices [first, ns) of each are listed in extra_map (first =
+// 1: slice 0 is built by the row's own k_build_rows block; first = 0: every
+// slice by k_build_slices).
+__global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int64_t split, int64_t slice,
+                             int first, int32_t* row_hot, HotInfo* hot, int2* extra_map,
+                             uint32_t* counters /* [0]=hot rows [1]=mapped slices */, uint64_t* norm, uint32_t* rowmax,
+                             int depth) {
   const int lane = (int)__lane_id();
   for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nrows; base += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = base + threadIdx.x;
     const int64_t c = r < nrows ? hi_[r] - lo_[r] : 0;
-    const bool is_hot = c > slice;
+    const bool is_hot = c > split;
     if (r < nrows && !is_hot) row_hot[r] = -1;
     int32_t ns = 0;
     uint32_t hidx = 0, e0 = 0;
     if (is_hot) {
       ns = (int32_t)((c + slice - 1) / slice);
-      // one 64-bit atomic claims the hot index (low word) and the extra slices (high word)
+      // one 64-bit atomic claims the hot index (low word) and the mapped slices (high word)
       const unsigned long long old =
-          atomicAdd(reinterpret_cast<unsigned long long*>(counters), ((unsigned long long)(ns - 1) << 32) | 1ULL);
+          atomicAdd(reinterpret_cast<unsigned long long*>(counters), ((unsigned long long)(ns - first) << 32) | 1ULL);
       hidx = (uint32_t)old;
       e0 = (uint32_t)(old >> 32);
       hot[hidx] = HotInfo{r, ns, (int32_t)e0};
@@ -81,7 +86,7 @@ __global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nro
       const int32_t nsl = __builtin_amdgcn_readlane(ns, l);
       const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hidx, l);
       const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)e0, l);
-      for (int32_t sl = 1 + lane; sl < nsl; sl += 64) extra_map[el + sl - 1] = make_int2((int)hl, sl);
+      for (int32_t sl = first + lane; sl < nsl; sl += 64) extra_map[el + sl - first] = make_int2((int)hl, sl);
     }
   }
 }
@@ -155,12 +160,12 @@ constexpr size_t kFormLdsMax = 64 * 1024;  // byte-form owners: [d][w] bytes of 
 #endif
 template <int SV>
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(CMS_BUILD_WAVES, 8))) void k_build_rows(
-    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
+    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, int64_t nrows, HashParams hp,
     int64_t slice,
     const int32_t* row_hot, const HotInfo* hot, const int2* extra_map, const uint32_t* counters, int64_t emax,
     TableView tv, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int accumulate,
     int slices_done, const uint64_t* bound, int forms, int skip_untouched, int32_t* hidx_w, uint32_t* cbound,
-    const int32_t* rows_list, const uint32_t* rows_cnt, uint16_t* part, int64_t hcap) {
+    const int32_t* rows_list, const uint32_t* rows_cnt) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row [w] u32, or a byte-form owner's [d][w] u8
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -189,6 +194,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
     }
     lo = lo_[row];
     atomic_mode = row_hot[row] >= 0;
+    if (atomic_mode && slices_done) return;  // a split row: all its slices ran in k_build_slices
     hi = atomic_mode ? lo + slice : hi_[row];
     // accumulating into a live table with current norms: a row without keys
     // keeps its counters, norms and form (a form row may only be touched
@@ -203,15 +209,6 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
   uint32_t* dst = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
   uint16_t* dst16 = tv.t16 + row * dw;
   const bool load_old = accumulate && !atomic_mode;
-  // slices with partial rows (part: unit increments, slice << frac_bits <
-  // 2^16): a slice writes its d x w counts as a u16 partial row with plain
-  // 16-B stores (slice 0 at the row's hot index, extra slice e at hcap + e);
-  // k_hot_reduce sums them into the slot row -- no global atomics here
-  const bool to_part = atomic_mode && part != nullptr;
-  if (to_part) {
-    dst16 = part + (blockIdx.x < emax ? hcap + (int64_t)blockIdx.x : (int64_t)row_hot[row]) * dw;
-    dst = nullptr;
-  }
   if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
   if (tid == 0) {
     s_mass = 0ULL;
@@ -236,13 +233,12 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
       kp[k] = 0;
       ik[k] = 0;
       if (i < hi) {
-        int64_t key = keys[i];
         uint32_t inc;
         if (!load_inc(vals, i, inc, hp.frac_bits)) {
           badv = true;
           inc = 0;
         }
-        kp[k] = reduce_key(key);
+        kp[k] = keys.at(i);
         ik[k] = inc;
         mass += inc;
       }
@@ -274,12 +270,12 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
         }
     } else {
       for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
-        int64_t kk[4];
+        uint64_t kk[4];
         uint32_t inc4[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           int64_t i = base + tid + (int64_t)u * kBuildThreads;
-          kk[u] = i < hi ? keys[i] : 0;
+          kk[u] = i < hi ? keys.at(i) : 0;
           inc4[u] = 0;
           if (i < hi) {
             uint32_t inc;
@@ -293,7 +289,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (inc4[u]) {
-            const uint64_t kr = reduce_key(kk[u]);
+            const uint64_t kr = kk[u];
             atomicAdd(&lds[bucket(hp, d, kr)], inc4[u]);
             if (two) atomicAdd(&lds[bucket(hp, d + 1, kr)], inc4[u] << 16);
           }
@@ -305,14 +301,14 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
     // ---- write-out of row d, zero/load the slot for row d+1, sum of squares ----
     const int64_t rofs = (int64_t)d * w;
     const bool more = load_old && d + 1 < hp.depth;
-    if (atomic_mode && two && !to_part) {  // paired slice rows: low halves row d, high halves row d + 1
+    if (atomic_mode && two) {  // paired slice rows: low halves row d, high halves row d + 1
       for (int j = tid; j < w; j += kBuildThreads) {
         const uint32_t v = lds[j];
         lds[j] = 0u;
         if (v & 0xFFFFu) atomicAdd(dst + rofs + j, v & 0xFFFFu);
         if (v >> 16) atomicAdd(dst + rofs + w + j, v >> 16);
       }
-    } else if (atomic_mode && !to_part) {  // slices of a split row: always a hot (u32) row
+    } else if (atomic_mode) {  // slices of a split row: always a hot (u32) row
       for (int j = tid; j < w; j += kBuildThreads) {
         uint32_t v = lds[j];
         lds[j] = 0u;
@@ -556,7 +552,7 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 // persistent grid walks the device-side list.
 template <int SV>
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(CMS_BUILD_WAVES, 8))) void k_build_mid(
-    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
+    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
     uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row, up to w u16 counters
@@ -586,7 +582,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
             badv = true;
             inc = 0;
           }
-          kp[k] = reduce_key(keys[i]);
+          kp[k] = keys.at(i);
           ik[k] = inc;
           mass += inc;
         }
@@ -628,12 +624,12 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
             if (ik[k]) add(kp[k], ik[k]);
         } else {
           for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
-            int64_t kk[4];
+            uint64_t kk[4];
             uint32_t inc4[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int64_t i = base + tid + (int64_t)u * kBuildThreads;
-              kk[u] = i < hi ? keys[i] : 0;
+              kk[u] = i < hi ? keys.at(i) : 0;
               inc4[u] = 0;
               if (i < hi) {
                 uint32_t inc;
@@ -646,7 +642,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              if (inc4[u]) add(reduce_key(kk[u]), inc4[u]);
+              if (inc4[u]) add(kk[u], inc4[u]);
               if (d == 0 && level == 0) mass += inc4[u];
             }
           }
@@ -702,12 +698,11 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
 // maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
 // one wave's LDS operations execute in program order.
 constexpr int kNibWaves = 4;
-// owners with at most kBitKeys keys try 1-bit rows first, with at most
-// kCrumbKeys 2-bit rows (CMS_BIT_KEYS / CMS_CRUMB_KEYS override)
-constexpr int kBitKeys = 64, kCrumbKeys = 256;
+// owners with at most Tunables::bit_keys (64) keys try 1-bit rows first, with
+// at most crumb_keys (256) 2-bit rows
 template <int SV>
 __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
-    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, int64_t nrows, HashParams hp,
+    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, int64_t nrows, HashParams hp,
     const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
     uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt, int bit_keys,
     int crumb_keys) {
@@ -734,7 +729,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
         badv = true;
         inc = 0;
       }
-      kp[k] = reduce_key(keys[i]);
+      kp[k] = keys.at(i);
       ik[k] = inc;
       mass += inc;
     }
@@ -803,7 +798,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
 // rows.  A persistent grid walks the device-side list (no host count).
 template <int SV>
 __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
-    const int64_t* lo_, const int64_t* hi_, const int64_t* keys, const float* vals, HashParams hp,
+    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
     uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
   extern __shared__ __align__(16) uint32_t lds[];  // [d][w] bytes
@@ -836,7 +831,7 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
           badv = true;
           inc = 0;
         }
-        kp[k] = reduce_key(keys[i]);
+        kp[k] = keys.at(i);
         ik[k] = inc;
         mass += inc;
       }
@@ -883,47 +878,62 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
   }
 }
 
-// The extra slices of the hot owners with unit increments (every slice of
-// `slice` keys counts at most slice << frac_bits < 2^16 per bucket): each key
-// is read and reduced mod p ONCE and counted into all d sketch rows at once,
-// two u16 counters per LDS word (d * w / 2 words), then the partial rows are
-// added to the owner's u32 slot row with coalesced atomics.  In k_build_rows
-// a slice walks its 8192+ keys once per sketch row (they do not fit its
-// register cache).  Experiment (CMS_SLICES_KERNEL=1): bit-exact, but slower,
-// since this launch cannot overlap the row build that follows it.
-__global__ __launch_bounds__(256) void k_build_slices(const int64_t* lo_, const int64_t* hi_, const int64_t* keys,
-                                                      HashParams hp, int64_t slice, const HotInfo* hot,
-                                                      const int2* extra_map, const uint32_t* counters, TableView tv,
-                                                      uint64_t* row_mass, uint32_t* flags) {
-  extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] packed u16 pairs
+// Hot (split) owners with unit increments: one workgroup per SLICE of up to
+// kHotSlice keys, all d sketch rows counted at once in an LDS image of u16
+// counters ([d][w] u16: a slice of < 2^16 >> frac_bits unit increments cannot
+// carry out of one), so each key is read and hashed ONCE (k_build_rows walks
+// a slice's keys once per pair of sketch rows).  The image is added into the
+// owner's u32 slot row (zeroed by promote_rows, or the old counters of an
+// accumulating build) with 64-bit global atomics, two adjacent counters per
+// add: a counter stays below its row mass < 2^32, so the low half never
+// carries into the high one.  Bigger slices than k_build_rows' mean fewer
+// dense slice images added into the slots.  No static LDS: two 80 KB images
+// share a CU at d = 5, w = 8192.
+constexpr int kSliceThreads = 512;
+constexpr int64_t kHotSlice = 65535;  // keys per slice (u16 image, frac_bits 0)
+__global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* lo_, const int64_t* hi_, Keys keys,
+                                                                HashParams hp, int64_t slice, const HotInfo* hot,
+                                                                const int2* smap, const uint32_t* counters,
+                                                                TableView tv, uint64_t* row_mass, uint32_t* flags) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] words, two u16 counters each
   if (blockIdx.x >= counters[1]) return;
   const int tid = threadIdx.x;
+  const int2 m = smap[blockIdx.x];
+  const int64_t row = hot[m.x].row;
+  const int64_t lo = lo_[row] + (int64_t)m.y * slice;
+  const int64_t end = min(hi_[row], lo + slice);
   const int w = (int)hp.width;
   const int64_t dw = (int64_t)hp.depth * w;
   const int words = (int)(dw >> 1);
-  const int2 m = extra_map[blockIdx.x];
-  const int64_t row = hot[m.x].row;
-  const int64_t lo = lo_[row] + (int64_t)m.y * slice;
-  const int64_t hi = min(hi_[row], lo + slice);
-  for (int j = tid; j < words; j += 256) lds[j] = 0u;
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+  for (int j = tid; j < (words >> 2); j += kSliceThreads) l4[j] = make_uint4(0, 0, 0, 0);
+  for (int j = (words & ~3) + tid; j < words; j += kSliceThreads) lds[j] = 0u;
   __syncthreads();
   const uint32_t one = 1u << hp.frac_bits;
-  for (int64_t i = lo + tid; i < hi; i += 256) {
-    const uint64_t kp = reduce_key(keys[i]);
-    for (int r = 0; r < hp.depth; ++r) {
-      const uint32_t c = (uint32_t)r * (uint32_t)w + bucket(hp, r, kp);
-      atomicAdd(&lds[c >> 1], one << ((c & 1u) * 16u));
+  for (int64_t base = lo; base < end; base += 4 * kSliceThreads) {
+    uint64_t kk[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // four key loads in flight
+      const int64_t i = base + tid + (int64_t)u * kSliceThreads;
+      kk[u] = i < end ? keys.at(i) : ~0ULL;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (kk[u] == ~0ULL) continue;
+      for (int r = 0; r < hp.depth; ++r) {
+        const uint32_t c = (uint32_t)r * (uint32_t)w + bucket(hp, r, kk[u]);
+        atomicAdd(&lds[c >> 1], one << ((c & 1u) << 4));
+      }
     }
   }
   __syncthreads();
-  uint32_t* dst = tv.hot + (int64_t)tv.hidx[row] * dw;
-  for (int j = tid; j < words; j += 256) {
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(tv.hot + (int64_t)tv.hidx[row] * dw);
+  for (int j = tid; j < words; j += kSliceThreads) {
     const uint32_t v = lds[j];
-    if (v & 0xFFFFu) atomicAdd(dst + 2 * j, v & 0xFFFFu);
-    if (v >> 16) atomicAdd(dst + 2 * j + 1, v >> 16);
+    if (v) atomicAdd(dst + j, (unsigned long long)(v & 0xFFFFu) | ((unsigned long long)(v >> 16) << 32));
   }
   if (tid == 0) {
-    const uint64_t tm = (uint64_t)(hi - lo) * one;
+    const uint64_t tm = (uint64_t)(end - lo) * one;
     const unsigned long long old = atomicAdd((unsigned long long*)&row_mass[row], (unsigned long long)tm);
     if (old + tm >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
   }
@@ -956,94 +966,6 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
   }
 }
 
-// The split rows' slot counters from their slices' u16 partial rows (slice 0
-// at part[h], slice s >= 1 at part[hcap + e0 + s - 1]), plus the old counters
-// when accumulating; the same pass derives the rows' sums of squares and
-// largest counter (k_hot_norms' job).  Block (h, sketch row, 512-counter
-// chunk): thread t sums 8 counters (one 16-B load per slice) over the slices
-// s = t / 64 mod 4, the four waves' sums meet in LDS.  Counter sums are
-// bounded by the row mass (< 2^32, checked by the build).
-constexpr int kRedChunk = 512;
-__global__ __launch_bounds__(256) void k_hot_reduce(const HotInfo* hot, const uint32_t* counters, HashParams hp,
-                                                    const uint16_t* part, int64_t hcap, TableView tv, int accumulate,
-                                                    uint64_t* norm, uint32_t* rowmax) {
-  __shared__ uint4 red[3][64][2];
-  const uint32_t nhot = counters[0];
-  const int w = (int)hp.width;
-  const int64_t dw = tv.dw;
-  const int d = blockIdx.y;
-  const int j0 = blockIdx.z * kRedChunk + (threadIdx.x & 63) * 8;  // this thread's 8 counters
-  const int q = threadIdx.x >> 6;
-  for (uint32_t hb = blockIdx.x; hb < nhot; hb += gridDim.x) {
-    const HotInfo hi = hot[hb];
-    const int64_t off = (int64_t)d * w + j0;
-    uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (j0 < w) {
-      auto add = [&](const u32x4_t v) {
-        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          s[2 * c] += x[c] & 0xFFFFu;
-          s[2 * c + 1] += x[c] >> 16;
-        }
-      };
-      auto src = [&](int sl) {
-        const int64_t pi = sl == 0 ? (int64_t)hb : hcap + hi.e0 + sl - 1;
-        return reinterpret_cast<const u32x4_t*>(part + pi * dw + off);
-      };
-      int sl = q;
-      for (; sl + 12 < hi.nslices; sl += 16) {  // four loads in flight
-        const u32x4_t a = __builtin_nontemporal_load(src(sl)), b = __builtin_nontemporal_load(src(sl + 4));
-        const u32x4_t c = __builtin_nontemporal_load(src(sl + 8)), e = __builtin_nontemporal_load(src(sl + 12));
-        add(a);
-        add(b);
-        add(c);
-        add(e);
-      }
-      for (; sl < hi.nslices; sl += 4) add(__builtin_nontemporal_load(src(sl)));
-    }
-    if (q > 0) {
-      red[q - 1][threadIdx.x & 63][0] = make_uint4(s[0], s[1], s[2], s[3]);
-      red[q - 1][threadIdx.x & 63][1] = make_uint4(s[4], s[5], s[6], s[7]);
-    }
-    __syncthreads();
-    uint64_t sq = 0;
-    uint32_t vmax = 0;
-    if (q == 0 && j0 < w) {
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const uint4 a = red[p][threadIdx.x][0], b = red[p][threadIdx.x][1];
-        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
-        s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
-      }
-      uint4* dst = reinterpret_cast<uint4*>(tv.hot + (int64_t)tv.hidx[hi.row] * dw + off);
-      if (accumulate) {
-        const uint4 a = dst[0], b = dst[1];
-        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
-        s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
-      }
-      dst[0] = make_uint4(s[0], s[1], s[2], s[3]);
-      dst[1] = make_uint4(s[4], s[5], s[6], s[7]);
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        sq = sat_add(sq, (uint64_t)s[c] * s[c]);
-        vmax = max(vmax, s[c]);
-      }
-    }
-    if (q == 0) {
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-      sq = wave_sum_u64_sat(sq);
-      if (threadIdx.x == 0) {
-        if (vmax) atomicMax(&rowmax[hi.row], vmax);
-        if (sq > (1ULL << 60)) sq = 1ULL << 60;
-        if (sq) atomicAdd((unsigned long long*)&norm[hi.row * hp.depth + d], (unsigned long long)sq);
-      }
-    }
-    __syncthreads();  // red[] is rewritten by the next row
-  }
-}
-
 int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,
                int64_t slice, uint64_t* bound, uint8_t* force) {
   const int64_t n = h->n;
@@ -1059,21 +981,29 @@ int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const fl
 
 int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs) {
   h->rf_valid = false;  // CSR batches do not mark touched owners: the next refresh is a full job
-  return ingest_spans_device(h, d_off, d_off + 1, d_key, d_val, npairs);
+  return ingest_spans_device(h, d_off, d_off + 1, d_key, nullptr, d_val, npairs);
 }
 
-int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const int64_t* d_key, const float* d_val,
-                        int64_t npairs) {
+int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const int64_t* d_key,
+                        const uint32_t* d_tok, const float* d_val, int64_t npairs) {
+  const Keys keys{d_key, d_tok};
   const int64_t n = h->n;
   int rc0;
   const int accumulate = h->empty ? 0 : 1;
-  // keys per build workgroup of a split (hot) owner: 8192, or 16384 for rows
-  // of 8192+ counters (config 3: build 19.4 -> 18.5 ms; config 2 prefers 8192)
-  int64_t kSlice = cms::kSlice;
-  if (h->p.width >= 8192) kSlice *= 2;
-  if (const char* e = getenv("CMS_SLICE_KEYS")) kSlice = std::max<int64_t>(1024, atoll(e));
-  const int64_t max_hot = std::min<int64_t>(n, npairs / kSlice + 1);
-  const int64_t emax = npairs / kSlice + 1;
+  // Rows with more than kSplit keys are hot: a u32 slot, built in slices.
+  // kSplit: 8192 keys, or 16384 for rows of 8192+ counters (config 3: build
+  // 19.4 -> 18.5 ms; config 2 prefers 8192).
+  int64_t kSplit = cms::kSlice;
+  if (h->p.width >= 8192) kSplit *= 2;
+  // Unit increments whose [d][w] u16 image fits a workgroup's LDS: the
+  // slices (every one, slice 0 included) run on k_build_slices, kHotSlice
+  // keys each, one key pass.  Otherwise (weighted increments, wide shapes)
+  // k_build_rows builds slices of kSplit keys, a pass per pair of sketch rows.
+  const size_t img_lds = (size_t)h->dw * 2;
+  const bool fast_slices = !d_val && (h->dw % 8) == 0 && img_lds <= 80 * 1024 && h->hp.frac_bits < 16;
+  const int64_t kSliceKeys = fast_slices ? (kHotSlice >> h->hp.frac_bits) : kSplit;
+  const int64_t max_hot = std::min<int64_t>(n, npairs / kSplit + 1);
+  const int64_t emax = npairs / kSliceKeys + max_hot + 1;  // mapped slices
   const size_t sz_rowhot = (sizeof(int32_t) * (size_t)n + 15) & ~size_t(15);
   const size_t sz_hot = (sizeof(HotInfo) * (size_t)max_hot + 15) & ~size_t(15);
   const size_t sz_extra = sizeof(int2) * (size_t)emax;
@@ -1082,7 +1012,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   int32_t* row_hot = reinterpret_cast<int32_t*>(base);
   HotInfo* hot = reinterpret_cast<HotInfo*>(base + sz_rowhot);
   int2* extra_map = reinterpret_cast<int2*>(base + sz_rowhot + sz_hot);
-  uint32_t* counters = h->d_flags + 4;  // [4..7]: hot rows, extra slices (one u64 atomic), spare
+  uint32_t* counters = h->d_flags + 4;  // [4..7]: hot rows, mapped slices (one u64 atomic), spare
   CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
   // table layout: rows that could reach 2^16, and split rows, get u32 slots
   {
@@ -1092,21 +1022,21 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     DevBuf& force = h->ws_force;
     CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1)));
     CMS_HIP(force.ensure((size_t)std::max<int64_t>(n, 1)));
-    if ((rc0 = row_bounds(h, d_lo, d_hi, d_val, accumulate ? h->d_row_mass : nullptr, kSlice, bound.as<uint64_t>(),
+    if ((rc0 = row_bounds(h, d_lo, d_hi, d_val, accumulate ? h->d_row_mass : nullptr, kSplit, bound.as<uint64_t>(),
                           force.as<uint8_t>())))
       return rc0;
     // A fresh build with implicit (unit) increments: a row needs a slot when
-    // it is split into slices (more than kSlice keys: at most
-    // npairs / (kSlice + 1) rows) or its mass reaches 2^16 (at most
-    // total / 2^16 rows; with 2^(16 - s) > kSlice keys such a row is split
-    // anyway) -- a bound the host knows without reading anything back.
-    // Reserving costs slot memory, so only a bound worth at most 2 GB of
-    // slots takes this path; a larger job reads the count back.
+    // it is split (more than kSplit keys: at most npairs / (kSplit + 1) rows)
+    // or its mass reaches 2^16 (at most total / 2^16 rows; with
+    // 2^(16 - s) > kSplit keys such a row is split anyway) -- a bound the host
+    // knows without reading anything back.  Reserving costs slot memory, so
+    // only a bound worth at most 2 GB of slots takes this path; a larger job
+    // reads the count back.
     int64_t max_new = -1;
     if (!accumulate && !d_val && h->hp.frac_bits < 16) {
-      const int64_t split = npairs / (kSlice + 1) + 1;
+      const int64_t split = npairs / (kSplit + 1) + 1;
       const int64_t heavy = (int64_t)(((uint64_t)npairs << h->hp.frac_bits) / kNarrowLimit);
-      const int64_t slots = (int64_t(1) << (16 - h->hp.frac_bits)) > kSlice ? split : split + heavy;
+      const int64_t slots = (int64_t(1) << (16 - h->hp.frac_bits)) > kSplit ? split : split + heavy;
       if ((double)slots * (double)h->dw * 4.0 <= 2.0e9) max_new = slots;
     }
     if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0, max_new))) return rc0;
@@ -1120,62 +1050,36 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   {
     TimedScope ts(h, "build_plan");
     unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-    hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_lo, d_hi, n, kSlice, row_hot, hot, extra_map,
-                       counters, h->d_norm, h->d_rowmax, h->p.depth);
+    hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_lo, d_hi, n, kSplit, kSliceKeys,
+                       fast_slices ? 0 : 1, row_hot, hot, extra_map, counters, h->d_norm, h->d_rowmax, h->p.depth);
     CMS_HIP(hipGetLastError());
-  }
-  // EXPERIMENT (CMS_SLICE_PARTIALS=1, read per call): split rows' slices
-  // write u16 partial rows (plain 16-B stores; unit increments, so a slice
-  // counts at most kSlice << frac_bits < 2^16 per bucket) that k_hot_reduce
-  // sums into the slot rows, instead of adding into them with global atomics.
-  // Measured at config 3 (scripts/ab_env.sh): k_build_rows 8.40 -> 8.18 ms,
-  // but the reduction pass costs 0.53 ms against k_hot_norms' 0.18 ms (it
-  // re-reads 1.9 GB of partials), so the step is 0.13 ms slower; bit-exact
-  // (tests/test_gpu_parity.py runs both).
-  const bool use_part = getenv("CMS_SLICE_PARTIALS") != nullptr && !d_val && (h->p.width % 8) == 0 &&
-                        (kSlice << h->hp.frac_bits) < 65536;
-  uint16_t* part = nullptr;
-  if (use_part) {
-    CMS_HIP(h->ws_slicepart.ensure(sizeof(uint16_t) * (size_t)(max_hot + emax) * (size_t)h->dw));
-    part = h->ws_slicepart.as<uint16_t>();
   }
   // fresh builds may store byte forms: the whole [d][w] byte image in LDS
   const int forms = h->forms_ok && !accumulate && (size_t)h->dw <= kFormLdsMax ? 1 : 0;
   const int skip_untouched = accumulate && h->norms_valid ? 1 : 0;
   const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
+  // k_build_rows: with fast slices it builds only the unsplit slot rows
+  const int64_t row_emax = fast_slices ? 0 : emax;
+  const int slices_done = fast_slices ? 1 : 0;
   {
     TimedScope ts(h, "build_rows");
-    static const int sv = [] {
-      const char* e = getenv("CMS_BUILD_SV");
-      return e ? std::max(0, std::min(2, atoi(e))) : kBuildStoreForm;
-    }();
-    // EXPERIMENT (CMS_SLICES_SIDE=1): the extra slices of the hot owners with
-    // unit increments on k_build_slices (each key read and reduced once for
-    // all d rows; LDS d*w*2 bytes) on a side stream, beside the row builds.
-    // Measured no faster (config 3 build 11.9 -> 12.5 ms, config 2 equal), so
-    // the slices stay in k_build_rows (d/2 passes over their keys).
-    const size_t slice_lds = (size_t)h->p.depth * (size_t)h->p.width * 2;
-    const int slices_done = !use_part && !d_val && (h->p.width % 2) == 0 && (kSlice << h->hp.frac_bits) < 65536 &&
-                            slice_lds <= 96 * 1024 && h->side_stream && getenv("CMS_SLICES_SIDE");
-    if (slices_done) {
+    auto kern = k_build_rows<kBuildStoreForm>;
+    if (fast_slices) {
       static bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)k_build_slices, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_build_slices, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
       (void)attr;
-      CMS_HIP(hipEventRecord(h->ev_fork, h->stream));  // plan, promotion (slot rows zeroed) are done
-      CMS_HIP(hipStreamWaitEvent(h->side_stream, h->ev_fork, 0));
-      hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(256), slice_lds, h->side_stream, d_lo, d_hi, d_key,
-                         h->hp, kSlice, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
+      hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
+                         keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
       CMS_HIP(hipGetLastError());
-      CMS_HIP(hipEventRecord(h->ev_join, h->side_stream));
     }
-    auto kern = sv == 2 ? k_build_rows<2> : sv == 1 ? k_build_rows<1> : k_build_rows<0>;
     if (forms) {
-      // owner classes: slot rows -> k_build_rows (the handle's stream), byte
-      // rows -> k_build_nibbles (+ k_build_bytes for the ones a counter >= 16
-      // sends back) and mid rows -> k_build_mid on the side stream, so the
-      // three classes' kernels overlap (their tails no longer leave CUs idle)
+      // owner classes: slot rows -> k_build_slices / k_build_rows (the
+      // handle's stream), byte rows -> k_build_nibbles (+ k_build_bytes for
+      // the ones a counter >= 16 sends back) and mid rows -> k_build_mid on the
+      // side stream, so the classes' kernels overlap (their tails no longer
+      // leave CUs idle)
       CMS_HIP(h->ws_blist.ensure(sizeof(int32_t) * (size_t)(2 * n + 4)));
       int32_t* slot_list = h->ws_blist.as<int32_t>();
       int32_t* mid_list = slot_list + n;
@@ -1207,30 +1111,26 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
         CMS_HIP(hipStreamWaitEvent(side, h->ev_fork2, 0));
         join.armed = true;
       }
-      auto nk = sv == 2 ? k_build_nibbles<2> : sv == 1 ? k_build_nibbles<1> : k_build_nibbles<0>;
-      const int bit_keys = getenv("CMS_BIT_KEYS") ? atoi(getenv("CMS_BIT_KEYS")) : kBitKeys;  // read per build (tests)
-      const int crumb_keys = getenv("CMS_CRUMB_KEYS") ? atoi(getenv("CMS_CRUMB_KEYS")) : kCrumbKeys;
-      hipLaunchKernelGGL(nk, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)), dim3(64 * kNibWaves),
-                         (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, d_key, d_val, n, h->hp,
-                         row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass,
-                         h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, bit_keys, crumb_keys);
-      auto mk = sv == 2 ? k_build_mid<2> : sv == 1 ? k_build_mid<1> : k_build_mid<0>;
-      hipLaunchKernelGGL(mk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)), dim3(kBuildThreads),
-                         (size_t)h->p.width * 2, side, d_lo, d_hi, d_key, d_val, h->hp, (const int32_t*)mid_list,
-                         (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
-                         h->d_rowmax, h->d_flags);
-      auto bk = sv == 2 ? k_build_bytes<2> : sv == 1 ? k_build_bytes<1> : k_build_bytes<0>;
-      hipLaunchKernelGGL(bk, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
-                         (size_t)h->dw, side, d_lo, d_hi, d_key, d_val, h->hp, redo, redo_cnt, h->tview(),
-                         h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+      hipLaunchKernelGGL(k_build_nibbles<kBuildStoreForm>, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)),
+                         dim3(64 * kNibWaves), (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, keys,
+                         d_val, n, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
+                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
+                         h->tune.crumb_keys);
+      hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
+                         dim3(kBuildThreads), (size_t)h->p.width * 2, side, d_lo, d_hi, keys, d_val, h->hp,
+                         (const int32_t*)mid_list, (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound,
+                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+      hipLaunchKernelGGL(k_build_bytes<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)),
+                         dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,
+                         h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       CMS_HIP(hipGetLastError());
-      // slot rows: at most the slots in use (host-known), plus the extra slices
+      // slot rows: at most the slots in use (host-known), plus the mapped slices
       const int64_t nslot = std::min<int64_t>(n, h->hot_used);
-      hipLaunchKernelGGL(kern, dim3((unsigned)(emax + nslot)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
-                         d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
-                         h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
-                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)slot_list, (const uint32_t*)lcnt, part,
-                         max_hot);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(row_emax + nslot)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi,
+                         keys, d_val, n, h->hp, kSliceKeys, row_hot, hot, extra_map, counters, row_emax, h->tview(),
+                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done,
+                         h->ws_bound.as<uint64_t>(), forms, skip_untouched, h->d_hidx, h->d_cbound,
+                         (const int32_t*)slot_list, (const uint32_t*)lcnt);
       CMS_HIP(hipGetLastError());
       if (join.armed) {
         join.armed = false;
@@ -1238,27 +1138,19 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
         CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join2, 0));
       }
     } else {
-      hipLaunchKernelGGL(kern, dim3((unsigned)(emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, d_key,
-                         d_val, n, h->hp, kSlice, row_hot, hot, extra_map, counters, emax, h->tview(), h->d_row_mass,
-                         h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done, h->ws_bound.as<uint64_t>(), forms,
-                         skip_untouched, h->d_hidx, h->d_cbound, (const int32_t*)nullptr, (const uint32_t*)nullptr, part,
-                         max_hot);
+      hipLaunchKernelGGL(kern, dim3((unsigned)(row_emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, keys,
+                         d_val, n, h->hp, kSliceKeys, row_hot, hot, extra_map, counters, row_emax, h->tview(),
+                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done,
+                         h->ws_bound.as<uint64_t>(), forms, skip_untouched, h->d_hidx, h->d_cbound,
+                         (const int32_t*)nullptr, (const uint32_t*)nullptr);
       CMS_HIP(hipGetLastError());
     }
-    if (slices_done) CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join, 0));  // the slices have landed
   }
   {
     TimedScope ts(h, "hot_norms");
-    if (use_part) {
-      dim3 grid((unsigned)std::min<int64_t>(max_hot, 1024), (unsigned)h->p.depth,
-                (unsigned)((h->p.width + kRedChunk - 1) / kRedChunk));
-      hipLaunchKernelGGL(k_hot_reduce, grid, dim3(256), 0, h->stream, hot, counters, h->hp, part, max_hot, h->tview(),
-                         accumulate, h->d_norm, h->d_rowmax);
-    } else {
-      dim3 grid((unsigned)std::min<int64_t>(max_hot, 256), (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
-      hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
-                         h->d_rowmax);
-    }
+    dim3 grid((unsigned)std::min<int64_t>(max_hot, 256), (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
+    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
+                       h->d_rowmax);
     CMS_HIP(hipGetLastError());
   }
   h->empty = false;

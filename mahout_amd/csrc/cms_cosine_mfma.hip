@@ -957,12 +957,8 @@ int cosine_prepare(cms_handle* h) {
   // fp4 operands need whole 128-B stages of packed counters (256 per stage)
   int fp4_ok = (h->p.width % 256) == 0 ? 1 : 0;
   // stage depth of the symmetric waves = K slice width of their blocked images
-  // (k_cosine_sym stages 64 B; CMS_OLD_SYM=1 keeps k_cosine_big's 128-B waves)
-  h->sym_sw = getenv("CMS_OLD_SYM") ? 128 : sym_stage_bytes();
-  if (const char* e = getenv("CMS_SYM_BK")) h->sym_sw = atoi(e) == 64 ? 64 : 128;
-#ifdef CMS_BOUND_ANALYSIS
-  if (getenv("CMS_NO_FP4")) fp4_ok = 0;
-#endif
+  h->sym_sw = sym_stage_bytes();
+  if (!h->tune.fp4) fp4_ok = 0;
   uint32_t host[8];
   {
     TimedScope ts(h, "limb_prep");
@@ -1185,8 +1181,8 @@ static int launch_big(cms_handle* h, const BigCfg& c, BigArgs g, int ls, int64_t
 
 static BigArgs big_base(cms_handle* h) {
   BigArgs b{};
-  b.noscreen = getenv("CMS_NO_SCREEN") ? 1 : 0;
 #ifdef CMS_BOUND_ANALYSIS
+  b.noscreen = getenv("CMS_NO_SCREEN") ? 1 : 0;
   if (const char* m = getenv("CMS_COS_MODE")) b.mode = atoi(m);
 #endif
   b.perm = h->ws_limbmeta.as<int64_t>();
@@ -1207,7 +1203,6 @@ static BigArgs big_base(cms_handle* h) {
 // room for it next to everything else.
 static bool ensure_i8blk(cms_handle* h) {
   if (h->i8blk_ready) return true;
-  if (getenv("CMS_NO_I8BLK")) return false;
   const int64_t nm = h->n_hot_limb, ns = h->n - nm;
   if (ns <= 0) return false;
   const int64_t blocks = (ns + kImgBlk - 1) / kImgBlk;
@@ -1281,7 +1276,7 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
       const int ls = G.ls, per = 32 / ls;
       const int8_t* vl = G.buf.as<int8_t>();
       TimedScope ts(h, "cosine_mfma_limbs");
-      if (q0 < G.o1 && qend > G.o0 && nm < n && h->i8blk_ready && mls_eligible(h) && !getenv("CMS_NO_MLS")) {
+      if (q0 < G.o1 && qend > G.o0 && nm < n && h->i8blk_ready && mls_eligible(h) && h->tune.mls) {
         // M x S on k_cosine_mls (256 x 192 tiles from the K-blocked images):
         // from the 64-row image block holding the slab's first owner of the group
         if ((rc = vl_blk_prepare(h, gi))) return rc;
@@ -1439,7 +1434,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   // symmetric waves on k_cosine_sym (256 x 192 tiles, 768-row blocks) when
   // the table allows it and the images are staged 64 B deep
   int32_t rb8 = 0, rb4 = 0;
-  const bool sym_img = h->sym_sw == sym_stage_bytes() && !getenv("CMS_OLD_SYM");
+  const bool sym_img = h->sym_sw == sym_stage_bytes();
   const bool sym8 = sym_img && sym_eligible(h, 0, &rb8);
   const bool sym4 = sym_img && sym_eligible(h, 1, &rb4);
   const int32_t cap = (sym8 || sym4) ? kCandCapSym : kCandCap;
@@ -1486,8 +1481,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // chunk: a slab of qc rows offers qc similarities to every S list, so a
     // chunk must leave room in a list compacted to cap - qc entries
     // (the lists are offered the slab cap/2 rows at a time: multi_rows_slab_offer)
-    int64_t chunk = getenv("CMS_M_SMALL") ? std::min<int64_t>(cap / 2, slab_rows_for(n)) : multi_slab_rows(h, n);
-    if (const char* e = getenv("CMS_M_CHUNK")) chunk = std::max<int64_t>(128, std::min<int64_t>(chunk, atoi(e)));
+    const int64_t chunk = multi_slab_rows(h, n);
     for (int64_t m0 = (int64_t)shard * chunk; m0 < nm; m0 += (int64_t)nshards * chunk) {
       const int64_t qc = std::min<int64_t>(chunk, nm - m0);
       if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts))) return rc;
@@ -1549,7 +1543,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
         const uint32_t limit = L == 1 ? (uint32_t)(cap - 2 * blk) : (uint32_t)cap / 2;
         if ((rc = cand_compact(h, cb, nm, ns, limit, k))) return rc;
         // wide bands of plain (non-fsel) waves: rectangle enumeration
-        const int rect = (L >= 8 && !(fp4 ? false : fb0 < nb_s) && !getenv("CMS_NO_RECT")) ? 1 : 0;
+        const int rect = (L >= 8 && !(fp4 ? false : fb0 < nb_s)) ? 1 : 0;
         TimedScope ts(h, "topk_all_waves");
         TimedScope tsub(h, fp4 ? "topk_all_waves_f4" : "topk_all_waves_i8");
         if (use_sym) {
@@ -1568,9 +1562,7 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
           g.rect = rect;
           g.si = 8;  // 8 A blocks x 2 J chunks: fp4 waves -5 % against 4 x 4 (8 x 1, 16 x 2 within 1 %)
           g.sj = 2;
-          if (const char* e = getenv("CMS_SYM_RECT")) sscanf(e, "%d,%d", &g.si, &g.sj);
           g.xchunk = 32;  // the XCDs side by side (xcd_chunk_map): int8 waves -7%, fp4 waves unchanged
-          if (const char* e = getenv("CMS_SYM_XCHUNK")) g.xchunk = std::max(0, atoi(e));
           g.thr = cb.thr;
           g.ccnt = cb.ccnt;
           g.cidx = cb.cidx;
@@ -1590,9 +1582,6 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
             g.tsel = 1;
             blocks(nm, nm + h->rf_t8, &g.ts0, &g.ts1);
             blocks(nm + h->rf_s8, nm + h->rf_s8 + h->rf_t4, &g.ts2, &g.ts3);
-            if (getenv("CMS_RF_DEBUG") && wv == 0)
-              fprintf(stderr, "refresh pass %d: nb %d blocks [%d,%d) [%d,%d) (t8 %ld t4 %ld s8 %ld nm %ld)\n", pass,
-                      g.nb, g.ts0, g.ts1, g.ts2, g.ts3, (long)h->rf_t8, (long)h->rf_t4, (long)h->rf_s8, (long)nm);
           }
           int64_t slots = nbk;
           if (!fp4 && fb0 < nb_s) {

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "cms_hash.h"
+
 namespace cms {
 
 // Increment of pair i in counter units: 1 << fb for implicit streams, else the
@@ -25,6 +27,28 @@ __device__ __forceinline__ bool load_inc(const float* val, int64_t i, uint32_t& 
   inc = (uint32_t)v;
   return true;
 }
+
+// Keys of a grouped batch.  CSR ingests hand the build the caller's int64
+// keys; the COO partition (cms_partition.hip) writes each key as a u32 TOKEN
+// instead, halving the bytes the partition moves and the build reads: a key in
+// [0, 2^31) is its own token, any other key travels as kTokEscape | i, its
+// index in the batch's key array (batches are < 2^31 pairs), and is read from
+// there.  at(i) is key i reduced mod p (the hash's input).
+constexpr uint32_t kTokEscape = 0x80000000u;
+__device__ __forceinline__ uint32_t make_token(int64_t key, int64_t idx) {
+  return (uint64_t)key < (uint64_t)kTokEscape ? (uint32_t)key : (kTokEscape | (uint32_t)idx);
+}
+struct Keys {
+  const int64_t* key;   // CSR keys (tok == null), or the batch's keys (escaped tokens index them)
+  const uint32_t* tok;  // partition output tokens, or null
+  __device__ __forceinline__ uint64_t at(int64_t i) const {
+    if (tok) {
+      const uint32_t t = tok[i];
+      return t < kTokEscape ? (uint64_t)t : reduce_key(key[t & (kTokEscape - 1u)]);
+    }
+    return reduce_key(key[i]);
+  }
+};
 
 __device__ __forceinline__ uint64_t sat_add(uint64_t a, uint64_t b) {
   uint64_t s = a + b;

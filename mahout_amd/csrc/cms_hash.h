@@ -65,9 +65,23 @@ CMS_HD uint64_t mulmod_p(uint64_t x, uint64_t y) {
   return z;
 }
 
+// (x * y) mod p for x in [0, p) and y < 2^32 (keys of the usual ID ranges):
+// the product is < 2^95, so one fold of 2^63 == 25 leaves z < 2p and one
+// conditional subtract finishes -- two 32x32 multiplies instead of four.
+CMS_HD uint64_t mulmod_p_small(uint64_t x, uint32_t y) {
+  const uint64_t p0 = (uint64_t)(uint32_t)x * y;
+  const uint64_t p1 = (x >> 32) * (uint64_t)y;  // < 2^63
+  const uint64_t lo = p0 + (p1 << 32);
+  const uint64_t hi = (p1 >> 32) + (lo < p0 ? 1u : 0u);  // prod >> 64 (< 2^31)
+  const uint64_t H = (hi << 1) | (lo >> 63);             // prod >> 63 (< 2^32)
+  uint64_t z = (lo & kMask63) + H * 25u;                  // < 2^63 + 2^37 < 2p
+  if (z >= kPrime) z -= kPrime;
+  return z;
+}
+
 // Bucket of a reduced key in sketch row r.
 CMS_HD uint32_t bucket(const HashParams& hp, int r, uint64_t kp) {
-  uint64_t s = mulmod_p(hp.ap[r], kp) + hp.bp[r];  // < 2p < 2^64
+  uint64_t s = ((kp >> 32) == 0 ? mulmod_p_small(hp.ap[r], (uint32_t)kp) : mulmod_p(hp.ap[r], kp)) + hp.bp[r];  // < 2p
   if (s >= kPrime) s -= kPrime;
   if (hp.pow2) return (uint32_t)(s & hp.wmask);
   uint64_t q = (uint64_t)(((unsigned __int128)s * hp.barrett) >> 64);

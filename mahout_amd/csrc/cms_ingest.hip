@@ -269,7 +269,7 @@ __device__ __forceinline__ uint64_t seg_suffix_sum(uint64_t v, int32_t r, int la
   return v;
 }
 
-__global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, const int64_t* key, const float* val,
+__global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, Keys keys, const float* val,
                                                         const int64_t* count, HashParams hp, TableView tv,
                                                         uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
                                                         uint32_t* flags) {
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void k_ingest_sorted(const int32_t* rows, cons
         atomicOr(flags, kFlagBadValue);
         inc = 0;
       }
-      kp = reduce_key(key[i]);
+      kp = keys.at(i);
     }
     const int32_t rprev = __shfl_up(r, 1, 64);
     const bool head = r >= 0 && (lane == 0 || rprev != r);
@@ -432,10 +432,11 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
     }
     if (!h->empty && h->norms_valid && npairs >= 32768 && n < (int64_t(1) << 31)) {
       // live table with current norms: group by owner, then wave-reduced atomics
-      int64_t *coff, *ckey;
+      int64_t* coff;
+      uint32_t* ctok;
       float* cval;
       CMS_HIP(h->ws_srow.ensure(sizeof(int32_t) * (size_t)npairs));
-      int rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &coff, &ckey, &cval, h->ws_srow.as<int32_t>());
+      int rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &coff, &ctok, &cval, h->ws_srow.as<int32_t>());
       if (rc) return rc;
       {  // rows this batch could lift to 2^16 move to u32 slots first
         DevBuf& bound = h->ws_bound;
@@ -452,7 +453,7 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
       TimedScope ts(h, "ingest_sorted");
       h->stale_possible = true;
       unsigned grid = (unsigned)std::min<int64_t>((npairs + 255) / 256, 16384);
-      hipLaunchKernelGGL(k_ingest_sorted, dim3(grid), dim3(256), 0, h->stream, h->ws_srow.as<int32_t>(), ckey, cval,
+      hipLaunchKernelGGL(k_ingest_sorted, dim3(grid), dim3(256), 0, h->stream, h->ws_srow.as<int32_t>(), Keys{d_key, ctok}, cval,
                          coff + n, h->hp, h->tview(), h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       CMS_HIP(hipGetLastError());
       return CMS_OK;
@@ -495,16 +496,17 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
   }
 
   // ---- group by owner (cms_partition.hip), then the LDS row build ----
-  int64_t *clo, *chi, *ckey;
+  int64_t *clo, *chi;
+  uint32_t* ctok;
   float* cval;
   int rc = kNoSpans;
-  if (!getenv("CMS_NO_HOT_ROUTING")) rc = partition_to_spans(h, d_row, d_key, d_val, npairs, &clo, &chi, &ckey, &cval);
+  if (h->tune.hot_routing) rc = partition_to_spans(h, d_row, d_key, d_val, npairs, &clo, &chi, &ctok, &cval);
   if (rc == kNoSpans) {
-    rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &clo, &ckey, &cval);
+    rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &clo, &ctok, &cval);
     chi = clo + 1;
   }
   if (rc) return rc;
-  return ingest_spans_device(h, clo, chi, ckey, cval, npairs);
+  return ingest_spans_device(h, clo, chi, d_key, ctok, cval, npairs);
 }
 
 }  // namespace cms

@@ -149,8 +149,23 @@ struct QueryCtx {
 };
 }  // namespace cms
 
+namespace cms {
+// Tunables read ONCE, from the environment, when the handle is created
+// (include/mahout_cms.h lists them); nothing in the library reads the
+// environment after cms_create.
+struct Tunables {
+  int bit_keys = 64;       // CMS_BIT_KEYS: byte-class owners of <= this many keys try 1-bit rows first
+  int crumb_keys = 256;    // CMS_CRUMB_KEYS: ... of <= this many keys 2-bit rows
+  bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
+  bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
+  bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)
+  bool mls = true;         // CMS_NO_MLS=1: multi-limb slabs on the 128-tile kernel instead of k_cosine_mls
+};
+}  // namespace cms
+
 struct cms_handle {
   cms_params p{};
+  cms::Tunables tune;
   int device = 0;
   int num_cus = 256;  // compute units of the device (persistent grids)
   hipStream_t stream = nullptr;
@@ -321,8 +336,10 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
 int ingest_csr_device(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs);
 // owner spans -> table: row r's keys are d_key[d_lo[r], d_hi[r]) (the spans
 // need not be in row order; a CSR is d_lo = off, d_hi = off + 1).
-int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const int64_t* d_key, const float* d_val,
-                        int64_t npairs);
+// d_tok: the partition's key tokens (cms_device.h Keys), d_key then the
+// batch's keys they escape into; null for a caller CSR (keys in d_key).
+int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const int64_t* d_key,
+                        const uint32_t* d_tok, const float* d_val, int64_t npairs);
 // owner IDs -> rows by binary search over h->d_owner_ids.
 int map_owner_ids(cms_handle* h, const int64_t* d_ids, int64_t n, int64_t* d_rows);
 int compute_norms(cms_handle* h);
@@ -375,15 +392,17 @@ int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d
 int scan_exclusive_u32(cms_handle* h, const uint32_t* in, uint32_t* out, int64_t L, uint32_t* bsum);
 // ---- cms_partition.hip ----
 // COO -> CSR grouped by row; outputs live in handle scratch.
+// Keys come out as u32 tokens (cms_device.h make_token / Keys) that escape
+// into d_key.
 int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                     int64_t** out_off, int64_t** out_key, float** out_val,
+                     int64_t** out_off, uint32_t** out_tok, float** out_val,
                      int32_t* out_rows = nullptr);
 // COO -> owner spans with the hottest owners routed straight to their final
 // place by pass 1 (only the other pairs take pass 2).  Returns kNoSpans when
 // the shape does not allow it (the caller then uses partition_to_csr).
 constexpr int kNoSpans = 1;
 int partition_to_spans(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                       int64_t** out_lo, int64_t** out_hi, int64_t** out_key, float** out_val);
+                       int64_t** out_lo, int64_t** out_hi, uint32_t** out_tok, float** out_val);
 
 // ---- launchers (cms_query.hip) ----
 // s: the stream to launch on (null = the handle's stream; a query context's

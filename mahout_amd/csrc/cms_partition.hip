@@ -4,7 +4,7 @@
 // one PreferenceArray per owner (T/impl/similarity/CosineCM.java:49-56).  A
 // streaming ingest has to group the pairs itself before the LDS row build
 // (cms_build.hip).  Two MSD passes, fan-out <= 4096 each:
-//   pass 1: coarse bin = row >> s2   (writes key + u16 fine index)
+//   pass 1: coarse bin = row >> s2   (writes the key token + u16 fine index)
 //   pass 2: fine bin   = row & (2^s2 - 1), segmented per coarse bin
 //           (writes the key at its final CSR position; the scan of pass 2 also
 //            yields the CSR row offsets)
@@ -243,7 +243,7 @@ __device__ __forceinline__ uint32_t scan_bins(const uint32_t* hist, uint32_t* of
 }
 
 struct TileLds {
-  int64_t* key;
+  uint32_t* key;  // key tokens (make_token)
   float* val;
   uint16_t* fine;
   uint16_t* bin;
@@ -258,8 +258,8 @@ struct TileLds {
 __device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_val, bool has_fine) {
   TileLds t;
   unsigned char* q = smem;
-  t.key = reinterpret_cast<int64_t*>(q);
-  q += sizeof(int64_t) * kPartTile;
+  t.key = reinterpret_cast<uint32_t*>(q);
+  q += sizeof(uint32_t) * kPartTile;
   t.val = reinterpret_cast<float*>(q);
   if (has_val) q += sizeof(float) * kPartTile;
   t.fine = reinterpret_cast<uint16_t*>(q);
@@ -274,19 +274,21 @@ __device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_va
 }
 
 static size_t tile_lds_bytes(int P, bool has_val, bool has_fine, bool hot = false) {
-  return (size_t)kPartTile * (8 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4 +
+  return (size_t)kPartTile * (4 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4 +
          (hot ? sizeof(uint32_t) * kHotBins : 0);
 }
 
 // Pass 1: block b owns tiles b, b + NB, ... of the stream; output region of
 // (coarse bin, block) starts at O1[bin*NB + b].
 // With hotkey: bins [P1, P1 + kHotBins) are hot owners, whose keys (and
-// values) go straight to okey_hot / oval_hot -- their final place.
+// values) go straight to okey_hot / oval_hot -- their final place.  Keys
+// leave as u32 tokens (make_token: the key itself below 2^31, else its
+// index in this batch).
 __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row, const int64_t* key, const float* val,
                                                              int64_t n, int s2, int P1, int64_t nrows,
                                                              const uint32_t* O1, int NB, uint16_t* ofine,
-                                                             int64_t* okey, float* oval,
-                                                             const unsigned long long* hotkey, int64_t* okey_hot,
+                                                             uint32_t* okey, float* oval,
+                                                             const unsigned long long* hotkey, uint32_t* okey_hot,
                                                              float* oval_hot) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int P = P1 + (hotkey ? kHotBins : 0);
@@ -316,6 +318,9 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
       }
     }
   };
+  auto tok = [&](int64_t t, int u) {
+    return make_token(kk[u], t * kPartTile + tid + (int64_t)u * kPartThreads);
+  };
   if ((int64_t)blockIdx.x < ntiles) load(blockIdx.x);
   __syncthreads();
   for (int64_t t = blockIdx.x; t < ntiles; t += NB) {
@@ -339,7 +344,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
       if (rk[u] != 0xFFFFFFFFu) {
         const uint32_t bin = bn[u];
         uint32_t p = L.off[bin] + rk[u];
-        L.key[p] = kk[u];
+        L.key[p] = tok(t, u);
         if (val) L.val[p] = vv[u];
         L.fine[p] = (uint16_t)(bb[u] & fmask);
         L.bin[p] = (uint16_t)bin;
@@ -582,10 +587,10 @@ __global__ __launch_bounds__(1024) void k_p2_offsets(const uint32_t* H2, const u
   }
 }
 
-__global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fine, const int64_t* key1,
+__global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fine, const uint32_t* key1,
                                                              const float* val1, const uint32_t* binStart,
                                                              const uint32_t* blkStart, int P1, int64_t CH2, int P2,
-                                                             const uint32_t* O2, int64_t* okey, float* oval,
+                                                             const uint32_t* O2, uint32_t* okey, float* oval,
                                                              int32_t* orow) {
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t nblk = blkStart[P1];
@@ -597,7 +602,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
   const int64_t lo = binStart[b] + (int64_t)(blockIdx.x - blkStart[b]) * CH2;
   const int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
   for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
-  int64_t kk[kPartPer];
+  uint32_t kk[kPartPer];
   float vv[kPartPer];
   uint32_t ff[kPartPer];
   auto load = [&](int64_t tb) {
@@ -685,18 +690,14 @@ __global__ void k_spans_hot(const unsigned long long* slotkey, const uint32_t* b
 }
 
 static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                          bool hot, int64_t** out_lo, int64_t** out_hi, int64_t** out_key, float** out_val,
+                          bool hot, int64_t** out_lo, int64_t** out_hi, uint32_t** out_tok, float** out_val,
                           int32_t* out_rows) {
   const int64_t n = h->n;
   const int B = std::max(1, ceil_log2(n));
   // fine bits: 11 for 2^19+ owners (config 3, 1M owners: 489 coarse bins give
   // the cold pairs' pass-1 runs twice the length of 977; partition 6.18 ->
-  // 5.79 ms), else CMS_PART_S2 (10); CMS_PART_S2 in the environment overrides
-  static const int s2_env = [] {
-    const char* e = getenv("CMS_PART_S2");
-    return e ? atoi(e) : 0;
-  }();
-  int s2 = std::min(B, s2_env > 0 ? s2_env : (B >= 20 ? 11 : CMS_PART_S2));
+  // 5.79 ms), else CMS_PART_S2 (10)
+  int s2 = std::min(B, B >= 20 ? 11 : CMS_PART_S2);
   if (B - s2 > 12) s2 = B - 12;
   const int P2 = 1 << s2;
   const int P1 = (int)((n + P2 - 1) / P2);
@@ -709,9 +710,9 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
   const int64_t nb2max = npairs / CH2 + P1 + 1;
 
   CMS_HIP(h->ws_p1_row.ensure(sizeof(uint16_t) * (size_t)npairs));
-  CMS_HIP(h->ws_p1_key.ensure(sizeof(int64_t) * (size_t)npairs));
+  CMS_HIP(h->ws_p1_key.ensure(sizeof(uint32_t) * (size_t)npairs));
   if (d_val) CMS_HIP(h->ws_p1_val.ensure(sizeof(float) * (size_t)npairs));
-  CMS_HIP(h->ws_csr_key.ensure(sizeof(int64_t) * (size_t)npairs));
+  CMS_HIP(h->ws_csr_key.ensure(sizeof(uint32_t) * (size_t)npairs));
   if (d_val) CMS_HIP(h->ws_csr_val.ensure(sizeof(float) * (size_t)npairs));
   CMS_HIP(h->ws_csr_off.ensure(sizeof(int64_t) * (size_t)(n + 1)));
   if (hot) {
@@ -734,9 +735,9 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
   uint32_t* seg1 = bs1 + (P + 1);                 // {0, NB}: pass 1 is one segment of NB blocks
 
   uint16_t* fine = h->ws_p1_row.as<uint16_t>();
-  int64_t* key1 = h->ws_p1_key.as<int64_t>();
+  uint32_t* key1 = h->ws_p1_key.as<uint32_t>();
   float* val1 = d_val ? h->ws_p1_val.as<float>() : nullptr;
-  int64_t* ckey = h->ws_csr_key.as<int64_t>();
+  uint32_t* ckey = h->ws_csr_key.as<uint32_t>();
   float* cval = d_val ? h->ws_csr_val.as<float>() : nullptr;
   int64_t* coff = h->ws_csr_off.as<int64_t>();
   unsigned long long* slotkey = hot ? h->ws_hotpart.as<unsigned long long>() : nullptr;
@@ -794,20 +795,20 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     CMS_HIP(hipGetLastError());
   }
   *out_lo = coff;
-  *out_key = ckey;
+  *out_tok = ckey;
   *out_val = cval;
   return CMS_OK;
 }
 
 int partition_to_csr(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                     int64_t** out_off, int64_t** out_key, float** out_val, int32_t* out_rows) {
+                     int64_t** out_off, uint32_t** out_tok, float** out_val, int32_t* out_rows) {
   int64_t* hi;
-  return partition_impl(h, d_row, d_key, d_val, npairs, false, out_off, &hi, out_key, out_val, out_rows);
+  return partition_impl(h, d_row, d_key, d_val, npairs, false, out_off, &hi, out_tok, out_val, out_rows);
 }
 
 int partition_to_spans(cms_handle* h, const int64_t* d_row, const int64_t* d_key, const float* d_val, int64_t npairs,
-                       int64_t** out_lo, int64_t** out_hi, int64_t** out_key, float** out_val) {
-  return partition_impl(h, d_row, d_key, d_val, npairs, true, out_lo, out_hi, out_key, out_val, nullptr);
+                       int64_t** out_lo, int64_t** out_hi, uint32_t** out_tok, float** out_val) {
+  return partition_impl(h, d_row, d_key, d_val, npairs, true, out_lo, out_hi, out_tok, out_val, nullptr);
 }
 
 }  // namespace cms

@@ -714,7 +714,7 @@ int cand_compact(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, uint
   hipLaunchKernelGGL(k_cand_select, dim3(g1), dim3(256), 0, h->stream, cb.ccnt, p0, np, limit, cb.list, cb.list_n);
   hipLaunchKernelGGL(k_cand_compact, dim3(4096), dim3(kCandThreads), 0, h->stream, cb.list, cb.list_n, cb.ccnt,
                      cb.cidx, cb.cval, cb.cap, k, cosine_perm_device(h), cb.thr, cb.ovf,
-                     limit == 0 || getenv("CMS_SORT_COMPACT") ? 1 : 0);  // only the final compaction sorts
+                     limit == 0 ? 1 : 0);  // only the final compaction sorts
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

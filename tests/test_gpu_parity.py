@@ -63,11 +63,14 @@ def test_ingest_partition_path_with_hot_rows(oracle, n, d, w, npairs):
     assert np.bincount(items, minlength=n).max() > 32768  # a hot row was split into several slices
 
 
-@pytest.mark.parametrize("shape", ["u32_max", "one_wide", "negative", "edge"])
+@pytest.mark.parametrize("shape", ["u32_max", "one_wide", "negative", "edge", "all_wide"])
 def test_partition_key_width_modes(oracle, shape):
-    """Keys at the u32 boundary, a single key past it, negative keys and the
-    int64 edge values through the COO partition (and a second batch through
-    the same partition workspace) give the oracle's table bit for bit."""
+    """Keys at the u32 boundary, a single key past it, negative keys, the
+    int64 edge values and a stream whose every key is wide, through the COO
+    partition (and a second batch through the same partition workspace), give
+    the oracle's table bit for bit.  The partition carries keys as u32 tokens:
+    keys in [0, 2^31) as themselves, all others as their index in the batch
+    (escapes), so every case but the plain one exercises the escape path."""
     n, d, w = 900, 5, 512
     items, users = zipf_stream(30000, n, 400_000, seed=17)
     keys = users.astype(np.int64).copy()
@@ -77,6 +80,8 @@ def test_partition_key_width_modes(oracle, shape):
         keys[len(keys) // 2] = 2 ** 32  # a single key needs the 8-byte path
     elif shape == "negative":
         keys[-1] = -1
+    elif shape == "all_wide":
+        keys = keys * 977 + 2 ** 40
     else:
         keys[: len(EDGE)] = EDGE
     with SketchTable(n, depth=d, width=w, seed=7) as t:
@@ -299,26 +304,28 @@ def test_owner_ids_and_errors(oracle):
         assert abs(t.similarity(3, 3) - 1.0) < 1e-15
 
 
-@pytest.mark.parametrize("partials", [False, True])
-def test_accumulate_equals_single_batch(oracle, monkeypatch, partials):
-    """Split rows' slices add into their slot rows with global atomics, or
-    (CMS_SLICE_PARTIALS, the experiment) write partial rows that k_hot_reduce
-    sums; both bit-exact, fresh and accumulating."""
-    if partials:
-        monkeypatch.setenv("CMS_SLICE_PARTIALS", "1")
+@pytest.mark.parametrize("weighted", [False, True])
+def test_accumulate_equals_single_batch(oracle, weighted):
+    """Split (hot) rows' slices add into their slot rows with global atomics:
+    unit streams through k_build_slices (all d sketch rows of a 65535-key
+    slice in one u16 LDS image, one key pass), valued streams through
+    k_build_rows' slices (a key pass per pair of sketch rows); both
+    bit-exact, fresh and accumulating."""
     n, d, w = 1500, 4, 512
     items, users = zipf_stream(30000, n, 800_000, seed=21)
+    vals = np.random.Generator(np.random.PCG64(21)).integers(1, 4, items.size).astype(np.float32) if weighted else None
+    part = (lambda lo, hi: None) if vals is None else (lambda lo, hi: vals[lo:hi])
     with SketchTable(n, depth=d, width=w, seed=42) as t:
-        t.ingest(items[:400_000], users[:400_000])       # partition build into an empty table
-        t.ingest(items[400_000:700_000], users[400_000:700_000])  # partition build, accumulate mode
-        t.ingest(items[700_000:], users[700_000:])       # atomic path (small batch)
+        t.ingest(items[:400_000], users[:400_000], part(0, 400_000))  # partition build into an empty table
+        t.ingest(items[400_000:700_000], users[400_000:700_000], part(400_000, 700_000))  # accumulate build
+        t.ingest(items[700_000:], users[700_000:], part(700_000, items.size))  # atomic path (small batch)
         t.finalize()
         got = t.read_counters()
-        exp = oracle_table(oracle, n, d, w, 42, items, users)
+        exp = oracle_table(oracle, n, d, w, 42, items, users, vals)
         assert same(got, exp)
         # the hottest owners were split into slices in both builds (their slot
-        # rows summed from slice partial rows, old counters included the second
-        # time): their norms show in every similarity of their rows
+        # rows summed from the slices, old counters included the second time):
+        # their norms show in every similarity of their rows
         cnt = np.bincount(items[:400_000], minlength=n)
         assert cnt.max() > 2 * 8192
         for q in np.argsort(cnt)[-3:]:
@@ -753,11 +760,15 @@ def test_multi_limb_slab_kernel_equals_reference_path(oracle):
         ids, sc, cnt = t.top_k_all(k)
         st = t.stats()
         assert st["deep_limb_owners"] > 0 and st["multi_limb_owners"] > st["deep_limb_owners"], st
-        os.environ["CMS_NO_MLS"] = "1"
-        try:
-            ids2, sc2, cnt2 = t.top_k_all(k)
-        finally:
-            del os.environ["CMS_NO_MLS"]
+    os.environ["CMS_NO_MLS"] = "1"  # a tunable: read when the handle is created
+    try:
+        t2 = SketchTable(n, depth=d, width=w, seed=42)
+    finally:
+        del os.environ["CMS_NO_MLS"]
+    with t2:
+        t2.ingest(items, users, vals)
+        t2.finalize()
+        ids2, sc2, cnt2 = t2.top_k_all(k)
         assert np.array_equal(cnt, cnt2)
         for q in range(n):
             assert ids[q, :cnt[q]].tolist() == ids2[q, :cnt2[q]].tolist(), q
