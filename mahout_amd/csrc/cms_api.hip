@@ -380,7 +380,9 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   h->empty = true;
   h->norms_valid = false;
   // u8 / nibble row forms need 64-B aligned slots and 16-B nibble rows
-  h->forms_ok = !per_owner && !f64 && h->dw % 32 == 0 && h->tune.forms;
+  // (the byte-class and mid kernels store whole 16-B words of a 4-bit sketch
+  // row: w % 32 == 0)
+  h->forms_ok = !per_owner && !f64 && h->p.width % 32 == 0 && h->tune.forms;
   *out = h;
   return CMS_OK;
 }

@@ -541,15 +541,15 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 }
 
 // Mid-class owners (narrow, more than 256 keys or a mass >= 256): one
-// workgroup per owner, one sketch row at a time in a 2w-byte LDS image, in
-// the narrowest form that holds it -- 4-bit first, u8 when a counter reaches
-// 16, u16 when one reaches 256 (each escalation restarts the owner; the wider
-// layout overwrites every byte the narrower one wrote).  As in
-// k_build_nibbles the returning LDS adds give each sketch row's sum of squares
-// and the row maximum, and each finished sketch row leaves LDS as is.  The
-// 16 KB image (config 3) keeps 8 workgroups per CU against 5 with the 32 KB
-// paired-u16 row image of k_build_rows; the stored rows shrink 2-4x.  A
-// persistent grid walks the device-side list.
+// workgroup per owner, in the narrowest form that holds it -- 4-bit first,
+// u8 when a counter reaches 16, u16 when one reaches 256 (each escalation
+// restarts the owner; the wider layout overwrites every byte the narrower one
+// wrote).  The 4-bit attempt counts ALL d sketch rows at once in a [d][w]
+// 4-bit LDS image (d*w/2 bytes, 20 KB at config 3), so each key is read and
+// hashed once; its sums of squares come from reading the image back (v_dot4
+// of the nibbles) as it is stored.  The u8 / u16 attempts go one sketch row
+// at a time (a w- or 2w-byte image), the returning LDS adds giving each
+// row's sum of squares.  A persistent grid walks the device-side list.
 template <int SV>
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(CMS_BUILD_WAVES, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
@@ -591,7 +591,90 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
     uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's slot (64-B aligned)
     int level = 0;  // 0: 4-bit, 1: u8, 2: u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
+    {  // 4-bit, all sketch rows in one key pass
+      const int nq_all = (int)((int64_t)hp.depth * w >> 5);  // uint4 of the [d][w] 4-bit image
+      uint4* l4 = reinterpret_cast<uint4*>(lds);
+      for (int j = tid; j < nq_all; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+      if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+      if (tid == 0) {
+        s_max = 0u;
+        s_ovf = 0u;
+        s_mass = 0ULL;
+      }
+      __syncthreads();
+      bool ovf = false;
+      auto add_all = [&](uint64_t kr, uint32_t inc) {
+        for (int d = 0; d < hp.depth; ++d) {
+          const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kr);
+          const uint32_t sh = (c & 7u) << 2;
+          const uint32_t old = (atomicAdd(&lds[c >> 3], inc << sh) >> sh) & 15u;
+          const uint32_t nv = old + inc;
+          ovf |= nv > 15u || inc > 15u;  // carried into the next counter: a wider form
+          vmax = max(vmax, nv);
+        }
+      };
+      if (cached) {
+#pragma unroll
+        for (int k = 0; k < kKeyRegs; ++k)
+          if (ik[k]) add_all(kp[k], ik[k]);
+      } else {
+        for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
+          uint64_t kk[4];
+          uint32_t inc4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            kk[u] = i < hi ? keys.at(i) : 0;
+            inc4[u] = 0;
+            if (i < hi) {
+              uint32_t inc;
+              if (!load_inc(vals, i, inc, hp.frac_bits)) {
+                badv = true;
+                inc = 0;
+              }
+              inc4[u] = inc;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (inc4[u]) add_all(kk[u], inc4[u]);
+            mass += inc4[u];
+          }
+        }
+      }
+      if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
+      __syncthreads();
+      const bool fits = s_ovf == 0u;
+      __syncthreads();  // every thread has read s_ovf before the u8 attempt resets it
+      if (fits) {
+        // read the image back: each sketch row's sum of squares (v_dot4 of its
+        // low and high nibbles) as its rows leave for the slot
+        const int nq = w >> 5;  // uint4 per 4-bit sketch row
+        for (int d = 0; d < hp.depth; ++d) {
+          uint32_t sq = 0;  // <= row mass * 15 < 2^32
+          for (int j = tid; j < nq; j += kBuildThreads) {
+            const uint4 v = l4[d * nq + j];
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint32_t lo4 = x[q] & 0x0F0F0F0Fu, hi4 = (x[q] >> 4) & 0x0F0F0F0Fu;
+              sq = __builtin_amdgcn_udot4(lo4, lo4, sq, false);
+              sq = __builtin_amdgcn_udot4(hi4, hi4, sq, false);
+            }
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+            if (false)
+#endif
+            store_row(d4 + d * nq + j, v, SV);
+          }
+          sq = wave_sum_u32(sq);
+          if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+        }
+      } else {
+        level = 1;  // a counter passed 15: u8 rows, one sketch row at a time
+      }
+    }
     for (;;) {
+      if (level == 0) break;  // the 4-bit image held every counter
       const int bits = 4 << level;
       const int lg = 3 - level;          // log2(counters per word)
       const uint32_t cap = (1u << bits) - 1u;
@@ -1117,8 +1200,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
                          h->tune.crumb_keys);
       hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
-                         dim3(kBuildThreads), (size_t)h->p.width * 2, side, d_lo, d_hi, keys, d_val, h->hp,
-                         (const int32_t*)mid_list, (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound,
+                         dim3(kBuildThreads), std::max<size_t>((size_t)h->p.width * 2, (size_t)h->dw / 2), side, d_lo,
+                         d_hi, keys, d_val, h->hp, (const int32_t*)mid_list, (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       hipLaunchKernelGGL(k_build_bytes<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)),
                          dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,

@@ -87,6 +87,25 @@ def test_extreme_shapes(oracle, d, w):
         assert ids.tolist() == eids.tolist()
 
 
+@pytest.mark.parametrize("d,w", [(32, 16), (2, 48), (4, 96), (1, 1024)])
+def test_bulk_csr_build_odd_widths(oracle, d, w):
+    """The LDS row build (CSR ingest) at widths whose sketch rows are not
+    whole 16-B words of 4-bit counters (d*w % 32 == 0 but w % 32 != 0) keeps
+    u16 rows; w % 32 == 0 takes the narrow forms -- all equal the oracle."""
+    n = 300
+    items, users = zipf_stream(5000, n, 60_000, seed=d + w)
+    off, keys, _ = to_csr(items, users, n)
+    exp = otable(oracle, n, d, w, items, users)
+    with SketchTable(n, depth=d, width=w) as t:
+        t.ingest_csr(off, keys)
+        t.finalize()
+        assert same(t.read_counters(), exp)
+        for q in [0, 7, n - 1]:
+            assert same(t.similarities(q, np.arange(n)), row_sims(oracle, exp, q))
+        st = t.stats()
+        assert (st["nibble_rows"] + st["crumb_rows"] + st["bit_rows"] + st["u8_rows"] > 0) == (w % 32 == 0), st
+
+
 def test_bulk_build_of_width_32768_owner_rows(oracle):
     """The LDS row build at the largest width (128 KiB rows) with hot rows."""
     n, d, w = 30, 2, 32768
