@@ -60,7 +60,7 @@ extern "C" {
                              (negative, non-dyadic); increments are applied per owner in ingest
                              order (the DataModel order CosineCM.exportProfile uses) and every sum
                              is the reference's sequential fp64 chain.  Single-GPU; fixed shapes
-                             up to width 16384, and per-owner shapes (cms_create_per_owner);
+                             up to width 2^20, and per-owner shapes (cms_create_per_owner);
                              owners are built by CSR ingest or host COO ingest (stable by
                              owner), not by cms_ingest_device_rows. */
 
@@ -70,7 +70,7 @@ extern "C" {
 typedef struct cms_params {
   uint32_t struct_size; /* = sizeof(cms_params); filled by cms_params_init */
   int32_t depth;        /* d, 1..32 (AbstractCountMinSketch.java:34-44 init; bound of this build) */
-  int32_t width;        /* w, 1..2^20 */
+  int32_t width;        /* w: 1..32768 with CMS_COUNTER_U32, 1..2^20 with CMS_COUNTER_F64 */
   int32_t counter_type; /* CMS_COUNTER_* */
   int64_t seed;         /* HashFunctionBuilder(long seed) (HashFunctionBuilder.java:23) */
   int64_t num_owners;   /* n: rows of the sketch table */

@@ -288,15 +288,17 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   if (!per_owner) {
     if (p->depth < 1 || p->depth > CMS_MAX_DEPTH)
       return set_error(CMS_E_PARAM, "depth must be in [1, %d]", CMS_MAX_DEPTH);
-    if (p->width < 1 || p->width > (1 << 15))
-      return set_error(CMS_E_PARAM, "width must be in [1, 32768] (LDS-staged sketch rows)");
+    // u32 counters: LDS-staged sketch rows up to 32768 counters; fp64
+    // counters (DoubleCountMinSketch's own type, any width the reference's
+    // constructor takes) up to 2^20, rows past the LDS built in place
+    const int32_t wmax = p->counter_type == CMS_COUNTER_F64 ? (1 << 20) : (1 << 15);
+    if (p->width < 1 || p->width > wmax) return set_error(CMS_E_PARAM, "width must be in [1, %d]", wmax);
   }
   if (p->num_owners < 1 || p->num_owners > (int64_t(1) << 24))
     return set_error(CMS_E_PARAM, "num_owners must be in [1, 2^24]");
   if (p->counter_type != CMS_COUNTER_U32 && p->counter_type != CMS_COUNTER_F64)
     return set_error(CMS_E_PARAM, "unsupported counter type");
   const bool f64 = p->counter_type == CMS_COUNTER_F64;
-  if (f64 && !per_owner && p->width > 16384) return set_error(CMS_E_PARAM, "fp64 counters: width must be <= 16384 (LDS sketch row)");
   if (p->frac_bits < 0 || p->frac_bits > 31) return set_error(CMS_E_PARAM, "frac_bits must be in [0, 31]");
   if (p->flags & ~CMS_FLAG_COLLECTIVE_SINGLE_RANK) return set_error(CMS_E_PARAM, "unknown flags 0x%x", p->flags);
   if (f64 && (p->flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK))

@@ -32,13 +32,17 @@ constexpr int kF64Chunk = 2048;  // keys staged per LDS round
 // One workgroup per owner row.  LDS: the current sketch row [w] fp64, plus a
 // staged chunk of (bucket, increment) pairs.  Thread t owns buckets j with
 // j % 256 == t and walks the chunk in key order, so each counter receives its
-// increments in exactly the reference's order.
+// increments in exactly the reference's order.  Rows wider than the LDS holds
+// (in_lds == 0: w > 16384) are updated in place in the table: the owning
+// thread's loads and stores of a bucket are in program order, so the order of
+// the adds -- and every rounding -- is the same.
 __global__ __launch_bounds__(kF64Threads) void k_f64_build(const int64_t* off, const int64_t* keys, const float* vals,
-                                                           int64_t nrows, HashParams hp, int accumulate, double* tab) {
+                                                           int64_t nrows, HashParams hp, int accumulate, int in_lds,
+                                                           double* tab) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int w = (int)hp.width;
-  double* row = reinterpret_cast<double*>(smem);                       // [w]
-  double* cv = row + w;                                                // [kF64Chunk]
+  double* lrow = reinterpret_cast<double*>(smem);                      // [w] (in_lds)
+  double* cv = lrow + (in_lds ? w : 0);                                // [kF64Chunk]
   uint32_t* cb = reinterpret_cast<uint32_t*>(cv + kF64Chunk);         // [kF64Chunk]
   const int tid = threadIdx.x;
   for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
@@ -46,7 +50,9 @@ __global__ __launch_bounds__(kF64Threads) void k_f64_build(const int64_t* off, c
     if (hi <= lo && accumulate) continue;  // nothing to add to this owner
     double* dst = tab + r * (int64_t)hp.depth * w;
     for (int d = 0; d < hp.depth; ++d) {
-      for (int j = tid; j < w; j += kF64Threads) row[j] = accumulate ? dst[(int64_t)d * w + j] : 0.0;
+      double* row = in_lds ? lrow : dst + (int64_t)d * w;
+      if (in_lds)
+        for (int j = tid; j < w; j += kF64Threads) row[j] = accumulate ? dst[(int64_t)d * w + j] : 0.0;
       for (int64_t c0 = lo; c0 < hi; c0 += kF64Chunk) {
         const int cnt = (int)min<int64_t>(kF64Chunk, hi - c0);
         __syncthreads();  // the previous chunk is consumed
@@ -61,7 +67,8 @@ __global__ __launch_bounds__(kF64Threads) void k_f64_build(const int64_t* off, c
         }
       }
       __syncthreads();
-      for (int j = tid; j < w; j += kF64Threads) dst[(int64_t)d * w + j] = row[j];
+      if (in_lds)
+        for (int j = tid; j < w; j += kF64Threads) dst[(int64_t)d * w + j] = row[j];
       __syncthreads();
     }
   }
@@ -325,7 +332,9 @@ static unsigned grid_for(int64_t work) {
 
 int f64_ingest_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val) {
   const int accumulate = h->empty ? 0 : 1;
-  const size_t lds = sizeof(double) * ((size_t)h->p.width + kF64Chunk) + sizeof(uint32_t) * kF64Chunk;
+  const size_t chunk_lds = (sizeof(double) + sizeof(uint32_t)) * kF64Chunk;
+  const int in_lds = sizeof(double) * (size_t)h->p.width + chunk_lds <= 160 * 1024 ? 1 : 0;
+  const size_t lds = (in_lds ? sizeof(double) * (size_t)h->p.width : 0) + chunk_lds;
   static bool attr = [] {
     (void)hipFuncSetAttribute((const void*)k_f64_build, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
@@ -336,7 +345,7 @@ int f64_ingest_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, co
   }
   TimedScope ts(h, "build_rows");
   hipLaunchKernelGGL(k_f64_build, dim3((unsigned)std::min<int64_t>(h->n, 65536)), dim3(kF64Threads), lds, h->stream,
-                     d_off, d_key, d_val, h->n, h->hp, 1, h->d_t64);
+                     d_off, d_key, d_val, h->n, h->hp, 1, in_lds, h->d_t64);
   (void)accumulate;  // the table was zeroed above, so every build accumulates
   CMS_HIP(hipGetLastError());
   h->empty = false;

@@ -115,8 +115,11 @@ def test_f64_mode_boundaries():
         with pytest.raises(CmsError) as ei:
             t.ingest_device_rows(rows, rows, None, 2)
         assert ei.value.code == CMS_E_STATE
-    with pytest.raises(CmsError) as ei:
-        SketchTable(10, depth=2, width=20000, counters="f64")
+    with pytest.raises(CmsError) as ei:  # past the fp64 mode's 2^20 counters per sketch row
+        SketchTable(10, depth=2, width=(1 << 20) + 1, counters="f64")
+    assert ei.value.code == CMS_E_PARAM
+    with pytest.raises(CmsError) as ei:  # u32 counters: LDS-staged rows up to 32768
+        SketchTable(10, depth=2, width=32769)
     assert ei.value.code == CMS_E_PARAM
 
 
@@ -191,3 +194,24 @@ def test_taste_mirror_float_datamodel(oracle, per_owner):
             assert same(sim.userSimilarity(int(uid[u1]), int(uid[u2])), oracle.cosine_cm(exp[u1], exp[u2]))
     assert sim.table.counters == "f64"
     sim.close()
+
+
+@pytest.mark.parametrize("w", [16385, 65536])
+def test_f64_wide_rows_built_in_place(oracle, w):
+    """fp64 counters wider than an LDS row (DoubleCountMinSketch(width, depth,
+    ...) has no width limit, `T/impl/common/DoubleCountMinSketch.java:32-36`):
+    the build updates the table rows in place, each bucket by one thread in
+    key order, so counters and similarities stay bit-exact."""
+    n, d = 60, 2
+    items, users, vals = _stream(n, 40_000, 5 + w, "ratings")
+    a, b = oracle.hash_params(42, d)
+    exp = oracle.build_table(n, d, w, a, b, items, users, vals)
+    with SketchTable(n, depth=d, width=w, seed=42, counters="f64") as t:
+        t.ingest(items, users, vals)
+        t.finalize()
+        assert same(t.read_counters(), exp)
+        for q in (0, n - 1):
+            ref = oracle.similarities_row(exp, q)
+            ref[q] = oracle.cosine_cm(exp[q], exp[q])
+            assert same(t.similarities(q, np.arange(n)), ref), q
+        assert t.point_query(1, int(users[0])) == oracle.sketch_get(exp[1], a, b, int(users[0]))
