@@ -300,6 +300,12 @@ struct cms_handle {
   cms::DevBuf po_shape;                          // PoShape [n]
   cms::DevBuf po_sk, po_norm, po_nsq;            // own sketches [sum d*w] u32; norms [sum d] u64 / f64 sqrt
   cms::DevBuf po_scratch;                        // per-block bucket rows for widths beyond LDS
+  // candidates grouped by shape class for the all-pairs slabs (po_allpairs_slab):
+  // PoGroup [po_ngroups] (LDS-sized groups of one (w, d) class, then the wide
+  // owners one per group), po_cmem the owner rows in group order
+  cms::DevBuf po_groups, po_cmem, po_redo;
+  int64_t po_ngroups = 0, po_nnarrow = 0;
+  int32_t po_gmax_lds = 0;                       // largest LDS image of a narrow group (bytes)
 
   // instrumentation
   int timing = 0;  // 0 off, 1 the roofline kernels' scopes only, 2 every scope (phase breakdown)
@@ -467,6 +473,14 @@ struct PoShape {
   int64_t roff;      // first (owner, row) norm slot
   uint64_t barrett;  // floor((2^64-1)/w)
   int32_t w, d;      // 0 when the owner's (delta, epsilon) raise CMException
+};
+// Candidates of one shape class (w, d) whose own sketches share a workgroup's
+// LDS (cnt <= kPoGroupMax), or one wide owner (wide = 1: sketch read from HBM)
+struct PoGroup {
+  uint64_t barrett;  // floor((2^64-1)/w)
+  int32_t w, d;
+  int32_t m0, cnt;   // members po_cmem[m0, m0 + cnt)
+  int32_t wide, pad;
 };
 int po_load_csr(cms_handle* h, const int64_t* d_off, const int64_t* d_key, const float* d_val, int64_t npairs,
                 const int64_t* h_off);

@@ -187,7 +187,8 @@ struct PoPairArgs {
   int64_t nq, m;
   uint32_t* scratch;     // [gridDim][max_w] zeroed u32 rows (widths > kPoHist)
   int64_t scratch_w;
-  double* out;           // [nq][m]
+  double* out;           // [nq][m], or with ldo > 0 a slab [nq][ldo] at column u2
+  int64_t ldo;
   int32_t weighted;
 };
 
@@ -214,26 +215,41 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     uint32_t* hist = (w <= (uint32_t)kPoHist) ? lds : gsc;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
     double minc = DBL_MAX;
-    for (int d = 0; d < s.d; ++d) {
-      const uint32_t* brow = a.sk + s.soff + (int64_t)d * w;
-      uint64_t ab = 0;
+    // u1's counters at u2's shape: pass 1 adds every preference into the
+    // bucket row; pass 2 takes each bucket back to zero with an exchange, so the
+    // first key of a bucket collects its whole count c (c^2 into valueA) and
+    // the row is clean for the next pair -- O(#preferences), not O(w)
+    auto add_pass = [&](int d, uint64_t* ab, const uint32_t* brow) {
       for (int64_t i = k0 + lane; i < k1; i += kPoThreads) {
         const uint32_t j = bucket_wb(hp, d, a.kp[i], w, s.barrett);
         const uint32_t v = a.inc[i];
         atomicAdd(&hist[j], v);
-        ab = sat_add(ab, (uint64_t)v * brow[j]);
+        if (ab) *ab = sat_add(*ab, (uint64_t)v * brow[j]);
       }
       __syncthreads();
+    };
+    auto clear_pass = [&](int d) {
       uint64_t a2 = 0;
-      for (uint32_t j = lane; j < w; j += kPoThreads) a2 = sat_add(a2, (uint64_t)hist[j] * hist[j]);
-      a2 = po_wave_sum(a2);
+      for (int64_t i = k0 + lane; i < k1; i += kPoThreads) {
+        const uint32_t c = atomicExch(&hist[bucket_wb(hp, d, a.kp[i], w, s.barrett)], 0u);
+        a2 = sat_add(a2, (uint64_t)c * c);
+      }
+      __syncthreads();
+      return a2;
+    };
+    for (int d = 0; d < s.d; ++d) {
+      const uint32_t* brow = a.sk + s.soff + (int64_t)d * w;
+      uint64_t ab = 0;
+      add_pass(d, &ab, brow);
+      const uint64_t a2 = po_wave_sum(clear_pass(d));
       ab = po_wave_sum(ab);
       const uint64_t b2 = a.norm[s.roff + d];
       double valueAB, den;
       if (a2 < (1ULL << 53) && b2 < (1ULL << 53)) {
         valueAB = (double)ab;  // ab <= sqrt(a2 * b2) < 2^53: exact
         den = __dmul_rn(__dsqrt_rn((double)a2), a.nsq[s.roff + d]);
-      } else {  // the reference's sequential fp64 loop (:128-134), every lane alike
+      } else {  // the reference's sequential fp64 loop (:128-134) over the rebuilt row, every lane alike
+        add_pass(d, nullptr, brow);
         double A = 0.0, B = 0.0, AB = 0.0;
         for (uint32_t j = 0; j < w; ++j) {
           const double xa = (double)hist[j], xb = (double)brow[j];
@@ -243,16 +259,130 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
         }
         valueAB = AB;
         den = __dmul_rn(__dsqrt_rn(A), __dsqrt_rn(B));
+        __syncthreads();
+        (void)clear_pass(d);
       }
-      __syncthreads();
-      for (uint32_t j = lane; j < w; j += kPoThreads) hist[j] = 0u;  // keep the row zero for the next use
-      __syncthreads();
       if (den != 0.0) minc = java_min(minc, __ddiv_rn(valueAB, den));
     }
     if (lane == 0) {
       double r = (minc == DBL_MAX) ? __builtin_nan("") : minc;
       if (r == r) r = normalize_weight(r, a.weighted);
-      a.out[t] = r;
+      a.out[a.ldo > 0 ? (t / a.m) * a.ldo + u2 : t] = r;
+    }
+  }
+}
+
+// ------------------------------------------- all-pairs slabs by shape class --
+// userSimilarity(u1, u2) for a block of query rows against every candidate,
+// the candidates grouped by their shape class (w, d): every member of a class
+// hashes u1's preferences identically (CosineCM.java:86 builds u1 at u2's
+// (delta, epsilon)), so a workgroup holds up to kPoGroupMax members' own
+// sketches in LDS and each of its waves takes one query at a time -- u1's
+// preferences are hashed ONCE per sketch row and gathered from every member's
+// row (valueAB, exact integers accumulated in fp64: each term and partial sum
+// is below 2^53 whenever both norms are), while a per-wave bucket row gives
+// valueA with the exchange pass of k_po_pairs.  Pairs past the exact regime
+// (a norm >= 2^53) are listed for k_po_pairs' sequential replay.
+constexpr int kPoGroupMax = 16;            // members per narrow group (fp64 accumulators per lane)
+constexpr int kPoGroupLds = 48 * 1024;     // LDS for a group's own sketches
+constexpr int kPoGroupHistW = 2048;        // narrow classes: one LDS bucket row per wave
+constexpr int kPoGroupWaves = 4;
+constexpr int64_t kPoQueryChunk = 1024;    // query rows per workgroup (the group loads once)
+
+struct PoAllArgs {
+  const int64_t* off;
+  const uint64_t* kp;
+  const uint32_t* inc;
+  const PoShape* shp;
+  const uint32_t* sk;
+  const uint64_t* norm;
+  const double* nsq;
+  const PoGroup* groups;
+  const int64_t* cmem;
+  int64_t q0, qc, n;
+  double* slab;  // [qc][n], column = candidate row
+  unsigned long long* redo;  // (u1 << 32) | u2 of pairs past the exact regime
+  uint32_t* redo_cnt;
+  uint32_t redo_cap;
+  int32_t weighted;
+};
+
+__device__ __forceinline__ double po_wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs a, HashParams hp) {
+  extern __shared__ __align__(16) uint32_t lds[];
+  const PoGroup g = a.groups[blockIdx.y];
+  const int w = g.w, d = g.d, cnt = g.cnt;
+  const int dw = d * w;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t* bl = lds;                           // [cnt][d][w] members' own sketches
+  uint32_t* hist = lds + cnt * dw + wv * w;     // this wave's bucket row
+  for (int m = 0; m < cnt; ++m) {
+    const uint32_t* src = a.sk + a.shp[a.cmem[g.m0 + m]].soff;
+    for (int j = tid; j < dw; j += 64 * kPoGroupWaves) bl[m * dw + j] = src[j];
+  }
+  for (int j = tid; j < kPoGroupWaves * w; j += 64 * kPoGroupWaves) lds[cnt * dw + j] = 0u;
+  __syncthreads();
+  const int64_t qa = (int64_t)blockIdx.x * kPoQueryChunk, qb = min(a.qc, qa + kPoQueryChunk);
+  for (int64_t q = qa + wv; q < qb; q += kPoGroupWaves) {
+    const int64_t u1 = a.q0 + q;
+    const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+    double minc[kPoGroupMax];
+#pragma unroll
+    for (int m = 0; m < kPoGroupMax; ++m) minc[m] = DBL_MAX;
+    uint32_t inexact = 0u;
+    for (int r = 0; r < d; ++r) {
+      double acc[kPoGroupMax];
+#pragma unroll
+      for (int m = 0; m < kPoGroupMax; ++m) acc[m] = 0.0;
+      const uint32_t* brow = bl + r * w;
+      for (int64_t i = k0 + lane; i < k1; i += 64) {
+        const uint32_t j = bucket_wb(hp, r, a.kp[i], (uint32_t)w, g.barrett);
+        const uint32_t v = a.inc[i];
+        atomicAdd(&hist[j], v);
+        const double vd = (double)v;
+#pragma unroll
+        for (int m = 0; m < kPoGroupMax; ++m)
+          if (m < cnt) acc[m] = __fma_rn(vd, (double)brow[m * dw + j], acc[m]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's adds land before its exchanges
+      uint64_t a2 = 0;
+      for (int64_t i = k0 + lane; i < k1; i += 64) {
+        const uint32_t c = atomicExch(&hist[bucket_wb(hp, r, a.kp[i], (uint32_t)w, g.barrett)], 0u);
+        a2 = sat_add(a2, (uint64_t)c * c);
+      }
+      a2 = po_wave_sum(a2);
+      const bool a_ok = a2 < (1ULL << 53);
+      const double sa = __dsqrt_rn((double)a2);
+#pragma unroll
+      for (int m = 0; m < kPoGroupMax; ++m) {
+        if (m >= cnt) continue;
+        const double ab = po_wave_sum_f64(acc[m]);
+        const int64_t ro = a.shp[a.cmem[g.m0 + m]].roff + r;
+        if (a_ok && a.norm[ro] < (1ULL << 53)) {
+          const double den = __dmul_rn(sa, a.nsq[ro]);
+          if (den != 0.0) minc[m] = java_min(minc[m], __ddiv_rn(ab, den));
+        } else {
+          inexact |= 1u << m;
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < kPoGroupMax; ++m) {
+      if (m >= cnt || lane != m) continue;
+      const int64_t u2 = a.cmem[g.m0 + m];
+      double res = minc[m] == DBL_MAX ? __builtin_nan("") : minc[m];
+      if (res == res) res = normalize_weight(res, a.weighted);
+      if ((inexact >> m) & 1u) {  // k_po_pairs replays the reference's sequential loop
+        res = __builtin_nan("");
+        const uint32_t slot = atomicAdd(a.redo_cnt, 1u);
+        if (slot < a.redo_cap) a.redo[slot] = ((unsigned long long)u1 << 32) | (unsigned long long)u2;
+      }
+      a.slab[q * a.n + u2] = res;
     }
   }
 }
@@ -407,6 +537,74 @@ int po_require_shapes(cms_handle* h, const int64_t* rows, int64_t m) {
   return CMS_OK;
 }
 
+// Candidate groups of the all-pairs slabs: owners sorted by shape class
+// (d, w); a class whose bucket row fits a wave's LDS row and whose sketches
+// fit the group image is cut into groups of up to kPoGroupMax members, every
+// other owner (wide) is its own group for k_po_pairs.  Narrow groups first.
+static int po_build_groups(cms_handle* h) {
+  const int64_t n = h->n;
+  std::vector<int64_t> ord;
+  ord.reserve(n);
+  for (int64_t r = 0; r < n; ++r)
+    if (h->h_po_w[r] > 0) ord.push_back(r);
+  std::stable_sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
+    return h->h_po_d[x] != h->h_po_d[y] ? h->h_po_d[x] < h->h_po_d[y] : h->h_po_w[x] < h->h_po_w[y];
+  });
+  std::vector<PoGroup> narrow, wide;
+  std::vector<int64_t> cmem_n, cmem_w;
+  int32_t gmax = 0;
+  for (size_t i = 0; i < ord.size();) {
+    const int32_t w = h->h_po_w[ord[i]], d = h->h_po_d[ord[i]];
+    size_t e = i;
+    while (e < ord.size() && h->h_po_w[ord[e]] == w && h->h_po_d[ord[e]] == d) ++e;
+    const int64_t img = (int64_t)w * d * 4;
+    if (w <= kPoGroupHistW && img <= kPoGroupLds) {
+      const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPoGroupMax, kPoGroupLds / img));
+      for (size_t m = i; m < e; m += G) {
+        const int cnt = (int)std::min<size_t>(G, e - m);
+        PoGroup g{};
+        g.w = w;
+        g.d = d;
+        g.barrett = (~0ULL) / (uint64_t)w;
+        g.m0 = (int32_t)cmem_n.size();
+        g.cnt = cnt;
+        for (int q = 0; q < cnt; ++q) cmem_n.push_back(ord[m + q]);
+        narrow.push_back(g);
+        gmax = std::max<int32_t>(gmax, (int32_t)(cnt * img + (int64_t)kPoGroupWaves * w * 4));
+      }
+    } else {
+      for (size_t m = i; m < e; ++m) cmem_w.push_back(ord[m]);
+    }
+    i = e;
+  }
+  std::vector<PoGroup> groups(narrow);
+  std::vector<int64_t> cmem(cmem_n);
+  cmem.insert(cmem.end(), cmem_w.begin(), cmem_w.end());
+  for (size_t m = 0; m < cmem_w.size(); ++m) {  // wide owners: one group each (members at the end of cmem)
+    PoGroup g{};
+    g.w = h->h_po_w[cmem_w[m]];
+    g.d = h->h_po_d[cmem_w[m]];
+    g.barrett = (~0ULL) / (uint64_t)g.w;
+    g.m0 = (int32_t)(cmem_n.size() + m);
+    g.cnt = 1;
+    g.wide = 1;
+    groups.push_back(g);
+  }
+  CMS_HIP(h->po_groups.ensure(sizeof(PoGroup) * std::max<size_t>(1, groups.size())));
+  CMS_HIP(h->po_cmem.ensure(sizeof(int64_t) * std::max<size_t>(1, cmem.size())));
+  if (!groups.empty())
+    CMS_HIP(hipMemcpyAsync(h->po_groups.ptr, groups.data(), sizeof(PoGroup) * groups.size(), hipMemcpyHostToDevice,
+                           h->stream));
+  if (!cmem.empty())
+    CMS_HIP(hipMemcpyAsync(h->po_cmem.ptr, cmem.data(), sizeof(int64_t) * cmem.size(), hipMemcpyHostToDevice,
+                           h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));  // the host vectors die on return
+  h->po_ngroups = (int64_t)groups.size();
+  h->po_nnarrow = (int64_t)narrow.size();
+  h->po_gmax_lds = gmax;
+  return CMS_OK;
+}
+
 int po_finalize(cms_handle* h) {
   if (!h->po_loaded) return set_error(CMS_E_STATE, "per-owner mode: ingest the DataModel (CSR) first");
   if (!h->po_configured)
@@ -442,6 +640,7 @@ int po_finalize(cms_handle* h) {
       CMS_HIP(hipMemsetAsync(h->po_scratch.ptr, 0, h->po_scratch.bytes, h->stream));
     }
   }
+  if (int rc = po_build_groups(h)) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
   return CMS_OK;
 }
@@ -466,6 +665,7 @@ int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int
   a.scratch = wide ? h->po_scratch.as<uint32_t>() : nullptr;
   a.scratch_w = wide ? h->po_max_w : 0;
   a.out = d_out;
+  a.ldo = 0;
   a.weighted = h->p.weighting == CMS_WEIGHTED;
   TimedScope ts(h, "po_pair_cosine", s == nullptr);
   hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(nq * m, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
@@ -496,6 +696,93 @@ int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb
   return CMS_OK;
 }
 
+// slab[q][c] = userSimilarity(q0 + q, c) for q < qc and every candidate c
+// (d_qrows: the rows q0 .. q0 + qc - 1 on the device): the narrow groups on
+// k_po_group_pairs, the wide owners and any pair past the exact regime on
+// k_po_pairs (scattered into the slab's columns).
+static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t* d_qrows, double* slab) {
+  const int64_t n = h->n;
+  PoAllArgs a{};
+  a.off = h->po_off.as<int64_t>();
+  a.kp = h->po_kp.as<uint64_t>();
+  a.inc = h->po_inc.as<uint32_t>();
+  a.shp = h->po_shape.as<PoShape>();
+  a.sk = h->po_sk.as<uint32_t>();
+  a.norm = h->po_norm.as<uint64_t>();
+  a.nsq = h->po_nsq.as<double>();
+  a.groups = h->po_groups.as<PoGroup>();
+  a.cmem = h->po_cmem.as<int64_t>();
+  a.q0 = q0;
+  a.qc = qc;
+  a.n = n;
+  a.slab = slab;
+  a.weighted = h->p.weighting == CMS_WEIGHTED;
+  constexpr uint32_t kRedoCap = 1u << 16;
+  CMS_HIP(h->po_redo.ensure(sizeof(unsigned long long) * kRedoCap + 16));
+  a.redo = h->po_redo.as<unsigned long long>();
+  a.redo_cnt = reinterpret_cast<uint32_t*>(a.redo + kRedoCap);
+  a.redo_cap = kRedoCap;
+  CMS_HIP(hipMemsetAsync(a.redo_cnt, 0, sizeof(uint32_t), h->stream));
+  if (h->po_nnarrow > 0) {
+    TimedScope ts(h, "po_group_pairs");
+    static bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)k_po_group_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return true;
+    }();
+    (void)attr;
+    const dim3 grid((unsigned)((qc + kPoQueryChunk - 1) / kPoQueryChunk), (unsigned)h->po_nnarrow);
+    hipLaunchKernelGGL(k_po_group_pairs, grid, dim3(64 * kPoGroupWaves), (size_t)h->po_gmax_lds, h->stream, a, h->hp);
+    CMS_HIP(hipGetLastError());
+  }
+  const int64_t nwide = h->po_ngroups - h->po_nnarrow;
+  if (nwide > 0) {  // wide candidates: one wave per pair, columns scattered into the slab
+    PoPairArgs p{};
+    p.off = a.off;
+    p.kp = a.kp;
+    p.inc = a.inc;
+    p.shp = a.shp;
+    p.sk = a.sk;
+    p.norm = a.norm;
+    p.nsq = a.nsq;
+    p.qrows = d_qrows;
+    p.crows = a.cmem + (n - nwide);  // the wide owners close po_cmem
+    p.nq = qc;
+    p.m = nwide;
+    const bool wide = h->po_max_w > kPoHist;
+    p.scratch = wide ? h->po_scratch.as<uint32_t>() : nullptr;
+    p.scratch_w = wide ? h->po_max_w : 0;
+    p.out = slab;
+    p.ldo = n;
+    p.weighted = a.weighted;
+    TimedScope ts(h, "po_pair_cosine");
+    hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(qc * nwide, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
+                       h->stream, p, h->hp);
+    CMS_HIP(hipGetLastError());
+  }
+  uint32_t nredo = 0;
+  CMS_HIP(hipMemcpyAsync(&nredo, a.redo_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (nredo > kRedoCap) return set_error(CMS_E_OVERFLOW, "per-owner all-pairs: %u pairs past the exact regime", nredo);
+  if (nredo > 0) {  // the reference's sequential fp64 loop for these pairs (k_po_pairs)
+    std::vector<unsigned long long> redo(nredo);
+    CMS_HIP(hipMemcpy(redo.data(), a.redo, sizeof(unsigned long long) * nredo, hipMemcpyDeviceToHost));
+    DevBuf rows;
+    CMS_HIP(rows.ensure(sizeof(int64_t) * 2 * nredo));
+    std::vector<int64_t> hr(2 * nredo);
+    for (uint32_t i = 0; i < nredo; ++i) {
+      hr[2 * i] = (int64_t)(redo[i] >> 32);
+      hr[2 * i + 1] = (int64_t)(redo[i] & 0xFFFFFFFFu);
+    }
+    CMS_HIP(hipMemcpy(rows.ptr, hr.data(), sizeof(int64_t) * 2 * nredo, hipMemcpyHostToDevice));
+    for (uint32_t i = 0; i < nredo; ++i) {
+      const int64_t* pr = rows.as<int64_t>() + 2 * i;
+      if (int rc = po_pair_cosines(h, pr, 1, pr + 1, 1, slab + (hr[2 * i] - q0) * n + hr[2 * i + 1])) return rc;
+    }
+    CMS_HIP(hipStreamSynchronize(h->stream));
+  }
+  return CMS_OK;
+}
+
 // mostSimilar for query rows [row_begin, row_begin + row_count): a slab of
 // userSimilarity(query, candidate) over every candidate (the MostSimilarEstimator
 // argument order, GenericUserBasedRecommender.java:231-247), then the shared
@@ -518,7 +805,11 @@ int po_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k
       qs.push_back(TopQuery{q, row_begin + r0 + q, r0 + q});
     }
     CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, qrows.data(), sizeof(int64_t) * rcnt, hipMemcpyHostToDevice, h->stream));
-    if ((rc = po_pair_cosines(h, h->ws_query.as<int64_t>(), rcnt, nullptr, n, h->ws_slab.as<double>()))) return rc;
+    if (h->f64) {
+      if ((rc = po_pair_cosines(h, h->ws_query.as<int64_t>(), rcnt, nullptr, n, h->ws_slab.as<double>()))) return rc;
+    } else if ((rc = po_allpairs_slab(h, row_begin + r0, rcnt, h->ws_query.as<int64_t>(), h->ws_slab.as<double>()))) {
+      return rc;
+    }
     if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, nullptr, d_ids, d_scores, d_counts))) return rc;
   }
   return CMS_OK;

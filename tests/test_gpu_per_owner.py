@@ -158,6 +158,48 @@ def test_wide_shapes_global_scratch_and_inexact_regime(oracle):
         for q in range(n):
             exp = np.array([oracle.per_owner_similarity(off, keys, vals, shapes, a, b, q, c) for c in range(n)])
             assert same(t.similarities(int(uid[q]), uid), exp)
+        # the all-pairs slabs: narrow classes on the grouped kernel, the wide
+        # owners (5000, 9000, 4097) on k_po_pairs, and owner 2's pairs (norms
+        # past 2^53) replayed through the sequential path
+        ids, sc, cnt = t.top_k_all(4)
+        for q in range(n):
+            row = np.array([oracle.per_owner_similarity(off, keys, vals, shapes, a, b, q, c) for c in range(n)])
+            row[q] = np.nan
+            eids, esc = oracle.top_users(uid, row, 4)
+            assert ids[q, :cnt[q]].tolist() == eids.tolist() and same(sc[q, :cnt[q]], esc), q
+
+
+def test_grouped_all_pairs_many_classes(oracle):
+    """The all-pairs top-k over a model whose owners share shape classes
+    (groups of up to 16 candidates per workgroup, classes split over several
+    groups): equal to the per-row similarities (k_po_pairs) and to the
+    oracle's TopItems loop on sampled rows."""
+    users, items, ratings = movielens_like(1500, 300, 45_000, seed=21, min_per_user=3)
+    uid = np.unique(users)
+    rows = np.searchsorted(uid, users)
+    order = np.lexsort((items, rows))
+    off, keys, vals = to_csr(rows[order], items[order], uid.size, ratings[order])
+    n, k = uid.size, 20
+    a, b = oracle.hash_params(SEED, 32)
+    with make(uid, off, keys, vals) as t:
+        t.configure_owner_shapes(1.0, 300)
+        t.finalize()
+        w, d = t.owner_shapes()[2:]
+        classes = {}
+        for r in range(n):
+            classes.setdefault((int(w[r]), int(d[r])), []).append(r)
+        assert max(len(v) for v in classes.values()) > 16  # a class spans several groups
+        ids, sc, cnt = t.top_k_all(k)
+        for q in [0, 1, n // 3, n // 2, n - 1]:
+            row = t.similarities(int(uid[q]), uid)  # per-pair kernel
+            row[q] = np.nan
+            eids, esc = oracle.top_users(uid, row, k)
+            assert ids[q, :cnt[q]].tolist() == eids.tolist() and same(sc[q, :cnt[q]], esc), q
+        for q in [0, n - 1]:
+            row = np.array([oracle.per_owner_similarity(off, keys, vals, (w, d), a, b, q, c) for c in range(n)])
+            row[q] = np.nan
+            eids, esc = oracle.top_users(uid, row, k)
+            assert ids[q, :cnt[q]].tolist() == eids.tolist() and same(sc[q, :cnt[q]], esc), q
 
 
 def test_errors_like_the_reference(oracle):
