@@ -121,7 +121,7 @@ def csr_on_device(items, users, n):
     return off, ckeys
 
 
-def per_owner_scale(items, users, n, n_users, rows=64):
+def per_owner_scale(items, users, n, n_users, rows=1024, all_pairs_budget_s=120.0):
     """The reference's native per-owner mode beyond
     config 1: the stream as the transposed DataModel (n items keyed by user),
     CountMinSketchConfig(q=1) shapes for every item (CountMinSketchConfig.java:
@@ -132,7 +132,8 @@ def per_owner_scale(items, users, n, n_users, rows=64):
     from mahout_amd import SketchTable
     off, ckeys = csr_on_device(items, users, n)
     po = {"workload": f"{int(items.numel())}-pair DataModel, {n} items x {n_users} users; CountMinSketchConfig(q=1) "
-                      f"per item, top-100 of {rows}-item query blocks over all {n} candidates (ordered pairs)"}
+                      f"per item, top-100 of {rows}-item query blocks over all {n} candidates (ordered pairs), "
+                      f"then the whole all-pairs top-100 of every item"}
     with SketchTable.per_owner_shapes(n, seed=42) as t:
         t.ingest_csr_device(off, ckeys)
         torch.cuda.synchronize()
@@ -151,6 +152,19 @@ def per_owner_scale(items, users, n, n_users, rows=64):
             dt = time.perf_counter() - t0
             po[f"{name}_rows"] = {"first_row": r0, "rows": rows, "s": dt, "ordered_pairs_per_s": rows * n / dt,
                                   "full_lists": int((cnt == 100).sum())}
+        # the WHOLE all-pairs top-100 (every one of the n*(n-1) ordered pairs),
+        # when the block rates predict it finishes within all_pairs_budget_s
+        rate = min(po["median_rows"]["ordered_pairs_per_s"], po["head_rows"]["ordered_pairs_per_s"])
+        po["all_pairs_predicted_s"] = n * n / rate
+        if n * n / rate <= all_pairs_budget_s:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            _, _, cnt = t.top_k_all(100)
+            dt = time.perf_counter() - t0
+            po["all_pairs"] = {"s": dt, "ordered_pairs": n * (n - 1), "ordered_pairs_per_s": n * (n - 1) / dt,
+                               "full_lists": int((cnt == 100).sum()),
+                               "path": "candidates grouped by (w, d) class: k_po_group_pairs for classes whose "
+                                       "sketches share a workgroup's LDS, k_po_pairs for the wide owners"}
     del off, ckeys
     return po
 
@@ -977,7 +991,7 @@ def config2_line(args, rank, world, local, device):
             "wall_s": dt, "unique_item_pair_cosines_per_s": n * (n - 1) / 2 / dt,
             "full_lists": int((cnt_all == 100).sum().item())}
         # the reference's per-owner-shape mode at this scale
-        extras["per_owner_shapes_cfg2"] = per_owner_scale(items, users, n, c2.n_users, 64)
+        extras["per_owner_shapes_cfg2"] = per_owner_scale(items, users, n, c2.n_users)
         out["extras"] = extras
     table.close()
     del items, users
