@@ -107,7 +107,17 @@ int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, i
 
 /* new DoubleCountMinSketch(width, depth, hfBuilder) for every owner at once
  * (T/impl/common/DoubleCountMinSketch.java:32-42) plus the CosineCM instance
- * state (CosineCM.java:26-39).  Counters start at zero. */
+ * state (CosineCM.java:26-39).  Counters start at zero.
+ *
+ * Tunables.  The library reads these environment variables once, here, and
+ * never again (a handle's behaviour is fixed at creation); none changes any
+ * result, only the storage or kernel a result comes from:
+ *   CMS_NO_FORMS=1        narrow rows stay u16 (no 1/2/4/8-bit row forms)
+ *   CMS_BIT_KEYS=<n>      byte-class owners of <= n keys try 1-bit rows first (64)
+ *   CMS_CRUMB_KEYS=<n>    ... of <= n keys 2-bit rows (256)
+ *   CMS_NO_HOT_ROUTING=1  the COO partition sends every owner through both passes
+ *   CMS_NO_FP4=1          no e2m1 operand image: every single-limb pair on int8 MFMA
+ *   CMS_NO_MLS=1          multi-limb slabs on the 128-row tile kernel instead of k_cosine_mls */
 int cms_create(const cms_params* p, cms_handle** out);
 void cms_destroy(cms_handle* h);
 const char* cms_last_error(void);
