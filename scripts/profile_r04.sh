@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-3 rocprofv3 passes (one counter group per run, kernel trace only; no
-# sys/runtime trace).  Usage: scripts/profile_r03.sh {ingest|config2|cosine}
+# Round-4 rocprofv3 passes (one counter group per run, kernel trace only; no
+# sys/runtime trace).  Usage: scripts/profile_r04.sh {ingest|config2|cosine}
 #   ingest  -- the headline (config-3 shape) bench command: kernel stats,
 #              FETCH_SIZE, WRITE_SIZE
 #   config2 -- the config-2 line alone (bench.py --no-headline): the same passes
 #   cosine  -- the config-4 job (scripts/cos_job_probe.py): kernel stats, then
 #              MFMA busy / waits, LDS, L2 hit, FETCH_SIZE passes
-# Summaries: scripts/summarize_profile.py / summarize_cos_pmc.py -> profiles/r03.
+# Summaries: scripts/summarize_profile.py / summarize_cos_pmc.py -> profiles/r04.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
