@@ -1147,7 +1147,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   {
     TimedScope ts(h, "build_rows");
     auto kern = k_build_rows<kBuildStoreForm>;
-    if (fast_slices) {
+    // the split owners' slices, on the handle's stream (after the side stream
+    // forks, so they overlap the byte and mid classes)
+    auto launch_slices = [&]() -> int {
+      if (!fast_slices) return CMS_OK;
       static bool attr = [] {
         (void)hipFuncSetAttribute((const void*)k_build_slices, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
@@ -1156,7 +1159,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
                          keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
       CMS_HIP(hipGetLastError());
-    }
+      return CMS_OK;
+    };
     if (forms) {
       // owner classes: slot rows -> k_build_slices / k_build_rows (the
       // handle's stream), byte rows -> k_build_nibbles (+ k_build_bytes for
@@ -1207,6 +1211,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,
                          h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
       CMS_HIP(hipGetLastError());
+      if ((rc0 = launch_slices())) return rc0;
       // slot rows: at most the slots in use (host-known), plus the mapped slices
       const int64_t nslot = std::min<int64_t>(n, h->hot_used);
       hipLaunchKernelGGL(kern, dim3((unsigned)(row_emax + nslot)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi,
@@ -1221,6 +1226,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
         CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join2, 0));
       }
     } else {
+      if ((rc0 = launch_slices())) return rc0;
       hipLaunchKernelGGL(kern, dim3((unsigned)(row_emax + n)), dim3(kBuildThreads), lds, h->stream, d_lo, d_hi, keys,
                          d_val, n, h->hp, kSliceKeys, row_hot, hot, extra_map, counters, row_emax, h->tview(),
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, accumulate, slices_done,
