@@ -51,9 +51,10 @@ constexpr int kMaxBins = 4096;
 #ifndef CMS_P1_BLOCKS
 #define CMS_P1_BLOCKS 2048
 #endif
-// issue the next tile's loads before this tile's write-out
-#ifndef CMS_P1_PREFETCH
-#define CMS_P1_PREFETCH 1
+// largest pass-1 tile, in rounds of kPartTile pairs (k_p1_scatter<R>: the
+// largest R <= CMS_P1_ROUNDS whose tile fits the LDS)
+#ifndef CMS_P1_ROUNDS
+#define CMS_P1_ROUNDS 4
 #endif
 #ifndef CMS_P2_PREFETCH
 #define CMS_P2_PREFETCH 1
@@ -169,21 +170,12 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t r, int s2, int P1, const uin
   return r >> s2;
 }
 
-// scatter stores: plain, or non-temporal with CMS_PART_NT (experiment)
-template <class T>
-__device__ __forceinline__ void pstore(T* p, T v) {
-#ifdef CMS_PART_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-
 // Pass-1 work is cut into tiles of kPartTile pairs, and block b takes tiles
 // b, b + NB, b + 2 NB, ... (the same assignment in k_p1_hist and
 // k_p1_scatter): at any moment the blocks stream one contiguous window of the
 // stream instead of NB separate regions (DRAM page locality; the contiguous
 // per-block chunks streamed the owner column at ~3.4 TB/s).
+template <int R>
 __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, int s2, int P1, int64_t nrows,
                                                  uint32_t* H1, int NB, uint32_t* flags,
                                                  const unsigned long long* hotkey) {
@@ -194,14 +186,18 @@ __global__ __launch_bounds__(256) void k_p1_hist(const int64_t* row, int64_t n, 
   if (tab) load_hot_table(hotkey, tab);
   __syncthreads();
   bool bad = false;
-  const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
+  // tiles of R * kPartTile pairs (k_p1_scatter<R>'s), each counted as R
+  // sub-tiles of kPartTile
+  const int64_t ntiles = (n + (int64_t)R * kPartTile - 1) / ((int64_t)R * kPartTile);
   const bool vec = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-  // 256 threads x 8 16-byte loads = one 4096-pair tile, all loads in flight;
+  // 256 threads x 8 16-byte loads = one 4096-pair sub-tile, all loads in flight;
   // whole waves step together so the aggregated increments see converged lanes
   constexpr int kL = kPartTile / 2 / 256;
   static_assert(kL * 2 * 256 == kPartTile, "tile = 256 threads x kL pair loads");
-  for (int64_t t = blockIdx.x; t < ntiles; t += NB) {
-    const int64_t t0 = t * kPartTile, tn = min<int64_t>(kPartTile, n - t0);
+  for (int64_t t = blockIdx.x; t < ntiles; t += NB)
+  for (int sub = 0; sub < R; ++sub) {
+    const int64_t t0 = (t * R + sub) * kPartTile, tn = min<int64_t>(kPartTile, n - t0);
+    if (tn <= 0) break;
     longlong2 v[kL];
 #pragma unroll
     for (int u = 0; u < kL; ++u) {
@@ -255,17 +251,17 @@ struct TileLds {
 
 // LDS image of a tile: keys, then values and fine indices only when the pass
 // carries them (a smaller image lets more workgroups share a CU).
-__device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_val, bool has_fine) {
+__device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_val, bool has_fine, int tile = kPartTile) {
   TileLds t;
   unsigned char* q = smem;
   t.key = reinterpret_cast<uint32_t*>(q);
-  q += sizeof(uint32_t) * kPartTile;
+  q += sizeof(uint32_t) * tile;
   t.val = reinterpret_cast<float*>(q);
-  if (has_val) q += sizeof(float) * kPartTile;
+  if (has_val) q += sizeof(float) * tile;
   t.fine = reinterpret_cast<uint16_t*>(q);
-  if (has_fine) q += sizeof(uint16_t) * kPartTile;
+  if (has_fine) q += sizeof(uint16_t) * tile;
   t.bin = reinterpret_cast<uint16_t*>(q);
-  q += sizeof(uint16_t) * kPartTile;
+  q += sizeof(uint16_t) * tile;
   t.cursor = reinterpret_cast<uint32_t*>(q);
   t.hist = t.cursor + P;
   t.off = t.hist + P;
@@ -273,8 +269,8 @@ __device__ __forceinline__ TileLds carve(unsigned char* smem, int P, bool has_va
   return t;
 }
 
-static size_t tile_lds_bytes(int P, bool has_val, bool has_fine, bool hot = false) {
-  return (size_t)kPartTile * (4 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4 +
+static size_t tile_lds_bytes(int P, bool has_val, bool has_fine, bool hot = false, int tile = kPartTile) {
+  return (size_t)tile * (4 + (has_val ? 4 : 0) + (has_fine ? 2 : 0) + 2) + (size_t)3 * P * 4 + 64 * 4 +
          (hot ? sizeof(uint32_t) * kHotBins : 0);
 }
 
@@ -284,93 +280,107 @@ static size_t tile_lds_bytes(int P, bool has_val, bool has_fine, bool hot = fals
 // values) go straight to okey_hot / oval_hot -- their final place.  Keys
 // leave as u32 tokens (make_token: the key itself below 2^31, else its
 // index in this batch).
+//
+// A tile is R rounds of kPartTile pairs.  Each round's pairs are binned and
+// ranked as they arrive (the next round's loads already in flight) and kept
+// in registers as (token, rank|bin, fine); one scan and one LDS placement per
+// tile then write the tile out as per-bin runs.  The runs are what the
+// partition pays for: a bin's run is a few keys at 4096 pairs per tile (config
+// 3: ~1500 bins), and each one costs about one partial-line write, so R = 4
+// (16384-pair tiles) writes a quarter of the runs.
+template <int R, bool HV>
 __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row, const int64_t* key, const float* val,
                                                              int64_t n, int s2, int P1, int64_t nrows,
                                                              const uint32_t* O1, int NB, uint16_t* ofine,
                                                              uint32_t* okey, float* oval,
                                                              const unsigned long long* hotkey, uint32_t* okey_hot,
                                                              float* oval_hot) {
+  constexpr int TILE = R * kPartTile;  // pairs per tile
+  constexpr int NP = R * kPartPer;     // pairs per thread per tile
   extern __shared__ __align__(16) unsigned char smem[];
   const int P = P1 + (hotkey ? kHotBins : 0);
-  TileLds L = carve(smem, P, val != nullptr, true);
+  TileLds L = carve(smem, P, HV, true, TILE);
   uint32_t* tab = hotkey ? L.scr + 64 : nullptr;
   const int tid = threadIdx.x;
   if (tab) load_hot_table(hotkey, tab);
   for (int b = tid; b < P; b += kPartThreads) L.cursor[b] = O1[(int64_t)blockIdx.x * P + b];
   const uint32_t fmask = (1u << s2) - 1u;
   for (int b = tid; b < P; b += kPartThreads) L.hist[b] = 0;
-  // tiles blockIdx.x, + NB, + 2 NB, ... (k_p1_hist's assignment)
-  const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
-  // software pipeline: the next tile's loads are issued before this tile's
-  // write-out and stay in flight across the LDS-only barriers
-  int64_t rr[kPartPer], kk[kPartPer];
-  float vv[kPartPer];
-  auto load = [&](int64_t t) {
-    const int64_t tb = t * kPartTile, hi = min(n, tb + kPartTile);
+  // tiles blockIdx.x, + NB, + 2 NB, ... (k_p1_hist<R>'s assignment)
+  const int64_t ntiles = (n + TILE - 1) / TILE;
+  // two load buffers: round u + 1's loads are issued before round u is binned,
+  // and the next tile's first round before this tile's write-out
+  int64_t rr[2][kPartPer], kk[2][kPartPer];
+  float vv[2][kPartPer];
+  auto load = [&](int64_t t, int u, int buf) {
+    const int64_t tb = t * TILE + (int64_t)u * kPartTile;
 #pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
-      const int64_t e = tb + tid + (int64_t)u * kPartThreads;
-      rr[u] = -1;
-      if (e < hi) {
-        rr[u] = row[e];
-        kk[u] = key[e];
-        vv[u] = val ? val[e] : 0.f;
+    for (int q = 0; q < kPartPer; ++q) {
+      const int64_t e = tb + tid + (int64_t)q * kPartThreads;
+      rr[buf][q] = -1;
+      if (e < n) {
+        rr[buf][q] = row[e];
+        kk[buf][q] = key[e];
+        if (HV) vv[buf][q] = val[e];
       }
     }
   };
-  auto tok = [&](int64_t t, int u) {
-    return make_token(kk[u], t * kPartTile + tid + (int64_t)u * kPartThreads);
-  };
-  if ((int64_t)blockIdx.x < ntiles) load(blockIdx.x);
+  uint32_t tk[NP], rb[NP], ff[NP / 2];  // token; rank << 12 | bin (~0: none); two fine indices
+  float va[HV ? NP : 1];
+  if ((int64_t)blockIdx.x < ntiles) load(blockIdx.x, 0, 0);
   __syncthreads();
   for (int64_t t = blockIdx.x; t < ntiles; t += NB) {
-#if !CMS_P1_PREFETCH
-    if (t != (int64_t)blockIdx.x) load(t);
-#endif
-    uint32_t bb[kPartPer], bn[kPartPer], rk[kPartPer];
 #pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
-      const bool ok = rr[u] >= 0 && rr[u] < nrows;
-      bb[u] = ok ? (uint32_t)rr[u] : 0u;
-      bn[u] = ok ? bin_of(bb[u], s2, P1, tab) : 0u;
-      const uint32_t q = lds_bin_add<CMS_PEEL_P1S, true>(L.hist, bn[u], ok);
-      rk[u] = ok ? q : 0xFFFFFFFFu;
+    for (int u = 0; u < R; ++u) {
+      if (u + 1 < R) load(t, u + 1, (u + 1) & 1);
+      const int cb = u & 1;
+#pragma unroll
+      for (int q = 0; q < kPartPer; ++q) {
+        const int x = u * kPartPer + q;
+        const bool ok = rr[cb][q] >= 0 && rr[cb][q] < nrows;
+        const uint32_t r32 = ok ? (uint32_t)rr[cb][q] : 0u;
+        const uint32_t bin = ok ? bin_of(r32, s2, P1, tab) : 0u;
+        const uint32_t rank = lds_bin_add<CMS_PEEL_P1S, true>(L.hist, bin, ok);
+        rb[x] = ok ? (rank << 12 | bin) : 0xFFFFFFFFu;
+        tk[x] = make_token(kk[cb][q], t * TILE + (int64_t)u * kPartTile + tid + (int64_t)q * kPartThreads);
+        const uint32_t f = r32 & fmask;
+        ff[x >> 1] = (x & 1) ? (ff[x >> 1] | f << 16) : f;
+        if (HV) va[x] = vv[cb][q];
+      }
     }
     lds_barrier();
     const uint32_t cnt = scan_bins(L.hist, L.off, P, L.scr);
     lds_barrier();
 #pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
-      if (rk[u] != 0xFFFFFFFFu) {
-        const uint32_t bin = bn[u];
-        uint32_t p = L.off[bin] + rk[u];
-        L.key[p] = tok(t, u);
-        if (val) L.val[p] = vv[u];
-        L.fine[p] = (uint16_t)(bb[u] & fmask);
+    for (int x = 0; x < NP; ++x) {
+      if (rb[x] != 0xFFFFFFFFu) {
+        const uint32_t bin = rb[x] & 0xFFFu;
+        const uint32_t p = L.off[bin] + (rb[x] >> 12);
+        L.key[p] = tk[x];
+        if (HV) L.val[p] = va[x];
+        L.fine[p] = (uint16_t)(ff[x >> 1] >> ((x & 1) << 4));
         L.bin[p] = (uint16_t)bin;
       }
     }
-#if CMS_P1_PREFETCH
-    if (t + NB < ntiles) load(t + NB);
-#endif
+    if (t + NB < ntiles) load(t + NB, 0, 0);
     lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t bin = L.bin[i];
       uint32_t g = L.cursor[bin] + (i - L.off[bin]);
 #ifdef CMS_PART_LINEAR  // bound analysis only: contiguous instead of per-bin destinations
-      g = (uint32_t)(t * kPartTile + i);
+      g = (uint32_t)(t * TILE + i);
 #endif
 #ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
       if (g != 0xFFFFFFFFu) continue;
 #endif
       if ((int)bin >= P1) {  // hot owner: final place
-        pstore(okey_hot + g, L.key[i]);
-        if (oval) oval_hot[g] = L.val[i];
+        okey_hot[g] = L.key[i];
+        if (HV) oval_hot[g] = L.val[i];
         continue;
       }
-      pstore(okey + g, L.key[i]);
-      pstore(ofine + g, L.fine[i]);
-      if (oval) oval[g] = L.val[i];
+      okey[g] = L.key[i];
+      ofine[g] = L.fine[i];
+      if (HV) oval[g] = L.val[i];
     }
     lds_barrier();
     for (int b = tid; b < P; b += kPartThreads) {
@@ -406,6 +416,17 @@ __global__ __launch_bounds__(1024) void k_p2_plan(const uint32_t* bs1, int P1, i
   }
 }
 
+// Pass-2 block order: workgroup bx runs on XCD bx % 8, and each XCD takes a
+// contiguous range of the logical blocks, in order -- so the blocks of one
+// coarse bin (adjacent output regions: fine bin f of block k ends where that
+// of block k + 1 starts, a few keys long) run together on ONE XCD, and the
+// short runs they write into a coarse bin's ~2 MB of output meet in that
+// XCD's L2 instead of leaving as partial lines from eight L2s.
+__device__ __forceinline__ uint32_t p2_block(uint32_t bx, uint32_t nblk) {
+  const uint32_t xcd = bx & 7u, q8 = nblk >> 3, r8 = nblk & 7u;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bx >> 3);
+}
+
 __device__ __forceinline__ int find_bin(const uint32_t* blkStart, int P1, uint32_t x) {
   int lo = 0, hi = P1;  // last b with blkStart[b] <= x
   while (lo < hi) {
@@ -422,10 +443,11 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
   extern __shared__ uint32_t lh[];
   uint32_t nblk = blkStart[P1];
   if (blockIdx.x >= nblk) return;
-  int b = find_bin(blkStart, P1, blockIdx.x);
+  const uint32_t lb = p2_block(blockIdx.x, nblk);
+  int b = find_bin(blkStart, P1, lb);
   for (int f = threadIdx.x; f < P2; f += blockDim.x) lh[f] = 0;
   __syncthreads();
-  int64_t lo = binStart[b] + (int64_t)(blockIdx.x - blkStart[b]) * CH2;
+  int64_t lo = binStart[b] + (int64_t)(lb - blkStart[b]) * CH2;
   int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
   // 8 fine indices per 16-byte load; the unaligned head and tail one by one
   const int64_t a0 = min(hi, (lo + 7) & ~int64_t(7));
@@ -446,7 +468,7 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
     }
   }
   __syncthreads();
-  for (int f = threadIdx.x; f < P2; f += blockDim.x) H2[(int64_t)blockIdx.x * P2 + f] = lh[f];
+  for (int f = threadIdx.x; f < P2; f += blockDim.x) H2[(int64_t)lb * P2 + f] = lh[f];
 }
 
 // Offsets of (pass-2 block, fine bin) and the CSR row starts, in three
@@ -597,9 +619,10 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
   if (blockIdx.x >= nblk) return;
   TileLds L = carve(smem, P2, val1 != nullptr, false);
   const int tid = threadIdx.x;
-  const int b = find_bin(blkStart, P1, blockIdx.x);
-  for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] = O2[(int64_t)blockIdx.x * P2 + f];
-  const int64_t lo = binStart[b] + (int64_t)(blockIdx.x - blkStart[b]) * CH2;
+  const uint32_t lb = p2_block(blockIdx.x, nblk);
+  const int b = find_bin(blkStart, P1, lb);
+  for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] = O2[(int64_t)lb * P2 + f];
+  const int64_t lo = binStart[b] + (int64_t)(lb - blkStart[b]) * CH2;
   const int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
   for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
   uint32_t kk[kPartPer];
@@ -655,7 +678,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
 #ifdef CMS_PART_NOWRITE  // bound analysis only: no global stores
       if (g != 0xFFFFFFFFu) continue;
 #endif
-      pstore(okey + g, L.key[i]);
+      okey[g] = L.key[i];
       if (oval) oval[g] = L.val[i];
       if (orow) orow[g] = b * P2 + (int32_t)f;
     }
@@ -705,7 +728,11 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     return set_error(CMS_E_PARAM, "num_owners %lld too large for the partition", (long long)n);
   if (hot && (P1 + kHotBins > kMaxBins || out_rows || n >= (int64_t(1) << 31))) return kNoSpans;
   const int P = P1 + (hot ? kHotBins : 0);  // pass-1 bins
-  const int NB = (int)std::max<int64_t>(1, std::min<int64_t>(CMS_P1_BLOCKS, (npairs + kPartTile - 1) / kPartTile));
+  // pass-1 tile: the most rounds whose LDS image fits a workgroup
+  int R = CMS_P1_ROUNDS;
+  while (R > 1 && tile_lds_bytes(P, d_val != nullptr, true, hot, R * kPartTile) > 160 * 1024) R >>= 1;
+  const int64_t tile1 = (int64_t)R * kPartTile;
+  const int NB = (int)std::max<int64_t>(1, std::min<int64_t>(CMS_P1_BLOCKS, (npairs + tile1 - 1) / tile1));
   const int64_t CH2 = 4 * kPartTile;
   const int64_t nb2max = npairs / CH2 + P1 + 1;
 
@@ -742,8 +769,11 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
   int64_t* coff = h->ws_csr_off.as<int64_t>();
   unsigned long long* slotkey = hot ? h->ws_hotpart.as<unsigned long long>() : nullptr;
   static bool lds_attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_p1_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)k_p2_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const void* fs[] = {(const void*)k_p1_scatter<1, false>, (const void*)k_p1_scatter<1, true>,
+                        (const void*)k_p1_scatter<2, false>, (const void*)k_p1_scatter<2, true>,
+                        (const void*)k_p1_scatter<4, false>, (const void*)k_p1_scatter<4, true>,
+                        (const void*)k_p2_scatter};
+    for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)lds_attr;
@@ -763,7 +793,8 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
       hipLaunchKernelGGL(k_hot_claim, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
                          h->stream, cnt, n, tau, slotkey);
     }
-    hipLaunchKernelGGL(k_p1_hist, dim3(NB), dim3(256), sizeof(uint32_t) * (P + (hot ? kHotBins : 0)), h->stream, d_row,
+    auto hist = R == 4 ? k_p1_hist<4> : R == 2 ? k_p1_hist<2> : k_p1_hist<1>;
+    hipLaunchKernelGGL(hist, dim3(NB), dim3(256), sizeof(uint32_t) * (P + (hot ? kHotBins : 0)), h->stream, d_row,
                        npairs, s2, P1, n, H1, NB, h->d_flags, slotkey);
     // block-major (block, bin) offsets: chunked column sums, one scan over
     // the bins, chunk prefixes (the pass-2 kernels with one segment)
@@ -772,7 +803,9 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     hipLaunchKernelGGL(k_p2_colsum<kP1Split>, dim3(kP1Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1);
     hipLaunchKernelGGL(k_p1_scan, dim3(1), dim3(1024), 0, h->stream, P, PS1, bs1);
     hipLaunchKernelGGL(k_p2_offsets<kP1Split>, dim3(kP1Split), dim3(1024), 0, h->stream, H1, seg1, P, PS1, O1);
-    hipLaunchKernelGGL(k_p1_scatter, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P, d_val != nullptr, true, hot),
+    auto scat = d_val ? (R == 4 ? k_p1_scatter<4, true> : R == 2 ? k_p1_scatter<2, true> : k_p1_scatter<1, true>)
+                      : (R == 4 ? k_p1_scatter<4, false> : R == 2 ? k_p1_scatter<2, false> : k_p1_scatter<1, false>);
+    hipLaunchKernelGGL(scat, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P, d_val != nullptr, true, hot, (int)tile1),
                        h->stream, d_row, d_key, d_val, npairs, s2, P1, n, O1, NB, fine, key1, val1, slotkey,
                        ckey, cval);
     hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, bs1, P1, CH2, binStart, blkStart);

@@ -25,4 +25,17 @@ timeout -k 10 700 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 
   || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 echo "bench ok"
 python -c "import json; print(json.dumps(json.load(open('gpurun_out/bench.json'))['summary']))"
+# A/B arms of the ingest step against variant libraries under ab/ (built on
+# the CPU side with build_lib.py --define ... --out ab/<name>.so)
+for i in 1 2; do
+  for lib in main ab/*.so; do
+    [ -e "$lib" ] || [ "$lib" = main ] || continue
+    tag=$(basename "$lib" .so)
+    if [ "$lib" = main ]; then envs=(); else envs=(MAHOUT_CMS_LIB="$PWD/$lib"); fi
+    env "${envs[@]}" timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras \
+        --no-config1 --no-config2 --no-cosine-1m > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err \
+      || { echo "A/B arm $tag failed"; exit 1; }
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], d.get('breakdown_ms_per_step'))" gpurun_out/ab_${tag}_$i.json
+  done
+done
 exit $rc
