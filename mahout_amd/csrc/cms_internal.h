@@ -304,7 +304,7 @@ struct cms_handle {
   // PoGroup [po_ngroups] (LDS-sized groups of one (w, d) class, then the wide
   // owners one per group), po_cmem the owner rows in group order
   cms::DevBuf po_groups, po_cmem, po_redo;
-  int64_t po_ngroups = 0, po_nnarrow = 0;
+  int64_t po_ngroups = 0, po_nnarrow = 0, po_wide0 = 0;  // groups, narrow groups, first wide member in po_cmem
   int32_t po_gmax_lds = 0;                       // largest LDS image of a narrow group (bytes)
 
   // instrumentation

@@ -601,6 +601,7 @@ static int po_build_groups(cms_handle* h) {
   CMS_HIP(hipStreamSynchronize(h->stream));  // the host vectors die on return
   h->po_ngroups = (int64_t)groups.size();
   h->po_nnarrow = (int64_t)narrow.size();
+  h->po_wide0 = (int64_t)cmem_n.size();
   h->po_gmax_lds = gmax;
   return CMS_OK;
 }
@@ -745,7 +746,7 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     p.norm = a.norm;
     p.nsq = a.nsq;
     p.qrows = d_qrows;
-    p.crows = a.cmem + (n - nwide);  // the wide owners close po_cmem
+    p.crows = a.cmem + h->po_wide0;  // the wide owners close po_cmem
     p.nq = qc;
     p.m = nwide;
     const bool wide = h->po_max_w > kPoHist;
