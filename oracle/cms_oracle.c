@@ -171,6 +171,82 @@ void orc_similarities_row(const double* table, int64_t rows, int32_t depth, int3
   }
 }
 
+/* userSimilarity(q, p) (CosineCM.java:83-96) of Q query owners -- their
+ * dense sketches qsk [Q][d][w], e.g. from orc_sketch_build -- against EVERY
+ * owner p of a CSR (off[n + 1], keys, vals or NULL = 1.0), each p's sketch
+ * rows taken from its own keys instead of a dense table (1M x d x w doubles
+ * do not fit): in row i, B_j = sum of p's increments hashed to j, added in key
+ * order as update (DoubleCountMinSketch.java:72-80) adds them, and cosine's
+ * sums (:128-134) visit the buckets with B_j != 0 in ascending j.  The terms
+ * skipped are products with xb = 0.0, and a partial sum that starts at +0.0
+ * never becomes -0.0 (x + (-x) rounds to +0.0), so adding them back (x + 0.0
+ * or x + -0.0) changes nothing: the result is orc_cosine_cm's on the dense
+ * rows, bit for bit.  out[q * n + p]; OpenMP over the owners. */
+void orc_cosine_queries_csr(const double* qsk, int64_t Q, const int64_t* off, const int64_t* keys, const float* vals,
+                            int64_t n, int32_t depth, int32_t width, const int64_t* a, const int64_t* b,
+                            int weighted, int32_t threads, double* out) {
+  const int64_t dw = (int64_t)depth * width;
+  const int32_t words = (width + 63) / 64;
+  double* qa = (double*)malloc(sizeof(double) * (size_t)(Q * depth)); /* valueA of every query row */
+  for (int64_t q = 0; q < Q; q++)
+    for (int32_t i = 0; i < depth; i++) {
+      double v = 0.0;
+      const double* r = qsk + q * dw + (int64_t)i * width;
+      for (int32_t j = 0; j < width; j++) v += r[j] * r[j];
+      qa[q * depth + i] = v;
+    }
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+  {
+    double* cnt = (double*)malloc(sizeof(double) * (size_t)width);
+    uint64_t* bits = (uint64_t*)calloc((size_t)words, sizeof(uint64_t));
+    double* ab = (double*)malloc(sizeof(double) * (size_t)Q);
+    double* mins = (double*)malloc(sizeof(double) * (size_t)Q);
+#pragma omp for schedule(dynamic, 64)
+    for (int64_t p = 0; p < n; p++) {
+      for (int64_t q = 0; q < Q; q++) mins[q] = DBL_MAX;
+      for (int32_t i = 0; i < depth; i++) {
+        for (int64_t t = off[p]; t < off[p + 1]; t++) {
+          const double inc = vals ? (double)vals[t] : 1.0;
+          const int32_t j = orc_hash(a[i], b[i], width, keys[t]);
+          if (bits[j >> 6] >> (j & 63) & 1ULL) {
+            cnt[j] = cnt[j] + inc;
+          } else {
+            bits[j >> 6] |= 1ULL << (j & 63);
+            cnt[j] = 0.0 + inc;
+          }
+        }
+        double vb = 0.0;
+        for (int64_t q = 0; q < Q; q++) ab[q] = 0.0;
+        for (int32_t wd = 0; wd < words; wd++) {
+          uint64_t m = bits[wd];
+          bits[wd] = 0;
+          while (m) {
+            const int32_t j = wd * 64 + __builtin_ctzll(m);
+            m &= m - 1;
+            const double xb = cnt[j];
+            vb += xb * xb;
+            for (int64_t q = 0; q < Q; q++) ab[q] += qsk[q * dw + (int64_t)i * width + j] * xb;
+          }
+        }
+        for (int64_t q = 0; q < Q; q++) {
+          const double den = sqrt(qa[q * depth + i]) * sqrt(vb);
+          if (den != 0) mins[q] = java_min(mins[q], ab[q] / den);
+        }
+      }
+      for (int64_t q = 0; q < Q; q++) {
+        double r = mins[q] == DBL_MAX ? NAN : mins[q];
+        if (!isnan(r)) r = orc_normalize_weight_result(r, 1, 0, weighted);
+        out[q * n + p] = r;
+      }
+    }
+    free(cnt);
+    free(bits);
+    free(ab);
+    free(mins);
+  }
+  free(qa);
+}
+
 float orc_estimate_preference(const double* table, int32_t depth, int32_t width, const int64_t* a, const int64_t* b,
                               int64_t user_row, const int64_t* nb_rows, int64_t m, int64_t item_key, int weighted,
                               int use_capper, float cap_min, float cap_max) {

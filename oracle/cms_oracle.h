@@ -84,6 +84,9 @@ float orc_estimate_preference(const double* table, int32_t depth, int32_t width,
 /* TopItems.getTopUsers (T/impl/recommender/TopItems.java:91-136) + SimilarUser.compareTo
  * (T/impl/recommender/SimilarUser.java:62-78), over candidates in ascending ID order.
  * Returns the count written to out_ids (<= k).  scores[i] belongs to ids[i]. */
+void orc_cosine_queries_csr(const double* qsk, int64_t Q, const int64_t* off, const int64_t* keys, const float* vals,
+                            int64_t n, int32_t depth, int32_t width, const int64_t* a, const int64_t* b,
+                            int weighted, int32_t threads, double* out);
 int32_t orc_top_users(const int64_t* ids, const double* scores, int64_t n, int32_t k,
                       int64_t* out_ids, double* out_scores);
 

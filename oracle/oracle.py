@@ -58,6 +58,8 @@ def _load():
         "orc_allpairs_efficient_par": (c.c_int64, [_f64p, c.c_int64, c.c_int32, c.c_int32, c.c_int64, c.c_int64,
                                                    c.c_int32, c.POINTER(c.c_double)]),
         "orc_max_threads": (c.c_int32, []),
+        "orc_cosine_queries_csr": (None, [_f64p, c.c_int64, _i64p, _i64p, c.c_void_p, c.c_int64, c.c_int32, c.c_int32,
+                                          _i64p, _i64p, c.c_int, c.c_int32, _f64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -154,6 +156,21 @@ def estimate_preference(table, a, b, user_row, nb_rows, item_key, weighted=False
     return lib().orc_estimate_preference(np.ascontiguousarray(table), d, w, np.ascontiguousarray(a, np.int64),
                                          np.ascontiguousarray(b, np.int64), int(user_row), nb, nb.size,
                                          int(item_key), int(weighted), int(capper is not None), float(lo), float(hi))
+
+
+def cosine_queries_csr(qsk, off, keys, vals, depth, width, a, b, weighted=False, threads=16):
+    """userSimilarity of each query sketch (qsk [Q][d][w] fp64) with EVERY
+    owner of the CSR (off [n+1], keys, vals or None), the owners' sketch rows
+    taken from their keys (orc_cosine_queries_csr): [Q][n] fp64."""
+    qsk = np.ascontiguousarray(qsk, dtype=np.float64).reshape(-1, depth * width)
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    n = off.size - 1
+    vals = None if vals is None else np.ascontiguousarray(vals, dtype=np.float32)
+    out = np.empty((qsk.shape[0], n), np.float64)
+    lib().orc_cosine_queries_csr(qsk, qsk.shape[0], off, keys, _vp(vals), n, depth, width, a, b, int(weighted),
+                                 int(threads), out)
+    return out
 
 
 def top_users(ids, scores, k):

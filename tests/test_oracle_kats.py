@@ -199,3 +199,28 @@ def test_faithful_pairs_match_prebuilt(oracle):
     for p in range(len(pi)):
         exp = oracle.cosine_cm(t[pi[p]], t[pj[p]])
         assert (np.isnan(exp) and np.isnan(got[p])) or got[p] == exp
+
+
+@pytest.mark.parametrize("vals_kind", ["unit", "float"])
+def test_cosine_queries_csr_equals_dense(oracle, vals_kind):
+    """The full-size test's all-owners check (orc_cosine_queries_csr: sketch
+    rows from each owner's keys, nonzero buckets in ascending order) equals
+    the dense CosineCM restatement bit for bit -- colliding keys, empty owners,
+    and negative / non-dyadic float preferences included."""
+    rng = np.random.default_rng(11)
+    n, d, w = 300, 4, 96
+    counts = rng.integers(0, 40, n)
+    counts[[3, 17]] = 0
+    counts[5] = 700  # more keys than buckets
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    owner = np.repeat(np.arange(n), counts).astype(np.int64)
+    keys = rng.integers(-2**40, 2**40, off[-1]).astype(np.int64)
+    vals = None if vals_kind == "unit" else rng.uniform(-2.5, 5.0, off[-1]).astype(np.float32)
+    a, b = oracle.hash_params(7, d)
+    table = oracle.build_table(n, d, w, a, b, owner, keys, vals)
+    qrows = [0, 5, 17, 42]
+    got = oracle.cosine_queries_csr(table[qrows], off, keys, vals, d, w, a, b, threads=4)
+    for qi, q in enumerate(qrows):
+        want = np.array([oracle.cosine_cm(table[q], table[p]) for p in range(n)])
+        same = (got[qi] == want) | (np.isnan(got[qi]) & np.isnan(want))
+        assert same.all(), (q, np.flatnonzero(~same)[:5])
