@@ -56,8 +56,10 @@ constexpr int kMaxBins = 4096;
 #ifndef CMS_P1_ROUNDS
 #define CMS_P1_ROUNDS 4
 #endif
-#ifndef CMS_P2_PREFETCH
-#define CMS_P2_PREFETCH 1
+// pass-2 tile in rounds of kPartTile pairs (1, 2 or 4: a block's chunk is
+// four rounds)
+#ifndef CMS_P2_ROUNDS
+#define CMS_P2_ROUNDS 1
 #endif
 
 // LDS histogram increment aggregated across the wave.  Zipf streams put most
@@ -609,15 +611,20 @@ __global__ __launch_bounds__(1024) void k_p2_offsets(const uint32_t* H2, const u
   }
 }
 
+// Pass 2: block lb takes its coarse bin's pairs [lo, lo + CH2) in tiles of R
+// rounds of kPartTile pairs (k_p1_scatter's scheme: binned and ranked from
+// registers, one scan and one LDS placement per tile), fine bin = owner.
+template <int R, bool HV>
 __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fine, const uint32_t* key1,
                                                              const float* val1, const uint32_t* binStart,
                                                              const uint32_t* blkStart, int P1, int64_t CH2, int P2,
                                                              const uint32_t* O2, uint32_t* okey, float* oval,
                                                              int32_t* orow) {
+  constexpr int TILE = R * kPartTile, NP = R * kPartPer;
   extern __shared__ __align__(16) unsigned char smem[];
   uint32_t nblk = blkStart[P1];
   if (blockIdx.x >= nblk) return;
-  TileLds L = carve(smem, P2, val1 != nullptr, false);
+  TileLds L = carve(smem, P2, HV, false, TILE);
   const int tid = threadIdx.x;
   const uint32_t lb = p2_block(blockIdx.x, nblk);
   const int b = find_bin(blkStart, P1, lb);
@@ -625,49 +632,53 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
   const int64_t lo = binStart[b] + (int64_t)(lb - blkStart[b]) * CH2;
   const int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
   for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
-  uint32_t kk[kPartPer];
-  float vv[kPartPer];
-  uint32_t ff[kPartPer];
-  auto load = [&](int64_t tb) {
+  uint32_t kk[2][kPartPer], ff[2][kPartPer];
+  float vv[2][kPartPer];
+  auto load = [&](int64_t tb, int buf) {
 #pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
-      const int64_t e = tb + tid + (int64_t)u * kPartThreads;
-      ff[u] = 0xFFFFFFFFu;
+    for (int q = 0; q < kPartPer; ++q) {
+      const int64_t e = tb + tid + (int64_t)q * kPartThreads;
+      ff[buf][q] = 0xFFFFFFFFu;
       if (e < hi) {
-        ff[u] = fine[e];
-        kk[u] = key1[e];
-        vv[u] = val1 ? val1[e] : 0.f;
+        ff[buf][q] = fine[e];
+        kk[buf][q] = key1[e];
+        if (HV) vv[buf][q] = val1[e];
       }
     }
   };
-  if (lo < hi) load(lo);
+  uint32_t tk[NP], rf[NP];  // key token; rank << 12 | fine bin (~0: none)
+  float va[HV ? NP : 1];
+  if (lo < hi) load(lo, 0);
   __syncthreads();
-  for (int64_t tb = lo; tb < hi; tb += kPartTile) {
-#if !CMS_P2_PREFETCH
-    if (tb != lo) load(tb);
-#endif
-    uint32_t rk[kPartPer];
+  for (int64_t tb = lo; tb < hi; tb += TILE) {
 #pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
-      const bool ok = ff[u] != 0xFFFFFFFFu;
-      const uint32_t q = lds_bin_add<CMS_PEEL_P2S, true>(L.hist, ok ? ff[u] : 0u, ok);
-      rk[u] = ok ? q : 0xFFFFFFFFu;
+    for (int u = 0; u < R; ++u) {
+      if (u + 1 < R) load(tb + (int64_t)(u + 1) * kPartTile, (u + 1) & 1);
+      const int cb = u & 1;
+#pragma unroll
+      for (int q = 0; q < kPartPer; ++q) {
+        const int x = u * kPartPer + q;
+        const bool ok = ff[cb][q] != 0xFFFFFFFFu;
+        const uint32_t rank = lds_bin_add<CMS_PEEL_P2S, true>(L.hist, ok ? ff[cb][q] : 0u, ok);
+        rf[x] = ok ? (rank << 12 | ff[cb][q]) : 0xFFFFFFFFu;
+        tk[x] = kk[cb][q];
+        if (HV) va[x] = vv[cb][q];
+      }
     }
     lds_barrier();
     const uint32_t cnt = scan_bins(L.hist, L.off, P2, L.scr);
     lds_barrier();
 #pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
-      if (rk[u] != 0xFFFFFFFFu) {
-        uint32_t p = L.off[ff[u]] + rk[u];
-        L.key[p] = kk[u];
-        if (val1) L.val[p] = vv[u];
-        L.bin[p] = (uint16_t)ff[u];
+    for (int x = 0; x < NP; ++x) {
+      if (rf[x] != 0xFFFFFFFFu) {
+        const uint32_t f = rf[x] & 0xFFFu;
+        const uint32_t p = L.off[f] + (rf[x] >> 12);
+        L.key[p] = tk[x];
+        if (HV) L.val[p] = va[x];
+        L.bin[p] = (uint16_t)f;
       }
     }
-#if CMS_P2_PREFETCH
-    if (tb + kPartTile < hi) load(tb + kPartTile);
-#endif
+    if (tb + TILE < hi) load(tb + TILE, 0);
     lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t f = L.bin[i];
@@ -679,7 +690,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
       if (g != 0xFFFFFFFFu) continue;
 #endif
       okey[g] = L.key[i];
-      if (oval) oval[g] = L.val[i];
+      if (HV) oval[g] = L.val[i];
       if (orow) orow[g] = b * P2 + (int32_t)f;
     }
     lds_barrier();
@@ -772,7 +783,9 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     const void* fs[] = {(const void*)k_p1_scatter<1, false>, (const void*)k_p1_scatter<1, true>,
                         (const void*)k_p1_scatter<2, false>, (const void*)k_p1_scatter<2, true>,
                         (const void*)k_p1_scatter<4, false>, (const void*)k_p1_scatter<4, true>,
-                        (const void*)k_p2_scatter};
+                        (const void*)k_p2_scatter<1, false>, (const void*)k_p2_scatter<1, true>,
+                        (const void*)k_p2_scatter<2, false>, (const void*)k_p2_scatter<2, true>,
+                        (const void*)k_p2_scatter<4, false>, (const void*)k_p2_scatter<4, true>};
     for (const void* f : fs) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
@@ -814,8 +827,13 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     hipLaunchKernelGGL(k_p2_colsum<kP2Split>, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS);
     hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, binStart, P1, P2, n, PS, coff);
     hipLaunchKernelGGL(k_p2_offsets<kP2Split>, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS, O2);
-    hipLaunchKernelGGL(k_p2_scatter, dim3((unsigned)nb2max), dim3(kPartThreads), tile_lds_bytes(P2, d_val != nullptr, false), h->stream, fine,
-                       key1, val1, binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
+    int R2 = CMS_P2_ROUNDS;
+    while (R2 > 1 && tile_lds_bytes(P2, d_val != nullptr, false, false, R2 * kPartTile) > 160 * 1024) R2 >>= 1;
+    auto scat2 = d_val ? (R2 == 4 ? k_p2_scatter<4, true> : R2 == 2 ? k_p2_scatter<2, true> : k_p2_scatter<1, true>)
+                       : (R2 == 4 ? k_p2_scatter<4, false> : R2 == 2 ? k_p2_scatter<2, false> : k_p2_scatter<1, false>);
+    hipLaunchKernelGGL(scat2, dim3((unsigned)nb2max), dim3(kPartThreads),
+                       tile_lds_bytes(P2, d_val != nullptr, false, false, R2 * kPartTile), h->stream, fine, key1, val1,
+                       binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     if (hot) {
       int64_t* chi = h->ws_csr_hi.as<int64_t>();
       hipLaunchKernelGGL(k_spans_hi, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
