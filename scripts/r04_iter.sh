@@ -27,7 +27,7 @@ echo "bench ok"
 python -c "import json; print(json.dumps(json.load(open('gpurun_out/bench.json'))['summary']))"
 # A/B arms of the ingest step against variant libraries under ab/ (built on
 # the CPU side with build_lib.py --define ... --out ab/<name>.so)
-for i in 1 2; do
+for i in 1; do
   for lib in main ab/*.so; do
     [ -e "$lib" ] || [ "$lib" = main ] || continue
     tag=$(basename "$lib" .so)
