@@ -505,17 +505,18 @@ def config3_shard(n_items, n_users, total_pairs, rank, world, device, seed=20261
     return torch.cat(out_i), torch.cat(out_u)
 
 
-BUILD_KERNELS = ["void cms::k_build_rows<2>", "void cms::k_build_nibbles<2>", "void cms::k_build_mid<2>",
-                 "void cms::k_build_bytes<2>"]
+BUILD_KERNELS = ["cms::k_build_slices", "void cms::k_build_rows<2>", "void cms::k_build_nibbles<2>",
+                 "void cms::k_build_mid<2>", "void cms::k_build_bytes<2>"]
 
 
 def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
-    """Roofline of the row build (the "build_rows" scope: k_build_rows for the
-    slot rows and slices, k_build_mid, k_build_nibbles, k_build_bytes -- the
-    ingest's dominant phase).
+    """Roofline of the row build (the "build_rows" scope: k_build_slices for
+    the split owners, k_build_rows for other slot rows, k_build_mid,
+    k_build_nibbles, k_build_bytes -- the ingest's dominant phase).
 
     Algorithmic bytes per launch = what the row build must move for the table
-    as it is stored: the grouped keys read once (8 B per pair), the owner spans
+    as it is stored: the grouped key tokens read once (4 B per pair: the COO
+    partition hands the build u32 tokens, cms_device.h Keys), the owner spans
     (2 x 8 B per owner) and every counter written once at its stored width
     (4-bit / u8 / u16 narrow rows, u32 hot rows: cms_stats.stored_bytes).  SURVEY 8(d)
     prices every counter at 4 B; that figure is reported beside it as
@@ -526,8 +527,8 @@ def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
     st = table.stats()
     n, d, w = table.num_owners, table.depth, table.width
     stored = int(st["stored_bytes"])
-    alg = local_pairs * 8 + n * 16 + stored
-    u32_alg = local_pairs * 8 + (n + 1) * 8 + n * d * w * 4
+    alg = local_pairs * 4 + n * 16 + stored
+    u32_alg = local_pairs * 4 + (n + 1) * 8 + n * d * w * 4
     avg_s = build_ms / build_n * 1e-3 if build_n else None
     # the scope's kernels each run once per build: their measured bytes add up
     kernels = pmc_kernel if isinstance(pmc_kernel, (list, tuple)) else [pmc_kernel]
@@ -541,10 +542,11 @@ def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
            "traffic": traffic, "traffic_source": src,
            "frac_traffic": traffic / avg_s / 1e9 / HBM_PEAK_GBPS if traffic and avg_s else None,
            "algorithmic_bytes_per_launch": alg,
-           "algorithmic_bytes_basis": "keys 8 B/pair + spans 16 B/owner + counters at stored width "
-                                      f"({int(st['bit_rows'])} 1-bit rows, {int(st['crumb_rows'])} 2-bit rows, "
+           "algorithmic_bytes_basis": "key tokens 4 B/pair + spans 16 B/owner + counters at stored width "
+                                      f"({int(st['list_rows'])} list rows, {int(st['bit_rows'])} 1-bit rows, "
+                                      f"{int(st['crumb_rows'])} 2-bit rows, "
                                       f"{int(st['nibble_rows'])} 4-bit rows, {int(st['u8_rows'])} u8 rows, "
-                                      f"{n - int(st['hot_rows']) - int(st['bit_rows']) - int(st['crumb_rows']) - int(st['nibble_rows']) - int(st['u8_rows'])} u16 rows, "
+                                      f"{n - int(st['hot_rows']) - int(st['list_rows']) - int(st['bit_rows']) - int(st['crumb_rows']) - int(st['nibble_rows']) - int(st['u8_rows'])} u16 rows, "
                                       f"{int(st['hot_rows'])} u32 rows)",
            "avg_launch_ms": avg_s * 1e3 if avg_s else None,
            "u32_priced_bytes_per_launch": u32_alg,

@@ -115,6 +115,7 @@ int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, i
  *   CMS_NO_FORMS=1        narrow rows stay u16 (no 1/2/4/8-bit row forms)
  *   CMS_BIT_KEYS=<n>      byte-class owners of <= n keys try 1-bit rows first (64)
  *   CMS_CRUMB_KEYS=<n>    ... of <= n keys 2-bit rows (256)
+ *   CMS_LIST_KEYS=<n>     ... of <= n keys, unit increments: sparse list rows (256; 0 = none)
  *   CMS_NO_HOT_ROUTING=1  the COO partition sends every owner through both passes
  *   CMS_NO_FP4=1          no e2m1 operand image: every single-limb pair on int8 MFMA
  *   CMS_NO_MLS=1          multi-limb slabs on the 128-row tile kernel instead of k_cosine_mls */
@@ -415,6 +416,7 @@ typedef struct cms_stats {
   int64_t collective_calls;  /* all-reduce / all-gather calls made through the communicator so far */
   int32_t comm_kind;         /* 0 none (single-GPU path), 1 RCCL (cms_comm_init), 2 caller transport */
   int32_t device;            /* HIP device ordinal of the handle */
+  int64_t list_rows;         /* narrow owners stored as sparse key-bucket lists (2 + 2 d m bytes, m keys) */
 } cms_stats;
 int cms_get_stats(cms_handle* h, cms_stats* out);
 

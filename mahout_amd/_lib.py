@@ -86,6 +86,7 @@ class CmsStats(ctypes.Structure):
         ("collective_calls", ctypes.c_int64),
         ("comm_kind", ctypes.c_int32),
         ("device", ctypes.c_int32),
+        ("list_rows", ctypes.c_int64),
     ]
 
 

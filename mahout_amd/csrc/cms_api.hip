@@ -311,6 +311,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     auto num = [](const char* name, int dflt) { const char* e = getenv(name); return e && *e ? atoi(e) : dflt; };
     h->tune.bit_keys = num("CMS_BIT_KEYS", h->tune.bit_keys);
     h->tune.crumb_keys = num("CMS_CRUMB_KEYS", h->tune.crumb_keys);
+    h->tune.list_keys = std::max(0, std::min(256, num("CMS_LIST_KEYS", h->tune.list_keys)));
     h->tune.forms = !flag("CMS_NO_FORMS");
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");
@@ -1489,7 +1490,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
-  int64_t forms[6] = {0, 0, 0, 0, 0, 0};  // hot, u16, u8, 4-bit, 2-bit, 1-bit rows
+  int64_t forms[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // hot, u16, u8, 4-bit, 2-bit, 1-bit, list rows, list bytes
   if (!h->per_owner && !h->f64 && h->d_hidx) {
     int rc = count_forms(h, forms);
     if (rc) return rc;
@@ -1507,7 +1508,8 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->stored_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                      : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
                                    : 4 * forms[0] * h->dw + 2 * forms[1] * h->dw + forms[2] * h->dw +
-                                    forms[3] * (h->dw / 2) + forms[4] * (h->dw / 4) + forms[5] * (h->dw / 8);
+                                    forms[3] * (h->dw / 2) + forms[4] * (h->dw / 4) + forms[5] * (h->dw / 8) +
+                                    forms[7];
   out->u8_rows = forms[2];
   out->nibble_rows = forms[3];
   out->crumb_rows = forms[4];
@@ -1515,6 +1517,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->collective_calls = h->coll_calls;
   out->comm_kind = h->comm ? 1 : h->ext_comm ? 2 : 0;
   out->device = h->device;
+  out->list_rows = forms[6];
   return CMS_OK;
 }
 

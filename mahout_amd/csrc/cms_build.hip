@@ -788,7 +788,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, int64_t nrows, HashParams hp,
     const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
     uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt, int bit_keys,
-    int crumb_keys) {
+    int crumb_keys, int list_keys) {
   extern __shared__ __align__(16) uint32_t lds[];  // [kNibWaves][w / 8] words: one sketch row of nibbles per wave
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -823,7 +823,12 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
   // (the wider rows overwrite every byte the narrower ones wrote), and past 15
   // the owner goes to k_build_bytes (u8)
   const int64_t m = hi - lo;
-  int bits = (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
+  // list rows (cms_internal.h kFormList): unit increments, at most list_keys
+  // keys; counted as 4-bit in LDS for the norms and the maximum only, the
+  // entries leave as the owner's buckets
+  const bool as_list = m <= list_keys && vals == nullptr && hp.frac_bits == 0;
+  int bits = as_list ? 4 : (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
+  uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;  // list row: [0] = m, then [d][m] buckets
   uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * (w >> 5);  // w/2 bytes per wave (the 4-bit row)
   uint32_t* slot = lds + wv * (w >> 3);
   uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's u16 slot (64-B aligned)
@@ -848,18 +853,21 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
           ovf |= nv > cap || ik[k] > cap;  // the add carried into the next counter: a wider form
           sq += (2u * old + ik[k]) * ik[k];
           vmax = max(vmax, nv);
+          if (as_list) lst[1 + (int64_t)d * m + lane + 64 * k] = (uint16_t)c;
         }
       if (__ballot(ovf)) break;  // uniform: escalate
       sq = wave_sum_u32(sq);  // <= mass * 15
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
       if (false)
 #endif
-      for (int j = lane; j < nq; j += 64) store_row(d4 + d * nq + j, slot4[j], SV);
+      if (!as_list)
+        for (int j = lane; j < nq; j += 64) store_row(d4 + d * nq + j, slot4[j], SV);
       if (lane == 0) norm[row * hp.depth + d] = sq;
     }
     if (!__ballot(ovf) || bits == 4) break;
     bits *= 2;
   }
+  if (as_list && lane == 0) lst[0] = (uint16_t)m;
   if (badv) atomicOr(flags, kFlagBadValue);
   if (__ballot(ovf)) {
     if (lane == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
@@ -871,7 +879,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
   if (lane == 0) {
     rowmax[row] = vmax;
     row_mass[row] = mass;
-    hidx_w[row] = bits == 1 ? kFormU1 : bits == 2 ? kFormU2 : kFormU4;
+    hidx_w[row] = as_list ? kFormList : bits == 1 ? kFormU1 : bits == 2 ? kFormU2 : kFormU4;
     cbound[row] = vmax;
   }
 }
@@ -979,9 +987,15 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
                                                                 const int2* smap, const uint32_t* counters,
                                                                 TableView tv, uint64_t* row_mass, uint32_t* flags) {
   extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] words, two u16 counters each
-  if (blockIdx.x >= counters[1]) return;
+  const uint32_t nsl = counters[1];
+  if (blockIdx.x >= nsl) return;
   const int tid = threadIdx.x;
-  const int2 m = smap[blockIdx.x];
+  // a Zipf head owner has hundreds of slices, adjacent in smap: workgroups
+  // take the slices in a strided order (a prime stride is a bijection unless
+  // it divides the count) so the ones running together belong to many owners
+  // and their row adds do not all land on one 160 KB slot row at once
+  const uint32_t stride = (nsl % 7919u) ? 7919u : 7907u;
+  const int2 m = smap[(uint32_t)(((uint64_t)blockIdx.x * stride) % nsl)];
   const int64_t row = hot[m.x].row;
   const int64_t lo = lo_[row] + (int64_t)m.y * slice;
   const int64_t end = min(hi_[row], lo + slice);
@@ -1011,7 +1025,12 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
   }
   __syncthreads();
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(tv.hot + (int64_t)tv.hidx[row] * dw);
-  for (int j = tid; j < words; j += kSliceThreads) {
+  // the slices of one owner start their sweep at different 512-B-aligned
+  // offsets of the slot row (same-address atomics from many workgroups queue)
+  const int units = (words + 63) >> 6;
+  const int rot = (int)(((uint32_t)m.y * 2654435761u >> 8) % (uint32_t)units) << 6;
+  for (int jj = tid; jj < words; jj += kSliceThreads) {
+    const int j = jj + rot < words ? jj + rot : jj + rot - words;
     const uint32_t v = lds[j];
     if (v) atomicAdd(dst + j, (unsigned long long)(v & 0xFFFFu) | ((unsigned long long)(v >> 16) << 32));
   }
@@ -1202,7 +1221,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          dim3(64 * kNibWaves), (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, keys,
                          d_val, n, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
-                         h->tune.crumb_keys);
+                         h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0);
       hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
                          dim3(kBuildThreads), std::max<size_t>((size_t)h->p.width * 2, (size_t)h->dw / 2), side, d_lo,
                          d_hi, keys, d_val, h->hp, (const int32_t*)mid_list, (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound,

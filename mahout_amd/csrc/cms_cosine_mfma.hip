@@ -106,12 +106,43 @@ __global__ void k_touch_class(const uint8_t* touch, const uint32_t* multi_flag, 
 
 // Limb images in permuted order: limb0[p] = c & 127 for every owner;
 // hl[p][k-1] = (c >> 7k) & 127 for the multi-limb prefix p < n_multi.
+// A list row (kFormList) is expanded one sketch row at a time: its entries
+// are counted into w u8 counters (a list row's counters are < 2^8, four per
+// LDS word, no carry), which then leave like any other row's.  Returns after
+// fn(r, lc) ran for every sketch row r with the row's counters in lc.
+template <class F>
+__device__ __forceinline__ void expand_list_rows(const TableView& tv, int64_t row, int64_t dw, uint32_t* lc, F fn) {
+  const uint32_t m = tv.list_m(row);
+  const int w = tv.w, wq = w >> 2;
+  for (int64_t r = 0; r * w < dw; ++r) {
+    for (int j = threadIdx.x; j < wq; j += blockDim.x) lc[j] = 0u;
+    __syncthreads();
+    const uint16_t* e = tv.list_row(row, r, m);
+    for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) atomicAdd(&lc[e[t] >> 2], 1u << ((e[t] & 3u) * 8u));
+    __syncthreads();
+    fn(r, lc);
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_limb_write(TableView tv, int64_t dw, const int64_t* perm,
                                                     const uint8_t* rowLp, int64_t n_multi, int8_t* limb0, int8_t* hl) {
+  extern __shared__ uint32_t lc[];  // [w / 4]: a list row's sketch row as u8 counters
   const int64_t p = blockIdx.x;
   const int64_t row = perm[p];
   int8_t* dst = limb0 + p * dw;
   const int L = p < n_multi ? rowLp[p] : 1;
+  if (tv.hidx[row] == kFormList) {  // counters < 2^8: limb 0 = c & 127, limb 1 = c >> 7
+    expand_list_rows(tv, row, dw, lc, [&](int64_t r, const uint32_t* c4) {
+      for (int j = threadIdx.x; j < (tv.w >> 2); j += blockDim.x) {
+        const uint32_t v = c4[j];
+        const int64_t o = r * tv.w + 4 * j;
+        *reinterpret_cast<uint32_t*>(dst + o) = v & 0x7F7F7F7Fu;
+        if (L > 1) *reinterpret_cast<uint32_t*>(hl + p * (kMaxLimbs - 1) * dw + o) = (v >> 7) & 0x01010101u;
+      }
+    });
+    return;
+  }
   for (int64_t j = threadIdx.x * 4; j < dw; j += 256 * 4) {
     const uint4 v = tv.get4(row, j);
     *reinterpret_cast<char4*>(dst + j) = make_char4((signed char)(v.x & 127u), (signed char)(v.y & 127u),
@@ -130,11 +161,24 @@ __global__ __launch_bounds__(256) void k_limb_write(TableView tv, int64_t dw, co
 //
 __global__ __launch_bounds__(256) void k_f4_write(TableView tv, int64_t dw, const int64_t* perm, int64_t f0,
                                                   uint8_t* f4, int sw) {
+  extern __shared__ uint32_t lc[];  // [w / 4]: a list row's sketch row as u8 counters
   const int64_t p = f0 + blockIdx.x;
   const int64_t row = perm[p];
   const int64_t rs = dw / 2;
   // e2m1: 0 -> 0x0, 1 -> 0x2 (1.0), 2 -> 0x4 (2.0), 3 -> 0x5 (3.0), 4 -> 0x6 (4.0)
   constexpr uint32_t kCode = 0x65420u;  // nibble c = code of value c
+  if (tv.hidx[row] == kFormList) {
+    expand_list_rows(tv, row, dw, lc, [&](int64_t r, const uint32_t* c4) {
+      for (int j = threadIdx.x; j < (tv.w >> 3); j += blockDim.x) {
+        const uint32_t lo = c4[2 * j], hi = c4[2 * j + 1];
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) packed |= ((kCode >> (4 * (((q < 4 ? lo : hi) >> (8 * (q & 3))) & 255u))) & 15u) << (4 * q);
+        *reinterpret_cast<uint32_t*>(f4 + blk_off(blockIdx.x, (r * tv.w + 8 * j) / 2, rs, sw)) = packed;
+      }
+    });
+    return;
+  }
   for (int64_t j = threadIdx.x * 8; j < dw; j += 256 * 8) {
     const uint4 v0 = tv.get4(row, j);
     const uint4 v1 = tv.get4(row, j + 4);
@@ -1028,7 +1072,7 @@ int cosine_prepare(cms_handle* h) {
     unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, fpos, fflag, rowL,
                        n, n_deep, n_multi, n_s8, touch, tpos8, tpos4, nt8, nt4, perm, inv, rowLp);
-    hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), 0, h->stream, h->tview(), dw, perm, rowLp, n_multi,
+    hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), (size_t)h->p.width, h->stream, h->tview(), dw, perm, rowLp, n_multi,
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
                        tileL);
@@ -1041,7 +1085,7 @@ int cosine_prepare(cms_handle* h) {
       CMS_HIP(h->ws_f4.ensure((size_t)blocks * kImgBlk * (size_t)(dw / 2)));
       CMS_HIP(hipMemsetAsync(h->ws_f4.as<uint8_t>() + (size_t)(blocks - 1) * kImgBlk * (dw / 2), 0,
                              (size_t)kImgBlk * (dw / 2), h->stream));
-      hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), 0, h->stream, h->tview(), dw, perm, f0,
+      hipLaunchKernelGGL(k_f4_write, dim3((unsigned)(n - f0)), dim3(256), (size_t)h->p.width, h->stream, h->tview(), dw, perm, f0,
                          h->ws_f4.as<uint8_t>(), h->sym_sw);
     }
     CMS_HIP(hipGetLastError());

@@ -186,6 +186,7 @@ __device__ __forceinline__ uint32_t table_add(const TableView& tv, int64_t r, in
     const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(tv.t16) + (g >> 1), inc << sh);
     return (old >> sh) & 0xffffu;
   }
+  if (s == kFormList) return tv.get(r, c);  // only inc == 0 reaches a list row (any mass widens it first)
   uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * tv.dw);  // slot start: 64-B aligned with forms
   if (s == kFormU8) {
     const uint32_t sh = (uint32_t)(c & 3) << 3;
@@ -328,10 +329,20 @@ __global__ __launch_bounds__(256) void k_norms(TableView tv, int64_t nrows, Hash
   const int w = (int)hp.width;
   for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
     uint32_t vmax = 0;
+    const bool list = tv.hidx[row] == kFormList;
+    const uint32_t lm = list ? tv.list_m(row) : 0u;
     for (int d = 0; d < hp.depth; ++d) {
       const int64_t c0 = (int64_t)d * w;
       uint64_t sq = 0;
-      if ((w & 3) == 0) {
+      if (list) {  // sum_j c_j^2 = sum over entries t of the count of t's bucket
+        const uint16_t* e = tv.list_row(row, d, lm);
+        for (uint32_t t = threadIdx.x; t < lm; t += blockDim.x) {
+          uint32_t c = 0;
+          for (uint32_t u = 0; u < lm; ++u) c += e[u] == e[t];
+          sq += c;
+          vmax = max(vmax, c);
+        }
+      } else if ((w & 3) == 0) {
         for (int j = threadIdx.x; j < (w >> 2); j += blockDim.x) {
           const uint4 v = tv.get4(row, c0 + 4 * j);
           vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));

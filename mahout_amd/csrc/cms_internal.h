@@ -81,10 +81,20 @@ struct PendingEvent {
 // widens a form row to u16 in place (widen_rows) before its bound could pass
 // the form's capacity.  Forms exist only when dw % 32 == 0 (every slot and
 // every nibble row then starts 64-byte aligned).
+//
+// LIST rows (kFormList): the smallest owners of a fresh build with unit
+// increments are stored sparse -- slot[0] = m, the owner's key count, then
+// for each sketch row r the m buckets its keys hash to, slot[1 + r m + t]
+// (u16, unsorted, repeats allowed): counter (r, j) is the number of entries
+// of row r equal to j.  2 + 2 d m bytes instead of a dense row (config 3: an
+// owner of 100 keys takes 1 KB instead of the 10 KB of its 2-bit rows).  A
+// list row takes no in-place adds (capacity 0: any write widens it to u16
+// first); whole-row readers expand it per sketch row (list_* helpers).
 constexpr uint64_t kNarrowLimit = 1ULL << 16;
-constexpr int32_t kFormU16 = -1, kFormU8 = -2, kFormU4 = -3, kFormU2 = -4, kFormU1 = -5;
+constexpr int32_t kFormU16 = -1, kFormU8 = -2, kFormU4 = -3, kFormU2 = -4, kFormU1 = -5, kFormList = -6;
 constexpr uint32_t form_cap(int32_t form) {
-  return form == kFormU1 ? 1u : form == kFormU2 ? 3u : form == kFormU4 ? 15u : form == kFormU8 ? 255u : 65535u;
+  return form == kFormList ? 0u : form == kFormU1 ? 1u : form == kFormU2 ? 3u : form == kFormU4 ? 15u
+       : form == kFormU8 ? 255u : 65535u;
 }
 
 struct TableView {
@@ -92,10 +102,25 @@ struct TableView {
   uint32_t* hot;        // [hot_cap][dw] u32 rows
   const int32_t* hidx;  // [n] slot of a hot row, or the narrow form (kForm*)
   int64_t dw;
+  int32_t w;            // sketch row width (list rows)
+  // list row: key count and the entries of sketch row r
+  __device__ __forceinline__ uint32_t list_m(int64_t row) const { return t16[row * dw]; }
+  __device__ __forceinline__ const uint16_t* list_row(int64_t row, int64_t r, uint32_t m) const {
+    return t16 + row * dw + 1 + r * (int64_t)m;
+  }
   __device__ __forceinline__ uint32_t get(int64_t row, int64_t j) const {
     const int32_t s = hidx[row];
     if (s >= 0) return hot[(int64_t)s * dw + j];
     if (s == kFormU16) return (uint32_t)t16[row * dw + j];
+    if (s == kFormList) {  // O(m): point queries; whole-row readers expand instead
+      const uint32_t m = list_m(row);
+      const int64_t r = j / w;
+      const uint32_t b = (uint32_t)(j - r * w);
+      const uint16_t* e = list_row(row, r, m);
+      uint32_t c = 0;
+      for (uint32_t t = 0; t < m; ++t) c += e[t] == b;
+      return c;
+    }
     const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
     if (s == kFormU8) return p[j];
     if (s == kFormU2) return (uint32_t)(p[j >> 2] >> ((j & 3) << 1)) & 3u;
@@ -109,6 +134,21 @@ struct TableView {
     if (s == kFormU16) {
       const ushort4 v = *reinterpret_cast<const ushort4*>(t16 + row * dw + j);
       return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    if (s == kFormList) {  // O(m), w % 4 == 0: the four counters share a sketch row
+      const uint32_t m = list_m(row);
+      const int64_t r = j / w;
+      const uint32_t b = (uint32_t)(j - r * w);
+      const uint16_t* e = list_row(row, r, m);
+      uint4 c = make_uint4(0, 0, 0, 0);
+      for (uint32_t t = 0; t < m; ++t) {
+        const uint32_t q = (uint32_t)e[t] - b;
+        c.x += q == 0u;
+        c.y += q == 1u;
+        c.z += q == 2u;
+        c.w += q == 3u;
+      }
+      return c;
     }
     const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
     if (s == kFormU8) {
@@ -156,6 +196,7 @@ namespace cms {
 struct Tunables {
   int bit_keys = 64;       // CMS_BIT_KEYS: byte-class owners of <= this many keys try 1-bit rows first
   int crumb_keys = 256;    // CMS_CRUMB_KEYS: ... of <= this many keys 2-bit rows
+  int list_keys = 256;     // CMS_LIST_KEYS: ... of <= this many keys (unit increments) list rows; 0: none
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
   bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)
@@ -198,7 +239,7 @@ struct cms_handle {
   cms::DevBuf ws_blist;                      // row build: slot-row and mid-class row lists + counts
   int64_t hot_cap = 0, hot_used = 0;
   cms::TableView tview() const {
-    return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw};
+    return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw, p.width};
   }
   uint64_t* d_row_mass = nullptr;   // [n] total increment mass per row
   uint64_t* d_norm = nullptr;       // [n][d] exact sum of squares (saturating)
@@ -361,7 +402,7 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 // rows holding a u32 slot (synchronises the stream)
 int count_hot_rows(cms_handle* h, int64_t* out);
 // rows per storage form: [0] hot, [1] u16, [2] u8, [3] nibble (synchronises)
-int count_forms(cms_handle* h, int64_t out[6]);  // hot, u16, u8, 4-bit, 2-bit, 1-bit rows
+int count_forms(cms_handle* h, int64_t out[8]);  // hot, u16, u8, 4-bit, 2-bit, 1-bit, list rows, list bytes
 // Form rows that a coming write could push past their capacity become u16 in
 // place: with d_bound (a u64 upper bound of each row's mass after the write)
 // and old_mass, a touched form row (bound > old mass) is widened when
@@ -396,6 +437,11 @@ int validate_batch(cms_handle* h, const int64_t* d_rows, const float* d_val, int
 int check_offsets_device(cms_handle* h, const int64_t* d_off);
 int hash_keys_device(cms_handle* h, const int64_t* d_keys, int64_t n, int32_t* d_out);
 int scan_exclusive_u32(cms_handle* h, const uint32_t* in, uint32_t* out, int64_t L, uint32_t* bsum);
+// List rows (kFormList) may be stored: forms, the tunable, and a d x w u16
+// image that fits the merge's LDS (k_merge_pack expands them there).
+inline bool lists_allowed(const cms_handle* h) {
+  return h->forms_ok && h->tune.list_keys > 0 && h->p.width % 8 == 0 && (size_t)h->dw * 2 <= 80 * 1024;
+}
 // ---- cms_partition.hip ----
 // COO -> CSR grouped by row; outputs live in handle scratch.
 // Keys come out as u32 tokens (cms_device.h make_token / Keys) that escape

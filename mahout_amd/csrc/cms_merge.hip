@@ -65,10 +65,22 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
     const int32_t slot = tv.hidx[o];
     const uint32_t* s32 = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
     const uint16_t* s16 = tv.t16 + o * dw;
-    if (use_img && slot == kFormU16) {
-      const uint4* g4 = reinterpret_cast<const uint4*>(s16);
+    if (use_img && (slot == kFormU16 || slot == kFormList)) {
       uint4* l4 = reinterpret_cast<uint4*>(img);
-      for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) l4[j] = g4[j];
+      if (slot == kFormList) {  // zeros, then each entry adds 1 into its half of an LDS word (counts < 2^8)
+        for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) l4[j] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        const uint32_t m = tv.list_m(o);
+        const int64_t ne = (dw / tv.w) * (int64_t)m;
+        uint32_t* i32 = reinterpret_cast<uint32_t*>(img);
+        for (int64_t t = threadIdx.x; t < ne; t += 256) {
+          const uint32_t idx = (uint32_t)((t / m) * tv.w + s16[1 + t]);
+          atomicAdd(i32 + (idx >> 1), 1u << ((idx & 1u) << 4));
+        }
+      } else {
+        const uint4* g4 = reinterpret_cast<const uint4*>(s16);
+        for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) l4[j] = g4[j];
+      }
       __syncthreads();
       for (int64_t i = threadIdx.x; i < nw; i += 256) {
         uint64_t wv = 0;

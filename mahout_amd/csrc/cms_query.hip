@@ -63,7 +63,13 @@ __global__ __launch_bounds__(256) void k_pair_cosine(TableView tv, const uint64_
     double valueAB, den;
     if (exact) {
       uint64_t dot = 0;
-      if ((w & 3) == 0) {
+      const bool la = tv.hidx[q_row] == kFormList, lb = tv.hidx[r2] == kFormList;
+      if (la || lb) {  // valueAB = sum over a list row's entries of the other row's counter (update is linear)
+        const int64_t lr = lb ? r2 : q_row, other = lb ? q_row : r2;
+        const uint32_t lm = tv.list_m(lr);
+        const uint16_t* e = tv.list_row(lr, d, lm);
+        for (uint32_t t = threadIdx.x; t < lm; t += 256) dot += tv.get(other, c0 + e[t]);
+      } else if ((w & 3) == 0) {
         for (int j = threadIdx.x; j < (w >> 2); j += 256) {
           const uint4 x = tv.get4(q_row, c0 + 4 * j), y = tv.get4(r2, c0 + 4 * j);
           dot += (uint64_t)x.x * y.x + (uint64_t)x.y * y.y + (uint64_t)x.z * y.z + (uint64_t)x.w * y.w;

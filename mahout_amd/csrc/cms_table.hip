@@ -151,6 +151,34 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
     const int32_t f = hidx[r];
     uint8_t* p8 = reinterpret_cast<uint8_t*>(tv.t16 + r * dw);
     uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + r * dw);
+    if (f == kFormList) {
+      // the entries (at most 32 per lane: d <= 32, m <= 256) are read before
+      // the slot is zeroed, then added back as u16 counters (each < 2^8: no
+      // carry into the neighbouring half of the word)
+      const uint32_t m = tv.list_m(r);
+      const uint32_t ne = (uint32_t)(dw / tv.w) * m;
+      uint32_t ent[32];
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        const uint32_t t = threadIdx.x + 256u * q;
+        ent[q] = 0xFFFFFFFFu;
+        if (t < ne) {
+          const uint32_t rr = t / m;
+          ent[q] = rr * (uint32_t)tv.w + tv.t16[r * dw + 1 + t];
+        }
+      }
+      __syncthreads();  // every entry is read before the zero fill
+      for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) d4[j] = make_uint4(0, 0, 0, 0);
+      __threadfence();
+      __syncthreads();  // the zeros are in L2 before the adds
+      uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * dw);
+#pragma unroll
+      for (int q = 0; q < 32; ++q)
+        if (ent[q] != 0xFFFFFFFFu) atomicAdd(w32 + (ent[q] >> 1), 1u << ((ent[q] & 1u) << 4));
+      __syncthreads();
+      if (threadIdx.x == 0) hidx[r] = kFormU16;
+      continue;
+    }
     for (int64_t c0 = ((dw - 1) / kChunk) * kChunk; c0 >= 0; c0 -= kChunk) {
       const int64_t j = c0 + (int64_t)threadIdx.x * 16;  // this lane's 16 counters
       uint32_t v[16];
@@ -206,27 +234,32 @@ int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass,
   return CMS_OK;
 }
 
-__global__ void k_count_forms(const int32_t* hidx, int64_t n, unsigned long long* out) {
-  uint32_t c[6] = {0, 0, 0, 0, 0, 0};
+// [0..5] hot, u16, u8, 4-bit, 2-bit, 1-bit rows, [6] list rows, [7] their bytes
+__global__ void k_count_forms(TableView tv, int64_t n, unsigned long long* out) {
+  uint32_t c[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long lb = 0;
+  const uint64_t d = (uint64_t)(tv.dw / tv.w);
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t f = hidx[r];
-    c[f >= 0 ? 0 : f == kFormU16 ? 1 : f == kFormU8 ? 2 : f == kFormU4 ? 3 : f == kFormU2 ? 4 : 5] += 1;
+    const int32_t f = tv.hidx[r];
+    c[f >= 0 ? 0 : f == kFormU16 ? 1 : f == kFormU8 ? 2 : f == kFormU4 ? 3 : f == kFormU2 ? 4 : f == kFormU1 ? 5 : 6] += 1;
+    if (f == kFormList) lb += 2 + 2 * d * tv.list_m(r);
   }
-  for (int q = 0; q < 6; ++q)
+  for (int q = 0; q < 7; ++q)
     if (c[q]) atomicAdd(out + q, (unsigned long long)c[q]);
+  if (lb) atomicAdd(out + 7, lb);
 }
 
-int count_forms(cms_handle* h, int64_t out[6]) {
+int count_forms(cms_handle* h, int64_t out[8]) {
   DevBuf tmp;
-  CMS_HIP(tmp.ensure(6 * sizeof(unsigned long long)));
-  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 6 * sizeof(unsigned long long), h->stream));
+  CMS_HIP(tmp.ensure(8 * sizeof(unsigned long long)));
+  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 8 * sizeof(unsigned long long), h->stream));
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 4096));
-  hipLaunchKernelGGL(k_count_forms, dim3(g), dim3(256), 0, h->stream, h->d_hidx, h->n, tmp.as<unsigned long long>());
+  hipLaunchKernelGGL(k_count_forms, dim3(g), dim3(256), 0, h->stream, h->tview(), h->n, tmp.as<unsigned long long>());
   CMS_HIP(hipGetLastError());
-  unsigned long long c[6];
+  unsigned long long c[8];
   CMS_HIP(hipMemcpyAsync(c, tmp.ptr, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
-  for (int q = 0; q < 6; ++q) out[q] = (int64_t)c[q];
+  for (int q = 0; q < 8; ++q) out[q] = (int64_t)c[q];
   return CMS_OK;
 }
 
@@ -258,13 +291,26 @@ __global__ void k_read_u32(TableView tv, int64_t r0, int64_t rc, uint32_t* out, 
        i += (int64_t)gridDim.x * blockDim.x * 4) {
     const int64_t r = i / tv.dw, j = i - r * tv.dw;
     if (vec) {
-      *reinterpret_cast<uint4*>(out + i) = tv.get4(r0 + r, j);
+      *reinterpret_cast<uint4*>(out + i) =
+          tv.hidx[r0 + r] == kFormList ? make_uint4(0, 0, 0, 0) : tv.get4(r0 + r, j);  // lists: k_read_lists
     } else {
       for (int64_t e = i; e < min(i + 4, total); ++e) {
         const int64_t re = e / tv.dw;
-        out[e] = tv.get(r0 + re, e - re * tv.dw);
+        out[e] = tv.hidx[r0 + re] == kFormList ? 0u : tv.get(r0 + re, e - re * tv.dw);
       }
     }
+  }
+}
+
+// list rows of [r0, r0 + rc): their entries added into the zeros k_read_u32 left
+__global__ void k_read_lists(TableView tv, int64_t r0, int64_t rc, uint32_t* out) {
+  for (int64_t r = blockIdx.x; r < rc; r += gridDim.x) {
+    if (tv.hidx[r0 + r] != kFormList) continue;
+    const uint32_t m = tv.list_m(r0 + r);
+    const int64_t ne = (tv.dw / tv.w) * (int64_t)m;
+    const uint16_t* e = tv.t16 + (r0 + r) * tv.dw + 1;
+    for (int64_t t = threadIdx.x; t < ne; t += blockDim.x)
+      atomicAdd(out + r * tv.dw + (t / m) * tv.w + e[t], 1u);
   }
 }
 
@@ -278,6 +324,9 @@ int read_counters_device(cms_handle* h, int64_t r0, int64_t rc, uint32_t* d_out)
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((quads + 255) / 256, 65536));
   const int vec = (h->dw & 3) == 0 && ((uintptr_t)d_out & 15) == 0;
   hipLaunchKernelGGL(k_read_u32, dim3(g), dim3(256), 0, h->stream, h->tview(), r0, rc, d_out, vec);
+  if (h->forms_ok)
+    hipLaunchKernelGGL(k_read_lists, dim3((unsigned)std::min<int64_t>(rc, 65536)), dim3(256), 0, h->stream,
+                       h->tview(), r0, rc, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

@@ -25,17 +25,20 @@ timeout -k 10 700 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 
   || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 echo "bench ok"
 python -c "import json; print(json.dumps(json.load(open('gpurun_out/bench.json'))['summary']))"
-# A/B arms of the ingest step against variant libraries under ab/ (built on
-# the CPU side with build_lib.py --define ... --out ab/<name>.so)
-for i in 1; do
-  for lib in main ab/*.so; do
-    [ -e "$lib" ] || [ "$lib" = main ] || continue
-    tag=$(basename "$lib" .so)
-    if [ "$lib" = main ]; then envs=(); else envs=(MAHOUT_CMS_LIB="$PWD/$lib"); fi
-    env "${envs[@]}" timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras \
-        --no-config1 --no-config2 --no-cosine-1m > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err \
-      || { echo "A/B arm $tag failed"; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], d.get('breakdown_ms_per_step'))" gpurun_out/ab_${tag}_$i.json
-  done
+# A/B arms of the ingest step: ARMS (default: the main library, every variant
+# library under ab/, then env:NAME=VALUE arms on the main library); variant
+# libraries are built on the CPU side with build_lib.py --define ... --out ab/<name>.so
+ARMS=${ARMS:-"main $(ls ab/*.so 2>/dev/null | tr '\n' ' ')"}
+for arm in $ARMS; do
+  envs=()
+  case "$arm" in
+    main) tag=main ;;
+    env:*) envs=("${arm#env:}"); tag=$(echo "${arm#env:}" | tr '=' '_') ;;
+    *) envs=(MAHOUT_CMS_LIB="$PWD/$arm"); tag=$(basename "$arm" .so) ;;
+  esac
+  env "${envs[@]}" timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras \
+      --no-config1 --no-config2 --no-cosine-1m > gpurun_out/ab_${tag}.json 2> gpurun_out/ab_${tag}.err \
+    || { echo "A/B arm $tag failed"; exit 1; }
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['ms_per_step'], d.get('breakdown_ms_per_step'))" gpurun_out/ab_${tag}.json
 done
 exit $rc

@@ -1,6 +1,6 @@
-"""GPU: narrow storage forms of the sketch table (u8, 4-bit and 2-bit rows
-inside their u16 slots; cms_internal.h TableView, cms_build.hip byte-form path,
-cms_table.hip widen_rows).
+"""GPU: narrow storage forms of the sketch table (u8, 4-bit, 2-bit and 1-bit
+rows, and sparse list rows, inside their u16 slots; cms_internal.h TableView,
+cms_build.hip byte-form path, cms_table.hip widen_rows).
 
 The form a row is stored in is an implementation detail: every counter must
 read back as DoubleCountMinSketch's value (`T/impl/common/DoubleCountMinSketch.java:72-80`)
@@ -32,34 +32,44 @@ def _stream(n, n_keys, pairs, seed):
     return items.astype(np.int64), users.astype(np.int64)
 
 
-def _handle(n, d, w, forms):
-    old = os.environ.pop("CMS_NO_FORMS", None)
+def _handle(n, d, w, forms, lists=True):
+    """forms=False: CMS_NO_FORMS=1 (every narrow row u16); lists=False:
+    CMS_LIST_KEYS=0 (the byte-class owners take the dense 1/2/4-bit rows)."""
+    saved = {k: os.environ.pop(k, None) for k in ("CMS_NO_FORMS", "CMS_LIST_KEYS")}
     if not forms:
         os.environ["CMS_NO_FORMS"] = "1"
+    if not lists:
+        os.environ["CMS_LIST_KEYS"] = "0"
     try:
         return SketchTable(n, depth=d, width=w, seed=42)
     finally:
-        os.environ.pop("CMS_NO_FORMS", None)
-        if old is not None:
-            os.environ["CMS_NO_FORMS"] = old
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
 
 
+@pytest.mark.parametrize("lists", [True, False])
 @pytest.mark.parametrize("n,d,w", [(3000, 5, 1024), (1500, 4, 256)])
-def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
+def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w, lists):
     rng = np.random.Generator(np.random.PCG64(n))
     # Zipf: a few hot owners (u32), a band of u16 owners, many u8 / nibble owners
     items, users = _stream(n, 20000, 600_000, seed=n)
     a, b = oracle.hash_params(42, d)
     stream = [(items, users, np.ones(items.size, np.float32))]
-    with _handle(n, d, w, True) as t, _handle(n, d, w, False) as plain:
+    with _handle(n, d, w, True, lists) as t, _handle(n, d, w, False) as plain:
         for x in (t, plain):
             x.ingest(items, users)
             x.finalize()
         st = t.stats()
-        assert st["crumb_rows"] > 0 and st["nibble_rows"] > 0 and st["u8_rows"] > 0 and st["hot_rows"] > 0, st
-        assert st["bit_rows"] + st["crumb_rows"] + st["nibble_rows"] + st["u8_rows"] + st["hot_rows"] < n  # and u16 rows
+        small_form = "list_rows" if lists else "crumb_rows"  # the byte-class owners' form
+        assert st[small_form] > 0 and st["nibble_rows"] > 0 and st["u8_rows"] > 0 and st["hot_rows"] > 0, st
+        assert (st["list_rows"] > 0) == lists and (st["crumb_rows"] + st["bit_rows"] == 0) == lists, st
+        assert st["bit_rows"] + st["crumb_rows"] + st["list_rows"] + st["nibble_rows"] + st["u8_rows"] + \
+            st["hot_rows"] < n  # and u16 rows
         ps = plain.stats()
         assert ps["bit_rows"] == 0 and ps["crumb_rows"] == 0 and ps["nibble_rows"] == 0 and ps["u8_rows"] == 0
+        assert ps["list_rows"] == 0
         assert st["stored_bytes"] < plain.stats()["stored_bytes"]
         exp = oracle.build_table(n, d, w, a, b, *[np.concatenate(c) for c in zip(*stream)])
         assert np.array_equal(t.read_counters(), exp)
@@ -99,9 +109,10 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
                 assert _same(s1, ref), (step, q)
             seen.append(t.stats())
         # the atomic batches widen only the rows they could push past their form
-        small = [x["nibble_rows"] + x["crumb_rows"] + x["bit_rows"] for x in seen]
-        assert 0 < small[0] < st["nibble_rows"] + st["crumb_rows"] + st["bit_rows"]
-        assert seen[0]["crumb_rows"] < st["crumb_rows"]  # 2-bit rows pushed past 3 were widened
+        small = [x["nibble_rows"] + x["crumb_rows"] + x["bit_rows"] + x["list_rows"] for x in seen]
+        assert 0 < small[0] < st["nibble_rows"] + st["crumb_rows"] + st["bit_rows"] + st["list_rows"]
+        # 2-bit rows pushed past 3 were widened; a list row takes no in-place add (any add widens it)
+        assert seen[0][small_form] < st[small_form]
         assert u8_rows.size < 2 or 0 < seen[1]["u8_rows"] < seen[0]["u8_rows"]
         assert seen[1]["hot_rows"] >= st["hot_rows"]
         assert small[2] <= small[1]
@@ -114,24 +125,27 @@ def test_forms_build_incremental_accumulate_bit_exact(oracle, n, d, w):
         assert all(np.array_equal(x, y, equal_nan=True) for x, y in zip(got, want))
 
 
-@pytest.mark.parametrize("bit_keys", ["0", None])
-def test_forms_point_queries_and_device_read(oracle, monkeypatch, bit_keys):
+@pytest.mark.parametrize("mode", ["bits", "nobits", "lists"])
+def test_forms_point_queries_and_device_read(oracle, monkeypatch, mode):
     """Point queries (DoubleCountMinSketch.get, :94-103) and the device
     counter read on 2-bit, 4-bit and u8 rows, with and without 1-bit rows
-    (owners of <= 64 keys try them first unless CMS_BIT_KEYS=0), then a batch
-    that widens some of every form."""
+    (owners of <= 64 keys try them first unless CMS_BIT_KEYS=0), or with the
+    byte-class owners as list rows, then a batch that widens some of every form."""
     import torch
-    if bit_keys:
-        monkeypatch.setenv("CMS_BIT_KEYS", bit_keys)
+    if mode == "nobits":
+        monkeypatch.setenv("CMS_BIT_KEYS", "0")
     n, d, w = 2000, 4, 512
     items, users = _stream(n, 5000, 300_000, seed=3)  # > 262143 pairs: the row build (smaller batches: atomics)
     a, b = oracle.hash_params(42, d)
     exp = oracle.build_table(n, d, w, a, b, items, users)
-    with _handle(n, d, w, True) as t:
+    with _handle(n, d, w, True, mode == "lists") as t:
         t.ingest(items, users)
         t.finalize()
         st = t.stats()
-        assert st["nibble_rows"] > 0 and st["crumb_rows"] > 0 and (st["bit_rows"] > 0) == (bit_keys is None), st
+        if mode == "lists":
+            assert st["list_rows"] > 0 and st["nibble_rows"] > 0 and st["crumb_rows"] + st["bit_rows"] == 0, st
+        else:
+            assert st["nibble_rows"] > 0 and st["crumb_rows"] > 0 and (st["bit_rows"] > 0) == (mode == "bits"), st
         dev = t.read_counters_device(0, n).cpu().numpy()
         assert np.array_equal(dev.astype(np.float64), exp)
         for r in (0, 5, 400, n - 1):
@@ -157,7 +171,8 @@ def test_forms_point_queries_and_device_read(oracle, monkeypatch, bit_keys):
         torch.cuda.synchronize()
 
 
-def test_accumulate_build_zero_valued_form_rows(oracle):
+@pytest.mark.parametrize("lists", [False, True])
+def test_accumulate_build_zero_valued_form_rows(oracle, lists):
     """A CSR batch into a live table with forms (the accumulate build) where
     narrow owners' keys all carry 0.0: the build rewrites every owner that has
     keys through its u16 image, so those rows must be widened first even though
@@ -167,11 +182,14 @@ def test_accumulate_build_zero_valued_form_rows(oracle):
     items, users = _stream(n, 5000, 300_000, seed=11)
     a, b = oracle.hash_params(42, d)
     exp = oracle.build_table(n, d, w, a, b, items, users)
-    with _handle(n, d, w, True) as t:
+    with _handle(n, d, w, True, lists) as t:
         t.ingest(items, users)
         t.finalize()
         st = t.stats()
-        assert st["bit_rows"] > 0 and st["crumb_rows"] > 0 and st["nibble_rows"] > 0, st
+        if lists:
+            assert st["list_rows"] > 0 and st["nibble_rows"] > 0, st
+        else:
+            assert st["bit_rows"] > 0 and st["crumb_rows"] > 0 and st["nibble_rows"] > 0, st
         mx = exp.max(axis=(1, 2))
         # owners in the 1-/2-bit, 4-bit and u8 forms
         picks = [np.flatnonzero(mx == 1)[:2], np.flatnonzero((mx >= 2) & (mx <= 3))[:2],
