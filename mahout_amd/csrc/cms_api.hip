@@ -1,6 +1,9 @@
 // cms_api.hip -- extern "C" entry points of libmahout_cms.so (see
 // include/mahout_cms.h for the reference interface each one replaces).
 #include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -31,8 +34,20 @@ int hip_fail(hipError_t e, const char* what) {
   return set_error(CMS_E_HIP, "%s failed: %s", what, hipGetErrorString(e));
 }
 
+// host time spent in device allocations (process-wide; cms_get_timing's
+// "host_alloc" scope): a first all-pairs job allocates its operand images and
+// candidate lists, tens of GB at config 4
+static std::atomic<int64_t> g_alloc_ns{0}, g_alloc_calls{0};
+
 hipError_t DevBuf::ensure(size_t need) {
   if (need <= bytes && ptr) return hipSuccess;
+  struct AllocClock {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~AllocClock() {
+      g_alloc_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+      ++g_alloc_calls;
+    }
+  } clock;
   if (ptr) {
     hipError_t e = hipFree(ptr);
     if (e != hipSuccess) return e;
@@ -1532,6 +1547,11 @@ int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* l
   Guard g(h);
   int rc = resolve_timing(h);
   if (rc) return rc;
+  if (std::strcmp(name, "host_alloc") == 0) {  // process-wide host time in device allocations (hipFree + hipMalloc)
+    *total_ms = (double)g_alloc_ns.load() * 1e-6;
+    *launches = g_alloc_calls.load();
+    return CMS_OK;
+  }
   auto it = h->timing_acc.find(name);
   *total_ms = it == h->timing_acc.end() ? 0.0 : it->second.total_ms;
   *launches = it == h->timing_acc.end() ? 0 : it->second.launches;
@@ -1543,6 +1563,8 @@ int cms_reset_timing(cms_handle* h) {
   Guard g(h);
   int rc = resolve_timing(h);
   h->timing_acc.clear();
+  g_alloc_ns = 0;
+  g_alloc_calls = 0;
   return rc;
 }
 

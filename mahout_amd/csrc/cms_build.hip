@@ -826,8 +826,12 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
   // list rows (cms_internal.h kFormList): unit increments, at most list_keys
   // keys; counted as 4-bit in LDS for the norms and the maximum only, the
   // entries leave as the owner's buckets
-  const bool as_list = m <= list_keys && vals == nullptr && hp.frac_bits == 0;
-  int bits = as_list ? 4 : (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
+  int bits = (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
+  // only where the list is no larger than the dense row the owner would take
+  // first (2 + 2 d m bytes against d w bits / 8; both fit the slot then)
+  const bool as_list = m <= list_keys && vals == nullptr && hp.frac_bits == 0 &&
+                       2 + 2 * (int64_t)hp.depth * m <= ((int64_t)hp.depth * w * bits) / 8;
+  if (as_list) bits = 4;
   uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;  // list row: [0] = m, then [d][m] buckets
   uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * (w >> 5);  // w/2 bytes per wave (the 4-bit row)
   uint32_t* slot = lds + wv * (w >> 3);

@@ -57,9 +57,10 @@ constexpr int kMaxBins = 4096;
 #define CMS_P1_ROUNDS 4
 #endif
 // pass-2 tile in rounds of kPartTile pairs (1, 2 or 4: a block's chunk is
-// four rounds)
+// four rounds; 4 = one 16384-pair tile per block: config-3 partition
+// 5.30-5.34 -> 5.08-5.11 ms in two A/B runs, profiles/r04/ab_*)
 #ifndef CMS_P2_ROUNDS
-#define CMS_P2_ROUNDS 1
+#define CMS_P2_ROUNDS 4
 #endif
 
 // LDS histogram increment aggregated across the wave.  Zipf streams put most

@@ -111,12 +111,13 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
   return CMS_OK;
 }
 
-// ---- narrow forms (u8 / 4-bit / 2-bit / 1-bit rows inside their u16 slots) ----
+// ---- narrow forms (u8 / 4-bit / 2-bit / 1-bit and list rows inside their u16 slots) ----
 
-// Rows to widen to u16 before a write (see widen_rows in cms_internal.h).
-// With span bounds (lo, hi: the accumulate build's owner spans) a row is
-// touched when it has keys -- the build rewrites every such row through its
-// u16 / u32 image even when all its increments are 0 (no mass added).
+// Rows to widen before a write (see widen_rows in cms_internal.h).  With span
+// bounds (lo, hi: the accumulate build's owner spans) a row is touched when it
+// has keys -- the build rewrites every such row through its u16 / u32 image
+// even when all its increments are 0 (no mass added).  A listed row's cbound
+// becomes its bound after the write, which picks the form it widens to.
 __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int64_t* lo, const int64_t* hi,
                              const int32_t* hidx, uint32_t* cbound, int64_t n, int all_touched, int32_t* list,
                              uint32_t* cnt) {
@@ -130,89 +131,123 @@ __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, co
       if (b <= m && !has_keys) continue;  // no update lands on this row
       const uint64_t nb = (uint64_t)cbound[r] + (b - m);
       need = all_touched || nb > (uint64_t)form_cap(f);
-      if (!need) cbound[r] = (uint32_t)nb;  // <= the form's capacity
+      cbound[r] = (uint32_t)min<uint64_t>(nb, 0xFFFFFFFFull);  // <= the capacity of the form it keeps or takes
     }
     if (need) list[atomicAdd(cnt, 1u)] = (int32_t)r;
   }
 }
 
-// One workgroup per listed row: its u8 / 4-bit / 2-bit / 1-bit counters rewritten as u16 in
-// the same slot.  The u16 image of counters [c0, c1) covers bytes
-// [2 c0, 2 c1), which holds only old bytes of counters >= c0; so chunks of
-// 4096 counters are processed from the top down, each read completely (16
-// counters per lane) before any lane writes it.
+__device__ __forceinline__ int form_bits(int32_t f) {  // counter bits of a form (0: a list row)
+  return f == kFormList ? 0 : f == kFormU1 ? 1 : f == kFormU2 ? 2 : f == kFormU4 ? 4 : f == kFormU8 ? 8 : 16;
+}
+
+// 16 counters v[0..16) packed at 32 / C bits into C-counter words at w32[j / C ...]
+template <int C>
+__device__ __forceinline__ void pack16(const uint32_t (&v)[16], uint32_t* w32, int64_t j) {
+#pragma unroll
+  for (int q = 0; q < 16; q += C) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < C; ++k) word |= v[q + k] << (k * (32 / C));
+    w32[(j + q) / C] = word;
+  }
+}
+
+// One workgroup per listed row, rewritten in place in the narrowest form
+// wider than its own whose capacity holds its new bound (cbound), u16 for an
+// accumulate build (to_u16) -- a 2-bit row that one more pair lifts to 4
+// becomes a 4-bit row (half the bytes of u8, a quarter of u16).
+//  * dense forms: the image of counters [c0, c1) at tb >= sb bits covers
+//    bytes [c0 tb/8, c1 tb/8), which hold only old bytes of counters >= c0;
+//    so chunks of 4096 counters go from the top down, each read completely
+//    (16 counters per lane) before any lane writes it.
+//  * list rows: every entry is read first (at most 32 per lane: d <= 32,
+//    m <= 256), then each sketch row is counted in LDS (u8 counters, four per
+//    word: a list row's counters are < 2^8) and leaves packed.
 __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const uint32_t* dcount, TableView tv,
-                                                    int32_t* hidx) {
+                                                    int32_t* hidx, const uint32_t* cbound, int to_u16) {
+  extern __shared__ uint32_t lc[];  // [w / 4] (list rows)
   const int64_t count = *dcount;
   const int64_t dw = tv.dw;
+  const int w = tv.w;
   constexpr int64_t kChunk = 256 * 16;
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int64_t r = list[i];
     const int32_t f = hidx[r];
+    const uint32_t nb = cbound[r];
+    int32_t tf = kFormU16;
+    if (!to_u16) {
+      if (f == kFormList && nb <= 1u && (w & 127) == 0) tf = kFormU1;
+      else if (form_bits(f) < 2 && nb <= 3u && (w & 63) == 0) tf = kFormU2;
+      else if (form_bits(f) < 4 && nb <= 15u) tf = kFormU4;
+      else if (form_bits(f) < 8 && nb <= 255u) tf = kFormU8;
+    }
+    const int tb = form_bits(tf);
     uint8_t* p8 = reinterpret_cast<uint8_t*>(tv.t16 + r * dw);
-    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + r * dw);
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * dw);
     if (f == kFormList) {
-      // the entries (at most 32 per lane: d <= 32, m <= 256) are read before
-      // the slot is zeroed, then added back as u16 counters (each < 2^8: no
-      // carry into the neighbouring half of the word)
       const uint32_t m = tv.list_m(r);
-      const uint32_t ne = (uint32_t)(dw / tv.w) * m;
+      const uint32_t ne = (uint32_t)(dw / w) * m;
       uint32_t ent[32];
 #pragma unroll
       for (int q = 0; q < 32; ++q) {
         const uint32_t t = threadIdx.x + 256u * q;
         ent[q] = 0xFFFFFFFFu;
-        if (t < ne) {
-          const uint32_t rr = t / m;
-          ent[q] = rr * (uint32_t)tv.w + tv.t16[r * dw + 1 + t];
+        if (t < ne) ent[q] = (t / m) << 16 | tv.t16[r * dw + 1 + t];  // sketch row, bucket
+      }
+      const int cpw = 32 / tb;  // counters per output word
+      for (int rr = 0; (int64_t)rr * w < dw; ++rr) {
+        for (int j = threadIdx.x; j < (w >> 2); j += 256) lc[j] = 0u;
+        __syncthreads();  // (the first pass: every entry is also read before any store below)
+#pragma unroll
+        for (int q = 0; q < 32; ++q)
+          if (ent[q] != 0xFFFFFFFFu && (int)(ent[q] >> 16) == rr)
+            atomicAdd(&lc[(ent[q] & 0xFFFFu) >> 2], 1u << ((ent[q] & 3u) * 8u));
+        __syncthreads();
+        const uint8_t* c8 = reinterpret_cast<const uint8_t*>(lc);
+        for (int q = threadIdx.x; q < w / cpw; q += 256) {
+          uint32_t word = 0;
+          for (int k = 0; k < cpw; ++k) word |= (uint32_t)c8[q * cpw + k] << (k * tb);
+          w32[((int64_t)rr * w) / cpw + q] = word;
         }
+        __syncthreads();  // the counts are packed before the next sketch row zeroes them
       }
-      __syncthreads();  // every entry is read before the zero fill
-      for (int64_t j = threadIdx.x; j < (dw >> 3); j += 256) d4[j] = make_uint4(0, 0, 0, 0);
-      __threadfence();
-      __syncthreads();  // the zeros are in L2 before the adds
-      uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * dw);
+    } else {
+      for (int64_t c0 = ((dw - 1) / kChunk) * kChunk; c0 >= 0; c0 -= kChunk) {
+        const int64_t j = c0 + (int64_t)threadIdx.x * 16;  // this lane's 16 counters
+        uint32_t v[16];
+        if (j < dw) {
+          if (f == kFormU8) {
+            const uint4 x = *reinterpret_cast<const uint4*>(p8 + j);
+            const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-      for (int q = 0; q < 32; ++q)
-        if (ent[q] != 0xFFFFFFFFu) atomicAdd(w32 + (ent[q] >> 1), 1u << ((ent[q] & 1u) << 4));
-      __syncthreads();
-      if (threadIdx.x == 0) hidx[r] = kFormU16;
-      continue;
-    }
-    for (int64_t c0 = ((dw - 1) / kChunk) * kChunk; c0 >= 0; c0 -= kChunk) {
-      const int64_t j = c0 + (int64_t)threadIdx.x * 16;  // this lane's 16 counters
-      uint32_t v[16];
-      if (j < dw) {
-        if (f == kFormU8) {
-          const uint4 x = *reinterpret_cast<const uint4*>(p8 + j);
-          const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+            for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 2] >> ((q & 3) * 8)) & 255u;
+          } else if (f == kFormU2) {
+            const uint32_t x = *reinterpret_cast<const uint32_t*>(p8 + (j >> 2));
 #pragma unroll
-          for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 2] >> ((q & 3) * 8)) & 255u;
-        } else if (f == kFormU2) {
-          const uint32_t x = *reinterpret_cast<const uint32_t*>(p8 + (j >> 2));
+            for (int q = 0; q < 16; ++q) v[q] = (x >> (q * 2)) & 3u;
+          } else if (f == kFormU1) {
+            const uint32_t x = *reinterpret_cast<const uint16_t*>(p8 + (j >> 3));
 #pragma unroll
-          for (int q = 0; q < 16; ++q) v[q] = (x >> (q * 2)) & 3u;
-        } else if (f == kFormU1) {
-          const uint32_t x = *reinterpret_cast<const uint16_t*>(p8 + (j >> 3));
+            for (int q = 0; q < 16; ++q) v[q] = (x >> q) & 1u;
+          } else {
+            const uint2 x = *reinterpret_cast<const uint2*>(p8 + (j >> 1));
+            const uint32_t wv[2] = {x.x, x.y};
 #pragma unroll
-          for (int q = 0; q < 16; ++q) v[q] = (x >> q) & 1u;
-        } else {
-          const uint2 x = *reinterpret_cast<const uint2*>(p8 + (j >> 1));
-          const uint32_t wv[2] = {x.x, x.y};
-#pragma unroll
-          for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 3] >> ((q & 7) * 4)) & 15u;
+            for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 3] >> ((q & 7) * 4)) & 15u;
+          }
         }
+        __syncthreads();  // the whole chunk is read before any lane overwrites it
+        if (j < dw) {  // 16 counters at tb bits: tb / 2 words from word j tb / 32
+          if (tb == 2) pack16<16>(v, w32, j);
+          else if (tb == 4) pack16<8>(v, w32, j);
+          else if (tb == 8) pack16<4>(v, w32, j);
+          else pack16<2>(v, w32, j);
+        }
+        __syncthreads();  // the next (lower) chunk's old bytes are read after these stores
       }
-      __syncthreads();  // the whole chunk is read before any lane overwrites it
-      if (j < dw) {
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2)
-          d4[(j >> 3) + h2] = make_uint4(v[8 * h2] | (v[8 * h2 + 1] << 16), v[8 * h2 + 2] | (v[8 * h2 + 3] << 16),
-                                         v[8 * h2 + 4] | (v[8 * h2 + 5] << 16), v[8 * h2 + 6] | (v[8 * h2 + 7] << 16));
-      }
-      __syncthreads();  // the next (lower) chunk's old bytes are read after these stores
     }
-    if (threadIdx.x == 0) hidx[r] = kFormU16;
+    if (threadIdx.x == 0) hidx[r] = tf;
   }
 }
 
@@ -227,9 +262,10 @@ int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass,
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
   hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, d_lo, d_hi, h->d_hidx,
                      h->d_cbound, n, all_touched ? 1 : 0, list, cnt);
-  // one workgroup per row, looping: the count stays on the device
-  hipLaunchKernelGGL(k_widen_rows, dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(256), 0, h->stream, list, cnt,
-                     h->tview(), h->d_hidx);
+  // one workgroup per row, looping: the count stays on the device; u16 for
+  // an accumulate build or when no bound is known
+  hipLaunchKernelGGL(k_widen_rows, dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(256), (size_t)h->p.width,
+                     h->stream, list, cnt, h->tview(), h->d_hidx, h->d_cbound, (all_touched || !d_bound) ? 1 : 0);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
