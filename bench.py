@@ -812,11 +812,20 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     touched_one = sum(torch.unique(b[0]).numel() for b in batches) / (n * nb)
     every = max(1, args.refresh_every)
     # the periodic refresh keeps 2k-deep lists: one whole job builds them
+    scope_names = ["limb_prep", "topk_all_multi_rows", "cosine_mfma_limbs", "cosine_mfma_multi", "topk_all_waves_f4",
+                   "topk_all_waves_i8", "topk_merge", "top_k", "cosine_mfma", "host_alloc"]
+
+    def scopes():  # GPU time of the job's phases (HIP events, this rank)
+        return {nm: round(t.timing(nm)[0], 1) for nm in scope_names if t.timing(nm)[0]}
+
+    t.set_timing(True)
+    t.reset_timing()
     bar()
     t0 = time.perf_counter()
     t.top_k_refresh_device(k)
     bar()
     keep_s = max_over_ranks(time.perf_counter() - t0)
+    keep_scopes = scopes()
     periods = []
     cnt = None
     for bi, (it_, us) in enumerate(batches):
@@ -828,13 +837,15 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
             t.finalize()  # with G ranks: the delta logs all-gathered and applied
             bar()
             fs = max_over_ranks(time.perf_counter() - t0)
+            t.reset_timing()
             t0 = time.perf_counter()
             _, _, cnt = t.top_k_refresh_device(k)  # lists stay in HBM (Refreshable consumers read them there)
             bar()
             rs = max_over_ranks(time.perf_counter() - t0)
             touched, redone, full = t.refresh_stats()
             periods.append({"after_batch": bi + 1, "finalize_s": round(fs, 5), "refresh_s": round(rs, 4),
-                            "touched_owner_frac": touched / n, "lists_redone": redone, "whole_jobs": full})
+                            "touched_owner_frac": touched / n, "lists_redone": redone, "whole_jobs": full,
+                            "scopes_ms": scopes()})
     cnt = cnt.cpu().numpy()
     t.set_timing(False)
     del batches
@@ -854,6 +865,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "refresh_batches": nb, "pairs_per_batch_per_gpu": per_batch,
         "refresh_every_batches": every,
         "keep_lists_whole_job_s": keep_s,
+        "keep_lists_whole_job_scopes_ms": keep_scopes,
         "refresh_latency_s": sum(lat) / len(lat),
         "refresh_latency_max_s": max(lat),
         # unique pairs with a touched owner (the ones a refresh recomputes) per second

@@ -551,11 +551,15 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 // at a time (a w- or 2w-byte image), the returning LDS adds giving each
 // row's sum of squares.  A persistent grid walks the device-side list.
 template <int SV>
-__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(CMS_BUILD_WAVES, 8))) void k_build_mid(
+// 4 waves per SIMD (up to 128 VGPRs): the u8 image's 40 KB leave room for
+// four workgroups per CU at config 3 anyway
+__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
-    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
-  extern __shared__ __align__(16) uint32_t lds[];  // one sketch row, up to w u16 counters
+    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int all8) {
+  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image, or
+  // (all8) the [d][w] u8 image
+  extern __shared__ __align__(16) uint32_t lds[];
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
   __shared__ uint32_t s_max, s_ovf;
@@ -589,10 +593,18 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
       }
     }
     uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's slot (64-B aligned)
-    int level = 0;  // 0: 4-bit, 1: u8, 2: u16 (the class bound keeps every counter < 2^16)
+    int level = -1;  // the form that holds the owner: 0 4-bit, 1 u8, 2 u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
-    {  // 4-bit, all sketch rows in one key pass
-      const int nq_all = (int)((int64_t)hp.depth * w >> 5);  // uint4 of the [d][w] 4-bit image
+    // ALL sketch rows in one key pass: a [d][w] 4-bit image, then (when it
+    // overflows and the launch gave dw bytes of LDS) a [d][w] u8 image -- a
+    // Zipf key set repeats its popular keys, so a mid owner of ~600+ keys
+    // usually has a counter past 15 (config 3: 40K u8 owners, which took a
+    // 4-bit pass and five one-row u8 passes before)
+    for (int ab = 4; ab <= 8 && level < 0; ab *= 2) {
+      if (ab == 8 && !all8) break;
+      const int lga = ab == 4 ? 3 : 2;  // log2(counters per word)
+      const uint32_t capa = (1u << ab) - 1u;
+      const int nq_all = (int)((int64_t)hp.depth * w * ab >> 7);  // uint4 of the [d][w] image
       uint4* l4 = reinterpret_cast<uint4*>(lds);
       for (int j = tid; j < nq_all; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
       if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
@@ -603,13 +615,14 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
       }
       __syncthreads();
       bool ovf = false;
+      vmax = 0;
       auto add_all = [&](uint64_t kr, uint32_t inc) {
         for (int d = 0; d < hp.depth; ++d) {
           const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kr);
-          const uint32_t sh = (c & 7u) << 2;
-          const uint32_t old = (atomicAdd(&lds[c >> 3], inc << sh) >> sh) & 15u;
+          const uint32_t sh = (c & ((1u << lga) - 1u)) * (uint32_t)ab;
+          const uint32_t old = (atomicAdd(&lds[c >> lga], inc << sh) >> sh) & capa;
           const uint32_t nv = old + inc;
-          ovf |= nv > 15u || inc > 15u;  // carried into the next counter: a wider form
+          ovf |= nv > capa || inc > capa;  // carried into the next counter: a wider form
           vmax = max(vmax, nv);
         }
       };
@@ -618,13 +631,24 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
         for (int k = 0; k < kKeyRegs; ++k)
           if (ik[k]) add_all(kp[k], ik[k]);
       } else {
-        for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
+        // the next step's key loads go out before this step's keys are added
+        constexpr int64_t kStep = 4 * kBuildThreads;
+        uint64_t nx[4];
+        auto fetch = [&](int64_t base) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            nx[u] = i < hi ? keys.raw(i) : 0ULL;
+          }
+        };
+        fetch(lo);
+        for (int64_t base = lo; base < hi; base += kStep) {
           uint64_t kk[4];
           uint32_t inc4[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
+            kk[u] = nx[u];
             const int64_t i = base + tid + (int64_t)u * kBuildThreads;
-            kk[u] = i < hi ? keys.at(i) : 0;
             inc4[u] = 0;
             if (i < hi) {
               uint32_t inc;
@@ -635,46 +659,53 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
               inc4[u] = inc;
             }
           }
+          if (base + kStep < hi) fetch(base + kStep);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            if (inc4[u]) add_all(kk[u], inc4[u]);
-            mass += inc4[u];
+            if (inc4[u]) add_all(keys.resolve(kk[u]), inc4[u]);
+            if (ab == 4) mass += inc4[u];  // counted on the first attempt only
           }
         }
       }
       if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
       __syncthreads();
       const bool fits = s_ovf == 0u;
-      __syncthreads();  // every thread has read s_ovf before the u8 attempt resets it
-      if (fits) {
-        // read the image back: each sketch row's sum of squares (v_dot4 of its
-        // low and high nibbles) as its rows leave for the slot
-        const int nq = w >> 5;  // uint4 per 4-bit sketch row
-        for (int d = 0; d < hp.depth; ++d) {
-          uint32_t sq = 0;  // <= row mass * 15 < 2^32
-          for (int j = tid; j < nq; j += kBuildThreads) {
-            const uint4 v = l4[d * nq + j];
-            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+      __syncthreads();  // every thread has read s_ovf before a later attempt resets it
+      if (!fits) continue;
+      level = ab == 4 ? 0 : 1;
+      // read the image back: each sketch row's sum of squares (v_dot4 of its
+      // bytes, or of its low and high nibbles) as its rows leave for the slot
+      const int nq = (w * ab) >> 7;  // uint4 per sketch row
+      for (int d = 0; d < hp.depth; ++d) {
+        uint32_t sq = 0;  // <= row mass * max counter < 2^32
+        for (int j = tid; j < nq; j += kBuildThreads) {
+          const uint4 v = l4[d * nq + j];
+          const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < 4; ++q) {
+            if (ab == 8) {
+              sq = __builtin_amdgcn_udot4(x[q], x[q], sq, false);
+            } else {
               const uint32_t lo4 = x[q] & 0x0F0F0F0Fu, hi4 = (x[q] >> 4) & 0x0F0F0F0Fu;
               sq = __builtin_amdgcn_udot4(lo4, lo4, sq, false);
               sq = __builtin_amdgcn_udot4(hi4, hi4, sq, false);
             }
-#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
-            if (false)
-#endif
-            store_row(d4 + d * nq + j, v, SV);
           }
-          sq = wave_sum_u32(sq);
-          if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+          if (false)
+#endif
+          store_row(d4 + d * nq + j, v, SV);
         }
-      } else {
-        level = 1;  // a counter passed 15: u8 rows, one sketch row at a time
+        sq = wave_sum_u32(sq);
+        if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
       }
     }
+    // both images overflowed (or u8 had no room): one sketch row at a time,
+    // u16 (u8 first when the u8 image was not tried)
+    if (level < 0) level = all8 ? 2 : 1;
+    else level = -level - 1;  // done: mark so the row passes are skipped
     for (;;) {
-      if (level == 0) break;  // the 4-bit image held every counter
+      if (level < 0) break;  // an all-rows image held every counter
       const int bits = 4 << level;
       const int lg = 3 - level;          // log2(counters per word)
       const uint32_t cap = (1u << bits) - 1u;
@@ -684,7 +715,6 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
       if (tid == 0) {
         s_max = 0u;
         s_ovf = 0u;
-        s_mass = 0ULL;
       }
       vmax = 0;
       for (int d = 0; d < hp.depth; ++d) {
@@ -745,6 +775,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
       __syncthreads();
       ++level;
     }
+    if (level < 0) level = -level - 1;
     if (badv) atomicOr(flags, kFlagBadValue);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
@@ -1011,18 +1042,31 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
   for (int j = (words & ~3) + tid; j < words; j += kSliceThreads) lds[j] = 0u;
   __syncthreads();
   const uint32_t one = 1u << hp.frac_bits;
-  for (int64_t base = lo; base < end; base += 4 * kSliceThreads) {
-    uint64_t kk[4];
+  // eight keys per thread per step; the next step's eight loads are issued
+  // before this step's keys are hashed, so a key load's latency is hidden
+  // behind the previous keys' d x 8 hashes and LDS adds
+  constexpr int kPer = 8;
+  constexpr int64_t kStep = kPer * kSliceThreads;
+  uint64_t nx[kPer];
+  auto fetch = [&](int64_t base) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // four key loads in flight
+    for (int u = 0; u < kPer; ++u) {
       const int64_t i = base + tid + (int64_t)u * kSliceThreads;
-      kk[u] = i < end ? keys.at(i) : ~0ULL;
+      nx[u] = i < end ? keys.raw(i) : 0ULL;
     }
+  };
+  if (lo < end) fetch(lo);
+  for (int64_t base = lo; base < end; base += kStep) {
+    uint64_t kk[kPer];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (kk[u] == ~0ULL) continue;
+    for (int u = 0; u < kPer; ++u) kk[u] = nx[u];
+    if (base + kStep < end) fetch(base + kStep);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      if (base + tid + (int64_t)u * kSliceThreads >= end) continue;  // (a raw key may be any 64-bit value)
+      const uint64_t kp = keys.resolve(kk[u]);
       for (int r = 0; r < hp.depth; ++r) {
-        const uint32_t c = (uint32_t)r * (uint32_t)w + bucket(hp, r, kk[u]);
+        const uint32_t c = (uint32_t)r * (uint32_t)w + bucket(hp, r, kp);
         atomicAdd(&lds[c >> 1], one << ((c & 1u) << 4));
       }
     }
@@ -1226,10 +1270,19 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          d_val, n, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
                          h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0);
+      // the u8 all-rows image when a [d][w] byte image fits 64 KB (config 3: 40 KB)
+      const int all8 = (size_t)h->dw <= 64 * 1024 ? 1 : 0;
+      const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, all8 ? (size_t)h->dw : (size_t)h->dw / 2);
+      static bool mid_attr = [] {
+        (void)hipFuncSetAttribute((const void*)k_build_mid<kBuildStoreForm>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  64 * 1024);
+        return true;
+      }();
+      (void)mid_attr;
       hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
-                         dim3(kBuildThreads), std::max<size_t>((size_t)h->p.width * 2, (size_t)h->dw / 2), side, d_lo,
-                         d_hi, keys, d_val, h->hp, (const int32_t*)mid_list, (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound,
-                         h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
+                         dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
+                         (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
+                         h->d_rowmax, h->d_flags, all8);
       hipLaunchKernelGGL(k_build_bytes<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)),
                          dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,
                          h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);

@@ -41,12 +41,13 @@ __device__ __forceinline__ uint32_t make_token(int64_t key, int64_t idx) {
 struct Keys {
   const int64_t* key;   // CSR keys (tok == null), or the batch's keys (escaped tokens index them)
   const uint32_t* tok;  // partition output tokens, or null
-  __device__ __forceinline__ uint64_t at(int64_t i) const {
-    if (tok) {
-      const uint32_t t = tok[i];
-      return t < kTokEscape ? (uint64_t)t : reduce_key(key[t & (kTokEscape - 1u)]);
-    }
-    return reduce_key(key[i]);
+  __device__ __forceinline__ uint64_t at(int64_t i) const { return resolve(raw(i)); }
+  // at(i) in two steps, so a loop can keep the next keys' loads in flight:
+  // raw(i) is the one load (the token, or the key itself), resolve() the rest
+  __device__ __forceinline__ uint64_t raw(int64_t i) const { return tok ? (uint64_t)tok[i] : (uint64_t)key[i]; }
+  __device__ __forceinline__ uint64_t resolve(uint64_t r) const {
+    if (tok) return r < kTokEscape ? r : reduce_key(key[r & (kTokEscape - 1u)]);
+    return reduce_key((int64_t)r);
   }
 };
 
