@@ -642,7 +642,8 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
     # host work: the operand images' and candidate lists' first allocations
     first_scopes = {name: t.timing(name)[0] for name in ["limb_prep", "topk_all_multi_rows", "cosine_mfma_limbs",
                                                          "cosine_mfma_multi", "topk_all_waves", "topk_merge",
-                                                         "host_alloc"]}
+                                                         "host_alloc", "host_free"]}
+    first_scopes["host_alloc_GB"] = t.timing("host_alloc_bytes")[0] / 1e9  # bytes the first job allocated
     t.reset_timing()
     bar()
     t0 = time.perf_counter()
@@ -813,7 +814,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     every = max(1, args.refresh_every)
     # the periodic refresh keeps 2k-deep lists: one whole job builds them
     scope_names = ["limb_prep", "topk_all_multi_rows", "cosine_mfma_limbs", "cosine_mfma_multi", "topk_all_waves_f4",
-                   "topk_all_waves_i8", "topk_merge", "top_k", "cosine_mfma", "host_alloc"]
+                   "topk_all_waves_i8", "topk_merge", "top_k", "cosine_mfma", "host_alloc", "host_free"]
 
     def scopes():  # GPU time of the job's phases (HIP events, this rank)
         return {nm: round(t.timing(nm)[0], 1) for nm in scope_names if t.timing(nm)[0]}

@@ -427,9 +427,11 @@ int cms_get_stats(cms_handle* h, cms_stats* out);
  * phases) included -- each recorded event costs the stream a few us. */
 int cms_set_timing(cms_handle* h, int32_t enabled);
 /* Accumulated (total ms, launches) for a kernel family name, e.g.
- * "build_rows", "partition", "norms", "allreduce", "cosine".  "host_alloc"
- * is the host wall time of the library's device allocations (process-wide,
- * whatever the timing switch; cleared by cms_reset_timing). */
+ * "build_rows", "partition", "norms", "allreduce", "cosine".  Process-wide
+ * host counters, whatever the timing switch (cleared by cms_reset_timing):
+ * "host_alloc" = ms in the library's hipMalloc calls (launches = calls),
+ * "host_free" = ms in the hipFree of a growing buffer (it waits for queued
+ * device work), "host_alloc_bytes" = bytes allocated (in total_ms). */
 int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* launches);
 int cms_reset_timing(cms_handle* h);
 

@@ -37,26 +37,31 @@ int hip_fail(hipError_t e, const char* what) {
 // host time spent in device allocations (process-wide; cms_get_timing's
 // "host_alloc" scope): a first all-pairs job allocates its operand images and
 // candidate lists, tens of GB at config 4
-static std::atomic<int64_t> g_alloc_ns{0}, g_alloc_calls{0};
+static std::atomic<int64_t> g_alloc_ns{0}, g_alloc_calls{0}, g_free_ns{0}, g_alloc_bytes{0};
+
+static int64_t ns_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
 
 hipError_t DevBuf::ensure(size_t need) {
   if (need <= bytes && ptr) return hipSuccess;
-  struct AllocClock {
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    ~AllocClock() {
-      g_alloc_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-      ++g_alloc_calls;
-    }
-  } clock;
-  if (ptr) {
+  if (ptr) {  // hipFree waits for the device's queued work: timed apart from the allocation
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipFree(ptr);
+    g_free_ns += ns_since(t0);
     if (e != hipSuccess) return e;
     ptr = nullptr;
     bytes = 0;
   }
   size_t alloc = std::max<size_t>(need, 256);
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&ptr, alloc);
-  if (e == hipSuccess) bytes = alloc;
+  g_alloc_ns += ns_since(t0);
+  ++g_alloc_calls;
+  if (e == hipSuccess) {
+    bytes = alloc;
+    g_alloc_bytes += (int64_t)alloc;
+  }
   return e;
 }
 
@@ -1547,9 +1552,19 @@ int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* l
   Guard g(h);
   int rc = resolve_timing(h);
   if (rc) return rc;
-  if (std::strcmp(name, "host_alloc") == 0) {  // process-wide host time in device allocations (hipFree + hipMalloc)
+  if (std::strcmp(name, "host_alloc") == 0) {  // process-wide host time in hipMalloc (launches = calls)
     *total_ms = (double)g_alloc_ns.load() * 1e-6;
     *launches = g_alloc_calls.load();
+    return CMS_OK;
+  }
+  if (std::strcmp(name, "host_alloc_bytes") == 0) {  // ... bytes allocated (in total_ms, as a count)
+    *total_ms = (double)g_alloc_bytes.load();
+    *launches = g_alloc_calls.load();
+    return CMS_OK;
+  }
+  if (std::strcmp(name, "host_free") == 0) {  // process-wide host time in the hipFree of a growing buffer
+    *total_ms = (double)g_free_ns.load() * 1e-6;
+    *launches = 0;
     return CMS_OK;
   }
   auto it = h->timing_acc.find(name);
@@ -1565,6 +1580,8 @@ int cms_reset_timing(cms_handle* h) {
   h->timing_acc.clear();
   g_alloc_ns = 0;
   g_alloc_calls = 0;
+  g_free_ns = 0;
+  g_alloc_bytes = 0;
   return rc;
 }
 

@@ -1045,7 +1045,10 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
   // eight keys per thread per step; the next step's eight loads are issued
   // before this step's keys are hashed, so a key load's latency is hidden
   // behind the previous keys' d x 8 hashes and LDS adds
-  constexpr int kPer = 8;
+#ifndef CMS_SLICE_KPER
+#define CMS_SLICE_KPER 8
+#endif
+  constexpr int kPer = CMS_SLICE_KPER;
   constexpr int64_t kStep = kPer * kSliceThreads;
   uint64_t nx[kPer];
   auto fetch = [&](int64_t base) {
@@ -1271,7 +1274,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
                          h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0);
       // the u8 all-rows image when a [d][w] byte image fits 64 KB (config 3: 40 KB)
-      const int all8 = (size_t)h->dw <= 64 * 1024 ? 1 : 0;
+#ifndef CMS_MID_ALL8
+#define CMS_MID_ALL8 1
+#endif
+      const int all8 = CMS_MID_ALL8 && (size_t)h->dw <= 64 * 1024 ? 1 : 0;
       const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, all8 ? (size_t)h->dw : (size_t)h->dw / 2);
       static bool mid_attr = [] {
         (void)hipFuncSetAttribute((const void*)k_build_mid<kBuildStoreForm>, hipFuncAttributeMaxDynamicSharedMemorySize,
