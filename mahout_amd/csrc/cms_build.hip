@@ -551,15 +551,13 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 // at a time (a w- or 2w-byte image), the returning LDS adds giving each
 // row's sum of squares.  A persistent grid walks the device-side list.
 template <int SV>
-// 4 waves per SIMD (up to 128 VGPRs): the u8 image's 40 KB leave room for
-// four workgroups per CU at config 3 anyway
+// 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
+// (it spilled there); the build measured the same (profiles/r04/ab_*_s5)
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
-    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int all8) {
-  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image, or
-  // (all8) the [d][w] u8 image
-  extern __shared__ __align__(16) uint32_t lds[];
+    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
+  extern __shared__ __align__(16) uint32_t lds[];  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
   __shared__ uint32_t s_max, s_ovf;
@@ -595,14 +593,13 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
     uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's slot (64-B aligned)
     int level = -1;  // the form that holds the owner: 0 4-bit, 1 u8, 2 u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
-    // ALL sketch rows in one key pass: a [d][w] 4-bit image, then (when it
-    // overflows and the launch gave dw bytes of LDS) a [d][w] u8 image -- a
-    // Zipf key set repeats its popular keys, so a mid owner of ~600+ keys
-    // usually has a counter past 15 (config 3: 40K u8 owners, which took a
-    // 4-bit pass and five one-row u8 passes before)
-    for (int ab = 4; ab <= 8 && level < 0; ab *= 2) {
-      if (ab == 8 && !all8) break;
-      const int lga = ab == 4 ? 3 : 2;  // log2(counters per word)
+    // ALL sketch rows in one key pass in a [d][w] 4-bit image.  (A [d][w] u8
+    // image after a 4-bit overflow -- a Zipf key set repeats its popular keys,
+    // and config 3 has 40K u8 owners -- measured slower: its 40 KB per
+    // workgroup halve the owners in flight, build 6.55 -> 7.01 ms.)
+    {
+      constexpr int ab = 4;
+      const int lga = 3;  // log2(counters per word)
       const uint32_t capa = (1u << ab) - 1u;
       const int nq_all = (int)((int64_t)hp.depth * w * ab >> 7);  // uint4 of the [d][w] image
       uint4* l4 = reinterpret_cast<uint4*>(lds);
@@ -663,19 +660,21 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             if (inc4[u]) add_all(keys.resolve(kk[u]), inc4[u]);
-            if (ab == 4) mass += inc4[u];  // counted on the first attempt only
+            mass += inc4[u];
           }
         }
       }
       if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
       __syncthreads();
       const bool fits = s_ovf == 0u;
-      __syncthreads();  // every thread has read s_ovf before a later attempt resets it
-      if (!fits) continue;
-      level = ab == 4 ? 0 : 1;
+      __syncthreads();  // every thread has read s_ovf before the row passes reset it
+      if (fits) level = 0;
+    }
+    if (level == 0) {
       // read the image back: each sketch row's sum of squares (v_dot4 of its
-      // bytes, or of its low and high nibbles) as its rows leave for the slot
-      const int nq = (w * ab) >> 7;  // uint4 per sketch row
+      // low and high nibbles) as its rows leave for the slot
+      const uint4* l4 = reinterpret_cast<const uint4*>(lds);
+      const int nq = w >> 5;  // uint4 per 4-bit sketch row
       for (int d = 0; d < hp.depth; ++d) {
         uint32_t sq = 0;  // <= row mass * max counter < 2^32
         for (int j = tid; j < nq; j += kBuildThreads) {
@@ -683,13 +682,9 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
           const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (ab == 8) {
-              sq = __builtin_amdgcn_udot4(x[q], x[q], sq, false);
-            } else {
-              const uint32_t lo4 = x[q] & 0x0F0F0F0Fu, hi4 = (x[q] >> 4) & 0x0F0F0F0Fu;
-              sq = __builtin_amdgcn_udot4(lo4, lo4, sq, false);
-              sq = __builtin_amdgcn_udot4(hi4, hi4, sq, false);
-            }
+            const uint32_t lo4 = x[q] & 0x0F0F0F0Fu, hi4 = (x[q] >> 4) & 0x0F0F0F0Fu;
+            sq = __builtin_amdgcn_udot4(lo4, lo4, sq, false);
+            sq = __builtin_amdgcn_udot4(hi4, hi4, sq, false);
           }
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
           if (false)
@@ -700,9 +695,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
         if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
       }
     }
-    // both images overflowed (or u8 had no room): one sketch row at a time,
-    // u16 (u8 first when the u8 image was not tried)
-    if (level < 0) level = all8 ? 2 : 1;
+    // the 4-bit image overflowed: one sketch row at a time, u8 then u16
+    if (level < 0) level = 1;
     else level = -level - 1;  // done: mark so the row passes are skipped
     for (;;) {
       if (level < 0) break;  // an all-rows image held every counter
@@ -1045,10 +1039,7 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
   // eight keys per thread per step; the next step's eight loads are issued
   // before this step's keys are hashed, so a key load's latency is hidden
   // behind the previous keys' d x 8 hashes and LDS adds
-#ifndef CMS_SLICE_KPER
-#define CMS_SLICE_KPER 8
-#endif
-  constexpr int kPer = CMS_SLICE_KPER;
+  constexpr int kPer = 8;  // (4: the same time, profiles/r04/ab_*_s5)
   constexpr int64_t kStep = kPer * kSliceThreads;
   uint64_t nx[kPer];
   auto fetch = [&](int64_t base) {
@@ -1274,21 +1265,11 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
                          h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0);
       // the u8 all-rows image when a [d][w] byte image fits 64 KB (config 3: 40 KB)
-#ifndef CMS_MID_ALL8
-#define CMS_MID_ALL8 1
-#endif
-      const int all8 = CMS_MID_ALL8 && (size_t)h->dw <= 64 * 1024 ? 1 : 0;
-      const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, all8 ? (size_t)h->dw : (size_t)h->dw / 2);
-      static bool mid_attr = [] {
-        (void)hipFuncSetAttribute((const void*)k_build_mid<kBuildStoreForm>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  64 * 1024);
-        return true;
-      }();
-      (void)mid_attr;
+      const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, (size_t)h->dw / 2);
       hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
                          dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
-                         h->d_rowmax, h->d_flags, all8);
+                         h->d_rowmax, h->d_flags);
       hipLaunchKernelGGL(k_build_bytes<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)),
                          dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,
                          h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);
