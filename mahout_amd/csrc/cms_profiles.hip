@@ -277,13 +277,17 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
 // the candidates grouped by their shape class (w, d): every member of a class
 // hashes u1's preferences identically (CosineCM.java:86 builds u1 at u2's
 // (delta, epsilon)), so a workgroup holds up to kPoGroupMax members' own
-// sketches in LDS and each of its waves takes one query at a time -- u1's
-// preferences are hashed ONCE per sketch row and gathered from every member's
-// row (valueAB, exact integers accumulated in fp64: each term and partial sum
-// is below 2^53 whenever both norms are), while a per-wave bucket row gives
-// valueA with the exchange pass of k_po_pairs.  Pairs past the exact regime
-// (a norm >= 2^53) are listed for k_po_pairs' sequential replay.
-constexpr int kPoGroupMax = 16;            // members per narrow group (fp64 accumulators per lane)
+// sketches in LDS (with their sqrt norms) and each of its waves takes one
+// query at a time.  Per sketch row, u1's preferences are hashed ONCE, 64 at a
+// time: lane k hashes preference k into the wave's bucket row (valueA by the
+// exchange pass of k_po_pairs) and parks (bucket, increment) in LDS; then
+// lane (m, part) gathers member m's counters at a quarter of the parked
+// buckets (valueAB, exact integers accumulated in fp64: each term and partial
+// sum is below 2^53 whenever both norms are), two shuffles sum the quarters,
+// and lane m takes member m's row cosine and running Math.min -- no per-member
+// reductions, no per-member global loads in the loop.  Pairs past the exact
+// regime (a norm >= 2^53) are listed for k_po_pairs' sequential replay.
+constexpr int kPoGroupMax = 16;            // members per narrow group (lanes m of a quarter-wave)
 constexpr int kPoGroupLds = 48 * 1024;     // LDS for a group's own sketches
 constexpr int kPoGroupHistW = 2048;        // narrow classes: one LDS bucket row per wave
 constexpr int kPoGroupWaves = 4;
@@ -307,10 +311,12 @@ struct PoAllArgs {
   int32_t weighted;
 };
 
-__device__ __forceinline__ double po_wave_sum_f64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// LDS of a group workgroup: sketches [cnt][d][w] u32, bucket rows [waves][w]
+// u32, parked (bucket, increment) [waves][64] x 2 u32, member sqrt norms
+// [kPoGroupMax][CMS_MAX_DEPTH] f64 (-1: norm >= 2^53), member rows [kPoGroupMax]
+__host__ __device__ constexpr size_t po_group_lds(int cnt, int w, int d) {
+  return (((size_t)cnt * d * w + (size_t)kPoGroupWaves * w + 2 * kPoGroupWaves * 64 + 1) & ~(size_t)1) * 4 +
+         (size_t)kPoGroupMax * CMS_MAX_DEPTH * 8 + kPoGroupMax * 8;
 }
 
 __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs a, HashParams hp) {
@@ -319,35 +325,44 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
   const int w = g.w, d = g.d, cnt = g.cnt;
   const int dw = d * w;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  uint32_t* bl = lds;                           // [cnt][d][w] members' own sketches
-  uint32_t* hist = lds + cnt * dw + wv * w;     // this wave's bucket row
+  uint32_t* bl = lds;                                        // [cnt][d][w] members' own sketches
+  uint32_t* hist = bl + cnt * dw + wv * w;                   // this wave's bucket row
+  uint32_t* pj = bl + cnt * dw + kPoGroupWaves * w + wv * 128;  // parked buckets [64], increments [64]
+  uint32_t* pv = pj + 64;
+  double* msq = reinterpret_cast<double*>(bl + ((cnt * dw + kPoGroupWaves * w + kPoGroupWaves * 128 + 1) & ~1));
+  int64_t* mrow = reinterpret_cast<int64_t*>(msq + kPoGroupMax * CMS_MAX_DEPTH);
   for (int m = 0; m < cnt; ++m) {
-    const uint32_t* src = a.sk + a.shp[a.cmem[g.m0 + m]].soff;
-    for (int j = tid; j < dw; j += 64 * kPoGroupWaves) bl[m * dw + j] = src[j];
+    const PoShape sm = a.shp[a.cmem[g.m0 + m]];
+    for (int j = tid; j < dw; j += 64 * kPoGroupWaves) bl[m * dw + j] = a.sk[sm.soff + j];
+    if (tid < d) msq[m * CMS_MAX_DEPTH + tid] = a.norm[sm.roff + tid] < (1ULL << 53) ? a.nsq[sm.roff + tid] : -1.0;
   }
+  if (tid < cnt) mrow[tid] = a.cmem[g.m0 + tid];
   for (int j = tid; j < kPoGroupWaves * w; j += 64 * kPoGroupWaves) lds[cnt * dw + j] = 0u;
   __syncthreads();
+  const int mm = lane & (kPoGroupMax - 1), part = lane >> 4;  // gather lanes: member, quarter of the parked keys
   const int64_t qa = (int64_t)blockIdx.x * kPoQueryChunk, qb = min(a.qc, qa + kPoQueryChunk);
   for (int64_t q = qa + wv; q < qb; q += kPoGroupWaves) {
     const int64_t u1 = a.q0 + q;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
-    double minc[kPoGroupMax];
-#pragma unroll
-    for (int m = 0; m < kPoGroupMax; ++m) minc[m] = DBL_MAX;
-    uint32_t inexact = 0u;
+    double minc = DBL_MAX;  // lane m < cnt: member m's running Math.min
+    bool inexact = false;
     for (int r = 0; r < d; ++r) {
-      double acc[kPoGroupMax];
-#pragma unroll
-      for (int m = 0; m < kPoGroupMax; ++m) acc[m] = 0.0;
-      const uint32_t* brow = bl + r * w;
-      for (int64_t i = k0 + lane; i < k1; i += 64) {
-        const uint32_t j = bucket_wb(hp, r, a.kp[i], (uint32_t)w, g.barrett);
-        const uint32_t v = a.inc[i];
-        atomicAdd(&hist[j], v);
-        const double vd = (double)v;
-#pragma unroll
-        for (int m = 0; m < kPoGroupMax; ++m)
-          if (m < cnt) acc[m] = __fma_rn(vd, (double)brow[m * dw + j], acc[m]);
+      double acc = 0.0;
+      const uint32_t* brow = bl + mm * dw + r * w;
+      for (int64_t base = k0; base < k1; base += 64) {
+        const int64_t i = base + lane;
+        uint32_t j = 0, v = 0;
+        if (i < k1) {
+          j = bucket_wb(hp, r, a.kp[i], (uint32_t)w, g.barrett);
+          v = a.inc[i];
+          atomicAdd(&hist[j], v);
+        }
+        pj[lane] = j;
+        pv[lane] = v;  // (a wave's LDS operations execute in order: the parked pairs are read back below)
+        if (mm < cnt) {
+#pragma unroll 4
+          for (int t = part * 16; t < part * 16 + 16; ++t) acc = __fma_rn((double)pv[t], (double)brow[pj[t]], acc);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's adds land before its exchanges
       uint64_t a2 = 0;
@@ -356,28 +371,23 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
         a2 = sat_add(a2, (uint64_t)c * c);
       }
       a2 = po_wave_sum(a2);
-      const bool a_ok = a2 < (1ULL << 53);
-      const double sa = __dsqrt_rn((double)a2);
-#pragma unroll
-      for (int m = 0; m < kPoGroupMax; ++m) {
-        if (m >= cnt) continue;
-        const double ab = po_wave_sum_f64(acc[m]);
-        const int64_t ro = a.shp[a.cmem[g.m0 + m]].roff + r;
-        if (a_ok && a.norm[ro] < (1ULL << 53)) {
-          const double den = __dmul_rn(sa, a.nsq[ro]);
-          if (den != 0.0) minc[m] = java_min(minc[m], __ddiv_rn(ab, den));
+      acc += __shfl_xor(acc, 16, 64);  // the four quarters (exact: integers below 2^53)
+      acc += __shfl_xor(acc, 32, 64);
+      if (lane < cnt) {
+        const double sb = msq[lane * CMS_MAX_DEPTH + r];
+        if (a2 < (1ULL << 53) && sb >= 0.0) {
+          const double den = __dmul_rn(__dsqrt_rn((double)a2), sb);
+          if (den != 0.0) minc = java_min(minc, __ddiv_rn(acc, den));
         } else {
-          inexact |= 1u << m;
+          inexact = true;
         }
       }
     }
-#pragma unroll
-    for (int m = 0; m < kPoGroupMax; ++m) {
-      if (m >= cnt || lane != m) continue;
-      const int64_t u2 = a.cmem[g.m0 + m];
-      double res = minc[m] == DBL_MAX ? __builtin_nan("") : minc[m];
+    if (lane < cnt) {
+      const int64_t u2 = mrow[lane];
+      double res = minc == DBL_MAX ? __builtin_nan("") : minc;
       if (res == res) res = normalize_weight(res, a.weighted);
-      if ((inexact >> m) & 1u) {  // k_po_pairs replays the reference's sequential loop
+      if (inexact) {  // k_po_pairs replays the reference's sequential loop
         res = __builtin_nan("");
         const uint32_t slot = atomicAdd(a.redo_cnt, 1u);
         if (slot < a.redo_cap) a.redo[slot] = ((unsigned long long)u1 << 32) | (unsigned long long)u2;
@@ -570,7 +580,7 @@ static int po_build_groups(cms_handle* h) {
         g.cnt = cnt;
         for (int q = 0; q < cnt; ++q) cmem_n.push_back(ord[m + q]);
         narrow.push_back(g);
-        gmax = std::max<int32_t>(gmax, (int32_t)(cnt * img + (int64_t)kPoGroupWaves * w * 4));
+        gmax = std::max<int32_t>(gmax, (int32_t)po_group_lds(cnt, w, d));
       }
     } else {
       for (size_t m = i; m < e; ++m) cmem_w.push_back(ord[m]);
