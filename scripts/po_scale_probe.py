@@ -3,10 +3,13 @@ config-2 stream (1M users x 100K items, 50M pairs) as the transposed
 DataModel, CountMinSketchConfig(q=1) for all 100K items, then mostSimilar
 top-100 for blocks of query rows over all 100K candidates.
 
-usage: python scripts/po_scale_probe.py [rows_per_block]"""
+usage: python scripts/po_scale_probe.py [rows_per_block] [whole_job_budget_s]
+
+A heartbeat line goes to stderr every 30 s (a profiled run stays visibly alive)."""
 import json
 import os
 import sys
+import threading
 import time
 
 import torch
@@ -16,7 +19,17 @@ from bench import csr_on_device, per_owner_scale  # noqa: E402
 from mahout_amd.synth import zipf_stream_torch  # noqa: E402
 
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-items, users = zipf_stream_torch(1_000_000, 100_000, 50_000_000, seed=20261016, device="cuda")
+budget = float(sys.argv[2]) if len(sys.argv) > 2 else 120.0
 t0 = time.perf_counter()
-print(json.dumps(per_owner_scale(items, users, 100_000, 1_000_000, rows)), flush=True)
+
+
+def beat():
+    while True:
+        time.sleep(30)
+        print(f"... {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+
+threading.Thread(target=beat, daemon=True).start()
+items, users = zipf_stream_torch(1_000_000, 100_000, 50_000_000, seed=20261016, device="cuda")
+print(json.dumps(per_owner_scale(items, users, 100_000, 1_000_000, rows, budget)), flush=True)
 print(f"total {time.perf_counter() - t0:.1f} s", file=sys.stderr)
