@@ -1012,10 +1012,13 @@ def config2_line(args, rank, world, local, device):
         extras["allpairs_top100_cfg2_streaming"] = {
             "wall_s": dt, "unique_item_pair_cosines_per_s": n * (n - 1) / 2 / dt,
             "full_lists": int((cnt_all == 100).sum().item())}
-        # the reference's per-owner-shape mode at this scale
-        extras["per_owner_shapes_cfg2"] = per_owner_scale(items, users, n, c2.n_users)
         out["extras"] = extras
     table.close()
+    torch.cuda.empty_cache()
+    if "extras" in out:
+        # the reference's per-owner-shape mode at this scale (SURVEY 8(f) rank
+        # 2), on the same stream, with the fixed-shape table released first
+        out["extras"]["per_owner_shapes_cfg2"] = per_owner_scale(items, users, n, c2.n_users)
     del items, users
     torch.cuda.empty_cache()
     return out
