@@ -58,4 +58,46 @@ for rnd in ("first", "reuse"):
     for p in ptrs:
         ok(hip.hipFreeAsync(p, stream), "hipFreeAsync")
     ok(hip.hipStreamSynchronize(stream), "sync")
+# near capacity: hold most of the device, then time further allocations
+free_b = ctypes.c_size_t()
+total_b = ctypes.c_size_t()
+ok(hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b)), "meminfo")
+res["total_GB"] = total_b.value / 1e9
+hold = []
+while True:
+    ok(hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b)), "meminfo")
+    if free_b.value < (int(gb * (1 << 30)) + (40 << 30)):
+        break
+    p = ctypes.c_void_p()
+    ok(hip.hipMalloc(ctypes.byref(p), size), "hold")
+    hold.append(p)
+res["held_GB"] = len(hold) * gb * (1 << 30) / 1e9
+near = []
+t0 = time.perf_counter()
+for _ in range(count):
+    ok(hip.hipMemGetInfo(ctypes.byref(free_b), ctypes.byref(total_b)), "meminfo")
+    if free_b.value < int(gb * (1 << 30)) + (6 << 30):
+        break
+    p = ctypes.c_void_p()
+    ok(hip.hipMalloc(ctypes.byref(p), size), "near")
+    near.append(p)
+res["near_full_allocs"] = len(near)
+res["hipMalloc_near_full_ms_per_GB"] = (time.perf_counter() - t0) * 1e3 / (gb * max(1, len(near)))
+for p in near + hold:
+    ok(hip.hipFree(p), "free")
+# while the device is busy: ~0.5 s of matmuls queued on torch's stream first
+import torch  # noqa: E402
+a = torch.randn(8192, 8192, device="cuda")
+torch.cuda.synchronize()
+for _ in range(40):
+    a = a @ a
+    a /= a.abs().max()
+p = ctypes.c_void_p()
+t0 = time.perf_counter()
+ok(hip.hipMalloc(ctypes.byref(p), size), "busy")
+res["hipMalloc_busy_ms"] = (time.perf_counter() - t0) * 1e3
+t0 = time.perf_counter()
+torch.cuda.synchronize()
+res["queue_left_after_malloc_ms"] = (time.perf_counter() - t0) * 1e3
+ok(hip.hipFree(p), "free")
 print(json.dumps(res))
