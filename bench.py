@@ -644,6 +644,9 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
                                                          "cosine_mfma_multi", "topk_all_waves", "topk_merge",
                                                          "host_alloc", "host_free"]}
     first_scopes["host_alloc_GB"] = t.timing("host_alloc_bytes")[0] / 1e9  # bytes the first job allocated
+    mx_ms, mx_bytes = t.timing("host_alloc_max")
+    first_scopes["host_alloc_max_ms"] = mx_ms
+    first_scopes["host_alloc_max_GB"] = mx_bytes / 1e9
     t.reset_timing()
     bar()
     t0 = time.perf_counter()

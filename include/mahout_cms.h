@@ -431,7 +431,8 @@ int cms_set_timing(cms_handle* h, int32_t enabled);
  * host counters, whatever the timing switch (cleared by cms_reset_timing):
  * "host_alloc" = ms in the library's hipMalloc calls (launches = calls),
  * "host_free" = ms in the hipFree of a growing buffer (it waits for queued
- * device work), "host_alloc_bytes" = bytes allocated (in total_ms). */
+ * device work), "host_alloc_bytes" = bytes allocated (in total_ms),
+ * "host_alloc_max" = the slowest single hipMalloc (ms; its bytes in launches). */
 int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* launches);
 int cms_reset_timing(cms_handle* h);
 

@@ -37,7 +37,8 @@ int hip_fail(hipError_t e, const char* what) {
 // host time spent in device allocations (process-wide; cms_get_timing's
 // "host_alloc" scope): a first all-pairs job allocates its operand images and
 // candidate lists, tens of GB at config 4
-static std::atomic<int64_t> g_alloc_ns{0}, g_alloc_calls{0}, g_free_ns{0}, g_alloc_bytes{0};
+static std::atomic<int64_t> g_alloc_ns{0}, g_alloc_calls{0}, g_free_ns{0}, g_alloc_bytes{0}, g_alloc_max_ns{0},
+    g_alloc_max_bytes{0};
 
 static int64_t ns_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -56,7 +57,12 @@ hipError_t DevBuf::ensure(size_t need) {
   size_t alloc = std::max<size_t>(need, 256);
   const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(&ptr, alloc);
-  g_alloc_ns += ns_since(t0);
+  const int64_t dt = ns_since(t0);
+  g_alloc_ns += dt;
+  if (dt > g_alloc_max_ns.load()) {  // the slowest single allocation (diagnostic; races only blur it)
+    g_alloc_max_ns = dt;
+    g_alloc_max_bytes = (int64_t)alloc;
+  }
   ++g_alloc_calls;
   if (e == hipSuccess) {
     bytes = alloc;
@@ -1562,6 +1568,11 @@ int cms_get_timing(cms_handle* h, const char* name, double* total_ms, int64_t* l
     *launches = g_alloc_calls.load();
     return CMS_OK;
   }
+  if (std::strcmp(name, "host_alloc_max") == 0) {  // the slowest single hipMalloc: ms, and its bytes in launches
+    *total_ms = (double)g_alloc_max_ns.load() * 1e-6;
+    *launches = g_alloc_max_bytes.load();
+    return CMS_OK;
+  }
   if (std::strcmp(name, "host_free") == 0) {  // process-wide host time in the hipFree of a growing buffer
     *total_ms = (double)g_free_ns.load() * 1e-6;
     *launches = 0;
@@ -1582,6 +1593,8 @@ int cms_reset_timing(cms_handle* h) {
   g_alloc_calls = 0;
   g_free_ns = 0;
   g_alloc_bytes = 0;
+  g_alloc_max_ns = 0;
+  g_alloc_max_bytes = 0;
   return rc;
 }
 
