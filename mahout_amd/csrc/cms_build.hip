@@ -550,13 +550,18 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 // of the nibbles) as it is stored.  The u8 / u16 attempts go one sketch row
 // at a time (a w- or 2w-byte image), the returning LDS adds giving each
 // row's sum of squares.  A persistent grid walks the device-side list.
+// mid owners of up to this many keys (the register-cached ones) may be list rows
+#ifndef CMS_MID_LIST_KEYS
+#define CMS_MID_LIST_KEYS (kBuildThreads * kKeyRegs)
+#endif
+constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
 template <int SV>
 // 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
 // (it spilled there); the build measured the same (profiles/r04/ab_*_s5)
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
-    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags) {
+    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int list_keys) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -591,6 +596,20 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       }
     }
     uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's slot (64-B aligned)
+    // a LIST row (cms_internal.h kFormList) when the owner's keys sit in
+    // registers, increments are units, and the list beats even the 4-bit row:
+    // the counting below then only yields the norms and the maximum, and the
+    // keys' buckets leave instead of the image (u16 counters -- a count past
+    // 255 -- keep the dense row)
+    const int64_t m = hi - lo;
+    const bool as_list = cached && m <= list_keys && vals == nullptr && hp.frac_bits == 0 &&
+                         (int64_t)hp.depth * m <= 8192 && 2 + 2 * (int64_t)hp.depth * m < (int64_t)hp.depth * w / 2;
+    uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;
+    auto write_list_row = [&](int d) {  // the cached keys' buckets in sketch row d
+#pragma unroll
+      for (int k = 0; k < kKeyRegs; ++k)
+        if (ik[k]) lst[1 + (int64_t)d * m + tid + k * kBuildThreads] = (uint16_t)bucket(hp, d, kp[k]);
+    };
     int level = -1;  // the form that holds the owner: 0 4-bit, 1 u8, 2 u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
     // ALL sketch rows in one key pass in a [d][w] 4-bit image.  (A [d][w] u8
@@ -689,10 +708,11 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
           if (false)
 #endif
-          store_row(d4 + d * nq + j, v, SV);
+          if (!as_list) store_row(d4 + d * nq + j, v, SV);
         }
         sq = wave_sum_u32(sq);
         if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+        if (as_list) write_list_row(d);
       }
     }
     // the 4-bit image overflowed: one sketch row at a time, u8 then u16
@@ -762,7 +782,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
         if (false)
 #endif
-        for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + d * nq + j, l4[j], SV);
+        if (as_list && level == 1) write_list_row(d);
+        else for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + d * nq + j, l4[j], SV);
         __syncthreads();  // the image is read out before the next sketch row zeroes it
       }
       if (!s_ovf || level == 2) break;
@@ -778,11 +799,13 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
     if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, (unsigned long long)mass);
     __syncthreads();
     if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+    const bool listed = as_list && level <= 1;
     if (tid == 0) {
       rowmax[row] = s_max;
       row_mass[row] = s_mass;
       if (s_mass >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
-      hidx_w[row] = level == 0 ? kFormU4 : level == 1 ? kFormU8 : kFormU16;
+      if (listed) lst[0] = (uint16_t)m;
+      hidx_w[row] = listed ? kFormList : level == 0 ? kFormU4 : level == 1 ? kFormU8 : kFormU16;
       cbound[row] = s_max;
     }
     __syncthreads();  // shared sums consumed before the next owner
@@ -1269,7 +1292,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
                          dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
-                         h->d_rowmax, h->d_flags);
+                         h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);
       hipLaunchKernelGGL(k_build_bytes<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)),
                          dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,
                          h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);

@@ -326,6 +326,7 @@ __global__ __launch_bounds__(256) void k_norms(TableView tv, int64_t nrows, Hash
                                                uint32_t* rowmax) {
   __shared__ uint64_t red[4];
   __shared__ uint32_t smax[4];
+  extern __shared__ uint32_t lc[];  // [w / 4]: a list row's sketch row as u8 counters
   const int w = (int)hp.width;
   for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
     uint32_t vmax = 0;
@@ -334,14 +335,18 @@ __global__ __launch_bounds__(256) void k_norms(TableView tv, int64_t nrows, Hash
     for (int d = 0; d < hp.depth; ++d) {
       const int64_t c0 = (int64_t)d * w;
       uint64_t sq = 0;
-      if (list) {  // sum_j c_j^2 = sum over entries t of the count of t's bucket
+      if (list) {  // the sketch row counted in LDS (u8 counters, four per word: a list row's are < 2^8)
         const uint16_t* e = tv.list_row(row, d, lm);
-        for (uint32_t t = threadIdx.x; t < lm; t += blockDim.x) {
-          uint32_t c = 0;
-          for (uint32_t u = 0; u < lm; ++u) c += e[u] == e[t];
-          sq += c;
-          vmax = max(vmax, c);
+        for (int j = threadIdx.x; j < (w >> 2); j += blockDim.x) lc[j] = 0u;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < lm; t += blockDim.x) atomicAdd(&lc[e[t] >> 2], 1u << ((e[t] & 3u) * 8u));
+        __syncthreads();
+        for (int j = threadIdx.x; j < (w >> 2); j += blockDim.x) {
+          const uint32_t v = lc[j];
+          sq += __builtin_amdgcn_udot4(v, v, 0u, false);
+          vmax = max(vmax, max(max(v & 255u, (v >> 8) & 255u), max((v >> 16) & 255u, v >> 24)));
         }
+        __syncthreads();
       } else if ((w & 3) == 0) {
         for (int j = threadIdx.x; j < (w >> 2); j += blockDim.x) {
           const uint4 v = tv.get4(row, c0 + 4 * j);
@@ -383,7 +388,8 @@ __global__ void k_norm_sqrt(const uint64_t* norm, int64_t cells, double* out, ui
 int local_norms(cms_handle* h) {
   const unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
   if (grid > 0)
-    hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->n, h->hp, h->d_norm, h->d_rowmax);
+    hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), (size_t)h->p.width, h->stream, h->tview(), h->n, h->hp, h->d_norm,
+                       h->d_rowmax);
   CMS_HIP(hipGetLastError());
   h->norms_valid = true;
   return CMS_OK;
@@ -400,8 +406,8 @@ int compute_norms(cms_handle* h) {
   if (!h->norms_valid) {
     CMS_HIP(hipMemsetAsync(h->d_flags + 2, 0, sizeof(uint32_t), h->stream));
     unsigned grid = (unsigned)std::min<int64_t>(h->n, 65536);
-    if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), 0, h->stream, h->tview(), h->n, h->hp, h->d_norm,
-                                     h->d_rowmax);
+    if (grid > 0) hipLaunchKernelGGL(k_norms, dim3(grid), dim3(256), (size_t)h->p.width, h->stream, h->tview(), h->n,
+                                     h->hp, h->d_norm, h->d_rowmax);
     CMS_HIP(hipGetLastError());
     h->norms_valid = true;
   }

@@ -47,6 +47,7 @@ __global__ __launch_bounds__(256) void k_pair_cosine(TableView tv, const uint64_
                                                      HashParams hp, int64_t q_row, const int64_t* rows, int64_t m,
                                                      int64_t nrows, int weighted, double* out) {
   __shared__ uint64_t red[4];
+  extern __shared__ uint32_t lc[];  // [w / 4]: a list query row's sketch row as u8 counters (list x list pairs)
   const int64_t t = blockIdx.x;
   if (t >= m) return;
   const int64_t r2 = rows[t];
@@ -64,7 +65,18 @@ __global__ __launch_bounds__(256) void k_pair_cosine(TableView tv, const uint64_
     if (exact) {
       uint64_t dot = 0;
       const bool la = tv.hidx[q_row] == kFormList, lb = tv.hidx[r2] == kFormList;
-      if (la || lb) {  // valueAB = sum over a list row's entries of the other row's counter (update is linear)
+      if (la && lb) {  // the query's row counted in LDS, summed at the other list's entries
+        const uint32_t qm = tv.list_m(q_row), lm = tv.list_m(r2);
+        const uint16_t* qe = tv.list_row(q_row, d, qm);
+        const uint16_t* e = tv.list_row(r2, d, lm);
+        for (int j = threadIdx.x; j < (w >> 2); j += 256) lc[j] = 0u;
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < qm; t += 256) atomicAdd(&lc[qe[t] >> 2], 1u << ((qe[t] & 3u) * 8u));
+        __syncthreads();
+        const uint8_t* c8 = reinterpret_cast<const uint8_t*>(lc);
+        for (uint32_t t = threadIdx.x; t < lm; t += 256) dot += c8[e[t]];
+        __syncthreads();  // read before the next sketch row zeroes the counts
+      } else if (la || lb) {  // valueAB = sum over a list row's entries of the other row's counter (update is linear)
         const int64_t lr = lb ? r2 : q_row, other = lb ? q_row : r2;
         const uint32_t lm = tv.list_m(lr);
         const uint16_t* e = tv.list_row(lr, d, lm);
@@ -102,7 +114,7 @@ int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m,
   if (m <= 0) return CMS_OK;
   if (h->f64) return f64_pair_cosines(h, q_row, d_rows, m, d_out, s);
   TimedScope ts(h, "pair_cosine", s == nullptr);
-  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), 0, s ? s : h->stream, h->tview(), h->d_norm,
+  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), (size_t)h->p.width, s ? s : h->stream, h->tview(), h->d_norm,
                      h->d_norm_sqrt, h->hp, q_row, d_rows, m, h->n, (int)h->p.weighting, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;

@@ -227,3 +227,52 @@ def test_accumulate_build_zero_valued_form_rows(oracle, lists, w):
             ref = oracle.similarities_row(exp2, int(r))
             ref[r] = oracle.cosine_cm(exp2[r], exp2[r])
             assert _same(s1, ref), r
+
+
+def test_mid_class_list_rows(oracle):
+    """Mid-class owners (257..1024 keys, unit increments) whose key-bucket
+    list is smaller than their 4-bit row are stored as list rows by
+    k_build_mid (cms_build.hip): counters, point queries, similarities
+    (list x list included) and the all-pairs top-k equal the oracle and a
+    form-free handle; a batch then widens the touched list rows in place and
+    an accumulating CSR batch widens every touched one to u16."""
+    n, d, w = 2000, 4, 4096
+    items, users = _stream(n, 20000, 1_200_000, seed=21)
+    a, b = oracle.hash_params(42, d)
+    exp = oracle.build_table(n, d, w, a, b, items, users)
+    counts = np.bincount(items, minlength=n)
+    with _handle(n, d, w, True) as t, _handle(n, d, w, False) as plain:
+        for x in (t, plain):
+            x.ingest(items, users)
+            x.finalize()
+        st = t.stats()
+        mid = np.flatnonzero((counts > 256) & (counts <= 1024))
+        assert mid.size > 100 and st["list_rows"] > mid.size // 2, (mid.size, st)
+        assert st["stored_bytes"] < plain.stats()["stored_bytes"]
+        assert np.array_equal(t.read_counters(), exp)
+        for r in (int(mid[0]), int(mid[-1]), n - 1):
+            for key in (0, 1, 17, 19999, -3):
+                assert t.point_query(r, key) == oracle.sketch_get(exp[r], a, b, key)
+            s1 = t.similarities(r, np.arange(n))
+            ref = oracle.similarities_row(exp, r)
+            ref[r] = oracle.cosine_cm(exp[r], exp[r])
+            assert _same(s1, ref), r
+            assert _same(s1, plain.similarities(r, np.arange(n))), r
+        got = t.top_k_all(20)
+        want = plain.top_k_all(20)
+        assert all(np.array_equal(x, y, equal_nan=True) for x, y in zip(got, want))
+        # a small batch onto mid list rows: widened to the narrowest dense form
+        rng = np.random.Generator(np.random.PCG64(4))
+        br = rng.choice(mid, 5000).astype(np.int64)
+        bk = rng.integers(0, 20000, 5000).astype(np.int64)
+        for x in (t, plain):
+            x.ingest(br, bk)
+            x.finalize()
+        exp2 = oracle.build_table(n, d, w, a, b, np.concatenate([items, br]), np.concatenate([users, bk]))
+        assert t.stats()["list_rows"] < st["list_rows"]
+        assert np.array_equal(t.read_counters(), exp2)
+        r = int(br[0])
+        s1 = t.similarities(r, np.arange(n))
+        ref = oracle.similarities_row(exp2, r)
+        ref[r] = oracle.cosine_cm(exp2[r], exp2[r])
+        assert _same(s1, ref)
