@@ -605,11 +605,6 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
     const bool as_list = cached && m <= list_keys && vals == nullptr && hp.frac_bits == 0 &&
                          (int64_t)hp.depth * m <= 8192 && 2 + 2 * (int64_t)hp.depth * m < (int64_t)hp.depth * w / 2;
     uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;
-    auto write_list_row = [&](int d) {  // the cached keys' buckets in sketch row d
-#pragma unroll
-      for (int k = 0; k < kKeyRegs; ++k)
-        if (ik[k]) lst[1 + (int64_t)d * m + tid + k * kBuildThreads] = (uint16_t)bucket(hp, d, kp[k]);
-    };
     int level = -1;  // the form that holds the owner: 0 4-bit, 1 u8, 2 u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
     // ALL sketch rows in one key pass in a [d][w] 4-bit image.  (A [d][w] u8
@@ -632,9 +627,13 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       __syncthreads();
       bool ovf = false;
       vmax = 0;
-      auto add_all = [&](uint64_t kr, uint32_t inc) {
+      // lt >= 0: the key's list index -- a list row's entries leave during
+      // the count (a count past 255 later rewrites the slot as u16 rows)
+      auto add_all = [&](uint64_t kr, uint32_t inc, int64_t lt) {
         for (int d = 0; d < hp.depth; ++d) {
-          const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kr);
+          const uint32_t bk = bucket(hp, d, kr);
+          if (lt >= 0) lst[1 + (int64_t)d * m + lt] = (uint16_t)bk;
+          const uint32_t c = (uint32_t)d * (uint32_t)w + bk;
           const uint32_t sh = (c & ((1u << lga) - 1u)) * (uint32_t)ab;
           const uint32_t old = (atomicAdd(&lds[c >> lga], inc << sh) >> sh) & capa;
           const uint32_t nv = old + inc;
@@ -645,7 +644,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       if (cached) {
 #pragma unroll
         for (int k = 0; k < kKeyRegs; ++k)
-          if (ik[k]) add_all(kp[k], ik[k]);
+          if (ik[k]) add_all(kp[k], ik[k], as_list ? (int64_t)(tid + k * kBuildThreads) : int64_t(-1));
       } else {
         // the next step's key loads go out before this step's keys are added
         constexpr int64_t kStep = 4 * kBuildThreads;
@@ -678,7 +677,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
           if (base + kStep < hi) fetch(base + kStep);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            if (inc4[u]) add_all(keys.resolve(kk[u]), inc4[u]);
+            if (inc4[u]) add_all(keys.resolve(kk[u]), inc4[u], -1);
             mass += inc4[u];
           }
         }
@@ -712,7 +711,6 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
         }
         sq = wave_sum_u32(sq);
         if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
-        if (as_list) write_list_row(d);
       }
     }
     // the 4-bit image overflowed: one sketch row at a time, u8 then u16
@@ -782,8 +780,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
         if (false)
 #endif
-        if (as_list && level == 1) write_list_row(d);
-        else for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + d * nq + j, l4[j], SV);
+        if (!(as_list && level == 1))  // a list row's entries left in the 4-bit pass
+          for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + d * nq + j, l4[j], SV);
         __syncthreads();  // the image is read out before the next sketch row zeroes it
       }
       if (!s_ovf || level == 2) break;
