@@ -37,6 +37,11 @@
 #include "cms_internal.h"
 #include "cms_mfma.h"
 
+#ifndef CMS_SYM_PROBE
+// bound analysis builds only (build_lib.py --define), bit flags: 1 every
+// workgroup loads the same panels, 2 no row-boundary work, 4 no MFMAs
+#define CMS_SYM_PROBE 0
+#endif
 #ifndef CMS_SYM_SCHED
 // 0: refill loads before the MFMAs, 1: interleaved with them, 2: also the next
 // k-step's fragments, 3: the barrier between the two k-steps (f4 -4 %, i8 -6 % over 2)
@@ -71,6 +76,17 @@ __device__ __forceinline__ uint32_t block_map(int bx, int nblk) {
 __device__ __forceinline__ uint32_t xcd_chunk_map(int bx, int C) {
   const int q = bx >> 3;
   return (uint32_t)((q / C) * 8 * C + (bx & 7) * C + q % C);
+}
+
+template <int FMT>
+__device__ __forceinline__ typename AccOf<FMT>::type sym_mma(const i8x16& a, const i8x16& b,
+                                                             typename AccOf<FMT>::type c) {
+#if CMS_SYM_PROBE & 4  // bound analysis: the fragments are consumed, no MFMA issued
+  c[0] += (int)a[0] ^ (int)b[0];
+  return c;
+#else
+  return mfma_step<FMT>(a, b, c);
+#endif
 }
 
 template <int NSTAGE, int BK, int FMT, int NW>
@@ -170,10 +186,15 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   // ---- operand fills: K-blocked images, panels start on a kImgBlk block ----
   const int64_t recA = (a_rows + kImgBlk - 1) / kImgBlk * kImgBlk * rs;
   const int64_t recB = (b_rows + kImgBlk - 1) / kImgBlk * kImgBlk * rs;
+#if CMS_SYM_PROBE & 1  // bound analysis: every workgroup streams the image's first panels (L2-resident)
+  const int64_t a_img = 0, b_img = 0;
+#else
+  const int64_t a_img = a_pos0 - g.img0, b_img = b_pos0 - g.img0;
+#endif
   const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + (a_pos0 - g.img0) * rs), (short)0, (int)recA, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + a_img * rs), (short)0, (int)recA, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + (b_pos0 - g.img0) * rs), (short)0, (int)recB, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.img + b_img * rs), (short)0, (int)recB, 0x00020000);
   // instruction u of wave wid fills panel rows [(wid + NW u) RPI, +RPI); lane i
   // lands at byte 16 i (row (wid + 8u) RPI + i / CPR, slot i % CPR) and
   // fetches the chunk the XOR swizzle puts there
@@ -270,7 +291,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa0[i], fb0[j], acc[i][j]);
+        for (int j = 0; j < 3; ++j) acc[i][j] = sym_mma<FMT>(fa0[i], fb0[j], acc[i][j]);
 #pragma unroll
       for (int m = 0; m < TI * 3; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -290,7 +311,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa1[i], fb1[j], acc[i][j]);
+        for (int j = 0; j < 3; ++j) acc[i][j] = sym_mma<FMT>(fa1[i], fb1[j], acc[i][j]);
 #pragma unroll
       for (int m = 0; m < TI * 3; ++m) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -337,7 +358,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #pragma unroll
         for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
+          for (int j = 0; j < 3; ++j) acc[i][j] = sym_mma<FMT>(fa[i], fb[j], acc[i][j]);
         if (ks == 0) issue(sn, s + NSTAGE - 1, 1);
       }
       constexpr int NV = OPA + OPB_LO, NF = TI + 3, NM = TI * 3, KS = BK / 32;
@@ -377,12 +398,15 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma_step<FMT>(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < 3; ++j) acc[i][j] = sym_mma<FMT>(fa[i], fb[j], acc[i][j]);
     }
 #endif
 #endif  // CMS_SYM_SCHED == 3
     const int r = s / cstages;
     if (s - r * cstages != cstages - 1) continue;
+#if CMS_SYM_PROBE & 2  // bound analysis: no row-boundary screening / minimum
+    continue;
+#endif
     // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
     const double* sa_r = s_sa + r * kSA;
     const double* sb_r = s_sb + r * kSB;

@@ -26,15 +26,18 @@ while done < pairs:
 items = torch.cat([c[0] for c in chunks])
 users = torch.cat([c[1] for c in chunks])
 del chunks
+print("stream generated", file=sys.stderr, flush=True)
 t = SketchTable(n, depth=d, width=w, seed=42, device=0)
 t.ingest_device_rows(items, users, None, pairs)
 t.finalize()
 del items, users
 torch.cuda.empty_cache()
 t.release_scratch()
+print("table built", file=sys.stderr, flush=True)
 t0 = time.perf_counter()
 t.top_k_all(k)  # first call: the limb / fp4 operand images are prepared
 wall_first = time.perf_counter() - t0
+print("first job done", file=sys.stderr, flush=True)
 reps = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 walls = []
 for _ in range(reps):  # untimed kernels: the job's wall clock
