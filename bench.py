@@ -849,7 +849,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
             touched, redone, full = t.refresh_stats()
             periods.append({"after_batch": bi + 1, "finalize_s": round(fs, 5), "refresh_s": round(rs, 4),
                             "touched_owner_frac": touched / n, "lists_redone": redone, "whole_jobs": full,
-                            "scopes_ms": scopes()})
+                            "classes": t.refresh_classes(), "scopes_ms": scopes()})
     cnt = cnt.cpu().numpy()
     t.set_timing(False)
     del batches
@@ -858,6 +858,28 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     recomputed_rate = sum((1 - (1 - p["touched_owner_frac"]) ** 2) * all_pairs / p["refresh_s"]
                           for p in periods) / len(periods)
     whole_rate = all_pairs / keep_s
+
+    def class_work(p):
+        # The pairs a refresh must redo, per operand class, priced at the whole
+        # job's own per-pair time for that class: multi-limb rows (every pair
+        # with a multi-limb owner), int8 waves (int8 x int8 and int8 x fp4) and
+        # fp4 waves.  Touched owners are the frequent ones, so they sit in the
+        # costly classes: this is the refresh's time at the whole job's per-pair
+        # cost, class by class.
+        c = p["classes"]
+        (m, tm), (i8, ti), (f4, tf) = c["multi"], c["int8"], c["fp4"]
+        um, ui, uf = m - tm, i8 - ti, f4 - tf
+
+        def tri(x):
+            return x * (x - 1) / 2
+        frac = {"multi": 1 - (um * (ui + uf) + tri(um)) / max(1, m * (i8 + f4) + tri(m)),
+                "i8": 1 - (ui * uf + tri(ui)) / max(1, i8 * f4 + tri(i8)),
+                "f4": 1 - tri(uf) / max(1, tri(f4))}
+        scope = {"multi": "topk_all_multi_rows", "i8": "topk_all_waves_i8", "f4": "topk_all_waves_f4"}
+        whole_ms = {k: keep_scopes.get(v, 0.0) for k, v in scope.items()}
+        return frac, sum(whole_ms[k] * frac[k] for k in frac) / 1e3
+
+    class_fracs, expect = zip(*[class_work(p) for p in periods])
     return {
         "workload": f"config 5: a {total}-pair Zipf stream (10M pairs/s) into the resident {n}-item table in "
                     f"{bsize}-pair batches; then {nb} batches of {per_batch} pairs per GPU, every {every} batch(es) "
@@ -877,6 +899,12 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         # ... against the whole job's unique pairs per second (1.0: a refresh is as efficient per pair)
         "refresh_pair_rate_vs_whole_job": recomputed_rate / whole_rate,
         "refresh_vs_whole_job": keep_s / (sum(lat) / len(lat)),
+        # per class: the fraction of the class's pairs a refresh must redo, and the refresh time those pairs
+        # would take at the whole job's per-pair time for their class (1.0: the refresh redoes them as fast)
+        "refresh_class_pair_fracs": [{k: round(v, 4) for k, v in f.items()} for f in class_fracs],
+        "refresh_s_at_whole_job_class_rates": sum(expect) / len(expect),
+        "refresh_class_weighted_rate_vs_whole_job": (sum(expect) / len(expect)) / (sum(p["refresh_s"] for p in periods)
+                                                                                 / len(periods)),
         # the refresh latency in arrival intervals: one interval = the time one refresh batch (all ranks)
         # takes to arrive at 10M pairs/s (0.125 s per 1.25M-pair batch on one GPU, 1 s on eight)
         "batch_interval_s": per_batch * world / 10e6,
@@ -1213,6 +1241,7 @@ def summary(res):
             out.update({"cfg5_sustained_updates_per_s": _r(st.get("sustained_updates_per_s")),
                         "cfg5_refresh_latency_s": _r(st.get("refresh_latency_s")),
                         "cfg5_refresh_pair_rate_vs_whole_job": _r(st.get("refresh_pair_rate_vs_whole_job"), 3),
+                        "cfg5_refresh_class_weighted_rate": _r(st.get("refresh_class_weighted_rate_vs_whole_job"), 3),
                         "cfg5_whole_job_s": _r(st.get("keep_lists_whole_job_s"))})
         if cos.get("cpu_baseline"):
             out["cfg4_cpu_pairs_per_s"] = _r(cos["cpu_baseline"].get("value"))

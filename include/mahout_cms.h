@@ -308,6 +308,13 @@ int cms_top_k_refresh_device(cms_handle* h, int32_t k, int64_t* d_ids, double* d
 /* Statistics of the last cms_top_k_refresh: owners touched (num_owners for a
  * whole job), lists recomputed whole, whole jobs so far. */
 int cms_refresh_stats(cms_handle* h, int64_t* touched, int64_t* redone, int64_t* full_jobs);
+/* Operand classes of the last cms_top_k_refresh's all-pairs job: out6 =
+ * {multi-limb owners, int8 owners, fp4 owners, touched multi-limb, touched
+ * int8, touched fp4} (a whole job counts every owner as touched).  Each class
+ * has its own pair cost (k_cosine_mls limb passes, int8 and fp4 symmetric
+ * waves), so the work a refresh must redo follows from these six counts.
+ * Zeros for per-owner and fp64 handles (no operand classes). */
+int cms_refresh_classes(cms_handle* h, int64_t* out6);
 
 /* cms_top_k_all written as FileSimilarItemsWriter does
  * (T/impl/similarity/precompute/FileSimilarItemsWriter.java:50-61): one line

@@ -42,7 +42,7 @@ EXPORTS = [
     "cms_set_timing", "cms_get_timing", "cms_reset_timing",
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
     "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities", "cms_write_similarities_threshold",
-    "cms_comm_init_transport", "cms_read_counters_device", "cms_top_k_refresh", "cms_refresh_stats",
+    "cms_comm_init_transport", "cms_read_counters_device", "cms_top_k_refresh", "cms_refresh_stats", "cms_refresh_classes",
     "cms_top_k_all_device", "cms_top_k_refresh_device", "cms_set_hash_params",
 ]
 
@@ -140,6 +140,7 @@ _SIGS = {
     "cms_set_hash_params": (_int, [_vp, _vp, _vp, _i32]),
     "cms_top_k_refresh_device": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "cms_refresh_stats": (_int, [_vp, _vp, _vp, _vp]),
+    "cms_refresh_classes": (_int, [_vp, _vp]),
     "cms_read_counters": (_int, [_vp, _i64, _i64, _vp]),
     "cms_get_stats": (_int, [_vp, ctypes.POINTER(CmsStats)]),
     "cms_set_timing": (_int, [_vp, _i32]),

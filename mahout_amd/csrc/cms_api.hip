@@ -1255,6 +1255,11 @@ static int top_k_refresh_job(cms_handle* h, int32_t k, int64_t* o_ids, double* o
     if ((rc = top_k_all_job(h, D, h->rf_ids.as<int64_t>(), h->rf_sc.as<double>(), h->rf_cnt.as<int32_t>())))
       return rc;
     if ((rc = refresh_set_full(h))) return rc;
+    {
+      const int64_t nm = h->n_hot_limb, nf = h->n_f4;
+      const int64_t cls[6] = {nm, n - nm - nf, nf, nm, n - nm - nf, nf};
+      std::copy(cls, cls + 6, h->rf_stat_class);
+    }
     h->rf_stat_full += 1;
     h->rf_stat_touched = n;
     h->rf_stat_redo = 0;
@@ -1282,6 +1287,13 @@ static int top_k_refresh_job(cms_handle* h, int32_t k, int64_t* o_ids, double* o
       }
       h->rf_restrict = false;
       if (rc) return rc;
+      {  // touched owners per operand class (positions: multi-limb, int8, fp4)
+        const int64_t nm = h->n_hot_limb, nf = h->n_f4;
+        int64_t tm = 0;
+        for (int64_t r = 0; r < n; ++r) tm += touch[r] && h->h_inv[r] < nm;
+        const int64_t cls[6] = {nm, n - nm - nf, nf, tm, h->rf_t8, h->rf_t4};
+        std::copy(cls, cls + 6, h->rf_stat_class);
+      }
       CMS_HIP(h->rf_redo.ensure(sizeof(uint32_t) * ((size_t)n + 1)));
       uint32_t* redo = h->rf_redo.as<uint32_t>();
       {
@@ -1350,6 +1362,13 @@ int cms_refresh_stats(cms_handle* h, int64_t* touched, int64_t* redone, int64_t*
   *touched = h->rf_stat_touched;
   *redone = h->rf_stat_redo;
   *full_jobs = h->rf_stat_full;
+  return CMS_OK;
+}
+
+int cms_refresh_classes(cms_handle* h, int64_t* out6) {
+  if (!h || !out6) return set_error(CMS_E_PARAM, "null argument");
+  Guard g(h);
+  std::copy(h->rf_stat_class, h->rf_stat_class + 6, out6);
   return CMS_OK;
 }
 

@@ -290,6 +290,9 @@ struct cms_handle {
   bool rf_restrict = false;
   int64_t rf_t8 = 0, rf_t4 = 0, rf_s8 = 0;  // touched int8 / fp4 single-limb owners; int8-class size
   int64_t rf_stat_touched = 0, rf_stat_redo = 0, rf_stat_full = 0;
+  // owners of the last all-pairs job per operand class (multi-limb, int8,
+  // fp4) and, for an incremental refresh, how many of each were touched
+  int64_t rf_stat_class[6] = {0, 0, 0, 0, 0, 0};
   int64_t pairs_ingested = 0;
   int32_t exact_norms = 1;
 

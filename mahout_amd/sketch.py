@@ -381,6 +381,13 @@ class SketchTable:
         check(self._lib.cms_refresh_stats(self._h, *[ctypes.byref(x) for x in v]))
         return tuple(int(x.value) for x in v)
 
+    def refresh_classes(self):
+        """{class: (owners, touched)} of the last refresh's job, classes
+        "multi" (multi-limb), "int8" and "fp4" (cms_refresh_classes)."""
+        v = (ctypes.c_int64 * 6)()
+        check(self._lib.cms_refresh_classes(self._h, v))
+        return {c: (int(v[i]), int(v[3 + i])) for i, c in enumerate(("multi", "int8", "fp4"))}
+
     # -- per-owner shapes (CountMinSketchConfig) --
     @classmethod
     def per_owner_shapes(cls, num_owners, seed=42, weighted=False, device=-1, owner_ids=None, frac_bits=0):
