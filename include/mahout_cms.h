@@ -118,9 +118,7 @@ int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, i
  *   CMS_LIST_KEYS=<n>     ... of <= n keys, unit increments: sparse list rows (256; 0 = none)
  *   CMS_NO_HOT_ROUTING=1  the COO partition sends every owner through both passes
  *   CMS_NO_FP4=1          no e2m1 operand image: every single-limb pair on int8 MFMA
- *   CMS_NO_MLS=1          multi-limb slabs on the 128-row tile kernel instead of k_cosine_mls
- *   CMS_SYM_PHASE=<t>     symmetric-wave tiles start at the sketch row of the device clock's phase, t
- *                         100 MHz ticks per K stage (60; 0 = every tile starts at row 0) */
+ *   CMS_NO_MLS=1          multi-limb slabs on the 128-row tile kernel instead of k_cosine_mls */
 int cms_create(const cms_params* p, cms_handle** out);
 void cms_destroy(cms_handle* h);
 const char* cms_last_error(void);

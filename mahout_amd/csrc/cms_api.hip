@@ -342,7 +342,6 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");
     h->tune.mls = !flag("CMS_NO_MLS");
-    h->tune.sym_phase = std::max(0, num("CMS_SYM_PHASE", h->tune.sym_phase));
   }
   h->per_owner = per_owner;
   h->f64 = f64;

@@ -1607,7 +1607,6 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
           g.si = 8;  // 8 A blocks x 2 J chunks: fp4 waves -5 % against 4 x 4 (8 x 1, 16 x 2 within 1 %)
           g.sj = 2;
           g.xchunk = 32;  // the XCDs side by side (xcd_chunk_map): int8 waves -7%, fp4 waves unchanged
-          g.phase_ticks = h->tune.sym_phase;
           g.thr = cb.thr;
           g.ccnt = cb.ccnt;
           g.cidx = cb.cidx;

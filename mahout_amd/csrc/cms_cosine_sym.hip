@@ -159,18 +159,6 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   const int64_t rs = g.rs;
   const int cstages = g.kw / BK;
   const int total = depth * cstages;
-  // Sketch rows are independent until the minimum (order-free: the running
-  // minimum keeps equal values either way, the screening is per row), so a
-  // tile may walk them from any row.  Every tile starts at the row the device
-  // clock's phase names: tiles that started at different times then walk K
-  // within a row of each other, and tiles sharing a panel find its stages in
-  // L2 instead of each pulling the panel from HBM at its own K offset.
-  int koff0 = 0, r0 = 0;
-  if (g.phase_ticks > 0) {
-    r0 = (int)((wall_clock64() / ((uint64_t)g.phase_ticks * (uint64_t)cstages)) % (uint64_t)depth);
-    koff0 = __builtin_amdgcn_readfirstlane(r0 * cstages);
-    r0 = __builtin_amdgcn_readfirstlane(r0);
-  }
 
   // sqrt norms of the panels' owners by LDS-DMA (256 B = 32 doubles per
   // instruction; past-the-end owners land as zeros), thresholds as fp16
@@ -222,8 +210,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   // stage s's data into ring slot `slot`; `part` 1: the loads every wave
   // issues, 2: the extra B load of waves < RB % NW, 3: both
   auto issue = [&](int s, int slot, int part) {
-    const int ks = s + koff0 < total ? s + koff0 : s + koff0 - total;  // the rotated K stage
-    const int32_t koff = ks * (kImgBlk * BK);
+    const int32_t koff = s * (kImgBlk * BK);
     unsigned char* st = lds + (slot % NSTAGE) * kStage;
     if (part & 1) {
 #pragma unroll
@@ -415,9 +402,8 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
     }
 #endif
 #endif  // CMS_SYM_SCHED == 3
-    const int rs_ = s / cstages;
-    if (s - rs_ * cstages != cstages - 1) continue;
-    const int r = rs_ + r0 < depth ? rs_ + r0 : rs_ + r0 - depth;  // the sketch row just completed
+    const int r = s / cstages;
+    if (s - r * cstages != cstages - 1) continue;
 #if CMS_SYM_PROBE & 2  // bound analysis: no row-boundary screening / minimum
     continue;
 #endif

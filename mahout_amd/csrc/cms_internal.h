@@ -201,8 +201,6 @@ struct Tunables {
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
   bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)
   bool mls = true;         // CMS_NO_MLS=1: multi-limb slabs on the 128-tile kernel instead of k_cosine_mls
-  int sym_phase = 60;      // CMS_SYM_PHASE: symmetric-wave tiles start at the sketch row of the clock's phase,
-                           // this many 100 MHz ticks per K stage; 0: every tile starts at row 0
 };
 }  // namespace cms
 
@@ -605,7 +603,6 @@ struct SymArgs {
   int32_t cap;
   int32_t rbits;  // bits of the sketch-row index in the packed running-min state
   int32_t xchunk; // > 0: runs of xchunk consecutive tiles per XCD, the 8 XCDs side by side (0: one contiguous range per XCD)
-  int32_t phase_ticks;  // > 0: a tile starts at the sketch row the device clock's phase names (ticks per stage)
 };
 // the kernel can run this table's waves (unweighted, its exact dot fits the
 // packed state, LDS budget); fmt 0 int8, 1 fp4

@@ -10,7 +10,6 @@ for arm in $ARMS; do
   envs=()
   case "$arm" in
     main) tag=main ;;
-    env:*) envs=("${arm#env:}"); tag=$(echo "${arm#env:}" | tr '=' '_') ;;
     *) envs=(MAHOUT_CMS_LIB="$PWD/$arm"); tag=$(basename "$arm" .so) ;;
   esac
   env "${envs[@]}" timeout -k 10 240 python -u scripts/cos_job_probe.py 1000000 500000000 8192 100 0 \
