@@ -244,6 +244,9 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         st[i][j][e] = kEmpty;
       }
   const uint32_t rbits = (uint32_t)g.rbits, rmask = (1u << rbits) - 1u;
+#if CMS_SYM_PROBE & 2
+  float probe_sink = 0.0f;
+#endif
 
   // the five fragments of k-step ks of a stage
   auto frags = [&](const unsigned char* A, int ks, i8x16* fa, i8x16* fb) {
@@ -404,7 +407,11 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #endif  // CMS_SYM_SCHED == 3
     const int r = s / cstages;
     if (s - r * cstages != cstages - 1) continue;
-#if CMS_SYM_PROBE & 2  // bound analysis: no row-boundary screening / minimum
+#if CMS_SYM_PROBE & 2  // bound analysis: no row-boundary screening / minimum (the MFMAs stay live)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) probe_sink += (float)acc[i][j][0];
     continue;
 #endif
     // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
@@ -465,6 +472,9 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   }
 #if CMS_SYM_SCHED
   wait_vmcnt<0>();  // the repeat loads land before the workgroup's LDS is released
+#endif
+#if CMS_SYM_PROBE & 2
+  if (probe_sink == 1234.5f) g.ccnt[tid] = 7u;  // never true in practice: keeps the sums (and MFMAs) live
 #endif
 
   // ---- the exact value of each surviving pair, offered to both lists ----
