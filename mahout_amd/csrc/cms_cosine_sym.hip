@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cmath>
 
 #include "cms_device.h"
 #include "cms_internal.h"
@@ -420,7 +421,50 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
     uint32_t any_alive = 0u;
 #pragma unroll
     for (int w = 0; w < NAW; ++w) any_alive |= alive[w];
-    if (__any(any_alive != 0u)) {
+    if constexpr (FMT == 1) {
+      // fp4: the running minimum is kept as its fp32 estimate (low rbits of
+      // the mantissa replaced by the row), from which the exact dot AB* is
+      // recovered at the end (sym_eligible bounds the error below 1/2).  So a
+      // row boundary needs no LDS lookups of the state's row and runs
+      // branch-free over the 96 outputs; only near ties (within 2^-17) take
+      // the exact fp64 comparison, in a second pass few waves enter.
+      if (__any(any_alive != 0u)) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int col = wc * 96 + j * 32 + (lane & 31);
+          const double sb = sb_r[col];
+          const float rb = __builtin_amdgcn_rcpf((float)sb);
+          const float tb = __half2float(s_tb[col]);
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int bit = (i * 3 + j) * 16 + e;
+              const uint32_t m = 1u << (bit & 31);
+              if (!(alive[bit >> 5] & m)) continue;
+              const int row = wr * WROWS + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+              const double sa = sa_r[row];
+              if (sa == 0.0 || sb == 0.0) continue;  // den == 0: this sketch row does not qualify
+              const float est = (float)acc[i][j][e] * __builtin_amdgcn_rcpf((float)sa) * rb;
+              if (est < fminf(__half2float(s_ta[row]), tb) - 4e-6f) {  // can never be admitted
+                alive[bit >> 5] &= ~m;
+                continue;
+              }
+              uint32_t& sv = st[i][j][e];
+              const float est0 = __uint_as_float(sv & ~rmask);  // NaN when empty
+              bool take = sv == kEmpty || est < est0 * (1.0f - 0x1p-17f);
+              if (!take && est <= est0 * (1.0f + 0x1p-17f)) {  // too close for fp32: the exact values
+                const int rr = (int)(sv & rmask);
+                const double sa0 = s_sa[rr * kSA + row], sb0 = s_sb[rr * kSB + col];
+                const double v = __ddiv_rn((double)acc[i][j][e], __dmul_rn(sa, sb));
+                const double v0 = __ddiv_rn(rint((double)est0 * sa0 * sb0), __dmul_rn(sa0, sb0));
+                take = v < v0;
+              }
+              if (take) sv = (__float_as_uint(est) & ~rmask) | (uint32_t)r;
+            }
+        }
+      }
+    } else if (__any(any_alive != 0u)) {
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int col = wc * 96 + j * 32 + (lane & 31);
@@ -496,7 +540,10 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         const int64_t ap = a_pos0 + row;
         if (ap == bp || (diag && ap > bp)) continue;
         const int rr = (int)(sv & rmask);
-        double v = __ddiv_rn((double)(sv >> rbits), __dmul_rn(s_sa[rr * kSA + row], s_sb[rr * kSB + col]));
+        const double sa = s_sa[rr * kSA + row], sb = s_sb[rr * kSB + col];
+        // the exact dot: packed (int8), or recovered from the fp32 estimate (fp4)
+        const double ab = FMT == 1 ? rint((double)__uint_as_float(sv & ~rmask) * sa * sb) : (double)(sv >> rbits);
+        double v = __ddiv_rn(ab, __dmul_rn(sa, sb));
         if (v > 1.0) v = 1.0;  // normalizeWeightResult, unweighted (values are >= 0)
         if (v >= g.thr[ap]) {
           const uint32_t slot = atomicAdd(&g.ccnt[ap], 1u);
@@ -543,6 +590,11 @@ bool sym_eligible(cms_handle* h, int fmt, int32_t* rbits) {
   // largest exact dot of one sketch row: fp4 counters <= 4, int8 limbs <= 127
   const double max_ab = (fmt == 1 ? 16.0 : 16129.0) * (double)h->p.width;
   *rbits = rb;
+  // fp4 keeps the running minimum as an fp32 estimate with its low rb mantissa
+  // bits replaced by the row: relative error <= 2^-21 (two rcp, two products)
+  // + 2^(rb-23) (the replaced bits); the dot recovered from it is exact while
+  // max_ab times that error stays below 1/2
+  if (fmt == 1 && max_ab * (std::ldexp(1.0, -21) + std::ldexp(1.0, rb - 23)) >= 0.5) return false;
   return h->p.weighting != CMS_WEIGHTED && max_ab < (double)((1ULL << (32 - rb)) - 1) &&
          sym_lds_bytes(h->p.depth) <= 160 * 1024 && (h->p.width % (fmt == 1 ? 2 * kSymBK : kSymBK)) == 0;
 }
