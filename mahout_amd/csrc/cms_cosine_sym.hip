@@ -245,6 +245,15 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         st[i][j][e] = kEmpty;
       }
   const uint32_t rbits = (uint32_t)g.rbits, rmask = (1u << rbits) - 1u;
+  // The running minimum of an output (kEmpty: no row qualified yet) is kept
+  // in one of two forms.  Estimate form (bit 31 clear): the fp32 estimate
+  // AB*/(sa* sb*) with its low rbits mantissa bits replaced by the row r*;
+  // its relative error is <= 2^-21 (two rcp, two products) + 2^(rbits-23),
+  // so AB* = rint(est * sa* * sb*) is exact while AB* <= ab_est_max, and a
+  // row boundary compares against it without looking row r* up.  Exact form
+  // (bit 31 set): AB* << rbits | r*, for larger dots (int8 rows; fp4 rows
+  // always take the estimate form, sym_eligible checks their bound).
+  const float ab_est_max = floorf(0.5f / (0x1p-21f + __builtin_ldexpf(1.0f, (int)rbits - 23)));
 #if CMS_SYM_PROBE & 2
   float probe_sink = 0.0f;
 #endif
@@ -464,7 +473,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
             }
         }
       }
-    } else if (__any(any_alive != 0u)) {
+    } else if (__any(any_alive != 0u)) {  // int8: estimate or exact form
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const int col = wc * 96 + j * 32 + (lane & 31);
@@ -472,7 +481,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         const float rb = __builtin_amdgcn_rcpf((float)sb);
         const float tb = __half2float(s_tb[col]);
 #pragma unroll
-        for (int i = 0; i < TI; ++i) {
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int bit = (i * 3 + j) * 16 + e;
@@ -491,20 +500,25 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
             bool take = sv == kEmpty;
             if (!take) {
               const int rr = (int)(sv & rmask);
-              const uint32_t ab0 = sv >> rbits;
-              const double sa0 = s_sa[rr * kSA + row], sb0 = s_sb[rr * kSB + col];
-              const float est0 = (float)ab0 * __builtin_amdgcn_rcpf((float)sa0) * __builtin_amdgcn_rcpf((float)sb0);
+              float est0;
+              if (!(sv >> 31)) {
+                est0 = __uint_as_float(sv & ~rmask);  // estimate form: no lookup of row rr
+              } else {
+                est0 = (float)((sv & 0x7FFFFFFFu) >> rbits) * __builtin_amdgcn_rcpf((float)s_sa[rr * kSA + row]) *
+                       __builtin_amdgcn_rcpf((float)s_sb[rr * kSB + col]);
+              }
               if (est < est0 * (1.0f - 0x1p-17f)) {
                 take = true;
               } else if (est <= est0 * (1.0f + 0x1p-17f)) {  // too close for fp32: the exact values
-                const double v = __ddiv_rn((double)ab, __dmul_rn(sa, sb));
-                const double v0 = __ddiv_rn((double)ab0, __dmul_rn(sa0, sb0));
-                take = v < v0;
+                const double sa0 = s_sa[rr * kSA + row], sb0 = s_sb[rr * kSB + col];
+                const double ab0 =
+                    (sv >> 31) ? (double)((sv & 0x7FFFFFFFu) >> rbits) : rint((double)est0 * sa0 * sb0);
+                take = __ddiv_rn((double)ab, __dmul_rn(sa, sb)) < __ddiv_rn(ab0, __dmul_rn(sa0, sb0));
               }
             }
-            if (take) sv = (ab << rbits) | (uint32_t)r;
+            if (take) sv = (float)ab <= ab_est_max ? (__float_as_uint(est) & ~rmask) | (uint32_t)r
+                                                                 : 0x80000000u | (ab << rbits) | (uint32_t)r;
           }
-        }
       }
     }
 #pragma unroll
@@ -541,8 +555,9 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         if (ap == bp || (diag && ap > bp)) continue;
         const int rr = (int)(sv & rmask);
         const double sa = s_sa[rr * kSA + row], sb = s_sb[rr * kSB + col];
-        // the exact dot: packed (int8), or recovered from the fp32 estimate (fp4)
-        const double ab = FMT == 1 ? rint((double)__uint_as_float(sv & ~rmask) * sa * sb) : (double)(sv >> rbits);
+        // the exact dot: packed, or recovered from the fp32 estimate
+        const double ab = (FMT == 0 && (sv >> 31)) ? (double)((sv & 0x7FFFFFFFu) >> rbits)
+                                                   : rint((double)__uint_as_float(sv & ~rmask) * sa * sb);
         double v = __ddiv_rn(ab, __dmul_rn(sa, sb));
         if (v > 1.0) v = 1.0;  // normalizeWeightResult, unweighted (values are >= 0)
         if (v >= g.thr[ap]) {
@@ -590,12 +605,12 @@ bool sym_eligible(cms_handle* h, int fmt, int32_t* rbits) {
   // largest exact dot of one sketch row: fp4 counters <= 4, int8 limbs <= 127
   const double max_ab = (fmt == 1 ? 16.0 : 16129.0) * (double)h->p.width;
   *rbits = rb;
-  // fp4 keeps the running minimum as an fp32 estimate with its low rb mantissa
-  // bits replaced by the row: relative error <= 2^-21 (two rcp, two products)
-  // + 2^(rb-23) (the replaced bits); the dot recovered from it is exact while
-  // max_ab times that error stays below 1/2
+  // the exact form of the running minimum packs AB* << rb | r* below bit 31;
+  // fp4 rows keep the estimate form only: relative error <= 2^-21 (two rcp,
+  // two products) + 2^(rb-23) (the replaced bits), and the dot recovered from
+  // it is exact while max_ab times that error stays below 1/2
   if (fmt == 1 && max_ab * (std::ldexp(1.0, -21) + std::ldexp(1.0, rb - 23)) >= 0.5) return false;
-  return h->p.weighting != CMS_WEIGHTED && max_ab < (double)((1ULL << (32 - rb)) - 1) &&
+  return h->p.weighting != CMS_WEIGHTED && max_ab < (double)((1ULL << (31 - rb)) - 1) &&
          sym_lds_bytes(h->p.depth) <= 160 * 1024 && (h->p.width % (fmt == 1 ? 2 * kSymBK : kSymBK)) == 0;
 }
 
