@@ -79,6 +79,20 @@ __device__ __forceinline__ uint32_t xcd_chunk_map(int bx, int C) {
   return (uint32_t)((q / C) * 8 * C + (bx & 7) * C + q % C);
 }
 
+// Row cosines as the reference forms them: v = AB / (sa * sb), both fp64
+// operations rounded (DoubleCountMinSketch.java:139-147).  Whether v < v0
+// without the two divisions: rounding is monotonic, so AB / D < AB0 / D0
+// exactly (D = rn(sa sb), D0 = rn(sa0 sb0) > 0) implies v <= v0, equal only
+// when both round to the same double -- either row then yields the same
+// minimum.  AB * D0 < AB0 * D is decided exactly on the FMA-split products
+// (p + e, |e| <= ulp(p) / 2; p1 < p2 implies p1 + e1 <= p2 + e2).
+__device__ __forceinline__ bool exact_less(double ab, double sa, double sb, double ab0, double sa0, double sb0) {
+  const double D = __dmul_rn(sa, sb), D0 = __dmul_rn(sa0, sb0);
+  const double p1 = __dmul_rn(ab, D0), e1 = __fma_rn(ab, D0, -p1);
+  const double p2 = __dmul_rn(ab0, D), e2 = __fma_rn(ab0, D, -p2);
+  return p1 < p2 || (p1 == p2 && e1 < e2);
+}
+
 template <int FMT>
 __device__ __forceinline__ typename AccOf<FMT>::type sym_mma(const i8x16& a, const i8x16& b,
                                                              typename AccOf<FMT>::type c) {
@@ -465,9 +479,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
               if (!take && est <= est0 * (1.0f + 0x1p-17f)) {  // too close for fp32: the exact values
                 const int rr = (int)(sv & rmask);
                 const double sa0 = s_sa[rr * kSA + row], sb0 = s_sb[rr * kSB + col];
-                const double v = __ddiv_rn((double)acc[i][j][e], __dmul_rn(sa, sb));
-                const double v0 = __ddiv_rn(rint((double)est0 * sa0 * sb0), __dmul_rn(sa0, sb0));
-                take = v < v0;
+                take = exact_less((double)acc[i][j][e], sa, sb, rint((double)est0 * sa0 * sb0), sa0, sb0);
               }
               if (take) sv = (__float_as_uint(est) & ~rmask) | (uint32_t)r;
             }
@@ -513,7 +525,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
                 const double sa0 = s_sa[rr * kSA + row], sb0 = s_sb[rr * kSB + col];
                 const double ab0 =
                     (sv >> 31) ? (double)((sv & 0x7FFFFFFFu) >> rbits) : rint((double)est0 * sa0 * sb0);
-                take = __ddiv_rn((double)ab, __dmul_rn(sa, sb)) < __ddiv_rn(ab0, __dmul_rn(sa0, sb0));
+                take = exact_less((double)ab, sa, sb, ab0, sa0, sb0);
               }
             }
             if (take) sv = (float)ab <= ab_est_max ? (__float_as_uint(est) & ~rmask) | (uint32_t)r
