@@ -419,12 +419,22 @@ def _pmc_file(name):
     return path if os.path.exists(path) else None
 
 
+def _pmc_lookup(summary, kernel):
+    """`kernel`'s record; a name with a `*` matches any one template
+    argument there (the ring depth of k_cosine_sym is a build constant)."""
+    if "*" not in kernel:
+        return summary.get(kernel)
+    import re
+    pat = re.compile(re.escape(kernel).replace(r"\*", r"[^,<>]+") + "$")
+    return next((v for k, v in summary.items() if pat.match(k)), None)
+
+
 def pmc_record(kernel, name):
     """This round's committed PMC summary record of `kernel` (or {})."""
     path = _pmc_file(name)
     if not path:
         return {}
-    rec = json.load(open(path)).get(kernel) or {}
+    rec = _pmc_lookup(json.load(open(path)), kernel) or {}
     return {k: v for k, v in rec.items() if k != "counters_avg_per_dispatch"}
 
 
@@ -436,7 +446,7 @@ def pmc_traffic(kernel, name="pmc_summary.json"):
     path = _pmc_file(name)
     if not path:
         return None, None
-    rec = json.load(open(path)).get(kernel)
+    rec = _pmc_lookup(json.load(open(path)), kernel)
     val = (rec.get("hbm_bytes_per_launch") or rec.get("fetch_bytes_per_dispatch")) if rec else None
     return val, os.path.relpath(path, ROOT)
 
@@ -683,9 +693,9 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
     job_f4 = nf * (nf - 1) / 2 * 2 * d * w
     job_peak = alg_ops / (job_f4 / FP4_MFMA_PEAK_TOPS + (alg_ops - job_f4) / INT8_MFMA_PEAK_TOPS)
     wave_ach = wave_ops / (waves_ms * 1e-3) / 1e12 if waves_ms else None
-    cos_traffic = pmc_traffic("void cms::k_cosine_sym<5, 64, 1, 8>", "cosine_pmc_summary.json")
-    cos_pmc = pmc_record("void cms::k_cosine_sym<5, 64, 1, 8>", "cosine_pmc_summary.json")
-    cos_pmc8 = pmc_record("void cms::k_cosine_sym<5, 64, 0, 8>", "cosine_pmc_summary.json")
+    cos_traffic = pmc_traffic("void cms::k_cosine_sym<*, 64, 1, 8>", "cosine_pmc_summary.json")
+    cos_pmc = pmc_record("void cms::k_cosine_sym<*, 64, 1, 8>", "cosine_pmc_summary.json")
+    cos_pmc8 = pmc_record("void cms::k_cosine_sym<*, 64, 0, 8>", "cosine_pmc_summary.json")
     cos_pmcm = pmc_record("void cms::k_cosine_mls<2>", "cosine_pmc_summary.json")
     return {
         "workload": f"config 4: top-{k} most similar items for every one of the {n} items of the config-3 table "
@@ -700,9 +710,9 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
         "frac_int8_peak_per_gpu": alg_ops / wall / 1e12 / INT8_MFMA_PEAK_TOPS / world,
         "mixed_peak_TOPS": job_peak,
         "frac_mixed_peak_per_gpu": alg_ops / wall / 1e12 / job_peak / world,
-        # dominant kernel: the fp4 symmetric waves (k_cosine_sym<5,64,1>, the
+        # dominant kernel: the fp4 symmetric waves (k_cosine_sym<NS,64,1>, the
         # largest share of the job); its avg launch matches rocprofv3's for that name
-        "roofline": {"bound": "mfma", "kernel": "k_cosine_sym<5,64,1> (fp4 symmetric waves)",
+        "roofline": {"bound": "mfma", "kernel": "k_cosine_sym<NS,64,1> (fp4 symmetric waves)",
                      "achieved": f4_ops / (f4_ms * 1e-3) / 1e12 if f4_ms else None,
                      "peak": FP4_MFMA_PEAK_TOPS, "unit": "TOP/s",
                      "frac": f4_ops / (f4_ms * 1e-3) / 1e12 / FP4_MFMA_PEAK_TOPS if f4_ms else None,
@@ -711,7 +721,7 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
                      "traffic": cos_traffic[0], "traffic_unit": "bytes per launch (2 x FETCH_SIZE)",
                      "traffic_source": cos_traffic[1],
                      "pmc_mfma_busy_frac": cos_pmc.get("mfma_busy_frac"), "pmc_l2_hit": cos_pmc.get("l2_hit")},
-        "roofline_int8_waves": {"bound": "mfma", "kernel": "k_cosine_sym<5,64,0> (int8 symmetric waves)",
+        "roofline_int8_waves": {"bound": "mfma", "kernel": "k_cosine_sym<NS,64,0> (int8 symmetric waves)",
                                 "pmc_mfma_busy_frac": cos_pmc8.get("mfma_busy_frac"),
                                 "achieved": i8_ops / (i8_ms * 1e-3) / 1e12 if i8_ms else None,
                                 "peak": INT8_MFMA_PEAK_TOPS, "unit": "TOP/s",
