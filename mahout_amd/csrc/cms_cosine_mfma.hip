@@ -66,27 +66,35 @@ __global__ __launch_bounds__(256) void k_limb_count(const uint32_t* rowmax, int6
 // Stable permutation: owners with 3+ limbs, then 2 limbs, then single-limb
 // owners with a counter above kF4Max, then the fp4 class (every counter
 // <= kF4Max), each class in row order (exclusive scans of the class flags).
-// For an incremental refresh (tpos8/tpos4 non-null) the touched owners of the
-// two single-limb classes come first within their class, so the touched rows
-// are two position ranges and whole symmetric-wave blocks of untouched rows
-// can be skipped.
+// For an incremental refresh (tpos non-null) the touched owners of every
+// class come first within their class, so the touched rows are four position
+// ranges: whole symmetric-wave blocks of untouched single-limb rows can be
+// skipped, and untouched multi-limb rows need only their touched columns.
+// tpos: [0] int8, [1] fp4, [2] 3+ limbs, [3] 2 limbs (exclusive scans of the
+// touched flags, n each); nt: their totals.
 __global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, const uint32_t* dpos,
                             const uint32_t* deep_flag, const uint32_t* fpos, const uint32_t* f4_flag,
                             const uint8_t* rowL, int64_t nrows, int64_t n_deep, int64_t n_multi, int64_t n_s8,
-                            const uint8_t* touch, const uint32_t* tpos8, const uint32_t* tpos4, int64_t nt8,
-                            int64_t nt4, int64_t* perm, int64_t* inv, uint8_t* rowLp) {
+                            const uint8_t* touch, const uint32_t* tpos, int64_t nt8, int64_t nt4, int64_t ntd,
+                            int64_t ntm, int64_t* perm, int64_t* inv, uint8_t* rowLp) {
+  // rank q within a class of nt touched owners, touched first
+  auto place = [&](int64_t r, int64_t q, const uint32_t* tp, int64_t nt) {
+    return !tpos ? q : touch[r] ? (int64_t)tp[r] : nt + q - (int64_t)tp[r];
+  };
+  const uint32_t* tpos8 = tpos;
+  const uint32_t* tpos4 = tpos ? tpos + nrows : nullptr;
+  const uint32_t* tposd = tpos ? tpos + 2 * nrows : nullptr;
+  const uint32_t* tposm = tpos ? tpos + 3 * nrows : nullptr;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
     int64_t p;
     if (deep_flag[r]) {
-      p = (int64_t)dpos[r];
+      p = place(r, (int64_t)dpos[r], tposd, ntd);
     } else if (multi_flag[r]) {
-      p = n_deep + ((int64_t)mpos[r] - (int64_t)dpos[r]);
+      p = n_deep + place(r, (int64_t)mpos[r] - (int64_t)dpos[r], tposm, ntm);
     } else if (f4_flag[r]) {
-      const int64_t q = (int64_t)fpos[r];  // rank in the fp4 class
-      p = n_multi + n_s8 + (!tpos4 ? q : touch[r] ? (int64_t)tpos4[r] : nt4 + q - (int64_t)tpos4[r]);
+      p = n_multi + n_s8 + place(r, (int64_t)fpos[r], tpos4, nt4);  // rank in the fp4 class
     } else {
-      const int64_t q = r - (int64_t)mpos[r] - (int64_t)fpos[r];  // rank in the int8 class
-      p = n_multi + (!tpos8 ? q : touch[r] ? (int64_t)tpos8[r] : nt8 + q - (int64_t)tpos8[r]);
+      p = n_multi + place(r, r - (int64_t)mpos[r] - (int64_t)fpos[r], tpos8, nt8);  // rank in the int8 class
     }
     perm[p] = r;
     inv[r] = p;
@@ -94,13 +102,15 @@ __global__ void k_limb_perm(const uint32_t* mpos, const uint32_t* multi_flag, co
   }
 }
 
-// refresh: touched flags of the int8 and fp4 single-limb classes
-__global__ void k_touch_class(const uint8_t* touch, const uint32_t* multi_flag, const uint32_t* f4_flag, int64_t n,
-                              uint32_t* t8, uint32_t* t4) {
+// refresh: touched flags per class, [0] int8, [1] fp4, [2] 3+ limbs, [3] 2 limbs (n each)
+__global__ void k_touch_class(const uint8_t* touch, const uint32_t* multi_flag, const uint32_t* deep_flag,
+                              const uint32_t* f4_flag, int64_t n, uint32_t* tf) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    const bool t = touch[r] != 0 && multi_flag[r] == 0;
-    t8[r] = (t && f4_flag[r] == 0) ? 1u : 0u;
-    t4[r] = (t && f4_flag[r] != 0) ? 1u : 0u;
+    const bool t = touch[r] != 0, m = multi_flag[r] != 0, dp = deep_flag[r] != 0, f = f4_flag[r] != 0;
+    tf[r] = (t && !m && !f) ? 1u : 0u;
+    tf[n + r] = (t && !m && f) ? 1u : 0u;
+    tf[2 * n + r] = (t && dp) ? 1u : 0u;
+    tf[3 * n + r] = (t && m && !dp) ? 1u : 0u;
   }
 }
 
@@ -1037,33 +1047,33 @@ int cosine_prepare(cms_handle* h) {
   h->n_inexact_rows = host[2];
   const uint32_t n_five = host[3];
   CMS_HIP(h->ws_limbhot.ensure((size_t)std::max<int64_t>(1, n_multi) * (kMaxLimbs - 1) * (size_t)dw));
-  // incremental refresh: touched single-limb owners first within their class
+  // incremental refresh: touched owners first within their class
   const uint8_t* touch = nullptr;
-  uint32_t *t8 = nullptr, *t4 = nullptr, *tpos8 = nullptr, *tpos4 = nullptr;
-  int64_t nt8 = 0, nt4 = 0;
+  uint32_t* tpos = nullptr;
+  int64_t nt[4] = {0, 0, 0, 0};  // touched int8, fp4, 3+ limb, 2-limb owners
   if (h->rf_restrict) {
-    CMS_HIP(h->rf_perm.ensure(sizeof(uint32_t) * 4 * (size_t)n));
-    t8 = h->rf_perm.as<uint32_t>();
-    t4 = t8 + n;
-    tpos8 = t4 + n;
-    tpos4 = tpos8 + n;
+    CMS_HIP(h->rf_perm.ensure(sizeof(uint32_t) * 8 * (size_t)n));
+    uint32_t* tf = h->rf_perm.as<uint32_t>();
+    tpos = tf + 4 * n;
     touch = h->rf_touch.as<uint8_t>();
     TimedScope ts(h, "limb_prep");
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_touch_class, dim3(grid), dim3(256), 0, h->stream, touch, mflag, fflag, n, t8, t4);
+    hipLaunchKernelGGL(k_touch_class, dim3(grid), dim3(256), 0, h->stream, touch, mflag, dflag, fflag, n, tf);
     CMS_HIP(hipGetLastError());
-    int rc = scan_exclusive_u32(h, t8, tpos8, n, bsum);
-    if (rc) return rc;
-    CMS_HIP(hipMemcpyAsync(&host[0], tpos8 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
-    CMS_HIP(hipMemcpyAsync(&host[1], t8 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
-    rc = scan_exclusive_u32(h, t4, tpos4, n, bsum);
-    if (rc) return rc;
-    CMS_HIP(hipMemcpyAsync(&host[2], tpos4 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
-    CMS_HIP(hipMemcpyAsync(&host[3], t4 + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    uint32_t th[8];
+    for (int c = 0; c < 4; ++c) {
+      int rc = scan_exclusive_u32(h, tf + c * n, tpos + c * n, n, bsum);
+      if (rc) return rc;
+      CMS_HIP(hipMemcpyAsync(&th[2 * c], tpos + c * n + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+      CMS_HIP(hipMemcpyAsync(&th[2 * c + 1], tf + c * n + n - 1, 4, hipMemcpyDeviceToHost, h->stream));
+    }
     CMS_HIP(hipStreamSynchronize(h->stream));
-    nt8 = (int64_t)host[0] + host[1];
-    nt4 = (int64_t)host[2] + host[3];
+    for (int c = 0; c < 4; ++c) nt[c] = (int64_t)th[2 * c] + th[2 * c + 1];
   }
+  const int64_t nt8 = nt[0], nt4 = nt[1];
+  h->rf_td = nt[2];
+  h->rf_tm = nt[3];
+  h->rf_nd = n_deep;
   h->rf_t8 = nt8;
   h->rf_t4 = nt4;
   h->rf_s8 = n_s8;
@@ -1071,7 +1081,7 @@ int cosine_prepare(cms_handle* h) {
     TimedScope ts(h, "limb_prep");
     unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(k_limb_perm, dim3(grid), dim3(256), 0, h->stream, mpos, mflag, dpos, dflag, fpos, fflag, rowL,
-                       n, n_deep, n_multi, n_s8, touch, tpos8, tpos4, nt8, nt4, perm, inv, rowLp);
+                       n, n_deep, n_multi, n_s8, touch, tpos, nt8, nt4, nt[2], nt[3], perm, inv, rowLp);
     hipLaunchKernelGGL(k_limb_write, dim3((unsigned)n), dim3(256), (size_t)h->p.width, h->stream, h->tview(), dw, perm, rowLp, n_multi,
                        h->ws_limb0.as<int8_t>(), h->ws_limbhot.as<int8_t>());
     hipLaunchKernelGGL(k_tile_limbs, dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, h->stream, rowLp, n,
@@ -1303,6 +1313,11 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
     base.q0 = q0;
     base.qcount = qc;
     const int64_t slo = std::max(q0, nm);  // single-limb query rows [slo, qend)
+    // candidate column ranges: every column, or (a refresh's untouched
+    // multi-limb rows) the caller's ranges; the other columns are left alone
+    std::vector<std::pair<int64_t, int64_t>> cols = h->slab_cols;
+    if (cols.empty()) cols.push_back({0, n});
+    else if (slo < qend) return set_error(CMS_E_STATE, "column-restricted slab with single-limb query rows");
     if (slo < qend && nm < n) {  // S x S
       BigArgs g = base;
       g.A = a.limb0 + slo * dw;
@@ -1326,14 +1341,19 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
         if ((rc = vl_blk_prepare(h, gi))) return rc;
         const int64_t oa0 = G.o0 + (std::max(q0, G.o0) - G.o0) / (2 * per) * (2 * per);
         const int64_t vrow0 = (oa0 - G.o0) / per * 32;
+        for (const auto& cr : cols) {
+        const int64_t lo = std::max(cr.first, nm), hi = std::min(cr.second, n);
+        if (lo >= hi) continue;
+        const int64_t blo = nm + (lo - nm) / kImgBlk * kImgBlk;  // image blocks start every kImgBlk rows from nm
         MlsArgs m{};
         m.A = G.bbuf.as<int8_t>() + vrow0 * dw;
         m.a_vrows = G.rows - vrow0;
         m.a_pos0 = oa0;
         m.a_owners = std::min(qend, G.o1) - oa0;
         m.B = h->ws_i8blk.as<int8_t>();
-        m.b_img0 = m.b_pos0 = nm;
-        m.b_rows = n - nm;
+        m.b_img0 = nm;
+        m.b_pos0 = blo;
+        m.b_rows = hi - blo;
         m.rs = dw;
         m.kw = h->p.width;
         m.depth = h->p.depth;
@@ -1345,18 +1365,23 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
         m.qcount = qc;
         m.weighted = h->p.weighting == CMS_WEIGHTED;
         if ((rc = launch_mls(h, m, ls))) return rc;
+        }
       } else if (q0 < G.o1 && qend > G.o0 && nm < n) {  // M x S: multi-limb queries against single-limb candidates
         const int64_t oa0 = G.o0 + (std::max(q0, G.o0) - G.o0) / per * per;
         const int64_t blk = (oa0 - G.o0) / per;
-        BigArgs g = base;
-        g.A = vl + blk * 32 * dw;
-        g.a_vrows = G.rows - blk * 32;
-        g.a_pos0 = oa0;
-        g.a_owners = std::min(qend, G.o1) - oa0;
-        g.B = a.limb0 + nm * dw;
-        g.b_pos0 = nm;
-        g.b_rows = n - nm;
-        if ((rc = launch(g, ls))) return rc;
+        for (const auto& cr : cols) {
+          const int64_t lo = std::max(cr.first, nm), hi = std::min(cr.second, n);
+          if (lo >= hi) continue;
+          BigArgs g = base;
+          g.A = vl + blk * 32 * dw;
+          g.a_vrows = G.rows - blk * 32;
+          g.a_pos0 = oa0;
+          g.a_owners = std::min(qend, G.o1) - oa0;
+          g.B = a.limb0 + lo * dw;
+          g.b_pos0 = lo;
+          g.b_rows = hi - lo;
+          if ((rc = launch(g, ls))) return rc;
+        }
       }
       if (slo < qend) {  // S x M, computed as M x S and written transposed
         BigArgs g = base;
@@ -1373,8 +1398,14 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
     }
     // M x M: the 128-tiles holding multi-limb queries and multi-limb candidates
     std::vector<int2> multi;
+    auto col_tile = [&](int64_t tc) {  // the 128-column tile meets a candidate range
+      for (const auto& cr : cols)
+        if (cr.first < (tc + 1) * kTile && cr.second > tc * kTile) return true;
+      return false;
+    };
     for (int64_t tr = 0; q0 + tr * kTile < std::min(qend, nm); ++tr)
-      for (int64_t tc = 0; tc * kTile < nm; ++tc) multi.push_back(make_int2((int)tc, (int)tr));
+      for (int64_t tc = 0; tc * kTile < nm; ++tc)
+        if (col_tile(tc)) multi.push_back(make_int2((int)tc, (int)tr));
     if (!multi.empty()) {
       CMS_HIP(h->ws_tiles.ensure(sizeof(int2) * multi.size()));
       CMS_HIP(hipMemcpyAsync(h->ws_tiles.ptr, multi.data(), sizeof(int2) * multi.size(), hipMemcpyHostToDevice,
@@ -1411,6 +1442,18 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
     CMS_HIP(hipStreamSynchronize(h->stream));  // the host tile list must outlive the copy
   }
   return CMS_OK;
+}
+
+// Refresh: admission thresholds of the untouched owners' lists from their
+// kept lists (position p holds owner row perm[p]); a kept list that holds
+// every candidate (full) or none keeps -inf.
+__global__ void k_rf_seed_thr(int64_t n, int32_t D, const int64_t* perm, const uint8_t* touch, const int32_t* kcnt,
+                              const double* ksc, const uint8_t* kfull, double* thr) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = perm[p];
+    const int32_t c = kcnt[r];
+    if (!touch[r] && !kfull[r] && c > 0) thr[p] = ksc[r * D + c - 1];
+  }
 }
 
 // ---------------------------------------------- all-pairs top-k, streaming --
@@ -1507,6 +1550,16 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     for (int64_t o = 0; o < n; o += (int64_t)ninf.size())
       CMS_HIP(hipMemcpyAsync(cb.thr + o, ninf.data(), sizeof(double) * std::min<int64_t>(ninf.size(), n - o),
                              hipMemcpyHostToDevice, h->stream));
+    if (h->rf_restrict) {
+      // refresh: an untouched owner's fold keeps only the merged entries at or
+      // above its kept list's last score (k_rf_fold's valid prefix), so its
+      // list here admits nothing below that score
+      const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+      hipLaunchKernelGGL(k_rf_seed_thr, dim3(grid), dim3(256), 0, h->stream, n, h->rf_depth, cosine_perm_device(h),
+                         h->rf_touch.as<uint8_t>(), h->rf_cnt.as<int32_t>(), h->rf_sc.as<double>(),
+                         h->rf_full.as<uint8_t>(), cb.thr);
+      CMS_HIP(hipGetLastError());
+    }
     CMS_HIP(hipStreamSynchronize(h->stream));
   }
   BigArgs base = big_base(h);
@@ -1526,9 +1579,31 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
     // chunk must leave room in a list compacted to cap - qc entries
     // (the lists are offered the slab cap/2 rows at a time: multi_rows_slab_offer)
     const int64_t chunk = multi_slab_rows(h, n);
-    for (int64_t m0 = (int64_t)shard * chunk; m0 < nm; m0 += (int64_t)nshards * chunk) {
-      const int64_t qc = std::min<int64_t>(chunk, nm - m0);
-      if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts))) return rc;
+    if (!h->rf_restrict) {
+      for (int64_t m0 = (int64_t)shard * chunk; m0 < nm; m0 += (int64_t)nshards * chunk) {
+        const int64_t qc = std::min<int64_t>(chunk, nm - m0);
+        if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts))) return rc;
+      }
+    } else {
+      // refresh: touched multi-limb rows (first in each limb group) against
+      // every column; untouched ones only against the touched owners' columns
+      // (multi-limb, int8 and fp4 ranges), the only pairs of theirs that changed
+      const int64_t nd = h->rf_nd;
+      const std::vector<std::pair<int64_t, int64_t>> touched = {
+          {0, h->rf_td}, {nd, nd + h->rf_tm}, {nm, nm + h->rf_t8}, {nm + h->rf_s8, nm + h->rf_s8 + h->rf_t4}};
+      const struct {
+        int64_t lo, hi;
+        bool all;
+      } runs[4] = {{0, h->rf_td, true}, {nd, nd + h->rf_tm, true}, {h->rf_td, nd, false}, {nd + h->rf_tm, nm, false}};
+      int64_t ctr = 0;
+      for (const auto& ru : runs)
+        for (int64_t m0 = ru.lo; m0 < ru.hi; m0 += chunk) {
+          if (ctr++ % nshards != shard) continue;
+          const int64_t qc = std::min<int64_t>(chunk, ru.hi - m0);
+          if ((rc = multi_rows_slab_offer(h, cb, m0, qc, nm, n, k, d_ids, d_scores, d_counts,
+                                          ru.all ? nullptr : &touched)))
+            return rc;
+        }
     }
   }
   // 3. S x S symmetric waves.  With fp4 owners (positions [f0, n), whole

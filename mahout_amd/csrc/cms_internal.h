@@ -289,6 +289,9 @@ struct cms_handle {
   // keep only block pairs holding a touched owner
   bool rf_restrict = false;
   int64_t rf_t8 = 0, rf_t4 = 0, rf_s8 = 0;  // touched int8 / fp4 single-limb owners; int8-class size
+  int64_t rf_td = 0, rf_tm = 0, rf_nd = 0;  // touched 3+-limb / 2-limb owners (first in their group); 3+-limb owners
+  // column ranges (permuted positions [lo, hi)) a slab is restricted to; empty: every column
+  std::vector<std::pair<int64_t, int64_t>> slab_cols;
   int64_t rf_stat_touched = 0, rf_stat_redo = 0, rf_stat_full = 0;
   // owners of the last all-pairs job per operand class (multi-limb, int8,
   // fp4) and, for an incremental refresh, how many of each were touched
@@ -492,7 +495,8 @@ int cand_emit(cms_handle* h, const CandBufs& cb, int64_t p0, int64_t np, int32_t
 // slab of positions [m0, m0+qc) against everyone: exact top-k of those rows,
 // and their similarities offered to the lists of columns [c0, c1)
 int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t qc, int64_t c0, int64_t c1, int32_t k,
-                          int64_t* d_ids, double* d_scores, int32_t* d_counts);
+                          int64_t* d_ids, double* d_scores, int32_t* d_counts,
+                          const std::vector<std::pair<int64_t, int64_t>>* cols = nullptr);
 int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_t* d_counts, int32_t shard = 0,
               int32_t nshards = 1);
 // merge nparts partial top-k lists ([nparts][n][k] ids by owner ID, scores; [nparts][n] counts)

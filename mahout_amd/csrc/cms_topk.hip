@@ -760,27 +760,51 @@ __global__ void k_slab_offer(const double* __restrict__ slab, int64_t ld, int64_
 }
 
 int multi_rows_slab_offer(cms_handle* h, const CandBufs& cb, int64_t m0, int64_t qc, int64_t c0, int64_t c1, int32_t k,
-                          int64_t* d_ids, double* d_scores, int32_t* d_counts) {
+                          int64_t* d_ids, double* d_scores, int32_t* d_counts,
+                          const std::vector<std::pair<int64_t, int64_t>>* cols) {
   const int64_t n = h->n;
   int rc;
   CMS_HIP(h->ws_slab.ensure(sizeof(double) * (size_t)(qc * n)));
   double* slab = h->ws_slab.as<double>();
-  if ((rc = cosine_slab(h, m0, qc, slab))) return rc;
+  if (cols) {
+    // a refresh's untouched multi-limb rows: only the pairs with a touched
+    // owner changed, so only those columns are computed; the rest of the
+    // slab stays NaN (never a candidate).  Columns a range rounds in are
+    // current values too, which the fold accepts (k_rf_fold drops pairs both
+    // lists hold).
+    CMS_HIP(hipMemsetAsync(slab, 0xFF, sizeof(double) * (size_t)(qc * n), h->stream));
+    h->slab_cols = *cols;
+    rc = cosine_slab(h, m0, qc, slab);
+    h->slab_cols.clear();
+    if (rc) return rc;
+  } else if ((rc = cosine_slab(h, m0, qc, slab))) {
+    return rc;
+  }
   // exact top-k of the slab rows
   std::vector<TopQuery> qs;
   for (int64_t p = m0; p < m0 + qc; ++p) qs.push_back(TopQuery{p - m0, p, h->h_perm[p]});
   if ((rc = launch_top_k(h, slab, qs, k, cosine_perm_device(h), d_ids, d_scores, d_counts))) return rc;
   // and the same similarities for the columns' lists, cap/2 slab rows at a
   // time: each part offers at most that many entries to a list compacted to
-  // cap - part first (a slab may hold more rows than a list has room for)
-  if (c1 > c0) {
+  // cap - part first (a slab may hold more rows than a list has room for);
+  // with column ranges, only the single-limb columns inside them
+  std::vector<std::pair<int64_t, int64_t>> offer;
+  if (cols) {
+    for (const auto& cr : *cols) {
+      const int64_t lo = std::max(cr.first, c0), hi = std::min(cr.second, c1);
+      if (lo < hi) offer.push_back({lo, hi});
+    }
+  } else if (c1 > c0) {
+    offer.push_back({c0, c1});
+  }
+  for (const auto& oc : offer) {
     const int64_t part = std::max<int64_t>(1, cb.cap / 2);
     for (int64_t s0 = 0; s0 < qc;) {
       const int64_t pc = std::min(part, qc - s0);
-      if ((rc = cand_compact(h, cb, c0, c1 - c0, (uint32_t)(cb.cap - pc), k))) return rc;
-      const unsigned g1 = (unsigned)std::min<int64_t>((c1 - c0 + 255) / 256, 8192);
-      hipLaunchKernelGGL(k_slab_offer, dim3(g1), dim3(256), 0, h->stream, slab + s0 * n, n, m0 + s0, pc, c0, c1,
-                         cb.thr, cb.ccnt, cb.cidx, cb.cval, cb.cap);
+      if ((rc = cand_compact(h, cb, oc.first, oc.second - oc.first, (uint32_t)(cb.cap - pc), k))) return rc;
+      const unsigned g1 = (unsigned)std::min<int64_t>((oc.second - oc.first + 255) / 256, 8192);
+      hipLaunchKernelGGL(k_slab_offer, dim3(g1), dim3(256), 0, h->stream, slab + s0 * n, n, m0 + s0, pc, oc.first,
+                         oc.second, cb.thr, cb.ccnt, cb.cidx, cb.cval, cb.cap);
       CMS_HIP(hipGetLastError());
       s0 += pc;
     }

@@ -48,7 +48,8 @@ def main():
         t.top_k_refresh(k)
         wall = time.perf_counter() - t0
         touched, redone, full = t.refresh_stats()
-        print(f"{nbat} batches: refresh {wall:.2f} s touched {touched / n:.3f} redone {redone} whole {full}")
+        print(f"{nbat} batches: refresh {wall:.2f} s touched {touched / n:.3f} redone {redone} whole {full} "
+              f"topk_redo {t.stats()['topk_redo']} classes {t.refresh_classes()}")
         for s in SCOPES:
             ms, cnt = t.timing(s)
             if cnt:
