@@ -459,7 +459,9 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
           const float rb = __builtin_amdgcn_rcpf((float)sb);
           const float tb = __half2float(s_tb[col]);
 #pragma unroll
-          for (int i = 0; i < TI; ++i)
+          for (int i = 0; i < TI; ++i) {
+            const int g0 = (i * 3 + j) * 16;  // the 16 outputs of MFMA tile (i, j): one test when the wave's are all dead
+            if (!__any(((alive[g0 >> 5] >> (g0 & 31)) & 0xFFFFu) != 0u)) continue;
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
               const int bit = (i * 3 + j) * 16 + e;
@@ -483,6 +485,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
               }
               if (take) sv = (__float_as_uint(est) & ~rmask) | (uint32_t)r;
             }
+          }
         }
       }
     } else if (__any(any_alive != 0u)) {  // int8: estimate or exact form
@@ -493,7 +496,9 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         const float rb = __builtin_amdgcn_rcpf((float)sb);
         const float tb = __half2float(s_tb[col]);
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i) {
+          const int g0 = (i * 3 + j) * 16;
+          if (!__any(((alive[g0 >> 5] >> (g0 & 31)) & 0xFFFFu) != 0u)) continue;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int bit = (i * 3 + j) * 16 + e;
@@ -531,6 +536,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
             if (take) sv = (float)ab <= ab_est_max ? (__float_as_uint(est) & ~rmask) | (uint32_t)r
                                                                  : 0x80000000u | (ab << rbits) | (uint32_t)r;
           }
+        }
       }
     }
 #pragma unroll
