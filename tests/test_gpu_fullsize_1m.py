@@ -141,9 +141,14 @@ def test_config34_full_size(oracle):
         bi, bu = zipf_stream_torch(N_USERS, N_ITEMS, 1_250_000, seed=777_000, device="cuda")
         t.ingest_device_rows(bi.contiguous(), bu.contiguous(), None, int(bi.numel()))
         t.finalize()
+        redo0 = t.stats()["topk_redo"]
         got = t.top_k_refresh(K)
         touched, redone, full = t.refresh_stats()
         assert full == 1 and 0 < touched < N_ITEMS // 2
+        # the refresh's lists keep their room (seeded thresholds): no whole-row recomputes
+        assert redone == 0 and t.stats()["topk_redo"] == redo0
+        cls = t.refresh_classes()
+        assert sum(c[0] for c in cls.values()) == N_ITEMS and sum(c[1] for c in cls.values()) == touched, cls
         assert same_lists(got, t.top_k_all(K))
         # refreshed lists of 2 touched and 2 untouched owners against the
         # oracle's TopItems loop over the updated table's exact similarities
