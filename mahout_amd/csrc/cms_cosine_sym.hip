@@ -309,6 +309,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
 #endif
 #endif
 
+  int s_in_row = 0, r_next = 0;  // stage within the current sketch row, and that row (no per-stage division)
   for (int s = 0; s < total; ++s) {
 #if CMS_SYM_SCHED == 3
     {
@@ -429,8 +430,9 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
     }
 #endif
 #endif  // CMS_SYM_SCHED == 3
-    const int r = s / cstages;
-    if (s - r * cstages != cstages - 1) continue;
+    if (++s_in_row != cstages) continue;
+    s_in_row = 0;
+    const int r = r_next++;
 #if CMS_SYM_PROBE & 2  // bound analysis: no row-boundary screening / minimum (the MFMAs stay live)
 #pragma unroll
     for (int i = 0; i < TI; ++i)
