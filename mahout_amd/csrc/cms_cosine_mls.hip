@@ -176,6 +176,7 @@ __global__ __launch_bounds__(512, 1) void k_cosine_mls(MlsArgs g) {
   i8x16 fa0[2], fb0[3];
   frags(lds, 0, fa0, fb0);
 
+  int s_in_row = 0, r_next = 0;  // stage within the current sketch row, and that row (no per-stage division)
   for (int s = 0; s < total; ++s) {
     {
       const unsigned char* A = lds + (s % NSTAGE) * kStage;
@@ -211,8 +212,9 @@ __global__ __launch_bounds__(512, 1) void k_cosine_mls(MlsArgs g) {
       }
       issue(sn, s, 2);
     }
-    const int r = s / cstages;
-    if (s - r * cstages != cstages - 1) continue;
+    if (++s_in_row != cstages) continue;
+    s_in_row = 0;
+    const int r = r_next++;
     // ---- sketch row r done (DoubleCountMinSketch.java:139-147) ----
     const double* sa_r = s_sa + r * OA;
     const double* sb_r = s_sb + r * kMB;
