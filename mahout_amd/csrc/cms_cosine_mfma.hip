@@ -1444,6 +1444,12 @@ int cosine_slab(cms_handle* h, int64_t q0, int64_t qc, double* d_out) {
   return CMS_OK;
 }
 
+// fp32 copies of admission thresholds, rounded toward -inf (never above)
+__global__ void k_thr_f32(const double* thr, float* t32, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    t32[i] = __double2float_rd(thr[i]);
+}
+
 // Refresh: admission thresholds of the untouched owners' lists from their
 // kept lists (position p holds owner row perm[p]); a kept list that holds
 // every candidate (full) or none keeps -inf.
@@ -1532,7 +1538,9 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
   const size_t off_ovf = off_thr + sizeof(double) * (size_t)n;
   const size_t off_list = off_ovf + sizeof(uint32_t) * (size_t)n;
   const size_t off_ln = off_list + sizeof(uint32_t) * (size_t)n;
-  CMS_HIP(ws.ensure(off_ln + 256));
+  const size_t off_t32 = (off_ln + 256 + 255) & ~size_t(255);
+  CMS_HIP(ws.ensure(off_t32 + sizeof(float) * (size_t)n + 256));
+  float* thr32 = reinterpret_cast<float*>(ws.as<char>() + off_t32);
   char* wsb = ws.as<char>();
   CandBufs cb;
   cb.ccnt = reinterpret_cast<uint32_t*>(wsb);
@@ -1733,6 +1741,12 @@ int top_k_all(cms_handle* h, int32_t k, int64_t* d_ids, double* d_scores, int32_
             } else {
               g.rect = 0;
             }
+          }
+          {  // the admission thresholds as fp32 rounded down, for the tiles' LDS-DMA
+            const unsigned tg = (unsigned)std::min<int64_t>((g.s_rows + 255) / 256, 4096);
+            hipLaunchKernelGGL(k_thr_f32, dim3(tg), dim3(256), 0, h->stream, cb.thr + g.s0, thr32 + g.s0, g.s_rows);
+            CMS_HIP(hipGetLastError());
+            g.thr32 = thr32;
           }
           if ((rc = launch_sym(h, g, fp4 ? 1 : 0, slots))) return rc;
           continue;

@@ -121,8 +121,8 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   const int depth = g.depth;
   double* s_sa = reinterpret_cast<double*>(lds + NSTAGE * kStage);  // [depth][256]
   double* s_sb = s_sa + depth * kSA;                                  // [depth][192]
-  __half* s_ta = reinterpret_cast<__half*>(s_sb + depth * kSB);      // admission thresholds, rounded down
-  __half* s_tb = s_ta + kSA;
+  float* s_ta = reinterpret_cast<float*>(s_sb + depth * kSB);        // admission thresholds, rounded down
+  float* s_tb = s_ta + kSA;
 
   // ---- which tile: band of waves, block pair {I, J}, A panel, B panel ----
   // a refresh's sparse pair set (tsel) is spread over the XCDs round-robin
@@ -190,12 +190,18 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
     double* dst = isA ? s_sa + r * kSA + first : s_sb + r * kSB + first;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsn, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
   }
-  for (int i = tid; i < kSA + kSB; i += NT) {
-    const bool isA = i < kSA;
-    const int64_t o = isA ? i : i - kSA;
-    const int64_t lim = isA ? a_rows : b_rows;
-    const double t = o < lim ? g.thr[(isA ? a_pos0 : b_pos0) + o] : __builtin_inf();
-    (isA ? s_ta : s_tb - kSA)[i] = __float2half_rd(__double2float_rd(t));
+  // thresholds: the launch's fp32 copy (rounded toward -inf) by LDS-DMA too,
+  // 256 B per instruction, so no load latency stands before the ring's fill
+  // (past-the-end owners land as 0: their rows never qualify, den == 0)
+  constexpr int kTIA = kSA / 64, kTI = (kSA + kSB) / 64;
+  for (int k = wid; k < kTI; k += NW) {
+    const bool isA = k < kTIA;
+    const int64_t first = (isA ? k : k - kTIA) * 64;
+    const int64_t cnt = max<int64_t>(0, min<int64_t>(64, (isA ? a_rows : b_rows) - first));
+    const float* src = g.thr32 + (isA ? a_pos0 : b_pos0) + first;
+    const __amdgpu_buffer_rsrc_t rst = __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, (int)(cnt * 4), 0x00020000);
+    float* dst = (isA ? s_ta : s_tb) + first;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rst, (__attribute__((address_space(3))) void*)dst, 4, lane * 4, 0, 0, 0);
   }
 
   // ---- operand fills: K-blocked images, panels start on a kImgBlk block ----
@@ -459,7 +465,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
           const int col = wc * 96 + j * 32 + (lane & 31);
           const double sb = sb_r[col];
           const float rb = __builtin_amdgcn_rcpf((float)sb);
-          const float tb = __half2float(s_tb[col]);
+          const float tb = s_tb[col];
 #pragma unroll
           for (int i = 0; i < TI; ++i) {
             const int g0 = (i * 3 + j) * 16;  // the 16 outputs of MFMA tile (i, j): one test when the wave's are all dead
@@ -473,7 +479,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
               const double sa = sa_r[row];
               if (sa == 0.0 || sb == 0.0) continue;  // den == 0: this sketch row does not qualify
               const float est = (float)acc[i][j][e] * __builtin_amdgcn_rcpf((float)sa) * rb;
-              if (est < fminf(__half2float(s_ta[row]), tb) - 4e-6f) {  // can never be admitted
+              if (est < fminf(s_ta[row], tb) - 4e-6f) {  // can never be admitted
                 alive[bit >> 5] &= ~m;
                 continue;
               }
@@ -496,7 +502,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
         const int col = wc * 96 + j * 32 + (lane & 31);
         const double sb = sb_r[col];
         const float rb = __builtin_amdgcn_rcpf((float)sb);
-        const float tb = __half2float(s_tb[col]);
+        const float tb = s_tb[col];
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           const int g0 = (i * 3 + j) * 16;
@@ -511,7 +517,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
             if (sa == 0.0 || sb == 0.0) continue;  // den == 0: this sketch row does not qualify
             const uint32_t ab = (uint32_t)acc[i][j][e];
             const float est = (float)ab * __builtin_amdgcn_rcpf((float)sa) * rb;
-            if (est < fminf(__half2float(s_ta[row]), tb) - 4e-6f) {  // can never be admitted
+            if (est < fminf(s_ta[row], tb) - 4e-6f) {  // can never be admitted
               alive[bit >> 5] &= ~m;
               continue;
             }
@@ -615,7 +621,7 @@ int sym_stage_bytes() { return kSymBK; }
 
 size_t sym_lds_bytes(int depth) {
   return (size_t)kSymNS * (kSA + kSB) * kSymBK + (size_t)depth * (kSA + kSB) * sizeof(double) +
-         (kSA + kSB) * sizeof(__half);
+         (kSA + kSB) * sizeof(float);
 }
 
 bool sym_eligible(cms_handle* h, int fmt, int32_t* rbits) {

@@ -601,6 +601,7 @@ struct SymArgs {
   int32_t tsel, ts0, ts1, ts2, ts3;  // refresh: only block pairs with a block in [ts0, ts1) or [ts2, ts3)
   int32_t rect, si, sj, njc;        // band enumerated by si x sj block rectangles
   const double* thr;                // candidate lists (CandBufs)
+  const float* thr32;               // the same thresholds as fp32 rounded toward -inf (k_thr_f32)
   uint32_t* ccnt;
   uint32_t* cidx;
   double* cval;
