@@ -823,6 +823,9 @@ int64_t multi_slab_rows(cms_handle* h, int64_t n) {
   const double have = (double)free_b + (double)h->ws_slab.bytes - 6.0 * (double)(1ULL << 30);
   int64_t rows = (int64_t)(have / (8.0 * (double)std::max<int64_t>(1, n)));
   rows = std::min<int64_t>(rows, ((int64_t(1) << 32) / std::max<int64_t>(1, n)));
+#ifdef CMS_MULTI_SLAB_GIB  // A/B builds: a smaller slab (fewer bytes in the first job's allocations)
+  rows = std::min<int64_t>(rows, ((int64_t)CMS_MULTI_SLAB_GIB << 27) / std::max<int64_t>(1, n));
+#endif
   rows = rows / 128 * 128;
   return std::max(base, rows);
 }

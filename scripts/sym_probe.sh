@@ -14,5 +14,5 @@ for arm in $ARMS; do
   esac
   env "${envs[@]}" timeout -k 10 240 python -u scripts/cos_job_probe.py 1000000 500000000 8192 100 0 \
       > gpurun_out/sym_${tag}.json 2> gpurun_out/sym_${tag}.err || { echo "arm $tag failed"; tail -5 gpurun_out/sym_${tag}.err; exit 1; }
-  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['wall_timed_s'],3), {k: round(v[0],1) for k, v in d['timing_ms'].items()})" gpurun_out/sym_${tag}.json $tag
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], 'first', round(d['wall_first_s'],3), 'steady', round(d['wall_timed_s'],3), {k: round(v[0],1) for k, v in d['timing_ms'].items()})" gpurun_out/sym_${tag}.json $tag
 done
