@@ -376,10 +376,8 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   }
   hp.width = (uint32_t)h->p.width;
   hp.depth = h->p.depth;
-  hp.pow2 = (h->p.width & (h->p.width - 1)) == 0;
-  hp.wmask = hp.pow2 ? (uint32_t)(h->p.width - 1) : 0u;
-  hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)h->p.width;
   hp.frac_bits = p->frac_bits;
+  hash_finish(hp);
   if (per_owner) h->dw = 0;
 
   size_t tbytes = sizeof(uint16_t) * (size_t)h->n * (size_t)h->dw;
@@ -490,6 +488,7 @@ int cms_set_hash_params(cms_handle* h, const int64_t* a, const int64_t* b, int32
     h->hp.ap[i] = reduce_key(a[i]);  // any int64, as BigInteger.valueOf(a).mod(p) takes it
     h->hp.bp[i] = reduce_key(b[i]);
   }
+  hash_finish(h->hp);
   return CMS_OK;
 }
 

@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 #define CMS_MID_LIST_KEYS (kBuildThreads * kKeyRegs)
 #endif
 constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
-template <int SV>
+template <int SV, int D>
 // 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
 // (it spilled there); the build measured the same (profiles/r04/ab_*_s5)
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
@@ -630,8 +630,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       // lt >= 0: the key's list index -- a list row's entries leave during
       // the count (a count past 255 later rewrites the slot as u16 rows)
       auto add_all = [&](uint64_t kr, uint32_t inc, int64_t lt) {
-        for (int d = 0; d < hp.depth; ++d) {
-          const uint32_t bk = bucket(hp, d, kr);
+        each_bucket<D>(hp, kr, [&](int d, uint32_t bk) {
           if (lt >= 0) lst[1 + (int64_t)d * m + lt] = (uint16_t)bk;
           const uint32_t c = (uint32_t)d * (uint32_t)w + bk;
           const uint32_t sh = (c & ((1u << lga) - 1u)) * (uint32_t)ab;
@@ -639,7 +638,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
           const uint32_t nv = old + inc;
           ovf |= nv > capa || inc > capa;  // carried into the next counter: a wider form
           vmax = max(vmax, nv);
-        }
+        });
       };
       if (cached) {
 #pragma unroll
@@ -1032,6 +1031,8 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
 // share a CU at d = 5, w = 8192.
 constexpr int kSliceThreads = 512;
 constexpr int64_t kHotSlice = 65535;  // keys per slice (u16 image, frac_bits 0)
+// D: the depth when it is 4 or 5 (rows unrolled, each_bucket), else 0
+template <int D>
 __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* lo_, const int64_t* hi_, Keys keys,
                                                                 HashParams hp, int64_t slice, const HotInfo* hot,
                                                                 const int2* smap, const uint32_t* counters,
@@ -1080,10 +1081,10 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
     for (int u = 0; u < kPer; ++u) {
       if (base + tid + (int64_t)u * kSliceThreads >= end) continue;  // (a raw key may be any 64-bit value)
       const uint64_t kp = keys.resolve(kk[u]);
-      for (int r = 0; r < hp.depth; ++r) {
-        const uint32_t c = (uint32_t)r * (uint32_t)w + bucket(hp, r, kp);
+      each_bucket<D>(hp, kp, [&](int r, uint32_t bk) {
+        const uint32_t c = (uint32_t)r * (uint32_t)w + bk;
         atomicAdd(&lds[c >> 1], one << ((c & 1u) << 4));
-      }
+      });
     }
   }
   __syncthreads();
@@ -1234,11 +1235,14 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     auto launch_slices = [&]() -> int {
       if (!fast_slices) return CMS_OK;
       static bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)k_build_slices, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        for (const void* f : {(const void*)k_build_slices<0>, (const void*)k_build_slices<4>,
+                              (const void*)k_build_slices<5>})
+          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
       (void)attr;
-      hipLaunchKernelGGL(k_build_slices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
+      auto kslices = h->p.depth == 5 ? k_build_slices<5> : h->p.depth == 4 ? k_build_slices<4> : k_build_slices<0>;
+      hipLaunchKernelGGL(kslices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
                          keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
       CMS_HIP(hipGetLastError());
       return CMS_OK;
@@ -1287,7 +1291,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0);
       // the u8 all-rows image when a [d][w] byte image fits 64 KB (config 3: 40 KB)
       const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, (size_t)h->dw / 2);
-      hipLaunchKernelGGL(k_build_mid<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
+      auto kmid = h->p.depth == 5   ? k_build_mid<kBuildStoreForm, 5>
+                  : h->p.depth == 4 ? k_build_mid<kBuildStoreForm, 4>
+                                    : k_build_mid<kBuildStoreForm, 0>;
+      hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
                          dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                          h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);

@@ -11,7 +11,19 @@
 // reciprocal otherwise.  Every step is exact integer arithmetic, so the
 // bucket equals the BigInteger result bit-for-bit for every int64 key
 // (negative keys included).
+//
+// Power-of-two widths (every fixed-shape config) take a cheaper exact route
+// for reduced keys below 2^32 (bucket_q): with X = a'k' + b' and
+// q = floor(X / p), s = X - q p == X + 25 q (mod 2^m) because p == -25
+// (mod 2^m) for m <= 63, so the bucket needs only q and the low m bits of
+// a', k', b' (24-bit multiplies).  q comes from one fp64 FMA,
+// y = fma(a'/p, k', b'/p) (both quotients rounded once on the host); its error
+// is below 2^-20 (a'/p within 2^-53 times k' < 2^32, plus the FMA's rounding
+// at y < 2^32), so floor(y) == q whenever y's fractional part lies in
+// [2^-16, 1 - 2^-16] -- otherwise (about 1 hash in 30,000) the folding
+// route above decides.  Either way the bucket is the BigInteger one.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #ifndef CMS_HD
@@ -35,7 +47,24 @@ struct HashParams {
   int32_t depth;
   int32_t pow2;
   int32_t frac_bits;           // counters hold preference * 2^frac_bits
+  int32_t fastq;               // bucket_q applies: power-of-two width <= 2^24
+  double qa[CMS_MAX_DEPTH];    // a'/p rounded to double (bucket_q)
+  double qb[CMS_MAX_DEPTH];    // b'/p rounded to double
 };
+
+// The derived fields of a HashParams whose ap, bp, width and depth are set.
+inline void hash_finish(HashParams& hp) {
+  hp.pow2 = hp.width != 0 && (hp.width & (hp.width - 1)) == 0;
+  hp.wmask = hp.pow2 ? hp.width - 1u : 0u;
+  hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)hp.width;
+  hp.fastq = hp.pow2 && hp.width <= (1u << 24);
+  for (int i = 0; i < CMS_MAX_DEPTH; ++i) {
+    // x87 long double holds a', b' and p exactly; the quotient rounds once
+    // to 64 bits, then to 53 (error < 2^-53 relative, far inside the margin)
+    hp.qa[i] = i < hp.depth ? (double)((long double)hp.ap[i] / (long double)kPrime) : 0.0;
+    hp.qb[i] = i < hp.depth ? (double)((long double)hp.bp[i] / (long double)kPrime) : 0.0;
+  }
+}
 
 // key mod p in [0, p) for any signed 64-bit key.
 CMS_HD uint64_t reduce_key(int64_t k) {
@@ -79,8 +108,8 @@ CMS_HD uint64_t mulmod_p_small(uint64_t x, uint32_t y) {
   return z;
 }
 
-// Bucket of a reduced key in sketch row r.
-CMS_HD uint32_t bucket(const HashParams& hp, int r, uint64_t kp) {
+// Bucket of a reduced key in sketch row r, by the folding route.
+CMS_HD uint32_t bucket_exact(const HashParams& hp, int r, uint64_t kp) {
   uint64_t s = ((kp >> 32) == 0 ? mulmod_p_small(hp.ap[r], (uint32_t)kp) : mulmod_p(hp.ap[r], kp)) + hp.bp[r];  // < 2p
   if (s >= kPrime) s -= kPrime;
   if (hp.pow2) return (uint32_t)(s & hp.wmask);
@@ -88,6 +117,65 @@ CMS_HD uint32_t bucket(const HashParams& hp, int r, uint64_t kp) {
   uint64_t rem = s - q * hp.width;
   while (rem >= hp.width) rem -= hp.width;
   return (uint32_t)rem;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define CMS_MUL24(x, y) __umul24((x), (y))
+#else
+#define CMS_MUL24(x, y) (((x) & 0xFFFFFFu) * ((y) & 0xFFFFFFu))
+#endif
+constexpr double kQEps = 1.0 / 65536.0;  // fractional-part margin of bucket_q (error < 2^-20)
+
+// bucket_q (header comment): hp.fastq, kp < 2^32; kf = (double)kp,
+// km = kp & wmask.  The low m bits: a'k' + b' + 25 q (mod 2^m), m <= 24, by
+// 24-bit multiplies (q's low 24 bits suffice).  Inside the margin the
+// estimate q0 = floor(y) is off by at most one, in the direction the
+// fractional part says, and the wrapping 64-bit residue s = X - q0 p
+// (mod 2^64) settles it: s < p exactly when q0 is right.
+CMS_HD uint32_t bucket_q(const HashParams& hp, int r, uint64_t kp, double kf, uint32_t km) {
+  const double y = fma(hp.qa[r], kf, hp.qb[r]);
+  const double fl = floor(y);
+  const double fr = y - fl;  // exact
+  union {
+    double d;
+    uint64_t u;
+  } qb;
+  qb.d = fl + 4503599627370496.0;  // 2^52: the integer q0 < 2^32 in the low mantissa bits
+  uint32_t q = (uint32_t)qb.u;
+  if (!(fr >= kQEps && fr <= 1.0 - kQEps)) {  // about 1 hash in 30,000
+    const uint64_t x = hp.ap[r] * kp + hp.bp[r];                      // X mod 2^64
+    const uint64_t s = x - (((uint64_t)q << 63) - 25u * (uint64_t)q);  // X - q0 p mod 2^64 (p = 2^63 - 25)
+    if (s >= kPrime) q = fr < 0.5 ? q - 1u : q + 1u;
+  }
+  const uint32_t xm = CMS_MUL24((uint32_t)hp.ap[r] & hp.wmask, km) + (uint32_t)hp.bp[r];
+  return (xm + CMS_MUL24(q, 25u)) & hp.wmask;
+}
+
+// Bucket of a reduced key in sketch row r.
+CMS_HD uint32_t bucket(const HashParams& hp, int r, uint64_t kp) {
+  if (hp.fastq && (kp >> 32) == 0) return bucket_q(hp, r, kp, (double)(uint32_t)kp, (uint32_t)kp & hp.wmask);
+  return bucket_exact(hp, r, kp);
+}
+
+// All d buckets of one reduced key: f(r, bucket).  D > 0: the handle's depth
+// is exactly D and the rows unroll (their constants stay in scalar registers
+// across a key loop instead of being reloaded per row; a key below 2^32 at a
+// power-of-two width converts once for all rows).  D == 0: any depth.
+template <int D, typename F>
+CMS_HD void each_bucket(const HashParams& hp, uint64_t kp, F&& f) {
+  if (D > 0) {
+    if (hp.fastq && (kp >> 32) == 0) {
+      const double kf = (double)(uint32_t)kp;
+      const uint32_t km = (uint32_t)kp & hp.wmask;
+#pragma unroll
+      for (int r = 0; r < D; ++r) f(r, bucket_q(hp, r, kp, kf, km));
+    } else {
+#pragma unroll
+      for (int r = 0; r < D; ++r) f(r, bucket_exact(hp, r, kp));
+    }
+  } else {
+    for (int r = 0; r < hp.depth; ++r) f(r, bucket(hp, r, kp));
+  }
 }
 
 // Bucket for an arbitrary width w with its Barrett constant floor((2^64-1)/w)

@@ -12,11 +12,42 @@ extern "C" void host_buckets(const int64_t* a, const int64_t* b, int depth, int 
   }
   hp.width = (uint32_t)width;
   hp.depth = depth;
-  hp.pow2 = (width & (width - 1)) == 0;
-  hp.wmask = hp.pow2 ? (uint32_t)(width - 1) : 0u;
-  hp.barrett = hp.pow2 ? 0 : (~0ULL) / (uint64_t)width;
+  cms::hash_finish(hp);
   for (int64_t i = 0; i < n; ++i) {
     uint64_t kp = cms::reduce_key(keys[i]);
     for (int r = 0; r < depth; ++r) out[i * depth + r] = (int32_t)cms::bucket(hp, r, kp);
   }
+}
+
+// The same keys through each_bucket (the kernels' unrolled form) and through
+// the folding route alone; fallbacks[0] counts the bucket_q hashes whose
+// fractional part fell inside the margin (decided by the folding route).
+extern "C" void host_buckets_modes(const int64_t* a, const int64_t* b, int depth, int width, const int64_t* keys,
+                                   int64_t n, int32_t* out_each, int32_t* out_exact, int64_t* fallbacks) {
+  cms::HashParams hp{};
+  for (int i = 0; i < depth; ++i) {
+    hp.ap[i] = cms::reduce_key(a[i]);
+    hp.bp[i] = cms::reduce_key(b[i]);
+  }
+  hp.width = (uint32_t)width;
+  hp.depth = depth;
+  cms::hash_finish(hp);
+  int64_t fb = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    uint64_t kp = cms::reduce_key(keys[i]);
+    auto put = [&](int r, uint32_t c) { out_each[i * depth + r] = (int32_t)c; };
+    if (depth == 4) cms::each_bucket<4>(hp, kp, put);
+    else if (depth == 5) cms::each_bucket<5>(hp, kp, put);
+    else if (depth == 6) cms::each_bucket<6>(hp, kp, put);
+    else cms::each_bucket<0>(hp, kp, put);
+    for (int r = 0; r < depth; ++r) {
+      out_exact[i * depth + r] = (int32_t)cms::bucket_exact(hp, r, kp);
+      if (hp.fastq && (kp >> 32) == 0) {
+        const double y = fma(hp.qa[r], (double)(uint32_t)kp, hp.qb[r]);
+        const double fr = y - floor(y);
+        if (!(fr >= cms::kQEps && fr <= 1.0 - cms::kQEps)) ++fb;
+      }
+    }
+  }
+  fallbacks[0] = fb;
 }

@@ -55,3 +55,61 @@ def test_extreme_hash_params(shim, oracle):
     b = np.array([2 ** 63 - 1, -2 ** 63, 9223372036854775800, 0, 9223372036854775783, 5], np.int64)
     for w in [1024, 1000]:
         np.testing.assert_array_equal(_host(shim, a, b, w, keys), oracle.hash_keys(a, b, w, keys))
+
+
+def _modes(shim, a, b, width, keys):
+    keys = np.ascontiguousarray(keys, np.int64)
+    d = len(a)
+    each = np.zeros((keys.size, d), np.int32)
+    exact = np.zeros((keys.size, d), np.int32)
+    fb = np.zeros(1, np.int64)
+    vp = ctypes.c_void_p
+    shim.host_buckets_modes(a.ctypes.data_as(vp), b.ctypes.data_as(vp), d, width, keys.ctypes.data_as(vp),
+                            ctypes.c_int64(keys.size), each.ctypes.data_as(vp), exact.ctypes.data_as(vp),
+                            fb.ctypes.data_as(vp))
+    return each, exact, int(fb[0])
+
+
+@pytest.mark.parametrize("depth", [4, 5, 6, 7])
+@pytest.mark.parametrize("width", [1, 2, 1024, 4096, 8192, 1 << 20, 1 << 24, 1 << 25])
+def test_quotient_route_small_keys(shim, oracle, depth, width):
+    """bucket_q (the fp64-quotient route for keys below 2^32 at power-of-two
+    widths) and each_bucket's unrolled rows equal the folding route and the
+    oracle, margin fallbacks included (about 1 hash in 30,000 takes one)."""
+    rng = np.random.Generator(np.random.PCG64(width * 10 + depth))
+    keys = np.concatenate([
+        rng.integers(0, 2 ** 32, size=400000, dtype=np.int64),
+        rng.integers(0, 10_000_000, size=100000, dtype=np.int64),
+        np.arange(0, 20000, dtype=np.int64),
+        np.array([2 ** 32 - 1, 2 ** 32, 2 ** 31, 2 ** 31 - 1, -1, 0], np.int64),
+    ])
+    a, b = oracle.hash_params(depth * 7 + 1, depth)
+    each, exact, fb = _modes(shim, a, b, width, keys)
+    np.testing.assert_array_equal(each, exact)
+    np.testing.assert_array_equal(each, oracle.hash_keys(a, b, width, keys))
+    if 1 < width <= (1 << 24):
+        assert fb > 0  # the margin route ran (and agreed)
+
+
+def test_quotient_route_margin_cases(shim, oracle):
+    """Keys whose quotient (a'k + b') / p lies within 2^-16 of an integer for
+    some row: the fp64 floor alone is unreliable there, so the residue check
+    decides.  Found by exact search over a key range per row."""
+    a, b = oracle.hash_params(42, 5)
+    p = 2 ** 63 - 25
+    picked = []
+    ks = np.arange(0, 3_000_000, dtype=np.int64)
+    for r in range(5):
+        ar, br = int(a[r]) % p, int(b[r]) % p
+        # fractional part of (ar k + br) / p in units of p, vectorised with
+        # Python ints over a strided subset (exact)
+        sub = ks[r::7]
+        fr = np.array([((ar * int(k) + br) % p) for k in sub], dtype=object)
+        near = [int(k) for k, f in zip(sub, fr) if f < p >> 17 or f > p - (p >> 17)]
+        picked += near[:200]
+    keys = np.array(sorted(set(picked)), np.int64)
+    assert keys.size > 20
+    for w in [1024, 8192, 1 << 20]:
+        each, exact, fb = _modes(shim, a, b, w, keys)
+        assert fb >= keys.size  # every picked key took the margin route in its row
+        np.testing.assert_array_equal(each, oracle.hash_keys(a, b, w, keys))
