@@ -408,6 +408,96 @@ def config1(budget_s=3.0):
                    "width_range": [int(ws.min()), int(ws.max())], "depth_range": [int(ds.min()), int(ds.max())],
                    "sketch_counters": int((ws.astype(np.int64) * ds).sum())})
     out["gpu_per_owner_shapes"] = po
+    out["recommender"] = config1_recommender()
+    return out
+
+
+def config1_recommender(nn=50, how_many=10, reps=5):
+    """The fork's use case on config 1's data:
+    GenericUserBasedRecommender.recommend(user, 10) for ALL 943 users of the
+    ML-100K-shaped stand-in (user-owner orientation: sketches keyed by item
+    ID, d=4, w=1024), NearestNUserNeighborhood(50) and the CosineCM
+    point-query estimate with EstimatedPreferenceCapper
+    (GenericUserBasedRecommender.java:84-184, NearestNUserNeighborhood.java:
+    84-95).  GPU: every user's neighbourhood in one cms_top_k_all, the
+    candidates (the neighbours' items minus the user's own) from the
+    incidence matrix, every candidate's estimate in one
+    cms_estimate_preferences_batch, the top 10 per user; timed end to end
+    (host glue included) over `reps` runs after a warm-up.  CPU beside it:
+    oracle/cms_baseline.c orc_recommend_par (prebuilt fp64 sketches, the same
+    neighbourhood / candidates / estimates) on all the run's threads and on
+    one.  The tie order among equal estimates follows FastIDSet in the
+    reference; this leg orders ties by item ID (the -m gpu test
+    tests/test_gpu_recommender.py checks exact lists with the FastIDSet
+    restatement)."""
+    from oracle import oracle as O
+    from mahout_amd import SketchTable
+    from mahout_amd.synth import movielens_like, to_csr
+    users, items, ratings = movielens_like()
+    uid, iid = np.unique(users), np.unique(items)
+    ur, ir = np.searchsorted(uid, users), np.searchsorted(iid, items)
+    nu, ni, d, w = uid.size, iid.size, 4, 1024
+    cap = (float(ratings.min()), float(ratings.max()))
+    inc = np.zeros((nu, ni), np.float32)
+    inc[ur, ir] = 1.0
+    out = {"workload": f"GenericUserBasedRecommender.recommend(user, {how_many}) for all {nu} users of the "
+                       f"ML-100K-shaped stand-in ({users.size} ratings, {ni} items), NearestNUserNeighborhood({nn}), "
+                       f"CosineCM d={d} w={w} point-query estimates, EstimatedPreferenceCapper{cap}",
+           "users": nu}
+    with SketchTable(nu, depth=d, width=w, seed=42, owner_ids=uid) as t:
+        t.ingest(users, items, ratings)
+        t.finalize()
+
+        def run():
+            ids, _, cnt = t.top_k_all(nn)  # every user's neighbourhood (NearestNUserNeighborhood order)
+            valid = np.arange(nn)[None, :] < cnt[:, None]
+            adj = np.zeros((nu, nu), np.float32)
+            rr = np.repeat(np.arange(nu), cnt)
+            adj[rr, np.searchsorted(uid, ids[valid])] = 1.0
+            cand = (adj @ inc > 0) & (inc == 0)  # getAllOtherItems
+            cu, ci = np.nonzero(cand)
+            it_off = np.zeros(nu + 1, np.int64)
+            np.cumsum(np.bincount(cu, minlength=nu), out=it_off[1:])
+            nb_off = np.zeros(nu + 1, np.int64)
+            np.cumsum(cnt, out=nb_off[1:])
+            est = t.estimate_preferences_batch(uid, nb_off, ids[valid], it_off, iid[ci], cap)
+            # TopItems.getTopItems: the how_many best values per user (NaN out)
+            ok = ~np.isnan(est)
+            order = np.lexsort((ci[ok], -est[ok], cu[ok]))
+            u_ok, i_ok, e_ok = cu[ok][order], ci[ok][order], est[ok][order]
+            first = np.searchsorted(u_ok, np.arange(nu))
+            rank = np.arange(u_ok.size) - first[u_ok]
+            keep = rank < how_many
+            return int(ci.size), u_ok[keep], iid[i_ok[keep]], e_ok[keep]
+
+        run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            q, ru, ritems, rvals = run()
+        dt = (time.perf_counter() - t0) / reps
+    out["gpu"] = {"all_users_s": dt, "users_per_s": nu / dt, "candidate_estimates": q,
+                  "estimates_per_s": q / dt, "recommended_checksum": float(rvals.astype(np.float64).sum()),
+                  "full_lists": int((np.bincount(ru, minlength=nu) == how_many).sum())}
+    a, b = O.hash_params(42, d)
+    table = O.build_table(nu, d, w, a, b, ur, items, ratings)
+    off, keys_idx, _ = to_csr(ur, ir, nu, ratings)
+    cpu = {}
+    T = host_threads()
+    for th in (T, 1):
+        hi = nu if th == T else max(1, nu // 8)
+        t0 = time.perf_counter()
+        nest, cs = O.recommend_par(table, a, b, off, keys_idx.astype(np.int32), iid, nn, how_many, 0, hi, th, cap)
+        dt = time.perf_counter() - t0
+        cpu[f"efficient_{th}t"] = {"users_per_s": hi / dt, "estimates_per_s": nest / dt, "users": int(hi),
+                                   "seconds": round(dt, 3), "extrapolated": hi < nu}
+        if th == T:
+            cpu[f"efficient_{th}t"]["candidate_estimates"] = int(nest)
+            cpu[f"efficient_{th}t"]["recommended_checksum"] = cs
+    out["cpu"] = cpu
+    out["cpu_threads"] = T
+    out["cpu_note"] = BASELINE_NOTE
+    out["vs_cpu_all_threads"] = out["gpu"]["users_per_s"] / cpu[f"efficient_{T}t"]["users_per_s"]
     return out
 
 

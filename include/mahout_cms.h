@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define CMS_ABI_VERSION 1
+#define CMS_ABI_VERSION 2 /* 2: cms_stats leads with struct_size */
 
 /* ---- status codes (mapped to Java exceptions by the JNI shim) ---------- */
 #define CMS_OK 0
@@ -259,6 +259,16 @@ int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out);
 int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neighbor_ids, int64_t m,
                              const int64_t* item_keys, int64_t q, int32_t use_capper, float cap_min, float cap_max,
                              float* out);
+/* cms_estimate_preferences for n users in one call -- the estimate phase of
+ * GenericUserBasedRecommender.recommend (:84-105) for a whole user batch:
+ * user u's neighbourhood is neighbor_ids[nb_offsets[u] .. nb_offsets[u+1])
+ * (in NearestNUserNeighborhood order) and its candidate items
+ * item_keys[item_offsets[u] .. item_offsets[u+1]); out is parallel to
+ * item_keys.  Both offset arrays hold n + 1 non-decreasing entries from 0.
+ * Every estimate equals the single-user call's (same order of fp64 sums). */
+int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
+                                   const int64_t* neighbor_ids, const int64_t* item_offsets, const int64_t* item_keys,
+                                   int32_t use_capper, float cap_min, float cap_max, float* out);
 /* GenericUserBasedRecommender.mostSimilarUserIDs(id, k) with the CosineCM
  * estimator (:119-127, :231-247) and TopItems.getTopUsers (TopItems.java:91-136):
  * the first k other owners under (similarity desc, ID asc), NaN excluded.
@@ -359,6 +369,18 @@ int cms_read_counters(cms_handle* h, int64_t row_begin, int64_t row_count, doubl
  * consumer of the sketches (getExportedCMProfile for many owners,
  * CosineCM.java:60-67) and for whole-table checks at sizes the host cannot hold. */
 int cms_read_counters_device(cms_handle* h, int64_t row_begin, int64_t row_count, uint32_t* d_out);
+/* How each owner's counters are stored (no reference counterpart: the
+ * reference keeps every sketch as fp64): out_form[i] is one of CMS_FORM_*,
+ * out_bound[i] the proven bound on the owner's counters the form was chosen
+ * for (0 for u32 rows; either output may be NULL).  For capacity checks. */
+#define CMS_FORM_U32 0  /* hot row: u32 slot */
+#define CMS_FORM_U16 1
+#define CMS_FORM_U8 2
+#define CMS_FORM_U4 3
+#define CMS_FORM_U2 4
+#define CMS_FORM_U1 5
+#define CMS_FORM_LIST 6 /* sparse key-bucket list */
+int cms_owner_forms(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t* out_form, uint32_t* out_bound);
 
 /* ---- per-owner sketch shapes: CosineCM with its CountMinSketchConfig --------
  * The reference sizes every owner's sketch separately.  CountMinSketchConfig
@@ -403,6 +425,7 @@ int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capaci
 
 /* ---- instrumentation ------------------------------------------------------- */
 typedef struct cms_stats {
+  uint32_t struct_size;     /* sizeof(cms_stats) as the caller compiled it: only fields that fit are written */
   int64_t pairs_ingested;   /* update() calls applied on this rank */
   int64_t num_owners;
   int32_t depth, width;
@@ -425,6 +448,8 @@ typedef struct cms_stats {
   int32_t device;            /* HIP device ordinal of the handle */
   int64_t list_rows;         /* narrow owners stored as sparse key-bucket lists (2 + 2 d m bytes, m keys) */
 } cms_stats;
+/* out->struct_size must be set (at least through pairs_ingested); a caller
+ * built against an older, shorter cms_stats receives the fields it knows. */
 int cms_get_stats(cms_handle* h, cms_stats* out);
 
 /* Per-kernel HIP-event timing on the handle's stream (off by default).

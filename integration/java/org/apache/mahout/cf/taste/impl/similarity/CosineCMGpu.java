@@ -16,6 +16,7 @@
 package org.apache.mahout.cf.taste.impl.similarity;
 
 import java.util.Collection;
+import java.util.concurrent.locks.ReentrantReadWriteLock;
 
 import org.apache.mahout.cf.taste.common.NoSuchItemException;
 import org.apache.mahout.cf.taste.common.NoSuchUserException;
@@ -50,6 +51,12 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private final long[] hashA;  // a HashFunctionBuilder's drawn (a_i, b_i), or null: drawn from seed
   private final long[] hashB;
   private volatile long handle;  // cms_handle*
+  /**
+   * Every native call on the handle holds the read side; build() swaps in a
+   * new table and close() ends it under the write side, so a handle is
+   * destroyed only once no call that read it is still inside the library.
+   */
+  private final ReentrantReadWriteLock handleLock = new ReentrantReadWriteLock();
   private volatile int builtUsers = -1;  // DataModel.getNumUsers() / getNumItems() the table was built from
   private volatile int builtItems = -1;
 
@@ -209,13 +216,33 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
       nativeDestroy(h);
       throw e;
     }
-    long old = handle;
-    handle = h;
-    builtUsers = n;
-    builtItems = numItems;
-    if (old != 0) {
-      nativeDestroy(old);
+    handleLock.writeLock().lock();
+    try {
+      long old = handle;
+      handle = h;
+      builtUsers = n;
+      builtItems = numItems;
+      if (old != 0) {
+        nativeDestroy(old);
+      }
+    } finally {
+      handleLock.writeLock().unlock();
     }
+  }
+
+  /** The current handle, with the read side held: pair with release(). */
+  private long acquire() throws TasteException {
+    handleLock.readLock().lock();
+    long h = handle;
+    if (h == 0) {
+      handleLock.readLock().unlock();
+      throw new TasteException("CosineCMGpu is closed");
+    }
+    return h;
+  }
+
+  private void release() {
+    handleLock.readLock().unlock();
   }
 
   /** The DataModel's user or item count differs from the one the table was built from. */
@@ -291,7 +318,12 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   /** CosineCM.userSimilarity (CosineCM.java:83-96). */
   @Override
   public double userSimilarity(long userID1, long userID2) throws TasteException {
-    return nativeSimilarity(handle, userID1, userID2, false);
+    long h = acquire();
+    try {
+      return nativeSimilarity(h, userID1, userID2, false);
+    } finally {
+      release();
+    }
   }
 
   @Override
@@ -305,12 +337,22 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   /** Sketch cosine between owners; owners are items over a transposed DataModel. */
   @Override
   public double itemSimilarity(long itemID1, long itemID2) throws TasteException {
-    return nativeSimilarity(handle, itemID1, itemID2, true);
+    long h = acquire();
+    try {
+      return nativeSimilarity(h, itemID1, itemID2, true);
+    } finally {
+      release();
+    }
   }
 
   @Override
   public double[] itemSimilarities(long itemID1, long[] itemID2s) throws TasteException {
-    return nativeSimilarities(handle, itemID1, itemID2s);
+    long h = acquire();
+    try {
+      return nativeSimilarities(h, itemID1, itemID2s);
+    } finally {
+      release();
+    }
   }
 
   /** GenericUserBasedRecommender.mostSimilarUserIDs + TopItems.getTopUsers semantics. */
@@ -318,22 +360,42 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
     if (howMany < 1) {
       throw new IllegalArgumentException("howMany must be at least 1");
     }
-    return nativeMostSimilar(handle, ownerID, howMany);
+    long h = acquire();
+    try {
+      return nativeMostSimilar(h, ownerID, howMany);
+    } finally {
+      release();
+    }
   }
 
   /** DoubleCountMinSketch.get(key) on the owner's sketch (point query). */
   public double pointQuery(long ownerID, long key) throws TasteException {
-    return nativePointQuery(handle, ownerID, key);
+    long h = acquire();
+    try {
+      return nativePointQuery(h, ownerID, key);
+    } finally {
+      release();
+    }
   }
 
   /** {width, depth} of the owner's own sketch (per-owner shapes). */
   int[] ownerShape(long ownerID) throws TasteException {
-    return nativeOwnerShape(handle, ownerID);
+    long h = acquire();
+    try {
+      return nativeOwnerShape(h, ownerID);
+    } finally {
+      release();
+    }
   }
 
   /** The owner's own sketch, [depth][width] row-major as DoubleCountMinSketch stores it. */
   double[] readOwnerSketch(long ownerID) throws TasteException {
-    return nativeReadOwnerSketch(handle, ownerID);
+    long h = acquire();
+    try {
+      return nativeReadOwnerSketch(h, ownerID);
+    } finally {
+      release();
+    }
   }
 
   /**
@@ -343,7 +405,12 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
    */
   public float[] estimatePreferences(long userID, long[] neighborhood, long[] itemIDs, float capMin, float capMax)
       throws TasteException {
-    return nativeEstimatePreferences(handle, userID, neighborhood, itemIDs, capMin, capMax);
+    long h = acquire();
+    try {
+      return nativeEstimatePreferences(h, userID, neighborhood, itemIDs, capMin, capMax);
+    } finally {
+      release();
+    }
   }
 
   /**
@@ -351,7 +418,12 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
    * row r of the result holds the IDs for the r-th owner in ascending ID order.
    */
   public long[][] allMostSimilarIDs(int howMany) throws TasteException {
-    return nativeTopKAll(handle, howMany);
+    long h = acquire();
+    try {
+      return nativeTopKAll(h, howMany);
+    } finally {
+      release();
+    }
   }
 
   /**
@@ -361,7 +433,12 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
    * call a whole job; the incremental path serves streaming callers.
    */
   public long[][] allMostSimilarIDsRefreshed(int howMany) throws TasteException {
-    return nativeTopKRefresh(handle, howMany);
+    long h = acquire();
+    try {
+      return nativeTopKRefresh(h, howMany);
+    } finally {
+      release();
+    }
   }
 
   @Override
@@ -375,9 +452,14 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   }
 
   public void close() {
-    if (handle != 0) {
-      nativeDestroy(handle);
-      handle = 0;
+    handleLock.writeLock().lock();
+    try {
+      if (handle != 0) {
+        nativeDestroy(handle);
+        handle = 0;
+      }
+    } finally {
+      handleLock.writeLock().unlock();
     }
   }
 

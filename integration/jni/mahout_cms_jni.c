@@ -116,6 +116,7 @@ JNIEXPORT void JNICALL JFN(nativeIngestCsr)(JNIEnv* env, jclass c, jlong h, jlon
     return;
   }
   cms_stats st;
+  st.struct_size = (uint32_t)sizeof st;
   if (fail(env, cms_get_stats(H(h), &st), 0)) return;
   const jsize no = (*env)->GetArrayLength(env, off);
   const jsize nk = (*env)->GetArrayLength(env, keys);
@@ -227,6 +228,7 @@ typedef int (*top_k_fn)(cms_handle*, int32_t, int64_t*, double*, int32_t*);
 
 static jobjectArray top_k_lists(JNIEnv* env, jlong h, jint k, top_k_fn fn) {
   cms_stats st;
+  st.struct_size = (uint32_t)sizeof st;
   st.pairs_ingested = 0;
   if (fail(env, cms_get_stats(H(h), &st), 0)) return NULL;
   const int64_t n = st.num_owners;

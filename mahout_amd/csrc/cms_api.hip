@@ -803,7 +803,10 @@ int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allr
                             cms_allgather_fn allgather, void* user) {
   if (!h) return set_error(CMS_E_PARAM, "null handle");
   if (world < 1 || rank < 0 || rank >= world) return set_error(CMS_E_PARAM, "bad rank/world");
-  if (world > 1 && (!allreduce || !allgather)) return set_error(CMS_E_PARAM, "null transport function");
+  // every argument check precedes any state change: a rejected call leaves
+  // the handle's communicator, rank and world as they were
+  if ((world > 1 || (h->p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK)) && (!allreduce || !allgather))
+    return set_error(CMS_E_PARAM, "null transport function");
   if (h->f64 && world > 1)
     return set_error(CMS_E_STATE, "fp64 counters are single-GPU: shard sums would not round in the reference's order");
   Guard g(h);
@@ -811,8 +814,6 @@ int cms_comm_init_transport(cms_handle* h, int32_t rank, int32_t world, cms_allr
     (void)ncclCommDestroy(h->comm);
     h->comm = nullptr;
   }
-  if (world == 1 && (h->p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK) && (!allreduce || !allgather))
-    return set_error(CMS_E_PARAM, "null transport function");
   h->rank = world > 1 ? rank : 0;
   h->world = world;
   h->ext_comm = world > 1 || (h->p.flags & CMS_FLAG_COLLECTIVE_SINGLE_RANK);
@@ -1060,6 +1061,68 @@ int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neig
                      false);
 }
 
+int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
+                                   const int64_t* neighbor_ids, const int64_t* item_offsets, const int64_t* item_keys,
+                                   int32_t use_capper, float cap_min, float cap_max, float* out) {
+  if (!h || n < 0 || (n > 0 && (!user_ids || !nb_offsets || !item_offsets)))
+    return set_error(CMS_E_PARAM, "null argument");
+  if (n == 0) return CMS_OK;
+  if (nb_offsets[0] != 0 || item_offsets[0] != 0) return set_error(CMS_E_PARAM, "offsets must start at 0");
+  for (int64_t u = 0; u < n; ++u)
+    if (nb_offsets[u + 1] < nb_offsets[u] || item_offsets[u + 1] < item_offsets[u])
+      return set_error(CMS_E_PARAM, "offsets must not decrease");
+  const int64_t M = nb_offsets[n], Q = item_offsets[n];
+  if ((M > 0 && !neighbor_ids) || (Q > 0 && (!item_keys || !out))) return set_error(CMS_E_PARAM, "null argument");
+  if (Q >= (int64_t(1) << 31)) return set_error(CMS_E_PARAM, "too many candidate items in one batch");
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  if (h->per_owner || h->f64) {  // per-user estimates (their own kernels), one user after another
+    QueryCtx tmp;
+    for (int64_t u = 0; u < n; ++u)
+      if ((rc = estimate_on(h, user_ids[u], neighbor_ids + nb_offsets[u], nb_offsets[u + 1] - nb_offsets[u],
+                            item_keys + item_offsets[u], item_offsets[u + 1] - item_offsets[u], use_capper, cap_min,
+                            cap_max, out + item_offsets[u], h->stream, tmp, false)))
+        return rc;
+    return CMS_OK;
+  }
+  // rows: users [n], then per pair (user row, neighbour row) [M] x 2; the
+  // owner of every candidate [Q]
+  std::vector<int64_t> rows((size_t)(n + 2 * M));
+  std::vector<int32_t> item_user((size_t)Q);
+  for (int64_t u = 0; u < n; ++u) {
+    if ((rc = row_of(h, user_ids[u], &rows[(size_t)u]))) return rc;
+    for (int64_t j = nb_offsets[u]; j < nb_offsets[u + 1]; ++j) {
+      rows[(size_t)(n + j)] = rows[(size_t)u];
+      if ((rc = row_of(h, neighbor_ids[j], &rows[(size_t)(n + M + j)]))) return rc;
+    }
+    for (int64_t i = item_offsets[u]; i < item_offsets[u + 1]; ++i) item_user[(size_t)i] = (int32_t)u;
+  }
+  if (Q == 0) return CMS_OK;
+  DevBuf d_rows, d_off, d_sims, d_items, d_iu, d_out;
+  CMS_HIP(d_rows.ensure(sizeof(int64_t) * rows.size()));
+  CMS_HIP(d_off.ensure(sizeof(int64_t) * (size_t)(n + 1)));
+  CMS_HIP(d_sims.ensure(sizeof(double) * (size_t)std::max<int64_t>(M, 1)));
+  CMS_HIP(d_items.ensure(sizeof(int64_t) * (size_t)Q));
+  CMS_HIP(d_iu.ensure(sizeof(int32_t) * (size_t)Q));
+  CMS_HIP(d_out.ensure(sizeof(float) * (size_t)Q));
+  hipStream_t st = h->stream;
+  CMS_HIP(hipMemcpyAsync(d_rows.ptr, rows.data(), sizeof(int64_t) * rows.size(), hipMemcpyHostToDevice, st));
+  CMS_HIP(hipMemcpyAsync(d_off.ptr, nb_offsets, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, st));
+  CMS_HIP(hipMemcpyAsync(d_items.ptr, item_keys, sizeof(int64_t) * (size_t)Q, hipMemcpyHostToDevice, st));
+  CMS_HIP(hipMemcpyAsync(d_iu.ptr, item_user.data(), sizeof(int32_t) * (size_t)Q, hipMemcpyHostToDevice, st));
+  const int64_t* dr = d_rows.as<int64_t>();
+  // userSimilarity(user, neighbour) for every pair of the batch (:162)
+  if ((rc = pair_cosines_many(h, dr + n, dr + n + M, M, d_sims.as<double>(), nullptr))) return rc;
+  if ((rc = estimate_preferences_batch(h, dr, d_off.as<int64_t>(), dr + n + M, d_sims.as<double>(), d_iu.as<int32_t>(),
+                                       d_items.as<int64_t>(), Q, use_capper, cap_min, cap_max, d_out.as<float>(),
+                                       nullptr)))
+    return rc;
+  CMS_HIP(hipMemcpyAsync(out, d_out.ptr, sizeof(float) * (size_t)Q, hipMemcpyDeviceToHost, st));
+  CMS_HIP(hipStreamSynchronize(st));
+  return CMS_OK;
+}
+
 int cms_point_query(cms_handle* h, int64_t id, int64_t key, double* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
   SharedGuard g(h);
@@ -1271,6 +1334,11 @@ static int top_k_refresh_job(cms_handle* h, int32_t k, int64_t* o_ids, double* o
     for (int64_t r = 0; r < n; ++r) nt += touch[r];
     h->rf_stat_touched = nt;
     h->rf_stat_redo = 0;
+    if (nt == 0) {  // nothing recomputed: the class counts say so (not the previous refresh's)
+      const int64_t nm = h->n_hot_limb, nf = h->n_f4;
+      const int64_t cls[6] = {nm, n - nm - nf, nf, 0, 0, 0};
+      std::copy(cls, cls + 6, h->rf_stat_class);
+    }
     if (nt > 0) {
       CMS_HIP(h->rf_new.ensure((sizeof(int64_t) + sizeof(double)) * (size_t)n * D + sizeof(int32_t) * (size_t)n));
       int64_t* n_ids = h->rf_new.as<int64_t>();
@@ -1498,6 +1566,30 @@ int cms_read_counters_device(cms_handle* h, int64_t row_begin, int64_t row_count
   return read_counters_device(h, row_begin, row_count, d_out);
 }
 
+int cms_owner_forms(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t* out_form, uint32_t* out_bound) {
+  if (!h) return set_error(CMS_E_PARAM, "null argument");
+  if (int rc0 = refuse_per_owner(h, "cms_owner_forms")) return rc0;
+  if (h->f64) return set_error(CMS_E_STATE, "fp64 counters have one form");
+  Guard g(h);
+  if (row_begin < 0 || row_count < 0 || row_begin + row_count > h->n) return set_error(CMS_E_PARAM, "row range");
+  if (row_count == 0) return CMS_OK;
+  std::vector<int32_t> hx((size_t)row_count);
+  CMS_HIP(hipMemcpyAsync(hx.data(), h->d_hidx + row_begin, sizeof(int32_t) * (size_t)row_count, hipMemcpyDeviceToHost,
+                         h->stream));
+  if (out_bound)
+    CMS_HIP(hipMemcpyAsync(out_bound, h->d_cbound + row_begin, sizeof(uint32_t) * (size_t)row_count,
+                           hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  for (int64_t i = 0; i < row_count; ++i) {
+    const int32_t s = hx[(size_t)i];
+    const int32_t f = s >= 0 ? CMS_FORM_U32 : s == kFormU16 ? CMS_FORM_U16 : s == kFormU8 ? CMS_FORM_U8
+                    : s == kFormU4 ? CMS_FORM_U4 : s == kFormU2 ? CMS_FORM_U2 : s == kFormU1 ? CMS_FORM_U1 : CMS_FORM_LIST;
+    if (out_form) out_form[i] = f;
+    if (out_bound && s >= 0) out_bound[i] = 0;
+  }
+  return CMS_OK;
+}
+
 int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capacity, int32_t* width, int32_t* depth) {
   if (!h) return set_error(CMS_E_PARAM, "null argument");
   if (!h->per_owner) return set_error(CMS_E_STATE, "fixed-shape handle: use cms_read_counters");
@@ -1526,6 +1618,13 @@ int cms_read_owner_sketch(cms_handle* h, int64_t id, double* out, int64_t capaci
 
 int cms_get_stats(cms_handle* h, cms_stats* out) {
   if (!h || !out) return set_error(CMS_E_PARAM, "null argument");
+  const uint32_t want = out->struct_size;
+  if (want < offsetof(cms_stats, pairs_ingested) + sizeof(int64_t))
+    return set_error(CMS_E_PARAM, "cms_stats.struct_size %u too small (set it to sizeof(cms_stats))", want);
+  cms_stats full;
+  std::memset(&full, 0, sizeof(full));
+  cms_stats* const dst = out;
+  out = &full;
   Guard g(h);
   out->pairs_ingested = h->pairs_ingested;
   out->num_owners = h->n;
@@ -1562,6 +1661,8 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->comm_kind = h->comm ? 1 : h->ext_comm ? 2 : 0;
   out->device = h->device;
   out->list_rows = forms[6];
+  out->struct_size = (uint32_t)std::min<size_t>(want, sizeof(cms_stats));
+  std::memcpy(dst, out, out->struct_size);  // the fields the caller's struct has room for
   return CMS_OK;
 }
 

@@ -1083,6 +1083,9 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
       const uint64_t kp = keys.resolve(kk[u]);
       each_bucket<D>(hp, kp, [&](int r, uint32_t bk) {
         const uint32_t c = (uint32_t)r * (uint32_t)w + bk;
+#ifdef CMS_BUILD_NOLDSADD  // bound analysis only: hashes kept live, no LDS adds
+        if (c == 0xFFFFFFFFu)
+#endif
         atomicAdd(&lds[c >> 1], one << ((c & 1u) << 4));
       });
     }
@@ -1096,6 +1099,9 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
   for (int jj = tid; jj < words; jj += kSliceThreads) {
     const int j = jj + rot < words ? jj + rot : jj + rot - words;
     const uint32_t v = lds[j];
+#ifdef CMS_BUILD_NOSLICEADD  // bound analysis only: the slices' global atomics skipped
+    if (v == 0xFFFFFFFFu)
+#endif
     if (v) atomicAdd(dst + j, (unsigned long long)(v & 0xFFFFu) | ((unsigned long long)(v >> 16) << 32));
   }
   if (tid == 0) {
@@ -1267,6 +1273,9 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          mid_list, lcnt);
       CMS_HIP(hipGetLastError());
       hipStream_t side = h->side_stream ? h->side_stream : h->stream;
+#ifdef CMS_BUILD_SERIAL  // bound analysis only: the classes' kernels one after another (isolated durations)
+      side = h->stream;
+#endif
       // once the side stream has forked, every exit (error returns included)
       // joins it back: the caller's next work on h->stream may reuse or free
       // the buffers the side kernels are still writing

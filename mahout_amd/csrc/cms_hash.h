@@ -163,6 +163,15 @@ CMS_HD uint32_t bucket(const HashParams& hp, int r, uint64_t kp) {
 // power-of-two width converts once for all rows).  D == 0: any depth.
 template <int D, typename F>
 CMS_HD void each_bucket(const HashParams& hp, uint64_t kp, F&& f) {
+#ifdef CMS_BUILD_CHEAPHASH  // bound analysis only: a trivial hash instead of the exact mod-p one
+  if (D > 0) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) f(r, (uint32_t)((kp >> r) & hp.wmask));
+  } else {
+    for (int r = 0; r < hp.depth; ++r) f(r, (uint32_t)((kp >> r) & hp.wmask));
+  }
+  return;
+#endif
   if (D > 0) {
     if (hp.fastq && (kp >> 32) == 0) {
       const double kf = (double)(uint32_t)kp;

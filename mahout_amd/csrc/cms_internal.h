@@ -468,6 +468,12 @@ int partition_to_spans(cms_handle* h, const int64_t* d_row, const int64_t* d_key
 int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m, double* d_out,
                  hipStream_t s = nullptr);
 int point_queries(cms_handle* h, int64_t row, const int64_t* d_keys, int64_t m, double* d_out, hipStream_t s = nullptr);
+int pair_cosines_many(cms_handle* h, const int64_t* d_qrows, const int64_t* d_rows, int64_t m, double* d_out,
+                      hipStream_t s);
+int estimate_preferences_batch(cms_handle* h, const int64_t* d_user_rows, const int64_t* d_nb_off,
+                               const int64_t* d_nb_rows, const double* d_sims, const int32_t* d_item_user,
+                               const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
+                               hipStream_t s);
 int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_rows, const double* d_sims, int64_t m,
                          const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
                          hipStream_t s = nullptr);

@@ -44,14 +44,16 @@ __device__ void seq_row_sums(const TableView& tv, int64_t ra, int64_t rb, int64_
 
 // One workgroup (256 threads) per (query, target) pair.
 __global__ __launch_bounds__(256) void k_pair_cosine(TableView tv, const uint64_t* norm, const double* nsqrt,
-                                                     HashParams hp, int64_t q_row, const int64_t* rows, int64_t m,
-                                                     int64_t nrows, int weighted, double* out) {
+                                                     HashParams hp, int64_t q_row0, const int64_t* q_rows,
+                                                     const int64_t* rows, int64_t m, int64_t nrows, int weighted,
+                                                     double* out) {
   __shared__ uint64_t red[4];
   extern __shared__ uint32_t lc[];  // [w / 4]: a list query row's sketch row as u8 counters (list x list pairs)
   const int64_t t = blockIdx.x;
   if (t >= m) return;
   const int64_t r2 = rows[t];
-  if (r2 < 0 || r2 >= nrows) {
+  const int64_t q_row = q_rows ? q_rows[t] : q_row0;  // one query row, or one per pair (batched estimates)
+  if (r2 < 0 || r2 >= nrows || q_row < 0 || q_row >= nrows) {
     if (threadIdx.x == 0) out[t] = __builtin_nan("");
     return;
   }
@@ -115,7 +117,21 @@ int pair_cosines(cms_handle* h, int64_t q_row, const int64_t* d_rows, int64_t m,
   if (h->f64) return f64_pair_cosines(h, q_row, d_rows, m, d_out, s);
   TimedScope ts(h, "pair_cosine", s == nullptr);
   hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), (size_t)h->p.width, s ? s : h->stream, h->tview(), h->d_norm,
-                     h->d_norm_sqrt, h->hp, q_row, d_rows, m, h->n, (int)h->p.weighting, d_out);
+                     h->d_norm_sqrt, h->hp, q_row, (const int64_t*)nullptr, d_rows, m, h->n, (int)h->p.weighting,
+                     d_out);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+// cos(q_rows[t], rows[t]) for t < m: one launch for the (user, neighbour)
+// pairs of many users (u32 counters).
+int pair_cosines_many(cms_handle* h, const int64_t* d_qrows, const int64_t* d_rows, int64_t m, double* d_out,
+                      hipStream_t s) {
+  if (m <= 0) return CMS_OK;
+  TimedScope ts(h, "pair_cosine", s == nullptr);
+  hipLaunchKernelGGL(k_pair_cosine, dim3((unsigned)m), dim3(256), (size_t)h->p.width, s ? s : h->stream, h->tview(),
+                     h->d_norm, h->d_norm_sqrt, h->hp, (int64_t)0, d_qrows, d_rows, m, h->n, (int)h->p.weighting,
+                     d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
@@ -187,6 +203,61 @@ int estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb_ro
   unsigned grid = (unsigned)std::min<int64_t>((q + 255) / 256, 4096);
   hipLaunchKernelGGL(k_estimate, dim3(grid), dim3(256), 0, s ? s : h->stream, h->tview(), h->hp, user_row, d_nb_rows, d_sims,
                      m, d_items, q, use_capper, lo, hi, d_out);
+  CMS_HIP(hipGetLastError());
+  return CMS_OK;
+}
+
+// k_estimate for many users in one launch: candidate i belongs to user
+// item_user[i], whose neighbourhood (rows and similarities, in the caller's
+// order) is nb_rows / sims [nb_off[u], nb_off[u + 1]).  Each candidate's
+// arithmetic is exactly k_estimate's.
+__global__ void k_estimate_batch(TableView tv, HashParams hp, const int64_t* user_rows, const int64_t* nb_off,
+                                 const int64_t* nb_rows, const double* sims, const int32_t* item_user,
+                                 const int64_t* items, int64_t q, int use_capper, float lo, float hi, float* out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < q; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = item_user[i];
+    const int64_t user_row = user_rows[u];
+    const uint64_t kp = reduce_key(items[i]);
+    uint32_t bk[CMS_MAX_DEPTH];
+    for (int d = 0; d < hp.depth; ++d) bk[d] = (uint32_t)d * hp.width + bucket(hp, d, kp);
+    double preference = 0.0, total = 0.0;
+    int count = 0;
+    for (int64_t j = nb_off[u]; j < nb_off[u + 1]; ++j) {
+      const int64_t r = nb_rows[j];
+      if (r == user_row) continue;
+      double est = DBL_MAX;
+      for (int d = 0; d < hp.depth; ++d) {
+        const double v = (double)tv.get(r, bk[d]);
+        if (v < est) est = v;
+      }
+      const float pref = (float)ldexp(est, -hp.frac_bits);
+      if (pref == 0.0f) continue;
+      const double s = sims[j];
+      if (s != s) continue;
+      preference = __dadd_rn(preference, __dmul_rn(s, (double)pref));
+      total = __dadd_rn(total, s);
+      ++count;
+    }
+    float e = __builtin_nanf("");
+    if (count > 1) {
+      e = (float)__ddiv_rn(preference, total);
+      if (use_capper) {
+        if (e > hi) e = hi;
+        else if (e < lo) e = lo;
+      }
+    }
+    out[i] = e;
+  }
+}
+
+int estimate_preferences_batch(cms_handle* h, const int64_t* d_user_rows, const int64_t* d_nb_off,
+                               const int64_t* d_nb_rows, const double* d_sims, const int32_t* d_item_user,
+                               const int64_t* d_items, int64_t q, int use_capper, float lo, float hi, float* d_out,
+                               hipStream_t s) {
+  if (q <= 0) return CMS_OK;
+  unsigned grid = (unsigned)std::min<int64_t>((q + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_estimate_batch, dim3(grid), dim3(256), 0, s ? s : h->stream, h->tview(), h->hp, d_user_rows,
+                     d_nb_off, d_nb_rows, d_sims, d_item_user, d_items, q, use_capper, lo, hi, d_out);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }

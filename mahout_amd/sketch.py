@@ -294,6 +294,26 @@ class SketchTable:
                                                  int(capper is not None), float(lo), float(hi), _ptr(out)))
         return out
 
+    def estimate_preferences_batch(self, user_ids, nb_offsets, neighbor_ids, item_offsets, item_keys, capper=None):
+        """estimate_preferences for many users in one call
+        (cms_estimate_preferences_batch): user u's neighbourhood is
+        neighbor_ids[nb_offsets[u]:nb_offsets[u+1]], its candidates
+        item_keys[item_offsets[u]:item_offsets[u+1]]; returns one float32
+        estimate per candidate."""
+        us = np.ascontiguousarray(user_ids, np.int64)
+        nbo = np.ascontiguousarray(nb_offsets, np.int64)
+        nb = np.ascontiguousarray(neighbor_ids, np.int64)
+        ito = np.ascontiguousarray(item_offsets, np.int64)
+        it = np.ascontiguousarray(item_keys, np.int64)
+        if nbo.size != us.size + 1 or ito.size != us.size + 1:
+            raise ValueError("offset arrays need len(user_ids) + 1 entries")
+        out = np.zeros(it.size, np.float32)
+        lo, hi = capper if capper is not None else (0.0, 0.0)
+        check(self._lib.cms_estimate_preferences_batch(self._h, us.size, _ptr(us), _ptr(nbo), _ptr(nb), _ptr(ito),
+                                                       _ptr(it), int(capper is not None), float(lo), float(hi),
+                                                       _ptr(out)))
+        return out
+
     def write_similar_items(self, path, k, as_float=True):
         """cms_top_k_all in FileSimilarItemsWriter's CSV format."""
         check(self._lib.cms_write_similar_items(self._h, os.fsencode(path), int(k), int(as_float)))
@@ -432,6 +452,19 @@ class SketchTable:
         check(self._lib.cms_read_counters(self._h, int(row_begin), int(row_count), _ptr(out)))
         return out
 
+    FORMS = ("u32", "u16", "u8", "u4", "u2", "u1", "list")
+
+    def owner_forms(self, row_begin=0, row_count=None):
+        """(form code per owner -- an index into FORMS --, the counter bound
+        each narrow form was chosen for) of owners [row_begin, +row_count)
+        (cms_owner_forms)."""
+        if row_count is None:
+            row_count = self.num_owners - row_begin
+        form = np.zeros(row_count, np.int32)
+        bound = np.zeros(row_count, np.uint32)
+        check(self._lib.cms_owner_forms(self._h, int(row_begin), int(row_count), _ptr(form), _ptr(bound)))
+        return form, bound
+
     def read_counters_device(self, row_begin=0, row_count=None, out=None):
         """Counters [row_count][d][w] on the handle's device, in counter units
         (cms_read_counters_device).  The tensor is torch.int32 holding the u32
@@ -462,6 +495,7 @@ class SketchTable:
     # -- instrumentation --
     def stats(self):
         s = _lib.CmsStats()
+        s.struct_size = ctypes.sizeof(s)
         check(self._lib.cms_get_stats(self._h, ctypes.byref(s)))
         return {f: getattr(s, f) for f, _ in s._fields_}
 

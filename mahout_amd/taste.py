@@ -287,6 +287,214 @@ class GenericUserBasedRecommender:
         except _lib.CmsError as e:
             raise _map_error(e, "user")
 
+    def getAllOtherItems(self, theNeighborhood, theUserID, includeKnownItems=False):
+        """getAllOtherItems (GenericUserBasedRecommender.java:187-198): the
+        neighbours' items as a FastIDSet, the user's own removed."""
+        possible = FastIDSet()
+        for u in theNeighborhood:
+            possible.addAll(self._item_set(u))
+        if not includeKnownItems:
+            possible.removeAll(self._item_set(theUserID))
+        return possible
+
+    def _item_set(self, userID):
+        """GenericDataModel.getItemIDsFromUser (GenericDataModel.java:219-227)."""
+        keys, _ = self._model.getPreferencesFromUser(userID)
+        s = FastIDSet(len(keys))
+        for k in keys.tolist():
+            s.add(k)
+        return s
+
+    def recommend(self, userID, howMany, includeKnownItems=False):
+        """recommend(userID, howMany) (GenericUserBasedRecommender.java:84-105):
+        the neighbourhood, the candidate items in FastIDSet iteration order,
+        their estimates (one GPU call), then TopItems.getTopItems
+        (TopItems.java:47-88) -- a JDK PriorityQueue under the reversed
+        ByValueRecommendedItemComparator and a stable sort, so tied values
+        come out in the reference's order.  [(itemID, float value)]."""
+        if howMany < 1:
+            raise ValueError("howMany must be at least 1")
+        nb = self._nb.getUserNeighborhood(userID)
+        if len(nb) == 0:
+            return []
+        items = self.getAllOtherItems(nb, userID, includeKnownItems).toList()
+        est = self.doEstimatePreferences(userID, nb, items) if items else np.zeros(0, np.float32)
+        return get_top_items(howMany, items, est)
+
+
+def _is_prime(n):
+    """Primality of n < 2^63 (deterministic Miller-Rabin bases)."""
+    if n < 2:
+        return False
+    for p in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        if n % p == 0:
+            return n == p
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for a in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def _next_prime(n):
+    """commons-math3 Primes.nextPrime(n): the smallest prime >= n."""
+    n = max(n, 2)
+    while not _is_prime(n):
+        n += 1
+    return n
+
+
+def next_twin_prime(n):
+    """RandomUtils.nextTwinPrime (math/.../common/RandomUtils.java:86-98): the
+    larger of the first twin-prime pair whose smaller member is >= n."""
+    if n > 2147482949:
+        raise ValueError(n)
+    if n <= 3:
+        return 5
+    nxt = _next_prime(n)
+    while not _is_prime(nxt + 2):
+        nxt = _next_prime(nxt + 4)
+    return nxt + 2
+
+
+class FastIDSet:
+    """T/impl/common/FastIDSet.java: open addressing with double hashing
+    (hash = (int) key & 0x7FFFFFFF, jump = 1 + hash % (size - 2)), REMOVED
+    markers, twin-prime table sizes and float load-factor arithmetic -- what
+    fixes its iteration order (the order TopItems.getTopItems sees the
+    candidates in, hence the order of tied recommendations)."""
+
+    NULL = -(1 << 63)
+    REMOVED = (1 << 63) - 1
+
+    def __init__(self, size=2, loadFactor=1.5):
+        self.lf = np.float32(loadFactor)
+        self.keys = [self.NULL] * next_twin_prime(int(self.lf * np.float32(size)))
+        self.numEntries = 0
+        self.numSlotsUsed = 0
+
+    def _probe(self, key, for_add):
+        h = (key & 0xFFFFFFFF) & 0x7FFFFFFF  # (int) key & 0x7FFFFFFF
+        keys = self.keys
+        n = len(keys)
+        jump = 1 + h % (n - 2)
+        index = h % n
+        cur = keys[index]
+        if not for_add:
+            while cur != self.NULL and key != cur:
+                index -= jump - n if index < jump else jump
+                cur = keys[index]
+            return index
+        while cur != self.NULL and cur != self.REMOVED and key != cur:
+            index -= jump - n if index < jump else jump
+            cur = keys[index]
+        if cur != self.REMOVED:
+            return index
+        add_index = index
+        while cur != self.NULL and key != cur:
+            index -= jump - n if index < jump else jump
+            cur = keys[index]
+        return index if key == cur else add_index
+
+    def add(self, key):
+        key = int(key)
+        if np.float32(self.numSlotsUsed) * self.lf >= np.float32(len(self.keys)):
+            if np.float32(self.numEntries) * self.lf >= np.float32(self.numSlotsUsed):
+                self._rehash(next_twin_prime(int(self.lf * np.float32(len(self.keys)))))
+            else:
+                self._rehash(next_twin_prime(int(self.lf * np.float32(self.numEntries))))
+        index = self._probe(key, True)
+        old = self.keys[index]
+        if old != key:
+            self.keys[index] = key
+            self.numEntries += 1
+            if old == self.NULL:
+                self.numSlotsUsed += 1
+            return True
+        return False
+
+    def remove(self, key):
+        key = int(key)
+        if key in (self.NULL, self.REMOVED):
+            return False
+        index = self._probe(key, False)
+        if self.keys[index] == self.NULL:
+            return False
+        self.keys[index] = self.REMOVED
+        self.numEntries -= 1
+        return True
+
+    def _rehash(self, new_size):
+        old = self.keys
+        self.numEntries = 0
+        self.numSlotsUsed = 0
+        self.keys = [self.NULL] * new_size
+        for k in old:
+            if k != self.NULL and k != self.REMOVED:
+                self.add(k)
+
+    def _live(self):
+        return [k for k in self.keys if k != self.NULL and k != self.REMOVED]
+
+    def addAll(self, other):
+        changed = False
+        for k in other._live():
+            changed |= self.add(k)
+        return changed
+
+    def removeAll(self, other):
+        changed = False
+        for k in other._live():
+            changed |= self.remove(k)
+        return changed
+
+    def toList(self):
+        """Iteration order (KeyIterator: table positions, NULL and REMOVED skipped)."""
+        return self._live()
+
+    def __len__(self):
+        return self.numEntries
+
+
+def _cmp_by_value_reversed(a, b):
+    """Collections.reverseOrder(ByValueRecommendedItemComparator): the queue
+    head is the lowest float value (ByValueRecommendedItemComparator.java:37-41)."""
+    return -1 if a[1] < b[1] else 1 if a[1] > b[1] else 0
+
+
+def get_top_items(howMany, itemIDs, estimates):
+    """TopItems.getTopItems (TopItems.java:47-88) with no rescorer: a
+    PriorityQueue of howMany + 1, items kept while their (double) estimate
+    beats the head once full, then the queue's array order stably sorted by
+    float value descending.  [(itemID, float32 value)]."""
+    q = _JavaPriorityQueue(_cmp_by_value_reversed)
+    full = False
+    lowest = float("-inf")
+    for item, e in zip(itemIDs, estimates):
+        pref = float(e)
+        if pref != pref or (full and not pref > lowest):
+            continue
+        q.add((int(item), np.float32(pref)))
+        if full:
+            q.poll()
+        elif len(q) > howMany:
+            full = True
+            q.poll()
+        lowest = float(q.peek()[1])
+    out = list(q.q)
+    out.sort(key=lambda x: -float(x[1]))  # Collections.sort is stable, as is list.sort
+    return out
+
 
 # ---- the precomputed-similarity consumer (SURVEY 8(f) rank 3) ----------------
 # GenericItemSimilarity(Iterable<ItemItemSimilarity>) is how Taste consumes

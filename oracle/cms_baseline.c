@@ -208,4 +208,135 @@ int64_t orc_allpairs_efficient_par(const double* table, int64_t rows, int32_t de
   return pairs;
 }
 
+/* GenericUserBasedRecommender.recommend (T/impl/recommender/
+ * GenericUserBasedRecommender.java:84-105) with NearestNUserNeighborhood(nn)
+ * (T/impl/neighborhood/NearestNUserNeighborhood.java:84-95) and the CosineCM
+ * point-query estimate (:134-184), for users [u_lo, u_hi) of a user-owner
+ * model over prebuilt fp64 sketches [rows][d][w] (efficient mode): per user
+ * the similarity to every other user (min over rows of AB / (|A| |B|),
+ * clamped as normalizeWeightResult), the first nn under (similarity desc,
+ * ID = row asc), the neighbours' items minus the user's own (item indices
+ * into item_keys; off/items: the model's CSR of item indices), each
+ * candidate's estimate, and the how_many best values.  Returns the
+ * estimates computed; *checksum sums the recommended values. */
+int64_t orc_recommend_par(const double* table, int64_t rows, int32_t depth, int32_t width, const int64_t* a,
+                          const int64_t* b, const int64_t* off, const int32_t* items, const int64_t* item_keys,
+                          int64_t n_items, int32_t nn, int32_t how_many, int32_t use_capper, float cap_min,
+                          float cap_max, int64_t u_lo, int64_t u_hi, int32_t nthreads, double* checksum) {
+  const size_t stride = (size_t)depth * (size_t)width;
+  double* nrm = (double*)malloc(sizeof(double) * (size_t)rows * (size_t)depth);
+  uint64_t ap[64], bp[64];
+  for (int i = 0; i < depth; i++) {
+    ap[i] = key_mod_p(a[i]);
+    bp[i] = key_mod_p(b[i]);
+  }
+  const uint32_t wmask = (width & (width - 1)) == 0 ? (uint32_t)width - 1u : 0u;
+  const int nt = use_threads(nthreads);
+#pragma omp parallel for num_threads(nt) schedule(static)
+  for (int64_t r = 0; r < rows; r++)
+    for (int32_t i = 0; i < depth; i++) {
+      const double* x = table + (size_t)r * stride + (size_t)i * width;
+      double s = 0.0;
+      for (int32_t j = 0; j < width; j++) s += x[j] * x[j];
+      nrm[r * depth + i] = sqrt(s);
+    }
+  double acc = 0.0;
+  int64_t nest = 0;
+#pragma omp parallel num_threads(nt) reduction(+ : acc, nest)
+  {
+    double* sims = (double*)malloc(sizeof(double) * (size_t)rows);
+    int64_t* ids = (int64_t*)malloc(sizeof(int64_t) * (size_t)rows);
+    int64_t* nb = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nn > 0 ? nn : 1));
+    double* nbs = (double*)malloc(sizeof(double) * (size_t)(nn > 0 ? nn : 1));
+    uint8_t* mark = (uint8_t*)calloc((size_t)n_items, 1);
+    int32_t* cand = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_items);
+    float* best = (float*)malloc(sizeof(float) * (size_t)(how_many + 1));
+    for (int64_t r = 0; r < rows; r++) ids[r] = r;
+#pragma omp for schedule(dynamic, 4)
+    for (int64_t u = u_lo; u < u_hi; u++) {
+      const double* A = table + (size_t)u * stride;
+      for (int64_t v = 0; v < rows; v++) {
+        if (v == u) {
+          sims[v] = NAN;  /* the user itself is never a neighbour */
+          continue;
+        }
+        const double* B = table + (size_t)v * stride;
+        double mn = INFINITY;
+        for (int32_t i = 0; i < depth; i++) {
+          const double* x = A + (size_t)i * width;
+          const double* y = B + (size_t)i * width;
+          double ab = 0.0;
+          for (int32_t j = 0; j < width; j++) ab += x[j] * y[j];
+          const double den = nrm[u * depth + i] * nrm[v * depth + i];
+          if (den != 0) {
+            const double c = ab / den;
+            if (c < mn) mn = c;
+          }
+        }
+        sims[v] = mn == INFINITY ? NAN : (mn > 1.0 ? 1.0 : mn < -1.0 ? -1.0 : mn);
+      }
+      const int32_t m = orc_top_users(ids, sims, rows, nn, nb, nbs);
+      int32_t nc = 0;
+      for (int32_t t = 0; t < m; t++)
+        for (int64_t k = off[nb[t]]; k < off[nb[t] + 1]; k++)
+          if (!mark[items[k]]) {
+            mark[items[k]] = 1;
+            cand[nc++] = items[k];
+          }
+      for (int64_t k = off[u]; k < off[u + 1]; k++) mark[items[k]] = 2;  /* the user's own items */
+      int32_t nbest = 0;
+      for (int32_t c = 0; c < nc; c++) {
+        const int32_t it = cand[c];
+        if (mark[it] == 2) continue;
+        uint32_t bk[64];
+        const uint64_t kp = key_mod_p(item_keys[it]);
+        for (int i = 0; i < depth; i++) bk[i] = (uint32_t)i * (uint32_t)width + fast_hash(ap[i], bp[i], kp, (uint32_t)width, wmask);
+        double preference = 0.0, total = 0.0;
+        int count = 0;
+        for (int32_t t = 0; t < m; t++) {
+          const double* S = table + (size_t)nb[t] * stride;
+          double est = 1.7976931348623157e308;
+          for (int i = 0; i < depth; i++)
+            if (S[bk[i]] < est) est = S[bk[i]];
+          const float pref = (float)est;
+          if (pref == 0.0f || isnan(nbs[t])) continue;
+          preference += nbs[t] * (double)pref;
+          total += nbs[t];
+          count++;
+        }
+        nest++;
+        if (count <= 1) continue;
+        float e = (float)(preference / total);
+        if (use_capper) e = e > cap_max ? cap_max : e < cap_min ? cap_min : e;
+        /* keep the how_many largest (insertion into a short sorted array) */
+        int32_t p;
+        if (nbest < how_many) {
+          p = nbest++;
+        } else {
+          if (!(e > best[how_many - 1])) continue;
+          p = how_many - 1;
+        }
+        while (p > 0 && best[p - 1] < e) {
+          best[p] = best[p - 1];
+          p--;
+        }
+        best[p] = e;
+      }
+      for (int32_t t = 0; t < nbest; t++) acc += best[t];
+      for (int32_t c = 0; c < nc; c++) mark[cand[c]] = 0;
+      for (int64_t k = off[u]; k < off[u + 1]; k++) mark[items[k]] = 0;
+    }
+    free(sims);
+    free(ids);
+    free(nb);
+    free(nbs);
+    free(mark);
+    free(cand);
+    free(best);
+  }
+  free(nrm);
+  if (checksum) *checksum = acc;
+  return nest;
+}
+
 int32_t orc_max_threads(void) { return omp_get_max_threads(); }

@@ -87,6 +87,10 @@ float orc_estimate_preference(const double* table, int32_t depth, int32_t width,
 void orc_cosine_queries_csr(const double* qsk, int64_t Q, const int64_t* off, const int64_t* keys, const float* vals,
                             int64_t n, int32_t depth, int32_t width, const int64_t* a, const int64_t* b,
                             int weighted, int32_t threads, double* out);
+int64_t orc_recommend_par(const double* table, int64_t rows, int32_t depth, int32_t width, const int64_t* a,
+                          const int64_t* b, const int64_t* off, const int32_t* items, const int64_t* item_keys,
+                          int64_t n_items, int32_t nn, int32_t how_many, int32_t use_capper, float cap_min,
+                          float cap_max, int64_t u_lo, int64_t u_hi, int32_t nthreads, double* checksum);
 int32_t orc_top_users(const int64_t* ids, const double* scores, int64_t n, int32_t k,
                       int64_t* out_ids, double* out_scores);
 

@@ -58,6 +58,9 @@ def _load():
         "orc_allpairs_efficient_par": (c.c_int64, [_f64p, c.c_int64, c.c_int32, c.c_int32, c.c_int64, c.c_int64,
                                                    c.c_int32, c.POINTER(c.c_double)]),
         "orc_max_threads": (c.c_int32, []),
+        "orc_recommend_par": (c.c_int64, [_f64p, c.c_int64, c.c_int32, c.c_int32, _i64p, _i64p, _i64p, _i32p, _i64p,
+                                          c.c_int64, c.c_int32, c.c_int32, c.c_int32, c.c_float, c.c_float, c.c_int64,
+                                          c.c_int64, c.c_int32, c.POINTER(c.c_double)]),
         "orc_cosine_queries_csr": (None, [_f64p, c.c_int64, _i64p, _i64p, c.c_void_p, c.c_int64, c.c_int32, c.c_int32,
                                           _i64p, _i64p, c.c_int, c.c_int32, _f64p]),
     }
@@ -303,4 +306,20 @@ def allpairs_efficient(table, i_lo, i_hi, threads):
     rows, d, w = t.shape
     cs = ctypes.c_double()
     n = lib().orc_allpairs_efficient_par(t.reshape(-1), rows, d, w, i_lo, i_hi, threads, ctypes.byref(cs))
+    return n, cs.value
+
+
+def recommend_par(table, a, b, off, items, item_keys, nn, how_many, u_lo, u_hi, threads, capper=None):
+    """orc_recommend_par: GenericUserBasedRecommender.recommend for users
+    [u_lo, u_hi) over prebuilt sketches (efficient CPU mode); returns
+    (estimates computed, checksum of the recommended values)."""
+    t = np.ascontiguousarray(table, np.float64)
+    rows, d, w = t.shape
+    lo, hi = capper if capper is not None else (0.0, 0.0)
+    cs = ctypes.c_double()
+    n = lib().orc_recommend_par(t.reshape(-1), rows, d, w, np.ascontiguousarray(a, np.int64),
+                                np.ascontiguousarray(b, np.int64), np.ascontiguousarray(off, np.int64),
+                                np.ascontiguousarray(items, np.int32), np.ascontiguousarray(item_keys, np.int64),
+                                len(item_keys), nn, how_many, int(capper is not None), float(lo), float(hi), u_lo, u_hi,
+                                threads, ctypes.byref(cs))
     return n, cs.value

@@ -49,6 +49,23 @@ for step in $STEPS; do
           || { echo "A/B arm $tag failed"; tail -5 gpurun_out/ab_${tag}.err; exit 1; }
         python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['ms_per_step'],3), d.get('breakdown_ms_per_step'))" gpurun_out/ab_${tag}.json
       done ;;
+    ktrace)
+      # per-arm kernel traces of the headline ingest (isolated kernel times
+      # with a CMS_BUILD_SERIAL variant); table: scripts/ktrace_table.py
+      ARMS=${ARMS:-"main $(ls ab/*.so 2>/dev/null | tr '\n' ' ')"}
+      rm -rf gpurun_out/kt
+      for arm in $ARMS; do
+        envs=()
+        case "$arm" in
+          main) tag=main ;;
+          env:*) envs=("${arm#env:}"); tag=$(echo "${arm#env:}" | tr '=' '_') ;;
+          *) envs=(MAHOUT_CMS_LIB="$PWD/$arm"); tag=$(basename "$arm" .so) ;;
+        esac
+        env "${envs[@]}" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt/$tag -o run --output-format csv -- \
+            python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-config1 --no-config2 --no-cosine-1m \
+            > gpurun_out/kt_$tag.log 2>&1 || { echo "ktrace arm $tag failed"; tail -5 gpurun_out/kt_$tag.log; exit 1; }
+      done
+      python3 scripts/ktrace_table.py gpurun_out/kt ;;
     bench)
       timeout -k 10 700 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err \
         || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.cms_abi_version() == 1
+    assert lib.cms_abi_version() == 2
 
 
 def test_params_init_defaults(lib):

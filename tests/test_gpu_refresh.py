@@ -235,3 +235,51 @@ def test_device_outputs_equal_host_outputs():
         t.finalize()
         dev = t.top_k_refresh_device(k)
         assert _same_lists(tuple(x.cpu().numpy() for x in dev), t.top_k_all(k)) is None
+
+
+def test_noop_refresh_reports_no_touched_classes():
+    """Two refreshes with no ingest between them: the second recomputes
+    nothing, and cms_refresh_classes says so (it used to repeat
+    the previous refresh's touched counts, which the bench prices)."""
+    n, d, w, k = 2500, 4, 256, 12
+    items, users = zipf_stream(3000, n, 150_000, seed=41)
+    rng = np.random.Generator(np.random.PCG64(41))
+    with SketchTable(n, depth=d, width=w, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        t.top_k_refresh(k)
+        rows, keys, v = _batch(rng, n, 0.1, 10_000, 1, 3000)
+        t.ingest(rows, keys, v)
+        t.finalize()
+        first = t.top_k_refresh(k)
+        assert t.refresh_stats()[0] > 0
+        assert sum(c[1] for c in t.refresh_classes().values()) > 0
+        again = t.top_k_refresh(k)
+        assert t.refresh_stats()[0] == 0
+        cls = t.refresh_classes()
+        assert all(c[1] == 0 for c in cls.values()), cls
+        assert sum(c[0] for c in cls.values()) == n
+        assert _same_lists(again, first) is None
+
+
+def test_stats_struct_size_contract():
+    """cms_get_stats writes only the fields a caller's (possibly older,
+    shorter) cms_stats has room for, and refuses a missing struct_size."""
+    import ctypes
+    from mahout_amd import _lib
+    lib = _lib.load()
+    items, users = zipf_stream(1000, 500, 20_000, seed=5)
+    with SketchTable(500, depth=4, width=256, seed=42) as t:
+        t.ingest(items, users)
+        t.finalize()
+        full = t.stats()
+        assert full["struct_size"] == ctypes.sizeof(_lib.CmsStats) and full["num_owners"] == 500
+        buf = (ctypes.c_uint8 * ctypes.sizeof(_lib.CmsStats))(*([0xAB] * ctypes.sizeof(_lib.CmsStats)))
+        s = _lib.CmsStats.from_buffer(buf)
+        short = _lib.CmsStats.num_owners.offset + 8  # an old caller's struct ending at num_owners
+        s.struct_size = short
+        assert lib.cms_get_stats(t._h, ctypes.byref(s)) == 0
+        assert s.struct_size == short and s.pairs_ingested == full["pairs_ingested"] and s.num_owners == 500
+        assert all(b == 0xAB for b in bytes(buf)[short:])  # nothing past the caller's struct
+        s.struct_size = 0
+        assert lib.cms_get_stats(t._h, ctypes.byref(s)) != 0

@@ -89,3 +89,25 @@ def test_cosinecm_refresh_semantics_documented():
     assert "ensureCurrent()" in src and "public void rebuild()" in src
     integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     assert "never clears" in integ  # the reference's sketches cache (CosineCM.java:60-67)
+
+
+def test_native_calls_hold_the_handle_lock():
+    """a lazy rebuild may swap and destroy the handle while other
+    threads query.  Every native call on the handle must run between
+    acquire() (read side of the handle lock) and release(); only build()'s
+    swap and close() destroy a handle, under the write side."""
+    src = _strip_comments(open(os.path.join(JAVA, "CosineCMGpu.java")).read())
+    body = src[src.index("class CosineCMGpu"):src.index("private static native")]  # up to the JNI declarations
+    calls = re.findall(r"\bnative(?!Create|Destroy|SetHashParams|SetOwnerIds|IngestCsr|SetOwnerDeltaEpsilon|"
+                       r"ConfigureOwnerShapes|Finalize)\w+\((\w+)", body)
+    assert calls and all(c == "h" for c in calls), calls
+    # each `long h = acquire();` is followed by a try/finally release()
+    for m in re.finditer(r"long h = acquire\(\);\s*try \{(.*?)\} finally \{\s*release\(\);", body, re.S):
+        assert "native" in m.group(1)
+    assert body.count("long h = acquire();") == body.count("release();") - 0
+    assert body.count("acquire();") >= len(calls)
+    destroy = [m.start() for m in re.finditer(r"nativeDestroy\(", body)]
+    wl = [m.start() for m in re.finditer(r"writeLock\(\)\.lock\(\)", body)]
+    # every destroy of a live (published) handle sits after a write-lock
+    # acquisition; the one in build()'s error path destroys an unpublished one
+    assert len(wl) >= 2 and sum(1 for d in destroy if any(w < d for w in wl)) >= 2
