@@ -338,6 +338,9 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.bit_keys = num("CMS_BIT_KEYS", h->tune.bit_keys);
     h->tune.crumb_keys = num("CMS_CRUMB_KEYS", h->tune.crumb_keys);
     h->tune.list_keys = std::max(0, std::min(256, num("CMS_LIST_KEYS", h->tune.list_keys)));
+    h->tune.mid_u4_keys = num("CMS_MID_U4_KEYS", h->tune.mid_u4_keys);
+    h->tune.mid_u8_keys = num("CMS_MID_U8_KEYS", h->tune.mid_u8_keys);
+    h->tune.mid_u8_image = num("CMS_MID_U8_IMAGE", h->tune.mid_u8_image);
     h->tune.forms = !flag("CMS_NO_FORMS");
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");

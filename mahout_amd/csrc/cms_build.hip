@@ -561,7 +561,8 @@ template <int SV, int D>
 __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
-    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int list_keys) {
+    uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int list_keys, int u4_keys, int u8_keys,
+    int u8img) {
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -607,11 +608,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
     uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;
     int level = -1;  // the form that holds the owner: 0 4-bit, 1 u8, 2 u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
+    // the first form tried (Tunables::mid_u4_keys / mid_u8_keys); a list row
+    // leaves its entries in the 4-bit pass, so it always takes that pass
+    const int start = as_list || m <= u4_keys ? 0 : m <= u8_keys ? 1 : 2;
+    bool mass_pending = !cached;  // uncached keys: the mass is summed by the first pass over them
     // ALL sketch rows in one key pass in a [d][w] 4-bit image.  (A [d][w] u8
     // image after a 4-bit overflow -- a Zipf key set repeats its popular keys,
     // and config 3 has 40K u8 owners -- measured slower: its 40 KB per
     // workgroup halve the owners in flight, build 6.55 -> 7.01 ms.)
-    {
+    if (start == 0) {
       constexpr int ab = 4;
       const int lga = 3;  // log2(counters per word)
       const uint32_t capa = (1u << ab) - 1u;
@@ -680,6 +685,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
             mass += inc4[u];
           }
         }
+        mass_pending = false;
       }
       if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
       __syncthreads();
@@ -712,8 +718,104 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
         if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
       }
     }
-    // the 4-bit image overflowed: one sketch row at a time, u8 then u16
-    if (level < 0) level = 1;
+    // owners that start at u8 (u8img): ALL sketch rows in one key pass in a
+    // [d][w] u8 image (d*w bytes of LDS), each key read and hashed once
+    // instead of once per sketch row; a counter past 255 goes on to u16 rows
+    bool u8_failed = false;
+    if (start == 1 && u8img) {
+      const int nq_all = (int)(((int64_t)hp.depth * w) >> 4);  // uint4 of the [d][w] byte image
+      uint4* l4 = reinterpret_cast<uint4*>(lds);
+      for (int j = tid; j < nq_all; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+      if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+      if (tid == 0) {
+        s_max = 0u;
+        s_ovf = 0u;
+        s_mass = 0ULL;
+      }
+      __syncthreads();
+      bool ovf = false;
+      vmax = 0;
+      auto add_all8 = [&](uint64_t kr, uint32_t inc) {
+        each_bucket<D>(hp, kr, [&](int d, uint32_t bk) {
+          const uint32_t c = (uint32_t)d * (uint32_t)w + bk;
+          const uint32_t sh = (c & 3u) << 3;
+          const uint32_t old = (atomicAdd(&lds[c >> 2], inc << sh) >> sh) & 255u;
+          const uint32_t nv = old + inc;
+          ovf |= nv > 255u || inc > 255u;  // carried into the next counter: u16 rows
+          vmax = max(vmax, nv);
+        });
+      };
+      if (cached) {
+#pragma unroll
+        for (int k = 0; k < kKeyRegs; ++k)
+          if (ik[k]) add_all8(kp[k], ik[k]);
+      } else {
+        constexpr int64_t kStep = 4 * kBuildThreads;
+        uint64_t nx[4];
+        auto fetch = [&](int64_t base) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            nx[u] = i < hi ? keys.raw(i) : 0ULL;
+          }
+        };
+        fetch(lo);
+        for (int64_t base = lo; base < hi; base += kStep) {
+          uint64_t kk[4];
+          uint32_t inc4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            kk[u] = nx[u];
+            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            inc4[u] = 0;
+            if (i < hi) {
+              uint32_t inc;
+              if (!load_inc(vals, i, inc, hp.frac_bits)) {
+                badv = true;
+                inc = 0;
+              }
+              inc4[u] = inc;
+            }
+          }
+          if (base + kStep < hi) fetch(base + kStep);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (inc4[u]) add_all8(keys.resolve(kk[u]), inc4[u]);
+            mass += inc4[u];
+          }
+        }
+        mass_pending = false;
+      }
+      if (__ballot(ovf) && (tid & 63) == 0) s_ovf = 1u;
+      __syncthreads();
+      const bool fits = s_ovf == 0u;
+      __syncthreads();  // every thread has read s_ovf before the row passes reset it
+      if (fits) {
+        level = 1;
+        const uint4* r4 = reinterpret_cast<const uint4*>(lds);
+        const int nq = w >> 4;  // uint4 per u8 sketch row
+        for (int d = 0; d < hp.depth; ++d) {
+          uint32_t sq = 0;  // <= row mass * max counter < 2^32
+          for (int j = tid; j < nq; j += kBuildThreads) {
+            const uint4 v = r4[d * nq + j];
+            sq = __builtin_amdgcn_udot4(v.x, v.x, sq, false);
+            sq = __builtin_amdgcn_udot4(v.y, v.y, sq, false);
+            sq = __builtin_amdgcn_udot4(v.z, v.z, sq, false);
+            sq = __builtin_amdgcn_udot4(v.w, v.w, sq, false);
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+            if (false)
+#endif
+            store_row(d4 + d * nq + j, v, SV);
+          }
+          sq = wave_sum_u32(sq);
+          if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+        }
+      } else {
+        u8_failed = true;
+      }
+    }
+    // the 4-bit image overflowed (or was skipped): one sketch row at a time, u8 then u16
+    if (level < 0) level = start > 1 || u8_failed ? 2 : 1;
     else level = -level - 1;  // done: mark so the row passes are skipped
     for (;;) {
       if (level < 0) break;  // an all-rows image held every counter
@@ -726,6 +828,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       if (tid == 0) {
         s_max = 0u;
         s_ovf = 0u;
+        s_mass = 0ULL;  // (added once, after the last pass; the 4-bit pass may not have run)
       }
       vmax = 0;
       for (int d = 0; d < hp.depth; ++d) {
@@ -767,9 +870,10 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               if (inc4[u]) add(kk[u], inc4[u]);
-              if (d == 0 && level == 0) mass += inc4[u];
+              if (mass_pending) mass += inc4[u];
             }
           }
+          mass_pending = false;  // summed once, by row 0 of the first pass
         }
         sq = wave_sum_u64_sat(sq);
         if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
@@ -1298,15 +1402,17 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          d_val, n, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
                          h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0);
-      // the u8 all-rows image when a [d][w] byte image fits 64 KB (config 3: 40 KB)
-      const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, (size_t)h->dw / 2);
+      // the u8 all-rows image (Tunables::mid_u8_image) when a [d][w] byte image fits 64 KB (config 3: 40 KB)
+      const int u8img = h->tune.mid_u8_image && h->dw <= 64 * 1024 ? 1 : 0;
+      const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, u8img ? (size_t)h->dw : (size_t)h->dw / 2);
       auto kmid = h->p.depth == 5   ? k_build_mid<kBuildStoreForm, 5>
                   : h->p.depth == 4 ? k_build_mid<kBuildStoreForm, 4>
                                     : k_build_mid<kBuildStoreForm, 0>;
       hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
                          dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
-                         h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);
+                         h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0, h->tune.mid_u4_keys,
+                         h->tune.mid_u8_keys, u8img);
       hipLaunchKernelGGL(k_build_bytes<kBuildStoreForm>, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)),
                          dim3(kBuildThreads), (size_t)h->dw, side, d_lo, d_hi, keys, d_val, h->hp, redo, redo_cnt,
                          h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags);

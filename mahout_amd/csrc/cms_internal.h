@@ -197,6 +197,13 @@ struct Tunables {
   int bit_keys = 64;       // CMS_BIT_KEYS: byte-class owners of <= this many keys try 1-bit rows first
   int crumb_keys = 256;    // CMS_CRUMB_KEYS: ... of <= this many keys 2-bit rows
   int list_keys = 256;     // CMS_LIST_KEYS: ... of <= this many keys (unit increments) list rows; 0: none
+  // mid-class owners start at the form their key count suggests: a Zipf key
+  // set repeats its most popular key about n / 40 times, so a counter passes
+  // 15 past a few hundred keys and 255 past ten thousand -- the 4-bit (and u8)
+  // attempts would only be thrown away (the escalation stays as the safety net)
+  int mid_u4_keys = 768;    // CMS_MID_U4_KEYS: more keys start at u8 (list-row owners always try 4-bit)
+  int mid_u8_keys = 12288;  // CMS_MID_U8_KEYS: more keys start at u16
+  int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
   bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)

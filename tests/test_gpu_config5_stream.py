@@ -94,7 +94,7 @@ def test_config5_full_stream_table(oracle):
             if name == "list" or not sel.any():
                 continue
             assert rowmax[sel].max() <= CAP[name], name
-            if name != "u32":
+            if name not in ("u32", "u16"):  # u16 rows are kept below 2^16 by their mass bound, not cbound
                 assert (rowmax[sel] <= bound[sel]).all(), name
         touched = counts > bulk_counts
         assert (forms[touched] != SketchTable.FORMS.index("list")).any()  # the stream widened list rows
