@@ -913,6 +913,175 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
   }
 }
 
+// Mid-class owners through ONE key pass (Tunables::mid_image, when the
+// [d][w] u16 image fits 80 KB): k_build_slices' scheme -- every sketch row
+// counted at once in a [d][w] u16 LDS image (no carry: a mid owner's mass,
+// hence every counter, stays below 2^16) with non-returning LDS adds -- then
+// one read-back pass that finds the largest counter and each row's sum of
+// squares, and a store pass that packs the image into the narrowest form
+// that holds it (4-bit, u8, u16; or the list row whose entries the key pass
+// wrote).  No escalation passes, no per-row reloads of the keys.
+constexpr int kImgThreads = 512;
+template <int SV, int D>
+__global__ __launch_bounds__(kImgThreads) void k_build_image(
+    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp, const int32_t* list,
+    const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass, uint64_t* norm,
+    uint32_t* rowmax, uint32_t* flags, int list_keys) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [d][w] u16 counters, two per word
+  __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
+  __shared__ unsigned long long s_mass;
+  __shared__ uint32_t s_max;
+  const int tid = threadIdx.x;
+  const int w = (int)hp.width;
+  const int64_t dw = (int64_t)hp.depth * w;
+  const int words = (int)(dw >> 1);
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+  const uint32_t count = *list_cnt;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const int64_t row = list[li];
+    const int64_t lo = lo_[row], hi = hi_[row];
+    const int64_t m = hi - lo;
+    for (int j = tid; j < (words >> 2); j += kImgThreads) l4[j] = make_uint4(0, 0, 0, 0);
+    if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
+    if (tid == 0) {
+      s_mass = 0ULL;
+      s_max = 0u;
+    }
+    __syncthreads();
+    // a LIST row when the increments are units and the list beats the 4-bit
+    // row (its entries leave during the key pass; a counter past 255 makes
+    // the owner a dense u16 row instead, which overwrites them)
+    const bool as_list = m <= list_keys && vals == nullptr && hp.frac_bits == 0 && (int64_t)hp.depth * m <= 8192 &&
+                         2 + 2 * (int64_t)hp.depth * m < (int64_t)hp.depth * w / 2;
+    uint16_t* lst = tv.t16 + row * dw;
+    uint64_t mass = 0;
+    bool badv = false;
+    constexpr int kPer = 4;
+    constexpr int64_t kStep = kPer * kImgThreads;
+    uint64_t nx[kPer];
+    auto fetch = [&](int64_t base) {
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int64_t i = base + tid + (int64_t)u * kImgThreads;
+        nx[u] = i < hi ? keys.raw(i) : 0ULL;
+      }
+    };
+    if (lo < hi) fetch(lo);
+    for (int64_t base = lo; base < hi; base += kStep) {
+      uint64_t kk[kPer];
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) kk[u] = nx[u];
+      if (base + kStep < hi) fetch(base + kStep);
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int64_t i = base + tid + (int64_t)u * kImgThreads;
+        if (i >= hi) continue;
+        uint32_t inc;
+        if (!load_inc(vals, i, inc, hp.frac_bits)) {
+          badv = true;
+          inc = 0;
+        }
+        mass += inc;
+        if (!inc) continue;
+        const uint64_t kp = keys.resolve(kk[u]);
+        const int64_t t = i - lo;
+        each_bucket<D>(hp, kp, [&](int r, uint32_t bk) {
+          if (as_list) lst[1 + (int64_t)r * m + t] = (uint16_t)bk;
+          const uint32_t c = (uint32_t)r * (uint32_t)w + bk;
+          atomicAdd(&lds[c >> 1], inc << ((c & 1u) << 4));
+        });
+      }
+    }
+    __syncthreads();
+    // read-back: largest counter and each sketch row's sum of squares (a row
+    // of w counters is w/8 uint4; w % 32 == 0 for forms)
+    {
+      const int q_row = w >> 3;
+      uint32_t vmax = 0;
+      for (int d = 0; d < hp.depth; ++d) {
+        uint32_t sq = 0;  // <= row mass * max counter < 2^32
+        for (int j = tid; j < q_row; j += kImgThreads) {
+          const uint4 v = l4[d * q_row + j];
+          const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const u16x2 p = __builtin_bit_cast(u16x2, x[q]);
+            sq = __builtin_amdgcn_udot2(p, p, sq, false);
+            vmax = max(vmax, max(x[q] & 0xFFFFu, x[q] >> 16));
+          }
+        }
+        sq = wave_sum_u32(sq);
+        if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+      if ((tid & 63) == 0 && vmax) atomicMax(&s_max, vmax);
+      mass = wave_sum_u64_sat(mass);
+      if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, (unsigned long long)mass);
+    }
+    __syncthreads();
+    const uint32_t vmax = s_max;
+    const bool listed = as_list && vmax <= 255u;
+    const int level = vmax <= 15u ? 0 : vmax <= 255u ? 1 : 2;  // 4-bit, u8, u16
+    uint4* d4 = reinterpret_cast<uint4*>(lst);
+    if (!listed) {
+      // 32 counters (4 uint4 of the image) per step: one uint4 of 4-bit,
+      // two of u8 or four of u16 counters
+      const int steps = (int)(dw >> 5);
+      for (int s = tid; s < steps; s += kImgThreads) {
+        const uint4 a = l4[4 * s], b = l4[4 * s + 1], c = l4[4 * s + 2], e = l4[4 * s + 3];
+        const uint32_t x[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, e.x, e.y, e.z, e.w};
+        if (level == 2) {
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+          if (false)
+#endif
+          {
+            store_row(d4 + 4 * s, a, SV);
+            store_row(d4 + 4 * s + 1, b, SV);
+            store_row(d4 + 4 * s + 2, c, SV);
+            store_row(d4 + 4 * s + 3, e, SV);
+          }
+        } else if (level == 1) {
+          uint32_t y[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) y[q] = __builtin_amdgcn_perm(x[2 * q + 1], x[2 * q], 0x06040200u);  // bytes 0, 2 of each
+#ifdef CMS_BUILD_NOWRITE
+          if (false)
+#endif
+          {
+            store_row(d4 + 2 * s, make_uint4(y[0], y[1], y[2], y[3]), SV);
+            store_row(d4 + 2 * s + 1, make_uint4(y[4], y[5], y[6], y[7]), SV);
+          }
+        } else {
+          uint32_t y[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            // 8 counters < 16: x[4q..4q+3] hold two each in their u16 halves
+            const uint32_t b0 = __builtin_amdgcn_perm(x[4 * q + 1], x[4 * q], 0x06040200u);
+            const uint32_t b1 = __builtin_amdgcn_perm(x[4 * q + 3], x[4 * q + 2], 0x06040200u);
+            y[q] = nibbles8(b0, b1);
+          }
+#ifdef CMS_BUILD_NOWRITE
+          if (false)
+#endif
+          store_row(d4 + s, make_uint4(y[0], y[1], y[2], y[3]), SV);
+        }
+      }
+    }
+    if (badv) atomicOr(flags, kFlagBadValue);
+    if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
+    if (tid == 0) {
+      rowmax[row] = vmax;
+      row_mass[row] = s_mass;
+      if (s_mass >= (1ULL << 32)) atomicOr(flags, kFlagOverflow);
+      if (listed) lst[0] = (uint16_t)m;
+      hidx_w[row] = listed ? kFormList : level == 0 ? kFormU4 : level == 1 ? kFormU8 : kFormU16;
+      cbound[row] = vmax;
+    }
+    __syncthreads();  // image and shared sums consumed before the next owner
+  }
+}
+
 // Byte-class owners (byte_class): ONE WAVE per owner, four owners per
 // workgroup, each wave with its own w/2-byte LDS slot (4 KB at w = 8192).  The
 // owner's keys are read once into registers; each sketch row in turn is
@@ -932,17 +1101,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 constexpr int kNibWaves = 4;
 // owners with at most Tunables::bit_keys (64) keys try 1-bit rows first, with
 // at most crumb_keys (256) 2-bit rows
+// One byte-class owner by one wave (k_build_nibbles).
 template <int SV>
-__global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
-    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, int64_t nrows, HashParams hp,
-    const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
-    uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt, int bit_keys,
-    int crumb_keys, int list_keys) {
-  extern __shared__ __align__(16) uint32_t lds[];  // [kNibWaves][w / 8] words: one sketch row of nibbles per wave
+__device__ __forceinline__ void nib_owner(
+    int64_t row, uint32_t* lds, const int64_t* lo_, const int64_t* hi_, const Keys& keys, const float* vals,
+    const HashParams& hp, const int32_t* row_hot, const uint64_t* bound, const TableView& tv, int32_t* hidx_w,
+    uint32_t* cbound, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo,
+    uint32_t* redo_cnt, int bit_keys, int crumb_keys, int list_keys) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  const int64_t row = (int64_t)blockIdx.x * kNibWaves + wv;
-  if (row >= nrows) return;
   const int64_t lo = lo_[row], hi = hi_[row];
   if (row_hot[row] >= 0 || !byte_class(tv.hidx[row], hi - lo, bound[row])) return;
   const int w = (int)hp.width;
@@ -1035,6 +1202,23 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
     hidx_w[row] = as_list ? kFormList : bits == 1 ? kFormU1 : bits == 2 ? kFormU2 : kFormU4;
     cbound[row] = vmax;
   }
+}
+
+
+// Grid: one owner per wave, or (Tunables::nib_persist) persistent waves that
+// take owners gw, gw + nw, ... -- a quarter of a million four-wave workgroups
+// of a few thousand cycles each can be bound by the workgroup dispatch rate.
+template <int SV>
+__global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
+    const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, int64_t nrows, HashParams hp,
+    const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
+    uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int32_t* redo, uint32_t* redo_cnt, int bit_keys,
+    int crumb_keys, int list_keys) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [kNibWaves][w / 8] words: one sketch row of nibbles per wave
+  const int64_t nw = (int64_t)gridDim.x * kNibWaves;
+  for (int64_t row = (int64_t)blockIdx.x * kNibWaves + (threadIdx.x >> 6); row < nrows; row += nw)
+    nib_owner<SV>(row, lds, lo_, hi_, keys, vals, hp, row_hot, bound, tv, hidx_w, cbound, row_mass, norm, rowmax, flags,
+                  redo, redo_cnt, bit_keys, crumb_keys, list_keys);
 }
 
 // The byte-class owners a counter >= 16 sent back from k_build_nibbles: the
@@ -1397,7 +1581,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
         CMS_HIP(hipStreamWaitEvent(side, h->ev_fork2, 0));
         join.armed = true;
       }
-      hipLaunchKernelGGL(k_build_nibbles<kBuildStoreForm>, dim3((unsigned)((n + kNibWaves - 1) / kNibWaves)),
+      const int64_t nib_blocks = (n + kNibWaves - 1) / kNibWaves;
+      hipLaunchKernelGGL(k_build_nibbles<kBuildStoreForm>,
+                         dim3((unsigned)(h->tune.nib_persist ? std::min<int64_t>(nib_blocks, (int64_t)h->num_cus * 8)
+                                                             : nib_blocks)),
                          dim3(64 * kNibWaves), (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, keys,
                          d_val, n, h->hp, row_hot, h->ws_bound.as<uint64_t>(), h->tview(), h->d_hidx, h->d_cbound,
                          h->d_row_mass, h->d_norm, h->d_rowmax, h->d_flags, redo, redo_cnt, h->tune.bit_keys,
@@ -1408,6 +1595,25 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       auto kmid = h->p.depth == 5   ? k_build_mid<kBuildStoreForm, 5>
                   : h->p.depth == 4 ? k_build_mid<kBuildStoreForm, 4>
                                     : k_build_mid<kBuildStoreForm, 0>;
+      // the one-pass image build when the [d][w] u16 image fits 80 KB and the
+      // row width packs into whole 4-bit words (Tunables::mid_image)
+      const bool img = h->tune.mid_image && h->dw * 2 <= 80 * 1024 && (h->dw % 32) == 0;
+      if (img) {
+        static bool attr = [] {
+          for (const void* f : {(const void*)k_build_image<kBuildStoreForm, 0>, (const void*)k_build_image<kBuildStoreForm, 4>,
+                                (const void*)k_build_image<kBuildStoreForm, 5>})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+          return true;
+        }();
+        (void)attr;
+        auto kimg = h->p.depth == 5   ? k_build_image<kBuildStoreForm, 5>
+                    : h->p.depth == 4 ? k_build_image<kBuildStoreForm, 4>
+                                      : k_build_image<kBuildStoreForm, 0>;
+        hipLaunchKernelGGL(kimg, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kImgThreads),
+                           (size_t)h->dw * 2, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
+                           (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
+                           h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);
+      } else
       hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
                          dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,

@@ -198,4 +198,28 @@ CMS_HD uint32_t bucket_wb(const HashParams& hp, int r, uint64_t kp, uint32_t w, 
   return (uint32_t)rem;
 }
 
+// bucket_wb for a reduced key below 2^32 (the usual DataModel IDs), without
+// the 128-bit fold: q0 = floor(fma(a'/p, k', b'/p)) is q or q +- 1 (its error
+// is below 2^-20), the wrapping 64-bit residue s = a'k' + b' - q0 p (mod 2^64)
+// is then < p exactly when q0 = q, and one add or subtract of p repairs it
+// otherwise (direction from the fractional part); Barrett mod w as bucket_wb.
+CMS_HD uint32_t bucket_wbq(const HashParams& hp, int r, uint64_t kp, uint32_t w, uint64_t barrett) {
+  if ((kp >> 32) != 0) return bucket_wb(hp, r, kp, w, barrett);
+  const double y = fma(hp.qa[r], (double)(uint32_t)kp, hp.qb[r]);
+  const double fl = floor(y);
+  const double fr = y - fl;
+  union {
+    double d;
+    uint64_t u;
+  } qb;
+  qb.d = fl + 4503599627370496.0;  // 2^52
+  const uint64_t q = (uint32_t)qb.u;
+  uint64_t s = hp.ap[r] * kp + hp.bp[r] - ((q << 63) - 25u * q);  // X - q0 p (mod 2^64)
+  if (s >= kPrime) s = fr < 0.5 ? s + kPrime : s - kPrime;
+  const uint64_t qq = (uint64_t)(((unsigned __int128)s * barrett) >> 64);
+  uint64_t rem = s - qq * w;
+  while (rem >= w) rem -= w;
+  return (uint32_t)rem;
+}
+
 }  // namespace cms

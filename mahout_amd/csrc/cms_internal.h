@@ -203,6 +203,8 @@ struct Tunables {
   // attempts would only be thrown away (the escalation stays as the safety net)
   int mid_u4_keys = 768;    // CMS_MID_U4_KEYS: more keys start at u8 (list-row owners always try 4-bit)
   int mid_u8_keys = 12288;  // CMS_MID_U8_KEYS: more keys start at u16
+  int nib_persist = 0;      // CMS_NIB_PERSIST=1: k_build_nibbles as persistent waves (else one owner per wave)
+  int mid_image = 1;        // CMS_MID_IMAGE=0: mid owners through k_build_mid's form passes, not the one-pass u16 image
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes

@@ -444,9 +444,12 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
                                                  const uint32_t* blkStart, int P1, int64_t CH2, int P2,
                                                  uint32_t* H2) {
   extern __shared__ uint32_t lh[];
-  uint32_t nblk = blkStart[P1];
-  if (blockIdx.x >= nblk) return;
-  const uint32_t lb = p2_block(blockIdx.x, nblk);
+  const uint32_t nblk = blkStart[P1];
+  // persistent over the device-side block count (the host's bound on it is
+  // loose: a launch of that many workgroups mostly dispatches empty ones);
+  // the grid is a multiple of 8, so every virtual block vb runs on XCD vb % 8
+  for (uint32_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+  const uint32_t lb = p2_block(vb, nblk);
   int b = find_bin(blkStart, P1, lb);
   for (int f = threadIdx.x; f < P2; f += blockDim.x) lh[f] = 0;
   __syncthreads();
@@ -472,6 +475,8 @@ __global__ __launch_bounds__(256) void k_p2_hist(const uint16_t* fine, const uin
   }
   __syncthreads();
   for (int f = threadIdx.x; f < P2; f += blockDim.x) H2[(int64_t)lb * P2 + f] = lh[f];
+  __syncthreads();  // lh read out before the next block zeroes it
+  }
 }
 
 // Offsets of (pass-2 block, fine bin) and the CSR row starts, in three
@@ -623,11 +628,12 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
                                                              int32_t* orow) {
   constexpr int TILE = R * kPartTile, NP = R * kPartPer;
   extern __shared__ __align__(16) unsigned char smem[];
-  uint32_t nblk = blkStart[P1];
-  if (blockIdx.x >= nblk) return;
+  const uint32_t nblk = blkStart[P1];
   TileLds L = carve(smem, P2, HV, false, TILE);
   const int tid = threadIdx.x;
-  const uint32_t lb = p2_block(blockIdx.x, nblk);
+  // persistent over the device-side block count (k_p2_hist)
+  for (uint32_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+  const uint32_t lb = p2_block(vb, nblk);
   const int b = find_bin(blkStart, P1, lb);
   for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] = O2[(int64_t)lb * P2 + f];
   const int64_t lo = binStart[b] + (int64_t)(lb - blkStart[b]) * CH2;
@@ -700,6 +706,8 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
       L.hist[f] = 0;
     }
     lds_barrier();
+  }
+  __syncthreads();  // this block's LDS use ends before the next block's cursors load
   }
 }
 
@@ -823,7 +831,8 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
                        h->stream, d_row, d_key, d_val, npairs, s2, P1, n, O1, NB, fine, key1, val1, slotkey,
                        ckey, cval);
     hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, bs1, P1, CH2, binStart, blkStart);
-    hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)nb2max), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,
+    const int64_t g2h = std::min<int64_t>((nb2max + 7) & ~int64_t(7), (int64_t)h->num_cus * 8);
+    hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)g2h), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,
                        binStart, blkStart, P1, CH2, P2, H2);
     hipLaunchKernelGGL(k_p2_colsum<kP2Split>, dim3(P1 * kP2Split), dim3(1024), 0, h->stream, H2, blkStart, P2, PS);
     hipLaunchKernelGGL(k_p2_scan, dim3(P1), dim3(1024), 0, h->stream, binStart, P1, P2, n, PS, coff);
@@ -832,7 +841,10 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     while (R2 > 1 && tile_lds_bytes(P2, d_val != nullptr, false, false, R2 * kPartTile) > 160 * 1024) R2 >>= 1;
     auto scat2 = d_val ? (R2 == 4 ? k_p2_scatter<4, true> : R2 == 2 ? k_p2_scatter<2, true> : k_p2_scatter<1, true>)
                        : (R2 == 4 ? k_p2_scatter<4, false> : R2 == 2 ? k_p2_scatter<2, false> : k_p2_scatter<1, false>);
-    hipLaunchKernelGGL(scat2, dim3((unsigned)nb2max), dim3(kPartThreads),
+    // one pass-2 workgroup per CU fits its LDS tile; a few per CU keep the
+    // dispatcher ahead of the exits (multiple of 8: XCD-contiguous blocks)
+    const int64_t g2s = std::min<int64_t>((nb2max + 7) & ~int64_t(7), (int64_t)h->num_cus * 2);
+    hipLaunchKernelGGL(scat2, dim3((unsigned)g2s), dim3(kPartThreads),
                        tile_lds_bytes(P2, d_val != nullptr, false, false, R2 * kPartTile), h->stream, fine, key1, val1,
                        binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     if (hot) {

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_po_build(const int64_t* off, const uint
       const uint64_t k = kp[i];
       const uint32_t v = inc[i];
       for (int d = 0; d < s.d; ++d)
-        atomicAdd(&sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, k, (uint32_t)s.w, s.barrett)], v);
+        atomicAdd(&sk[s.soff + (int64_t)d * s.w + bucket_wbq(hp, d, k, (uint32_t)s.w, s.barrett)], v);
     }
   }
 }
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     // the row is clean for the next pair -- O(#preferences), not O(w)
     auto add_pass = [&](int d, uint64_t* ab, const uint32_t* brow) {
       for (int64_t i = k0 + lane; i < k1; i += kPoThreads) {
-        const uint32_t j = bucket_wb(hp, d, a.kp[i], w, s.barrett);
+        const uint32_t j = bucket_wbq(hp, d, a.kp[i], w, s.barrett);
         const uint32_t v = a.inc[i];
         atomicAdd(&hist[j], v);
         if (ab) *ab = sat_add(*ab, (uint64_t)v * brow[j]);
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     auto clear_pass = [&](int d) {
       uint64_t a2 = 0;
       for (int64_t i = k0 + lane; i < k1; i += kPoThreads) {
-        const uint32_t c = atomicExch(&hist[bucket_wb(hp, d, a.kp[i], w, s.barrett)], 0u);
+        const uint32_t c = atomicExch(&hist[bucket_wbq(hp, d, a.kp[i], w, s.barrett)], 0u);
         a2 = sat_add(a2, (uint64_t)c * c);
       }
       __syncthreads();
@@ -277,18 +277,20 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
 // the candidates grouped by their shape class (w, d): every member of a class
 // hashes u1's preferences identically (CosineCM.java:86 builds u1 at u2's
 // (delta, epsilon)), so a workgroup holds up to kPoGroupMax members' own
-// sketches in LDS (with their sqrt norms) and each of its waves takes one
-// query at a time.  Per sketch row, u1's preferences are hashed ONCE, 64 at a
-// time: lane k hashes preference k into the wave's bucket row (valueA by the
-// exchange pass of k_po_pairs) and parks (bucket, increment) in LDS; then
-// lane (m, part) gathers member m's counters at a quarter of the parked
-// buckets (valueAB, exact integers accumulated in fp64: each term and partial
-// sum is below 2^53 whenever both norms are), two shuffles sum the quarters,
-// and lane m takes member m's row cosine and running Math.min -- no per-member
-// reductions, no per-member global loads in the loop.  Pairs past the exact
-// regime (a norm >= 2^53) are listed for k_po_pairs' sequential replay.
-constexpr int kPoGroupMax = 16;            // members per narrow group (lanes m of a quarter-wave)
-constexpr int kPoGroupLds = 48 * 1024;     // LDS for a group's own sketches
+// sketches in LDS (with their sqrt norms; one lane per member) and each of
+// its waves takes one query at a time.  Per sketch row, u1's preferences are
+// hashed ONCE for the whole group into the wave's bucket row -- u1's sketch
+// row at the class shape -- and then, whichever is less work:
+//   dense (w <= 4 nnz(u1)): lane m forms valueAB = sum_j U1[j] * S_m[j] over
+//     the w buckets (U1[j] a broadcast read, S_m[j] at an odd member stride:
+//     conflict-free), valueA from one sweep over the row, which also zeroes it;
+//   sparse: 64 preferences at a time are parked as (bucket, increment) and
+//     lane m gathers its member's counters at them; the row is cleared by an
+//     exchange pass that yields valueA (k_po_pairs' scheme).
+// Every sum is an exact integer in fp64 while both norms are below 2^53;
+// pairs past that are listed for k_po_pairs' sequential replay.
+constexpr int kPoGroupMax = 64;            // members per narrow group: one lane each
+constexpr int kPoGroupLds = 96 * 1024;     // LDS for a group's own sketches
 constexpr int kPoGroupHistW = 2048;        // narrow classes: one LDS bucket row per wave
 constexpr int kPoGroupWaves = 4;
 constexpr int64_t kPoQueryChunk = 1024;    // query rows per workgroup (the group loads once)
@@ -311,11 +313,16 @@ struct PoAllArgs {
   int32_t weighted;
 };
 
-// LDS of a group workgroup: sketches [cnt][d][w] u32, bucket rows [waves][w]
+// member stride in LDS: odd, so lanes (members) reading the same bucket hit
+// distinct banks
+__host__ __device__ constexpr int po_member_stride(int w, int d) { return (w * d) | 1; }
+
+// LDS of a group workgroup: sketches [cnt][stride] u32, bucket rows [waves][w]
 // u32, parked (bucket, increment) [waves][64] x 2 u32, member sqrt norms
 // [kPoGroupMax][CMS_MAX_DEPTH] f64 (-1: norm >= 2^53), member rows [kPoGroupMax]
 __host__ __device__ constexpr size_t po_group_lds(int cnt, int w, int d) {
-  return (((size_t)cnt * d * w + (size_t)kPoGroupWaves * w + 2 * kPoGroupWaves * 64 + 1) & ~(size_t)1) * 4 +
+  return (((size_t)cnt * po_member_stride(w, d) + (size_t)kPoGroupWaves * w + 2 * kPoGroupWaves * 64 + 1) & ~(size_t)1) *
+             4 +
          (size_t)kPoGroupMax * CMS_MAX_DEPTH * 8 + kPoGroupMax * 8;
 }
 
@@ -323,57 +330,73 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
   extern __shared__ __align__(16) uint32_t lds[];
   const PoGroup g = a.groups[blockIdx.y];
   const int w = g.w, d = g.d, cnt = g.cnt;
-  const int dw = d * w;
+  const int dw = d * w, ms = po_member_stride(w, d);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  uint32_t* bl = lds;                                        // [cnt][d][w] members' own sketches
-  uint32_t* hist = bl + cnt * dw + wv * w;                   // this wave's bucket row
-  uint32_t* pj = bl + cnt * dw + kPoGroupWaves * w + wv * 128;  // parked buckets [64], increments [64]
+  uint32_t* bl = lds;                                        // [cnt][ms] members' own sketches
+  uint32_t* hist = bl + cnt * ms + wv * w;                   // this wave's bucket row
+  uint32_t* pj = bl + cnt * ms + kPoGroupWaves * w + wv * 128;  // parked buckets [64], increments [64]
   uint32_t* pv = pj + 64;
-  double* msq = reinterpret_cast<double*>(bl + ((cnt * dw + kPoGroupWaves * w + kPoGroupWaves * 128 + 1) & ~1));
+  double* msq = reinterpret_cast<double*>(bl + ((cnt * ms + kPoGroupWaves * w + kPoGroupWaves * 128 + 1) & ~1));
   int64_t* mrow = reinterpret_cast<int64_t*>(msq + kPoGroupMax * CMS_MAX_DEPTH);
   for (int m = 0; m < cnt; ++m) {
     const PoShape sm = a.shp[a.cmem[g.m0 + m]];
-    for (int j = tid; j < dw; j += 64 * kPoGroupWaves) bl[m * dw + j] = a.sk[sm.soff + j];
+    for (int j = tid; j < dw; j += 64 * kPoGroupWaves) bl[m * ms + j] = a.sk[sm.soff + j];
     if (tid < d) msq[m * CMS_MAX_DEPTH + tid] = a.norm[sm.roff + tid] < (1ULL << 53) ? a.nsq[sm.roff + tid] : -1.0;
   }
   if (tid < cnt) mrow[tid] = a.cmem[g.m0 + tid];
-  for (int j = tid; j < kPoGroupWaves * w; j += 64 * kPoGroupWaves) lds[cnt * dw + j] = 0u;
+  for (int j = tid; j < kPoGroupWaves * w; j += 64 * kPoGroupWaves) lds[cnt * ms + j] = 0u;
   __syncthreads();
-  const int mm = lane & (kPoGroupMax - 1), part = lane >> 4;  // gather lanes: member, quarter of the parked keys
+  const bool member = lane < cnt;
+  const uint32_t* brow0 = bl + (member ? lane : 0) * ms;
   const int64_t qa = (int64_t)blockIdx.x * kPoQueryChunk, qb = min(a.qc, qa + kPoQueryChunk);
   for (int64_t q = qa + wv; q < qb; q += kPoGroupWaves) {
     const int64_t u1 = a.q0 + q;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+    const bool dense = (int64_t)w <= 4 * (k1 - k0);
     double minc = DBL_MAX;  // lane m < cnt: member m's running Math.min
     bool inexact = false;
     for (int r = 0; r < d; ++r) {
       double acc = 0.0;
-      const uint32_t* brow = bl + mm * dw + r * w;
-      for (int64_t base = k0; base < k1; base += 64) {
-        const int64_t i = base + lane;
-        uint32_t j = 0, v = 0;
-        if (i < k1) {
-          j = bucket_wb(hp, r, a.kp[i], (uint32_t)w, g.barrett);
-          v = a.inc[i];
-          atomicAdd(&hist[j], v);
-        }
-        pj[lane] = j;
-        pv[lane] = v;  // (a wave's LDS operations execute in order: the parked pairs are read back below)
-        if (mm < cnt) {
-#pragma unroll 4
-          for (int t = part * 16; t < part * 16 + 16; ++t) acc = __fma_rn((double)pv[t], (double)brow[pj[t]], acc);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's adds land before its exchanges
       uint64_t a2 = 0;
-      for (int64_t i = k0 + lane; i < k1; i += 64) {
-        const uint32_t c = atomicExch(&hist[bucket_wb(hp, r, a.kp[i], (uint32_t)w, g.barrett)], 0u);
-        a2 = sat_add(a2, (uint64_t)c * c);
+      const uint32_t* brow = brow0 + r * w;
+      if (dense) {
+        for (int64_t i = k0 + lane; i < k1; i += 64)
+          atomicAdd(&hist[bucket_wbq(hp, r, a.kp[i], (uint32_t)w, g.barrett)], a.inc[i]);
+        // (a wave's LDS operations execute in order: the row is complete below)
+        if (member) {
+#pragma unroll 4
+          for (int j = 0; j < w; ++j) acc = __fma_rn((double)hist[j], (double)brow[j], acc);
+        }
+        for (int j = lane; j < w; j += 64) {
+          const uint32_t c = hist[j];
+          a2 = sat_add(a2, (uint64_t)c * c);
+          hist[j] = 0u;
+        }
+      } else {
+        for (int64_t base = k0; base < k1; base += 64) {
+          const int64_t i = base + lane;
+          uint32_t j = 0, v = 0;
+          if (i < k1) {
+            j = bucket_wbq(hp, r, a.kp[i], (uint32_t)w, g.barrett);
+            v = a.inc[i];
+            atomicAdd(&hist[j], v);
+          }
+          pj[lane] = j;
+          pv[lane] = v;  // read back below by every lane (in-order LDS)
+          const int nt = (int)min<int64_t>(64, k1 - base);
+          if (member) {
+#pragma unroll 4
+            for (int t = 0; t < nt; ++t) acc = __fma_rn((double)pv[t], (double)brow[pj[t]], acc);
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's adds land before its exchanges
+        for (int64_t i = k0 + lane; i < k1; i += 64) {
+          const uint32_t c = atomicExch(&hist[bucket_wbq(hp, r, a.kp[i], (uint32_t)w, g.barrett)], 0u);
+          a2 = sat_add(a2, (uint64_t)c * c);
+        }
       }
       a2 = po_wave_sum(a2);
-      acc += __shfl_xor(acc, 16, 64);  // the four quarters (exact: integers below 2^53)
-      acc += __shfl_xor(acc, 32, 64);
-      if (lane < cnt) {
+      if (member) {
         const double sb = msq[lane * CMS_MAX_DEPTH + r];
         if (a2 < (1ULL << 53) && sb >= 0.0) {
           const double den = __dmul_rn(__dsqrt_rn((double)a2), sb);
@@ -383,7 +406,7 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
         }
       }
     }
-    if (lane < cnt) {
+    if (member) {
       const int64_t u2 = mrow[lane];
       double res = minc == DBL_MAX ? __builtin_nan("") : minc;
       if (res == res) res = normalize_weight(res, a.weighted);
@@ -405,7 +428,7 @@ __global__ void k_po_point(const PoShape* shp, const uint32_t* sk, HashParams hp
     const uint64_t kp = reduce_key(keys[i]);
     double est = DBL_MAX;
     for (int d = 0; d < s.d; ++d) {
-      const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, kp, (uint32_t)s.w, s.barrett)];
+      const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wbq(hp, d, kp, (uint32_t)s.w, s.barrett)];
       if (v < est) est = v;
     }
     out[i] = ldexp(est, -hp.frac_bits);
@@ -427,7 +450,7 @@ __global__ void k_po_estimate(const PoShape* shp, const uint32_t* sk, HashParams
       const PoShape s = shp[r];
       double est = DBL_MAX;
       for (int d = 0; d < s.d; ++d) {
-        const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wb(hp, d, kp, (uint32_t)s.w, s.barrett)];
+        const double v = (double)sk[s.soff + (int64_t)d * s.w + bucket_wbq(hp, d, kp, (uint32_t)s.w, s.barrett)];
         if (v < est) est = v;
       }
       const float pref = (float)ldexp(est, -hp.frac_bits);
@@ -567,7 +590,7 @@ static int po_build_groups(cms_handle* h) {
     const int32_t w = h->h_po_w[ord[i]], d = h->h_po_d[ord[i]];
     size_t e = i;
     while (e < ord.size() && h->h_po_w[ord[e]] == w && h->h_po_d[ord[e]] == d) ++e;
-    const int64_t img = (int64_t)w * d * 4;
+    const int64_t img = (int64_t)po_member_stride(w, d) * 4;
     if (w <= kPoGroupHistW && img <= kPoGroupLds) {
       const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPoGroupMax, kPoGroupLds / img));
       for (size_t m = i; m < e; m += G) {

@@ -51,3 +51,25 @@ extern "C" void host_buckets_modes(const int64_t* a, const int64_t* b, int depth
   }
   fallbacks[0] = fb;
 }
+
+// bucket_wbq (the per-owner kernels' route for keys below 2^32) against
+// bucket_wb, any width: out_q / out_w [n][depth]
+extern "C" void host_buckets_wb(const int64_t* a, const int64_t* b, int depth, int width, const int64_t* keys,
+                                int64_t n, int32_t* out_q, int32_t* out_w) {
+  cms::HashParams hp{};
+  for (int i = 0; i < depth; ++i) {
+    hp.ap[i] = cms::reduce_key(a[i]);
+    hp.bp[i] = cms::reduce_key(b[i]);
+  }
+  hp.width = 1;
+  hp.depth = depth;
+  cms::hash_finish(hp);
+  const uint64_t barrett = (~0ULL) / (uint64_t)width;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t kp = cms::reduce_key(keys[i]);
+    for (int r = 0; r < depth; ++r) {
+      out_q[i * depth + r] = (int32_t)cms::bucket_wbq(hp, r, kp, (uint32_t)width, barrett);
+      out_w[i * depth + r] = (int32_t)cms::bucket_wb(hp, r, kp, (uint32_t)width, barrett);
+    }
+  }
+}

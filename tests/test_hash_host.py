@@ -113,3 +113,22 @@ def test_quotient_route_margin_cases(shim, oracle):
         each, exact, fb = _modes(shim, a, b, w, keys)
         assert fb >= keys.size  # every picked key took the margin route in its row
         np.testing.assert_array_equal(each, oracle.hash_keys(a, b, w, keys))
+
+
+@pytest.mark.parametrize("width", [1, 2, 7, 24, 39, 1000, 2047, 30011, 2440690, (1 << 31) - 1])
+def test_wbq_route_equals_barrett_route(shim, oracle, width):
+    """bucket_wbq (per-owner shapes: fp64 quotient + wrapping residue, then
+    Barrett) equals bucket_wb and the oracle for every width, keys below and
+    above 2^32 and the margin keys of test_quotient_route_margin_cases."""
+    rng = np.random.Generator(np.random.PCG64(width))
+    keys = np.concatenate([rng.integers(0, 2 ** 32, size=300000, dtype=np.int64),
+                           rng.integers(-2 ** 63, 2 ** 63 - 1, size=20000, dtype=np.int64),
+                           np.arange(0, 5000, dtype=np.int64), np.array([2 ** 32 - 1, 2 ** 32, -1], np.int64)])
+    a, b = oracle.hash_params(width % 1000 + 3, 24)
+    q = np.zeros((keys.size, 24), np.int32)
+    w = np.zeros((keys.size, 24), np.int32)
+    vp = ctypes.c_void_p
+    shim.host_buckets_wb(a.ctypes.data_as(vp), b.ctypes.data_as(vp), 24, width, keys.ctypes.data_as(vp),
+                         ctypes.c_int64(keys.size), q.ctypes.data_as(vp), w.ctypes.data_as(vp))
+    np.testing.assert_array_equal(q, w)
+    np.testing.assert_array_equal(q[:, :6], oracle.hash_keys(a[:6], b[:6], width, keys))
