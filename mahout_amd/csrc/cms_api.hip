@@ -343,6 +343,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.mid_u8_image = num("CMS_MID_U8_IMAGE", h->tune.mid_u8_image);
     h->tune.nib_persist = num("CMS_NIB_PERSIST", h->tune.nib_persist);
     h->tune.mid_image = num("CMS_MID_IMAGE", h->tune.mid_image);
+    h->tune.po_no_bigq = num("CMS_PO_NO_BIGQ", h->tune.po_no_bigq);
     h->tune.forms = !flag("CMS_NO_FORMS");
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");

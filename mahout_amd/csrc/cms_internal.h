@@ -204,7 +204,8 @@ struct Tunables {
   int mid_u4_keys = 768;    // CMS_MID_U4_KEYS: more keys start at u8 (list-row owners always try 4-bit)
   int mid_u8_keys = 12288;  // CMS_MID_U8_KEYS: more keys start at u16
   int nib_persist = 0;      // CMS_NIB_PERSIST=1: k_build_nibbles as persistent waves (else one owner per wave)
-  int mid_image = 1;        // CMS_MID_IMAGE=0: mid owners through k_build_mid's form passes, not the one-pass u16 image
+  int mid_image = 1;
+  int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)        // CMS_MID_IMAGE=0: mid owners through k_build_mid's form passes, not the one-pass u16 image
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
@@ -316,7 +317,7 @@ struct cms_handle {
   cms::DevBuf ws_hotpart;  // hot-owner routing of the partition: slot keys [1024] u64, sample counts [n] u32
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
   cms::DevBuf ws_slicepart;  // row build: u16 [hot + extra slices][d*w] partial rows of split owners (k_hot_reduce)
-  cms::DevBuf ws_query, ws_out, ws_srow, ws_f4, ws_i8blk;
+  cms::DevBuf ws_query, ws_query2, ws_out, ws_srow, ws_f4, ws_i8blk;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 
   // communicator: RCCL (cms_comm_init) or a caller transport (cms_comm_init_transport)
@@ -362,6 +363,12 @@ struct cms_handle {
   cms::DevBuf po_groups, po_cmem, po_redo;
   int64_t po_ngroups = 0, po_nnarrow = 0, po_wide0 = 0;  // groups, narrow groups, first wide member in po_cmem
   int32_t po_gmax_lds = 0;                       // largest LDS image of a narrow group (bytes)
+  // the narrow classes whole (one PoGroup each, po_classes) with their
+  // members' sketches transposed, [class][d * w][members] (po_skT): the
+  // big-query kernel's coalesced operand
+  cms::DevBuf po_classes, po_skT;
+  int64_t po_nclasses = 0;
+  int32_t po_class_maxdw = 0;
 
   // instrumentation
   int timing = 0;  // 0 off, 1 the roofline kernels' scopes only, 2 every scope (phase breakdown)

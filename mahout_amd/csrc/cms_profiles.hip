@@ -190,6 +190,9 @@ struct PoPairArgs {
   double* out;           // [nq][m], or with ldo > 0 a slab [nq][ldo] at column u2
   int64_t ldo;
   int32_t weighted;
+  // pairs k_po_bigq computes instead: queries of more than big_skip
+  // preferences against candidates of at most big_dw counters
+  int64_t big_skip = INT64_MAX, big_dw = 0;
 };
 
 __device__ __forceinline__ uint64_t po_wave_sum(uint64_t v) {
@@ -214,6 +217,7 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     const uint32_t w = (uint32_t)s.w;
     uint32_t* hist = (w <= (uint32_t)kPoHist) ? lds : gsc;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+    if (k1 - k0 > a.big_skip && (int64_t)s.w * s.d <= a.big_dw) continue;  // k_po_bigq's pair (uniform)
     double minc = DBL_MAX;
     // u1's counters at u2's shape: pass 1 adds every preference into the
     // bucket row; pass 2 takes each bucket back to zero with an exchange, so the
@@ -237,11 +241,47 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
       __syncthreads();
       return a2;
     };
+    // u1 with at most 4 preferences per lane: keys, increments and each
+    // row's buckets stay in registers (one load per pair, one hash per key
+    // and row; the exchange pass reuses the buckets)
+    const bool cached = k1 - k0 <= 4 * kPoThreads;
+    uint64_t ck[4];
+    uint32_t cv[4], cj[4];
+    if (cached) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = k0 + lane + (int64_t)u * kPoThreads;
+        ck[u] = i < k1 ? a.kp[i] : 0ULL;
+        cv[u] = i < k1 ? a.inc[i] : 0u;
+      }
+    }
     for (int d = 0; d < s.d; ++d) {
       const uint32_t* brow = a.sk + s.soff + (int64_t)d * w;
       uint64_t ab = 0;
-      add_pass(d, &ab, brow);
-      const uint64_t a2 = po_wave_sum(clear_pass(d));
+      uint64_t a2p = 0;
+      if (cached) {
+        uint32_t bv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          cj[u] = cv[u] ? bucket_wbq(hp, d, ck[u], w, s.barrett) : 0u;
+          bv[u] = cv[u] ? brow[cj[u]] : 0u;  // the gathers of all four keys in flight together
+          if (cv[u]) atomicAdd(&hist[cj[u]], cv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ab = sat_add(ab, (uint64_t)cv[u] * bv[u]);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (cv[u]) {
+            const uint32_t c = atomicExch(&hist[cj[u]], 0u);
+            a2p = sat_add(a2p, (uint64_t)c * c);
+          }
+        __syncthreads();
+      } else {
+        add_pass(d, &ab, brow);
+        a2p = clear_pass(d);
+      }
+      const uint64_t a2 = po_wave_sum(a2p);
       ab = po_wave_sum(ab);
       const uint64_t b2 = a.norm[s.roff + d];
       double valueAB, den;
@@ -311,6 +351,7 @@ struct PoAllArgs {
   uint32_t* redo_cnt;
   uint32_t redo_cap;
   int32_t weighted;
+  int64_t big_skip;  // queries with more preferences than this are k_po_bigq's
 };
 
 // member stride in LDS: odd, so lanes (members) reading the same bucket hit
@@ -352,6 +393,7 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
   for (int64_t q = qa + wv; q < qb; q += kPoGroupWaves) {
     const int64_t u1 = a.q0 + q;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+    if (k1 - k0 > a.big_skip) continue;  // k_po_bigq builds this query once per class
     const bool dense = (int64_t)w <= 4 * (k1 - k0);
     double minc = DBL_MAX;  // lane m < cnt: member m's running Math.min
     bool inexact = false;
@@ -417,6 +459,119 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
       }
       a.slab[q * a.n + u2] = res;
     }
+  }
+}
+
+// Queries with many preferences (more than kPoBigQuery): hashing u1 once
+// per group of 64 candidates would cost nnz(u1) x d per group -- the bulk of
+// the whole job at config 2, where the head items hold millions of
+// preferences.  Here u1's sketch at a narrow class's shape is built ONCE per
+// class by a whole workgroup in LDS, and every member of the class takes its
+// dense dot from the transposed member image po_skT (thread = member, so the
+// loads coalesce).  Same exact arithmetic and epilogue as k_po_group_pairs.
+constexpr int64_t kPoBigQuery = 4096;
+constexpr int64_t kPoBigMaxDW = 38 * 1024;  // u1's [d][w] u32 image in LDS (152 KiB)
+constexpr int kPoBigThreads = 256;
+struct PoBigArgs {
+  const int64_t* off;
+  const uint64_t* kp;
+  const uint32_t* inc;
+  const PoShape* shp;
+  const uint64_t* norm;
+  const double* nsq;
+  const PoGroup* classes;   // m0: first member in cmem, pad: offset of the class in skT (in counters / 64)
+  const int64_t* cmem;
+  const uint32_t* skT;
+  const int64_t* toff;      // [nclasses] offset of each class in skT
+  const int64_t* bigq;      // [nbig] slab rows (0-based within the block) of the big queries
+  int64_t q0, n;
+  double* slab;
+  unsigned long long* redo;
+  uint32_t* redo_cnt;
+  uint32_t redo_cap;
+  int32_t weighted;
+};
+
+__global__ __launch_bounds__(kPoBigThreads) void k_po_bigq(PoBigArgs a, HashParams hp) {
+  extern __shared__ __align__(16) uint32_t lds[];  // u1 at the class shape [d][w] u32
+  __shared__ unsigned long long s_a2[CMS_MAX_DEPTH];
+  const PoGroup c = a.classes[blockIdx.x];
+  const int64_t q = a.bigq[blockIdx.y];
+  const int64_t u1 = a.q0 + q;
+  const int w = c.w, d = c.d, dw = w * d;
+  const int tid = threadIdx.x;
+  for (int j = tid; j < dw; j += kPoBigThreads) lds[j] = 0u;
+  if (tid < CMS_MAX_DEPTH) s_a2[tid] = 0ULL;
+  __syncthreads();
+  const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+  for (int64_t i = k0 + tid; i < k1; i += kPoBigThreads) {
+    const uint64_t kp = a.kp[i];
+    const uint32_t v = a.inc[i];
+    for (int r = 0; r < d; ++r) atomicAdd(&lds[r * w + bucket_wbq(hp, r, kp, (uint32_t)w, c.barrett)], v);
+  }
+  __syncthreads();
+  for (int r = 0; r < d; ++r) {  // valueA of every row
+    uint64_t a2 = 0;
+    for (int j = tid; j < w; j += kPoBigThreads) {
+      const uint32_t x = lds[r * w + j];
+      a2 = sat_add(a2, (uint64_t)x * x);
+    }
+    a2 = po_wave_sum(a2);
+    if ((tid & 63) == 0 && a2) atomicAdd(&s_a2[r], (unsigned long long)a2);
+  }
+  __syncthreads();
+  const uint32_t* T = a.skT + a.toff[blockIdx.x];
+  // `parts` threads per member (a power of two up to a wave) split each dot
+  // over j; classes of 64+ members take one thread per member
+  int parts = 1;
+  while (parts < 64 && parts * 2 * c.cnt <= kPoBigThreads) parts *= 2;
+  const int part = tid & (parts - 1);
+  for (int m0 = tid / parts; m0 < ((c.cnt + (kPoBigThreads / parts) - 1) / (kPoBigThreads / parts)) * (kPoBigThreads / parts);
+       m0 += kPoBigThreads / parts) {
+    const int m = m0;
+    const bool live = m < c.cnt;
+    const int64_t u2 = live ? a.cmem[c.m0 + m] : 0;
+    const PoShape s2 = a.shp[u2];
+    double minc = DBL_MAX;
+    bool inexact = false;
+    for (int r = 0; r < d; ++r) {
+      double acc = 0.0;
+      if (live) {
+        const uint32_t* tr = T + (int64_t)r * w * c.cnt + m;
+#pragma unroll 4
+        for (int j = part; j < w; j += parts) acc = __fma_rn((double)lds[r * w + j], (double)tr[(int64_t)j * c.cnt], acc);
+      }
+      for (int o = 1; o < parts; o <<= 1) acc += __shfl_xor(acc, o, 64);  // exact: integers below 2^53
+      const uint64_t a2 = s_a2[r];
+      if (live && a2 < (1ULL << 53) && a.norm[s2.roff + r] < (1ULL << 53)) {
+        const double den = __dmul_rn(__dsqrt_rn((double)a2), a.nsq[s2.roff + r]);
+        if (den != 0.0) minc = java_min(minc, __ddiv_rn(acc, den));
+      } else {
+        inexact = true;
+      }
+    }
+    if (!live || part != 0) continue;
+    double res = minc == DBL_MAX ? __builtin_nan("") : minc;
+    if (res == res) res = normalize_weight(res, a.weighted);
+    if (inexact) {
+      res = __builtin_nan("");
+      const uint32_t slot = atomicAdd(a.redo_cnt, 1u);
+      if (slot < a.redo_cap) a.redo[slot] = ((unsigned long long)u1 << 32) | (unsigned long long)u2;
+    }
+    a.slab[q * a.n + u2] = res;
+  }
+}
+
+// po_skT[toff[c] + t * cnt_c + m] = member m's counter t (t < d w), every
+// narrow class c; one workgroup per (class, member)
+__global__ __launch_bounds__(256) void k_po_transpose(const PoGroup* classes, const int64_t* cmem, const int64_t* toff,
+                                                      const PoShape* shp, const uint32_t* sk, uint32_t* skT) {
+  const PoGroup c = classes[blockIdx.x];
+  for (int m = blockIdx.y; m < c.cnt; m += gridDim.y) {
+    const PoShape s = shp[cmem[c.m0 + m]];
+    const int dw = c.w * c.d;
+    uint32_t* T = skT + toff[blockIdx.x] + m;
+    for (int t = threadIdx.x; t < dw; t += 256) T[(int64_t)t * c.cnt] = sk[s.soff + t];
   }
 }
 
@@ -631,6 +786,55 @@ static int po_build_groups(cms_handle* h) {
   if (!cmem.empty())
     CMS_HIP(hipMemcpyAsync(h->po_cmem.ptr, cmem.data(), sizeof(int64_t) * cmem.size(), hipMemcpyHostToDevice,
                            h->stream));
+  // the narrow classes whole (consecutive narrow groups of one shape), with
+  // their offsets in the transposed member image
+  std::vector<PoGroup> classes;
+  std::vector<int64_t> toff;
+  int64_t tot = 0;
+  int32_t maxdw = 0;
+  for (const PoGroup& g : narrow) {
+    if (!classes.empty() && classes.back().w == g.w && classes.back().d == g.d) {
+      classes.back().cnt += g.cnt;
+    } else {
+      PoGroup c = g;
+      classes.push_back(c);
+    }
+  }
+  // wide owners small enough for k_po_bigq's LDS image: one class each (big
+  // queries only; k_po_pairs keeps their small queries)
+  for (size_t m = 0; m < cmem_w.size(); ++m) {
+    const int32_t w = h->h_po_w[cmem_w[m]], d = h->h_po_d[cmem_w[m]];
+    if ((int64_t)w * d > kPoBigMaxDW) continue;
+    PoGroup c{};
+    c.w = w;
+    c.d = d;
+    c.barrett = (~0ULL) / (uint64_t)w;
+    c.m0 = (int32_t)(cmem_n.size() + m);
+    c.cnt = 1;
+    classes.push_back(c);
+  }
+  for (const PoGroup& c : classes) {
+    toff.push_back(tot);
+    tot += (int64_t)c.cnt * c.w * c.d;
+    maxdw = std::max<int32_t>(maxdw, c.w * c.d);
+  }
+  h->po_nclasses = (int64_t)classes.size();
+  h->po_class_maxdw = maxdw;
+  if (!classes.empty()) {
+    CMS_HIP(h->po_classes.ensure(sizeof(PoGroup) * classes.size() + sizeof(int64_t) * toff.size()));
+    CMS_HIP(hipMemcpyAsync(h->po_classes.ptr, classes.data(), sizeof(PoGroup) * classes.size(), hipMemcpyHostToDevice,
+                           h->stream));
+    CMS_HIP(hipMemcpyAsync(h->po_classes.as<char>() + sizeof(PoGroup) * classes.size(), toff.data(),
+                           sizeof(int64_t) * toff.size(), hipMemcpyHostToDevice, h->stream));
+    CMS_HIP(h->po_skT.ensure(sizeof(uint32_t) * (size_t)std::max<int64_t>(tot, 1)));
+    int32_t maxcnt = 1;
+    for (const PoGroup& c : classes) maxcnt = std::max(maxcnt, c.cnt);
+    hipLaunchKernelGGL(k_po_transpose, dim3((unsigned)classes.size(), (unsigned)std::min(maxcnt, 256)), dim3(256), 0,
+                       h->stream, h->po_classes.as<PoGroup>(), h->po_cmem.as<int64_t>(),
+                       reinterpret_cast<const int64_t*>(h->po_classes.as<char>() + sizeof(PoGroup) * classes.size()),
+                       h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->po_skT.as<uint32_t>());
+    CMS_HIP(hipGetLastError());
+  }
   CMS_HIP(hipStreamSynchronize(h->stream));  // the host vectors die on return
   h->po_ngroups = (int64_t)groups.size();
   h->po_nnarrow = (int64_t)narrow.size();
@@ -757,6 +961,46 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
   a.redo_cnt = reinterpret_cast<uint32_t*>(a.redo + kRedoCap);
   a.redo_cap = kRedoCap;
   CMS_HIP(hipMemsetAsync(a.redo_cnt, 0, sizeof(uint32_t), h->stream));
+  // queries of more than kPoBigQuery preferences take the narrow classes
+  // through k_po_bigq (u1 hashed once per class); the group kernel skips them
+  std::vector<int64_t> bigq;
+  if (h->po_nclasses > 0 && !h->tune.po_no_bigq)
+    for (int64_t q = 0; q < qc; ++q)
+      if (h->h_po_off[q0 + q + 1] - h->h_po_off[q0 + q] > kPoBigQuery) bigq.push_back(q);
+  a.big_skip = bigq.empty() ? INT64_MAX : kPoBigQuery;
+  if (!bigq.empty()) {
+    TimedScope ts(h, "po_bigq");
+    CMS_HIP(h->ws_query2.ensure(sizeof(int64_t) * bigq.size()));
+    CMS_HIP(hipMemcpyAsync(h->ws_query2.ptr, bigq.data(), sizeof(int64_t) * bigq.size(), hipMemcpyHostToDevice,
+                           h->stream));
+    PoBigArgs b{};
+    b.off = a.off;
+    b.kp = a.kp;
+    b.inc = a.inc;
+    b.shp = a.shp;
+    b.norm = a.norm;
+    b.nsq = a.nsq;
+    b.classes = h->po_classes.as<PoGroup>();
+    b.cmem = a.cmem;
+    b.skT = h->po_skT.as<uint32_t>();
+    b.toff = reinterpret_cast<const int64_t*>(h->po_classes.as<char>() + sizeof(PoGroup) * h->po_nclasses);
+    b.bigq = h->ws_query2.as<int64_t>();
+    b.q0 = q0;
+    b.n = n;
+    b.slab = slab;
+    b.redo = a.redo;
+    b.redo_cnt = a.redo_cnt;
+    b.redo_cap = a.redo_cap;
+    b.weighted = a.weighted;
+    static bool battr = [] {
+      (void)hipFuncSetAttribute((const void*)k_po_bigq, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return true;
+    }();
+    (void)battr;
+    hipLaunchKernelGGL(k_po_bigq, dim3((unsigned)h->po_nclasses, (unsigned)bigq.size()), dim3(kPoBigThreads),
+                       sizeof(uint32_t) * (size_t)h->po_class_maxdw, h->stream, b, h->hp);
+    CMS_HIP(hipGetLastError());
+  }
   if (h->po_nnarrow > 0) {
     TimedScope ts(h, "po_group_pairs");
     static bool attr = [] {
@@ -788,6 +1032,8 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     p.out = slab;
     p.ldo = n;
     p.weighted = a.weighted;
+    p.big_skip = a.big_skip;
+    p.big_dw = bigq.empty() ? 0 : kPoBigMaxDW;
     TimedScope ts(h, "po_pair_cosine");
     hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(qc * nwide, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
                        h->stream, p, h->hp);

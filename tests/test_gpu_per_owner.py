@@ -248,3 +248,63 @@ def test_taste_mirror_cosinecm_with_countminsketchconfig(oracle):
         exp = oracle.per_owner_similarity(off, keys, vals, shapes, a, b, u1, u2)
         assert same(sim.userSimilarity(int(uid[u1]), int(uid[u2])), exp)
     sim.close()
+
+
+def test_big_queries_and_full_classes(oracle):
+    """Owners with more than 4096 preferences (k_po_bigq: u1 hashed once per
+    shape class, dense dots against the transposed member image) and classes
+    of more than 64 members (several 64-member groups, the dense and the
+    sparse dot path): the all-pairs top-k equals the per-pair kernel's rows,
+    a handle without the big-query kernel (CMS_PO_NO_BIGQ=1), and the
+    oracle's TopItems loop on sampled big and small rows."""
+    import os
+    from mahout_amd.synth import zipf_stream
+    items, users = zipf_stream(50_000, 3000, 300_000, seed=33)
+    off, keys, _ = to_csr(items, users, 3000)
+    nnz = np.diff(off)
+    assert (nnz > 4096).sum() >= 3 and (nnz <= 64).sum() > 1000
+    uid = np.arange(3000, dtype=np.int64) * 7 + 3
+    n, k = uid.size, 25
+    a, b = oracle.hash_params(SEED, 32)
+
+    def run(env):
+        old = {kk: os.environ.get(kk) for kk in env}
+        os.environ.update(env)
+        try:
+            with make(uid, off, keys, None) as t:
+                t.configure_owner_shapes(1.0, 50_000)
+                t.finalize()
+                shapes = t.owner_shapes()[2:]
+                lists = t.top_k_all(k)
+                big = np.flatnonzero(nnz > 4096)[:3].tolist()
+                rows = {q: t.similarities(int(uid[q]), uid) for q in big + [0, n // 2, n - 1]}
+                return shapes, lists, rows
+        finally:
+            for kk, v in old.items():
+                if v is None:
+                    os.environ.pop(kk, None)
+                else:
+                    os.environ[kk] = v
+
+    shapes, (ids, sc, cnt), rows = run({})
+    w, d = shapes
+    cls = {}
+    for r in range(n):
+        cls.setdefault((int(w[r]), int(d[r])), []).append(r)
+    assert max(len(v) for v in cls.values()) > 64
+    _, (ids2, sc2, cnt2), _ = run({"CMS_PO_NO_BIGQ": "1"})
+    assert np.array_equal(cnt, cnt2) and np.array_equal(ids, ids2) and same(sc, sc2)
+    for q, row in rows.items():
+        row = row.copy()
+        row[q] = np.nan
+        eids, esc = oracle.top_users(uid, row, k)
+        assert ids[q, :cnt[q]].tolist() == eids.tolist() and same(sc[q, :cnt[q]], esc), q
+    # the per-pair kernel's rows against the oracle (a big and a small query;
+    # the candidates of their lists plus a random sample: the oracle rebuilds
+    # both sketches per pair)
+    rng = np.random.default_rng(4)
+    for q in [list(rows)[0], n - 1]:
+        cols = np.unique(np.concatenate([np.searchsorted(uid, ids[q, :cnt[q]]), rng.choice(n, 60, replace=False)]))
+        cols = cols[cols != q]
+        exp = np.array([oracle.per_owner_similarity(off, keys, None, shapes, a, b, q, int(c)) for c in cols])
+        assert same(rows[q][cols], exp), q
