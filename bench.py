@@ -150,8 +150,11 @@ def per_owner_scale(items, users, n, n_users, rows=1024, all_pairs_budget_s=120.
             t0 = time.perf_counter()
             _, _, cnt = t.top_k_rows(r0, rows, 100)
             dt = time.perf_counter() - t0
+            st = t.stats()
             po[f"{name}_rows"] = {"first_row": r0, "rows": rows, "s": dt, "ordered_pairs_per_s": rows * n / dt,
-                                  "full_lists": int((cnt == 100).sum())}
+                                  "full_lists": int((cnt == 100).sum()),
+                                  "wide_pairs_bounded_total": st["po_wide_pairs"],
+                                  "wide_pairs_exact_total": st["po_wide_exact"]}
         # the WHOLE all-pairs top-100 (every one of the n*(n-1) ordered pairs),
         # when the block rates predict it finishes within all_pairs_budget_s
         rate = min(po["median_rows"]["ordered_pairs_per_s"], po["head_rows"]["ordered_pairs_per_s"])

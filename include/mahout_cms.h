@@ -447,6 +447,8 @@ typedef struct cms_stats {
   int32_t comm_kind;         /* 0 none (single-GPU path), 1 RCCL (cms_comm_init), 2 caller transport */
   int32_t device;            /* HIP device ordinal of the handle */
   int64_t list_rows;         /* narrow owners stored as sparse key-bucket lists (2 + 2 d m bytes, m keys) */
+  int64_t po_wide_pairs;     /* per-owner top-k: (query, wide owner) pairs given the row-0 bound so far */
+  int64_t po_wide_exact;     /* of those, pairs the bound could not rule out (computed exactly) */
 } cms_stats;
 /* out->struct_size must be set (at least through pairs_ingested); a caller
  * built against an older, shorter cms_stats receives the fields it knows. */

@@ -88,6 +88,8 @@ class CmsStats(ctypes.Structure):
         ("comm_kind", ctypes.c_int32),
         ("device", ctypes.c_int32),
         ("list_rows", ctypes.c_int64),
+        ("po_wide_pairs", ctypes.c_int64),
+        ("po_wide_exact", ctypes.c_int64),
     ]
 
 

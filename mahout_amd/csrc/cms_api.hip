@@ -343,6 +343,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.mid_u8_image = num("CMS_MID_U8_IMAGE", h->tune.mid_u8_image);
     h->tune.nib_persist = num("CMS_NIB_PERSIST", h->tune.nib_persist);
     h->tune.mid_image = num("CMS_MID_IMAGE", h->tune.mid_image);
+    h->tune.po_no_prune = num("CMS_PO_NO_PRUNE", h->tune.po_no_prune);
     h->tune.po_no_bigq = num("CMS_PO_NO_BIGQ", h->tune.po_no_bigq);
     h->tune.forms = !flag("CMS_NO_FORMS");
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
@@ -451,7 +452,7 @@ void cms_destroy(cms_handle* h) {
                   &h->ws_hotlist, &h->ws_tiles, &h->ws_slab, &h->ws_topq, &h->vl[0].buf, &h->vl[1].buf, &h->ws_nsq, &h->ws_cand,
                   &h->dlog_row, &h->dlog_key, &h->dlog_val, &h->dlog_cnt, &h->dlog_all, &h->ws_srow,
                   &h->ws_f4, &h->ws_i8blk, &h->po_off, &h->po_kp, &h->po_inc, &h->po_shape, &h->po_sk, &h->po_norm, &h->po_nsq,
-                  &h->po_scratch, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist, &h->ws_blist,
+                  &h->po_scratch, &h->po_wrows, &h->po_s0, &h->ws_pothr, &h->ws_posurv, &h->hot_tab, &h->ws_bound, &h->ws_force, &h->ws_plist, &h->ws_blist,
                   &h->ws_mbnd, &h->ws_mbits, &h->ws_mwoff, &h->ws_mpacked, &h->rf_ids, &h->rf_sc, &h->rf_cnt,
                   &h->rf_full, &h->rf_touch, &h->rf_new, &h->rf_redo, &h->rf_perm};
   for (DevBuf* b : ws) b->release();
@@ -1667,6 +1668,8 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->comm_kind = h->comm ? 1 : h->ext_comm ? 2 : 0;
   out->device = h->device;
   out->list_rows = forms[6];
+  out->po_wide_pairs = h->po_wide_pairs;
+  out->po_wide_exact = h->po_wide_exact;
   out->struct_size = (uint32_t)std::min<size_t>(want, sizeof(cms_stats));
   std::memcpy(dst, out, out->struct_size);  // the fields the caller's struct has room for
   return CMS_OK;

@@ -203,8 +203,13 @@ CMS_HD uint32_t bucket_wb(const HashParams& hp, int r, uint64_t kp, uint32_t w, 
 // is below 2^-20), the wrapping 64-bit residue s = a'k' + b' - q0 p (mod 2^64)
 // is then < p exactly when q0 = q, and one add or subtract of p repairs it
 // otherwise (direction from the fractional part); Barrett mod w as bucket_wb.
-CMS_HD uint32_t bucket_wbq(const HashParams& hp, int r, uint64_t kp, uint32_t w, uint64_t barrett) {
-  if ((kp >> 32) != 0) return bucket_wb(hp, r, kp, w, barrett);
+// residue_wbq is the width-independent part, (a_r k + b_r) mod p.
+CMS_HD uint64_t residue_wbq(const HashParams& hp, int r, uint64_t kp) {
+  if ((kp >> 32) != 0) {
+    uint64_t s = mulmod_p(hp.ap[r], kp) + hp.bp[r];
+    if (s >= kPrime) s -= kPrime;
+    return s;
+  }
   const double y = fma(hp.qa[r], (double)(uint32_t)kp, hp.qb[r]);
   const double fl = floor(y);
   const double fr = y - fl;
@@ -216,10 +221,19 @@ CMS_HD uint32_t bucket_wbq(const HashParams& hp, int r, uint64_t kp, uint32_t w,
   const uint64_t q = (uint32_t)qb.u;
   uint64_t s = hp.ap[r] * kp + hp.bp[r] - ((q << 63) - 25u * q);  // X - q0 p (mod 2^64)
   if (s >= kPrime) s = fr < 0.5 ? s + kPrime : s - kPrime;
+  return s;
+}
+
+// s mod w for s < 2^63 by the Barrett constant floor((2^64-1)/w)
+CMS_HD uint32_t mod_barrett(uint64_t s, uint32_t w, uint64_t barrett) {
   const uint64_t qq = (uint64_t)(((unsigned __int128)s * barrett) >> 64);
   uint64_t rem = s - qq * w;
   while (rem >= w) rem -= w;
   return (uint32_t)rem;
+}
+
+CMS_HD uint32_t bucket_wbq(const HashParams& hp, int r, uint64_t kp, uint32_t w, uint64_t barrett) {
+  return mod_barrett(residue_wbq(hp, r, kp), w, barrett);
 }
 
 }  // namespace cms

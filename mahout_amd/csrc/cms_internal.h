@@ -204,8 +204,9 @@ struct Tunables {
   int mid_u4_keys = 768;    // CMS_MID_U4_KEYS: more keys start at u8 (list-row owners always try 4-bit)
   int mid_u8_keys = 12288;  // CMS_MID_U8_KEYS: more keys start at u16
   int nib_persist = 0;      // CMS_NIB_PERSIST=1: k_build_nibbles as persistent waves (else one owner per wave)
-  int mid_image = 1;
-  int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)        // CMS_MID_IMAGE=0: mid owners through k_build_mid's form passes, not the one-pass u16 image
+  int mid_image = 0;        // CMS_MID_IMAGE=1: mid owners through the one-pass u16 image (k_build_image; slower on MI355X)
+  int po_no_prune = 0;      // CMS_PO_NO_PRUNE=1: every (query, wide owner) pair through k_po_pairs (no row-0 bound)
+  int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
@@ -362,13 +363,19 @@ struct cms_handle {
   // owners one per group), po_cmem the owner rows in group order
   cms::DevBuf po_groups, po_cmem, po_redo;
   int64_t po_ngroups = 0, po_nnarrow = 0, po_wide0 = 0;  // groups, narrow groups, first wide member in po_cmem
-  int32_t po_gmax_lds = 0;                       // largest LDS image of a narrow group (bytes)
+  int32_t po_gmax_lds = 0;                       // LDS of a group workgroup (bytes)
+  int32_t po_hist_w = 1;                         // widest narrow class (the waves' LDS bucket rows)
   // the narrow classes whole (one PoGroup each, po_classes) with their
   // members' sketches transposed, [class][d * w][members] (po_skT): the
   // big-query kernel's coalesced operand
   cms::DevBuf po_classes, po_skT;
   int64_t po_nclasses = 0;
   int32_t po_class_maxdw = 0;
+  // the wide owners by width (po_wrows) and every preference's row-0 residue
+  // (a_0 k + b_0) mod p (po_s0): k_po_wide_bound's operands; the top-k
+  // threshold scratch and the surviving (query, wide owner) pairs
+  cms::DevBuf po_wrows, po_s0, ws_pothr, ws_posurv;
+  int64_t po_wide_pairs = 0, po_wide_exact = 0;  // (query, wide owner) pairs bounded / computed exactly
 
   // instrumentation
   int timing = 0;  // 0 off, 1 the roofline kernels' scopes only, 2 every scope (phase breakdown)

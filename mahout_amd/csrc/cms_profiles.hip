@@ -190,15 +190,27 @@ struct PoPairArgs {
   double* out;           // [nq][m], or with ldo > 0 a slab [nq][ldo] at column u2
   int64_t ldo;
   int32_t weighted;
-  // pairs k_po_bigq computes instead: queries of more than big_skip
-  // preferences against candidates of at most big_dw counters
-  int64_t big_skip = INT64_MAX, big_dw = 0;
+  // list mode: the pairs (u1 << 32) | u2 of plist[0, nq) into slab row u1 - q0
+  const unsigned long long* plist = nullptr;
+  int64_t q0 = 0;
 };
 
 __device__ __forceinline__ uint64_t po_wave_sum(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = sat_add(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// Open-addressed LDS table of at most 256 distinct buckets: keys (bucket + 1)
+// at lds[0, kPoTab), counts at lds[kPoTab, 2 kPoTab); the slot of bucket j.
+constexpr int kPoTab = 512;
+__device__ __forceinline__ uint32_t po_tab_insert(uint32_t* lds, uint32_t j) {
+  uint32_t slot = (j * 2654435761u) >> 23;  // 9 bits
+  for (;;) {
+    const uint32_t prev = atomicCAS(&lds[slot], 0u, j + 1u);
+    if (prev == 0u || prev == j + 1u) return slot;
+    slot = (slot + 1u) & (kPoTab - 1);
+  }
 }
 
 // userSimilarity(u1 = qrows[t / m], u2 = crows[t % m]): one wave per pair.
@@ -208,16 +220,22 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
   for (int j = lane; j < kPoHist; j += kPoThreads) lds[j] = 0u;
   __syncthreads();
   uint32_t* gsc = a.scratch ? a.scratch + (int64_t)blockIdx.x * a.scratch_w : nullptr;
-  const int64_t total = a.nq * a.m;
+  const int64_t total = a.plist ? a.nq : a.nq * a.m;
   for (int64_t t = blockIdx.x; t < total; t += gridDim.x) {
-    const int64_t u1 = a.qrows[t / a.m];
-    const int64_t c = t % a.m;
-    const int64_t u2 = a.crows ? a.crows[c] : c;
+    int64_t u1, u2;
+    if (a.plist) {
+      const unsigned long long e = a.plist[t];
+      u1 = (int64_t)(e >> 32);
+      u2 = (int64_t)(e & 0xFFFFFFFFu);
+    } else {
+      u1 = a.qrows[t / a.m];
+      const int64_t c = t % a.m;
+      u2 = a.crows ? a.crows[c] : c;
+    }
     const PoShape s = a.shp[u2];
     const uint32_t w = (uint32_t)s.w;
     uint32_t* hist = (w <= (uint32_t)kPoHist) ? lds : gsc;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
-    if (k1 - k0 > a.big_skip && (int64_t)s.w * s.d <= a.big_dw) continue;  // k_po_bigq's pair (uniform)
     double minc = DBL_MAX;
     // u1's counters at u2's shape: pass 1 adds every preference into the
     // bucket row; pass 2 takes each bucket back to zero with an exchange, so the
@@ -245,6 +263,9 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     // row's buckets stay in registers (one load per pair, one hash per key
     // and row; the exchange pass reuses the buckets)
     const bool cached = k1 - k0 <= 4 * kPoThreads;
+    // a cached u1 against a width past the LDS row: its (at most 256) buckets
+    // go into an LDS hash table instead of a global bucket row
+    const bool tab = cached && w > (uint32_t)kPoHist;
     uint64_t ck[4];
     uint32_t cv[4], cj[4];
     if (cached) {
@@ -260,23 +281,38 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
       uint64_t ab = 0;
       uint64_t a2p = 0;
       if (cached) {
-        uint32_t bv[4];
+        uint32_t bv[4], sl[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           cj[u] = cv[u] ? bucket_wbq(hp, d, ck[u], w, s.barrett) : 0u;
           bv[u] = cv[u] ? brow[cj[u]] : 0u;  // the gathers of all four keys in flight together
-          if (cv[u]) atomicAdd(&hist[cj[u]], cv[u]);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (cv[u]) {
+            if (tab) {
+              sl[u] = po_tab_insert(lds, cj[u]);
+              atomicAdd(&lds[kPoTab + sl[u]], cv[u]);
+            } else {
+              atomicAdd(&hist[cj[u]], cv[u]);
+            }
+          }
 #pragma unroll
         for (int u = 0; u < 4; ++u) ab = sat_add(ab, (uint64_t)cv[u] * bv[u]);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (cv[u]) {
-            const uint32_t c = atomicExch(&hist[cj[u]], 0u);
+            const uint32_t c = atomicExch(tab ? &lds[kPoTab + sl[u]] : &hist[cj[u]], 0u);
             a2p = sat_add(a2p, (uint64_t)c * c);
           }
         __syncthreads();
+        if (tab) {  // every count is collected: the keys may go
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (cv[u]) lds[sl[u]] = 0u;
+          __syncthreads();
+        }
       } else {
         add_pass(d, &ab, brow);
         a2p = clear_pass(d);
@@ -307,7 +343,7 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     if (lane == 0) {
       double r = (minc == DBL_MAX) ? __builtin_nan("") : minc;
       if (r == r) r = normalize_weight(r, a.weighted);
-      a.out[a.ldo > 0 ? (t / a.m) * a.ldo + u2 : t] = r;
+      a.out[a.plist ? (u1 - a.q0) * a.ldo + u2 : a.ldo > 0 ? (t / a.m) * a.ldo + u2 : t] = r;
     }
   }
 }
@@ -316,24 +352,29 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
 // userSimilarity(u1, u2) for a block of query rows against every candidate,
 // the candidates grouped by their shape class (w, d): every member of a class
 // hashes u1's preferences identically (CosineCM.java:86 builds u1 at u2's
-// (delta, epsilon)), so a workgroup holds up to kPoGroupMax members' own
-// sketches in LDS (with their sqrt norms; one lane per member) and each of
-// its waves takes one query at a time.  Per sketch row, u1's preferences are
-// hashed ONCE for the whole group into the wave's bucket row -- u1's sketch
-// row at the class shape -- and then, whichever is less work:
+// (delta, epsilon)), so a group of up to 64 members of one class (one lane
+// each) shares the hashing, and each wave of a workgroup takes one query at
+// a time.  The members' own sketches are read from the class's transposed
+// image po_skT ([d w][members]: lane m's counter t at t * cnt + m, so a
+// wave's 64 member loads are one contiguous 256-byte read, L2-resident while
+// the workgroups of one XCD work through the same group); LDS holds only each
+// wave's bucket row.  Per sketch row, u1's preferences are hashed ONCE into
+// the wave's bucket row -- u1's sketch row at the class shape -- and then,
+// whichever is less work:
 //   dense (w <= 4 nnz(u1)): lane m forms valueAB = sum_j U1[j] * S_m[j] over
-//     the w buckets (U1[j] a broadcast read, S_m[j] at an odd member stride:
-//     conflict-free), valueA from one sweep over the row, which also zeroes it;
+//     the w buckets (U1[j] a broadcast LDS read), valueA from one sweep over
+//     the row, which also zeroes it;
 //   sparse: 64 preferences at a time are parked as (bucket, increment) and
 //     lane m gathers its member's counters at them; the row is cleared by an
 //     exchange pass that yields valueA (k_po_pairs' scheme).
 // Every sum is an exact integer in fp64 while both norms are below 2^53;
 // pairs past that are listed for k_po_pairs' sequential replay.
+constexpr int64_t kPoBigQuery = 4096;       // queries past this many preferences: k_po_bigq
+constexpr int64_t kPoBigMaxDW = 38 * 1024;  // k_po_bigq: u1's [d][w] u32 image in LDS (152 KiB)
 constexpr int kPoGroupMax = 64;            // members per narrow group: one lane each
-constexpr int kPoGroupLds = 96 * 1024;     // LDS for a group's own sketches
 constexpr int kPoGroupHistW = 2048;        // narrow classes: one LDS bucket row per wave
-constexpr int kPoGroupWaves = 4;
-constexpr int64_t kPoQueryChunk = 1024;    // query rows per workgroup (the group loads once)
+constexpr int kPoGroupWaves = 8;
+constexpr int64_t kPoQueryChunk = 64;      // query rows per workgroup
 
 struct PoAllArgs {
   const int64_t* off;
@@ -343,8 +384,13 @@ struct PoAllArgs {
   const uint32_t* sk;
   const uint64_t* norm;
   const double* nsq;
-  const PoGroup* groups;
+  const PoGroup* groups;   // narrow groups: pad = class index
+  const PoGroup* classes;  // m0 = the class's first member in cmem
+  const int64_t* toff;     // [nclasses] class offsets in skT
+  const uint32_t* skT;
   const int64_t* cmem;
+  int64_t ngroups, nchunks, per_xcd;
+  int32_t hist_w;          // LDS bucket row stride per wave
   int64_t q0, qc, n;
   double* slab;  // [qc][n], column = candidate row
   unsigned long long* redo;  // (u1 << 32) | u2 of pairs past the exact regime
@@ -354,64 +400,65 @@ struct PoAllArgs {
   int64_t big_skip;  // queries with more preferences than this are k_po_bigq's
 };
 
-// member stride in LDS: odd, so lanes (members) reading the same bucket hit
-// distinct banks
-__host__ __device__ constexpr int po_member_stride(int w, int d) { return (w * d) | 1; }
-
-// LDS of a group workgroup: sketches [cnt][stride] u32, bucket rows [waves][w]
-// u32, parked (bucket, increment) [waves][64] x 2 u32, member sqrt norms
-// [kPoGroupMax][CMS_MAX_DEPTH] f64 (-1: norm >= 2^53), member rows [kPoGroupMax]
-__host__ __device__ constexpr size_t po_group_lds(int cnt, int w, int d) {
-  return (((size_t)cnt * po_member_stride(w, d) + (size_t)kPoGroupWaves * w + 2 * kPoGroupWaves * 64 + 1) & ~(size_t)1) *
-             4 +
-         (size_t)kPoGroupMax * CMS_MAX_DEPTH * 8 + kPoGroupMax * 8;
+// LDS of a group workgroup: bucket rows [waves][hist_w] u32, parked
+// (bucket, increment) [waves][64] x 2 u32
+__host__ __device__ constexpr size_t po_group_lds(int hist_w) {
+  return (size_t)kPoGroupWaves * ((size_t)hist_w + 128) * 4;
 }
 
 __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs a, HashParams hp) {
   extern __shared__ __align__(16) uint32_t lds[];
-  const PoGroup g = a.groups[blockIdx.y];
+  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so the
+  // (group, query chunk) tiles are numbered per XCD -- each XCD works through
+  // consecutive groups, all query chunks of one group back to back, and the
+  // group's member image stays in that XCD's L2
+  const int64_t c = (int64_t)(blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
+  if (c >= a.ngroups * a.nchunks) return;
+  const PoGroup g = a.groups[c / a.nchunks];
+  const int64_t chunk = c % a.nchunks;
+  const PoGroup cl = a.classes[g.pad];
   const int w = g.w, d = g.d, cnt = g.cnt;
-  const int dw = d * w, ms = po_member_stride(w, d);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  uint32_t* bl = lds;                                        // [cnt][ms] members' own sketches
-  uint32_t* hist = bl + cnt * ms + wv * w;                   // this wave's bucket row
-  uint32_t* pj = bl + cnt * ms + kPoGroupWaves * w + wv * 128;  // parked buckets [64], increments [64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* hist = lds + wv * (a.hist_w + 128);  // this wave's bucket row
+  uint32_t* pj = hist + a.hist_w;                // parked buckets [64], increments [64]
   uint32_t* pv = pj + 64;
-  double* msq = reinterpret_cast<double*>(bl + ((cnt * ms + kPoGroupWaves * w + kPoGroupWaves * 128 + 1) & ~1));
-  int64_t* mrow = reinterpret_cast<int64_t*>(msq + kPoGroupMax * CMS_MAX_DEPTH);
-  for (int m = 0; m < cnt; ++m) {
-    const PoShape sm = a.shp[a.cmem[g.m0 + m]];
-    for (int j = tid; j < dw; j += 64 * kPoGroupWaves) bl[m * ms + j] = a.sk[sm.soff + j];
-    if (tid < d) msq[m * CMS_MAX_DEPTH + tid] = a.norm[sm.roff + tid] < (1ULL << 53) ? a.nsq[sm.roff + tid] : -1.0;
-  }
-  if (tid < cnt) mrow[tid] = a.cmem[g.m0 + tid];
-  for (int j = tid; j < kPoGroupWaves * w; j += 64 * kPoGroupWaves) lds[cnt * ms + j] = 0u;
-  __syncthreads();
+  for (int j = lane; j < w; j += 64) hist[j] = 0u;
   const bool member = lane < cnt;
-  const uint32_t* brow0 = bl + (member ? lane : 0) * ms;
-  const int64_t qa = (int64_t)blockIdx.x * kPoQueryChunk, qb = min(a.qc, qa + kPoQueryChunk);
+  const int64_t u2 = member ? a.cmem[g.m0 + lane] : 0;
+  const int64_t roff = member ? a.shp[u2].roff : 0;
+  const int64_t ccnt = cl.cnt;  // member stride of the class image
+  const uint32_t* T = a.skT + a.toff[g.pad] + (g.m0 - cl.m0) + (member ? lane : 0);
+  const int64_t qa = chunk * kPoQueryChunk, qb = min(a.qc, qa + kPoQueryChunk);
   for (int64_t q = qa + wv; q < qb; q += kPoGroupWaves) {
     const int64_t u1 = a.q0 + q;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
-    if (k1 - k0 > a.big_skip) continue;  // k_po_bigq builds this query once per class
+    if (k1 - k0 > a.big_skip && w * d <= kPoBigMaxDW) continue;  // k_po_bigq builds this query once per class
     const bool dense = (int64_t)w <= 4 * (k1 - k0);
     double minc = DBL_MAX;  // lane m < cnt: member m's running Math.min
     bool inexact = false;
     for (int r = 0; r < d; ++r) {
       double acc = 0.0;
       uint64_t a2 = 0;
-      const uint32_t* brow = brow0 + r * w;
+      const uint32_t* trow = T + (int64_t)r * w * ccnt;
       if (dense) {
         for (int64_t i = k0 + lane; i < k1; i += 64)
           atomicAdd(&hist[bucket_wbq(hp, r, a.kp[i], (uint32_t)w, g.barrett)], a.inc[i]);
         // (a wave's LDS operations execute in order: the row is complete below)
         if (member) {
-#pragma unroll 4
-          for (int j = 0; j < w; ++j) acc = __fma_rn((double)hist[j], (double)brow[j], acc);
+          int j = 0;
+          for (; j + 8 <= w; j += 8) {
+            uint32_t t8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t8[u] = trow[(int64_t)(j + u) * ccnt];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = __fma_rn((double)hist[j + u], (double)t8[u], acc);
+          }
+          for (; j < w; ++j) acc = __fma_rn((double)hist[j], (double)trow[(int64_t)j * ccnt], acc);
         }
         for (int j = lane; j < w; j += 64) {
-          const uint32_t c = hist[j];
-          a2 = sat_add(a2, (uint64_t)c * c);
+          const uint32_t cc = hist[j];
+          a2 = sat_add(a2, (uint64_t)cc * cc);
           hist[j] = 0u;
         }
       } else {
@@ -427,21 +474,27 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
           pv[lane] = v;  // read back below by every lane (in-order LDS)
           const int nt = (int)min<int64_t>(64, k1 - base);
           if (member) {
-#pragma unroll 4
-            for (int t = 0; t < nt; ++t) acc = __fma_rn((double)pv[t], (double)brow[pj[t]], acc);
+            int t = 0;
+            for (; t + 8 <= nt; t += 8) {
+              uint32_t t8[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) t8[u] = trow[(int64_t)pj[t + u] * ccnt];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) acc = __fma_rn((double)pv[t + u], (double)t8[u], acc);
+            }
+            for (; t < nt; ++t) acc = __fma_rn((double)pv[t], (double)trow[(int64_t)pj[t] * ccnt], acc);
           }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's adds land before its exchanges
         for (int64_t i = k0 + lane; i < k1; i += 64) {
-          const uint32_t c = atomicExch(&hist[bucket_wbq(hp, r, a.kp[i], (uint32_t)w, g.barrett)], 0u);
-          a2 = sat_add(a2, (uint64_t)c * c);
+          const uint32_t cc = atomicExch(&hist[bucket_wbq(hp, r, a.kp[i], (uint32_t)w, g.barrett)], 0u);
+          a2 = sat_add(a2, (uint64_t)cc * cc);
         }
       }
       a2 = po_wave_sum(a2);
       if (member) {
-        const double sb = msq[lane * CMS_MAX_DEPTH + r];
-        if (a2 < (1ULL << 53) && sb >= 0.0) {
-          const double den = __dmul_rn(__dsqrt_rn((double)a2), sb);
+        if (a2 < (1ULL << 53) && a.norm[roff + r] < (1ULL << 53)) {
+          const double den = __dmul_rn(__dsqrt_rn((double)a2), a.nsq[roff + r]);
           if (den != 0.0) minc = java_min(minc, __ddiv_rn(acc, den));
         } else {
           inexact = true;
@@ -449,7 +502,6 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
       }
     }
     if (member) {
-      const int64_t u2 = mrow[lane];
       double res = minc == DBL_MAX ? __builtin_nan("") : minc;
       if (res == res) res = normalize_weight(res, a.weighted);
       if (inexact) {  // k_po_pairs replays the reference's sequential loop
@@ -469,8 +521,6 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
 // class by a whole workgroup in LDS, and every member of the class takes its
 // dense dot from the transposed member image po_skT (thread = member, so the
 // loads coalesce).  Same exact arithmetic and epilogue as k_po_group_pairs.
-constexpr int64_t kPoBigQuery = 4096;
-constexpr int64_t kPoBigMaxDW = 38 * 1024;  // u1's [d][w] u32 image in LDS (152 KiB)
 constexpr int kPoBigThreads = 256;
 struct PoBigArgs {
   const int64_t* off;
@@ -499,6 +549,7 @@ __global__ __launch_bounds__(kPoBigThreads) void k_po_bigq(PoBigArgs a, HashPara
   const int64_t q = a.bigq[blockIdx.y];
   const int64_t u1 = a.q0 + q;
   const int w = c.w, d = c.d, dw = w * d;
+  if (dw > kPoBigMaxDW) return;  // (uniform) the group kernel keeps this class's big queries
   const int tid = threadIdx.x;
   for (int j = tid; j < dw; j += kPoBigThreads) lds[j] = 0u;
   if (tid < CMS_MAX_DEPTH) s_a2[tid] = 0ULL;
@@ -572,6 +623,134 @@ __global__ __launch_bounds__(256) void k_po_transpose(const PoGroup* classes, co
     const int dw = c.w * c.d;
     uint32_t* T = skT + toff[blockIdx.x] + m;
     for (int t = threadIdx.x; t < dw; t += 256) T[(int64_t)t * c.cnt] = sk[s.soff + t];
+  }
+}
+
+// ------------------------------------------ wide candidates: row-0 bound --
+// A wide owner u2 (its sketch too large for a group's LDS) against a query u1
+// costs nnz(u1) x d2 hashes and gathers per pair, and config 2 has 1,289 of
+// them against 100K queries (2.1e11 key-rows).  mostSimilar only keeps the
+// top k, so each pair first gets a cheap UPPER bound from sketch row 0:
+//   userSimilarity = normalize(min over rows r with den != 0 of AB_r / den_r)
+//                 <= normalize(AB_0 / (sqrt(sum v^2) * sqrt(B_0)))
+// (valueA_0 = sum_j U1_0[j]^2 >= max(sum_k v_k^2, (sum_k v_k)^2 / w2) because
+// the increments are non-negative; every fp64 step is correctly rounded and monotone, and
+// normalize is non-decreasing).  A pair whose bound is below the query's
+// current k-th best score (the narrow candidates' top k, computed first) can
+// not enter the list and is written NaN, which TopItems skips; every other
+// pair is listed for k_po_pairs' exact computation.  The bound applies only
+// while the exact regime holds (sum v < 2^26 so every valueA < 2^53, and
+// B_0 < 2^53): row 0's value is then the same exact expression with the true
+// valueA_0.  The row-0 residues (a_0 k + b_0) mod p are precomputed per
+// preference (po_s0), so a key costs a Barrett reduction by u2's width and
+// one gather.  Lane = wide owner (sorted by width), wave = query: the keys
+// are wave-uniform (scalar loads), no reductions.
+constexpr int kPoBoundWaves = 4;
+struct PoBoundArgs {
+  const int64_t* off;
+  const uint32_t* inc;
+  const uint64_t* s0;
+  const PoShape* shp;
+  const uint32_t* sk;
+  const uint64_t* norm;
+  const double* nsq;
+  const int64_t* wrows;  // [nwide] wide owner rows
+  int64_t nwide;
+  const double* tsc;     // [qc][k] the narrow candidates' top-k scores
+  const int32_t* tcnt;   // [qc] their list lengths
+  int32_t k;
+  int64_t q0, qc, n;
+  double* slab;
+  unsigned long long* surv;  // surviving pairs (u1 << 32) | u2
+  uint32_t* surv_cnt;
+  int32_t weighted;
+};
+
+// s mod w (s < 2^63, w < 2^30) by the Barrett constant floor((2^64-1)/w):
+// the quotient estimate is q - 2 .. q, so the remainder is below 3w < 2^32
+// and its low 32 bits are the whole of it; two branch-free corrections
+__device__ __forceinline__ uint32_t po_mod_w(uint64_t s, uint32_t w, uint64_t barrett) {
+  const uint64_t qq = (uint64_t)(((unsigned __int128)s * barrett) >> 64);
+  uint32_t rem = (uint32_t)s - (uint32_t)qq * w;
+  rem = rem >= w ? rem - w : rem;
+  rem = rem >= w ? rem - w : rem;
+  return rem;
+}
+
+__global__ __launch_bounds__(256) void k_po_s0(const uint64_t* kp, int64_t np, HashParams hp, uint64_t* s0) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x)
+    s0[i] = residue_wbq(hp, 0, kp[i]);
+}
+
+__global__ __launch_bounds__(256) void k_po_nanfill(double* slab, int64_t n, const int64_t* wrows, int64_t nwide) {
+  double* row = slab + (int64_t)blockIdx.x * n;
+  for (int64_t m = threadIdx.x; m < nwide; m += blockDim.x) row[wrows[m]] = __builtin_nan("");
+}
+
+__global__ __launch_bounds__(64 * kPoBoundWaves) void k_po_wide_bound(PoBoundArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int64_t q = (int64_t)blockIdx.y * kPoBoundWaves + wv;
+  if (q >= a.qc) return;  // wave-uniform
+  const int64_t m = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = m < a.nwide;
+  const int64_t u2 = a.wrows[live ? m : 0];
+  const PoShape s = a.shp[u2];
+  const uint32_t* row0 = a.sk + s.soff;
+  const uint32_t w = (uint32_t)s.w;
+  const int64_t u1 = a.q0 + q;
+  const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+  uint64_t ab = 0, a2 = 0, as = 0;
+  int64_t i = k0;
+  for (; i + 8 <= k1; i += 8) {  // the keys' scalar loads together, then eight gathers in flight
+    uint64_t sv[8];
+    uint32_t v[8], c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      sv[u] = a.s0[i + u];
+      v[u] = a.inc[i + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c[u] = row0[po_mod_w(sv[u], w, s.barrett)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ab += (uint64_t)v[u] * c[u];
+      a2 += (uint64_t)v[u] * v[u];
+      as += v[u];
+    }
+  }
+  for (; i < k1; ++i) {
+    const uint32_t v = a.inc[i];
+    ab += (uint64_t)v * row0[po_mod_w(a.s0[i], w, s.barrett)];
+    a2 += (uint64_t)v * v;
+    as += v;
+  }
+  // (sums wrap only past sum v >= 2^26, where no pair is pruned)
+  bool prune = false;
+  const int32_t tc = a.tcnt[q];
+  if (live && tc >= a.k && as < (1ULL << 26) && a2 != 0 && a.norm[s.roff] < (1ULL << 53)) {
+    const double sb = a.nsq[s.roff];
+    // valueA_0 >= (sum_j U1_0[j])^2 / w as well (Cauchy-Schwarz over the w
+    // buckets): the tighter of the two when u1 has many more preferences than
+    // u2 has buckets
+    const uint64_t spread = (as * as + w - 1) / w;
+    if (spread > a2) a2 = spread;
+    if (sb != 0.0) {
+      const double ub = normalize_weight(__ddiv_rn((double)ab, __dmul_rn(__dsqrt_rn((double)a2), sb)), a.weighted);
+      prune = ub < a.tsc[q * a.k + a.k - 1];
+    }
+  }
+  if (live && prune) a.slab[q * a.n + u2] = __builtin_nan("");
+  const bool keep = live && !prune;
+  const uint64_t mask = __ballot(keep);
+  if (mask == 0) return;
+  const int first = __builtin_ctzll(mask);
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(a.surv_cnt, (uint32_t)__builtin_popcountll(mask));
+  base = __shfl(base, first, 64);
+  if (keep) {
+    const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ULL << lane) - 1ULL));
+    a.surv[base + rank] = ((unsigned long long)u1 << 32) | (unsigned long long)u2;
   }
 }
 
@@ -726,9 +905,11 @@ int po_require_shapes(cms_handle* h, const int64_t* rows, int64_t m) {
 }
 
 // Candidate groups of the all-pairs slabs: owners sorted by shape class
-// (d, w); a class whose bucket row fits a wave's LDS row and whose sketches
-// fit the group image is cut into groups of up to kPoGroupMax members, every
-// other owner (wide) is its own group for k_po_pairs.  Narrow groups first.
+// (d, w); a class whose bucket row fits a wave's LDS row (narrow) is cut into
+// groups of up to kPoGroupMax members, every other owner (wide) is its own
+// group for k_po_pairs.  Narrow groups first.  The narrow classes whole, with
+// their members' sketches transposed (po_skT), are the operand of both the
+// group kernel and k_po_bigq.
 static int po_build_groups(cms_handle* h) {
   const int64_t n = h->n;
   std::vector<int64_t> ord;
@@ -738,27 +919,34 @@ static int po_build_groups(cms_handle* h) {
   std::stable_sort(ord.begin(), ord.end(), [&](int64_t x, int64_t y) {
     return h->h_po_d[x] != h->h_po_d[y] ? h->h_po_d[x] < h->h_po_d[y] : h->h_po_w[x] < h->h_po_w[y];
   });
-  std::vector<PoGroup> narrow, wide;
-  std::vector<int64_t> cmem_n, cmem_w;
-  int32_t gmax = 0;
+  std::vector<PoGroup> narrow, classes;
+  std::vector<int64_t> cmem_n, cmem_w, toff;
+  int32_t hist_w = 1, maxdw = 0;
+  int64_t tot = 0;
   for (size_t i = 0; i < ord.size();) {
     const int32_t w = h->h_po_w[ord[i]], d = h->h_po_d[ord[i]];
     size_t e = i;
     while (e < ord.size() && h->h_po_w[ord[e]] == w && h->h_po_d[ord[e]] == d) ++e;
-    const int64_t img = (int64_t)po_member_stride(w, d) * 4;
-    if (w <= kPoGroupHistW && img <= kPoGroupLds) {
-      const int G = (int)std::max<int64_t>(1, std::min<int64_t>(kPoGroupMax, kPoGroupLds / img));
-      for (size_t m = i; m < e; m += G) {
-        const int cnt = (int)std::min<size_t>(G, e - m);
-        PoGroup g{};
-        g.w = w;
-        g.d = d;
-        g.barrett = (~0ULL) / (uint64_t)w;
+    if (w <= kPoGroupHistW) {
+      PoGroup c{};
+      c.w = w;
+      c.d = d;
+      c.barrett = (~0ULL) / (uint64_t)w;
+      c.m0 = (int32_t)cmem_n.size();
+      c.cnt = (int32_t)(e - i);
+      const int32_t ci = (int32_t)classes.size();
+      classes.push_back(c);
+      toff.push_back(tot);
+      tot += (int64_t)c.cnt * w * d;
+      maxdw = std::max<int32_t>(maxdw, w * d);
+      hist_w = std::max(hist_w, w);
+      for (size_t m = i; m < e; m += kPoGroupMax) {
+        PoGroup g = c;
         g.m0 = (int32_t)cmem_n.size();
-        g.cnt = cnt;
-        for (int q = 0; q < cnt; ++q) cmem_n.push_back(ord[m + q]);
+        g.cnt = (int)std::min<size_t>(kPoGroupMax, e - m);
+        g.pad = ci;
+        for (int q = 0; q < g.cnt; ++q) cmem_n.push_back(ord[m + q]);
         narrow.push_back(g);
-        gmax = std::max<int32_t>(gmax, (int32_t)po_group_lds(cnt, w, d));
       }
     } else {
       for (size_t m = i; m < e; ++m) cmem_w.push_back(ord[m]);
@@ -786,38 +974,6 @@ static int po_build_groups(cms_handle* h) {
   if (!cmem.empty())
     CMS_HIP(hipMemcpyAsync(h->po_cmem.ptr, cmem.data(), sizeof(int64_t) * cmem.size(), hipMemcpyHostToDevice,
                            h->stream));
-  // the narrow classes whole (consecutive narrow groups of one shape), with
-  // their offsets in the transposed member image
-  std::vector<PoGroup> classes;
-  std::vector<int64_t> toff;
-  int64_t tot = 0;
-  int32_t maxdw = 0;
-  for (const PoGroup& g : narrow) {
-    if (!classes.empty() && classes.back().w == g.w && classes.back().d == g.d) {
-      classes.back().cnt += g.cnt;
-    } else {
-      PoGroup c = g;
-      classes.push_back(c);
-    }
-  }
-  // wide owners small enough for k_po_bigq's LDS image: one class each (big
-  // queries only; k_po_pairs keeps their small queries)
-  for (size_t m = 0; m < cmem_w.size(); ++m) {
-    const int32_t w = h->h_po_w[cmem_w[m]], d = h->h_po_d[cmem_w[m]];
-    if ((int64_t)w * d > kPoBigMaxDW) continue;
-    PoGroup c{};
-    c.w = w;
-    c.d = d;
-    c.barrett = (~0ULL) / (uint64_t)w;
-    c.m0 = (int32_t)(cmem_n.size() + m);
-    c.cnt = 1;
-    classes.push_back(c);
-  }
-  for (const PoGroup& c : classes) {
-    toff.push_back(tot);
-    tot += (int64_t)c.cnt * c.w * c.d;
-    maxdw = std::max<int32_t>(maxdw, c.w * c.d);
-  }
   h->po_nclasses = (int64_t)classes.size();
   h->po_class_maxdw = maxdw;
   if (!classes.empty()) {
@@ -835,11 +991,20 @@ static int po_build_groups(cms_handle* h) {
                        h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->po_skT.as<uint32_t>());
     CMS_HIP(hipGetLastError());
   }
+  // the wide owners by width for k_po_wide_bound (lanes of a wave alike)
+  std::vector<int64_t> wrows(cmem_w);
+  std::stable_sort(wrows.begin(), wrows.end(), [&](int64_t x, int64_t y) { return h->h_po_w[x] < h->h_po_w[y]; });
+  if (!wrows.empty()) {
+    CMS_HIP(h->po_wrows.ensure(sizeof(int64_t) * wrows.size()));
+    CMS_HIP(hipMemcpyAsync(h->po_wrows.ptr, wrows.data(), sizeof(int64_t) * wrows.size(), hipMemcpyHostToDevice,
+                           h->stream));
+  }
   CMS_HIP(hipStreamSynchronize(h->stream));  // the host vectors die on return
   h->po_ngroups = (int64_t)groups.size();
   h->po_nnarrow = (int64_t)narrow.size();
   h->po_wide0 = (int64_t)cmem_n.size();
-  h->po_gmax_lds = gmax;
+  h->po_hist_w = hist_w;
+  h->po_gmax_lds = (int32_t)po_group_lds(hist_w);
   return CMS_OK;
 }
 
@@ -877,6 +1042,12 @@ int po_finalize(cms_handle* h) {
       CMS_HIP(h->po_scratch.ensure(need));
       CMS_HIP(hipMemsetAsync(h->po_scratch.ptr, 0, h->po_scratch.bytes, h->stream));
     }
+  }
+  CMS_HIP(h->po_s0.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(h->po_npairs, 1)));
+  if (h->po_npairs > 0) {
+    hipLaunchKernelGGL(k_po_s0, dim3(grid_for((h->po_npairs + 255) / 256, 16384)), dim3(256), 0, h->stream,
+                       h->po_kp.as<uint64_t>(), h->po_npairs, h->hp, h->po_s0.as<uint64_t>());
+    CMS_HIP(hipGetLastError());
   }
   if (int rc = po_build_groups(h)) return rc;
   CMS_HIP(hipStreamSynchronize(h->stream));
@@ -936,9 +1107,12 @@ int po_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_nb
 
 // slab[q][c] = userSimilarity(q0 + q, c) for q < qc and every candidate c
 // (d_qrows: the rows q0 .. q0 + qc - 1 on the device): the narrow groups on
-// k_po_group_pairs, the wide owners and any pair past the exact regime on
-// k_po_pairs (scattered into the slab's columns).
-static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t* d_qrows, double* slab) {
+// k_po_group_pairs (big queries on k_po_bigq), the wide owners and any pair
+// past the exact regime on k_po_pairs (scattered into the slab's columns).
+// prune_k > 0: the slab feeds a top-prune_k selection, and wide pairs whose
+// row-0 bound (k_po_wide_bound) cannot reach a query's list are NaN instead.
+static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t* d_qrows, double* slab,
+                            int32_t prune_k) {
   const int64_t n = h->n;
   PoAllArgs a{};
   a.off = h->po_off.as<int64_t>();
@@ -993,23 +1167,34 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     b.redo_cap = a.redo_cap;
     b.weighted = a.weighted;
     static bool battr = [] {
-      (void)hipFuncSetAttribute((const void*)k_po_bigq, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      // the dynamic image only: the static s_a2 counts against the same 160 KiB
+      (void)hipFuncSetAttribute((const void*)k_po_bigq, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(uint32_t) * kPoBigMaxDW));
       return true;
     }();
     (void)battr;
     hipLaunchKernelGGL(k_po_bigq, dim3((unsigned)h->po_nclasses, (unsigned)bigq.size()), dim3(kPoBigThreads),
-                       sizeof(uint32_t) * (size_t)h->po_class_maxdw, h->stream, b, h->hp);
+                       sizeof(uint32_t) * (size_t)std::min<int64_t>(h->po_class_maxdw, kPoBigMaxDW), h->stream, b,
+                       h->hp);
     CMS_HIP(hipGetLastError());
   }
   if (h->po_nnarrow > 0) {
     TimedScope ts(h, "po_group_pairs");
     static bool attr = [] {
-      (void)hipFuncSetAttribute((const void*)k_po_group_pairs, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)k_po_group_pairs, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)po_group_lds(kPoGroupHistW));
       return true;
     }();
     (void)attr;
-    const dim3 grid((unsigned)((qc + kPoQueryChunk - 1) / kPoQueryChunk), (unsigned)h->po_nnarrow);
-    hipLaunchKernelGGL(k_po_group_pairs, grid, dim3(64 * kPoGroupWaves), (size_t)h->po_gmax_lds, h->stream, a, h->hp);
+    a.classes = h->po_classes.as<PoGroup>();
+    a.toff = reinterpret_cast<const int64_t*>(h->po_classes.as<char>() + sizeof(PoGroup) * h->po_nclasses);
+    a.skT = h->po_skT.as<uint32_t>();
+    a.ngroups = h->po_nnarrow;
+    a.nchunks = (qc + kPoQueryChunk - 1) / kPoQueryChunk;
+    a.per_xcd = (a.ngroups * a.nchunks + 7) / 8;
+    a.hist_w = h->po_hist_w;
+    hipLaunchKernelGGL(k_po_group_pairs, dim3((unsigned)(8 * a.per_xcd)), dim3(64 * kPoGroupWaves),
+                       (size_t)h->po_gmax_lds, h->stream, a, h->hp);
     CMS_HIP(hipGetLastError());
   }
   const int64_t nwide = h->po_ngroups - h->po_nnarrow;
@@ -1032,12 +1217,69 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     p.out = slab;
     p.ldo = n;
     p.weighted = a.weighted;
-    p.big_skip = a.big_skip;
-    p.big_dw = bigq.empty() ? 0 : kPoBigMaxDW;
-    TimedScope ts(h, "po_pair_cosine");
-    hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(qc * nwide, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
-                       h->stream, p, h->hp);
-    CMS_HIP(hipGetLastError());
+    int64_t npairs = qc * nwide;
+    if (prune_k > 0 && !h->tune.po_no_prune) {
+      // the narrow candidates' top k of every query (wide columns NaN), then
+      // the row-0 bound against its k-th score; survivors listed
+      const int32_t k = prune_k;
+      const size_t ids_b = sizeof(int64_t) * (size_t)(qc * k), sc_b = sizeof(double) * (size_t)(qc * k);
+      CMS_HIP(h->ws_pothr.ensure(ids_b + sc_b + sizeof(int32_t) * (size_t)qc));
+      int64_t* tids = h->ws_pothr.as<int64_t>();
+      double* tsc = reinterpret_cast<double*>(h->ws_pothr.as<char>() + ids_b);
+      int32_t* tcnt = reinterpret_cast<int32_t*>(h->ws_pothr.as<char>() + ids_b + sc_b);
+      CMS_HIP(h->ws_posurv.ensure(sizeof(unsigned long long) * (size_t)npairs + 16));
+      unsigned long long* surv = h->ws_posurv.as<unsigned long long>();
+      uint32_t* surv_cnt = reinterpret_cast<uint32_t*>(surv + npairs);
+      CMS_HIP(hipMemsetAsync(surv_cnt, 0, sizeof(uint32_t), h->stream));
+      hipLaunchKernelGGL(k_po_nanfill, dim3((unsigned)qc), dim3(256), 0, h->stream, slab, n, h->po_wrows.as<int64_t>(),
+                         nwide);
+      CMS_HIP(hipGetLastError());
+      std::vector<TopQuery> tq(qc);
+      for (int64_t q = 0; q < qc; ++q) tq[q] = TopQuery{q, q0 + q, q};
+      if (int rc = launch_top_k(h, slab, tq, k, nullptr, tids, tsc, tcnt)) return rc;
+      PoBoundArgs b{};
+      b.off = a.off;
+      b.inc = a.inc;
+      b.s0 = h->po_s0.as<uint64_t>();
+      b.shp = a.shp;
+      b.sk = a.sk;
+      b.norm = a.norm;
+      b.nsq = a.nsq;
+      b.wrows = h->po_wrows.as<int64_t>();
+      b.nwide = nwide;
+      b.tsc = tsc;
+      b.tcnt = tcnt;
+      b.k = k;
+      b.q0 = q0;
+      b.qc = qc;
+      b.n = n;
+      b.slab = slab;
+      b.surv = surv;
+      b.surv_cnt = surv_cnt;
+      b.weighted = a.weighted;
+      {
+        TimedScope ts(h, "po_wide_bound");
+        hipLaunchKernelGGL(k_po_wide_bound, dim3((unsigned)((nwide + 63) / 64), (unsigned)((qc + kPoBoundWaves - 1) / kPoBoundWaves)),
+                           dim3(64 * kPoBoundWaves), 0, h->stream, b);
+        CMS_HIP(hipGetLastError());
+      }
+      uint32_t ns = 0;
+      CMS_HIP(hipMemcpyAsync(&ns, surv_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+      CMS_HIP(hipStreamSynchronize(h->stream));
+      h->po_wide_pairs += npairs;
+      h->po_wide_exact += ns;
+      npairs = ns;
+      p.plist = surv;
+      p.q0 = q0;
+      p.nq = ns;
+      p.m = 1;
+    }
+    if (npairs > 0) {
+      TimedScope ts(h, "po_pair_cosine");
+      hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(npairs, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
+                         h->stream, p, h->hp);
+      CMS_HIP(hipGetLastError());
+    }
   }
   uint32_t nredo = 0;
   CMS_HIP(hipMemcpyAsync(&nredo, a.redo_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
@@ -1087,7 +1329,8 @@ int po_top_k_rows(cms_handle* h, int64_t row_begin, int64_t row_count, int32_t k
     CMS_HIP(hipMemcpyAsync(h->ws_query.ptr, qrows.data(), sizeof(int64_t) * rcnt, hipMemcpyHostToDevice, h->stream));
     if (h->f64) {
       if ((rc = po_pair_cosines(h, h->ws_query.as<int64_t>(), rcnt, nullptr, n, h->ws_slab.as<double>()))) return rc;
-    } else if ((rc = po_allpairs_slab(h, row_begin + r0, rcnt, h->ws_query.as<int64_t>(), h->ws_slab.as<double>()))) {
+    } else if ((rc = po_allpairs_slab(h, row_begin + r0, rcnt, h->ws_query.as<int64_t>(), h->ws_slab.as<double>(),
+                                      k))) {
       return rc;
     }
     if ((rc = launch_top_k(h, h->ws_slab.as<double>(), qs, k, nullptr, d_ids, d_scores, d_counts))) return rc;

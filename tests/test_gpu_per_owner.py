@@ -255,7 +255,8 @@ def test_big_queries_and_full_classes(oracle):
     shape class, dense dots against the transposed member image) and classes
     of more than 64 members (several 64-member groups, the dense and the
     sparse dot path): the all-pairs top-k equals the per-pair kernel's rows,
-    a handle without the big-query kernel (CMS_PO_NO_BIGQ=1), and the
+    a handle without the big-query kernel (CMS_PO_NO_BIGQ=1), a handle
+    without the wide owners' row-0 bound (CMS_PO_NO_PRUNE=1), and the
     oracle's TopItems loop on sampled big and small rows."""
     import os
     from mahout_amd.synth import zipf_stream
@@ -278,6 +279,8 @@ def test_big_queries_and_full_classes(oracle):
                 lists = t.top_k_all(k)
                 big = np.flatnonzero(nnz > 4096)[:3].tolist()
                 rows = {q: t.similarities(int(uid[q]), uid) for q in big + [0, n // 2, n - 1]}
+                st = t.stats()
+                run.pruned = (st["po_wide_pairs"], st["po_wide_exact"])
                 return shapes, lists, rows
         finally:
             for kk, v in old.items():
@@ -292,8 +295,14 @@ def test_big_queries_and_full_classes(oracle):
     for r in range(n):
         cls.setdefault((int(w[r]), int(d[r])), []).append(r)
     assert max(len(v) for v in cls.values()) > 64
+    wide_pairs, wide_exact = run.pruned
+    assert wide_pairs > 0 and wide_exact < wide_pairs  # the row-0 bound ruled wide pairs out
     _, (ids2, sc2, cnt2), _ = run({"CMS_PO_NO_BIGQ": "1"})
     assert np.array_equal(cnt, cnt2) and np.array_equal(ids, ids2) and same(sc, sc2)
+    # every (query, wide owner) pair computed exactly: the same lists
+    _, (ids3, sc3, cnt3), _ = run({"CMS_PO_NO_PRUNE": "1"})
+    assert run.pruned == (0, 0)
+    assert np.array_equal(cnt, cnt3) and np.array_equal(ids, ids3) and same(sc, sc3)
     for q, row in rows.items():
         row = row.copy()
         row[q] = np.nan
