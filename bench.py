@@ -157,7 +157,9 @@ def per_owner_scale(items, users, n, n_users, rows=1024, all_pairs_budget_s=120.
                                   "wide_pairs_exact_total": st["po_wide_exact"]}
         # the WHOLE all-pairs top-100 (every one of the n*(n-1) ordered pairs),
         # when the block rates predict it finishes within all_pairs_budget_s
-        rate = min(po["median_rows"]["ordered_pairs_per_s"], po["head_rows"]["ordered_pairs_per_s"])
+        # (zipf_stream_torch permutes the item IDs, so both blocks are random
+        # samples of the items: their pooled rate predicts the whole job)
+        rate = 2 * rows * n / (po["median_rows"]["s"] + po["head_rows"]["s"])
         po["all_pairs_predicted_s"] = n * n / rate
         if n * n / rate <= all_pairs_budget_s:
             torch.cuda.synchronize()

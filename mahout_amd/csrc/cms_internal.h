@@ -205,6 +205,8 @@ struct Tunables {
   int mid_u8_keys = 12288;  // CMS_MID_U8_KEYS: more keys start at u16
   int nib_persist = 0;      // CMS_NIB_PERSIST=1: k_build_nibbles as persistent waves (else one owner per wave)
   int mid_image = 0;        // CMS_MID_IMAGE=1: mid owners through the one-pass u16 image (k_build_image; slower on MI355X)
+  int po_dense_x4 = 4;      // CMS_PO_DENSE_X4: group kernel's dense dots when 4 w <= this x nnz(u1)
+  int po_bound_rows = 1;    // CMS_PO_BOUND_ROWS: sketch rows of the wide owners' upper bound (1 or 2)
   int po_no_prune = 0;      // CMS_PO_NO_PRUNE=1: every (query, wide owner) pair through k_po_pairs (no row-0 bound)
   int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
@@ -364,6 +366,7 @@ struct cms_handle {
   cms::DevBuf po_groups, po_cmem, po_redo;
   int64_t po_ngroups = 0, po_nnarrow = 0, po_wide0 = 0;  // groups, narrow groups, first wide member in po_cmem
   int32_t po_gmax_lds = 0;                       // LDS of a group workgroup (bytes)
+  int64_t po_nnarrow_part[3] = {};               // narrow groups of width <= 512, <= 1024, <= 2048 (in that order)
   int32_t po_hist_w = 1;                         // widest narrow class (the waves' LDS bucket rows)
   // the narrow classes whole (one PoGroup each, po_classes) with their
   // members' sketches transposed, [class][d * w][members] (po_skT): the
@@ -375,6 +378,7 @@ struct cms_handle {
   // (a_0 k + b_0) mod p (po_s0): k_po_wide_bound's operands; the top-k
   // threshold scratch and the surviving (query, wide owner) pairs
   cms::DevBuf po_wrows, po_s0, ws_pothr, ws_posurv;
+  int32_t po_s0_rows = 1;                        // sketch rows in po_s0 (the bound's rows)
   int64_t po_wide_pairs = 0, po_wide_exact = 0;  // (query, wide owner) pairs bounded / computed exactly
 
   // instrumentation

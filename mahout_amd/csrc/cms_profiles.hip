@@ -33,9 +33,11 @@
 namespace cms {
 
 constexpr int kPoThreads = 64;     // one wave per (u1, u2) pair
+constexpr int kPoBigThreadsPair = 256;  // listed pairs of a big u1: four waves per pair
 constexpr int kPoHist = 4096;      // LDS bucket row (u32); wider shapes use global scratch
 constexpr int kPoGrid = 8192;      // pair-kernel blocks with LDS rows
 constexpr int kPoGridWide = 1024;  // pair-kernel blocks when some width exceeds kPoHist
+constexpr int kPoGridList = 32768; // pair-kernel blocks for a listed batch that needs no global rows
 constexpr int kCfgThreads = 256;
 
 // ------------------------------------------------ CountMinSketchConfig --
@@ -193,6 +195,7 @@ struct PoPairArgs {
   // list mode: the pairs (u1 << 32) | u2 of plist[0, nq) into slab row u1 - q0
   const unsigned long long* plist = nullptr;
   int64_t q0 = 0;
+  uint32_t* no_rows = nullptr;  // pairs that needed a global bucket row without scratch (a host error)
 };
 
 __device__ __forceinline__ uint64_t po_wave_sum(uint64_t v) {
@@ -213,9 +216,28 @@ __device__ __forceinline__ uint32_t po_tab_insert(uint32_t* lds, uint32_t j) {
   }
 }
 
-// userSimilarity(u1 = qrows[t / m], u2 = crows[t % m]): one wave per pair.
-__global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParams hp) {
+// Sum over the NT threads of a block (every thread gets it).
+template <int NT>
+__device__ __forceinline__ uint64_t po_block_sum(uint64_t v, unsigned long long* red) {
+  v = po_wave_sum(v);
+  if (NT == 64) return v;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t = sat_add(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+// userSimilarity(u1 = qrows[t / m], u2 = crows[t % m]): one block of NT
+// threads per pair (one wave; four for listed pairs whose u1 has more than
+// kPoBigQuery preferences).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_po_pairs(PoPairArgs a, HashParams hp) {
+  constexpr int kPoThreads = NT;  // (the body's stride)
   __shared__ uint32_t lds[kPoHist];
+  __shared__ unsigned long long red[NT / 64];
   const int lane = threadIdx.x;
   for (int j = lane; j < kPoHist; j += kPoThreads) lds[j] = 0u;
   __syncthreads();
@@ -262,10 +284,14 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
     // u1 with at most 4 preferences per lane: keys, increments and each
     // row's buckets stay in registers (one load per pair, one hash per key
     // and row; the exchange pass reuses the buckets)
-    const bool cached = k1 - k0 <= 4 * kPoThreads;
+    const bool cached = NT == 64 && k1 - k0 <= 4 * kPoThreads;
     // a cached u1 against a width past the LDS row: its (at most 256) buckets
     // go into an LDS hash table instead of a global bucket row
     const bool tab = cached && w > (uint32_t)kPoHist;
+    if (hist == nullptr && !tab) {  // (uniform) a launch without scratch got a pair that needs it
+      if (lane == 0) atomicAdd(a.no_rows, 1u);
+      continue;
+    }
     uint64_t ck[4];
     uint32_t cv[4], cj[4];
     if (cached) {
@@ -317,14 +343,18 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
         add_pass(d, &ab, brow);
         a2p = clear_pass(d);
       }
-      const uint64_t a2 = po_wave_sum(a2p);
-      ab = po_wave_sum(ab);
+      const uint64_t a2 = po_block_sum<NT>(a2p, red);
+      ab = po_block_sum<NT>(ab, red);
       const uint64_t b2 = a.norm[s.roff + d];
       double valueAB, den;
       if (a2 < (1ULL << 53) && b2 < (1ULL << 53)) {
         valueAB = (double)ab;  // ab <= sqrt(a2 * b2) < 2^53: exact
         den = __dmul_rn(__dsqrt_rn((double)a2), a.nsq[s.roff + d]);
       } else {  // the reference's sequential fp64 loop (:128-134) over the rebuilt row, every lane alike
+        if (hist == nullptr) {  // (uniform) as above
+          if (lane == 0) atomicAdd(a.no_rows, 1u);
+          break;
+        }
         add_pass(d, nullptr, brow);
         double A = 0.0, B = 0.0, AB = 0.0;
         for (uint32_t j = 0; j < w; ++j) {
@@ -361,7 +391,7 @@ __global__ __launch_bounds__(kPoThreads) void k_po_pairs(PoPairArgs a, HashParam
 // wave's bucket row.  Per sketch row, u1's preferences are hashed ONCE into
 // the wave's bucket row -- u1's sketch row at the class shape -- and then,
 // whichever is less work:
-//   dense (w <= 4 nnz(u1)): lane m forms valueAB = sum_j U1[j] * S_m[j] over
+//   dense (w <= nnz(u1); CMS_PO_DENSE_X4 / 4 x nnz): lane m forms valueAB = sum_j U1[j] * S_m[j] over
 //     the w buckets (U1[j] a broadcast LDS read), valueA from one sweep over
 //     the row, which also zeroes it;
 //   sparse: 64 preferences at a time are parked as (bucket, increment) and
@@ -375,6 +405,9 @@ constexpr int kPoGroupMax = 64;            // members per narrow group: one lane
 constexpr int kPoGroupHistW = 2048;        // narrow classes: one LDS bucket row per wave
 constexpr int kPoGroupWaves = 8;
 constexpr int64_t kPoQueryChunk = 64;      // query rows per workgroup
+constexpr int kPoSmallHist = 512;          // narrow groups launched by width: rows of 512, 1024, 2048 counters
+constexpr int kPoHistParts = 3;            // (less LDS per workgroup for the narrower ones: more of them per CU)
+__host__ __device__ constexpr int po_hist_part(int w) { return w <= kPoSmallHist ? 0 : w <= 2 * kPoSmallHist ? 1 : 2; }
 
 struct PoAllArgs {
   const int64_t* off;
@@ -389,8 +422,9 @@ struct PoAllArgs {
   const int64_t* toff;     // [nclasses] class offsets in skT
   const uint32_t* skT;
   const int64_t* cmem;
-  int64_t ngroups, nchunks, per_xcd;
+  int64_t g0, ngroups, nchunks, per_xcd;  // groups [g0, g0 + ngroups) of this launch
   int32_t hist_w;          // LDS bucket row stride per wave
+  int32_t dense_x4;        // dense dots when 4 w <= dense_x4 nnz(u1)
   int64_t q0, qc, n;
   double* slab;  // [qc][n], column = candidate row
   unsigned long long* redo;  // (u1 << 32) | u2 of pairs past the exact regime
@@ -414,7 +448,7 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
   // group's member image stays in that XCD's L2
   const int64_t c = (int64_t)(blockIdx.x & 7) * a.per_xcd + (blockIdx.x >> 3);
   if (c >= a.ngroups * a.nchunks) return;
-  const PoGroup g = a.groups[c / a.nchunks];
+  const PoGroup g = a.groups[a.g0 + c / a.nchunks];
   const int64_t chunk = c % a.nchunks;
   const PoGroup cl = a.classes[g.pad];
   const int w = g.w, d = g.d, cnt = g.cnt;
@@ -434,7 +468,7 @@ __global__ __launch_bounds__(64 * kPoGroupWaves) void k_po_group_pairs(PoAllArgs
     const int64_t u1 = a.q0 + q;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
     if (k1 - k0 > a.big_skip && w * d <= kPoBigMaxDW) continue;  // k_po_bigq builds this query once per class
-    const bool dense = (int64_t)w <= 4 * (k1 - k0);
+    const bool dense = 4 * (int64_t)w <= a.dense_x4 * (k1 - k0);
     double minc = DBL_MAX;  // lane m < cnt: member m's running Math.min
     bool inexact = false;
     for (int r = 0; r < d; ++r) {
@@ -632,7 +666,7 @@ __global__ __launch_bounds__(256) void k_po_transpose(const PoGroup* classes, co
 // them against 100K queries (2.1e11 key-rows).  mostSimilar only keeps the
 // top k, so each pair first gets a cheap UPPER bound from sketch row 0:
 //   userSimilarity = normalize(min over rows r with den != 0 of AB_r / den_r)
-//                 <= normalize(AB_0 / (sqrt(sum v^2) * sqrt(B_0)))
+//                 <= normalize(AB_0 / (sqrt(valueA_0 lower bound) * sqrt(B_0)))
 // (valueA_0 = sum_j U1_0[j]^2 >= max(sum_k v_k^2, (sum_k v_k)^2 / w2) because
 // the increments are non-negative; every fp64 step is correctly rounded and monotone, and
 // normalize is non-decreasing).  A pair whose bound is below the query's
@@ -640,16 +674,20 @@ __global__ __launch_bounds__(256) void k_po_transpose(const PoGroup* classes, co
 // not enter the list and is written NaN, which TopItems skips; every other
 // pair is listed for k_po_pairs' exact computation.  The bound applies only
 // while the exact regime holds (sum v < 2^26 so every valueA < 2^53, and
-// B_0 < 2^53): row 0's value is then the same exact expression with the true
-// valueA_0.  The row-0 residues (a_0 k + b_0) mod p are precomputed per
-// preference (po_s0), so a key costs a Barrett reduction by u2's width and
-// one gather.  Lane = wide owner (sorted by width), wave = query: the keys
-// are wave-uniform (scalar loads), no reductions.
+// B_r < 2^53): row r's value is then the same exact expression with the true
+// valueA_r.  With h->tune.po_bound_rows = 2 (CMS_PO_BOUND_ROWS) the bound is
+// the smaller of rows 0 and 1.  The residues (a_r k + b_r) mod p of those
+// rows are precomputed per preference (po_s0), so a key costs a Barrett
+// reduction by u2's width and one gather per row.  Lane = wide owner (sorted
+// by width), wave = query: the keys are wave-uniform (scalar loads), no
+// reductions.
 constexpr int kPoBoundWaves = 4;
+constexpr int kPoBoundMaxRows = 2;
 struct PoBoundArgs {
   const int64_t* off;
   const uint32_t* inc;
-  const uint64_t* s0;
+  const uint64_t* s0;    // [rows][np] residues (a_r k + b_r) mod p of every preference
+  int64_t np;
   const PoShape* shp;
   const uint32_t* sk;
   const uint64_t* norm;
@@ -661,8 +699,11 @@ struct PoBoundArgs {
   int32_t k;
   int64_t q0, qc, n;
   double* slab;
-  unsigned long long* surv;  // surviving pairs (u1 << 32) | u2
-  uint32_t* surv_cnt;
+  // surviving pairs (u1 << 32) | u2: list 0 for k_po_pairs' LDS paths, list 1
+  // for pairs that need its global bucket rows (w > kPoHist, nnz(u1) > 256),
+  // list 2 for a u1 of more than kPoBigQuery preferences (four waves a pair)
+  unsigned long long* surv[3];
+  uint32_t* surv_cnt;    // [3]
   int32_t weighted;
 };
 
@@ -677,9 +718,11 @@ __device__ __forceinline__ uint32_t po_mod_w(uint64_t s, uint32_t w, uint64_t ba
   return rem;
 }
 
-__global__ __launch_bounds__(256) void k_po_s0(const uint64_t* kp, int64_t np, HashParams hp, uint64_t* s0) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x)
-    s0[i] = residue_wbq(hp, 0, kp[i]);
+__global__ __launch_bounds__(256) void k_po_s0(const uint64_t* kp, int64_t np, int rows, HashParams hp, uint64_t* s0) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = kp[i];
+    for (int r = 0; r < rows; ++r) s0[r * np + i] = residue_wbq(hp, r, k);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_po_nanfill(double* slab, int64_t n, const int64_t* wrows, int64_t nwide) {
@@ -687,6 +730,19 @@ __global__ __launch_bounds__(256) void k_po_nanfill(double* slab, int64_t n, con
   for (int64_t m = threadIdx.x; m < nwide; m += blockDim.x) row[wrows[m]] = __builtin_nan("");
 }
 
+// wave-aggregated append of this lane's pair to list l when `keep`
+__device__ __forceinline__ void po_append(const PoBoundArgs& a, int l, bool keep, unsigned long long e) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t mask = __ballot(keep);
+  if (mask == 0) return;
+  const int first = __builtin_ctzll(mask);
+  uint32_t base = 0;
+  if (lane == first) base = atomicAdd(&a.surv_cnt[l], (uint32_t)__builtin_popcountll(mask));
+  base = __shfl(base, first, 64);
+  if (keep) a.surv[l][base + (uint32_t)__builtin_popcountll(mask & ((1ULL << lane) - 1ULL))] = e;
+}
+
+template <int R>
 __global__ __launch_bounds__(64 * kPoBoundWaves) void k_po_wide_bound(PoBoundArgs a) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -696,61 +752,78 @@ __global__ __launch_bounds__(64 * kPoBoundWaves) void k_po_wide_bound(PoBoundArg
   const bool live = m < a.nwide;
   const int64_t u2 = a.wrows[live ? m : 0];
   const PoShape s = a.shp[u2];
-  const uint32_t* row0 = a.sk + s.soff;
   const uint32_t w = (uint32_t)s.w;
+  // rows past u2's depth read row 0 (in bounds; left out of the bound below)
+  const uint32_t* rowp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) rowp[r] = a.sk + s.soff + (int64_t)(r < s.d ? r : 0) * w;
   const int64_t u1 = a.q0 + q;
   const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
-  uint64_t ab = 0, a2 = 0, as = 0;
-  int64_t i = k0;
-  for (; i + 8 <= k1; i += 8) {  // the keys' scalar loads together, then eight gathers in flight
-    uint64_t sv[8];
-    uint32_t v[8], c[8];
+  uint64_t ab[R], a2 = 0, as = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      sv[u] = a.s0[i + u];
+  for (int r = 0; r < R; ++r) ab[r] = 0;
+  int64_t i = k0;
+  constexpr int U = 8 / R;
+  for (; i + U <= k1; i += U) {  // the keys' scalar loads together, then the gathers in flight
+    uint64_t sv[R][U];
+    uint32_t v[U], c[R][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
       v[u] = a.inc[i + u];
+#pragma unroll
+      for (int r = 0; r < R; ++r) sv[r][u] = a.s0[r * a.np + i + u];
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) c[u] = row0[po_mod_w(sv[u], w, s.barrett)];
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      ab += (uint64_t)v[u] * c[u];
+      for (int u = 0; u < U; ++u) c[r][u] = rowp[r][po_mod_w(sv[r][u], w, s.barrett)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) ab[r] += (uint64_t)v[u] * c[r][u];
       a2 += (uint64_t)v[u] * v[u];
       as += v[u];
     }
   }
   for (; i < k1; ++i) {
     const uint32_t v = a.inc[i];
-    ab += (uint64_t)v * row0[po_mod_w(a.s0[i], w, s.barrett)];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ab[r] += (uint64_t)v * rowp[r][po_mod_w(a.s0[r * a.np + i], w, s.barrett)];
     a2 += (uint64_t)v * v;
     as += v;
   }
   // (sums wrap only past sum v >= 2^26, where no pair is pruned)
   bool prune = false;
-  const int32_t tc = a.tcnt[q];
-  if (live && tc >= a.k && as < (1ULL << 26) && a2 != 0 && a.norm[s.roff] < (1ULL << 53)) {
-    const double sb = a.nsq[s.roff];
-    // valueA_0 >= (sum_j U1_0[j])^2 / w as well (Cauchy-Schwarz over the w
+  if (live && a.tcnt[q] >= a.k && as < (1ULL << 26) && a2 != 0) {
+    // valueA_r >= (sum_j U1_r[j])^2 / w as well (Cauchy-Schwarz over the w
     // buckets): the tighter of the two when u1 has many more preferences than
     // u2 has buckets
     const uint64_t spread = (as * as + w - 1) / w;
     if (spread > a2) a2 = spread;
-    if (sb != 0.0) {
-      const double ub = normalize_weight(__ddiv_rn((double)ab, __dmul_rn(__dsqrt_rn((double)a2), sb)), a.weighted);
-      prune = ub < a.tsc[q * a.k + a.k - 1];
+    const double sa = __dsqrt_rn((double)a2);
+    double ub = DBL_MAX;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r >= s.d) break;  // (that row's sums hashed row r against row 0's counters: no bound)
+      const double sb = a.nsq[s.roff + r];
+      if (a.norm[s.roff + r] < (1ULL << 53) && sb != 0.0) ub = java_min(ub, __ddiv_rn((double)ab[r], __dmul_rn(sa, sb)));
     }
+    if (ub != DBL_MAX) prune = normalize_weight(ub, a.weighted) < a.tsc[q * a.k + a.k - 1];
   }
   if (live && prune) a.slab[q * a.n + u2] = __builtin_nan("");
   const bool keep = live && !prune;
-  const uint64_t mask = __ballot(keep);
-  if (mask == 0) return;
-  const int first = __builtin_ctzll(mask);
-  uint32_t base = 0;
-  if (lane == first) base = atomicAdd(a.surv_cnt, (uint32_t)__builtin_popcountll(mask));
-  base = __shfl(base, first, 64);
-  if (keep) {
-    const uint32_t rank = (uint32_t)__builtin_popcountll(mask & ((1ULL << lane) - 1ULL));
-    a.surv[base + rank] = ((unsigned long long)u1 << 32) | (unsigned long long)u2;
+  // k_po_pairs needs a global bucket row for u1 past its register cache, or
+  // for the sequential replay of a pair past the exact regime
+  bool norms_ok = as < (1ULL << 26);
+  for (int r = 0; r < s.d && norms_ok; ++r) norms_ok = a.norm[s.roff + r] < (1ULL << 53);
+  const bool global_rows = w > (uint32_t)kPoHist && (k1 - k0 > 4 * kPoThreads || !norms_ok);
+  const unsigned long long e = ((unsigned long long)u1 << 32) | (unsigned long long)u2;
+  const bool big = k1 - k0 > kPoBigQuery;  // (wave-uniform)
+  if (big) {
+    po_append(a, 2, keep, e);
+  } else {
+    po_append(a, 0, keep && !global_rows, e);
+    po_append(a, 1, keep && global_rows, e);
   }
 }
 
@@ -953,6 +1026,13 @@ static int po_build_groups(cms_handle* h) {
     }
     i = e;
   }
+  // narrow groups by width part (each part's launch takes only the LDS its
+  // widest row needs, so more workgroups share a CU); class order kept within
+  std::stable_sort(narrow.begin(), narrow.end(), [](const PoGroup& x, const PoGroup& y) {
+    return po_hist_part(x.w) < po_hist_part(y.w);
+  });
+  int64_t nsmall[kPoHistParts] = {};
+  for (const PoGroup& g : narrow) ++nsmall[po_hist_part(g.w)];
   std::vector<PoGroup> groups(narrow);
   std::vector<int64_t> cmem(cmem_n);
   cmem.insert(cmem.end(), cmem_w.begin(), cmem_w.end());
@@ -1004,6 +1084,7 @@ static int po_build_groups(cms_handle* h) {
   h->po_nnarrow = (int64_t)narrow.size();
   h->po_wide0 = (int64_t)cmem_n.size();
   h->po_hist_w = hist_w;
+  for (int i = 0; i < kPoHistParts; ++i) h->po_nnarrow_part[i] = nsmall[i];
   h->po_gmax_lds = (int32_t)po_group_lds(hist_w);
   return CMS_OK;
 }
@@ -1043,10 +1124,11 @@ int po_finalize(cms_handle* h) {
       CMS_HIP(hipMemsetAsync(h->po_scratch.ptr, 0, h->po_scratch.bytes, h->stream));
     }
   }
-  CMS_HIP(h->po_s0.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(h->po_npairs, 1)));
+  h->po_s0_rows = std::max(1, std::min(std::min(h->tune.po_bound_rows, kPoBoundMaxRows), (int)h->hp.depth));
+  CMS_HIP(h->po_s0.ensure(sizeof(uint64_t) * (size_t)h->po_s0_rows * (size_t)std::max<int64_t>(h->po_npairs, 1)));
   if (h->po_npairs > 0) {
     hipLaunchKernelGGL(k_po_s0, dim3(grid_for((h->po_npairs + 255) / 256, 16384)), dim3(256), 0, h->stream,
-                       h->po_kp.as<uint64_t>(), h->po_npairs, h->hp, h->po_s0.as<uint64_t>());
+                       h->po_kp.as<uint64_t>(), h->po_npairs, h->po_s0_rows, h->hp, h->po_s0.as<uint64_t>());
     CMS_HIP(hipGetLastError());
   }
   if (int rc = po_build_groups(h)) return rc;
@@ -1077,7 +1159,7 @@ int po_pair_cosines(cms_handle* h, const int64_t* d_qrows, int64_t nq, const int
   a.ldo = 0;
   a.weighted = h->p.weighting == CMS_WEIGHTED;
   TimedScope ts(h, "po_pair_cosine", s == nullptr);
-  hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(nq * m, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
+  hipLaunchKernelGGL(k_po_pairs<kPoThreads>, dim3(grid_for(nq * m, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
                      s ? s : h->stream, a, h->hp);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
@@ -1189,13 +1271,20 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     a.classes = h->po_classes.as<PoGroup>();
     a.toff = reinterpret_cast<const int64_t*>(h->po_classes.as<char>() + sizeof(PoGroup) * h->po_nclasses);
     a.skT = h->po_skT.as<uint32_t>();
-    a.ngroups = h->po_nnarrow;
     a.nchunks = (qc + kPoQueryChunk - 1) / kPoQueryChunk;
-    a.per_xcd = (a.ngroups * a.nchunks + 7) / 8;
-    a.hist_w = h->po_hist_w;
-    hipLaunchKernelGGL(k_po_group_pairs, dim3((unsigned)(8 * a.per_xcd)), dim3(64 * kPoGroupWaves),
-                       (size_t)h->po_gmax_lds, h->stream, a, h->hp);
-    CMS_HIP(hipGetLastError());
+    a.dense_x4 = h->tune.po_dense_x4;
+    int64_t g0 = 0;
+    for (int pi = 0; pi < kPoHistParts; ++pi) {
+      a.g0 = g0;
+      a.ngroups = h->po_nnarrow_part[pi];
+      g0 += a.ngroups;
+      if (a.ngroups <= 0) continue;
+      a.per_xcd = (a.ngroups * a.nchunks + 7) / 8;
+      a.hist_w = std::min<int32_t>(kPoSmallHist << pi, h->po_hist_w);
+      hipLaunchKernelGGL(k_po_group_pairs, dim3((unsigned)(8 * a.per_xcd)), dim3(64 * kPoGroupWaves),
+                         po_group_lds(a.hist_w), h->stream, a, h->hp);
+      CMS_HIP(hipGetLastError());
+    }
   }
   const int64_t nwide = h->po_ngroups - h->po_nnarrow;
   if (nwide > 0) {  // wide candidates: one wave per pair, columns scattered into the slab
@@ -1217,7 +1306,7 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     p.out = slab;
     p.ldo = n;
     p.weighted = a.weighted;
-    int64_t npairs = qc * nwide;
+    const int64_t npairs = qc * nwide;
     if (prune_k > 0 && !h->tune.po_no_prune) {
       // the narrow candidates' top k of every query (wide columns NaN), then
       // the row-0 bound against its k-th score; survivors listed
@@ -1227,10 +1316,10 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       int64_t* tids = h->ws_pothr.as<int64_t>();
       double* tsc = reinterpret_cast<double*>(h->ws_pothr.as<char>() + ids_b);
       int32_t* tcnt = reinterpret_cast<int32_t*>(h->ws_pothr.as<char>() + ids_b + sc_b);
-      CMS_HIP(h->ws_posurv.ensure(sizeof(unsigned long long) * (size_t)npairs + 16));
+      CMS_HIP(h->ws_posurv.ensure(sizeof(unsigned long long) * 3 * (size_t)npairs + 16));
       unsigned long long* surv = h->ws_posurv.as<unsigned long long>();
-      uint32_t* surv_cnt = reinterpret_cast<uint32_t*>(surv + npairs);
-      CMS_HIP(hipMemsetAsync(surv_cnt, 0, sizeof(uint32_t), h->stream));
+      uint32_t* surv_cnt = reinterpret_cast<uint32_t*>(surv + 3 * npairs);  // [0..2] the lists; [3] no_rows
+      CMS_HIP(hipMemsetAsync(surv_cnt, 0, 4 * sizeof(uint32_t), h->stream));
       hipLaunchKernelGGL(k_po_nanfill, dim3((unsigned)qc), dim3(256), 0, h->stream, slab, n, h->po_wrows.as<int64_t>(),
                          nwide);
       CMS_HIP(hipGetLastError());
@@ -1241,6 +1330,7 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       b.off = a.off;
       b.inc = a.inc;
       b.s0 = h->po_s0.as<uint64_t>();
+      b.np = h->po_npairs;
       b.shp = a.shp;
       b.sk = a.sk;
       b.norm = a.norm;
@@ -1254,29 +1344,62 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       b.qc = qc;
       b.n = n;
       b.slab = slab;
-      b.surv = surv;
+      b.surv[0] = surv;
+      b.surv[1] = surv + npairs;
+      b.surv[2] = surv + 2 * npairs;
       b.surv_cnt = surv_cnt;
       b.weighted = a.weighted;
       {
         TimedScope ts(h, "po_wide_bound");
-        hipLaunchKernelGGL(k_po_wide_bound, dim3((unsigned)((nwide + 63) / 64), (unsigned)((qc + kPoBoundWaves - 1) / kPoBoundWaves)),
-                           dim3(64 * kPoBoundWaves), 0, h->stream, b);
+        const dim3 grid((unsigned)((nwide + 63) / 64), (unsigned)((qc + kPoBoundWaves - 1) / kPoBoundWaves));
+        if (h->po_s0_rows >= 2)
+          hipLaunchKernelGGL(k_po_wide_bound<2>, grid, dim3(64 * kPoBoundWaves), 0, h->stream, b);
+        else
+          hipLaunchKernelGGL(k_po_wide_bound<1>, grid, dim3(64 * kPoBoundWaves), 0, h->stream, b);
         CMS_HIP(hipGetLastError());
       }
-      uint32_t ns = 0;
-      CMS_HIP(hipMemcpyAsync(&ns, surv_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+      uint32_t ns[3] = {0, 0, 0};
+      CMS_HIP(hipMemcpyAsync(ns, surv_cnt, sizeof ns, hipMemcpyDeviceToHost, h->stream));
       CMS_HIP(hipStreamSynchronize(h->stream));
       h->po_wide_pairs += npairs;
-      h->po_wide_exact += ns;
-      npairs = ns;
-      p.plist = surv;
+      h->po_wide_exact += ns[0] + ns[1] + ns[2];
       p.q0 = q0;
-      p.nq = ns;
       p.m = 1;
-    }
-    if (npairs > 0) {
+      p.no_rows = surv_cnt + 3;
       TimedScope ts(h, "po_pair_cosine");
-      hipLaunchKernelGGL(k_po_pairs, dim3(grid_for(npairs, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
+      if (ns[0] > 0) {  // LDS bucket rows or tables only: a full grid of one-wave blocks
+        p.plist = surv;
+        p.nq = ns[0];
+        p.scratch = nullptr;
+        p.scratch_w = 0;
+        hipLaunchKernelGGL(k_po_pairs<kPoThreads>, dim3(grid_for(ns[0], kPoGridList)), dim3(kPoThreads), 0, h->stream, p, h->hp);
+        CMS_HIP(hipGetLastError());
+      }
+      if (ns[1] > 0) {  // global bucket rows: the scratch's blocks
+        p.plist = surv + npairs;
+        p.nq = ns[1];
+        p.scratch = wide ? h->po_scratch.as<uint32_t>() : nullptr;
+        p.scratch_w = wide ? h->po_max_w : 0;
+        hipLaunchKernelGGL(k_po_pairs<kPoThreads>, dim3(grid_for(ns[1], wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
+                           h->stream, p, h->hp);
+        CMS_HIP(hipGetLastError());
+      }
+      if (ns[2] > 0) {  // big u1: four waves per pair, the scratch's blocks
+        p.plist = surv + 2 * npairs;
+        p.nq = ns[2];
+        p.scratch = wide ? h->po_scratch.as<uint32_t>() : nullptr;
+        p.scratch_w = wide ? h->po_max_w : 0;
+        hipLaunchKernelGGL(k_po_pairs<kPoBigThreadsPair>, dim3(grid_for(ns[2], wide ? kPoGridWide : kPoGrid)),
+                           dim3(kPoBigThreadsPair), 0, h->stream, p, h->hp);
+        CMS_HIP(hipGetLastError());
+      }
+      uint32_t bad = 0;
+      CMS_HIP(hipMemcpyAsync(&bad, surv_cnt + 3, sizeof bad, hipMemcpyDeviceToHost, h->stream));
+      CMS_HIP(hipStreamSynchronize(h->stream));
+      if (bad) return set_error(CMS_E_STATE, "per-owner all-pairs: %u listed pairs needed a global bucket row", bad);
+    } else {
+      TimedScope ts(h, "po_pair_cosine");
+      hipLaunchKernelGGL(k_po_pairs<kPoThreads>, dim3(grid_for(npairs, wide ? kPoGridWide : kPoGrid)), dim3(kPoThreads), 0,
                          h->stream, p, h->hp);
       CMS_HIP(hipGetLastError());
     }
