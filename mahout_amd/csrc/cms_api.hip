@@ -345,6 +345,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.mid_image = num("CMS_MID_IMAGE", h->tune.mid_image);
     h->tune.po_no_prune = num("CMS_PO_NO_PRUNE", h->tune.po_no_prune);
     h->tune.po_bound_rows = num("CMS_PO_BOUND_ROWS", h->tune.po_bound_rows);
+    h->tune.po_bound_part2 = num("CMS_PO_BOUND_PART2", h->tune.po_bound_part2);
     h->tune.po_dense_x4 = num("CMS_PO_DENSE_X4", h->tune.po_dense_x4);
     h->tune.po_no_bigq = num("CMS_PO_NO_BIGQ", h->tune.po_no_bigq);
     h->tune.forms = !flag("CMS_NO_FORMS");

@@ -206,6 +206,7 @@ struct Tunables {
   int nib_persist = 0;      // CMS_NIB_PERSIST=1: k_build_nibbles as persistent waves (else one owner per wave)
   int mid_image = 0;        // CMS_MID_IMAGE=1: mid owners through the one-pass u16 image (k_build_image; slower on MI355X)
   int po_dense_x4 = 4;      // CMS_PO_DENSE_X4: group kernel's dense dots when 4 w <= this x nnz(u1)
+  int po_bound_part2 = 1;   // CMS_PO_BOUND_PART2=0: the widest narrow part through the group kernel, unbounded
   int po_bound_rows = 1;    // CMS_PO_BOUND_ROWS: sketch rows of the wide owners' upper bound (1 or 2)
   int po_no_prune = 0;      // CMS_PO_NO_PRUNE=1: every (query, wide owner) pair through k_po_pairs (no row-0 bound)
   int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)
@@ -378,6 +379,7 @@ struct cms_handle {
   // (a_0 k + b_0) mod p (po_s0): k_po_wide_bound's operands; the top-k
   // threshold scratch and the surviving (query, wide owner) pairs
   cms::DevBuf po_wrows, po_s0, ws_pothr, ws_posurv;
+  int64_t po_nbound = 0, po_nbound_narrow = 0;   // k_po_wide_bound's candidates (po_wrows), narrow ones among them
   int32_t po_s0_rows = 1;                        // sketch rows in po_s0 (the bound's rows)
   int64_t po_wide_pairs = 0, po_wide_exact = 0;  // (query, wide owner) pairs bounded / computed exactly
 

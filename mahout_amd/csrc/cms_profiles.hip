@@ -34,6 +34,7 @@ namespace cms {
 
 constexpr int kPoThreads = 64;     // one wave per (u1, u2) pair
 constexpr int kPoBigThreadsPair = 256;  // listed pairs of a big u1: four waves per pair
+constexpr int kPoBigRow = 16384;        // their LDS bucket row (64 KiB)
 constexpr int kPoHist = 4096;      // LDS bucket row (u32); wider shapes use global scratch
 constexpr int kPoGrid = 8192;      // pair-kernel blocks with LDS rows
 constexpr int kPoGridWide = 1024;  // pair-kernel blocks when some width exceeds kPoHist
@@ -236,10 +237,14 @@ __device__ __forceinline__ uint64_t po_block_sum(uint64_t v, unsigned long long*
 template <int NT>
 __global__ __launch_bounds__(NT) void k_po_pairs(PoPairArgs a, HashParams hp) {
   constexpr int kPoThreads = NT;  // (the body's stride)
-  __shared__ uint32_t lds[kPoHist];
+  // the four-wave blocks (a big u1) keep rows of up to kPoBigRow counters in
+  // LDS and take valueAB / valueA from one sweep over the row instead of a
+  // second hashing pass (u1's buckets outnumber or rival the row's width)
+  constexpr int kRow = NT > 64 ? kPoBigRow : kPoHist;
+  __shared__ uint32_t lds[kRow];
   __shared__ unsigned long long red[NT / 64];
   const int lane = threadIdx.x;
-  for (int j = lane; j < kPoHist; j += kPoThreads) lds[j] = 0u;
+  for (int j = lane; j < kRow; j += kPoThreads) lds[j] = 0u;
   __syncthreads();
   uint32_t* gsc = a.scratch ? a.scratch + (int64_t)blockIdx.x * a.scratch_w : nullptr;
   const int64_t total = a.plist ? a.nq : a.nq * a.m;
@@ -256,7 +261,8 @@ __global__ __launch_bounds__(NT) void k_po_pairs(PoPairArgs a, HashParams hp) {
     }
     const PoShape s = a.shp[u2];
     const uint32_t w = (uint32_t)s.w;
-    uint32_t* hist = (w <= (uint32_t)kPoHist) ? lds : gsc;
+    uint32_t* hist = (w <= (uint32_t)kRow) ? lds : gsc;
+    const bool sweep = NT > 64 && w <= (uint32_t)kRow;
     const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
     double minc = DBL_MAX;
     // u1's counters at u2's shape: pass 1 adds every preference into the
@@ -339,6 +345,19 @@ __global__ __launch_bounds__(NT) void k_po_pairs(PoPairArgs a, HashParams hp) {
             if (cv[u]) lds[sl[u]] = 0u;
           __syncthreads();
         }
+      } else if (sweep) {
+        for (int64_t i = k0 + lane; i < k1; i += kPoThreads)
+          atomicAdd(&hist[bucket_wbq(hp, d, a.kp[i], w, s.barrett)], a.inc[i]);
+        __syncthreads();
+        for (uint32_t j = lane; j < w; j += kPoThreads) {
+          const uint32_t c = hist[j];
+          if (c) {
+            ab = sat_add(ab, (uint64_t)c * brow[j]);
+            a2p = sat_add(a2p, (uint64_t)c * c);
+            hist[j] = 0u;
+          }
+        }
+        __syncthreads();
       } else {
         add_pass(d, &ab, brow);
         a2p = clear_pass(d);
@@ -692,8 +711,9 @@ struct PoBoundArgs {
   const uint32_t* sk;
   const uint64_t* norm;
   const double* nsq;
-  const int64_t* wrows;  // [nwide] wide owner rows
+  const int64_t* wrows;  // [nwide] bounded candidate rows (wide owners, the widest narrow part)
   int64_t nwide;
+  int64_t big_skip;      // k_po_bigq's queries (more preferences than this) skip narrow candidates
   const double* tsc;     // [qc][k] the narrow candidates' top-k scores
   const int32_t* tcnt;   // [qc] their list lengths
   int32_t k;
@@ -749,8 +769,7 @@ __global__ __launch_bounds__(64 * kPoBoundWaves) void k_po_wide_bound(PoBoundArg
   const int64_t q = (int64_t)blockIdx.y * kPoBoundWaves + wv;
   if (q >= a.qc) return;  // wave-uniform
   const int64_t m = (int64_t)blockIdx.x * 64 + lane;
-  const bool live = m < a.nwide;
-  const int64_t u2 = a.wrows[live ? m : 0];
+  const int64_t u2 = a.wrows[m < a.nwide ? m : 0];
   const PoShape s = a.shp[u2];
   const uint32_t w = (uint32_t)s.w;
   // rows past u2's depth read row 0 (in bounds; left out of the bound below)
@@ -759,6 +778,8 @@ __global__ __launch_bounds__(64 * kPoBoundWaves) void k_po_wide_bound(PoBoundArg
   for (int r = 0; r < R; ++r) rowp[r] = a.sk + s.soff + (int64_t)(r < s.d ? r : 0) * w;
   const int64_t u1 = a.q0 + q;
   const int64_t k0 = a.off[u1], k1 = a.off[u1 + 1];
+  // a narrow candidate of a big query is k_po_bigq's (exact already)
+  const bool live = m < a.nwide && !(k1 - k0 > a.big_skip && w <= (uint32_t)kPoGroupHistW && s.w * s.d <= kPoBigMaxDW);
   uint64_t ab[R], a2 = 0, as = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) ab[r] = 0;
@@ -1071,9 +1092,19 @@ static int po_build_groups(cms_handle* h) {
                        h->po_shape.as<PoShape>(), h->po_sk.as<uint32_t>(), h->po_skT.as<uint32_t>());
     CMS_HIP(hipGetLastError());
   }
-  // the wide owners by width for k_po_wide_bound (lanes of a wave alike)
+  // k_po_wide_bound's candidates by width (lanes of a wave alike): the wide
+  // owners, and the narrow ones of the widest part (their member images are
+  // the group kernel's costliest) unless h->tune.po_bound_part2 is off
   std::vector<int64_t> wrows(cmem_w);
+  h->po_nbound_narrow = 0;
+  if (h->tune.po_bound_part2)
+    for (const PoGroup& g : narrow)
+      if (po_hist_part(g.w) == kPoHistParts - 1) {
+        for (int q = 0; q < g.cnt; ++q) wrows.push_back(cmem_n[g.m0 + q]);
+        h->po_nbound_narrow += g.cnt;
+      }
   std::stable_sort(wrows.begin(), wrows.end(), [&](int64_t x, int64_t y) { return h->h_po_w[x] < h->h_po_w[y]; });
+  h->po_nbound = (int64_t)wrows.size();
   if (!wrows.empty()) {
     CMS_HIP(h->po_wrows.ensure(sizeof(int64_t) * wrows.size()));
     CMS_HIP(hipMemcpyAsync(h->po_wrows.ptr, wrows.data(), sizeof(int64_t) * wrows.size(), hipMemcpyHostToDevice,
@@ -1217,6 +1248,15 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
   a.redo_cnt = reinterpret_cast<uint32_t*>(a.redo + kRedoCap);
   a.redo_cap = kRedoCap;
   CMS_HIP(hipMemsetAsync(a.redo_cnt, 0, sizeof(uint32_t), h->stream));
+  const int64_t nwide = h->po_ngroups - h->po_nnarrow;
+  const bool prune = prune_k > 0 && !h->tune.po_no_prune && h->po_nbound > 0;
+  // pruning: the bounded candidates' columns start NaN (the narrow top k
+  // below is taken without them; k_po_bigq's big queries overwrite theirs)
+  if (prune) {
+    hipLaunchKernelGGL(k_po_nanfill, dim3((unsigned)qc), dim3(256), 0, h->stream, slab, n, h->po_wrows.as<int64_t>(),
+                       h->po_nbound);
+    CMS_HIP(hipGetLastError());
+  }
   // queries of more than kPoBigQuery preferences take the narrow classes
   // through k_po_bigq (u1 hashed once per class); the group kernel skips them
   std::vector<int64_t> bigq;
@@ -1274,7 +1314,9 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     a.nchunks = (qc + kPoQueryChunk - 1) / kPoQueryChunk;
     a.dense_x4 = h->tune.po_dense_x4;
     int64_t g0 = 0;
-    for (int pi = 0; pi < kPoHistParts; ++pi) {
+    // (pruning with the widest part bounded: that part is k_po_wide_bound's)
+    const int nparts = prune && h->po_nbound_narrow > 0 ? kPoHistParts - 1 : kPoHistParts;
+    for (int pi = 0; pi < nparts; ++pi) {
       a.g0 = g0;
       a.ngroups = h->po_nnarrow_part[pi];
       g0 += a.ngroups;
@@ -1286,8 +1328,7 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       CMS_HIP(hipGetLastError());
     }
   }
-  const int64_t nwide = h->po_ngroups - h->po_nnarrow;
-  if (nwide > 0) {  // wide candidates: one wave per pair, columns scattered into the slab
+  if (nwide > 0 || prune) {  // wide candidates: one wave per pair, columns scattered into the slab
     PoPairArgs p{};
     p.off = a.off;
     p.kp = a.kp;
@@ -1306,8 +1347,9 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
     p.out = slab;
     p.ldo = n;
     p.weighted = a.weighted;
-    const int64_t npairs = qc * nwide;
-    if (prune_k > 0 && !h->tune.po_no_prune) {
+    const int64_t nb = prune ? h->po_nbound : nwide;
+    const int64_t npairs = qc * nb;
+    if (prune) {
       // the narrow candidates' top k of every query (wide columns NaN), then
       // the row-0 bound against its k-th score; survivors listed
       const int32_t k = prune_k;
@@ -1320,9 +1362,6 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       unsigned long long* surv = h->ws_posurv.as<unsigned long long>();
       uint32_t* surv_cnt = reinterpret_cast<uint32_t*>(surv + 3 * npairs);  // [0..2] the lists; [3] no_rows
       CMS_HIP(hipMemsetAsync(surv_cnt, 0, 4 * sizeof(uint32_t), h->stream));
-      hipLaunchKernelGGL(k_po_nanfill, dim3((unsigned)qc), dim3(256), 0, h->stream, slab, n, h->po_wrows.as<int64_t>(),
-                         nwide);
-      CMS_HIP(hipGetLastError());
       std::vector<TopQuery> tq(qc);
       for (int64_t q = 0; q < qc; ++q) tq[q] = TopQuery{q, q0 + q, q};
       if (int rc = launch_top_k(h, slab, tq, k, nullptr, tids, tsc, tcnt)) return rc;
@@ -1336,7 +1375,8 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       b.norm = a.norm;
       b.nsq = a.nsq;
       b.wrows = h->po_wrows.as<int64_t>();
-      b.nwide = nwide;
+      b.nwide = nb;
+      b.big_skip = a.big_skip;
       b.tsc = tsc;
       b.tcnt = tcnt;
       b.k = k;
@@ -1351,7 +1391,7 @@ static int po_allpairs_slab(cms_handle* h, int64_t q0, int64_t qc, const int64_t
       b.weighted = a.weighted;
       {
         TimedScope ts(h, "po_wide_bound");
-        const dim3 grid((unsigned)((nwide + 63) / 64), (unsigned)((qc + kPoBoundWaves - 1) / kPoBoundWaves));
+        const dim3 grid((unsigned)((nb + 63) / 64), (unsigned)((qc + kPoBoundWaves - 1) / kPoBoundWaves));
         if (h->po_s0_rows >= 2)
           hipLaunchKernelGGL(k_po_wide_bound<2>, grid, dim3(64 * kPoBoundWaves), 0, h->stream, b);
         else
