@@ -126,9 +126,11 @@ def per_owner_scale(items, users, n, n_users, rows=1024, all_pairs_budget_s=120.
     config 1: the stream as the transposed DataModel (n items keyed by user),
     CountMinSketchConfig(q=1) shapes for every item (CountMinSketchConfig.java:
     120-158, on the GPU), then mostSimilar top-100 (userSimilarity(u1, u2)
-    hashes u1 at u2's shape, CosineCM.java:83-96) for a block of `rows`
-    query items at the median rank and one at the head, each over all n
-    candidates."""
+    hashes u1 at u2's shape, CosineCM.java:83-96) for two blocks of `rows`
+    query items (rows n/2.. and 0..; the stream permutes item IDs, so both are
+    random samples of the items), each over all n candidates, then the whole
+    all-pairs top-100 when the pooled block rate predicts it within
+    `all_pairs_budget_s`."""
     from mahout_amd import SketchTable
     off, ckeys = csr_on_device(items, users, n)
     po = {"workload": f"{int(items.numel())}-pair DataModel, {n} items x {n_users} users; CountMinSketchConfig(q=1) "
@@ -168,8 +170,12 @@ def per_owner_scale(items, users, n, n_users, rows=1024, all_pairs_budget_s=120.
             dt = time.perf_counter() - t0
             po["all_pairs"] = {"s": dt, "ordered_pairs": n * (n - 1), "ordered_pairs_per_s": n * (n - 1) / dt,
                                "full_lists": int((cnt == 100).sum()),
-                               "path": "candidates grouped by (w, d) class: k_po_group_pairs for classes whose "
-                                       "sketches share a workgroup's LDS, k_po_pairs for the wide owners"}
+                               "path": "narrow candidates grouped by (w, d) class (k_po_group_pairs; k_po_bigq for "
+                                       "queries of > 4096 preferences); wide owners and the widest narrow part "
+                                       "bounded by sketch row 0 against each query's narrow top-k "
+                                       "(k_po_wide_bound), the survivors exact (k_po_pairs)",
+                               "wide_pairs_bounded_total": t.stats()["po_wide_pairs"],
+                               "wide_pairs_exact_total": t.stats()["po_wide_exact"]}
     del off, ckeys
     return po
 
