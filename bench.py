@@ -433,8 +433,9 @@ def config1_recommender(nn=50, how_many=10, reps=5):
     84-95).  GPU: every user's neighbourhood in one cms_top_k_all, the
     candidates (the neighbours' items minus the user's own) from the
     incidence matrix, every candidate's estimate in one
-    cms_estimate_preferences_batch, the top 10 per user; timed end to end
-    (host glue included) over `reps` runs after a warm-up.  CPU beside it:
+    cms_estimate_preferences_batch, the top 10 per user (candidate sets and
+    the selection as device tensor ops); timed end to end (host glue
+    included) over `reps` runs after a warm-up.  CPU beside it:
     oracle/cms_baseline.c orc_recommend_par (prebuilt fp64 sketches, the same
     neighbourhood / candidates / estimates) on all the run's threads and on
     one.  The tie order among equal estimates follows FastIDSet in the
@@ -459,27 +460,37 @@ def config1_recommender(nn=50, how_many=10, reps=5):
         t.ingest(users, items, ratings)
         t.finalize()
 
+        dev = torch.device("cuda")
+        inc_d = torch.from_numpy(inc).to(dev)  # the model's incidence matrix, resident like the table
+
         def run():
             ids, _, cnt = t.top_k_all(nn)  # every user's neighbourhood (NearestNUserNeighborhood order)
             valid = np.arange(nn)[None, :] < cnt[:, None]
-            adj = np.zeros((nu, nu), np.float32)
-            rr = np.repeat(np.arange(nu), cnt)
-            adj[rr, np.searchsorted(uid, ids[valid])] = 1.0
-            cand = (adj @ inc > 0) & (inc == 0)  # getAllOtherItems
-            cu, ci = np.nonzero(cand)
-            it_off = np.zeros(nu + 1, np.int64)
-            np.cumsum(np.bincount(cu, minlength=nu), out=it_off[1:])
+            nb = ids[valid]
+            cnt_d = torch.from_numpy(cnt).to(dev)
+            adj = torch.zeros((nu, nu), device=dev)
+            rows_d = torch.repeat_interleave(torch.arange(nu, device=dev), cnt_d.long())
+            adj[rows_d, torch.from_numpy(np.searchsorted(uid, nb)).to(dev)] = 1.0
+            cand = ((adj @ inc_d) > 0) & (inc_d == 0)  # getAllOtherItems (counts <= nn: exact in fp32)
+            cu, ci = torch.nonzero(cand, as_tuple=True)  # row-major: each user's items ascending
+            it_off = torch.zeros(nu + 1, dtype=torch.int64, device=dev)
+            it_off[1:] = torch.cumsum(torch.bincount(cu, minlength=nu), 0)
             nb_off = np.zeros(nu + 1, np.int64)
             np.cumsum(cnt, out=nb_off[1:])
-            est = t.estimate_preferences_batch(uid, nb_off, ids[valid], it_off, iid[ci], cap)
-            # TopItems.getTopItems: the how_many best values per user (NaN out)
-            ok = ~np.isnan(est)
-            order = np.lexsort((ci[ok], -est[ok], cu[ok]))
-            u_ok, i_ok, e_ok = cu[ok][order], ci[ok][order], est[ok][order]
-            first = np.searchsorted(u_ok, np.arange(nu))
-            rank = np.arange(u_ok.size) - first[u_ok]
-            keep = rank < how_many
-            return int(ci.size), u_ok[keep], iid[i_ok[keep]], e_ok[keep]
+            ci_h = ci.cpu().numpy()
+            est = t.estimate_preferences_batch(uid, nb_off, nb, it_off.cpu().numpy(), iid[ci_h], cap)
+            # TopItems.getTopItems: the how_many best values per user (NaN out),
+            # ties by item ID: two stable sorts on the device
+            e = torch.from_numpy(est).to(dev)
+            ok = ~torch.isnan(e)
+            e, u, i = e[ok], cu[ok], ci[ok]
+            o1 = torch.sort(-e, stable=True).indices
+            o2 = torch.sort(u[o1], stable=True).indices
+            order = o1[o2]
+            u, i, e = u[order], i[order], e[order]
+            first = torch.searchsorted(u, torch.arange(nu, device=dev))
+            keep = (torch.arange(u.numel(), device=dev) - first[u]) < how_many
+            return int(ci_h.size), u[keep].cpu().numpy(), iid[i[keep].cpu().numpy()], e[keep].cpu().numpy()
 
         run()
         torch.cuda.synchronize()
