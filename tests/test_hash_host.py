@@ -132,3 +132,28 @@ def test_wbq_route_equals_barrett_route(shim, oracle, width):
                          ctypes.c_int64(keys.size), q.ctypes.data_as(vp), w.ctypes.data_as(vp))
     np.testing.assert_array_equal(q, w)
     np.testing.assert_array_equal(q[:, :6], oracle.hash_keys(a[:6], b[:6], width, keys))
+
+
+def test_per_owner_barrett_low_word_remainder():
+    """k_po_wide_bound's po_mod_w (cms_profiles.hip): s mod w for s < 2^63 and
+    w < 2^30 from the Barrett estimate qq = (s * floor((2^64-1)/w)) >> 64 with
+    only the low 32 bits of s - qq * w and two conditional subtractions --
+    sound because qq is q - 2 .. q, so the true remainder s - qq * w < 3w <
+    2^32.  Checked in exact integers at random and at the edges (s near
+    multiples of w, s = 2^63 - 26, widths 1, 2, powers of two, 2^30 - 1)."""
+    import random
+    rng = random.Random(11)
+    widths = [1, 2, 3, 7, 1025, 2049, 4096, 65537, 2440690, (1 << 30) - 1, 1 << 29]
+    widths += [rng.randrange(1, 1 << 30) for _ in range(200)]
+    for w in widths:
+        m = ((1 << 64) - 1) // w
+        ss = [0, 1, w - 1, w, w + 1, (1 << 63) - 26, (1 << 63) - 26 - ((1 << 63) - 26) % w]
+        ss += [rng.randrange(0, (1 << 63) - 25) for _ in range(200)]
+        ss += [k * w + d for k in (rng.randrange(0, ((1 << 63) - 26) // w) for _ in range(20)) for d in (0, w - 1)]
+        for s in ss:
+            qq = (s * m) >> 64
+            assert s // w - 2 <= qq <= s // w
+            rem = (s - qq * w) & 0xFFFFFFFF
+            rem = rem - w if rem >= w else rem
+            rem = rem - w if rem >= w else rem
+            assert rem == s % w, (s, w)
