@@ -514,29 +514,46 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
 // owners and masses >= 2^16: k_build_rows), byte-class rows (k_build_nibbles
 // finds them itself) and the rest, the mid class (k_build_mid).  Each wave
 // appends its rows with one atomic per list.
+// Rows of chunks of kClassChunk owners per workgroup: the class lists are
+// gathered in LDS (wave-aggregated LDS counters) and reserved with one global
+// atomic per chunk and list -- with one atomic per wave the two list counters
+// took ~200 us of contention at 1M owners.
+constexpr int kClassChunk = 4096;
 __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const int64_t* hi_, int64_t nrows,
                                                        const int32_t* hidx, const uint64_t* bound, int32_t* slot_list,
                                                        int32_t* mid_list, uint32_t* cnt /* [0] slot, [1] mid */) {
+  __shared__ int32_t s_slot[kClassChunk], s_mid[kClassChunk];
+  __shared__ uint32_t s_n[2], s_b[2];
   const int lane = (int)__lane_id();
-  for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nrows; base += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = base + threadIdx.x;
-    bool is_slot = false, is_mid = false;
-    if (r < nrows) {
-      const int32_t sl = hidx[r];
-      is_slot = sl >= 0;
-      is_mid = !is_slot && !byte_class(sl, hi_[r] - lo_[r], bound[r]);
+  const int tid = threadIdx.x;
+  const unsigned long long below = (1ULL << lane) - 1ULL;
+  for (int64_t r0 = (int64_t)blockIdx.x * kClassChunk; r0 < nrows; r0 += (int64_t)gridDim.x * kClassChunk) {
+    if (tid < 2) s_n[tid] = 0;
+    __syncthreads();
+    for (int64_t r = r0 + tid; r < r0 + kClassChunk; r += 256) {  // (whole waves: the ballots)
+      bool is_slot = false, is_mid = false;
+      if (r < nrows) {
+        const int32_t sl = hidx[r];
+        is_slot = sl >= 0;
+        is_mid = !is_slot && !byte_class(sl, hi_[r] - lo_[r], bound[r]);
+      }
+      const unsigned long long ms = __ballot(is_slot), mm = __ballot(is_mid);
+      uint32_t b0 = 0, b1 = 0;
+      if (lane == 0) {
+        if (ms) b0 = atomicAdd(&s_n[0], (uint32_t)__popcll(ms));
+        if (mm) b1 = atomicAdd(&s_n[1], (uint32_t)__popcll(mm));
+      }
+      b0 = (uint32_t)__shfl((int)b0, 0, 64);
+      b1 = (uint32_t)__shfl((int)b1, 0, 64);
+      if (is_slot) s_slot[b0 + __popcll(ms & below)] = (int32_t)r;
+      if (is_mid) s_mid[b1 + __popcll(mm & below)] = (int32_t)r;
     }
-    const unsigned long long ms = __ballot(is_slot), mm = __ballot(is_mid);
-    const unsigned long long below = (1ULL << lane) - 1ULL;
-    uint32_t b0 = 0, b1 = 0;
-    if (lane == 0) {
-      if (ms) b0 = atomicAdd(&cnt[0], (uint32_t)__popcll(ms));
-      if (mm) b1 = atomicAdd(&cnt[1], (uint32_t)__popcll(mm));
-    }
-    b0 = (uint32_t)__shfl((int)b0, 0, 64);
-    b1 = (uint32_t)__shfl((int)b1, 0, 64);
-    if (is_slot) slot_list[b0 + __popcll(ms & below)] = (int32_t)r;
-    if (is_mid) mid_list[b1 + __popcll(mm & below)] = (int32_t)r;
+    __syncthreads();
+    if (tid < 2) s_b[tid] = s_n[tid] ? atomicAdd(&cnt[tid], s_n[tid]) : 0u;
+    __syncthreads();
+    for (uint32_t i = tid; i < s_n[0]; i += 256) slot_list[s_b[0] + i] = s_slot[i];
+    for (uint32_t i = tid; i < s_n[1]; i += 256) mid_list[s_b[1] + i] = s_mid[i];
+    __syncthreads();
   }
 }
 
@@ -1402,27 +1419,40 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
 // Sum of squares of the hot rows after every slice landed; grid (<= 256, depth,
 // chunks of 1024), blocks striding over the hot rows the plan counted (the
 // host's bound on them is loose, and empty blocks still cost launch time).
+// Norms and maxima of the hot (u32 slot) rows: one workgroup per (row,
+// sketch row) at a time, the whole w counters in 16-byte loads (eight in
+// flight per thread at w = 8192), one block reduction per sketch row.
 __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uint32_t* counters, HashParams hp,
                                                    TableView tv, uint64_t* norm, uint32_t* rowmax) {
   __shared__ uint64_t red[4];
   const uint32_t nhot = counters[0];
-  for (uint32_t hb = blockIdx.x; hb < nhot; hb += gridDim.x) {
-  const int64_t row = hot[hb].row;
   const int d = blockIdx.y;
   const int w = (int)hp.width;
-  const uint32_t* p = tv.hot + (int64_t)tv.hidx[row] * tv.dw + (int64_t)d * w;  // split rows are slots
-  uint64_t sq = 0;
-  uint32_t vmax = 0;
-  for (int j = blockIdx.z * 1024 + threadIdx.x; j < min(w, (int)(blockIdx.z + 1) * 1024); j += 256) {
-    sq = sat_add(sq, (uint64_t)p[j] * p[j]);
-    vmax = max(vmax, p[j]);
-  }
+  for (uint32_t hb = blockIdx.x; hb < nhot; hb += gridDim.x) {
+    const int64_t row = hot[hb].row;
+    const uint32_t* p = tv.hot + (int64_t)tv.hidx[row] * tv.dw + (int64_t)d * w;  // split rows are slots
+    uint64_t sq = 0;
+    uint32_t vmax = 0;
+    if ((w & 3) == 0 && (((uintptr_t)p) & 15) == 0) {
+      const uint4* p4 = reinterpret_cast<const uint4*>(p);
+      for (int j = threadIdx.x; j < (w >> 2); j += 256) {
+        const uint4 v = p4[j];
+        sq = sat_add(sq, (uint64_t)v.x * v.x + (uint64_t)v.y * v.y);
+        sq = sat_add(sq, (uint64_t)v.z * v.z + (uint64_t)v.w * v.w);
+        vmax = max(vmax, max(max(v.x, v.y), max(v.z, v.w)));
+      }
+    } else {
+      for (int j = threadIdx.x; j < w; j += 256) {
+        sq = sat_add(sq, (uint64_t)p[j] * p[j]);
+        vmax = max(vmax, p[j]);
+      }
+    }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
-  if ((threadIdx.x & 63) == 0 && vmax) atomicMax(&rowmax[row], vmax);
-  uint64_t tot = block_sum_u64_sat(sq, red);
-  if (tot > (1ULL << 60)) tot = 1ULL << 60;
-  if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((threadIdx.x & 63) == 0 && vmax) atomicMax(&rowmax[row], vmax);
+    uint64_t tot = block_sum_u64_sat(sq, red);
+    if (tot > (1ULL << 60)) tot = 1ULL << 60;
+    if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
   }
 }
 
@@ -1556,7 +1586,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       uint32_t* redo_cnt = reinterpret_cast<uint32_t*>(redo + n);
       CMS_HIP(hipMemsetAsync(lcnt, 0, 2 * sizeof(uint32_t), h->stream));
       CMS_HIP(hipMemsetAsync(redo_cnt, 0, sizeof(uint32_t), h->stream));
-      hipLaunchKernelGGL(k_build_classes, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096))),
+      hipLaunchKernelGGL(k_build_classes,
+                         dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kClassChunk - 1) / kClassChunk, 1024))),
                          dim3(256), 0, h->stream, d_lo, d_hi, n, h->d_hidx, h->ws_bound.as<uint64_t>(), slot_list,
                          mid_list, lcnt);
       CMS_HIP(hipGetLastError());
@@ -1649,7 +1680,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   }
   {
     TimedScope ts(h, "hot_norms");
-    dim3 grid((unsigned)std::min<int64_t>(max_hot, 256), (unsigned)h->p.depth, (unsigned)((h->p.width + 1023) / 1024));
+    dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(max_hot, 1024)), (unsigned)h->p.depth);
     hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
                        h->d_rowmax);
     CMS_HIP(hipGetLastError());
