@@ -343,6 +343,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.mid_u8_image = num("CMS_MID_U8_IMAGE", h->tune.mid_u8_image);
     h->tune.nib_persist = num("CMS_NIB_PERSIST", h->tune.nib_persist);
     h->tune.mid_image = num("CMS_MID_IMAGE", h->tune.mid_image);
+    h->tune.build_streams = num("CMS_BUILD_STREAMS", h->tune.build_streams);
     h->tune.po_no_prune = num("CMS_PO_NO_PRUNE", h->tune.po_no_prune);
     h->tune.po_bound_rows = num("CMS_PO_BOUND_ROWS", h->tune.po_bound_rows);
     h->tune.po_bound_part2 = num("CMS_PO_BOUND_PART2", h->tune.po_bound_part2);
@@ -393,6 +394,8 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   size_t tbytes = sizeof(uint16_t) * (size_t)h->n * (size_t)h->dw;
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&h->side_stream2, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_join3, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_fork2, hipEventDisableTiming)) != hipSuccess ||
@@ -439,6 +442,8 @@ void cms_destroy(cms_handle* h) {
   for (hipEvent_t e : h->event_pool) (void)hipEventDestroy(e);
   if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
+  if (h->side_stream2) (void)hipStreamSynchronize(h->side_stream2);
+  if (h->ev_join3) (void)hipEventDestroy(h->ev_join3);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev_fork2) (void)hipEventDestroy(h->ev_fork2);
@@ -461,6 +466,7 @@ void cms_destroy(cms_handle* h) {
   for (DevBuf* b : ws) b->release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
+  if (h->side_stream2) (void)hipStreamDestroy(h->side_stream2);
   delete h;
 }
 

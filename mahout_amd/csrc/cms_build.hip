@@ -1551,6 +1551,16 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   // k_build_rows: with fast slices it builds only the unsplit slot rows
   const int64_t row_emax = fast_slices ? 0 : emax;
   const int slices_done = fast_slices ? 1 : 0;
+  bool hot_norms_done = false;
+  auto launch_hot_norms = [&]() -> int {
+    TimedScope ts(h, "hot_norms");
+    dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(max_hot, 1024)), (unsigned)h->p.depth);
+    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
+                       h->d_rowmax);
+    CMS_HIP(hipGetLastError());
+    hot_norms_done = true;
+    return CMS_OK;
+  };
   {
     TimedScope ts(h, "build_rows");
     auto kern = k_build_rows<kBuildStoreForm>;
@@ -1598,18 +1608,23 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       // once the side stream has forked, every exit (error returns included)
       // joins it back: the caller's next work on h->stream may reuse or free
       // the buffers the side kernels are still writing
+      // the mid class on a third stream (Tunables::build_streams == 3)
+      const hipStream_t side2 = side != h->stream && h->tune.build_streams >= 3 ? h->side_stream2 : side;
       struct SideJoin {
         cms_handle* h;
-        hipStream_t side;
+        hipStream_t side, side2;
         bool armed = false;
         ~SideJoin() {
           if (armed && hipEventRecord(h->ev_join2, side) == hipSuccess)
             (void)hipStreamWaitEvent(h->stream, h->ev_join2, 0);
+          if (armed && side2 != side && hipEventRecord(h->ev_join3, side2) == hipSuccess)
+            (void)hipStreamWaitEvent(h->stream, h->ev_join3, 0);
         }
-      } join{h, side};
+      } join{h, side, side2};
       if (side != h->stream) {
         CMS_HIP(hipEventRecord(h->ev_fork2, h->stream));
         CMS_HIP(hipStreamWaitEvent(side, h->ev_fork2, 0));
+        if (side2 != side) CMS_HIP(hipStreamWaitEvent(side2, h->ev_fork2, 0));
         join.armed = true;
       }
       const int64_t nib_blocks = (n + kNibWaves - 1) / kNibWaves;
@@ -1646,7 +1661,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                            h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);
       } else
       hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
-                         dim3(kBuildThreads), mid_lds, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
+                         dim3(kBuildThreads), mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                          h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0, h->tune.mid_u4_keys,
                          h->tune.mid_u8_keys, u8img);
@@ -1663,10 +1678,16 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          h->ws_bound.as<uint64_t>(), forms, skip_untouched, h->d_hidx, h->d_cbound,
                          (const int32_t*)slot_list, (const uint32_t*)lcnt);
       CMS_HIP(hipGetLastError());
+      // (k_hot_norms here, overlapping the side streams' tail, measured no
+      // faster: it competes with them for the CUs)
       if (join.armed) {
         join.armed = false;
         CMS_HIP(hipEventRecord(h->ev_join2, side));
         CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join2, 0));
+        if (side2 != side) {
+          CMS_HIP(hipEventRecord(h->ev_join3, side2));
+          CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_join3, 0));
+        }
       }
     } else {
       if ((rc0 = launch_slices())) return rc0;
@@ -1678,13 +1699,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       CMS_HIP(hipGetLastError());
     }
   }
-  {
-    TimedScope ts(h, "hot_norms");
-    dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(max_hot, 1024)), (unsigned)h->p.depth);
-    hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
-                       h->d_rowmax);
-    CMS_HIP(hipGetLastError());
-  }
+  if (!hot_norms_done && (rc0 = launch_hot_norms())) return rc0;
   h->empty = false;
   h->norms_valid = true;  // build_rows + hot_norms wrote the norm of every row
   return CMS_OK;
