@@ -344,6 +344,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.nib_persist = num("CMS_NIB_PERSIST", h->tune.nib_persist);
     h->tune.mid_image = num("CMS_MID_IMAGE", h->tune.mid_image);
     h->tune.build_streams = num("CMS_BUILD_STREAMS", h->tune.build_streams);
+    h->tune.plan_side = num("CMS_PLAN_SIDE", h->tune.plan_side);
     h->tune.po_no_prune = num("CMS_PO_NO_PRUNE", h->tune.po_no_prune);
     h->tune.po_bound_rows = num("CMS_PO_BOUND_ROWS", h->tune.po_bound_rows);
     h->tune.po_bound_part2 = num("CMS_PO_BOUND_PART2", h->tune.po_bound_part2);
@@ -396,6 +397,8 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
       (e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&h->side_stream2, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_join3, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_spans, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_plan, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_fork2, hipEventDisableTiming)) != hipSuccess ||
@@ -444,6 +447,8 @@ void cms_destroy(cms_handle* h) {
   if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
   if (h->side_stream2) (void)hipStreamSynchronize(h->side_stream2);
   if (h->ev_join3) (void)hipEventDestroy(h->ev_join3);
+  if (h->ev_spans) (void)hipEventDestroy(h->ev_spans);
+  if (h->ev_plan) (void)hipEventDestroy(h->ev_plan);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev_fork2) (void)hipEventDestroy(h->ev_fork2);

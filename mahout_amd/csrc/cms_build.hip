@@ -1503,6 +1503,27 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   HotInfo* hot = reinterpret_cast<HotInfo*>(base + sz_rowhot);
   int2* extra_map = reinterpret_cast<int2*>(base + sz_rowhot + sz_hot);
   uint32_t* counters = h->d_flags + 4;  // [4..7]: hot rows, mapped slices (one u64 atomic), spare
+  // A fresh unit-increment build right after a partition that marked its
+  // spans (ingest_coo): the plan below needs only the spans, so it runs on
+  // the side stream beside the partition's last scatter (h->stream swapped
+  // for the section; joined back before the build reads the keys).
+  struct PlanSide {
+    cms_handle* h;
+    bool on = false;
+    void end() {
+      if (!on) return;
+      on = false;
+      std::swap(h->stream, h->side_stream);
+      if (hipEventRecord(h->ev_plan, h->side_stream) == hipSuccess) (void)hipStreamWaitEvent(h->stream, h->ev_plan, 0);
+    }
+    ~PlanSide() { end(); }
+  } plan_side{h};
+  if (h->spans_event && !accumulate && !d_val && h->side_stream) {
+    h->spans_event = false;
+    CMS_HIP(hipStreamWaitEvent(h->side_stream, h->ev_spans, 0));
+    std::swap(h->stream, h->side_stream);
+    plan_side.on = true;
+  }
   CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
   // table layout: rows that could reach 2^16, and split rows, get u32 slots
   {
@@ -1544,6 +1565,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                        fast_slices ? 0 : 1, row_hot, hot, extra_map, counters, h->d_norm, h->d_rowmax, h->p.depth);
     CMS_HIP(hipGetLastError());
   }
+  plan_side.end();
   // fresh builds may store byte forms: the whole [d][w] byte image in LDS
   const int forms = h->forms_ok && !accumulate && (size_t)h->dw <= kFormLdsMax ? 1 : 0;
   const int skip_untouched = accumulate && h->norms_valid ? 1 : 0;

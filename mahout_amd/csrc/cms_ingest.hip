@@ -517,13 +517,23 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
   uint32_t* ctok;
   float* cval;
   int rc = kNoSpans;
+  // the partition marks its spans ready before its last scatter, and the
+  // build plan (which needs only the spans) runs beside that scatter
+  h->plan_side_request = h->tune.plan_side != 0;
+  h->spans_event = false;
   if (h->tune.hot_routing) rc = partition_to_spans(h, d_row, d_key, d_val, npairs, &clo, &chi, &ctok, &cval);
   if (rc == kNoSpans) {
     rc = partition_to_csr(h, d_row, d_key, d_val, npairs, &clo, &ctok, &cval);
     chi = clo + 1;
   }
-  if (rc) return rc;
-  return ingest_spans_device(h, clo, chi, d_key, ctok, cval, npairs);
+  h->plan_side_request = false;
+  if (rc) {
+    h->spans_event = false;
+    return rc;
+  }
+  rc = ingest_spans_device(h, clo, chi, d_key, ctok, cval, npairs);
+  h->spans_event = false;
+  return rc;
 }
 
 }  // namespace cms

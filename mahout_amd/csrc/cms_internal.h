@@ -204,6 +204,7 @@ struct Tunables {
   int mid_u4_keys = 768;    // CMS_MID_U4_KEYS: more keys start at u8 (list-row owners always try 4-bit)
   int mid_u8_keys = 12288;  // CMS_MID_U8_KEYS: more keys start at u16
   int nib_persist = 0;      // CMS_NIB_PERSIST=1: k_build_nibbles as persistent waves (else one owner per wave)
+  int plan_side = 1;        // CMS_PLAN_SIDE=0: the build plan after the whole partition on the handle's stream
   int build_streams = 3;    // CMS_BUILD_STREAMS=2: the mid class after the byte class on one side stream
   int mid_image = 0;        // CMS_MID_IMAGE=1: mid owners through the one-pass u16 image (k_build_image; slower on MI355X)
   int po_dense_x4 = 4;      // CMS_PO_DENSE_X4: group kernel's dense dots when 4 w <= this x nnz(u1)
@@ -232,6 +233,10 @@ struct cms_handle {
   hipEvent_t ev_fork2 = nullptr, ev_join2 = nullptr;  // byte / mid class kernels beside the slot rows
   hipStream_t side_stream2 = nullptr;                 // the mid class beside the byte class (Tunables::build_streams 3)
   hipEvent_t ev_join3 = nullptr;
+  // the owner spans of a partition are ready (recorded before its last
+  // scatter): the build plan may start on the side stream meanwhile
+  hipEvent_t ev_spans = nullptr, ev_plan = nullptr;
+  bool spans_event = false, plan_side_request = false;
   // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
   // the point queries after cms_finalize hold it shared and run concurrently,
   // each on a QueryCtx of its own (the table and norms are read-only then).

@@ -844,9 +844,8 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     // one pass-2 workgroup per CU fits its LDS tile; a few per CU keep the
     // dispatcher ahead of the exits (multiple of 8: XCD-contiguous blocks)
     const int64_t g2s = std::min<int64_t>((nb2max + 7) & ~int64_t(7), (int64_t)h->num_cus * 2);
-    hipLaunchKernelGGL(scat2, dim3((unsigned)g2s), dim3(kPartThreads),
-                       tile_lds_bytes(P2, d_val != nullptr, false, false, R2 * kPartTile), h->stream, fine, key1, val1,
-                       binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
+    // the owner spans need only the offsets: computed before the last
+    // scatter, and marked so the build plan can run beside it
     if (hot) {
       int64_t* chi = h->ws_csr_hi.as<int64_t>();
       hipLaunchKernelGGL(k_spans_hi, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0,
@@ -856,6 +855,14 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     } else {
       *out_hi = coff + 1;
     }
+    h->spans_event = false;
+    if (h->plan_side_request && h->side_stream && !d_val) {
+      CMS_HIP(hipEventRecord(h->ev_spans, h->stream));
+      h->spans_event = true;
+    }
+    hipLaunchKernelGGL(scat2, dim3((unsigned)g2s), dim3(kPartThreads),
+                       tile_lds_bytes(P2, d_val != nullptr, false, false, R2 * kPartTile), h->stream, fine, key1, val1,
+                       binStart, blkStart, P1, CH2, P2, O2, ckey, cval, out_rows);
     CMS_HIP(hipGetLastError());
   }
   *out_lo = coff;
