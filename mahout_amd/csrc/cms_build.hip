@@ -649,6 +649,14 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       __syncthreads();
       bool ovf = false;
       vmax = 0;
+      // a list row at an unrolled depth takes its sums of squares from the
+      // adds (2 c inc + inc^2 per update, telescoping to sum c^2) instead of
+      // reading the image back: nothing of it is stored
+      constexpr int kSq = D > 0 ? D : 1;
+      uint32_t sqr[kSq];
+#pragma unroll
+      for (int d = 0; d < kSq; ++d) sqr[d] = 0u;
+      const bool tele = D > 0 && as_list;
       // lt >= 0: the key's list index -- a list row's entries leave during
       // the count (a count past 255 later rewrites the slot as u16 rows)
       auto add_all = [&](uint64_t kr, uint32_t inc, int64_t lt) {
@@ -660,6 +668,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
           const uint32_t nv = old + inc;
           ovf |= nv > capa || inc > capa;  // carried into the next counter: a wider form
           vmax = max(vmax, nv);
+          if (D > 0) sqr[D > 0 ? d : 0] += (2u * old + inc) * inc;
         });
       };
       if (cached) {
@@ -709,8 +718,17 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       const bool fits = s_ovf == 0u;
       __syncthreads();  // every thread has read s_ovf before the row passes reset it
       if (fits) level = 0;
+      if (fits && tele) {
+#pragma unroll
+        for (int d = 0; d < kSq; ++d) {
+          const uint32_t sq = wave_sum_u32(sqr[d]);
+          if ((tid & 63) == 0 && sq) atomicAdd(&s_norm[d], (unsigned long long)sq);
+        }
+        level = 3;  // a list row, norms done: no read-back
+      }
     }
-    if (level == 0) {
+    if (level == 3) level = 0;
+    else if (level == 0) {
       // read the image back: each sketch row's sum of squares (v_dot4 of its
       // low and high nibbles) as its rows leave for the slot
       const uint4* l4 = reinterpret_cast<const uint4*>(lds);
