@@ -1133,7 +1133,10 @@ __global__ __launch_bounds__(kImgThreads) void k_build_image(
 // owner is queued for k_build_bytes, which rewrites its whole slot, norms and
 // maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
 // one wave's LDS operations execute in program order.
-constexpr int kNibWaves = 4;
+#ifndef CMS_NIB_WAVES
+#define CMS_NIB_WAVES 4
+#endif
+constexpr int kNibWaves = CMS_NIB_WAVES;
 // owners with at most Tunables::bit_keys (64) keys try 1-bit rows first, with
 // at most crumb_keys (256) 2-bit rows
 // One byte-class owner by one wave (k_build_nibbles).
