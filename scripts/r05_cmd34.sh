@@ -1,2 +1,2 @@
 set -o pipefail
-STEPS="ab" ARMS="main ab/nw8.so ab/nw16.so main ab/nw8.so ab/nw16.so" bash scripts/r05_iter.sh
+STEPS="ab" ARMS="main ab/nw2.so ab/nw1.so main ab/nw2.so ab/nw1.so" bash scripts/r05_iter.sh
