@@ -1133,6 +1133,9 @@ __global__ __launch_bounds__(kImgThreads) void k_build_image(
 // owner is queued for k_build_bytes, which rewrites its whole slot, norms and
 // maximum as a u8 row.  Waves never wait on each other (no workgroup barrier):
 // one wave's LDS operations execute in program order.
+#ifndef CMS_MID_GRID_PER_CU  // persistent k_build_mid workgroups per CU
+#define CMS_MID_GRID_PER_CU 8
+#endif
 #ifndef CMS_NIB_WAVES
 #define CMS_NIB_WAVES 4
 #endif
@@ -1703,7 +1706,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                            (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                            h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);
       } else
-      hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 8)),
+      hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * CMS_MID_GRID_PER_CU)),
                          dim3(kBuildThreads), mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                          h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0, h->tune.mid_u4_keys,
