@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--width", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--detail-out", default=None, help="also write the full record (one JSON line) to this file")
     ap.add_argument("--no-extras", action="store_true", help="skip the CSR, host-buffer and query side measurements")
     ap.add_argument("--no-config1", action="store_true")
     ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (100K items) secondary ingest line")
@@ -1331,9 +1332,16 @@ def main():
                                          ("bound", "achieved", "peak", "unit", "frac", "avg_launch_ms",
                                           "pmc_mfma_busy_frac", "pmc_l2_hit")}
             result["cosine_roofline"]["kernel"] = "k_cosine_sym fp4"
-        # last key: a compact record of every line, so the stdout tail carries it
         result["summary"] = summary(result)
-        print(json.dumps(result))
+        # the whole record (config 1/2 extras, the cosine and config-5 objects)
+        # goes to stderr and, with --detail-out, to a file; stdout ends with
+        # ONE compact line (<= COMPACT_LIMIT chars) that the driver parses
+        full = json.dumps(result)
+        print("bench-detail: " + full, file=sys.stderr, flush=True)
+        if args.detail_out:
+            with open(args.detail_out, "w") as f:
+                f.write(full + "\n")
+        print(json.dumps(compact_line(result)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -1341,6 +1349,51 @@ def main():
 
 def _r(x, nd=4):
     return None if x is None else float(f"{x:.{nd}g}")
+
+
+COMPACT_LIMIT = 7000  # the driver's stdout tail window is ~8 KB; the line must fit it whole
+
+# keys of the full record carried verbatim by the compact line
+_COMPACT_TOP = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config", "roofline", "step_roofline", "breakdown_ms_per_step",
+                "allreduce_ms_per_step", "table", "vs_cpu_baseline", "memory", "merge", "cosines_per_s",
+                "cosine_wall_s", "cosine_first_job_s", "cosine_roofline")
+
+
+def compact_line(res):
+    """The one JSON line the driver parses: the contract's keys, the build
+    and step rooflines, the CPU baseline with its modes, the cosine keys and
+    the summary of every other line. Long prose fields are shortened and the
+    full record is printed separately (stderr / --detail-out)."""
+    out = {k: res[k] for k in _COMPACT_TOP if k in res}
+    if "config" in out:
+        cfg = dict(out["config"])
+        cfg.pop("sharding", None)
+        out["config"] = cfg
+    if "roofline" in out:
+        out["roofline"] = {k: v for k, v in out["roofline"].items() if k != "algorithmic_bytes_basis"}
+    cb = res.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "best_updates_per_s")}
+        out["cpu_baseline"]["modes"] = {m: {k: _r(v) if isinstance(v, float) else v for k, v in mv.items()}
+                                        for m, mv in (cb.get("modes") or {}).items()}
+        out["cpu_baseline"]["host"] = cb.get("host")
+    out["summary"] = res.get("summary") or summary(res)
+    out["detail"] = "full record on stderr ('bench-detail: ' line) and in --detail-out"
+    s = json.dumps(out)
+    # shed optional keys (never the contract's) until the line fits
+    for k in ("memory", "table", "breakdown_ms_per_step", "step_roofline"):
+        if len(s) <= COMPACT_LIMIT:
+            break
+        if k == "step_roofline" and "step_roofline" in out:
+            out[k] = {kk: out[k].get(kk) for kk in ("achieved_GBps", "frac")}
+        else:
+            out.pop(k, None)
+        s = json.dumps(out)
+    if len(s) > COMPACT_LIMIT and "cpu_baseline" in out:
+        out["cpu_baseline"].pop("modes", None)
+        out["cpu_baseline"]["sample"] = str(out["cpu_baseline"].get("sample"))[:120]
+    return out
 
 
 def summary(res):
