@@ -524,7 +524,7 @@ def config1_recommender(nn=50, how_many=10, reps=5):
     return out
 
 
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")  # this round's committed rocprofv3 summaries
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")  # this round's committed rocprofv3 summaries
 
 
 def _pmc_file(name):

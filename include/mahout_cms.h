@@ -450,8 +450,11 @@ typedef struct cms_stats {
   int64_t po_wide_pairs;     /* per-owner top-k: (query, wide owner) pairs given the row-0 bound so far */
   int64_t po_wide_exact;     /* of those, pairs the bound could not rule out (computed exactly) */
 } cms_stats;
-/* out->struct_size must be set (at least through pairs_ingested); a caller
- * built against an older, shorter cms_stats receives the fields it knows. */
+/* out->struct_size must be set (at least through pairs_ingested); an ABI-2
+ * caller whose cms_stats is shorter (built before later fields were appended)
+ * receives the fields it knows. ABI-1 structs had no struct_size: bindings
+ * compare cms_abi_version() with CMS_ABI_VERSION at load time (mahout_amd/_lib.py,
+ * the JNI shim's JNI_OnLoad) and refuse a mismatch. */
 int cms_get_stats(cms_handle* h, cms_stats* out);
 
 /* Per-kernel HIP-event timing on the handle's stream (off by default).

@@ -40,6 +40,15 @@ static int fail(JNIEnv* env, int rc, int item_ids) {
   return 1;
 }
 
+/* The shim is compiled against one cms_stats / cms_params layout: refuse a
+   libmahout_cms.so of another ABI (System.loadLibrary then throws
+   UnsatisfiedLinkError) instead of reading its structs with the wrong shape. */
+JNIEXPORT jint JNICALL JNI_OnLoad(JavaVM* vm, void* reserved) {
+  (void)vm;
+  (void)reserved;
+  return cms_abi_version() == CMS_ABI_VERSION ? JNI_VERSION_1_6 : JNI_ERR;
+}
+
 #define H(x) ((cms_handle*)(intptr_t)(x))
 #define JFN(name) Java_org_apache_mahout_cf_taste_impl_similarity_CosineCMGpu_##name
 

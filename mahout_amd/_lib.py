@@ -11,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SO_PATH = os.environ.get("MAHOUT_CMS_LIB") or os.path.join(HERE, "libmahout_cms.so")  # override: experiments
 
 # status codes (include/mahout_cms.h)
+CMS_ABI_VERSION = 2  # include/mahout_cms.h CMS_ABI_VERSION: the layout of the structs below
 CMS_OK = 0
 CMS_E_PARAM = 1
 CMS_E_SHAPE = 2
@@ -188,6 +189,12 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the ctypes structs above mirror one header layout: a stale library (or
+    # stale bindings) must fail here, not read cms_stats with the wrong shape
+    got = lib.cms_abi_version()
+    if got != CMS_ABI_VERSION:
+        raise RuntimeError(f"{SO_PATH} has ABI version {got}, these bindings need {CMS_ABI_VERSION}: rebuild it "
+                           "with `python -m mahout_amd.build_lib`")
     _lib = lib
     return lib
 

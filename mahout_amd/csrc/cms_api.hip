@@ -1082,31 +1082,15 @@ int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neig
                      false);
 }
 
-int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
-                                   const int64_t* neighbor_ids, const int64_t* item_offsets, const int64_t* item_keys,
-                                   int32_t use_capper, float cap_min, float cap_max, float* out) {
-  if (!h || n < 0 || (n > 0 && (!user_ids || !nb_offsets || !item_offsets)))
-    return set_error(CMS_E_PARAM, "null argument");
-  if (n == 0) return CMS_OK;
-  if (nb_offsets[0] != 0 || item_offsets[0] != 0) return set_error(CMS_E_PARAM, "offsets must start at 0");
-  for (int64_t u = 0; u < n; ++u)
-    if (nb_offsets[u + 1] < nb_offsets[u] || item_offsets[u + 1] < item_offsets[u])
-      return set_error(CMS_E_PARAM, "offsets must not decrease");
-  const int64_t M = nb_offsets[n], Q = item_offsets[n];
-  if ((M > 0 && !neighbor_ids) || (Q > 0 && (!item_keys || !out))) return set_error(CMS_E_PARAM, "null argument");
-  if (Q >= (int64_t(1) << 31)) return set_error(CMS_E_PARAM, "too many candidate items in one batch");
-  Guard g(h);
+// cms_estimate_preferences_batch on a fixed-shape table, under the shared
+// guard: c.r rows, c.y neighbour offsets, c.x similarities, c.q item keys,
+// c.z candidate -> user, c.o estimates, all on c.stream.
+static int estimate_batch_on(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
+                             const int64_t* neighbor_ids, const int64_t* item_offsets, const int64_t* item_keys,
+                             int32_t use_capper, float cap_min, float cap_max, float* out, QueryCtx& c) {
   int rc = require_finalized(h);
   if (rc) return rc;
-  if (h->per_owner || h->f64) {  // per-user estimates (their own kernels), one user after another
-    QueryCtx tmp;
-    for (int64_t u = 0; u < n; ++u)
-      if ((rc = estimate_on(h, user_ids[u], neighbor_ids + nb_offsets[u], nb_offsets[u + 1] - nb_offsets[u],
-                            item_keys + item_offsets[u], item_offsets[u + 1] - item_offsets[u], use_capper, cap_min,
-                            cap_max, out + item_offsets[u], h->stream, tmp, false)))
-        return rc;
-    return CMS_OK;
-  }
+  const int64_t M = nb_offsets[n], Q = item_offsets[n];
   // rows: users [n], then per pair (user row, neighbour row) [M] x 2; the
   // owner of every candidate [Q]
   std::vector<int64_t> rows((size_t)(n + 2 * M));
@@ -1120,27 +1104,61 @@ int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user
     for (int64_t i = item_offsets[u]; i < item_offsets[u + 1]; ++i) item_user[(size_t)i] = (int32_t)u;
   }
   if (Q == 0) return CMS_OK;
-  DevBuf d_rows, d_off, d_sims, d_items, d_iu, d_out;
+  DevBuf &d_rows = c.r, &d_off = c.y, &d_sims = c.x, &d_items = c.q, &d_iu = c.z, &d_out = c.o;
   CMS_HIP(d_rows.ensure(sizeof(int64_t) * rows.size()));
   CMS_HIP(d_off.ensure(sizeof(int64_t) * (size_t)(n + 1)));
   CMS_HIP(d_sims.ensure(sizeof(double) * (size_t)std::max<int64_t>(M, 1)));
   CMS_HIP(d_items.ensure(sizeof(int64_t) * (size_t)Q));
   CMS_HIP(d_iu.ensure(sizeof(int32_t) * (size_t)Q));
   CMS_HIP(d_out.ensure(sizeof(float) * (size_t)Q));
-  hipStream_t st = h->stream;
+  hipStream_t st = c.stream;
   CMS_HIP(hipMemcpyAsync(d_rows.ptr, rows.data(), sizeof(int64_t) * rows.size(), hipMemcpyHostToDevice, st));
   CMS_HIP(hipMemcpyAsync(d_off.ptr, nb_offsets, sizeof(int64_t) * (size_t)(n + 1), hipMemcpyHostToDevice, st));
   CMS_HIP(hipMemcpyAsync(d_items.ptr, item_keys, sizeof(int64_t) * (size_t)Q, hipMemcpyHostToDevice, st));
   CMS_HIP(hipMemcpyAsync(d_iu.ptr, item_user.data(), sizeof(int32_t) * (size_t)Q, hipMemcpyHostToDevice, st));
   const int64_t* dr = d_rows.as<int64_t>();
   // userSimilarity(user, neighbour) for every pair of the batch (:162)
-  if ((rc = pair_cosines_many(h, dr + n, dr + n + M, M, d_sims.as<double>(), nullptr))) return rc;
+  if ((rc = pair_cosines_many(h, dr + n, dr + n + M, M, d_sims.as<double>(), st))) return rc;
   if ((rc = estimate_preferences_batch(h, dr, d_off.as<int64_t>(), dr + n + M, d_sims.as<double>(), d_iu.as<int32_t>(),
                                        d_items.as<int64_t>(), Q, use_capper, cap_min, cap_max, d_out.as<float>(),
-                                       nullptr)))
+                                       st)))
     return rc;
   CMS_HIP(hipMemcpyAsync(out, d_out.ptr, sizeof(float) * (size_t)Q, hipMemcpyDeviceToHost, st));
   CMS_HIP(hipStreamSynchronize(st));
+  return CMS_OK;
+}
+
+int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
+                                   const int64_t* neighbor_ids, const int64_t* item_offsets, const int64_t* item_keys,
+                                   int32_t use_capper, float cap_min, float cap_max, float* out) {
+  if (!h || n < 0 || (n > 0 && (!user_ids || !nb_offsets || !item_offsets)))
+    return set_error(CMS_E_PARAM, "null argument");
+  if (n == 0) return CMS_OK;
+  if (nb_offsets[0] != 0 || item_offsets[0] != 0) return set_error(CMS_E_PARAM, "offsets must start at 0");
+  for (int64_t u = 0; u < n; ++u)
+    if (nb_offsets[u + 1] < nb_offsets[u] || item_offsets[u + 1] < item_offsets[u])
+      return set_error(CMS_E_PARAM, "offsets must not decrease");
+  const int64_t M = nb_offsets[n], Q = item_offsets[n];
+  if ((M > 0 && !neighbor_ids) || (Q > 0 && (!item_keys || !out))) return set_error(CMS_E_PARAM, "null argument");
+  if (Q >= (int64_t(1) << 31)) return set_error(CMS_E_PARAM, "too many candidate items in one batch");
+  if (!h->per_owner && !h->f64) {
+    // fixed-shape u32 table: one batched pass, shared with other readers, on
+    // a leased stream and scratch (no per-call hipMalloc)
+    SharedGuard g(h);
+    CtxLease L(h);
+    if (int rc = L.ready()) return rc;
+    return estimate_batch_on(h, n, user_ids, nb_offsets, neighbor_ids, item_offsets, item_keys, use_capper, cap_min,
+                             cap_max, out, *L.c);
+  }
+  Guard g(h);
+  int rc = require_finalized(h);
+  if (rc) return rc;
+  QueryCtx tmp;  // per-user estimates (their own kernels), one user after another
+  for (int64_t u = 0; u < n; ++u)
+    if ((rc = estimate_on(h, user_ids[u], neighbor_ids + nb_offsets[u], nb_offsets[u + 1] - nb_offsets[u],
+                          item_keys + item_offsets[u], item_offsets[u + 1] - item_offsets[u], use_capper, cap_min,
+                          cap_max, out + item_offsets[u], h->stream, tmp, false)))
+      return rc;
   return CMS_OK;
 }
 

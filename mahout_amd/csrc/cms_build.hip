@@ -1538,6 +1538,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       if (!on) return;
       on = false;
       std::swap(h->stream, h->side_stream);
+      h->plan_side_active = false;
       if (hipEventRecord(h->ev_plan, h->side_stream) == hipSuccess) (void)hipStreamWaitEvent(h->stream, h->ev_plan, 0);
     }
     ~PlanSide() { end(); }
@@ -1546,6 +1547,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     h->spans_event = false;
     CMS_HIP(hipStreamWaitEvent(h->side_stream, h->ev_spans, 0));
     std::swap(h->stream, h->side_stream);
+    h->plan_side_active = true;  // nothing in the section may launch on h->side_stream (it is the main stream now)
     plan_side.on = true;
   }
   CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
@@ -1647,6 +1649,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                          dim3(256), 0, h->stream, d_lo, d_hi, n, h->d_hidx, h->ws_bound.as<uint64_t>(), slot_list,
                          mid_list, lcnt);
       CMS_HIP(hipGetLastError());
+      if (h->plan_side_active) return set_error(CMS_E_STATE, "internal: side stream used while swapped for the plan");
       hipStream_t side = h->side_stream ? h->side_stream : h->stream;
 #ifdef CMS_BUILD_SERIAL  // bound analysis only: the classes' kernels one after another (isolated durations)
       side = h->stream;

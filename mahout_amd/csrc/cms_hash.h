@@ -140,11 +140,13 @@ CMS_HD uint32_t bucket_q(const HashParams& hp, int r, uint64_t kp, double kf, ui
     double d;
     uint64_t u;
   } qb;
-  qb.d = fl + 4503599627370496.0;  // 2^52: the integer q0 < 2^32 in the low mantissa bits
+  qb.d = fl + 4503599627370496.0;  // 2^52: the integer q0 <= 2^32 in the low mantissa bits
   uint32_t q = (uint32_t)qb.u;
   if (!(fr >= kQEps && fr <= 1.0 - kQEps)) {  // about 1 hash in 30,000
-    const uint64_t x = hp.ap[r] * kp + hp.bp[r];                      // X mod 2^64
-    const uint64_t s = x - (((uint64_t)q << 63) - 25u * (uint64_t)q);  // X - q0 p mod 2^64 (p = 2^63 - 25)
+    // q0 needs 33 bits here: y can round up to exactly 2^32 (true q 2^32 - 1)
+    const uint64_t q0 = qb.u & 0xFFFFFFFFFFFFFULL;
+    const uint64_t x = hp.ap[r] * kp + hp.bp[r];    // X mod 2^64
+    const uint64_t s = x - ((q0 << 63) - 25u * q0);  // X - q0 p mod 2^64 (p = 2^63 - 25)
     if (s >= kPrime) q = fr < 0.5 ? q - 1u : q + 1u;
   }
   const uint32_t xm = CMS_MUL24((uint32_t)hp.ap[r] & hp.wmask, km) + (uint32_t)hp.bp[r];
@@ -218,7 +220,7 @@ CMS_HD uint64_t residue_wbq(const HashParams& hp, int r, uint64_t kp) {
     uint64_t u;
   } qb;
   qb.d = fl + 4503599627370496.0;  // 2^52
-  const uint64_t q = (uint32_t)qb.u;
+  const uint64_t q = qb.u & 0xFFFFFFFFFFFFFULL;  // q0 <= 2^32: y can round up to exactly 2^32
   uint64_t s = hp.ap[r] * kp + hp.bp[r] - ((q << 63) - 25u * q);  // X - q0 p (mod 2^64)
   if (s >= kPrime) s = fr < 0.5 ? s + kPrime : s - kPrime;
   return s;

@@ -185,7 +185,7 @@ namespace cms {
 // own stream and buffers, taken from the handle's pool for the call.
 struct QueryCtx {
   hipStream_t stream = nullptr;
-  DevBuf q, o, r, x;
+  DevBuf q, o, r, x, y, z;
 };
 }  // namespace cms
 
@@ -237,6 +237,7 @@ struct cms_handle {
   // scatter): the build plan may start on the side stream meanwhile
   hipEvent_t ev_spans = nullptr, ev_plan = nullptr;
   bool spans_event = false, plan_side_request = false;
+  bool plan_side_active = false;  // h->stream and h->side_stream are swapped (the build plan's section)
   // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
   // the point queries after cms_finalize hold it shared and run concurrently,
   // each on a QueryCtx of its own (the table and norms are read-only then).

@@ -856,6 +856,7 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
       *out_hi = coff + 1;
     }
     h->spans_event = false;
+    if (h->plan_side_active) return set_error(CMS_E_STATE, "internal: partition inside the plan's swapped-stream section");
     if (h->plan_side_request && h->side_stream && !d_val) {
       CMS_HIP(hipEventRecord(h->ev_spans, h->stream));
       h->spans_event = true;

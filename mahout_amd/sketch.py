@@ -307,6 +307,12 @@ class SketchTable:
         it = np.ascontiguousarray(item_keys, np.int64)
         if nbo.size != us.size + 1 or ito.size != us.size + 1:
             raise ValueError("offset arrays need len(user_ids) + 1 entries")
+        # the library reads neighbor_ids / item_keys up to the last offsets and
+        # writes item_offsets[-1] estimates: the offsets must describe exactly
+        # these arrays, or the call would run past the host buffers
+        for name, o, arr in (("nb_offsets", nbo, nb), ("item_offsets", ito, it)):
+            if o[0] != 0 or o[-1] != arr.size or (o.size > 1 and bool(np.any(np.diff(o) < 0))):
+                raise ValueError(f"{name} must start at 0, never decrease and end at the length of its array")
         out = np.zeros(it.size, np.float32)
         lo, hi = capper if capper is not None else (0.0, 0.0)
         check(self._lib.cms_estimate_preferences_batch(self._h, us.size, _ptr(us), _ptr(nbo), _ptr(nb), _ptr(ito),

@@ -119,3 +119,21 @@ def test_frac_bits_for_preference_granularity():
     assert frac_bits_for(np.array([0.1], np.float32)) == 27  # 0.1f = 13421773 * 2^-27
     with pytest.raises(ValueError):
         frac_bits_for(np.array([1e-12], np.float32))
+
+
+@pytest.mark.parametrize("nbo,ito", [
+    ([0, 2, 9], [0, 1, 3]),   # neighbour offsets past neighbor_ids
+    ([0, 2, 3], [0, 1, 7]),   # item offsets past item_keys (the output buffer is sized from item_keys)
+    ([1, 2, 3], [0, 1, 3]),   # does not start at 0
+    ([0, 3, 2], [0, 1, 3]),   # decreasing
+    ([0, 2, 3], [0, 2, 1]),   # decreasing, ends short
+])
+def test_estimate_batch_rejects_offsets_outside_the_arrays(nbo, ito):
+    """the offsets must describe exactly the arrays handed over,
+    or the library call would read / write past the host buffers. Checked in
+    the binding before any library call (no handle or device needed)."""
+    import types
+    from mahout_amd.sketch import SketchTable
+    fake = types.SimpleNamespace()  # never reached: the checks raise first
+    with pytest.raises(ValueError):
+        SketchTable.estimate_preferences_batch(fake, [1, 2], nbo, [5, 6, 7], ito, [10, 11, 12])

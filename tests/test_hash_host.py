@@ -157,3 +157,28 @@ def test_per_owner_barrett_low_word_remainder():
             rem = rem - w if rem >= w else rem
             rem = rem - w if rem >= w else rem
             assert rem == s % w, (s, w)
+
+
+@pytest.mark.parametrize("width", [1024, 8192, 1 << 24, 1000, 30011, 2440690])
+def test_quotient_routes_at_two_to_the_32(shim, oracle, width):
+    """a', b' within ~2^10 of p make a'/p and b'/p round to 1.0, so for
+    k' = 2^32 - 1 the fp64 quotient y = fma(a'/p, k', b'/p) rounds up to
+    exactly 2^32 while the true quotient is 2^32 - 1: the estimate needs 33
+    bits. bucket_q (power-of-two widths) and bucket_wbq (any
+    width) must still equal the folding route and the oracle."""
+    p = 2 ** 63 - 25
+    a = np.array([p - 1, p - 2, p - 1000, -2 ** 63, p - 1, 2 ** 63 - 1], np.int64)
+    b = np.array([p - 1, p - 1, p - 3, 2 ** 63 - 1, p - 700, p - 1], np.int64)
+    keys = np.array([2 ** 32 - 1, 2 ** 32 - 2, 2 ** 32 - 3, 2 ** 32 - 1000, 2 ** 32, 2 ** 31, 0, 1], np.int64)
+    ref = oracle.hash_keys(a, b, width, keys)
+    if width & (width - 1) == 0:
+        each, exact, _ = _modes(shim, a, b, width, keys)
+        np.testing.assert_array_equal(exact, ref)
+        np.testing.assert_array_equal(each, ref)
+    q = np.zeros((keys.size, a.size), np.int32)
+    w = np.zeros((keys.size, a.size), np.int32)
+    vp = ctypes.c_void_p
+    shim.host_buckets_wb(a.ctypes.data_as(vp), b.ctypes.data_as(vp), a.size, width, keys.ctypes.data_as(vp),
+                         ctypes.c_int64(keys.size), q.ctypes.data_as(vp), w.ctypes.data_as(vp))
+    np.testing.assert_array_equal(w, ref)
+    np.testing.assert_array_equal(q, ref)
