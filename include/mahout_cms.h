@@ -269,6 +269,25 @@ int cms_estimate_preferences(cms_handle* h, int64_t user_id, const int64_t* neig
 int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
                                    const int64_t* neighbor_ids, const int64_t* item_offsets, const int64_t* item_keys,
                                    int32_t use_capper, float cap_min, float cap_max, float* out);
+/* GenericUserBasedRecommender.recommend(userID, how_many) for n users at
+ * once (GenericUserBasedRecommender.java:84-105), replacing one
+ * Recommender.recommend call per user.  The caller supplies each user's
+ * neighbourhood (nb_offsets / neighbor_ids: IDs in NearestNUserNeighborhood
+ * order, e.g. from cms_top_k_all) and the DataModel's item IDs per user
+ * (model_user_ids ascending; row r's items pref_items[pref_offsets[r] ..
+ * pref_offsets[r + 1]) in getPreferencesFromUser order).  Per user: the
+ * candidates are getAllOtherItems (:187-198) in FastIDSet iteration order,
+ * their estimates come from one cms_estimate_preferences_batch over all
+ * users, and the list is TopItems.getTopItems (TopItems.java:47-88) with the
+ * JDK PriorityQueue's order for ties.  out_counts[n] (<= how_many, 0 for an
+ * empty neighbourhood), out_items / out_values [n][how_many] (float values,
+ * as RecommendedItem.getValue()).  A user or neighbour missing from the model
+ * is CMS_E_NO_SUCH_ID (NoSuchUserException). */
+int cms_recommend_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
+                        const int64_t* neighbor_ids, int64_t n_model_users, const int64_t* model_user_ids,
+                        const int64_t* pref_offsets, const int64_t* pref_items, int32_t how_many,
+                        int32_t include_known, int32_t use_capper, float cap_min, float cap_max, int32_t* out_counts,
+                        int64_t* out_items, float* out_values);
 /* GenericUserBasedRecommender.mostSimilarUserIDs(id, k) with the CosineCM
  * estimator (:119-127, :231-247) and TopItems.getTopUsers (TopItems.java:91-136):
  * the first k other owners under (similarity desc, ID asc), NaN excluded.

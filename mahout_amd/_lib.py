@@ -44,7 +44,7 @@ EXPORTS = [
     "cms_create_per_owner", "cms_configure_owner_shapes", "cms_set_owner_delta_epsilon", "cms_get_owner_shapes",
     "cms_read_owner_sketch", "cms_finalize_with", "cms_write_similarities", "cms_write_similarities_threshold",
     "cms_comm_init_transport", "cms_read_counters_device", "cms_owner_forms", "cms_estimate_preferences_batch", "cms_top_k_refresh", "cms_refresh_stats", "cms_refresh_classes",
-    "cms_top_k_all_device", "cms_top_k_refresh_device", "cms_set_hash_params",
+    "cms_top_k_all_device", "cms_top_k_refresh_device", "cms_set_hash_params", "cms_recommend_batch",
 ]
 
 
@@ -157,6 +157,8 @@ _SIGS = {
     "cms_owner_forms": (_int, [_vp, _i64, _i64, _vp, _vp]),
     "cms_estimate_preferences_batch": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _int, ctypes.c_float, ctypes.c_float,
                                               _vp]),
+    "cms_recommend_batch": (_int, [_vp, _i64, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i32, _i32, _int, ctypes.c_float,
+                                   ctypes.c_float, _vp, _vp, _vp]),
     "cms_write_similarities": (_int, [_vp, ctypes.c_char_p, _i32, _i32]),
     "cms_write_similarities_threshold": (_int, [_vp, ctypes.c_char_p, _i32, _i32, ctypes.c_double]),
     "cms_configure_owner_shapes": (_int, [_vp, _dbl, _i64]),

@@ -7,7 +7,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmahout_cms.so")
-SOURCES = ["cms_api.hip", "cms_ingest.hip", "cms_build.hip", "cms_partition.hip", "cms_query.hip", "cms_topk.hip", "cms_cosine_mfma.hip", "cms_cosine_sym.hip", "cms_cosine_mls.hip", "cms_profiles.hip", "cms_merge.hip", "cms_table.hip", "cms_f64.hip", "cms_output.cpp"]
+SOURCES = ["cms_api.hip", "cms_ingest.hip", "cms_build.hip", "cms_partition.hip", "cms_query.hip", "cms_topk.hip", "cms_cosine_mfma.hip", "cms_cosine_sym.hip", "cms_cosine_mls.hip", "cms_profiles.hip", "cms_merge.hip", "cms_table.hip", "cms_f64.hip", "cms_output.cpp", "cms_recommend.cpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-ffp-contract=off",
          "-mcode-object-version=5", "-Wall", "-Wno-unused-function", "-I/opt/rocm/include"]
 

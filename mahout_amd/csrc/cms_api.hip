@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <thread>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1159,6 +1160,73 @@ int cms_estimate_preferences_batch(cms_handle* h, int64_t n, const int64_t* user
                           item_keys + item_offsets[u], item_offsets[u + 1] - item_offsets[u], use_capper, cap_min,
                           cap_max, out + item_offsets[u], h->stream, tmp, false)))
       return rc;
+  return CMS_OK;
+}
+
+int cms_recommend_batch(cms_handle* h, int64_t n, const int64_t* user_ids, const int64_t* nb_offsets,
+                        const int64_t* neighbor_ids, int64_t n_model_users, const int64_t* model_user_ids,
+                        const int64_t* pref_offsets, const int64_t* pref_items, int32_t how_many,
+                        int32_t include_known, int32_t use_capper, float cap_min, float cap_max, int32_t* out_counts,
+                        int64_t* out_items, float* out_values) {
+  if (!h || n < 0 || n_model_users < 0 || (n > 0 && (!user_ids || !nb_offsets || !out_counts || !out_items ||
+                                                     !out_values)) ||
+      (n_model_users > 0 && (!model_user_ids || !pref_offsets)))
+    return set_error(CMS_E_PARAM, "null argument");
+  if (how_many < 1) return set_error(CMS_E_PARAM, "howMany must be at least 1");
+  if (n == 0) return CMS_OK;
+  if (nb_offsets[0] != 0) return set_error(CMS_E_PARAM, "nb_offsets must start at 0");
+  for (int64_t u = 0; u < n; ++u)
+    if (nb_offsets[u + 1] < nb_offsets[u]) return set_error(CMS_E_PARAM, "nb_offsets must not decrease");
+  if (nb_offsets[n] > 0 && !neighbor_ids) return set_error(CMS_E_PARAM, "null argument");
+  if (n_model_users > 0) {
+    if (pref_offsets[0] != 0) return set_error(CMS_E_PARAM, "pref_offsets must start at 0");
+    for (int64_t r = 0; r < n_model_users; ++r) {
+      if (pref_offsets[r + 1] < pref_offsets[r]) return set_error(CMS_E_PARAM, "pref_offsets must not decrease");
+      if (r > 0 && model_user_ids[r] <= model_user_ids[r - 1])
+        return set_error(CMS_E_PARAM, "model_user_ids must be strictly ascending");
+    }
+    if (pref_offsets[n_model_users] > 0 && !pref_items) return set_error(CMS_E_PARAM, "null argument");
+  }
+  const int64_t* mb = model_user_ids;
+  const int64_t* me = model_user_ids + n_model_users;
+  auto model_row = [&](int64_t id) -> int64_t {
+    const int64_t* it = std::lower_bound(mb, me, id);
+    return it != me && *it == id ? it - mb : -1;
+  };
+  // neighbourhood rows in the model (a neighbour the model lacks would throw
+  // NoSuchUserException from getItemIDsFromUser)
+  std::vector<int64_t> nb_rows((size_t)nb_offsets[n]);
+  std::vector<int64_t> user_rows((size_t)n);
+  for (int64_t u = 0; u < n; ++u) {
+    const bool empty = nb_offsets[u + 1] == nb_offsets[u];
+    user_rows[(size_t)u] = model_row(user_ids[u]);
+    if (!empty && !include_known && user_rows[(size_t)u] < 0)
+      return set_error(CMS_E_NO_SUCH_ID, "no such user ID %lld in the data model", (long long)user_ids[u]);
+    for (int64_t j = nb_offsets[u]; j < nb_offsets[u + 1]; ++j)
+      if ((nb_rows[(size_t)j] = model_row(neighbor_ids[j])) < 0)
+        return set_error(CMS_E_NO_SUCH_ID, "no such user ID %lld in the data model", (long long)neighbor_ids[j]);
+  }
+  // candidates per user (host threads), then one concatenated estimate batch
+  std::vector<std::vector<int64_t>> cand((size_t)n);
+  const int threads = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  parallel_users(n, threads, [&](int64_t u) {
+    if (nb_offsets[u + 1] == nb_offsets[u]) return;  // recommend(): an empty neighbourhood recommends nothing
+    recommend_candidates(nb_rows.data() + nb_offsets[u], nb_offsets[u + 1] - nb_offsets[u], user_rows[(size_t)u],
+                         pref_offsets, pref_items, include_known != 0, cand[(size_t)u]);
+  });
+  std::vector<int64_t> it_off((size_t)n + 1, 0);
+  for (int64_t u = 0; u < n; ++u) it_off[(size_t)u + 1] = it_off[(size_t)u] + (int64_t)cand[(size_t)u].size();
+  std::vector<int64_t> keys((size_t)it_off[(size_t)n]);
+  for (int64_t u = 0; u < n; ++u) std::copy(cand[(size_t)u].begin(), cand[(size_t)u].end(), keys.begin() + it_off[(size_t)u]);
+  std::vector<float> est(keys.size());
+  if (int rc = cms_estimate_preferences_batch(h, n, user_ids, nb_offsets, neighbor_ids, it_off.data(), keys.data(),
+                                              use_capper, cap_min, cap_max, est.data()))
+    return rc;
+  parallel_users(n, threads, [&](int64_t u) {
+    const int64_t o = it_off[(size_t)u];
+    out_counts[u] = recommend_top_items(how_many, keys.data() + o, est.data() + o, it_off[(size_t)u + 1] - o,
+                                        out_items + u * (int64_t)how_many, out_values + u * (int64_t)how_many);
+  });
   return CMS_OK;
 }
 

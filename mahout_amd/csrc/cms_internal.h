@@ -628,6 +628,13 @@ int f64_estimate_preferences(cms_handle* h, int64_t user_row, const int64_t* d_n
                              float* d_out, hipStream_t s);
 // ---- cms_output.cpp ----
 int java_double_to_string(double v, char* out, int cap);
+// cms_recommend.cpp: GenericUserBasedRecommender's host logic (FastIDSet
+// candidates, TopItems.getTopItems) around the device estimates
+void recommend_candidates(const int64_t* nb_rows, int64_t m, int64_t user_row, const int64_t* pref_offsets,
+                          const int64_t* pref_items, bool include_known, std::vector<int64_t>& out);
+int32_t recommend_top_items(int32_t how_many, const int64_t* items, const float* est, int64_t q, int64_t* out_items,
+                            float* out_values);
+void parallel_users(int64_t n, int threads, const std::function<void(int64_t)>& fn);
 int write_similar_items(cms_handle* h, const char* path, int32_t k, int32_t as_float);
 int write_similarities(cms_handle* h, const char* path, int32_t k, int32_t format, double threshold);
 // ---- cms_cosine_sym.hip: symmetric all-pairs waves, 256 x 192 tiles ----

@@ -320,6 +320,38 @@ class SketchTable:
                                                        _ptr(out)))
         return out
 
+    def recommend_batch(self, user_ids, nb_offsets, neighbor_ids, model_user_ids, pref_offsets, pref_items,
+                        how_many, include_known=False, capper=None):
+        """cms_recommend_batch: GenericUserBasedRecommender.recommend for every
+        user of user_ids at once. User u's neighbourhood is
+        neighbor_ids[nb_offsets[u]:nb_offsets[u+1]] (IDs); the DataModel is
+        model_user_ids (ascending) with row r's item IDs
+        pref_items[pref_offsets[r]:pref_offsets[r+1]]. Returns (counts [n],
+        items [n][how_many], values [n][how_many] float32)."""
+        us = np.ascontiguousarray(user_ids, np.int64)
+        nbo = np.ascontiguousarray(nb_offsets, np.int64)
+        nb = np.ascontiguousarray(neighbor_ids, np.int64)
+        mu = np.ascontiguousarray(model_user_ids, np.int64)
+        po = np.ascontiguousarray(pref_offsets, np.int64)
+        pi = np.ascontiguousarray(pref_items, np.int64)
+        # the library reads every array up to its last offset: they must match
+        if nbo.size != us.size + 1 or nbo[0] != 0 or nbo[-1] != nb.size or bool(np.any(np.diff(nbo) < 0)):
+            raise ValueError("nb_offsets must hold len(user_ids) + 1 non-decreasing entries from 0 to len(neighbor_ids)")
+        if po.size != mu.size + 1 or po[0] != 0 or po[-1] != pi.size or bool(np.any(np.diff(po) < 0)):
+            raise ValueError("pref_offsets must hold len(model_user_ids) + 1 non-decreasing entries from 0 to "
+                             "len(pref_items)")
+        if how_many < 1:
+            raise ValueError("howMany must be at least 1")
+        counts = np.zeros(us.size, np.int32)
+        items = np.full((us.size, how_many), -1, np.int64)
+        vals = np.full((us.size, how_many), np.nan, np.float32)
+        lo, hi = capper if capper is not None else (0.0, 0.0)
+        check(self._lib.cms_recommend_batch(self._h, us.size, _ptr(us), _ptr(nbo), _ptr(nb), mu.size, _ptr(mu),
+                                            _ptr(po), _ptr(pi), int(how_many), int(bool(include_known)),
+                                            int(capper is not None), float(lo), float(hi), _ptr(counts),
+                                            _ptr(items), _ptr(vals)))
+        return counts, items, vals
+
     def write_similar_items(self, path, k, as_float=True):
         """cms_top_k_all in FileSimilarItemsWriter's CSV format."""
         check(self._lib.cms_write_similar_items(self._h, os.fsencode(path), int(k), int(as_float)))

@@ -258,6 +258,25 @@ class NearestNUserNeighborhood:
     def getUserNeighborhood(self, userID):
         return self._sim.mostSimilarUserIDs(userID, self.n)
 
+    def getUserNeighborhoods(self, userIDs):
+        """getUserNeighborhood for many users: (offsets, neighbour IDs) from
+        one all-owners top-n pass (cms_top_k_all: the same lists as
+        mostSimilarUserIDs, each unordered pair scored once)."""
+        table = self._sim.table
+        ids, _, cnt = table.top_k_all(self.n)
+        owners = self._model.getUserIDs()
+        users = np.ascontiguousarray(userIDs, np.int64)
+        rows = np.searchsorted(owners, users)
+        if np.any(rows >= owners.size) or np.any(owners[np.minimum(rows, owners.size - 1)] != users):
+            bad = users[(rows >= owners.size) | (owners[np.minimum(rows, owners.size - 1)] != users)][0]
+            raise NoSuchUserException(int(bad))
+        c = cnt[rows].astype(np.int64)
+        off = np.zeros(users.size + 1, np.int64)
+        np.cumsum(c, out=off[1:])
+        sel = ids[rows]
+        nb = sel[np.arange(self.n)[None, :] < c[:, None]]
+        return off, np.ascontiguousarray(nb, np.int64)
+
 
 class GenericUserBasedRecommender:
     """GenericUserBasedRecommender(model, neighborhood, CosineCM): the
@@ -304,6 +323,39 @@ class GenericUserBasedRecommender:
         for k in keys.tolist():
             s.add(k)
         return s
+
+    def _model_csr(self):
+        """The DataModel as (user IDs ascending, offsets, item IDs in
+        getPreferencesFromUser order), built once."""
+        if getattr(self, "_csr", None) is None:
+            m = self._model
+            if all(hasattr(m, a) for a in ("user_ids", "offsets", "keys")):
+                self._csr = (m.user_ids, m.offsets, m.keys)
+            else:
+                uids = np.asarray(m.getUserIDs(), np.int64)
+                parts = [np.asarray(m.getPreferencesFromUser(int(u))[0], np.int64) for u in uids]
+                off = np.zeros(uids.size + 1, np.int64)
+                np.cumsum([p.size for p in parts], out=off[1:])
+                self._csr = (uids, off, np.concatenate(parts) if parts else np.zeros(0, np.int64))
+        return self._csr
+
+    def recommend_all(self, userIDs, howMany, includeKnownItems=False):
+        """recommend(userID, howMany) for every user of userIDs in one native
+        call (cms_recommend_batch): the neighbourhoods from one all-owners
+        top-n pass, the candidates in FastIDSet order and TopItems.getTopItems
+        on the host side of the library, every estimate in one device batch.
+        Returns one [(itemID, float value)] list per user, equal to recommend()."""
+        if howMany < 1:
+            raise ValueError("howMany must be at least 1")
+        users = np.ascontiguousarray(userIDs, np.int64)
+        nb_off, nb = self._nb.getUserNeighborhoods(users)
+        mu, po, pi = self._model_csr()
+        try:
+            cnt, items, vals = self._sim.table.recommend_batch(users, nb_off, nb, mu, po, pi, howMany,
+                                                               includeKnownItems, self._capper)
+        except _lib.CmsError as e:
+            raise _map_error(e, "user")
+        return [[(int(items[u, j]), vals[u, j]) for j in range(int(cnt[u]))] for u in range(users.size)]
 
     def recommend(self, userID, howMany, includeKnownItems=False):
         """recommend(userID, howMany) (GenericUserBasedRecommender.java:84-105):

@@ -98,3 +98,41 @@ def test_estimate_batch_equals_single_calls(oracle):
             for j, u in enumerate(users.tolist()):
                 one = t.estimate_preferences(u, nbs[j], its[j], cap)
                 assert np.array_equal(got[it_off[j]:it_off[j + 1]], one, equal_nan=True), (counter, u)
+
+
+@pytest.mark.parametrize("counters", ["u32", "f64"])
+def test_recommend_all_equals_recommend_for_every_user(counters):
+    """GenericUserBasedRecommender.recommend_all (cms_recommend_batch: the
+    neighbourhoods from one top-n pass, FastIDSet candidates and
+    TopItems.getTopItems in the library, every estimate in one device batch)
+    gives, for ALL 943 users, exactly the lists of the per-user recommend()
+    path that test_recommend_equals_oracle pins against the oracle: items in
+    the same order (ties included) and the same float values. The same path
+    is what bench.py's config1.recommender times."""
+    model, rows, items, ratings = _model()
+    uid = model.getUserIDs()
+    if counters == "f64":  # non-dyadic preferences: DoubleCountMinSketch's fp64 counters (taste.counter_units)
+        model = GenericDataModel.from_csr(uid, model.offsets, model.keys, model.values * np.float32(0.3))
+    sim = taste.CosineCM(model, taste.FixedShapeConfig(D, W), taste.HashFunctionBuilder(SEED))
+    assert sim.table.counters == counters
+    try:
+        nbh = taste.NearestNUserNeighborhood(NN, sim, model)
+        rec = taste.GenericUserBasedRecommender(model, nbh, sim)
+        users = uid if counters == "u32" else uid[::9]
+        got = rec.recommend_all(users, HOW)
+        assert len(got) == users.size
+        ties = 0
+        for u, lst in zip(users.tolist(), got):
+            want = rec.recommend(u, HOW)
+            assert [i for i, _ in lst] == [i for i, _ in want], u
+            assert [float(v) for _, v in lst] == [float(v) for _, v in want], u
+            vals = [float(v) for _, v in want]
+            ties += len(vals) - len(set(vals))
+        assert ties > 0  # capped estimates tie: the tie order was exercised
+        # includeKnownItems keeps the user's own items among the candidates
+        sub = users[:25]
+        got_k = rec.recommend_all(sub, HOW, includeKnownItems=True)
+        for u, lst in zip(sub.tolist(), got_k):
+            assert lst == rec.recommend(u, HOW, includeKnownItems=True), u
+    finally:
+        sim.close()
