@@ -431,77 +431,49 @@ def config1_recommender(nn=50, how_many=10, reps=5):
     ID, d=4, w=1024), NearestNUserNeighborhood(50) and the CosineCM
     point-query estimate with EstimatedPreferenceCapper
     (GenericUserBasedRecommender.java:84-184, NearestNUserNeighborhood.java:
-    84-95).  GPU: every user's neighbourhood in one cms_top_k_all, the
-    candidates (the neighbours' items minus the user's own) from the
-    incidence matrix, every candidate's estimate in one
-    cms_estimate_preferences_batch, the top 10 per user (candidate sets and
-    the selection as device tensor ops); timed end to end (host glue
-    included) over `reps` runs after a warm-up.  CPU beside it:
-    oracle/cms_baseline.c orc_recommend_par (prebuilt fp64 sketches, the same
-    neighbourhood / candidates / estimates) on all the run's threads and on
-    one.  The tie order among equal estimates follows FastIDSet in the
-    reference; this leg orders ties by item ID (the -m gpu test
-    tests/test_gpu_recommender.py checks exact lists with the FastIDSet
-    restatement)."""
+    84-95).  GPU: the package's mahout_amd.taste.GenericUserBasedRecommender
+    .recommend_all -- every neighbourhood from one cms_top_k_all, then
+    cms_recommend_batch (FastIDSet candidates and TopItems.getTopItems with
+    the JDK heap's tie order in the library, every estimate in one device
+    batch); timed end to end over `reps` runs after a warm-up.  The same call
+    is checked list for list against per-user recommend() for all 943 users by
+    tests/test_gpu_recommender.py::test_recommend_all_equals_recommend_for_every_user.
+    CPU beside it: oracle/cms_baseline.c orc_recommend_par (prebuilt fp64
+    sketches, the same neighbourhood / candidates / estimates) on all the
+    run's threads and on one."""
     from oracle import oracle as O
-    from mahout_amd import SketchTable
+    from mahout_amd import taste
+    from mahout_amd.datamodel import GenericDataModel
     from mahout_amd.synth import movielens_like, to_csr
     users, items, ratings = movielens_like()
     uid, iid = np.unique(users), np.unique(items)
     ur, ir = np.searchsorted(uid, users), np.searchsorted(iid, items)
     nu, ni, d, w = uid.size, iid.size, 4, 1024
+    order = np.lexsort((items, ur))  # GenericDataModel: each user's preferences by item ID
+    moff = np.zeros(nu + 1, np.int64)
+    np.cumsum(np.bincount(ur, minlength=nu), out=moff[1:])
+    model = GenericDataModel.from_csr(uid, moff, items[order], ratings[order])
     cap = (float(ratings.min()), float(ratings.max()))
-    inc = np.zeros((nu, ni), np.float32)
-    inc[ur, ir] = 1.0
     out = {"workload": f"GenericUserBasedRecommender.recommend(user, {how_many}) for all {nu} users of the "
                        f"ML-100K-shaped stand-in ({users.size} ratings, {ni} items), NearestNUserNeighborhood({nn}), "
                        f"CosineCM d={d} w={w} point-query estimates, EstimatedPreferenceCapper{cap}",
-           "users": nu}
-    with SketchTable(nu, depth=d, width=w, seed=42, owner_ids=uid) as t:
-        t.ingest(users, items, ratings)
-        t.finalize()
-
-        dev = torch.device("cuda")
-        inc_d = torch.from_numpy(inc).to(dev)  # the model's incidence matrix, resident like the table
-
-        def run():
-            ids, _, cnt = t.top_k_all(nn)  # every user's neighbourhood (NearestNUserNeighborhood order)
-            valid = np.arange(nn)[None, :] < cnt[:, None]
-            nb = ids[valid]
-            cnt_d = torch.from_numpy(cnt).to(dev)
-            adj = torch.zeros((nu, nu), device=dev)
-            rows_d = torch.repeat_interleave(torch.arange(nu, device=dev), cnt_d.long())
-            adj[rows_d, torch.from_numpy(np.searchsorted(uid, nb)).to(dev)] = 1.0
-            cand = ((adj @ inc_d) > 0) & (inc_d == 0)  # getAllOtherItems (counts <= nn: exact in fp32)
-            cu, ci = torch.nonzero(cand, as_tuple=True)  # row-major: each user's items ascending
-            it_off = torch.zeros(nu + 1, dtype=torch.int64, device=dev)
-            it_off[1:] = torch.cumsum(torch.bincount(cu, minlength=nu), 0)
-            nb_off = np.zeros(nu + 1, np.int64)
-            np.cumsum(cnt, out=nb_off[1:])
-            ci_h = ci.cpu().numpy()
-            est = t.estimate_preferences_batch(uid, nb_off, nb, it_off.cpu().numpy(), iid[ci_h], cap)
-            # TopItems.getTopItems: the how_many best values per user (NaN out),
-            # ties by item ID: two stable sorts on the device
-            e = torch.from_numpy(est).to(dev)
-            ok = ~torch.isnan(e)
-            e, u, i = e[ok], cu[ok], ci[ok]
-            o1 = torch.sort(-e, stable=True).indices
-            o2 = torch.sort(u[o1], stable=True).indices
-            order = o1[o2]
-            u, i, e = u[order], i[order], e[order]
-            first = torch.searchsorted(u, torch.arange(nu, device=dev))
-            keep = (torch.arange(u.numel(), device=dev) - first[u]) < how_many
-            return int(ci_h.size), u[keep].cpu().numpy(), iid[i[keep].cpu().numpy()], e[keep].cpu().numpy()
-
-        run()
+           "users": nu, "path": "mahout_amd.taste.GenericUserBasedRecommender.recommend_all (cms_top_k_all + "
+                                "cms_recommend_batch)"}
+    sim = taste.CosineCM(model, taste.FixedShapeConfig(d, w), taste.HashFunctionBuilder(42))
+    try:
+        rec = taste.GenericUserBasedRecommender(model, taste.NearestNUserNeighborhood(nn, sim, model), sim)
+        rec.recommend_all(uid, how_many)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            q, ru, ritems, rvals = run()
+            lists = rec.recommend_all(uid, how_many)
         dt = (time.perf_counter() - t0) / reps
-    out["gpu"] = {"all_users_s": dt, "users_per_s": nu / dt, "candidate_estimates": q,
-                  "estimates_per_s": q / dt, "recommended_checksum": float(rvals.astype(np.float64).sum()),
-                  "full_lists": int((np.bincount(ru, minlength=nu) == how_many).sum())}
+    finally:
+        sim.close()
+    rvals = np.array([float(v) for lst in lists for _, v in lst], np.float64)
+    out["gpu"] = {"all_users_s": dt, "users_per_s": nu / dt,
+                  "recommended_checksum": float(rvals.sum()),
+                  "full_lists": int(sum(len(lst) == how_many for lst in lists))}
     a, b = O.hash_params(42, d)
     table = O.build_table(nu, d, w, a, b, ur, items, ratings)
     off, keys_idx, _ = to_csr(ur, ir, nu, ratings)
@@ -521,6 +493,9 @@ def config1_recommender(nn=50, how_many=10, reps=5):
     out["cpu_threads"] = T
     out["cpu_note"] = BASELINE_NOTE
     out["vs_cpu_all_threads"] = out["gpu"]["users_per_s"] / cpu[f"efficient_{T}t"]["users_per_s"]
+    # the recommended value multisets agree (tied items may differ only in ID order on the CPU side)
+    cs_all = cpu[f"efficient_{T}t"]["recommended_checksum"]  # the all-users leg
+    out["checksum_equal"] = bool(abs(out["gpu"]["recommended_checksum"] - cs_all) <= 1e-9 * max(1.0, abs(cs_all)))
     return out
 
 
@@ -1430,6 +1405,9 @@ def summary(res):
         if po.get("all_pairs"):
             out["cfg2_per_owner_all_pairs_s"] = _r(po["all_pairs"].get("s"))
             out["cfg2_per_owner_ordered_pairs_per_s"] = _r(po["all_pairs"].get("ordered_pairs_per_s"))
+    rc1 = ((res.get("config1") or {}).get("recommender") or {})
+    if rc1.get("gpu"):
+        out["cfg1_recommend_all_users_s"] = _r(rc1["gpu"].get("all_users_s"))
     if res.get("cpu_baseline"):
         out["cfg3_cpu_updates_per_s"] = _r(res["cpu_baseline"].get("value"))
     if res.get("merge"):
