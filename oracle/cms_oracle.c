@@ -6,6 +6,7 @@
  *
  * "T/" = /root/reference/mr/src/main/java/org/apache/mahout/cf/taste/
  */
+#define _GNU_SOURCE 1 /* qsort_r */
 #include "cms_oracle.h"
 
 #include <float.h>
@@ -437,4 +438,147 @@ int64_t orc_build_rows_reuse(const int64_t* offsets, const int64_t* keys, const 
   free(sk);
   if (checksum) *checksum = acc;
   return updates;
+}
+
+/* ---- per-owner shapes at scale (CosineCM.userSimilarity, CosineCM.java:83-96) ----
+ * userSimilarity(u1, u2) for Q query owners u1 against EVERY owner u2 of a
+ * CSR with unit increments (vals NULL): u1's sketch built at u2's (w, d)
+ * (exportProfile with u2's delta/epsilon, :41-58) against u2's own sketch.
+ * Both rows are taken sparsely, as (bucket, count) runs in ascending bucket
+ * order: the dense sums of orc_sketch_cosine add +0.0 for every other bucket,
+ * which changes no partial sum (see orc_cosine_queries_csr), so the result is
+ * orc_cosine_cm's on the dense rows bit for bit -- without materialising
+ * rows of up to millions of counters per pair.  The owners are grouped by
+ * shape so each query is hashed once per (w, d) class.  w[u2] == 0 (no
+ * configuration) gives NaN.  out[q * n + u2]; OpenMP over the classes. */
+typedef struct { int32_t bucket; int32_t count; } orc_run;
+
+static int cmp_i32(const void* x, const void* y) {
+  const int32_t a = *(const int32_t*)x, b = *(const int32_t*)y;
+  return a < b ? -1 : a > b;
+}
+
+/* sorted runs of the buckets of keys[0..m) in sketch row (a, b, w); returns the run count */
+static int64_t sparse_row(const int64_t* keys, int64_t m, int64_t a, int64_t b, int32_t w, int32_t* scratch,
+                          orc_run* runs) {
+  for (int64_t i = 0; i < m; i++) scratch[i] = orc_hash(a, b, w, keys[i]);
+  qsort(scratch, (size_t)m, sizeof(int32_t), cmp_i32);
+  int64_t nr = 0;
+  for (int64_t i = 0; i < m; i++) {
+    if (nr > 0 && runs[nr - 1].bucket == scratch[i]) runs[nr - 1].count++;
+    else { runs[nr].bucket = scratch[i]; runs[nr].count = 1; nr++; }
+  }
+  return nr;
+}
+
+static int cmp_shape_idx(const void* x, const void* y, void* ctx) {
+  const int32_t* w = ((const int32_t**)ctx)[0];
+  const int32_t* d = ((const int32_t**)ctx)[1];
+  const int64_t i = *(const int64_t*)x, j = *(const int64_t*)y;
+  if (w[i] != w[j]) return w[i] < w[j] ? -1 : 1;
+  if (d[i] != d[j]) return d[i] < d[j] ? -1 : 1;
+  return i < j ? -1 : i > j;
+}
+
+void orc_per_owner_rows_csr(const int64_t* off, const int64_t* keys, int64_t n, const int32_t* shape_w,
+                            const int32_t* shape_d, const int64_t* a, const int64_t* b, const int64_t* queries,
+                            int64_t Q, int32_t threads, double* out) {
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  for (int64_t i = 0; i < n; i++) order[i] = i;
+  const int32_t* ctx[2] = {shape_w, shape_d};
+  qsort_r(order, (size_t)n, sizeof(int64_t), cmp_shape_idx, ctx);
+  /* class boundaries */
+  int64_t* cls = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n + 1));
+  int64_t nc = 0;
+  for (int64_t i = 0; i < n; i++)
+    if (i == 0 || shape_w[order[i]] != shape_w[order[i - 1]] || shape_d[order[i]] != shape_d[order[i - 1]])
+      cls[nc++] = i;
+  cls[nc] = n;
+  int64_t qmax = 1, mmax = 1;
+  for (int64_t q = 0; q < Q; q++) {
+    const int64_t m = off[queries[q] + 1] - off[queries[q]];
+    if (m > qmax) qmax = m;
+  }
+  for (int64_t i = 0; i < n; i++)
+    if (off[i + 1] - off[i] > mmax) mmax = off[i + 1] - off[i];
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
+  {
+    const int64_t big = qmax > mmax ? qmax : mmax;
+    int32_t* scratch = (int32_t*)malloc(sizeof(int32_t) * (size_t)big);
+    orc_run* mr = (orc_run*)malloc(sizeof(orc_run) * (size_t)mmax);
+    /* each query's runs for every sketch row of the class: [Q][d][qmax] */
+    orc_run* qr = NULL;
+    int64_t* qn = NULL;
+    double* qa = NULL;
+    int32_t qd_cap = 0;
+#pragma omp for schedule(dynamic, 1)
+    for (int64_t c = 0; c < nc; c++) {
+      const int64_t first = order[cls[c]];
+      const int32_t w = shape_w[first], d = shape_d[first];
+      if (w <= 0 || d <= 0) {
+        for (int64_t t = cls[c]; t < cls[c + 1]; t++)
+          for (int64_t q = 0; q < Q; q++) out[q * n + order[t]] = NAN;
+        continue;
+      }
+      if (d > qd_cap) {
+        free(qr);
+        free(qn);
+        free(qa);
+        qd_cap = d;
+        qr = (orc_run*)malloc(sizeof(orc_run) * (size_t)(Q * d * qmax));
+        qn = (int64_t*)malloc(sizeof(int64_t) * (size_t)(Q * d));
+        qa = (double*)malloc(sizeof(double) * (size_t)(Q * d));
+      }
+      for (int64_t q = 0; q < Q; q++) {
+        const int64_t u1 = queries[q];
+        for (int32_t r = 0; r < d; r++) {
+          orc_run* runs = qr + (q * d + r) * qmax;
+          const int64_t nr = sparse_row(keys + off[u1], off[u1 + 1] - off[u1], a[r], b[r], w, scratch, runs);
+          qn[q * d + r] = nr;
+          double v = 0.0;
+          for (int64_t t = 0; t < nr; t++) v += (double)runs[t].count * (double)runs[t].count;
+          qa[q * d + r] = v;
+        }
+      }
+      for (int64_t t = cls[c]; t < cls[c + 1]; t++) {
+        const int64_t u2 = order[t];
+        double mins[64];
+        for (int64_t q = 0; q < Q && q < 64; q++) mins[q] = DBL_MAX;
+        for (int32_t r = 0; r < d; r++) {
+          const int64_t nr = sparse_row(keys + off[u2], off[u2 + 1] - off[u2], a[r], b[r], w, scratch, mr);
+          double vb = 0.0;
+          for (int64_t s = 0; s < nr; s++) vb += (double)mr[s].count * (double)mr[s].count;
+          for (int64_t q = 0; q < Q && q < 64; q++) {
+            const orc_run* ra = qr + (q * d + r) * qmax;
+            const int64_t na = qn[q * d + r];
+            double ab = 0.0;
+            int64_t i = 0, j = 0;
+            while (i < na && j < nr) {
+              if (ra[i].bucket < mr[j].bucket) i++;
+              else if (ra[i].bucket > mr[j].bucket) j++;
+              else {
+                ab += (double)ra[i].count * (double)mr[j].count;
+                i++;
+                j++;
+              }
+            }
+            const double den = sqrt(qa[q * d + r]) * sqrt(vb);
+            if (den != 0) mins[q] = java_min(mins[q], ab / den);
+          }
+        }
+        for (int64_t q = 0; q < Q && q < 64; q++) {
+          double res = mins[q] == DBL_MAX ? NAN : mins[q];
+          if (!isnan(res)) res = orc_normalize_weight_result(res, 1, 0, 0);
+          out[q * n + u2] = res;
+        }
+      }
+    }
+    free(scratch);
+    free(mr);
+    free(qr);
+    free(qn);
+    free(qa);
+  }
+  free(order);
+  free(cls);
 }

@@ -119,6 +119,14 @@ int64_t orc_build_rows_reuse(const int64_t* offsets, const int64_t* keys, const 
                              int64_t row_lo, int64_t row_hi, int32_t depth, int32_t width,
                              const int64_t* a, const int64_t* b, double* checksum);
 
+/* CosineCM.userSimilarity(u1, u2) (CosineCM.java:83-96) of Q <= 64 query
+ * owners against every owner of a unit-increment CSR, each pair at u2's
+ * per-owner shape (w, d); sparse rows, bit-identical to orc_cosine_cm on the
+ * dense rows.  out[q * n + u2]. */
+void orc_per_owner_rows_csr(const int64_t* off, const int64_t* keys, int64_t n, const int32_t* shape_w,
+                            const int32_t* shape_d, const int64_t* a, const int64_t* b, const int64_t* queries,
+                            int64_t Q, int32_t threads, double* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,8 @@ def _load():
         "orc_recommend_par": (c.c_int64, [_f64p, c.c_int64, c.c_int32, c.c_int32, _i64p, _i64p, _i64p, _i32p, _i64p,
                                           c.c_int64, c.c_int32, c.c_int32, c.c_int32, c.c_float, c.c_float, c.c_int64,
                                           c.c_int64, c.c_int32, c.POINTER(c.c_double)]),
+        "orc_per_owner_rows_csr": (None, [_i64p, _i64p, c.c_int64, _i32p, _i32p, _i64p, _i64p, _i64p, c.c_int64,
+                                          c.c_int32, _f64p]),
         "orc_cosine_queries_csr": (None, [_f64p, c.c_int64, _i64p, _i64p, c.c_void_p, c.c_int64, c.c_int32, c.c_int32,
                                           _i64p, _i64p, c.c_int, c.c_int32, _f64p]),
     }
@@ -263,6 +265,23 @@ def per_owner_similarity(offsets, keys, vals, shapes, a, b, u1, u2, weighted=Fal
     s1 = export_profile(offsets, keys, vals, u1, w, d, a, b)
     s2 = export_profile(offsets, keys, vals, u2, w, d, a, b)
     return cosine_cm(s1, s2, weighted)
+
+
+def per_owner_rows_csr(offsets, keys, shapes, a, b, queries, threads=16):
+    """per_owner_similarity(offsets, keys, None, shapes, a, b, u1, u2) for
+    every u1 in queries (<= 64) and EVERY owner u2 (sparse rows, grouped by
+    shape; orc_per_owner_rows_csr): [len(queries)][n] float64."""
+    off = np.ascontiguousarray(offsets, np.int64)
+    n = off.size - 1
+    q = np.ascontiguousarray(queries, np.int64)
+    if q.size > 64:
+        raise ValueError("at most 64 queries per call")
+    out = np.zeros((q.size, n), np.float64)
+    lib().orc_per_owner_rows_csr(off, np.ascontiguousarray(keys, np.int64), n,
+                                 np.ascontiguousarray(shapes[0], np.int32), np.ascontiguousarray(shapes[1], np.int32),
+                                 np.ascontiguousarray(a, np.int64), np.ascontiguousarray(b, np.int64), q, q.size,
+                                 int(threads), out)
+    return out
 
 
 # ---- CPU baselines (oracle/cms_baseline.c; bench.py's cpu_baseline legs) ----

@@ -57,3 +57,27 @@ def test_row0_bound_is_an_upper_bound(oracle, seed):
             checked += 1
             tight += ub == sim
     assert checked > 300 and tight > 0  # (collision-free rows make it exact)
+
+
+def test_sparse_per_owner_rows_equal_dense_oracle(oracle):
+    """oracle.per_owner_rows_csr (the sparse, shape-grouped restatement the
+    bench-scale per-owner GPU test checks against) equals the dense
+    per_owner_similarity bit for bit, including a missing shape (w = 0: NaN)."""
+    from mahout_amd.synth import zipf_stream, to_csr
+    items, users = zipf_stream(5000, 300, 30000, seed=5)
+    off, keys, _ = to_csr(items, users, 300)
+    rng = np.random.default_rng(1)
+    n = 300
+    w = rng.choice([7, 64, 100, 1024, 3001], n).astype(np.int32)
+    d = rng.integers(1, 9, n).astype(np.int32)
+    w[5] = 0
+    a, b = oracle.hash_params(42, 32)
+    qs = np.array([0, 3, 150, 299])
+    got = oracle.per_owner_rows_csr(off, keys, (w, d), a, b, qs, threads=4)
+    for qi, q in enumerate(qs):
+        for u2 in range(n):
+            if w[u2] == 0:
+                assert np.isnan(got[qi, u2])
+                continue
+            e = oracle.per_owner_similarity(off, keys, None, (w, d), a, b, int(q), u2)
+            assert (np.isnan(e) and np.isnan(got[qi, u2])) or e == got[qi, u2], (q, u2)
