@@ -1365,7 +1365,8 @@ template <int D>
 __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* lo_, const int64_t* hi_, Keys keys,
                                                                 HashParams hp, int64_t slice, const HotInfo* hot,
                                                                 const int2* smap, const uint32_t* counters,
-                                                                TableView tv, uint64_t* row_mass, uint32_t* flags) {
+                                                                TableView tv, uint64_t* row_mass, uint32_t* flags,
+                                                                uint16_t* img_out) {
   extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] words, two u16 counters each
   const uint32_t nsl = counters[1];
   if (blockIdx.x >= nsl) return;
@@ -1375,7 +1376,8 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
   // it divides the count) so the ones running together belong to many owners
   // and their row adds do not all land on one 160 KB slot row at once
   const uint32_t stride = (nsl % 7919u) ? 7919u : 7907u;
-  const int2 m = smap[(uint32_t)(((uint64_t)blockIdx.x * stride) % nsl)];
+  const uint32_t sidx = (uint32_t)(((uint64_t)blockIdx.x * stride) % nsl);  // the mapped slice (its image index)
+  const int2 m = smap[sidx];
   const int64_t row = hot[m.x].row;
   const int64_t lo = lo_[row] + (int64_t)m.y * slice;
   const int64_t end = min(hi_[row], lo + slice);
@@ -1420,6 +1422,18 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
     }
   }
   __syncthreads();
+  if (img_out) {
+    // the slice's image leaves whole, as u16 counters with 16-B non-temporal
+    // stores; k_slice_reduce sums an owner's images into its slot row (no
+    // global atomics here)
+    u32x4_t* o4 = reinterpret_cast<u32x4_t*>(img_out + (int64_t)sidx * dw);
+    const uint4* s4 = reinterpret_cast<const uint4*>(lds);
+    for (int j = tid; j < (words >> 2); j += kSliceThreads) {
+      const uint4 v = s4[j];
+      const u32x4_t x = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(x, o4 + j);
+    }
+  } else {
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(tv.hot + (int64_t)tv.hidx[row] * dw);
   // the slices of one owner start their sweep at different 512-B-aligned
   // offsets of the slot row (same-address atomics from many workgroups queue)
@@ -1432,6 +1446,7 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
     if (v == 0xFFFFFFFFu)
 #endif
     if (v) atomicAdd(dst + j, (unsigned long long)(v & 0xFFFFu) | ((unsigned long long)(v >> 16) << 32));
+  }
   }
   if (tid == 0) {
     const uint64_t tm = (uint64_t)(end - lo) * one;
@@ -1446,13 +1461,16 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
 // Norms and maxima of the hot (u32 slot) rows: one workgroup per (row,
 // sketch row) at a time, the whole w counters in 16-byte loads (eight in
 // flight per thread at w = 8192), one block reduction per sketch row.
+// done_ns > 0: rows of at most done_ns slices already have their norms
+// (k_slice_reduce stored them whole) and are skipped.
 __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uint32_t* counters, HashParams hp,
-                                                   TableView tv, uint64_t* norm, uint32_t* rowmax) {
+                                                   TableView tv, uint64_t* norm, uint32_t* rowmax, int done_ns) {
   __shared__ uint64_t red[4];
   const uint32_t nhot = counters[0];
   const int d = blockIdx.y;
   const int w = (int)hp.width;
   for (uint32_t hb = blockIdx.x; hb < nhot; hb += gridDim.x) {
+    if (hot[hb].nslices <= done_ns) continue;  // (uniform per block)
     const int64_t row = hot[hb].row;
     const uint32_t* p = tv.hot + (int64_t)tv.hidx[row] * tv.dw + (int64_t)d * w;  // split rows are slots
     uint64_t sq = 0;
@@ -1477,6 +1495,106 @@ __global__ __launch_bounds__(256) void k_hot_norms(const HotInfo* hot, const uin
     uint64_t tot = block_sum_u64_sat(sq, red);
     if (tot > (1ULL << 60)) tot = 1ULL << 60;
     if (threadIdx.x == 0) atomicAdd((unsigned long long*)&norm[row * hp.depth + d], (unsigned long long)tot);
+  }
+}
+
+// The split owners' slot rows from their slices' u16 images (k_build_slices
+// with img_out; Tunables::slice_reduce).  Task = (group of kRedGroup slices of
+// one owner, chunk of 2048 counters): thread t sums 8 counters (one 16-B load
+// per slice, four in flight) over the group's slices.  An owner of at most
+// kRedGroup slices (nearly all: a split owner has a few) is one group per
+// chunk, so its counters are stored whole -- the old ones added when
+// accumulating -- and the same pass derives its rows' sums of squares and
+// largest counter (k_hot_norms then skips it).  A Zipf head owner (hundreds of
+// slices) has many groups, each adding its sums into the pre-zeroed (or old)
+// slot with 64-bit atomics, two counters per add (no carry: every sum stays
+// below the row mass < 2^32); k_hot_norms derives those rows' norms.
+constexpr int kRedGroup = 16, kRedChunk = 2048;
+__global__ __launch_bounds__(256) void k_slice_reduce(const HotInfo* hot, const int2* smap, const uint32_t* counters,
+                                                      const uint16_t* img, HashParams hp, TableView tv, int accumulate,
+                                                      uint64_t* norm, uint32_t* rowmax) {
+  const uint32_t nsl = counters[1];
+  const int64_t dw = tv.dw;
+  const int w = (int)hp.width;
+  const int nchunk = (int)((dw + kRedChunk - 1) / kRedChunk);
+  const int lane = threadIdx.x & 63;
+  for (int64_t t = blockIdx.x; t < (int64_t)nsl * nchunk; t += gridDim.x) {
+    const uint32_t e = (uint32_t)(t / nchunk);
+    const int ch = (int)(t - (int64_t)e * nchunk);
+    const int2 m = smap[e];
+    if (m.y % kRedGroup) continue;  // not a group's first slice (uniform per block)
+    const HotInfo hi = hot[m.x];
+    const int s1 = min(hi.nslices, m.y + kRedGroup);
+    const int64_t j0 = (int64_t)ch * kRedChunk + (int64_t)threadIdx.x * 8;  // this thread's 8 counters
+    const bool in = j0 < dw;
+    uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto add = [&](const u32x4_t v) {
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        s[2 * c] += x[c] & 0xFFFFu;
+        s[2 * c + 1] += x[c] >> 16;
+      }
+    };
+    if (in) {
+      const uint16_t* base = img + (int64_t)hi.e0 * dw + j0;
+      auto src = [&](int sl) { return reinterpret_cast<const u32x4_t*>(base + (int64_t)sl * dw); };
+      int sl = m.y;
+      for (; sl + 3 < s1; sl += 4) {
+        const u32x4_t a = __builtin_nontemporal_load(src(sl)), b = __builtin_nontemporal_load(src(sl + 1));
+        const u32x4_t c = __builtin_nontemporal_load(src(sl + 2)), f = __builtin_nontemporal_load(src(sl + 3));
+        add(a);
+        add(b);
+        add(c);
+        add(f);
+      }
+      for (; sl < s1; ++sl) add(__builtin_nontemporal_load(src(sl)));
+    }
+    uint32_t* dst = tv.hot + (int64_t)tv.hidx[hi.row] * dw + j0;
+    if (hi.nslices > kRedGroup) {  // several groups: add into the slot
+      if (in) {
+        unsigned long long* d2 = reinterpret_cast<unsigned long long*>(dst);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (s[2 * c] | s[2 * c + 1])
+            atomicAdd(d2 + c, (unsigned long long)s[2 * c] | ((unsigned long long)s[2 * c + 1] << 32));
+      }
+      continue;
+    }
+    uint64_t sq = 0;
+    uint32_t vmax = 0;
+    if (in) {
+      uint4* d4 = reinterpret_cast<uint4*>(dst);
+      if (accumulate) {
+        const uint4 a = d4[0], b = d4[1];
+        s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+        s[4] += b.x; s[5] += b.y; s[6] += b.z; s[7] += b.w;
+      }
+      d4[0] = make_uint4(s[0], s[1], s[2], s[3]);
+      d4[1] = make_uint4(s[4], s[5], s[6], s[7]);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        sq = sat_add(sq, (uint64_t)s[c] * s[c]);
+        vmax = max(vmax, s[c]);
+      }
+    }
+    // the wave's 512 counters lie in one sketch row when w is a multiple of
+    // 512 (config 3); otherwise each lane adds its own (w % 8 == 0: a
+    // thread's 8 counters never straddle two rows)
+    const int r = in ? (int)(j0 / w) : -1;
+    const int r0 = __builtin_amdgcn_readfirstlane(r);
+    if (__ballot(r != r0) == 0ULL) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+      sq = wave_sum_u64_sat(sq);
+      if (lane == 0 && r0 >= 0) {
+        if (vmax) atomicMax(&rowmax[hi.row], vmax);
+        if (sq) atomicAdd((unsigned long long*)&norm[hi.row * hp.depth + r0], (unsigned long long)(sq > (1ULL << 60) ? (1ULL << 60) : sq));
+      }
+    } else if (in) {
+      if (vmax) atomicMax(&rowmax[hi.row], vmax);
+      if (sq) atomicAdd((unsigned long long*)&norm[hi.row * hp.depth + r], (unsigned long long)(sq > (1ULL << 60) ? (1ULL << 60) : sq));
+    }
   }
 }
 
@@ -1600,11 +1718,19 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   const int64_t row_emax = fast_slices ? 0 : emax;
   const int slices_done = fast_slices ? 1 : 0;
   bool hot_norms_done = false;
+  // slice images summed by k_slice_reduce instead of global slot atomics
+  // (Tunables::slice_reduce): emax images of d*w u16 counters
+  const bool sreduce = fast_slices && h->tune.slice_reduce && (h->p.width % 8) == 0;
+  uint16_t* simg = nullptr;
+  if (sreduce) {
+    CMS_HIP(h->ws_slicepart.ensure(sizeof(uint16_t) * (size_t)emax * (size_t)h->dw));
+    simg = h->ws_slicepart.as<uint16_t>();
+  }
   auto launch_hot_norms = [&]() -> int {
     TimedScope ts(h, "hot_norms");
     dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(max_hot, 1024)), (unsigned)h->p.depth);
     hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
-                       h->d_rowmax);
+                       h->d_rowmax, sreduce ? kRedGroup : 0);
     CMS_HIP(hipGetLastError());
     hot_norms_done = true;
     return CMS_OK;
@@ -1625,8 +1751,15 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       (void)attr;
       auto kslices = h->p.depth == 5 ? k_build_slices<5> : h->p.depth == 4 ? k_build_slices<4> : k_build_slices<0>;
       hipLaunchKernelGGL(kslices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
-                         keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags);
+                         keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags,
+                         simg);
       CMS_HIP(hipGetLastError());
+      if (sreduce) {
+        TimedScope ts(h, "slice_reduce");
+        hipLaunchKernelGGL(k_slice_reduce, dim3((unsigned)((int64_t)h->num_cus * 8)), dim3(256), 0, h->stream, hot,
+                           extra_map, counters, simg, h->hp, h->tview(), accumulate, h->d_norm, h->d_rowmax);
+        CMS_HIP(hipGetLastError());
+      }
       return CMS_OK;
     };
     if (forms) {

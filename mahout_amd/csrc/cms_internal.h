@@ -213,6 +213,7 @@ struct Tunables {
   int po_no_prune = 0;      // CMS_PO_NO_PRUNE=1: every (query, wide owner) pair through k_po_pairs (no row-0 bound)
   int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
+  int slice_reduce = 0;     // CMS_SLICE_REDUCE=1: split owners' slices leave u16 images summed by k_slice_reduce (no slot atomics)
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
   bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)
@@ -329,7 +330,7 @@ struct cms_handle {
   cms::DevBuf ws_csr_key, ws_csr_val, ws_csr_off, ws_csr_hi;
   cms::DevBuf ws_hotpart;  // hot-owner routing of the partition: slot keys [1024] u64, sample counts [n] u32
   cms::DevBuf ws_hist, ws_small, ws_partials, ws_hot;
-  cms::DevBuf ws_slicepart;  // row build: u16 [hot + extra slices][d*w] partial rows of split owners (k_hot_reduce)
+  cms::DevBuf ws_slicepart;  // row build: u16 [mapped slices][d*w] slice images of split owners (k_slice_reduce)
   cms::DevBuf ws_query, ws_query2, ws_out, ws_srow, ws_f4, ws_i8blk;
   cms::DevBuf ws_limb0, ws_limbmeta, ws_limbhot, ws_hotlist, ws_tiles, ws_slab, ws_topq, ws_nsq, ws_cand;
 

@@ -779,3 +779,48 @@ def test_multi_limb_slab_kernel_equals_reference_path(oracle):
             eids, esc = oracle.top_users(np.arange(n), sims, k)
             assert ids[q, :cnt[q]].tolist() == eids.tolist(), q
             assert same(sc[q, :cnt[q]], esc), q
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_slice_images_reduce_equals_slot_atomics(oracle, accumulate, monkeypatch):
+    """k_build_slices with CMS_SLICE_REDUCE=1 writes each 65535-key slice's
+    u16 image and k_slice_reduce sums them into the slot rows (stored whole,
+    norms and maxima derived in the same pass, for owners of <= 16 slices;
+    64-bit atomics plus k_hot_norms for the Zipf head's many-slice owners):
+    the table, the norms (through the similarities) and the row maxima equal
+    the slot-atomic path's bit for bit, in a fresh build and in an
+    accumulating one (a second bulk batch into the live table), and the
+    heaviest owners match the oracle."""
+    import torch
+    n, d, w = 4096, 5, 8192
+    rng = np.random.Generator(np.random.PCG64(21))
+    # owner 0: 1.3M keys (20 slices: two groups), owner 1: 300K (5 slices),
+    # owner 2: 70K (2 slices), owners 3..: a Zipf tail (narrow and mid rows)
+    heavy = [np.zeros(1_300_000, np.int64), np.ones(300_000, np.int64), np.full(70_000, 2, np.int64)]
+    tail_items, tail_users = zipf_stream(3_000_000, n - 3, 2_000_000, seed=8)
+    items = np.concatenate(heavy + [tail_items + 3])
+    users = np.concatenate([rng.integers(0, 5_000_000, sum(h.size for h in heavy)), tail_users]).astype(np.int64)
+    perm = rng.permutation(items.size)
+    items, users = items[perm], users[perm]
+    half = items.size // 2
+    got = {}
+    for mode in ("atomics", "reduce"):
+        monkeypatch.setenv("CMS_SLICE_REDUCE", "1" if mode == "reduce" else "0")
+        with SketchTable(n, depth=d, width=w, seed=13) as t:
+            if accumulate:
+                t.ingest(items[:half], users[:half])
+                t.ingest(items[half:], users[half:])
+            else:
+                t.ingest(items, users)
+            t.finalize()
+            got[mode] = (t.read_counters_device().cpu(),
+                         np.stack([t.similarities(q, np.arange(n)) for q in (0, 1, 2, 3, 100)]),
+                         t.stats()["hot_rows"])
+            torch.cuda.synchronize()
+    assert torch.equal(got["atomics"][0], got["reduce"][0])
+    assert same(got["atomics"][1], got["reduce"][1])
+    assert got["reduce"][2] >= 3
+    sel = np.array([0, 1, 2, 3])
+    m = np.isin(items, sel)
+    exp = oracle_table(oracle, sel.size, d, w, 13, items[m], users[m], None)
+    assert same(got["reduce"][0].numpy()[sel].astype(np.float64), exp)
