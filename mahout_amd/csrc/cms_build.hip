@@ -948,6 +948,119 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
   }
 }
 
+// Mid-class owners, one WAVE per owner (Tunables::mid_waves; unit
+// increments): k_build_nibbles' scheme at the mid class's sizes.  Each wave
+// counts one sketch row at a time in its own w-byte LDS slot -- 4-bit
+// counters first for owners of <= mid_u4_keys keys (and list-row owners),
+// else u8 -- with the returning LDS adds giving each row's sum of squares
+// and maximum, and stores the row as it finishes.  No workgroup barrier: a
+// wave's LDS operations execute in program order, so the waves of a
+// workgroup never wait on each other (k_build_mid's 256-thread owners pass
+// ~15 barriers per owner).  Keys are streamed per sketch row (L2-resident
+// after the first), the next loads in flight; hashes take bucket_q's route
+// (power-of-two widths), and an owner with a reduced key >= 2^32 goes to
+// k_build_mid.  A counter past 15 restarts the
+// owner at u8; past 255 (or more than mid_u8_keys keys) the owner is queued
+// for k_build_mid's u16 rows (redo list).
+template <int SV, int D>
+__global__ __launch_bounds__(256) void k_build_mid_waves(
+    const int64_t* lo_, const int64_t* hi_, Keys keys, HashParams hp, const int32_t* list, const uint32_t* list_cnt,
+    TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax,
+    int list_keys, int u4_keys, int u8_keys, int32_t* redo, uint32_t* redo_cnt) {
+  extern __shared__ __align__(16) uint32_t lds[];  // [4][w / 4] words: one u8 (or 4-bit) sketch row per wave
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int w = (int)hp.width;
+  const int depth = D > 0 ? D : hp.depth;
+  const int64_t dw = (int64_t)depth * w;
+  uint32_t* slot = lds + wv * (w >> 2);
+  uint4* slot4 = reinterpret_cast<uint4*>(slot);
+  const uint32_t count = *list_cnt;
+  const uint32_t nwv = gridDim.x * 4u;
+  for (uint32_t li = blockIdx.x * 4u + (uint32_t)wv; li < count; li += nwv) {
+    const int64_t row = list[li];
+    const int64_t lo = lo_[row], hi = hi_[row];
+    const int64_t m = hi - lo;
+    if (m > u8_keys) {  // starts at u16: k_build_mid
+      if (lane == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
+      continue;
+    }
+    const bool as_list = m <= list_keys && (int64_t)depth * m <= 8192 && 2 + 2 * (int64_t)depth * m < dw / 2;
+    uint16_t* lst = tv.t16 + row * dw;  // list row: [0] = m, then [d][m] buckets
+    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * dw);
+    int bits = (as_list || m <= u4_keys) ? 4 : 8;
+    uint32_t vmax = 0;
+    bool ovf = false, slow = false;  // slow: a reduced key >= 2^32 (bucket_q's route does not take it)
+    for (;;) {
+      const int lg = bits == 4 ? 3 : 2;  // log2(counters per word)
+      const uint32_t cap = (1u << bits) - 1u;
+      const int nq = (w * bits) >> 7;  // uint4 per sketch row
+      vmax = 0;
+      ovf = false;
+      for (int r = 0; r < depth; ++r) {
+        for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
+        uint32_t sq = 0;  // <= m * 255 < 2^22
+        // the owner's keys, 4 per lane per step, the next step's loads in
+        // flight (re-read per sketch row: an owner's tokens stay in L2)
+        constexpr int kAhead = 4;
+        uint64_t nx[kAhead];
+        auto fetch = [&](int64_t base) {
+#pragma unroll
+          for (int u = 0; u < kAhead; ++u) {
+            const int64_t i = base + lane + (int64_t)u * 64;
+            nx[u] = i < hi ? keys.raw(i) : 0ULL;
+          }
+        };
+        fetch(lo);
+        for (int64_t base = lo; base < hi; base += 64 * kAhead) {
+          uint64_t kk[kAhead];
+#pragma unroll
+          for (int u = 0; u < kAhead; ++u) kk[u] = nx[u];
+          if (base + 64 * kAhead < hi) fetch(base + 64 * kAhead);
+#pragma unroll
+          for (int u = 0; u < kAhead; ++u) {
+            const int64_t i = base + lane + (int64_t)u * 64;
+            const uint64_t kp = keys.resolve(kk[u]);
+            slow |= i < hi && (kp >> 32) != 0;
+            if (i < hi && (kp >> 32) == 0) {
+              const uint32_t c = bucket_q(hp, r, kp, (double)(uint32_t)kp, (uint32_t)kp & hp.wmask);
+              const uint32_t sh = (c & ((1u << lg) - 1u)) * (uint32_t)bits;
+              const uint32_t old = (atomicAdd(&slot[c >> lg], 1u << sh) >> sh) & cap;
+              ovf |= old == cap;  // the add carried into the next counter: a wider form
+              sq += 2u * old + 1u;
+              vmax = max(vmax, old + 1u);
+              if (as_list) lst[1 + (int64_t)r * m + (i - lo)] = (uint16_t)c;
+            }
+          }
+        }
+        if (__ballot(ovf | slow)) break;  // uniform: escalate (or hand the owner to k_build_mid)
+        sq = wave_sum_u32(sq);
+#ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
+        if (false)
+#endif
+        if (!as_list)
+          for (int j = lane; j < nq; j += 64) store_row(d4 + r * nq + j, slot4[j], SV);
+        if (lane == 0) norm[row * depth + r] = sq;
+      }
+      if (!__ballot(ovf) || bits == 8 || __ballot(slow)) break;
+      bits = 8;
+    }
+    if (__ballot(ovf | slow)) {  // a counter past 255 (u16 rows) or a key the quotient route does not take
+      if (lane == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
+      continue;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if (lane == 0) {
+      if (as_list) lst[0] = (uint16_t)m;
+      rowmax[row] = vmax;
+      row_mass[row] = (uint64_t)m;
+      hidx_w[row] = as_list ? kFormList : bits == 4 ? kFormU4 : kFormU8;
+      cbound[row] = vmax;
+    }
+  }
+}
+
 // Mid-class owners through ONE key pass (Tunables::mid_image, when the
 // [d][w] u16 image fits 80 KB): k_build_slices' scheme -- every sketch row
 // counted at once in a [d][w] u16 LDS image (no carry: a mid owner's mass,
@@ -1768,14 +1881,15 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       // the ones a counter >= 16 sends back) and mid rows -> k_build_mid on the
       // side stream, so the classes' kernels overlap (their tails no longer
       // leave CUs idle)
-      CMS_HIP(h->ws_blist.ensure(sizeof(int32_t) * (size_t)(2 * n + 4)));
+      CMS_HIP(h->ws_blist.ensure(sizeof(int32_t) * (size_t)(3 * n + 4)));
       int32_t* slot_list = h->ws_blist.as<int32_t>();
       int32_t* mid_list = slot_list + n;
-      uint32_t* lcnt = reinterpret_cast<uint32_t*>(mid_list + n);
+      uint32_t* lcnt = reinterpret_cast<uint32_t*>(mid_list + n);  // [0] slot rows, [1] mid rows, [2] mid redo
+      int32_t* mid_redo = mid_list + n + 4;                         // k_build_mid_waves -> k_build_mid (u16)
       CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
       int32_t* redo = h->ws_plist.as<int32_t>();
       uint32_t* redo_cnt = reinterpret_cast<uint32_t*>(redo + n);
-      CMS_HIP(hipMemsetAsync(lcnt, 0, 2 * sizeof(uint32_t), h->stream));
+      CMS_HIP(hipMemsetAsync(lcnt, 0, 3 * sizeof(uint32_t), h->stream));
       CMS_HIP(hipMemsetAsync(redo_cnt, 0, sizeof(uint32_t), h->stream));
       hipLaunchKernelGGL(k_build_classes,
                          dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kClassChunk - 1) / kClassChunk, 1024))),
@@ -1841,6 +1955,22 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                            (size_t)h->dw * 2, side, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                            (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                            h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0);
+      } else if (h->tune.mid_waves && !d_val && h->hp.frac_bits == 0 && h->hp.fastq && (h->p.width % 32) == 0 &&
+                 (size_t)h->p.width * 4 <= 64 * 1024) {
+        // one wave per mid owner (4-bit / u8 rows), then k_build_mid for the
+        // owners that need u16 rows
+        auto kmw = h->p.depth == 5   ? k_build_mid_waves<kBuildStoreForm, 5>
+                   : h->p.depth == 4 ? k_build_mid_waves<kBuildStoreForm, 4>
+                                     : k_build_mid_waves<kBuildStoreForm, 0>;
+        hipLaunchKernelGGL(kmw, dim3((unsigned)std::min<int64_t>((n + 3) / 4, (int64_t)h->num_cus * h->tune.mid_waves)),
+                           dim3(256), (size_t)h->p.width * 4, side2, d_lo, d_hi, keys, h->hp, (const int32_t*)mid_list,
+                           (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
+                           h->d_rowmax, lists_allowed(h) ? kMidListKeys : 0, h->tune.mid_u4_keys,
+                           h->tune.mid_u8_keys, mid_redo, lcnt + 2);
+        hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
+                           mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_redo,
+                           (const uint32_t*)(lcnt + 2), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
+                           h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0, 0, 0, 0);
       } else
       hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * CMS_MID_GRID_PER_CU)),
                          dim3(kBuildThreads), mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,

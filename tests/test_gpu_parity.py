@@ -824,3 +824,43 @@ def test_slice_images_reduce_equals_slot_atomics(oracle, accumulate, monkeypatch
     m = np.isin(items, sel)
     exp = oracle_table(oracle, sel.size, d, w, 13, items[m], users[m], None)
     assert same(got["reduce"][0].numpy()[sel].astype(np.float64), exp)
+
+
+def test_mid_waves_equal_mid_workgroups(oracle, monkeypatch):
+    """k_build_mid_waves (CMS_MID_WAVES: one wave per mid-class owner, 4-bit
+    then u8 rows, list rows for owners of <= 1024 keys; u16 owners and keys
+    >= 2^32 handed to k_build_mid) builds the same table, the same row forms
+    and the same norms as k_build_mid's 256-thread owners, and sampled mid
+    owners match the oracle."""
+    import torch
+    n, d, w = 20_000, 5, 8192
+    rng = np.random.Generator(np.random.PCG64(31))
+    # mid owners of 300..14000 keys with Zipf users (repeats: u8 and u16 rows),
+    # a byte-class tail, and one owner whose keys reach past 2^32
+    sizes = np.concatenate([rng.integers(300, 1100, 3000), rng.integers(1100, 14000, 1500),
+                            rng.integers(1, 200, n - 4500)])
+    items = np.repeat(np.arange(n, dtype=np.int64), sizes)
+    users = (rng.zipf(1.3, items.size) % 3_000_000).astype(np.int64)
+    big = items == 7
+    users[big] = users[big] + (1 << 33)
+    perm = rng.permutation(items.size)
+    items, users = items[perm], users[perm]
+    got = {}
+    for mode in ("workgroups", "waves"):
+        monkeypatch.setenv("CMS_MID_WAVES", "5" if mode == "waves" else "0")
+        with SketchTable(n, depth=d, width=w, seed=17) as t:
+            t.ingest(items, users)
+            t.finalize()
+            got[mode] = (t.read_counters_device().cpu(), t.owner_forms(),
+                         np.stack([t.similarities(q, np.arange(n)) for q in (0, 7, 4000, 9000)]))
+            torch.cuda.synchronize()
+    assert torch.equal(got["workgroups"][0], got["waves"][0])
+    for a, b in zip(got["workgroups"][1], got["waves"][1]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert same(got["workgroups"][2], got["waves"][2])
+    sel = np.array([0, 7, 11, 3100, 4000])
+    m = np.isin(items, sel)
+    remap = np.full(n, -1, np.int64)
+    remap[sel] = np.arange(sel.size)
+    exp = oracle_table(oracle, sel.size, d, w, 17, remap[items[m]], users[m], None)
+    assert same(got["waves"][0].numpy()[sel].astype(np.float64), exp)
