@@ -41,7 +41,7 @@ for step in $STEPS; do
         envs=()
         case "$arm" in
           main) tag=main ;;
-          env:*) envs=("${arm#env:}"); tag=$(echo "${arm#env:}" | tr '=' '_') ;;
+          env:*) IFS='+' read -r -a envs <<< "${arm#env:}"; tag=$(echo "${arm#env:}" | tr '=+' '__') ;;
           *) envs=(MAHOUT_CMS_LIB="$PWD/$arm"); tag=$(basename "$arm" .so) ;;
         esac
         env "${envs[@]}" timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras \
