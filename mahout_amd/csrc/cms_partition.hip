@@ -56,6 +56,11 @@ constexpr int kMaxBins = 4096;
 #ifndef CMS_P1_ROUNDS
 #define CMS_P1_ROUNDS 4
 #endif
+// the next tile's first round is loaded as the last round of this tile is
+// binned (before the scan, placement and write-out), not after the placement
+#ifndef CMS_PART_EARLY_NEXT
+#define CMS_PART_EARLY_NEXT 1
+#endif
 // pass-2 tile in rounds of kPartTile pairs (1, 2 or 4: a block's chunk is
 // four rounds; 4 = one 16384-pair tile per block: config-3 partition
 // 5.30-5.34 -> 5.08-5.11 ms in two A/B runs, profiles/r04/ab_*)
@@ -336,6 +341,9 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       if (u + 1 < R) load(t, u + 1, (u + 1) & 1);
+      // the last round: the next tile's first round into the other buffer
+      // (free: its round was binned), in flight through the epilogue
+      else if (CMS_PART_EARLY_NEXT && (R % 2) == 0 && t + NB < ntiles) load(t + NB, 0, 0);
       const int cb = u & 1;
 #pragma unroll
       for (int q = 0; q < kPartPer; ++q) {
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
         L.bin[p] = (uint16_t)bin;
       }
     }
-    if (t + NB < ntiles) load(t + NB, 0, 0);
+    if (!(CMS_PART_EARLY_NEXT && (R % 2) == 0) && t + NB < ntiles) load(t + NB, 0, 0);
     lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t bin = L.bin[i];
@@ -661,6 +669,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       if (u + 1 < R) load(tb + (int64_t)(u + 1) * kPartTile, (u + 1) & 1);
+      else if (CMS_PART_EARLY_NEXT && (R % 2) == 0 && tb + TILE < hi) load(tb + TILE, 0);  // (k_p1_scatter)
       const int cb = u & 1;
 #pragma unroll
       for (int q = 0; q < kPartPer; ++q) {
@@ -685,7 +694,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
         L.bin[p] = (uint16_t)f;
       }
     }
-    if (tb + TILE < hi) load(tb + TILE, 0);
+    if (!(CMS_PART_EARLY_NEXT && (R % 2) == 0) && tb + TILE < hi) load(tb + TILE, 0);
     lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t f = L.bin[i];
