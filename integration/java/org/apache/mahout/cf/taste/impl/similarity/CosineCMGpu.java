@@ -15,7 +15,9 @@
  */
 package org.apache.mahout.cf.taste.impl.similarity;
 
+import java.util.ArrayList;
 import java.util.Collection;
+import java.util.List;
 import java.util.concurrent.locks.ReentrantReadWriteLock;
 
 import org.apache.mahout.cf.taste.common.NoSuchItemException;
@@ -25,8 +27,10 @@ import org.apache.mahout.cf.taste.common.TasteException;
 import org.apache.mahout.cf.taste.common.Weighting;
 import org.apache.mahout.cf.taste.impl.common.CountMinSketchConfig;
 import org.apache.mahout.cf.taste.impl.common.LongPrimitiveIterator;
+import org.apache.mahout.cf.taste.impl.recommender.GenericRecommendedItem;
 import org.apache.mahout.cf.taste.model.DataModel;
 import org.apache.mahout.cf.taste.model.PreferenceArray;
+import org.apache.mahout.cf.taste.recommender.RecommendedItem;
 import org.apache.mahout.cf.taste.similarity.PreferenceInferrer;
 import org.apache.mahout.cf.taste.similarity.UserSimilarity;
 
@@ -48,6 +52,9 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private final long seed;
   private final boolean weighted;
   private final int device;
+  // the DataModel as built (sorted owner IDs, offsets, item IDs in
+  // getPreferencesFromUser order): recommendAll's getAllOtherItems source
+  private volatile long[][] modelCsr;
   private final long[] hashA;  // a HashFunctionBuilder's drawn (a_i, b_i), or null: drawn from seed
   private final long[] hashB;
   private volatile long handle;  // cms_handle*
@@ -192,6 +199,7 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
       }
     }
     int fracBits = counterUnits(offsets, vals);
+    modelCsr = new long[][] {ids, offsets, keys};
     long h = perOwner() ? nativeCreatePerOwner(seed, n, weighted, device, fracBits)
                         : nativeCreate(depth, width, seed, n, weighted, device, fracBits);
     try {
@@ -414,6 +422,54 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   }
 
   /**
+   * GenericUserBasedRecommender.recommend(userID, howMany) (:84-105) with
+   * NearestNUserNeighborhood(neighborhoodSize) for every user of userIDs in
+   * one call (cms_recommend_batch): the neighbourhoods from one all-owners
+   * top-n pass, the candidates in FastIDSet iteration order and
+   * TopItems.getTopItems (JDK PriorityQueue tie order) in the library, every
+   * estimate in one device batch. Pass capMin/capMax = NaN for no capper.
+   * Element u is user u's list, equal to recommend(userIDs[u], howMany).
+   */
+  public List<List<RecommendedItem>> recommendAll(long[] userIDs, int neighborhoodSize, int howMany,
+                                                  boolean includeKnownItems, float capMin, float capMax)
+      throws TasteException {
+    long h = acquire();
+    try {
+      long[][] csr = modelCsr;
+      long[][] lists = nativeTopKAll(h, neighborhoodSize);  // rows in ascending owner-ID order
+      long[] nbOffsets = new long[userIDs.length + 1];
+      for (int u = 0; u < userIDs.length; u++) {
+        int r = java.util.Arrays.binarySearch(csr[0], userIDs[u]);
+        if (r < 0) {
+          throw new NoSuchUserException(userIDs[u]);
+        }
+        nbOffsets[u + 1] = nbOffsets[u] + lists[r].length;
+      }
+      long[] nbIds = new long[(int) nbOffsets[userIDs.length]];
+      for (int u = 0; u < userIDs.length; u++) {
+        long[] nb = lists[java.util.Arrays.binarySearch(csr[0], userIDs[u])];
+        System.arraycopy(nb, 0, nbIds, (int) nbOffsets[u], nb.length);
+      }
+      int[] counts = new int[userIDs.length];
+      long[] items = new long[userIDs.length * howMany];
+      float[] values = new float[userIDs.length * howMany];
+      nativeRecommendBatch(h, userIDs, nbOffsets, nbIds, csr[0], csr[1], csr[2], howMany, includeKnownItems, capMin,
+                           capMax, counts, items, values);
+      List<List<RecommendedItem>> out = new ArrayList<>(userIDs.length);
+      for (int u = 0; u < userIDs.length; u++) {
+        List<RecommendedItem> l = new ArrayList<>(counts[u]);
+        for (int j = 0; j < counts[u]; j++) {
+          l.add(new GenericRecommendedItem(items[u * howMany + j], values[u * howMany + j]));
+        }
+        out.add(l);
+      }
+      return out;
+    } finally {
+      release();
+    }
+  }
+
+  /**
    * mostSimilarIDs for every owner at once (each unordered pair computed once):
    * row r of the result holds the IDs for the r-th owner in ascending ID order.
    */
@@ -490,6 +546,10 @@ public final class CosineCMGpu extends AbstractItemSimilarity implements UserSim
   private static native float[] nativeEstimatePreferences(long h, long user, long[] neighbors, long[] items,
                                                           float capMin, float capMax) throws TasteException;
   private static native long[][] nativeTopKAll(long h, int k) throws TasteException;
+  private static native void nativeRecommendBatch(long h, long[] users, long[] nbOffsets, long[] nbIds, long[] modelIds,
+                                                  long[] prefOffsets, long[] prefItems, int howMany,
+                                                  boolean includeKnown, float capMin, float capMax, int[] outCounts,
+                                                  long[] outItems, float[] outValues) throws TasteException;
   private static native long[][] nativeTopKRefresh(long h, int k) throws TasteException;
   private static native void nativeDestroy(long h);
 }

@@ -233,6 +233,58 @@ JNIEXPORT jfloatArray JNICALL JFN(nativeEstimatePreferences)(JNIEnv* env, jclass
   return fail(env, rc, 0) ? NULL : res;
 }
 
+/* GenericUserBasedRecommender.recommend for many users (cms_recommend_batch);
+ * the outputs are Java arrays the caller sized: counts[n], items/values
+ * [n * howMany]. */
+static int64_t* longs_of(JNIEnv* env, jlongArray a, jsize* len) {
+  *len = a ? (*env)->GetArrayLength(env, a) : 0;
+  int64_t* p = (int64_t*)malloc(sizeof(int64_t) * (size_t)(*len ? *len : 1));
+  if (p && *len) (*env)->GetLongArrayRegion(env, a, 0, *len, (jlong*)p);
+  return p;
+}
+
+JNIEXPORT void JNICALL JFN(nativeRecommendBatch)(JNIEnv* env, jclass c, jlong h, jlongArray users, jlongArray nbo,
+                                                 jlongArray nbs, jlongArray mids, jlongArray po, jlongArray pi,
+                                                 jint how_many, jboolean include_known, jfloat cap_min,
+                                                 jfloat cap_max, jintArray out_counts, jlongArray out_items,
+                                                 jfloatArray out_values) {
+  (void)c;
+  jsize n, n_nbo, n_nb, n_m, n_po, n_pi;
+  int64_t* u = longs_of(env, users, &n);
+  int64_t* o = longs_of(env, nbo, &n_nbo);
+  int64_t* nb = longs_of(env, nbs, &n_nb);
+  int64_t* m = longs_of(env, mids, &n_m);
+  int64_t* p_off = longs_of(env, po, &n_po);
+  int64_t* p_it = longs_of(env, pi, &n_pi);
+  const size_t outn = (size_t)n * (size_t)(how_many > 0 ? how_many : 1);
+  int32_t* cnt = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+  int64_t* it = (int64_t*)malloc(sizeof(int64_t) * (outn ? outn : 1));
+  float* val = (float*)malloc(sizeof(float) * (outn ? outn : 1));
+  int rc = CMS_E_OOM;
+  /* the offsets must describe exactly the arrays handed over */
+  if (u && o && nb && m && p_off && p_it && cnt && it && val) {
+    rc = (n_nbo != n + 1 || o[0] != 0 || o[n] != n_nb || n_po != n_m + 1 || p_off[0] != 0 || p_off[n_m] != n_pi)
+             ? CMS_E_PARAM
+             : cms_recommend_batch(H(h), n, u, o, nb, n_m, m, p_off, p_it, how_many, include_known,
+                                   !(cap_min != cap_min && cap_max != cap_max), cap_min, cap_max, cnt, it, val);
+  }
+  if (rc == CMS_OK) {
+    (*env)->SetIntArrayRegion(env, out_counts, 0, n, (const jint*)cnt);
+    (*env)->SetLongArrayRegion(env, out_items, 0, (jsize)outn, (const jlong*)it);
+    (*env)->SetFloatArrayRegion(env, out_values, 0, (jsize)outn, val);
+  }
+  free(u);
+  free(o);
+  free(nb);
+  free(m);
+  free(p_off);
+  free(p_it);
+  free(cnt);
+  free(it);
+  free(val);
+  fail(env, rc, 0);
+}
+
 typedef int (*top_k_fn)(cms_handle*, int32_t, int64_t*, double*, int32_t*);
 
 static jobjectArray top_k_lists(JNIEnv* env, jlong h, jint k, top_k_fn fn) {

@@ -101,11 +101,17 @@ def test_native_calls_hold_the_handle_lock():
     calls = re.findall(r"\bnative(?!Create|Destroy|SetHashParams|SetOwnerIds|IngestCsr|SetOwnerDeltaEpsilon|"
                        r"ConfigureOwnerShapes|Finalize)\w+\((\w+)", body)
     assert calls and all(c == "h" for c in calls), calls
-    # each `long h = acquire();` is followed by a try/finally release()
+    # each `long h = acquire();` is followed by a try/finally release(), and
+    # every native call on the handle lies inside one of those spans
+    spans = []
     for m in re.finditer(r"long h = acquire\(\);\s*try \{(.*?)\} finally \{\s*release\(\);", body, re.S):
         assert "native" in m.group(1)
+        spans.append((m.start(1), m.end(1)))
     assert body.count("long h = acquire();") == body.count("release();") - 0
-    assert body.count("acquire();") >= len(calls)
+    call_pos = [m.start() for m in re.finditer(r"\bnative(?!Create|Destroy|SetHashParams|SetOwnerIds|IngestCsr|"
+                                               r"SetOwnerDeltaEpsilon|ConfigureOwnerShapes|Finalize)\w+\(h\b", body)]
+    assert len(call_pos) == len(calls)
+    assert all(any(a <= c < b for a, b in spans) for c in call_pos)
     destroy = [m.start() for m in re.finditer(r"nativeDestroy\(", body)]
     wl = [m.start() for m in re.finditer(r"writeLock\(\)\.lock\(\)", body)]
     # every destroy of a live (published) handle sits after a write-lock
