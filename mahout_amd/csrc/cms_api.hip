@@ -406,6 +406,9 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
       (e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_fork2, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_join2, hipEventDisableTiming)) != hipSuccess ||
+#ifdef CMS_BUILD_GATHERHASH  // bound analysis only (cms_hash.h): the gathered table, contents unset
+      (e = hipMalloc((void**)&h->hp.gtab, sizeof(uint4) << 24)) != hipSuccess ||
+#endif
       (!per_owner && !f64 && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
       (f64 && (e = hipMalloc(&h->d_t64, 4 * tbytes)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||

@@ -28,6 +28,10 @@ namespace cms {
 #ifdef CMS_BUILD_CHEAPHASH  // bound analysis only: a trivial hash instead of the exact mod-p one
 #define bucket(hp, d, kp) ((uint32_t)(((kp) >> (d)) & (hp).wmask))
 #endif
+#ifdef CMS_BUILD_GATHERHASH  // bound analysis only: the row's bucket gathered from a per-key table
+#define bucket(hp, d, kp) \
+  ((uint32_t)(((&(hp).gtab[(kp) & 0xFFFFFFu].x)[((d) >> 1) & 3] >> (((d) & 1) << 4)) & (hp).wmask))
+#endif
 
 struct HotInfo {
   int64_t row;

@@ -50,6 +50,9 @@ struct HashParams {
   int32_t fastq;               // bucket_q applies: power-of-two width <= 2^24
   double qa[CMS_MAX_DEPTH];    // a'/p rounded to double (bucket_q)
   double qb[CMS_MAX_DEPTH];    // b'/p rounded to double
+#ifdef CMS_BUILD_GATHERHASH    // bound analysis only: [2^24] x 16 B per-key bucket table (contents unset)
+  const uint4* gtab;
+#endif
 };
 
 // The derived fields of a HashParams whose ap, bp, width and depth are set.
@@ -173,6 +176,14 @@ CMS_HD void each_bucket(const HashParams& hp, uint64_t kp, F&& f) {
     for (int r = 0; r < hp.depth; ++r) f(r, (uint32_t)((kp >> r) & hp.wmask));
   }
   return;
+#endif
+#ifdef CMS_BUILD_GATHERHASH  // bound analysis only: one 16-B gather per key instead of d mod-p hashes
+  {
+    const uint4 e = hp.gtab[kp & 0xFFFFFFu];
+    const uint32_t v[4] = {e.x, e.y, e.z, e.w};
+    for (int r = 0; r < (D > 0 ? D : hp.depth); ++r) f(r, (v[(r >> 1) & 3] >> ((r & 1) << 4)) & hp.wmask);
+    return;
+  }
 #endif
   if (D > 0) {
     if (hp.fastq && (kp >> 32) == 0) {
