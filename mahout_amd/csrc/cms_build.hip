@@ -1256,11 +1256,16 @@ __global__ __launch_bounds__(kImgThreads) void k_build_image(
 #ifndef CMS_NIB_WAVES
 #define CMS_NIB_WAVES 4
 #endif
+
 constexpr int kNibWaves = CMS_NIB_WAVES;
 // owners with at most Tunables::bit_keys (64) keys try 1-bit rows first, with
 // at most crumb_keys (256) 2-bit rows
-// One byte-class owner by one wave (k_build_nibbles).
-template <int SV>
+// One byte-class owner by one wave (k_build_nibbles).  D > 0 (the handle's
+// depth is 4 or 5): every key's d buckets are hashed up front, as d
+// independent chains (an owner here has one key or a few per lane, so one
+// row at a time left the wave waiting on each hash's fp64 dependency chain),
+// kept in registers through the row passes and the form escalations.
+template <int SV, int D>
 __device__ __forceinline__ void nib_owner(
     int64_t row, uint32_t* lds, const int64_t* lo_, const int64_t* hi_, const Keys& keys, const float* vals,
     const HashParams& hp, const int32_t* row_hot, const uint64_t* bound, const TableView& tv, int32_t* hidx_w,
@@ -1312,6 +1317,18 @@ __device__ __forceinline__ void nib_owner(
   uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's u16 slot (64-B aligned)
   uint32_t vmax = 0;
   bool ovf = false;
+  // D > 0: the first register slot's key (an owner of <= 64 keys: its only
+  // one) has its d buckets hashed up front; a row pass picks its bucket by a
+  // select chain (the row index is not a compile-time constant there)
+  uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0, b4 = 0;
+  if (D > 0 && ik[0])
+    each_bucket<D>(hp, kp[0], [&](int r, uint32_t c) {
+      if (r == 0) b0 = c;
+      else if (r == 1) b1 = c;
+      else if (r == 2) b2 = c;
+      else if (r == 3) b3 = c;
+      else b4 = c;
+    });
   for (;;) {
     const int lg = bits == 1 ? 5 : bits == 2 ? 4 : 3;  // log2(counters per 32-bit word)
     const uint32_t cap = (1u << bits) - 1u;
@@ -1324,7 +1341,9 @@ __device__ __forceinline__ void nib_owner(
 #pragma unroll
       for (int k = 0; k < kKeyRegs; ++k)
         if (ik[k]) {
-          const uint32_t c = bucket(hp, d, kp[k]);
+          const uint32_t c = (D > 0 && k == 0)
+                                 ? (d == 0 ? b0 : d == 1 ? b1 : d == 2 ? b2 : d == 3 ? b3 : b4)
+                                 : bucket(hp, d, kp[k]);
           const uint32_t sh = (c & ((1u << lg) - 1u)) * (uint32_t)bits;
           const uint32_t old = (atomicAdd(&slot[c >> lg], ik[k] << sh) >> sh) & cap;
           const uint32_t nv = old + ik[k];
@@ -1366,7 +1385,7 @@ __device__ __forceinline__ void nib_owner(
 // Grid: one owner per wave, or (Tunables::nib_persist) persistent waves that
 // take owners gw, gw + nw, ... -- a quarter of a million four-wave workgroups
 // of a few thousand cycles each can be bound by the workgroup dispatch rate.
-template <int SV>
+template <int SV, int D>
 __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_build_nibbles(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, int64_t nrows, HashParams hp,
     const int32_t* row_hot, const uint64_t* bound, TableView tv, int32_t* hidx_w, uint32_t* cbound, uint64_t* row_mass,
@@ -1375,7 +1394,7 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
   extern __shared__ __align__(16) uint32_t lds[];  // [kNibWaves][w / 8] words: one sketch row of nibbles per wave
   const int64_t nw = (int64_t)gridDim.x * kNibWaves;
   for (int64_t row = (int64_t)blockIdx.x * kNibWaves + (threadIdx.x >> 6); row < nrows; row += nw)
-    nib_owner<SV>(row, lds, lo_, hi_, keys, vals, hp, row_hot, bound, tv, hidx_w, cbound, row_mass, norm, rowmax, flags,
+    nib_owner<SV, D>(row, lds, lo_, hi_, keys, vals, hp, row_hot, bound, tv, hidx_w, cbound, row_mass, norm, rowmax, flags,
                   redo, redo_cnt, bit_keys, crumb_keys, list_keys);
 }
 
@@ -1928,7 +1947,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
         join.armed = true;
       }
       const int64_t nib_blocks = (n + kNibWaves - 1) / kNibWaves;
-      hipLaunchKernelGGL(k_build_nibbles<kBuildStoreForm>,
+      auto knib = h->tune.nib_rows_once && h->p.depth == 5   ? k_build_nibbles<kBuildStoreForm, 5>
+                  : h->tune.nib_rows_once && h->p.depth == 4 ? k_build_nibbles<kBuildStoreForm, 4>
+                                                             : k_build_nibbles<kBuildStoreForm, 0>;
+      hipLaunchKernelGGL(knib,
                          dim3((unsigned)(h->tune.nib_persist ? std::min<int64_t>(nib_blocks, (int64_t)h->num_cus * 8)
                                                              : nib_blocks)),
                          dim3(64 * kNibWaves), (size_t)kNibWaves * (size_t)h->p.width / 2, side, d_lo, d_hi, keys,

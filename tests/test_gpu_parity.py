@@ -826,6 +826,41 @@ def test_slice_images_reduce_equals_slot_atomics(oracle, accumulate, monkeypatch
     assert same(got["reduce"][0].numpy()[sel].astype(np.float64), exp)
 
 
+def test_byte_class_rows_once_equal_row_by_row(oracle, monkeypatch):
+    """k_build_nibbles with CMS_NIB_ROWS_ONCE=1 (the first key slot's d
+    buckets hashed up front, d = 5) builds the same table and forms as the
+    row-by-row hashing, on a byte-class-heavy model (list rows, 1-/2-/4-bit
+    rows, k_build_bytes escalations, keys past 2^32)."""
+    import torch
+    n, d, w = 30_000, 5, 8192
+    rng = np.random.Generator(np.random.PCG64(41))
+    sizes = rng.integers(1, 257, n)
+    items = np.repeat(np.arange(n, dtype=np.int64), sizes)
+    users = (rng.zipf(1.2, items.size) % 200_000).astype(np.int64)
+    users[items % 97 == 0] += 1 << 33
+    perm = rng.permutation(items.size)
+    items, users = items[perm], users[perm]
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CMS_NIB_ROWS_ONCE", mode)
+        with SketchTable(n, depth=d, width=w, seed=19) as t:
+            t.ingest(items, users)
+            t.finalize()
+            got[mode] = (t.read_counters_device().cpu(), t.owner_forms(),
+                         np.stack([t.similarities(q, np.arange(n)) for q in (0, 97, 5000)]))
+            torch.cuda.synchronize()
+    assert torch.equal(got["0"][0], got["1"][0])
+    for a, b in zip(got["0"][1], got["1"][1]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert same(got["0"][2], got["1"][2])
+    sel = np.array([0, 97, 5000, 29_999])
+    m = np.isin(items, sel)
+    remap = np.full(n, -1, np.int64)
+    remap[sel] = np.arange(sel.size)
+    exp = oracle_table(oracle, sel.size, d, w, 19, remap[items[m]], users[m], None)
+    assert same(got["1"][0].numpy()[sel].astype(np.float64), exp)
+
+
 def test_mid_waves_equal_mid_workgroups(oracle, monkeypatch):
     """k_build_mid_waves (CMS_MID_WAVES: one wave per mid-class owner, 4-bit
     then u8 rows, list rows for owners of <= 1024 keys; u16 owners and keys
