@@ -41,7 +41,7 @@ for step in $STEPS; do
         envs=()
         case "$arm" in
           main) tag=main ;;
-          env:*) IFS='+' read -r -a envs <<< "${arm#env:}"; tag=$(echo "${arm#env:}" | tr '=+' '__') ;;
+          env:*) IFS='+' read -r -a envs <<< "${arm#env:}"; tag=$(echo "${arm#env:}" | tr '=+/.' '____') ;;
           *) envs=(MAHOUT_CMS_LIB="$PWD/$arm"); tag=$(basename "$arm" .so) ;;
         esac
         env "${envs[@]}" timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-extras \
@@ -52,13 +52,13 @@ for step in $STEPS; do
     ktrace)
       # per-arm kernel traces of the headline ingest (isolated kernel times
       # with a CMS_BUILD_SERIAL variant); table: scripts/ktrace_table.py
-      ARMS=${ARMS:-"main $(ls ab/*.so 2>/dev/null | tr '\n' ' ')"}
+      KT_ARMS=${KT_ARMS:-${ARMS:-"main $(ls ab/*.so 2>/dev/null | tr '\n' ' ')"}}
       rm -rf gpurun_out/kt
-      for arm in $ARMS; do
+      for arm in $KT_ARMS; do
         envs=()
         case "$arm" in
           main) tag=main ;;
-          env:*) envs=("${arm#env:}"); tag=$(echo "${arm#env:}" | tr '=' '_') ;;
+          env:*) IFS='+' read -r -a envs <<< "${arm#env:}"; tag=$(echo "${arm#env:}" | tr '=+/.' '____') ;;
           *) envs=(MAHOUT_CMS_LIB="$PWD/$arm"); tag=$(basename "$arm" .so) ;;
         esac
         env "${envs[@]}" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/kt/$tag -o run --output-format csv -- \
