@@ -61,6 +61,11 @@ constexpr int kMaxBins = 4096;
 #ifndef CMS_PART_EARLY_NEXT
 #define CMS_PART_EARLY_NEXT 1
 #endif
+// pass 2: the next virtual block's first round and cursors loaded during this
+// block's last round (k_p2_scatter)
+#ifndef CMS_P2_AHEAD
+#define CMS_P2_AHEAD 1
+#endif
 // pass-2 tile in rounds of kPartTile pairs (1, 2 or 4: a block's chunk is
 // four rounds; 4 = one 16384-pair tile per block: config-3 partition
 // 5.30-5.34 -> 5.08-5.11 ms in two A/B runs, profiles/r04/ab_*)
@@ -639,37 +644,87 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
   const uint32_t nblk = blkStart[P1];
   TileLds L = carve(smem, P2, HV, false, TILE);
   const int tid = threadIdx.x;
-  // persistent over the device-side block count (k_p2_hist)
-  for (uint32_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
-  const uint32_t lb = p2_block(vb, nblk);
-  const int b = find_bin(blkStart, P1, lb);
-  for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] = O2[(int64_t)lb * P2 + f];
-  const int64_t lo = binStart[b] + (int64_t)(lb - blkStart[b]) * CH2;
-  const int64_t hi = min((int64_t)binStart[b + 1], lo + CH2);
-  for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
+  // persistent over the device-side block count (k_p2_hist).  With
+  // CMS_P2_AHEAD the next virtual block's first round and its row of
+  // cursors are loaded while this block's last round is binned, so they are
+  // in flight through this block's epilogue (a block is one tile at the
+  // default CH2: without this, every block started with two exposed loads).
+  constexpr bool kAhead = CMS_P2_AHEAD && (R % 2) == 0;
+  constexpr int kCurPer = kMaxBins / kPartThreads;  // cursor words per thread (P2 <= kMaxBins)
   uint32_t kk[2][kPartPer], ff[2][kPartPer];
   float vv[2][kPartPer];
-  auto load = [&](int64_t tb, int buf) {
+  auto load = [&](int64_t tb, int buf, int64_t end) {
 #pragma unroll
     for (int q = 0; q < kPartPer; ++q) {
       const int64_t e = tb + tid + (int64_t)q * kPartThreads;
       ff[buf][q] = 0xFFFFFFFFu;
-      if (e < hi) {
+      if (e < end) {
         ff[buf][q] = fine[e];
         kk[buf][q] = key1[e];
         if (HV) vv[buf][q] = val1[e];
       }
     }
   };
+  struct Blk {
+    uint32_t lb;
+    int b;
+    int64_t lo, hi;
+  };
+  auto block_of = [&](uint32_t vb) {
+    Blk k;
+    k.lb = p2_block(vb, nblk);
+    k.b = find_bin(blkStart, P1, k.lb);
+    k.lo = binStart[k.b] + (int64_t)(k.lb - blkStart[k.b]) * CH2;
+    k.hi = min((int64_t)binStart[k.b + 1], k.lo + CH2);
+    return k;
+  };
+  uint32_t cur[kCurPer];
+  auto load_cursors = [&](uint32_t lb) {
+#pragma unroll
+    for (int c = 0; c < kCurPer; ++c) {
+      const int f = tid + c * kPartThreads;
+      if (f < P2) cur[c] = O2[(int64_t)lb * P2 + f];
+    }
+  };
+  Blk nx{};
+  if (kAhead && blockIdx.x < nblk) {
+    nx = block_of(blockIdx.x);
+    load_cursors(nx.lb);
+    if (nx.lo < nx.hi) load(nx.lo, 0, nx.hi);
+  }
+  for (uint32_t vb = blockIdx.x; vb < nblk; vb += gridDim.x) {
+  const Blk blk = kAhead ? nx : block_of(vb);
+  const uint32_t lb = blk.lb;
+  const int b = blk.b;
+  const int64_t lo = blk.lo, hi = blk.hi;
+  if (kAhead) {
+#pragma unroll
+    for (int c = 0; c < kCurPer; ++c) {
+      const int f = tid + c * kPartThreads;
+      if (f < P2) L.cursor[f] = cur[c];
+    }
+  } else {
+    for (int f = tid; f < P2; f += kPartThreads) L.cursor[f] = O2[(int64_t)lb * P2 + f];
+  }
+  for (int f = tid; f < P2; f += kPartThreads) L.hist[f] = 0;
   uint32_t tk[NP], rf[NP];  // key token; rank << 12 | fine bin (~0: none)
   float va[HV ? NP : 1];
-  if (lo < hi) load(lo, 0);
+  if (!kAhead && lo < hi) load(lo, 0, hi);
   __syncthreads();
   for (int64_t tb = lo; tb < hi; tb += TILE) {
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      if (u + 1 < R) load(tb + (int64_t)(u + 1) * kPartTile, (u + 1) & 1);
-      else if (CMS_PART_EARLY_NEXT && (R % 2) == 0 && tb + TILE < hi) load(tb + TILE, 0);  // (k_p1_scatter)
+      if (u + 1 < R) {
+        load(tb + (int64_t)(u + 1) * kPartTile, (u + 1) & 1, hi);
+      } else if (kAhead) {
+        if (tb + TILE < hi) {
+          load(tb + TILE, 0, hi);  // the next tile of this block (k_p1_scatter)
+        } else if (vb + gridDim.x < nblk) {
+          nx = block_of(vb + gridDim.x);  // the next block's first round and cursors
+          load_cursors(nx.lb);
+          if (nx.lo < nx.hi) load(nx.lo, 0, nx.hi);
+        }
+      }
       const int cb = u & 1;
 #pragma unroll
       for (int q = 0; q < kPartPer; ++q) {
@@ -694,7 +749,7 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
         L.bin[p] = (uint16_t)f;
       }
     }
-    if (!(CMS_PART_EARLY_NEXT && (R % 2) == 0) && tb + TILE < hi) load(tb + TILE, 0);
+    if (!kAhead && tb + TILE < hi) load(tb + TILE, 0, hi);
     lds_barrier();
     for (uint32_t i = tid; i < cnt; i += kPartThreads) {
       uint32_t f = L.bin[i];
@@ -716,7 +771,12 @@ __global__ __launch_bounds__(kPartThreads) void k_p2_scatter(const uint16_t* fin
     }
     lds_barrier();
   }
-  __syncthreads();  // this block's LDS use ends before the next block's cursors load
+  if (kAhead && lo >= hi && vb + gridDim.x < nblk) {  // an empty block had no last round
+    nx = block_of(vb + gridDim.x);
+    load_cursors(nx.lb);
+    if (nx.lo < nx.hi) load(nx.lo, 0, nx.hi);
+  }
+  __syncthreads();  // this block's LDS use ends before the next block's cursors are stored
   }
 }
 
