@@ -109,7 +109,7 @@ __device__ __forceinline__ void sym_tile(SymArgs g, int bx) {
   using AccT = typename AccOf<FMT>::type;
   // NW waves in (NW/2) x 2; a wave holds TI x 3 MFMA tiles (TI = 2 at 8 waves;
   // 3 at 4 waves: one wave per SIMD with 512 registers, 6 fragments per 9 MFMAs)
-  constexpr int NT = 64 * NW, TI = kSA / (NW / 2) / 32, WROWS = 32 * TI, NAW = (TI * 48 + 31) / 32;
+  constexpr int TI = kSA / (NW / 2) / 32, WROWS = 32 * TI, NAW = (TI * 48 + 31) / 32;
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   constexpr int kStageA = kSA * BK, kStageB = kSB * BK, kStage = kStageA + kStageB;
   constexpr int RPI = 1024 / BK;                 // rows per 1-KiB LDS-DMA instruction

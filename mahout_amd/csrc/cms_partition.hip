@@ -63,6 +63,9 @@ constexpr int kMaxBins = 4096;
 #endif
 // pass 2: the next virtual block's first round and cursors loaded during this
 // block's last round (k_p2_scatter)
+#ifndef CMS_P1_NT
+#define CMS_P1_NT 0
+#endif
 #ifndef CMS_P2_AHEAD
 #define CMS_P2_AHEAD 1
 #endif
@@ -332,9 +335,15 @@ __global__ __launch_bounds__(kPartThreads) void k_p1_scatter(const int64_t* row,
       const int64_t e = tb + tid + (int64_t)q * kPartThreads;
       rr[buf][q] = -1;
       if (e < n) {
+#if CMS_P1_NT  // the stream read once: non-temporal loads (the runs' partial lines keep L2)
+        rr[buf][q] = __builtin_nontemporal_load(row + e);
+        kk[buf][q] = __builtin_nontemporal_load(key + e);
+        if (HV) vv[buf][q] = __builtin_nontemporal_load(val + e);
+#else
         rr[buf][q] = row[e];
         kk[buf][q] = key[e];
         if (HV) vv[buf][q] = val[e];
+#endif
       }
     }
   };
