@@ -576,6 +576,10 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 #define CMS_MID_LIST_KEYS (kBuildThreads * kKeyRegs)
 #endif
 constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
+// the row passes of owners past the register cache prefetch their keys a step ahead
+#ifndef CMS_MID_ROW_PREFETCH
+#define CMS_MID_ROW_PREFETCH 1
+#endif
 template <int SV, int D>
 // 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
 // (it spilled there); the build measured the same (profiles/r04/ab_*_s5)
@@ -889,13 +893,37 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
           for (int k = 0; k < kKeyRegs; ++k)
             if (ik[k]) add(kp[k], ik[k]);
         } else {
-          for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
-            uint64_t kk[4];
-            uint32_t inc4[4];
+#if CMS_MID_ROW_PREFETCH
+          // the next step's key loads go out before this step's keys are
+          // added (the 4-bit pass's scheme; every row pass re-reads the keys)
+          constexpr int64_t kStep = 4 * kBuildThreads;
+          uint64_t nx[4];
+          auto fetch = [&](int64_t base) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+              nx[u] = i < hi ? keys.raw(i) : 0ULL;
+            }
+          };
+          fetch(lo);
+#endif
+          for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
+            uint64_t kk[4];
+            uint32_t inc4[4];
+#if CMS_MID_ROW_PREFETCH
+            uint64_t raw[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) raw[u] = nx[u];
+            if (base + kStep < hi) fetch(base + kStep);
+#endif
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+#if CMS_MID_ROW_PREFETCH
+              kk[u] = i < hi ? keys.resolve(raw[u]) : 0;
+#else
               kk[u] = i < hi ? keys.at(i) : 0;
+#endif
               inc4[u] = 0;
               if (i < hi) {
                 uint32_t inc;
