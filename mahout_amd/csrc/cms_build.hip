@@ -576,9 +576,10 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
 #define CMS_MID_LIST_KEYS (kBuildThreads * kKeyRegs)
 #endif
 constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
-// the row passes of owners past the register cache prefetch their keys a step ahead
+// the row passes of owners past the register cache prefetch their keys a step
+// ahead (measured slower: build scope 5.32 vs 5.11 ms, profiles/r06/ab)
 #ifndef CMS_MID_ROW_PREFETCH
-#define CMS_MID_ROW_PREFETCH 1
+#define CMS_MID_ROW_PREFETCH 0
 #endif
 template <int SV, int D>
 // 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
