@@ -1524,6 +1524,11 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
 // dense slice images added into the slots.  No static LDS: two 80 KB images
 // share a CU at d = 5, w = 8192.
 constexpr int kSliceThreads = 512;
+// a fresh build's single-slice owners store their slot rows whole (no slot
+// zeroing, no 64-bit slot atomics; norms from the same pass)
+#ifndef CMS_WHOLE_SLICES
+#define CMS_WHOLE_SLICES 1
+#endif
 constexpr int64_t kHotSlice = 65535;  // keys per slice (u16 image, frac_bits 0)
 // D: the depth when it is 4 or 5 (rows unrolled, each_bucket), else 0
 template <int D>
@@ -1531,7 +1536,8 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
                                                                 HashParams hp, int64_t slice, const HotInfo* hot,
                                                                 const int2* smap, const uint32_t* counters,
                                                                 TableView tv, uint64_t* row_mass, uint32_t* flags,
-                                                                uint16_t* img_out) {
+                                                                uint16_t* img_out, int whole, uint64_t* norm,
+                                                                uint32_t* rowmax) {
   extern __shared__ __align__(16) uint32_t lds[];  // [d * w / 2] words, two u16 counters each
   const uint32_t nsl = counters[1];
   if (blockIdx.x >= nsl) return;
@@ -1587,7 +1593,32 @@ __global__ __launch_bounds__(kSliceThreads) void k_build_slices(const int64_t* l
     }
   }
   __syncthreads();
-  if (img_out) {
+  if (whole && hot[m.x].nslices == 1) {
+    // the owner's only slice, in a fresh build: its slot row is the image
+    // itself (the slot was not zeroed), stored whole as u32 counters with
+    // 16-B non-temporal stores; its sums of squares and largest counter come
+    // from the same pass (k_hot_norms skips it)
+    u32x4_t* o4 = reinterpret_cast<u32x4_t*>(tv.hot + (int64_t)tv.hidx[row] * dw);
+    const uint2* s2 = reinterpret_cast<const uint2*>(lds);
+    uint32_t vmax = 0;
+    for (int r = 0; r < hp.depth; ++r) {
+      uint64_t sq = 0;
+      const int q0 = r * (w >> 2), q1 = q0 + (w >> 2);  // uint4 of u32 counters (4 per) of sketch row r
+      for (int q = q0 + tid; q < q1; q += kSliceThreads) {
+        const uint2 v = s2[q];  // four u16 counters
+        const uint32_t c0 = v.x & 0xFFFFu, c1 = v.x >> 16, c2 = v.y & 0xFFFFu, c3 = v.y >> 16;
+        sq += (uint64_t)c0 * c0 + (uint64_t)c1 * c1 + (uint64_t)c2 * c2 + (uint64_t)c3 * c3;
+        vmax = max(max(vmax, max(c0, c1)), max(c2, c3));
+        const u32x4_t x = {c0, c1, c2, c3};
+        __builtin_nontemporal_store(x, o4 + q);
+      }
+      sq = wave_sum_u64_sat(sq);  // (no static LDS: two 80 KB images share a CU)
+      if ((tid & 63) == 0 && sq) atomicAdd((unsigned long long*)&norm[row * hp.depth + r], (unsigned long long)sq);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) vmax = max(vmax, (uint32_t)__shfl_xor((int)vmax, o, 64));
+    if ((tid & 63) == 0 && vmax) atomicMax(&rowmax[row], vmax);
+  } else if (img_out) {
     // the slice's image leaves whole, as u16 counters with 16-B non-temporal
     // stores; k_slice_reduce sums an owner's images into its slot row (no
     // global atomics here)
@@ -1792,6 +1823,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   // 19.4 -> 18.5 ms; config 2 prefers 8192).
   int64_t kSplit = cms::kSlice;
   if (h->p.width >= 8192) kSplit *= 2;
+  if (h->tune.split_keys > 0) kSplit = h->tune.split_keys;
   // Unit increments whose [d][w] u16 image fits a workgroup's LDS: the
   // slices (every one, slice 0 included) run on k_build_slices, kHotSlice
   // keys each, one key pass.  Otherwise (weighted increments, wide shapes)
@@ -1799,6 +1831,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   const size_t img_lds = (size_t)h->dw * 2;
   const bool fast_slices = !d_val && (h->dw % 8) == 0 && img_lds <= 80 * 1024 && h->hp.frac_bits < 16;
   const int64_t kSliceKeys = fast_slices ? (kHotSlice >> h->hp.frac_bits) : kSplit;
+  // a fresh build: single-slice owners store their slot rows whole
+  // (k_build_slices), so their slots are not zeroed by the promotion
+  const int whole_slices =
+      CMS_WHOLE_SLICES && fast_slices && !accumulate && !h->tune.slice_reduce && (h->p.width % 4) == 0 ? 1 : 0;
   const int64_t max_hot = std::min<int64_t>(n, npairs / kSplit + 1);
   const int64_t emax = npairs / kSliceKeys + max_hot + 1;  // mapped slices
   const size_t sz_rowhot = (sizeof(int32_t) * (size_t)n + 15) & ~size_t(15);
@@ -1859,7 +1895,11 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       const int64_t slots = (int64_t(1) << (16 - h->hp.frac_bits)) > kSplit ? split : split + heavy;
       if ((double)slots * (double)h->dw * 4.0 <= 2.0e9) max_new = slots;
     }
-    if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0, max_new))) return rc0;
+    // a fresh build's single-slice owners store their slot rows whole
+    // (k_build_slices): their slots are not zeroed first
+    const uint64_t whole_bound = whole_slices ? (uint64_t)kSliceKeys << h->hp.frac_bits : 0;
+    if ((rc0 = promote_rows(h, bound.as<uint64_t>(), force.as<uint8_t>(), accumulate != 0, max_new, whole_bound)))
+      return rc0;
     // accumulating: every touched u8 / nibble row becomes u16 first (the build
     // adds into u16 or u32 rows); untouched rows are skipped by the build when
     // their norms are current, otherwise every form row is widened
@@ -1895,7 +1935,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     TimedScope ts(h, "hot_norms");
     dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(max_hot, 1024)), (unsigned)h->p.depth);
     hipLaunchKernelGGL(k_hot_norms, grid, dim3(256), 0, h->stream, hot, counters, h->hp, h->tview(), h->d_norm,
-                       h->d_rowmax, sreduce ? kRedGroup : 0);
+                       h->d_rowmax, sreduce ? kRedGroup : whole_slices);
     CMS_HIP(hipGetLastError());
     hot_norms_done = true;
     return CMS_OK;
@@ -1917,7 +1957,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       auto kslices = h->p.depth == 5 ? k_build_slices<5> : h->p.depth == 4 ? k_build_slices<4> : k_build_slices<0>;
       hipLaunchKernelGGL(kslices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
                          keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags,
-                         simg);
+                         simg, whole_slices, h->d_norm, h->d_rowmax);
       CMS_HIP(hipGetLastError());
       if (sreduce) {
         TimedScope ts(h, "slice_reduce");

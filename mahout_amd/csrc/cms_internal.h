@@ -214,6 +214,7 @@ struct Tunables {
   int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
   int nib_rows_once = 0;    // CMS_NIB_ROWS_ONCE=1: a byte-class wave hashes its first key slot's d rows up front (d = 4 or 5)
+  int split_keys = 0;       // CMS_SPLIT_KEYS: rows with more keys get a u32 slot and k_build_slices (0: 8192, 16384 at w >= 8192)
   int mid_waves = 0;        // CMS_MID_WAVES=<k>: mid owners one wave each (k_build_mid_waves), k persistent 4-wave workgroups per CU; 0: k_build_mid
   int slice_reduce = 0;     // CMS_SLICE_REDUCE=1: split owners' slices leave u16 images summed by k_slice_reduce (no slot atomics)
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
@@ -445,7 +446,8 @@ int local_norms(cms_handle* h);
 // slot is zeroed).  bound may be null when only force is used.
 // max_new >= 0: a proven bound on the rows this call can promote (no host
 // round trip: that many slots are reserved and claimed on the device).
-int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new = -1);
+int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new = -1,
+                 uint64_t whole_bound = 0);
 // rows holding a u32 slot (synchronises the stream)
 int count_hot_rows(cms_handle* h, int64_t* out);
 // rows per storage form: [0] hot, [1] u16, [2] u8, [3] nibble (synchronises)

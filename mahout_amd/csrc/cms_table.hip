@@ -37,15 +37,20 @@ __global__ void k_promote_list(const uint64_t* bound, const uint8_t* force, int3
 }
 
 // one workgroup per promoted row: slot base + i, old narrow counters copied
-// (or zeros); dcount != nullptr: the list length is read on the device
+// (or zeros); dcount != nullptr: the list length is read on the device.
+// whole_bound > 0 (a fresh build whose single-slice owners store their rows
+// whole, k_build_slices): rows of bound <= whole_bound are not zeroed.
 __global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64_t count, const uint32_t* dcount,
-                                                      int64_t base, TableView tv, int32_t* hidx, int copy_old) {
+                                                      int64_t base, TableView tv, int32_t* hidx, int copy_old,
+                                                      const uint64_t* bound, uint64_t whole_bound) {
   if (dcount) count = min<int64_t>(count, (int64_t)*dcount);
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int64_t r = list[i];
     const int64_t slot = base + i;
     uint32_t* dst = tv.hot + slot * tv.dw;
-    for (int64_t j = threadIdx.x; j < tv.dw; j += 256) dst[j] = copy_old ? tv.get(r, j) : 0u;  // any narrow form
+    const bool skip = !copy_old && whole_bound > 0 && bound && bound[r] <= whole_bound;
+    if (!skip)
+      for (int64_t j = threadIdx.x; j < tv.dw; j += 256) dst[j] = copy_old ? tv.get(r, j) : 0u;  // any narrow form
     __syncthreads();  // every lane has read the row through its old form before the form changes
     if (threadIdx.x == 0) hidx[r] = (int32_t)slot;
   }
@@ -69,7 +74,8 @@ static int grow_hot(cms_handle* h, int64_t need) {
   return CMS_OK;
 }
 
-int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new) {
+int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new,
+                 uint64_t whole_bound) {
   const int64_t n = h->n;
   CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
   int32_t* list = h->ws_plist.as<int32_t>();
@@ -81,14 +87,14 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
     // Unclaimed reserved slots stay unused until the next layout reset.
     max_new = std::min<int64_t>(max_new, n);
     if (max_new == 0) return CMS_OK;
-    if (h->hot_used + max_new > n) return promote_rows(h, d_bound, d_force, copy_old, -1);  // reservations spent
+    if (h->hot_used + max_new > n) return promote_rows(h, d_bound, d_force, copy_old, -1, whole_bound);  // reservations spent
     int rc = grow_hot(h, h->hot_used + max_new);
     if (rc) return rc;
     CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
     hipLaunchKernelGGL(k_promote_list, dim3(g), dim3(256), 0, h->stream, d_bound, d_force, h->d_hidx, n, cnt, list,
                        h->hot_used, max_new, h->d_flags);
     hipLaunchKernelGGL(k_promote_rows, dim3((unsigned)std::min<int64_t>(max_new, 65536)), dim3(256), 0, h->stream,
-                       list, max_new, cnt, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
+                       list, max_new, cnt, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0, d_bound, whole_bound);
     CMS_HIP(hipGetLastError());
     h->hot_used += max_new;
     return CMS_OK;
@@ -105,7 +111,8 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
   int rc = grow_hot(h, need);
   if (rc) return rc;
   hipLaunchKernelGGL(k_promote_rows, dim3((unsigned)std::min<int64_t>(c, 65536)), dim3(256), 0, h->stream, list,
-                     (int64_t)c, (const uint32_t*)nullptr, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0);
+                     (int64_t)c, (const uint32_t*)nullptr, h->hot_used, h->tview(), h->d_hidx, copy_old ? 1 : 0, d_bound,
+                     whole_bound);
   CMS_HIP(hipGetLastError());
   h->hot_used = need;
   return CMS_OK;

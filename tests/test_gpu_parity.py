@@ -899,3 +899,50 @@ def test_mid_waves_equal_mid_workgroups(oracle, monkeypatch):
     remap[sel] = np.arange(sel.size)
     exp = oracle_table(oracle, sel.size, d, w, 17, remap[items[m]], users[m], None)
     assert same(got["waves"][0].numpy()[sel].astype(np.float64), exp)
+
+
+@pytest.mark.parametrize("split", ["1024", "4096"])
+def test_lower_split_threshold_same_table(oracle, split, monkeypatch):
+    """CMS_SPLIT_KEYS moves owners of more than that many keys from the mid
+    class to u32 slots built by k_build_slices (single-slice owners of a
+    fresh build store their rows whole: no slot zeroing, no atomics): the
+    counters and similarities equal the default split's, fresh and after an
+    accumulating batch, and sampled owners match the oracle."""
+    import torch
+    n, d, w = 6000, 5, 8192
+    rng = np.random.Generator(np.random.PCG64(51))
+    sizes = np.concatenate([rng.integers(1000, 30000, 300), rng.integers(1, 1500, n - 300)])
+    items = np.repeat(np.arange(n, dtype=np.int64), sizes)
+    users = (rng.zipf(1.3, items.size) % 2_000_000).astype(np.int64)
+    perm = rng.permutation(items.size)
+    items, users = items[perm], users[perm]
+    half = items.size // 2
+    got = {}
+    for mode in ("default", split):
+        if mode == "default":
+            monkeypatch.delenv("CMS_SPLIT_KEYS", raising=False)
+        else:
+            monkeypatch.setenv("CMS_SPLIT_KEYS", mode)
+        for acc in (False, True):
+            with SketchTable(n, depth=d, width=w, seed=23) as t:
+                if acc:
+                    t.ingest(items[:half], users[:half])
+                    t.ingest(items[half:], users[half:])
+                else:
+                    t.ingest(items, users)
+                t.finalize()
+                got[(mode, acc)] = (t.read_counters_device().cpu(),
+                                    np.stack([t.similarities(q, np.arange(n)) for q in (0, 150, 3000)]),
+                                    t.stats()["hot_rows"])
+                torch.cuda.synchronize()
+    for acc in (False, True):
+        a, b = got[("default", acc)], got[(split, acc)]
+        assert torch.equal(a[0], b[0]), acc
+        assert same(a[1], b[1]), acc
+        assert b[2] > a[2]  # more owners on u32 slots
+    sel = np.array([0, 150, 299, 3000])
+    m = np.isin(items, sel)
+    remap = np.full(n, -1, np.int64)
+    remap[sel] = np.arange(sel.size)
+    exp = oracle_table(oracle, sel.size, d, w, 23, remap[items[m]], users[m], None)
+    assert same(got[(split, False)][0].numpy()[sel].astype(np.float64), exp)
