@@ -349,6 +349,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.slice_reduce = num("CMS_SLICE_REDUCE", h->tune.slice_reduce);
     h->tune.mid_waves = num("CMS_MID_WAVES", h->tune.mid_waves);
     h->tune.split_keys = num("CMS_SPLIT_KEYS", h->tune.split_keys);
+    h->tune.mid_threads = num("CMS_MID_THREADS", h->tune.mid_threads);
     h->tune.nib_rows_once = num("CMS_NIB_ROWS_ONCE", h->tune.nib_rows_once);
     h->tune.po_no_prune = num("CMS_PO_NO_PRUNE", h->tune.po_no_prune);
     h->tune.po_bound_rows = num("CMS_PO_BOUND_ROWS", h->tune.po_bound_rows);

@@ -581,14 +581,16 @@ constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
 #ifndef CMS_MID_ROW_PREFETCH
 #define CMS_MID_ROW_PREFETCH 0
 #endif
-template <int SV, int D>
+template <int SV, int D, int MT>
 // 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
 // (it spilled there); the build measured the same (profiles/r04/ab_*_s5)
-__global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
+__global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_build_mid(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
     const int32_t* list, const uint32_t* list_cnt, TableView tv, int32_t* hidx_w, uint32_t* cbound,
     uint64_t* row_mass, uint64_t* norm, uint32_t* rowmax, uint32_t* flags, int list_keys, int u4_keys, int u8_keys,
     int u8img) {
+  constexpr int MTH = MT;                   // threads per owner (a workgroup)
+  constexpr int MKR = kKeyRegs * 256 / MT;  // key registers per thread: 1024 keys cached per owner
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -599,15 +601,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
     const int64_t row = list[li];
     const int64_t lo = lo_[row], hi = hi_[row];
-    const bool cached = (hi - lo) <= (int64_t)kBuildThreads * kKeyRegs;
-    uint64_t kp[kKeyRegs];
-    uint32_t ik[kKeyRegs];
+    const bool cached = (hi - lo) <= (int64_t)MTH * MKR;
+    uint64_t kp[MKR];
+    uint32_t ik[MKR];
     uint64_t mass = 0;
     bool badv = false;
     if (cached) {
 #pragma unroll
-      for (int k = 0; k < kKeyRegs; ++k) {
-        const int64_t i = lo + tid + (int64_t)k * kBuildThreads;
+      for (int k = 0; k < MKR; ++k) {
+        const int64_t i = lo + tid + (int64_t)k * MTH;
         kp[k] = 0;
         ik[k] = 0;
         if (i < hi) {
@@ -648,7 +650,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       const uint32_t capa = (1u << ab) - 1u;
       const int nq_all = (int)((int64_t)hp.depth * w * ab >> 7);  // uint4 of the [d][w] image
       uint4* l4 = reinterpret_cast<uint4*>(lds);
-      for (int j = tid; j < nq_all; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+      for (int j = tid; j < nq_all; j += MTH) l4[j] = make_uint4(0, 0, 0, 0);
       if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
       if (tid == 0) {
         s_max = 0u;
@@ -682,16 +684,16 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       };
       if (cached) {
 #pragma unroll
-        for (int k = 0; k < kKeyRegs; ++k)
-          if (ik[k]) add_all(kp[k], ik[k], as_list ? (int64_t)(tid + k * kBuildThreads) : int64_t(-1));
+        for (int k = 0; k < MKR; ++k)
+          if (ik[k]) add_all(kp[k], ik[k], as_list ? (int64_t)(tid + k * MTH) : int64_t(-1));
       } else {
         // the next step's key loads go out before this step's keys are added
-        constexpr int64_t kStep = 4 * kBuildThreads;
+        constexpr int64_t kStep = 4 * MTH;
         uint64_t nx[4];
         auto fetch = [&](int64_t base) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            const int64_t i = base + tid + (int64_t)u * MTH;
             nx[u] = i < hi ? keys.raw(i) : 0ULL;
           }
         };
@@ -702,7 +704,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             kk[u] = nx[u];
-            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            const int64_t i = base + tid + (int64_t)u * MTH;
             inc4[u] = 0;
             if (i < hi) {
               uint32_t inc;
@@ -744,7 +746,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       const int nq = w >> 5;  // uint4 per 4-bit sketch row
       for (int d = 0; d < hp.depth; ++d) {
         uint32_t sq = 0;  // <= row mass * max counter < 2^32
-        for (int j = tid; j < nq; j += kBuildThreads) {
+        for (int j = tid; j < nq; j += MTH) {
           const uint4 v = l4[d * nq + j];
           const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -769,7 +771,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
     if (start == 1 && u8img) {
       const int nq_all = (int)(((int64_t)hp.depth * w) >> 4);  // uint4 of the [d][w] byte image
       uint4* l4 = reinterpret_cast<uint4*>(lds);
-      for (int j = tid; j < nq_all; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+      for (int j = tid; j < nq_all; j += MTH) l4[j] = make_uint4(0, 0, 0, 0);
       if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
       if (tid == 0) {
         s_max = 0u;
@@ -791,15 +793,15 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       };
       if (cached) {
 #pragma unroll
-        for (int k = 0; k < kKeyRegs; ++k)
+        for (int k = 0; k < MKR; ++k)
           if (ik[k]) add_all8(kp[k], ik[k]);
       } else {
-        constexpr int64_t kStep = 4 * kBuildThreads;
+        constexpr int64_t kStep = 4 * MTH;
         uint64_t nx[4];
         auto fetch = [&](int64_t base) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            const int64_t i = base + tid + (int64_t)u * MTH;
             nx[u] = i < hi ? keys.raw(i) : 0ULL;
           }
         };
@@ -810,7 +812,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             kk[u] = nx[u];
-            const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+            const int64_t i = base + tid + (int64_t)u * MTH;
             inc4[u] = 0;
             if (i < hi) {
               uint32_t inc;
@@ -840,7 +842,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
         const int nq = w >> 4;  // uint4 per u8 sketch row
         for (int d = 0; d < hp.depth; ++d) {
           uint32_t sq = 0;  // <= row mass * max counter < 2^32
-          for (int j = tid; j < nq; j += kBuildThreads) {
+          for (int j = tid; j < nq; j += MTH) {
             const uint4 v = r4[d * nq + j];
             sq = __builtin_amdgcn_udot4(v.x, v.x, sq, false);
             sq = __builtin_amdgcn_udot4(v.y, v.y, sq, false);
@@ -876,7 +878,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
       }
       vmax = 0;
       for (int d = 0; d < hp.depth; ++d) {
-        for (int j = tid; j < nq; j += kBuildThreads) l4[j] = make_uint4(0, 0, 0, 0);
+        for (int j = tid; j < nq; j += MTH) l4[j] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         uint64_t sq = 0;
         bool ovf = false;
@@ -891,24 +893,24 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
         };
         if (cached) {
 #pragma unroll
-          for (int k = 0; k < kKeyRegs; ++k)
+          for (int k = 0; k < MKR; ++k)
             if (ik[k]) add(kp[k], ik[k]);
         } else {
 #if CMS_MID_ROW_PREFETCH
           // the next step's key loads go out before this step's keys are
           // added (the 4-bit pass's scheme; every row pass re-reads the keys)
-          constexpr int64_t kStep = 4 * kBuildThreads;
+          constexpr int64_t kStep = 4 * MTH;
           uint64_t nx[4];
           auto fetch = [&](int64_t base) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+              const int64_t i = base + tid + (int64_t)u * MTH;
               nx[u] = i < hi ? keys.raw(i) : 0ULL;
             }
           };
           fetch(lo);
 #endif
-          for (int64_t base = lo; base < hi; base += 4 * kBuildThreads) {
+          for (int64_t base = lo; base < hi; base += 4 * MTH) {
             uint64_t kk[4];
             uint32_t inc4[4];
 #if CMS_MID_ROW_PREFETCH
@@ -919,7 +921,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
 #endif
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const int64_t i = base + tid + (int64_t)u * kBuildThreads;
+              const int64_t i = base + tid + (int64_t)u * MTH;
 #if CMS_MID_ROW_PREFETCH
               kk[u] = i < hi ? keys.resolve(raw[u]) : 0;
 #else
@@ -952,7 +954,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(4
         if (false)
 #endif
         if (!(as_list && level == 1))  // a list row's entries left in the 4-bit pass
-          for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + d * nq + j, l4[j], SV);
+          for (int j = tid; j < nq; j += MTH) store_row(d4 + d * nq + j, l4[j], SV);
         __syncthreads();  // the image is read out before the next sketch row zeroes it
       }
       if (!s_ovf || level == 2) break;
@@ -2029,9 +2031,11 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       // the u8 all-rows image (Tunables::mid_u8_image) when a [d][w] byte image fits 64 KB (config 3: 40 KB)
       const int u8img = h->tune.mid_u8_image && h->dw <= 64 * 1024 ? 1 : 0;
       const size_t mid_lds = std::max<size_t>((size_t)h->p.width * 2, u8img ? (size_t)h->dw : (size_t)h->dw / 2);
-      auto kmid = h->p.depth == 5   ? k_build_mid<kBuildStoreForm, 5>
-                  : h->p.depth == 4 ? k_build_mid<kBuildStoreForm, 4>
-                                    : k_build_mid<kBuildStoreForm, 0>;
+      const bool mid128 = h->tune.mid_threads == 128;
+      auto kmid = h->p.depth == 5   ? (mid128 ? k_build_mid<kBuildStoreForm, 5, 128> : k_build_mid<kBuildStoreForm, 5, 256>)
+                  : h->p.depth == 4 ? (mid128 ? k_build_mid<kBuildStoreForm, 4, 128> : k_build_mid<kBuildStoreForm, 4, 256>)
+                                    : (mid128 ? k_build_mid<kBuildStoreForm, 0, 128> : k_build_mid<kBuildStoreForm, 0, 256>);
+      const int mid_nt = mid128 ? 128 : 256;
       // the one-pass image build when the [d][w] u16 image fits 80 KB and the
       // row width packs into whole 4-bit words (Tunables::mid_image)
       const bool img = h->tune.mid_image && h->dw * 2 <= 80 * 1024 && (h->dw % 32) == 0;
@@ -2062,13 +2066,14 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                            (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                            h->d_rowmax, lists_allowed(h) ? kMidListKeys : 0, h->tune.mid_u4_keys,
                            h->tune.mid_u8_keys, mid_redo, lcnt + 2);
-        hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(kBuildThreads),
+        hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * 2)), dim3(mid_nt),
                            mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_redo,
                            (const uint32_t*)(lcnt + 2), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                            h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0, 0, 0, 0);
       } else
-      hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * CMS_MID_GRID_PER_CU)),
-                         dim3(kBuildThreads), mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
+      hipLaunchKernelGGL(kmid, dim3((unsigned)std::min<int64_t>(n, (int64_t)h->num_cus * CMS_MID_GRID_PER_CU *
+                                                                 (mid128 ? 2 : 1))),
+                         dim3(mid_nt), mid_lds, side2, d_lo, d_hi, keys, d_val, h->hp, (const int32_t*)mid_list,
                          (const uint32_t*)(lcnt + 1), h->tview(), h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm,
                          h->d_rowmax, h->d_flags, lists_allowed(h) ? kMidListKeys : 0, h->tune.mid_u4_keys,
                          h->tune.mid_u8_keys, u8img);

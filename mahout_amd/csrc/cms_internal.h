@@ -214,6 +214,7 @@ struct Tunables {
   int po_no_bigq = 0;       // CMS_PO_NO_BIGQ=1: per-owner all-pairs without k_po_bigq (every query in the group kernel)
   int mid_u8_image = 0;     // CMS_MID_U8_IMAGE=1: mid owners starting at u8 count all sketch rows in one [d][w] u8 image
   int nib_rows_once = 0;    // CMS_NIB_ROWS_ONCE=1: a byte-class wave hashes its first key slot's d rows up front (d = 4 or 5)
+  int mid_threads = 256;    // CMS_MID_THREADS=128: k_build_mid owners on 2-wave workgroups (twice as many in flight)
   int split_keys = 0;       // CMS_SPLIT_KEYS: rows with more keys get a u32 slot and k_build_slices (0: 8192, 16384 at w >= 8192)
   int mid_waves = 0;        // CMS_MID_WAVES=<k>: mid owners one wave each (k_build_mid_waves), k persistent 4-wave workgroups per CU; 0: k_build_mid
   int slice_reduce = 0;     // CMS_SLICE_REDUCE=1: split owners' slices leave u16 images summed by k_slice_reduce (no slot atomics)

@@ -861,12 +861,15 @@ def test_byte_class_rows_once_equal_row_by_row(oracle, monkeypatch):
     assert same(got["1"][0].numpy()[sel].astype(np.float64), exp)
 
 
-def test_mid_waves_equal_mid_workgroups(oracle, monkeypatch):
+@pytest.mark.parametrize("variant", ["CMS_MID_WAVES=5", "CMS_MID_THREADS=128"])
+def test_mid_waves_equal_mid_workgroups(oracle, monkeypatch, variant):
     """k_build_mid_waves (CMS_MID_WAVES: one wave per mid-class owner, 4-bit
     then u8 rows, list rows for owners of <= 1024 keys; u16 owners and keys
-    >= 2^32 handed to k_build_mid) builds the same table, the same row forms
-    and the same norms as k_build_mid's 256-thread owners, and sampled mid
-    owners match the oracle."""
+    >= 2^32 handed to k_build_mid) and k_build_mid on 128-thread workgroups
+    (CMS_MID_THREADS=128) build the same table, the same row forms and the
+    same norms as k_build_mid's 256-thread owners, and sampled mid owners
+    match the oracle."""
+    var, val = variant.split("=")
     import torch
     n, d, w = 20_000, 5, 8192
     rng = np.random.Generator(np.random.PCG64(31))
@@ -882,7 +885,10 @@ def test_mid_waves_equal_mid_workgroups(oracle, monkeypatch):
     items, users = items[perm], users[perm]
     got = {}
     for mode in ("workgroups", "waves"):
-        monkeypatch.setenv("CMS_MID_WAVES", "5" if mode == "waves" else "0")
+        if mode == "waves":
+            monkeypatch.setenv(var, val)
+        else:
+            monkeypatch.delenv(var, raising=False)
         with SketchTable(n, depth=d, width=w, seed=17) as t:
             t.ingest(items, users)
             t.finalize()
