@@ -604,8 +604,8 @@ def config3_shard(n_items, n_users, total_pairs, rank, world, device, seed=20261
 
 
 # (the depth-unrolled kernels carry the handle's depth as a template argument)
-BUILD_KERNELS = ["void cms::k_build_slices<*>", "void cms::k_build_rows<2>", "void cms::k_build_nibbles<2>",
-                 "void cms::k_build_mid<2, *>", "void cms::k_build_bytes<2>"]
+BUILD_KERNELS = ["void cms::k_build_slices<*>", "void cms::k_build_rows<2>", "void cms::k_build_nibbles<2, *>",
+                 "void cms::k_build_mid<2, *, *>", "void cms::k_build_bytes<2>"]
 
 
 def build_roofline(table, local_pairs, build_ms, build_n, pmc_kernel, pmc_file):
