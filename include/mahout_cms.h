@@ -450,7 +450,7 @@ typedef struct cms_stats {
   int32_t depth, width;
   int32_t exact_norms;      /* 1 if every (owner,row) norm is < 2^53 (bit-exact fast path) */
   int32_t world, rank;
-  int64_t table_bytes;
+  int64_t table_bytes;       /* narrow-row arena allocation + the u32 rows of the hot owners */
   int64_t multi_limb_owners; /* owners with a counter >= 128 (all-pairs limb split; -1 before the first all-pairs call) */
   int64_t topk_redo;         /* top-k rows that needed the radix-select fallback */
   int64_t deep_limb_owners;  /* of those, owners with a counter >= 2^14 (3+ limbs); -1 before */

@@ -357,6 +357,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.po_dense_x4 = num("CMS_PO_DENSE_X4", h->tune.po_dense_x4);
     h->tune.po_no_bigq = num("CMS_PO_NO_BIGQ", h->tune.po_no_bigq);
     h->tune.forms = !flag("CMS_NO_FORMS");
+    h->tune.no_compact = flag("CMS_NO_COMPACT");
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");
     h->tune.mls = !flag("CMS_NO_MLS");
@@ -412,7 +413,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
 #ifdef CMS_BUILD_GATHERHASH  // bound analysis only (cms_hash.h): the gathered table, contents unset
       (e = hipMalloc((void**)&h->hp.gtab, sizeof(uint4) << 24)) != hipSuccess ||
 #endif
-      (!per_owner && !f64 && (e = hipMalloc(&h->d_t16, tbytes)) != hipSuccess) ||
+      (!per_owner && !f64 && (e = hipMalloc(&h->d_off, sizeof(int64_t) * h->n)) != hipSuccess) ||
       (f64 && (e = hipMalloc(&h->d_t64, 4 * tbytes)) != hipSuccess) ||
       (!per_owner && (e = hipMalloc(&h->d_hidx, sizeof(int32_t) * h->n)) != hipSuccess) ||
       (!per_owner && (e = hipMemset(h->d_hidx, 0xff, sizeof(int32_t) * h->n)) != hipSuccess) ||
@@ -435,6 +436,16 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   // (the byte-class and mid kernels store whole 16-B words of a 4-bit sketch
   // row: w % 32 == 0)
   h->forms_ok = !per_owner && !f64 && h->p.width % 32 == 0 && h->tune.forms;
+  // compact rows (cms_internal.h TableView) when the layout's 64-B units fit
+  // the u32 scan; the arena then starts as the zero row alone
+  h->compact = h->forms_ok && !h->tune.no_compact &&
+               (double)h->n * (double)(slot_units(h->dw) / kRowAlign + 1) < 4.0e9;
+  if (!per_owner && !f64) {
+    if (int rc = init_row_offsets(h)) {
+      cms_destroy(h);
+      return rc;
+    }
+  }
   *out = h;
   return CMS_OK;
 }
@@ -464,7 +475,7 @@ void cms_destroy(cms_handle* h) {
   if (h->ev_join2) (void)hipEventDestroy(h->ev_join2);
   free_query_pool(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  void* bufs[] = {h->d_t16, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
+  void* bufs[] = {h->d_t16, h->d_off, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -887,8 +898,7 @@ int cms_finalize(cms_handle* h) {
     return CMS_OK;
   }
   if (h->empty) {
-    CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * h->n * h->dw, h->stream));
-    if (int rc0 = reset_table_layout(h)) return rc0;
+    if (int rc0 = reset_rows_zero(h)) return rc0;
     h->empty = false;
     h->norms_valid = false;
   }
@@ -929,8 +939,7 @@ int cms_finalize_with(cms_handle* h, cms_allreduce_fn fn, void* user) {
   if (h->comm || h->ext_comm) return set_error(CMS_E_STATE, "handle has a communicator: use cms_finalize");
   if (h->ext_merged) return set_error(CMS_E_STATE, "already merged: cms_reset starts a new epoch");
   if (h->empty) {
-    CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * h->n * h->dw, h->stream));
-    if (int rc0 = reset_table_layout(h)) return rc0;
+    if (int rc0 = reset_rows_zero(h)) return rc0;
     h->empty = false;
     h->norms_valid = false;
   }
@@ -1748,7 +1757,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->exact_norms = h->exact_norms;
   out->world = h->world;
   out->rank = h->rank;
-  int64_t forms[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // hot, u16, u8, 4-bit, 2-bit, 1-bit, list rows, list bytes
+  int64_t forms[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // hot, u16, u8, 4-bit, 2-bit, 1-bit, list rows, list bytes, zero rows
   if (!h->per_owner && !h->f64 && h->d_hidx) {
     int rc = count_forms(h, forms);
     if (rc) return rc;
@@ -1756,7 +1765,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   const int64_t hot_rows = forms[0];
   out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                     : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
-                                  : (int64_t)sizeof(uint16_t) * h->n * h->dw + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
+                                  : (int64_t)sizeof(uint16_t) * h->t16_cap + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;
@@ -1765,7 +1774,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   out->hot_rows = hot_rows;
   out->stored_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                      : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
-                                   : 4 * forms[0] * h->dw + 2 * forms[1] * h->dw + forms[2] * h->dw +
+                                   : 4 * forms[0] * h->dw + 2 * (forms[1] - forms[8]) * h->dw + forms[2] * h->dw +
                                     forms[3] * (h->dw / 2) + forms[4] * (h->dw / 4) + forms[5] * (h->dw / 8) +
                                     forms[7];
   out->u8_rows = forms[2];

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
   // a hot row (slot) is u32, any other row u16 (promote_rows ran before the launch)
   const int32_t slot = tv.hidx[row];
   uint32_t* dst = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
-  uint16_t* dst16 = tv.t16 + row * dw;
+  uint16_t* dst16 = tv.row16(row);
   const bool load_old = accumulate && !atomic_mode;
   if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
   if (tid == 0) {
@@ -398,8 +398,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
       // 16-B u32 stores for slots, 8-B u16 stores for narrow rows (when the
       // row offset keeps them aligned); the next sketch row's old counters
       // are loaded into the slot as it is drained
-      const bool vec = (w & 3) == 0 && (dst != nullptr || ((row * dw) & 3) == 0);
-      if (vec && !dst && !more && SV > 0 && (w & 7) == 0 && ((row * dw) & 7) == 0) {
+      const bool vec = (w & 3) == 0 && (dst != nullptr || (tv.base(row) & 3) == 0);
+      if (vec && !dst && !more && SV > 0 && (w & 7) == 0 && (tv.base(row) & 7) == 0) {
         // narrow row, fresh build, 16-B stores (8 counters per lane)
         uint4* l4 = reinterpret_cast<uint4*>(lds);
         uint4* d4 = reinterpret_cast<uint4*>(dst16 + rofs);
@@ -624,7 +624,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         }
       }
     }
-    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's slot (64-B aligned)
+    uint4* d4 = reinterpret_cast<uint4*>(tv.row16(row));  // the row's slot (64-B aligned)
     // a LIST row (cms_internal.h kFormList) when the owner's keys sit in
     // registers, increments are units, and the list beats even the 4-bit row:
     // the counting below then only yields the norms and the maximum, and the
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const int64_t m = hi - lo;
     const bool as_list = cached && m <= list_keys && vals == nullptr && hp.frac_bits == 0 &&
                          (int64_t)hp.depth * m <= 8192 && 2 + 2 * (int64_t)hp.depth * m < (int64_t)hp.depth * w / 2;
-    uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;
+    uint16_t* lst = tv.row16(row);
     int level = -1;  // the form that holds the owner: 0 4-bit, 1 u8, 2 u16 (the class bound keeps every counter < 2^16)
     uint32_t vmax = 0;
     // the first form tried (Tunables::mid_u4_keys / mid_u8_keys); a list row
@@ -1021,8 +1021,8 @@ __global__ __launch_bounds__(256) void k_build_mid_waves(
       continue;
     }
     const bool as_list = m <= list_keys && (int64_t)depth * m <= 8192 && 2 + 2 * (int64_t)depth * m < dw / 2;
-    uint16_t* lst = tv.t16 + row * dw;  // list row: [0] = m, then [d][m] buckets
-    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * dw);
+    uint16_t* lst = tv.row16(row);  // list row: [0] = m, then [d][m] buckets
+    uint4* d4 = reinterpret_cast<uint4*>(tv.row16(row));
     int bits = (as_list || m <= u4_keys) ? 4 : 8;
     uint32_t vmax = 0;
     bool ovf = false, slow = false;  // slow: a reduced key >= 2^32 (bucket_q's route does not take it)
@@ -1136,7 +1136,7 @@ __global__ __launch_bounds__(kImgThreads) void k_build_image(
     // the owner a dense u16 row instead, which overwrites them)
     const bool as_list = m <= list_keys && vals == nullptr && hp.frac_bits == 0 && (int64_t)hp.depth * m <= 8192 &&
                          2 + 2 * (int64_t)hp.depth * m < (int64_t)hp.depth * w / 2;
-    uint16_t* lst = tv.t16 + row * dw;
+    uint16_t* lst = tv.row16(row);
     uint64_t mass = 0;
     bool badv = false;
     constexpr int kPer = 4;
@@ -1291,6 +1291,45 @@ __global__ __launch_bounds__(kImgThreads) void k_build_image(
 constexpr int kNibWaves = CMS_NIB_WAVES;
 // owners with at most Tunables::bit_keys (64) keys try 1-bit rows first, with
 // at most crumb_keys (256) 2-bit rows
+// A byte-class owner's first form: 1-bit rows up to bit_keys keys, 2-bit up
+// to crumb_keys, else 4-bit
+__host__ __device__ __forceinline__ int nib_first_bits(int64_t m, int w, int bit_keys, int crumb_keys) {
+  return (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
+}
+// ... stored as a list row: unit increments, at most list_keys keys, and the
+// list (2 + 2 d m bytes) no larger than the dense row it would take first
+__host__ __device__ __forceinline__ bool nib_list_row(int64_t m, int w, int d, bool weighted, int frac_bits,
+                                                      int bit_keys, int crumb_keys, int list_keys) {
+  return m <= list_keys && !weighted && frac_bits == 0 &&
+         2 + 2 * (int64_t)d * m <= ((int64_t)d * w * nib_first_bits(m, w, bit_keys, crumb_keys)) / 8;
+}
+
+// Compact layout of a fresh build (row_layout): each row's arena capacity in
+// 64-B units, by what its class's kernel can store -- a hot row nothing (its
+// counters are u32 slot rows), a byte-class row its list entries or its u8
+// image (k_build_nibbles' forms up to k_build_bytes' u8 rows), any other row
+// (the mid class, or every row without forms) a whole u16 slot (kRowFull).
+__global__ void k_row_caps(const int64_t* lo_, const int64_t* hi_, int64_t n, const uint64_t* bound,
+                           const int32_t* hidx, int forms, int weighted, int frac_bits, int d, int w, int bit_keys,
+                           int crumb_keys, int list_keys, uint32_t* caps) {
+  const int64_t dw = (int64_t)d * w;
+  const uint32_t full = (uint32_t)(slot_units(dw) / kRowAlign);
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = hidx[r];
+    const int64_t m = hi_[r] - lo_[r];
+    uint32_t c = full;
+    if (s >= 0) {
+      c = 0;
+    } else if (forms && byte_class(s, m, bound[r])) {
+      const int64_t u16s = nib_list_row(m, w, d, weighted != 0, frac_bits, bit_keys, crumb_keys, list_keys)
+                               ? 1 + (int64_t)d * m  // [0] = m, then the d x m entries
+                               : dw / 2;             // the u8 image
+      c = (uint32_t)((u16s + kRowAlign - 1) / kRowAlign);
+    }
+    caps[r] = c;
+  }
+}
+
 // One byte-class owner by one wave (k_build_nibbles).  D > 0 (the handle's
 // depth is 4 or 5): every key's d buckets are hashed up front, as d
 // independent chains (an owner here has one key or a few per lane, so one
@@ -1335,17 +1374,15 @@ __device__ __forceinline__ void nib_owner(
   const int64_t m = hi - lo;
   // list rows (cms_internal.h kFormList): unit increments, at most list_keys
   // keys; counted as 4-bit in LDS for the norms and the maximum only, the
-  // entries leave as the owner's buckets
-  int bits = (m <= bit_keys && (w & 127) == 0) ? 1 : (m <= crumb_keys && (w & 63) == 0) ? 2 : 4;
-  // only where the list is no larger than the dense row the owner would take
-  // first (2 + 2 d m bytes against d w bits / 8; both fit the slot then)
-  const bool as_list = m <= list_keys && vals == nullptr && hp.frac_bits == 0 &&
-                       2 + 2 * (int64_t)hp.depth * m <= ((int64_t)hp.depth * w * bits) / 8;
+  // entries leave as the owner's buckets (nib_first_bits / nib_list_row: the
+  // compact layout sizes the row by the same rule, k_row_caps)
+  int bits = nib_first_bits(m, w, bit_keys, crumb_keys);
+  const bool as_list = nib_list_row(m, w, hp.depth, vals != nullptr, hp.frac_bits, bit_keys, crumb_keys, list_keys);
   if (as_list) bits = 4;
-  uint16_t* lst = tv.t16 + row * (int64_t)hp.depth * w;  // list row: [0] = m, then [d][m] buckets
+  uint16_t* lst = tv.row16(row);  // list row: [0] = m, then [d][m] buckets
   uint4* slot4 = reinterpret_cast<uint4*>(lds) + wv * (w >> 5);  // w/2 bytes per wave (the 4-bit row)
   uint32_t* slot = lds + wv * (w >> 3);
-  uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * (int64_t)hp.depth * w);  // the row's u16 slot (64-B aligned)
+  uint4* d4 = reinterpret_cast<uint4*>(tv.row16(row));  // the row's u16 slot (64-B aligned)
   uint32_t vmax = 0;
   bool ovf = false;
   // D > 0: the first register slot's key (an owner of <= 64 keys: its only
@@ -1397,8 +1434,8 @@ __device__ __forceinline__ void nib_owner(
   }
   if (as_list && lane == 0) lst[0] = (uint16_t)m;
   if (badv) atomicOr(flags, kFlagBadValue);
-  if (__ballot(ovf)) {
-    if (lane == 0) redo[atomicAdd(redo_cnt, 1u)] = (int32_t)row;
+  if (__ballot(ovf)) {  // to k_build_bytes; a list row (~row) stays one there: its counters are < 2^8 (m < 2^8)
+    if (lane == 0) redo[atomicAdd(redo_cnt, 1u)] = as_list ? ~(int32_t)row : (int32_t)row;
     return;
   }
 #pragma unroll
@@ -1431,7 +1468,10 @@ __global__ __launch_bounds__(64 * kNibWaves) __attribute__((amdgpu_waves_per_eu(
 
 // The byte-class owners a counter >= 16 sent back from k_build_nibbles: the
 // same one-pass build on a [d][w] u8 image (dw bytes of LDS), stored as u8
-// rows.  A persistent grid walks the device-side list (no host count).
+// rows -- or, for a list row (listed as ~row), its entries written whole and
+// the list kept (the compact layout sized it as a list; a list holds any
+// counter below 2^8).  A persistent grid walks the device-side list (no host
+// count).
 template <int SV>
 __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
     const int64_t* lo_, const int64_t* hi_, Keys keys, const float* vals, HashParams hp,
@@ -1445,8 +1485,10 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
   const int64_t dw = (int64_t)hp.depth * w;
   const uint32_t count = *list_cnt;
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
-    const int64_t row = list[li];
+    const bool keep_list = list[li] < 0;
+    const int64_t row = keep_list ? ~(int64_t)list[li] : (int64_t)list[li];
     const int64_t lo = lo_[row], hi = hi_[row];
+    uint16_t* lst = tv.row16(row);  // list row: [0] = m (k_build_nibbles wrote it), then [d][m] buckets
     if (tid < CMS_MAX_DEPTH) s_norm[tid] = 0ULL;
     if (tid == 0) {
       s_max = 0u;
@@ -1482,7 +1524,9 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
 #pragma unroll
       for (int k = 0; k < kKeyRegs; ++k)
         if (ik[k]) {
-          const uint32_t c = (uint32_t)d * (uint32_t)w + bucket(hp, d, kp[k]);
+          const uint32_t bk = bucket(hp, d, kp[k]);
+          const uint32_t c = (uint32_t)d * (uint32_t)w + bk;
+          if (keep_list) lst[1 + (int64_t)d * (hi - lo) + tid + (int64_t)k * kBuildThreads] = (uint16_t)bk;
           const uint32_t sh = (c & 3u) << 3;
           const uint32_t old = (atomicAdd(&lds[c >> 2], ik[k] << sh) >> sh) & 255u;  // < 2^8: no carry
           sq += (2u * old + ik[k]) * ik[k];
@@ -1497,17 +1541,18 @@ __global__ __launch_bounds__(kBuildThreads) void k_build_bytes(
     mass = wave_sum_u32(mass);
     if ((tid & 63) == 0 && mass) atomicAdd(&s_mass, mass);
     __syncthreads();
-    uint4* d4 = reinterpret_cast<uint4*>(tv.t16 + row * dw);
+    uint4* d4 = reinterpret_cast<uint4*>(lst);
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
     if (false)
 #endif
-    for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
+    if (!keep_list)
+      for (int j = tid; j < nq; j += kBuildThreads) store_row(d4 + j, l4[j], SV);
     if (badv) atomicOr(flags, kFlagBadValue);
     if (tid < hp.depth) norm[row * hp.depth + tid] = s_norm[tid];
     if (tid == 0) {
       rowmax[row] = s_max;
       row_mass[row] = s_mass;
-      hidx_w[row] = kFormU8;
+      hidx_w[row] = keep_list ? kFormList : kFormU8;
       cbound[row] = s_max;
     }
     __syncthreads();  // the image and the shared sums are consumed before the next owner
@@ -1916,9 +1961,23 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
                        fast_slices ? 0 : 1, row_hot, hot, extra_map, counters, h->d_norm, h->d_rowmax, h->p.depth);
     CMS_HIP(hipGetLastError());
   }
-  plan_side.end();
   // fresh builds may store byte forms: the whole [d][w] byte image in LDS
   const int forms = h->forms_ok && !accumulate && (size_t)h->dw <= kFormLdsMax ? 1 : 0;
+  if (h->compact && !accumulate) {
+    // the compact layout: capacities by class, their scan, the arena sized
+    // (the one read-back of the build; beside the last scatter when the
+    // plan runs on the side stream)
+    TimedScope ts(h, "build_plan");
+    CMS_HIP(h->ws_layout.ensure(sizeof(uint32_t) * (size_t)(2 * n + n / 4096 + 16)));
+    uint32_t* caps = h->ws_layout.as<uint32_t>();
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_row_caps, dim3(grid), dim3(256), 0, h->stream, d_lo, d_hi, n, h->ws_bound.as<uint64_t>(),
+                       h->d_hidx, forms, d_val ? 1 : 0, h->hp.frac_bits, h->p.depth, h->p.width, h->tune.bit_keys,
+                       h->tune.crumb_keys, lists_allowed(h) ? h->tune.list_keys : 0, caps);
+    CMS_HIP(hipGetLastError());
+    if ((rc0 = row_layout(h, caps, caps + n))) return rc0;
+  }
+  plan_side.end();
   const int skip_untouched = accumulate && h->norms_valid ? 1 : 0;
   const size_t lds = sizeof(uint32_t) * (size_t)((h->p.width + 3) & ~3);
   // k_build_rows: with fast slices it builds only the unsplit slot rows

@@ -181,13 +181,13 @@ __device__ __forceinline__ uint32_t table_add(const TableView& tv, int64_t r, in
   const int32_t s = tv.hidx[r];
   if (s >= 0) return atomicAdd(tv.hot + (int64_t)s * tv.dw + c, inc);
   if (s == kFormU16) {
-    const int64_t g = r * tv.dw + c;
+    const int64_t g = tv.base(r) + c;  // (the row's base is even: 64-B aligned)
     const uint32_t sh = (uint32_t)(g & 1) << 4;
     const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(tv.t16) + (g >> 1), inc << sh);
     return (old >> sh) & 0xffffu;
   }
   if (s == kFormList) return tv.get(r, c);  // only inc == 0 reaches a list row (any mass widens it first)
-  uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * tv.dw);  // slot start: 64-B aligned with forms
+  uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.row16(r));  // slot start: 64-B aligned
   if (s == kFormU8) {
     const uint32_t sh = (uint32_t)(c & 3) << 3;
     return (atomicAdd(w32 + (c >> 2), inc << sh) >> sh) & 0xffu;
@@ -477,8 +477,7 @@ int ingest_coo_device(cms_handle* h, const int64_t* d_row, const int64_t* d_key,
     }
     TimedScope ts(h, "ingest_atomic");
     if (h->empty) {
-      CMS_HIP(hipMemsetAsync(h->d_t16, 0, sizeof(uint16_t) * (size_t)(n * h->dw), h->stream));
-      int rc = reset_table_layout(h);
+      int rc = reset_rows_zero(h);
       if (rc) return rc;
       CMS_HIP(hipMemsetAsync(h->d_row_mass, 0, sizeof(uint64_t) * (size_t)n, h->stream));
       CMS_HIP(hipMemsetAsync(h->d_norm, 0, sizeof(uint64_t) * (size_t)(n * h->p.depth), h->stream));

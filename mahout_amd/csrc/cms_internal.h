@@ -68,8 +68,17 @@ struct PendingEvent {
 // bytes the row build writes.  Writers promote a row to a slot before its
 // bound can reach 2^16 (promote_rows), so a u16 counter never overflows.
 //
-// Narrow FORMS: every non-hot row owns a u16-sized slot ([dw] u16 at
-// t16 + row * dw), but a fresh build stores a row whose counters are all
+// ROW STORAGE: the narrow rows live in one arena (t16) at per-row offsets
+// (off[row], u16 units, 64-B aligned; bit 0 = kRowFull: the row owns a whole
+// u16 slot of dw counters there).  Offset 0 is a shared row of zeros that
+// every row of an empty table points to.  A fresh build with forms lays the
+// rows out compactly (row_layout: each row gets what its form can need -- a
+// list row its entries, a byte-class row its u8 image, a mid row a whole
+// slot); any later writer first gives a row that is not kRowFull a whole
+// slot at the arena's end (widen_rows relocates it), so in-place adds only
+// ever touch full slots.  Handles without forms keep every row in a full slot.
+//
+// Narrow FORMS: a fresh build stores a row whose counters are all
 // below 2^8 as u8 in the first dw bytes of its slot, and one whose counters
 // are all below 2^4 as packed nibbles (counter j in bits 4*(j&1) of byte j/2)
 // in the first dw/2 bytes, and one whose counters are all below 2^2 as 2-bit
@@ -97,21 +106,28 @@ constexpr uint32_t form_cap(int32_t form) {
        : form == kFormU8 ? 255u : 65535u;
 }
 
+constexpr int64_t kRowFull = 1;  // off[row] bit 0: the row owns a whole u16 slot (in-place writes allowed)
+constexpr int64_t kRowAlign = 32;  // u16 units (64 B) per arena allocation unit
+__host__ __device__ constexpr int64_t slot_units(int64_t dw) { return (dw + kRowAlign - 1) / kRowAlign * kRowAlign; }
+
 struct TableView {
-  uint16_t* t16;        // [n][dw] narrow slots
+  uint16_t* t16;        // the narrow-row arena (row r at off[r] & ~kRowFull)
   uint32_t* hot;        // [hot_cap][dw] u32 rows
   const int32_t* hidx;  // [n] slot of a hot row, or the narrow form (kForm*)
   int64_t dw;
   int32_t w;            // sketch row width (list rows)
+  const int64_t* off;   // [n] arena offset of each narrow row (u16 units) | kRowFull
+  __device__ __forceinline__ int64_t base(int64_t row) const { return off[row] & ~kRowFull; }
+  __device__ __forceinline__ uint16_t* row16(int64_t row) const { return t16 + base(row); }
   // list row: key count and the entries of sketch row r
-  __device__ __forceinline__ uint32_t list_m(int64_t row) const { return t16[row * dw]; }
+  __device__ __forceinline__ uint32_t list_m(int64_t row) const { return t16[base(row)]; }
   __device__ __forceinline__ const uint16_t* list_row(int64_t row, int64_t r, uint32_t m) const {
-    return t16 + row * dw + 1 + r * (int64_t)m;
+    return row16(row) + 1 + r * (int64_t)m;
   }
   __device__ __forceinline__ uint32_t get(int64_t row, int64_t j) const {
     const int32_t s = hidx[row];
     if (s >= 0) return hot[(int64_t)s * dw + j];
-    if (s == kFormU16) return (uint32_t)t16[row * dw + j];
+    if (s == kFormU16) return (uint32_t)t16[base(row) + j];
     if (s == kFormList) {  // O(m): point queries; whole-row readers expand instead
       const uint32_t m = list_m(row);
       const int64_t r = j / w;
@@ -121,7 +137,7 @@ struct TableView {
       for (uint32_t t = 0; t < m; ++t) c += e[t] == b;
       return c;
     }
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(row16(row));
     if (s == kFormU8) return p[j];
     if (s == kFormU2) return (uint32_t)(p[j >> 2] >> ((j & 3) << 1)) & 3u;
     if (s == kFormU1) return (uint32_t)(p[j >> 3] >> (j & 7)) & 1u;
@@ -132,7 +148,7 @@ struct TableView {
     const int32_t s = hidx[row];
     if (s >= 0) return *reinterpret_cast<const uint4*>(hot + (int64_t)s * dw + j);
     if (s == kFormU16) {
-      const ushort4 v = *reinterpret_cast<const ushort4*>(t16 + row * dw + j);
+      const ushort4 v = *reinterpret_cast<const ushort4*>(row16(row) + j);
       return make_uint4(v.x, v.y, v.z, v.w);
     }
     if (s == kFormList) {  // O(m), w % 4 == 0: the four counters share a sketch row
@@ -150,7 +166,7 @@ struct TableView {
       }
       return c;
     }
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(t16 + row * dw);
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(row16(row));
     if (s == kFormU8) {
       const uint32_t v = *reinterpret_cast<const uint32_t*>(p + j);
       return make_uint4(v & 255u, (v >> 8) & 255u, (v >> 16) & 255u, v >> 24);
@@ -219,6 +235,7 @@ struct Tunables {
   int mid_waves = 0;        // CMS_MID_WAVES=<k>: mid owners one wave each (k_build_mid_waves), k persistent 4-wave workgroups per CU; 0: k_build_mid
   int slice_reduce = 0;     // CMS_SLICE_REDUCE=1: split owners' slices leave u16 images summed by k_slice_reduce (no slot atomics)
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
+  bool no_compact = false; // CMS_NO_COMPACT=1: every narrow row keeps a whole u16 slot (no compact layout)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
   bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)
   bool mls = true;         // CMS_NO_MLS=1: multi-limb slabs on the 128-tile kernel instead of k_cosine_mls
@@ -256,7 +273,10 @@ struct cms_handle {
 
   int64_t n = 0;       // rows
   int64_t dw = 0;      // d*w counters per row
-  uint16_t* d_t16 = nullptr;        // [n][d][w] narrow counters
+  uint16_t* d_t16 = nullptr;        // arena of the narrow rows (TableView; [0, slot_units(dw)) the zero row)
+  int64_t t16_cap = 0, t16_used = 0;  // arena capacity and end of the allocated part (u16 units)
+  int64_t* d_off = nullptr;         // [n] arena offset of each narrow row | kRowFull
+  bool compact = false;             // forms_ok: fresh builds lay the rows out compactly (row_layout)
   bool f64 = false;                 // CMS_COUNTER_F64: fp64 counters in d_t64 (cms_f64.hip), no u16/u32 table
   double* d_t64 = nullptr;          // [n][d][w] fp64 counters
   int32_t* d_hidx = nullptr;        // [n] hot slot, or the narrow form (kFormU16 / kFormU8 / kFormU4 / kFormU2 / kFormU1)
@@ -265,9 +285,10 @@ struct cms_handle {
   cms::DevBuf hot_tab;              // [hot_cap][d][w] u32 counters of the hot rows
   cms::DevBuf ws_bound, ws_force, ws_plist;  // promotion scratch: u64 [n], u8 [n], i32 [n] + count
   cms::DevBuf ws_blist;                      // row build: slot-row and mid-class row lists + counts
+  cms::DevBuf ws_layout;                     // row layout: capacities / scan (u32 [2n + ...]); widen: movers
   int64_t hot_cap = 0, hot_used = 0;
   cms::TableView tview() const {
-    return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw, p.width};
+    return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw, p.width, d_off};
   }
   uint64_t* d_row_mass = nullptr;   // [n] total increment mass per row
   uint64_t* d_norm = nullptr;       // [n][d] exact sum of squares (saturating)
@@ -452,7 +473,7 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 // rows holding a u32 slot (synchronises the stream)
 int count_hot_rows(cms_handle* h, int64_t* out);
 // rows per storage form: [0] hot, [1] u16, [2] u8, [3] nibble (synchronises)
-int count_forms(cms_handle* h, int64_t out[8]);  // hot, u16, u8, 4-bit, 2-bit, 1-bit, list rows, list bytes
+int count_forms(cms_handle* h, int64_t out[9]);  // hot, u16, u8, 4-bit, 2-bit, 1-bit, list rows, list bytes, zero rows
 // Form rows that a coming write could push past their capacity become u16 in
 // place: with d_bound (a u64 upper bound of each row's mass after the write)
 // and old_mass, a touched form row (bound > old mass) is widened when
@@ -470,6 +491,19 @@ int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const fl
 int read_counters_device(cms_handle* h, int64_t r0, int64_t rc, uint32_t* d_out);
 // all rows narrow and zero-able again (empty table)
 int reset_table_layout(cms_handle* h);
+// every row back to zeros: compact handles point every row at the arena's
+// zero row (nothing is cleared), the others zero their full slots
+int reset_rows_zero(cms_handle* h);
+// the arena holds at least need u16 units; keep: its allocated part
+// [0, t16_used) is copied over (else the table is dead: only the zero row
+// is restored)
+int arena_reserve(cms_handle* h, int64_t need, bool keep);
+// the arena and off[] of a new handle (cms_create)
+int init_row_offsets(cms_handle* h);
+// Compact layout of a fresh build (cms_build.hip): caps[r] (64-B units) ->
+// off[] after the zero row; returns the arena units in use.  Synchronises
+// h->stream (the plan's stream) to size the arena.
+int row_layout(cms_handle* h, const uint32_t* d_caps, uint32_t* d_scratch);
 // ---- collectives over the handle's communicator (cms_api.hip) ----
 // in-place u64 sum over all ranks (RCCL all-reduce or the caller transport)
 int coll_allreduce_u64(cms_handle* h, uint64_t* d_buf, int64_t count);

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
     const int64_t w0 = L.woff[o], nw = L.woff[o + 1] - w0;
     const int32_t slot = tv.hidx[o];
     const uint32_t* s32 = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
-    const uint16_t* s16 = tv.t16 + o * dw;
+    const uint16_t* s16 = tv.row16(o);
     if (use_img && (slot == kFormU16 || slot == kFormList)) {
       uint4* l4 = reinterpret_cast<uint4*>(img);
       if (slot == kFormList) {  // zeros, then each entry adds 1 into its half of an LDS word (counts < 2^8)
@@ -108,9 +108,22 @@ __global__ __launch_bounds__(256) void k_merge_pack(TableView tv, int64_t n, int
 // owner's fields are first scattered into an LDS image of its d x w u16
 // counters (one word read per F counters, no per-counter division), which
 // then leaves as 16-byte row-major stores while the norms are summed.
+// mforms (compact rows, row_layout by k_merge_caps): a narrow owner whose
+// field width b <= 8 (so every merged counter < 2^b) leaves as a u8 row, b <= 4
+// as a 4-bit row; an owner of b = 0 stays on the zero row.
+__global__ void k_merge_caps(const uint8_t* bits, const int32_t* hidx, int64_t n, int64_t dw, int mforms,
+                             uint32_t* caps) {
+  const uint32_t full = (uint32_t)(slot_units(dw) / kRowAlign);
+  for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < n; o += (int64_t)gridDim.x * blockDim.x) {
+    const int b = bits[o];
+    const int64_t u16s = !mforms || b > 8 ? slot_units(dw) : b > 4 ? dw / 2 : dw / 4;
+    caps[o] = hidx[o] >= 0 || b == 0 ? 0u : u16s == slot_units(dw) ? full : (uint32_t)((u16s + kRowAlign - 1) / kRowAlign);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int64_t n, HashParams hp, PackLayout L,
                                                       TableView tv, uint64_t* norm, uint32_t* rowmax, int use_img,
-                                                      int32_t* hidx_w) {
+                                                      int32_t* hidx_w, uint32_t* cbound, int mforms) {
   extern __shared__ __align__(16) uint16_t img[];  // [dw] (use_img)
   __shared__ uint64_t red[4];
   __shared__ uint32_t smax[4];
@@ -121,12 +134,13 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
     const int b = L.bits[o];
     const int32_t slot = tv.hidx[o];  // rows whose merged mass reaches 2^16 were promoted
     uint32_t* dst = slot >= 0 ? tv.hot + (int64_t)slot * dw : nullptr;
-    uint16_t* dst16 = tv.t16 + o * dw;
-    if (b == 0) {  // every rank's counters of this owner are zero
-      for (int64_t i = threadIdx.x; i < dw; i += 256) {
-        if (dst) dst[i] = 0u;
-        else dst16[i] = 0;
-      }
+    uint16_t* dst16 = tv.row16(o);
+    if (b == 0) {  // every rank's counters of this owner are zero (a compact row: the zero row)
+      if (dst || tv.off[o] != 0)
+        for (int64_t i = threadIdx.x; i < dw; i += 256) {
+          if (dst) dst[i] = 0u;
+          else dst16[i] = 0;
+        }
       if (threadIdx.x < hp.depth) norm[o * hp.depth + threadIdx.x] = 0;
       if (threadIdx.x == 0) {
         rowmax[o] = 0;
@@ -162,13 +176,29 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
       // a narrow row's sum of squares is at most mass * max < 2^32: u32 partial
       // sums by v_dot2_u32_u16 are exact; one wave atomic per row, one barrier
       u16x2 pm = {0, 0};
+      const int fm = mforms ? (b <= 4 ? 4 : b <= 8 ? 8 : 16) : 16;  // the stored form's counter bits
       for (int d = 0; d < hp.depth; ++d) {
         uint32_t sq = 0;
         const uint4* r4 = reinterpret_cast<const uint4*>(img + (int64_t)d * w);
         uint4* g4 = reinterpret_cast<uint4*>(dst16 + (int64_t)d * w);
+        uint2* g2 = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(dst16) + (int64_t)d * w);
+        uint32_t* g1 = reinterpret_cast<uint32_t*>(dst16) + (int64_t)d * (w >> 3);
         for (int j = threadIdx.x; j < (w >> 3); j += 256) {
-          const uint4 v = r4[j];
-          g4[j] = v;
+          const uint4 v = r4[j];  // counters 8j .. 8j + 7 of sketch row d
+          if (fm == 16) {
+            g4[j] = v;
+          } else if (fm == 8) {  // counter c at byte c
+            auto b4 = [](uint32_t x, uint32_t y) {
+              return (x & 0xFFu) | ((x >> 16) & 0xFFu) << 8 | (y & 0xFFu) << 16 | ((y >> 16) & 0xFFu) << 24;
+            };
+            g2[j] = make_uint2(b4(v.x, v.y), b4(v.z, v.w));
+          } else {  // counter c in bits 4 (c & 7) of word c / 8
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+            uint32_t q = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q |= ((x[k] & 0xFu) | ((x[k] >> 16) & 0xFu) << 4) << (8 * k);
+            g1[j] = q;
+          }
           const u16x2 a = __builtin_bit_cast(u16x2, v.x), bq = __builtin_bit_cast(u16x2, v.y),
                       c = __builtin_bit_cast(u16x2, v.z), e = __builtin_bit_cast(u16x2, v.w);
           sq = __builtin_amdgcn_udot2(a, a, sq, false);
@@ -184,6 +214,7 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
       vmax = max((uint32_t)pm.x, (uint32_t)pm.y);
       __syncthreads();
       if (threadIdx.x < hp.depth) norm[o * hp.depth + threadIdx.x] = s_sq[threadIdx.x];
+      if (threadIdx.x == 0 && fm < 16) hidx_w[o] = fm == 8 ? kFormU8 : kFormU4;  // (after the U16 default below)
     } else {
     for (int d = 0; d < hp.depth; ++d) {
       uint64_t sq = 0;
@@ -205,8 +236,11 @@ __global__ __launch_bounds__(256) void k_merge_unpack(const uint64_t* words, int
     if ((threadIdx.x & 63) == 0) smax[threadIdx.x >> 6] = vmax;
     __syncthreads();
     if (threadIdx.x == 0) {
-      rowmax[o] = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
-      if (slot < 0) hidx_w[o] = kFormU16;  // a u8 / nibble row now holds u16 merged counters
+      const uint32_t rm = max(max(smax[0], smax[1]), max(smax[2], smax[3]));
+      rowmax[o] = rm;
+      // a narrow row holds u16 merged counters, or (mforms) the u8 / 4-bit form set above
+      if (slot < 0 && !(mforms && use_img && b <= 8)) hidx_w[o] = kFormU16;
+      if (slot < 0) cbound[o] = rm;
     }
     __syncthreads();
   }
@@ -279,10 +313,21 @@ int merge_packed(cms_handle* h, const AllReduceU64& allreduce) {
   }
   // rows whose merged mass reaches 2^16 need u32 slots (row_mass is merged)
   if ((rc = promote_rows(h, h->d_row_mass, nullptr, false))) return rc;
+  // compact rows: the table's bytes now live in the packed words, so the
+  // narrow rows are laid out anew by their merged field widths
+  const int mforms = h->compact && use_img ? 1 : 0;
+  if (h->compact) {
+    CMS_HIP(h->ws_layout.ensure(sizeof(uint32_t) * (size_t)(2 * n + n / 4096 + 16)));
+    uint32_t* caps = h->ws_layout.as<uint32_t>();
+    hipLaunchKernelGGL(k_merge_caps, dim3(g), dim3(256), 0, h->stream, d_bits.as<uint8_t>(), h->d_hidx, n, dw, mforms,
+                       caps);
+    CMS_HIP(hipGetLastError());
+    if ((rc = row_layout(h, caps, caps + n))) return rc;
+  }
   {
     TimedScope ts(h, "merge_unpack");
     hipLaunchKernelGGL(k_merge_unpack, dim3(go), dim3(256), use_img ? img : 0, h->stream, packed.as<uint64_t>(), n,
-                       h->hp, L, h->tview(), h->d_norm, h->d_rowmax, use_img, h->d_hidx);
+                       h->hp, L, h->tview(), h->d_norm, h->d_rowmax, use_img, h->d_hidx, h->d_cbound, mforms);
     CMS_HIP(hipGetLastError());
   }
   h->norms_valid = true;  // the unpack wrote the merged norms

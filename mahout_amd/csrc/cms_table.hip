@@ -125,22 +125,31 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 // has keys -- the build rewrites every such row through its u16 / u32 image
 // even when all its increments are 0 (no mass added).  A listed row's cbound
 // becomes its bound after the write, which picks the form it widens to.
+// A touched row without a full slot (a compact row, or the zero row) is
+// listed too, whatever its bound: it moves to a slot of its own (mv[i], the
+// mover's index among cnt[1] movers) -- in-place adds need a whole slot.
 __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int64_t* lo, const int64_t* hi,
-                             const int32_t* hidx, uint32_t* cbound, int64_t n, int all_touched, int32_t* list,
-                             uint32_t* cnt) {
+                             const int32_t* hidx, const int64_t* off, uint32_t* cbound, int64_t n, int all_touched,
+                             int32_t* list, int32_t* mv, uint32_t* cnt) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = hidx[r];
-    if (f >= 0 || f == kFormU16) continue;
+    if (f >= 0) continue;
+    const bool full = (off[r] & kRowFull) != 0;
+    if (f == kFormU16 && full) continue;
     bool need = true;
     if (bound) {
       const uint64_t b = bound[r], m = old_mass ? old_mass[r] : 0ULL;
       const bool has_keys = lo && hi[r] > lo[r];
       if (b <= m && !has_keys) continue;  // no update lands on this row
       const uint64_t nb = (uint64_t)cbound[r] + (b - m);
-      need = all_touched || nb > (uint64_t)form_cap(f);
+      need = all_touched || nb > (uint64_t)form_cap(f) || !full;
       cbound[r] = (uint32_t)min<uint64_t>(nb, 0xFFFFFFFFull);  // <= the capacity of the form it keeps or takes
     }
-    if (need) list[atomicAdd(cnt, 1u)] = (int32_t)r;
+    if (need) {
+      const uint32_t i = atomicAdd(cnt, 1u);
+      list[i] = (int32_t)r;
+      mv[i] = full ? -1 : (int32_t)atomicAdd(cnt + 1, 1u);
+    }
   }
 }
 
@@ -160,7 +169,8 @@ __device__ __forceinline__ void pack16(const uint32_t (&v)[16], uint32_t* w32, i
   }
 }
 
-// One workgroup per listed row, rewritten in place in the narrowest form
+// One workgroup per listed row, rewritten (in place, or into a mover's new
+// slot at base + mv[i] * slot_units(dw)) in the narrowest form
 // wider than its own whose capacity holds its new bound (cbound), u16 for an
 // accumulate build (to_u16) -- a 2-bit row that one more pair lifts to 4
 // becomes a 4-bit row (half the bytes of u8, a quarter of u16).
@@ -171,8 +181,9 @@ __device__ __forceinline__ void pack16(const uint32_t (&v)[16], uint32_t* w32, i
 //  * list rows: every entry is read first (at most 32 per lane: d <= 32,
 //    m <= 256), then each sketch row is counted in LDS (u8 counters, four per
 //    word: a list row's counters are < 2^8) and leaves packed.
-__global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const uint32_t* dcount, TableView tv,
-                                                    int32_t* hidx, const uint32_t* cbound, int to_u16) {
+__global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const int32_t* mv, const uint32_t* dcount,
+                                                    TableView tv, int64_t* off_w, int64_t base, int32_t* hidx,
+                                                    const uint32_t* cbound, int to_u16) {
   extern __shared__ uint32_t lc[];  // [w / 4] (list rows)
   const int64_t count = *dcount;
   const int64_t dw = tv.dw;
@@ -190,8 +201,10 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
       else if (form_bits(f) < 8 && nb <= 255u) tf = kFormU8;
     }
     const int tb = form_bits(tf);
-    uint8_t* p8 = reinterpret_cast<uint8_t*>(tv.t16 + r * dw);
-    uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + r * dw);
+    const uint16_t* src = tv.row16(r);
+    const int64_t dst_off = mv[i] >= 0 ? base + (int64_t)mv[i] * slot_units(dw) : tv.base(r);
+    const uint8_t* p8 = reinterpret_cast<const uint8_t*>(src);
+    uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + dst_off);
     if (f == kFormList) {
       const uint32_t m = tv.list_m(r);
       const uint32_t ne = (uint32_t)(dw / w) * m;
@@ -200,7 +213,7 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
       for (int q = 0; q < 32; ++q) {
         const uint32_t t = threadIdx.x + 256u * q;
         ent[q] = 0xFFFFFFFFu;
-        if (t < ne) ent[q] = (t / m) << 16 | tv.t16[r * dw + 1 + t];  // sketch row, bucket
+        if (t < ne) ent[q] = (t / m) << 16 | src[1 + t];  // sketch row, bucket
       }
       const int cpw = 32 / tb;  // counters per output word
       for (int rr = 0; (int64_t)rr * w < dw; ++rr) {
@@ -224,7 +237,13 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
         const int64_t j = c0 + (int64_t)threadIdx.x * 16;  // this lane's 16 counters
         uint32_t v[16];
         if (j < dw) {
-          if (f == kFormU8) {
+          if (f == kFormU16) {  // a mover's u16 row (the zero row): copied
+            const uint4 x0 = *reinterpret_cast<const uint4*>(src + j);
+            const uint4 x1 = *reinterpret_cast<const uint4*>(src + j + 8);
+            const uint32_t wv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = (wv[q >> 1] >> ((q & 1) * 16)) & 0xFFFFu;
+          } else if (f == kFormU8) {
             const uint4 x = *reinterpret_cast<const uint4*>(p8 + j);
             const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -254,55 +273,78 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const u
         __syncthreads();  // the next (lower) chunk's old bytes are read after these stores
       }
     }
-    if (threadIdx.x == 0) hidx[r] = tf;
+    if (threadIdx.x == 0) {
+      hidx[r] = tf;
+      if (mv[i] >= 0) off_w[r] = dst_off | kRowFull;
+    }
   }
 }
 
 int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched, const int64_t* d_lo,
                const int64_t* d_hi) {
-  if (!h->forms_ok) return CMS_OK;
+  if (!h->forms_ok) return CMS_OK;  // (every row in a full slot, u16)
   const int64_t n = h->n;
   CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
+  CMS_HIP(h->ws_layout.ensure(sizeof(int32_t) * (size_t)(n + 2)));
   int32_t* list = h->ws_plist.as<int32_t>();
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(list + n);
-  CMS_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+  int32_t* mv = h->ws_layout.as<int32_t>();
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(mv + n);  // [0] listed rows, [1] movers
+  CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
   hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, d_lo, d_hi, h->d_hidx,
-                     h->d_cbound, n, all_touched ? 1 : 0, list, cnt);
-  // one workgroup per row, looping: the count stays on the device; u16 for
-  // an accumulate build or when no bound is known
+                     h->d_off, h->d_cbound, n, all_touched ? 1 : 0, list, mv, cnt);
+  CMS_HIP(hipGetLastError());
+  // movers get whole slots at the arena's end: their count sizes it (a
+  // handle without compact rows has none and skips the read-back)
+  int64_t base = h->t16_used;
+  if (h->compact) {
+    CMS_HIP(hipMemcpyAsync(h->h_pin + 8, cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+    CMS_HIP(hipStreamSynchronize(h->stream));
+    const int64_t movers = h->h_pin[8];
+    if (movers > 0) {
+      int rc = arena_reserve(h, h->t16_used + movers * slot_units(h->dw), true);
+      if (rc) return rc;
+      h->t16_used += movers * slot_units(h->dw);
+    }
+  }
+  // one workgroup per row, looping: the row count stays on the device; u16
+  // for an accumulate build or when no bound is known
   hipLaunchKernelGGL(k_widen_rows, dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(256), (size_t)h->p.width,
-                     h->stream, list, cnt, h->tview(), h->d_hidx, h->d_cbound, (all_touched || !d_bound) ? 1 : 0);
+                     h->stream, list, mv, cnt, h->tview(), h->d_off, base, h->d_hidx, h->d_cbound,
+                     (all_touched || !d_bound) ? 1 : 0);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
 
-// [0..5] hot, u16, u8, 4-bit, 2-bit, 1-bit rows, [6] list rows, [7] their bytes
+// [0..5] hot, u16, u8, 4-bit, 2-bit, 1-bit rows, [6] list rows, [7] their
+// bytes, [8] u16 rows on the shared zero row (counted in [1] too)
 __global__ void k_count_forms(TableView tv, int64_t n, unsigned long long* out) {
-  uint32_t c[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint32_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long lb = 0;
   const uint64_t d = (uint64_t)(tv.dw / tv.w);
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = tv.hidx[r];
     c[f >= 0 ? 0 : f == kFormU16 ? 1 : f == kFormU8 ? 2 : f == kFormU4 ? 3 : f == kFormU2 ? 4 : f == kFormU1 ? 5 : 6] += 1;
     if (f == kFormList) lb += 2 + 2 * d * tv.list_m(r);
+    if (f == kFormU16 && tv.off[r] == 0) c[7] += 1;
   }
   for (int q = 0; q < 7; ++q)
     if (c[q]) atomicAdd(out + q, (unsigned long long)c[q]);
   if (lb) atomicAdd(out + 7, lb);
+  if (c[7]) atomicAdd(out + 8, (unsigned long long)c[7]);
 }
 
-int count_forms(cms_handle* h, int64_t out[8]) {
+int count_forms(cms_handle* h, int64_t out[9]) {
   DevBuf tmp;
-  CMS_HIP(tmp.ensure(8 * sizeof(unsigned long long)));
-  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 8 * sizeof(unsigned long long), h->stream));
+  CMS_HIP(tmp.ensure(9 * sizeof(unsigned long long)));
+  CMS_HIP(hipMemsetAsync(tmp.ptr, 0, 9 * sizeof(unsigned long long), h->stream));
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 4096));
   hipLaunchKernelGGL(k_count_forms, dim3(g), dim3(256), 0, h->stream, h->tview(), h->n, tmp.as<unsigned long long>());
   CMS_HIP(hipGetLastError());
-  unsigned long long c[8];
+  unsigned long long c[9];
   CMS_HIP(hipMemcpyAsync(c, tmp.ptr, sizeof(c), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
-  for (int q = 0; q < 8; ++q) out[q] = (int64_t)c[q];
+  for (int q = 0; q < 9; ++q) out[q] = (int64_t)c[q];
   return CMS_OK;
 }
 
@@ -351,7 +393,7 @@ __global__ void k_read_lists(TableView tv, int64_t r0, int64_t rc, uint32_t* out
     if (tv.hidx[r0 + r] != kFormList) continue;
     const uint32_t m = tv.list_m(r0 + r);
     const int64_t ne = (tv.dw / tv.w) * (int64_t)m;
-    const uint16_t* e = tv.t16 + (r0 + r) * tv.dw + 1;
+    const uint16_t* e = tv.row16(r0 + r) + 1;
     for (int64_t t = threadIdx.x; t < ne; t += blockDim.x)
       atomicAdd(out + r * tv.dw + (t / m) * tv.w + e[t], 1u);
   }
@@ -377,6 +419,105 @@ int read_counters_device(cms_handle* h, int64_t r0, int64_t rc, uint32_t* d_out)
 int reset_table_layout(cms_handle* h) {
   CMS_HIP(hipMemsetAsync(h->d_hidx, 0xff, sizeof(int32_t) * (size_t)h->n, h->stream));
   h->hot_used = 0;
+  return CMS_OK;
+}
+
+// ---- the narrow-row arena (cms_internal.h TableView) ----
+
+__global__ void k_off_identity(int64_t* off, int64_t n, int64_t su) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    off[r] = (su + r * su) | kRowFull;
+}
+
+int arena_reserve(cms_handle* h, int64_t need, bool keep) {
+  const int64_t su = slot_units(h->dw);
+  need = std::max(need, su);
+  if (need <= h->t16_cap) return CMS_OK;
+  // a growing arena takes some headroom (bounded by every row in a slot of its own)
+  int64_t cap = need;
+  if (keep) cap = std::max(need, std::min<int64_t>(h->t16_cap + h->t16_cap / 2, su * (h->n + 1) + h->t16_used));
+  uint16_t* nb = nullptr;
+  hipError_t e = hipMalloc((void**)&nb, sizeof(uint16_t) * (size_t)cap);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(CMS_E_OOM, "row arena of %.2f GB: %s", 2e-9 * (double)cap, hipGetErrorString(e));
+  }
+  if (keep && h->t16_used > 0) {
+    CMS_HIP(hipMemcpyAsync(nb, h->d_t16, sizeof(uint16_t) * (size_t)h->t16_used, hipMemcpyDeviceToDevice, h->stream));
+  } else {
+    CMS_HIP(hipMemsetAsync(nb, 0, sizeof(uint16_t) * (size_t)su, h->stream));  // the zero row
+  }
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  if (h->d_t16) CMS_HIP(hipFree(h->d_t16));
+  h->d_t16 = nb;
+  h->t16_cap = cap;
+  return CMS_OK;
+}
+
+int init_row_offsets(cms_handle* h) {
+  const int64_t su = slot_units(h->dw);
+  if (h->compact) {  // every row on the zero row until a build lays it out
+    int rc = arena_reserve(h, su, false);
+    if (rc) return rc;
+    CMS_HIP(hipMemsetAsync(h->d_off, 0, sizeof(int64_t) * (size_t)h->n, h->stream));
+    h->t16_used = su;
+  } else {  // a full slot per row, in row order
+    int rc = arena_reserve(h, su * (h->n + 1), false);
+    if (rc) return rc;
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((h->n + 255) / 256, 8192));
+    hipLaunchKernelGGL(k_off_identity, dim3(g), dim3(256), 0, h->stream, h->d_off, h->n, su);
+    CMS_HIP(hipGetLastError());
+    h->t16_used = su * (h->n + 1);
+  }
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  return CMS_OK;
+}
+
+int reset_rows_zero(cms_handle* h) {
+  const int64_t su = slot_units(h->dw);
+  if (h->compact) {
+    CMS_HIP(hipMemsetAsync(h->d_off, 0, sizeof(int64_t) * (size_t)h->n, h->stream));
+    h->t16_used = su;
+  } else {
+    CMS_HIP(hipMemsetAsync(h->d_t16 + su, 0, sizeof(uint16_t) * (size_t)(su * h->n), h->stream));
+  }
+  return reset_table_layout(h);
+}
+
+// off[r] from the rows' capacities (64-B units): the rows follow the zero
+// row in row order; a row of capacity 0 (a hot row) points at the zero row
+__global__ void k_row_offsets(const uint32_t* caps, const uint32_t* ex, int64_t n, int64_t su, int64_t* off,
+                              uint32_t* total) {
+  const int64_t full_units = su / kRowAlign;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = caps[r];
+    off[r] = c ? (su + (int64_t)ex[r] * kRowAlign) | (c == full_units ? kRowFull : 0) : 0;
+    if (r == n - 1) *total = ex[r] + c;
+  }
+}
+
+int row_layout(cms_handle* h, const uint32_t* d_caps, uint32_t* d_scratch) {
+  const int64_t n = h->n, su = slot_units(h->dw);
+  if (n <= 0) return CMS_OK;
+  uint32_t* ex = d_scratch;           // [n]
+  uint32_t* total = d_scratch + n;    // [1]
+  uint32_t* bsum = d_scratch + n + 4; // [n / 4096 + 1]
+  int rc = scan_exclusive_u32(h, d_caps, ex, n, bsum);
+  if (rc) return rc;
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(k_row_offsets, dim3(g), dim3(256), 0, h->stream, d_caps, ex, n, su, h->d_off, total);
+  CMS_HIP(hipGetLastError());
+  CMS_HIP(hipMemcpyAsync(h->h_pin + 8, total, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
+  CMS_HIP(hipStreamSynchronize(h->stream));
+  const int64_t used = su + (int64_t)h->h_pin[8] * kRowAlign;
+  const int64_t want = used + used / 16;  // (a little headroom for the next build)
+  if (h->t16_cap > 4 * want) {  // an arena grown by earlier writers shrinks back (its rows are dead)
+    CMS_HIP(hipFree(h->d_t16));
+    h->d_t16 = nullptr;
+    h->t16_cap = 0;
+  }
+  if ((rc = arena_reserve(h, want, false))) return rc;
+  h->t16_used = used;
   return CMS_OK;
 }
 

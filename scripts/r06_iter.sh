@@ -3,6 +3,8 @@
 #   tests   -- pytest -m gpu ($TESTS, default tests/)
 #   smoke   -- __graft_entry__.smoke()
 #   trace   -- rocprofv3 kernel trace + stats of the headline ingest
+#   prof_ingest / prof_cosine -- scripts/profile_r06.sh passes, summarized
+#              into profiles/r06 (the bench step after them reads those)
 #   ab      -- headline ingest bench per arm (ARMS: main, ab/*.so variant
 #              libraries, env:NAME=VALUE arms)
 #   bench   -- the full bench
@@ -70,7 +72,8 @@ for step in $STEPS; do
       bash scripts/profile_r06.sh ingest || exit 1
       python3 scripts/summarize_profile.py gpurun_out/prof_ingest r06 || exit 1 ;;
     prof_cosine)
-      bash scripts/profile_r06.sh cosine || exit 1 ;;
+      bash scripts/profile_r06.sh cosine || exit 1
+      python3 scripts/summarize_cos_pmc.py gpurun_out/prof_cosine r06 || exit 1 ;;
     bench)
       timeout -k 10 700 python bench.py --steps 10 --warmup 3 --detail-out gpurun_out/bench_detail.json > gpurun_out/bench.json 2> gpurun_out/bench.err \
         || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }

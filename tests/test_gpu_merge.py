@@ -92,11 +92,14 @@ def _worker(rank, world, port, q, case):
         exp = O.similarities_row(full, 1)
         exp[1] = O.cosine_cm(full[1], full[1])
         ok_t = bool(np.array_equal(got, full))
-        # k_merge_unpack writes every narrow row back as u16 (hidx kFormU16) or a hot slot
+        # k_merge_unpack writes every narrow row back as u16 (hidx kFormU16) or a
+        # hot slot -- or, with compact rows (w % 32 == 0), as u8 / 4-bit rows
+        # where the merged field width allows (never 1-/2-bit or list rows)
         forms = ("bit_rows", "crumb_rows", "nibble_rows", "u8_rows")
         if w % 32 == 0 and npairs // world >= 262144:  # a bulk build per rank: narrow forms exist before the merge
             ok_t = ok_t and sum(pre[f] for f in forms) > 0
-        ok_t = ok_t and all(post[f] == 0 for f in forms)
+        after = ("bit_rows", "crumb_rows", "list_rows") if w % 32 == 0 else forms
+        ok_t = ok_t and all(post[f] == 0 for f in after)
         ok_s = bool(np.all((sims == exp) | (np.isnan(sims) & np.isnan(exp))))
         if refresh_k:
             ids, sc, cnt = lists
