@@ -113,6 +113,9 @@ int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, i
  * never again (a handle's behaviour is fixed at creation); none changes any
  * result, only the storage or kernel a result comes from:
  *   CMS_NO_FORMS=1        narrow rows stay u16 (no 1/2/4/8-bit row forms)
+ *   CMS_NO_COMPACT=1      every narrow row keeps a whole u16 slot (no compact row layout)
+ *   CMS_NO_VMM=1          the compact row arena as one hipMalloc grown by copying
+ *                         (no reserved virtual range mapped in chunks)
  *   CMS_BIT_KEYS=<n>      byte-class owners of <= n keys try 1-bit rows first (64)
  *   CMS_CRUMB_KEYS=<n>    ... of <= n keys 2-bit rows (256)
  *   CMS_LIST_KEYS=<n>     ... of <= n keys, unit increments: sparse list rows (256; 0 = none)
@@ -450,7 +453,7 @@ typedef struct cms_stats {
   int32_t depth, width;
   int32_t exact_norms;      /* 1 if every (owner,row) norm is < 2^53 (bit-exact fast path) */
   int32_t world, rank;
-  int64_t table_bytes;       /* narrow-row arena allocation + the u32 rows of the hot owners */
+  int64_t table_bytes;       /* the narrow rows' arena as laid out (zero row + every row's place) + the hot owners' u32 rows */
   int64_t multi_limb_owners; /* owners with a counter >= 128 (all-pairs limb split; -1 before the first all-pairs call) */
   int64_t topk_redo;         /* top-k rows that needed the radix-select fallback */
   int64_t deep_limb_owners;  /* of those, owners with a counter >= 2^14 (3+ limbs); -1 before */

@@ -358,6 +358,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.po_no_bigq = num("CMS_PO_NO_BIGQ", h->tune.po_no_bigq);
     h->tune.forms = !flag("CMS_NO_FORMS");
     h->tune.no_compact = flag("CMS_NO_COMPACT");
+    h->tune.no_vmm = flag("CMS_NO_VMM");
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");
     h->tune.mls = !flag("CMS_NO_MLS");
@@ -475,7 +476,8 @@ void cms_destroy(cms_handle* h) {
   if (h->ev_join2) (void)hipEventDestroy(h->ev_join2);
   free_query_pool(h);
   if (h->comm) (void)ncclCommDestroy(h->comm);
-  void* bufs[] = {h->d_t16, h->d_off, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
+  arena_release(h);
+  void* bufs[] = {h->d_off, h->d_t64, h->d_hidx, h->d_cbound, h->d_row_mass, h->d_norm, h->d_norm_sqrt, h->d_rowmax, h->d_flags, h->d_owner_ids};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->h_pin) (void)hipHostFree(h->h_pin);
@@ -1765,7 +1767,7 @@ int cms_get_stats(cms_handle* h, cms_stats* out) {
   const int64_t hot_rows = forms[0];
   out->table_bytes = h->per_owner ? (int64_t)h->po_sk.bytes
                     : h->f64      ? (int64_t)sizeof(double) * h->n * h->dw
-                                  : (int64_t)sizeof(uint16_t) * h->t16_cap + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
+                                  : (int64_t)sizeof(uint16_t) * h->t16_used + (int64_t)sizeof(uint32_t) * hot_rows * h->dw;
   out->multi_limb_owners = h->mfma_ready ? (int64_t)h->n_hot_limb : -1;
   out->topk_redo = h->topk_redo;
   out->deep_limb_owners = h->mfma_ready ? h->vl[0].o1 - h->vl[0].o0 : -1;

@@ -236,6 +236,7 @@ struct Tunables {
   int slice_reduce = 0;     // CMS_SLICE_REDUCE=1: split owners' slices leave u16 images summed by k_slice_reduce (no slot atomics)
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool no_compact = false; // CMS_NO_COMPACT=1: every narrow row keeps a whole u16 slot (no compact layout)
+  bool no_vmm = false;     // CMS_NO_VMM=1: the compact arena as one hipMalloc grown by copying (no virtual range)
   bool hot_routing = true; // CMS_NO_HOT_ROUTING=1: the partition sends every owner through both passes
   bool fp4 = true;         // CMS_NO_FP4=1: no e2m1 operand image (every single-limb pair on int8)
   bool mls = true;         // CMS_NO_MLS=1: multi-limb slabs on the 128-tile kernel instead of k_cosine_mls
@@ -276,6 +277,17 @@ struct cms_handle {
   uint16_t* d_t16 = nullptr;        // arena of the narrow rows (TableView; [0, slot_units(dw)) the zero row)
   int64_t t16_cap = 0, t16_used = 0;  // arena capacity and end of the allocated part (u16 units)
   int64_t* d_off = nullptr;         // [n] arena offset of each narrow row | kRowFull
+  // compact handles: the arena is a reserved virtual range whose physical
+  // memory is mapped (and unmapped) in chunks at its end -- growing never
+  // copies and the base never moves (arena_reserve); without the virtual
+  // memory API it is one hipMalloc grown by copying
+  struct ArenaChunk {
+    hipMemGenericAllocationHandle_t mem;
+    size_t bytes;
+  };
+  void* arena_va = nullptr;
+  size_t arena_va_bytes = 0, arena_mapped = 0, arena_gran = 0;
+  std::vector<ArenaChunk> arena_chunks;
   bool compact = false;             // forms_ok: fresh builds lay the rows out compactly (row_layout)
   bool f64 = false;                 // CMS_COUNTER_F64: fp64 counters in d_t64 (cms_f64.hip), no u16/u32 table
   double* d_t64 = nullptr;          // [n][d][w] fp64 counters
@@ -500,6 +512,8 @@ int reset_rows_zero(cms_handle* h);
 int arena_reserve(cms_handle* h, int64_t need, bool keep);
 // the arena and off[] of a new handle (cms_create)
 int init_row_offsets(cms_handle* h);
+// unmaps and frees the arena (cms_destroy)
+void arena_release(cms_handle* h);
 // Compact layout of a fresh build (cms_build.hip): caps[r] (64-B units) ->
 // off[] after the zero row; returns the arena units in use.  Synchronises
 // h->stream (the plan's stream) to size the arena.

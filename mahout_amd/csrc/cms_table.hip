@@ -283,6 +283,7 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const i
 int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass, bool all_touched, const int64_t* d_lo,
                const int64_t* d_hi) {
   if (!h->forms_ok) return CMS_OK;  // (every row in a full slot, u16)
+  TimedScope ts(h, "widen_rows");
   const int64_t n = h->n;
   CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
   CMS_HIP(h->ws_layout.ensure(sizeof(int32_t) * (size_t)(n + 2)));
@@ -429,9 +430,89 @@ __global__ void k_off_identity(int64_t* off, int64_t n, int64_t su) {
     off[r] = (su + r * su) | kRowFull;
 }
 
+// Virtual arena: physical chunks mapped at the end of the reserved range.
+static int arena_map(cms_handle* h, size_t want) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = h->device;
+  const size_t g = h->arena_gran;
+  const size_t bytes = std::min(h->arena_va_bytes - h->arena_mapped, (want - h->arena_mapped + g - 1) / g * g);
+  if (h->arena_mapped + bytes < want) return set_error(CMS_E_OOM, "row arena: %.2f GB exceeds its reserved range", 1e-9 * want);
+  hipMemGenericAllocationHandle_t mem;
+  hipError_t e = hipMemCreate(&mem, bytes, &prop, 0);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return set_error(CMS_E_OOM, "row arena chunk of %.2f GB: %s", 1e-9 * bytes, hipGetErrorString(e));
+  }
+  char* at = static_cast<char*>(h->arena_va) + h->arena_mapped;
+  hipMemAccessDesc acc = {};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  // (access is set over the whole mapped range from the reservation's start:
+  // on this ROCm a sub-range starting inside it is refused once other
+  // allocations exist -- scripts/vmm_probe.cpp)
+  if ((e = hipMemMap(at, bytes, 0, mem, 0)) != hipSuccess ||
+      (e = hipMemSetAccess(h->arena_va, h->arena_mapped + bytes, &acc, 1)) != hipSuccess) {
+    (void)hipMemUnmap(at, bytes);
+    (void)hipMemRelease(mem);
+    (void)hipGetLastError();
+    return set_error(CMS_E_HIP, "row arena map: %s", hipGetErrorString(e));
+  }
+  h->arena_chunks.push_back({mem, bytes});
+  h->arena_mapped += bytes;
+  return CMS_OK;
+}
+
+// unmaps trailing chunks wholly above `keep_bytes` (the caller has drained the stream)
+static void arena_unmap_above(cms_handle* h, size_t keep_bytes) {
+  while (!h->arena_chunks.empty()) {
+    const auto c = h->arena_chunks.back();
+    if (h->arena_mapped - c.bytes < keep_bytes) break;
+    char* at = static_cast<char*>(h->arena_va) + (h->arena_mapped - c.bytes);
+    (void)hipMemUnmap(at, c.bytes);
+    (void)hipMemRelease(c.mem);
+    h->arena_chunks.pop_back();
+    h->arena_mapped -= c.bytes;
+  }
+}
+
+void arena_release(cms_handle* h) {
+  if (h->arena_va) {
+    arena_unmap_above(h, 0);
+    (void)hipMemAddressFree(h->arena_va, h->arena_va_bytes);
+    h->arena_va = nullptr;
+    h->d_t16 = nullptr;  // (not a hipMalloc pointer)
+  } else if (h->d_t16) {
+    (void)hipFree(h->d_t16);
+    h->d_t16 = nullptr;
+  }
+}
+
 int arena_reserve(cms_handle* h, int64_t need, bool keep) {
   const int64_t su = slot_units(h->dw);
   need = std::max(need, su);
+  if (h->arena_va) {
+    const size_t want = sizeof(uint16_t) * (size_t)need;
+    if (!keep && h->arena_mapped > 4 * want + h->arena_gran) {  // a re-laid-out table gives back what it no longer needs
+      CMS_HIP(hipDeviceSynchronize());
+      arena_unmap_above(h, want);
+    }
+    if (want > h->arena_mapped) {
+      const bool first = h->arena_mapped == 0;
+      // a growing table (rows moving to slots) maps a quarter more than it needs
+      const size_t ask = keep ? std::min(h->arena_va_bytes, want + want / 4) : want;
+      if (int rc = arena_map(h, std::max(ask, want))) return rc;
+      if (first) CMS_HIP(hipMemsetAsync(h->arena_va, 0, sizeof(uint16_t) * (size_t)su, h->stream));  // the zero row
+    }
+    h->t16_cap = (int64_t)(h->arena_mapped / sizeof(uint16_t));
+    return CMS_OK;
+  }
+  if (!keep && h->t16_cap > 4 * need) {  // a re-laid-out table shrinks back (its rows are dead)
+    CMS_HIP(hipFree(h->d_t16));
+    h->d_t16 = nullptr;
+    h->t16_cap = 0;
+  }
   if (need <= h->t16_cap) return CMS_OK;
   // a growing arena takes some headroom (bounded by every row in a slot of its own)
   int64_t cap = need;
@@ -456,6 +537,29 @@ int arena_reserve(cms_handle* h, int64_t need, bool keep) {
 
 int init_row_offsets(cms_handle* h) {
   const int64_t su = slot_units(h->dw);
+  if (h->compact && !h->tune.no_vmm) {
+    // the virtual range: room for a compact layout plus every row moved once
+    // to a whole slot of its own (2 x a slot per row); physical chunks map on demand
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = h->device;
+    size_t g = 0;
+    if (hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended) == hipSuccess && g > 0) {
+      // map in chunks of 64 MB multiples (a small table: 1/64 of its slot layout)
+      const size_t slots = sizeof(uint16_t) * (size_t)su * (size_t)(h->n + 1);
+      g = std::max(g, std::min<size_t>(size_t(64) << 20, (slots / 64 + g - 1) / g * g));
+      const size_t va = ((size_t)4 * sizeof(uint16_t) * (size_t)su * (size_t)(h->n + 1) + 2 * g) / g * g;
+      void* p = nullptr;
+      if (hipMemAddressReserve(&p, va, g, nullptr, 0) == hipSuccess) {
+        h->arena_va = p;
+        h->arena_va_bytes = va;
+        h->arena_gran = g;
+        h->d_t16 = static_cast<uint16_t*>(p);
+      }
+    }
+    (void)hipGetLastError();  // (no virtual memory API: the hipMalloc arena)
+  }
   if (h->compact) {  // every row on the zero row until a build lays it out
     int rc = arena_reserve(h, su, false);
     if (rc) return rc;
@@ -511,12 +615,7 @@ int row_layout(cms_handle* h, const uint32_t* d_caps, uint32_t* d_scratch) {
   CMS_HIP(hipStreamSynchronize(h->stream));
   const int64_t used = su + (int64_t)h->h_pin[8] * kRowAlign;
   const int64_t want = used + used / 16;  // (a little headroom for the next build)
-  if (h->t16_cap > 4 * want) {  // an arena grown by earlier writers shrinks back (its rows are dead)
-    CMS_HIP(hipFree(h->d_t16));
-    h->d_t16 = nullptr;
-    h->t16_cap = 0;
-  }
-  if ((rc = arena_reserve(h, want, false))) return rc;
+  if ((rc = arena_reserve(h, want, false))) return rc;  // (an arena grown by earlier writers shrinks back)
   h->t16_used = used;
   return CMS_OK;
 }
