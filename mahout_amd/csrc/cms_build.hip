@@ -581,6 +581,12 @@ constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
 #ifndef CMS_MID_ROW_PREFETCH
 #define CMS_MID_ROW_PREFETCH 0
 #endif
+// register-cached owners keep their keys' d buckets (u16 pairs) from one
+// all-rows hash, so the u8 / u16 row passes (an escalation from 4-bit, or an
+// owner starting at u8) do not hash again
+#ifndef CMS_MID_BKT_CACHE
+#define CMS_MID_BKT_CACHE 0
+#endif
 template <int SV, int D, int MT>
 // 4 waves per SIMD: the key prefetch needs more than the 80 VGPRs of 6
 // (it spilled there); the build measured the same (profiles/r04/ab_*_s5)
@@ -591,6 +597,8 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     int u8img) {
   constexpr int MTH = MT;                   // threads per owner (a workgroup)
   constexpr int MKR = kKeyRegs * 256 / MT;  // key registers per thread: 1024 keys cached per owner
+  constexpr bool kBc = CMS_MID_BKT_CACHE && D > 0 && MKR <= 4;  // cached buckets (w <= 65536: u16)
+  constexpr int kBcW = kBc ? (D + 1) / 2 : 1;                   // u16 pairs per key
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
   __shared__ unsigned long long s_mass;
@@ -604,6 +612,8 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     const bool cached = (hi - lo) <= (int64_t)MTH * MKR;
     uint64_t kp[MKR];
     uint32_t ik[MKR];
+    uint32_t bc[MKR][kBcW];  // kBc: key k's bucket in sketch row r at bits 16 (r & 1) of bc[k][r / 2]
+    bool have_bc = false;
     uint64_t mass = 0;
     bool badv = false;
     if (cached) {
@@ -670,8 +680,9 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       const bool tele = D > 0 && as_list;
       // lt >= 0: the key's list index -- a list row's entries leave during
       // the count (a count past 255 later rewrites the slot as u16 rows)
-      auto add_all = [&](uint64_t kr, uint32_t inc, int64_t lt) {
+      auto add_all = [&](uint64_t kr, uint32_t inc, int64_t lt, uint32_t* bcache) {
         each_bucket<D>(hp, kr, [&](int d, uint32_t bk) {
+          if (kBc && bcache) bcache[d >> 1] = (d & 1) ? (bcache[d >> 1] | bk << 16) : bk;
           if (lt >= 0) lst[1 + (int64_t)d * m + lt] = (uint16_t)bk;
           const uint32_t c = (uint32_t)d * (uint32_t)w + bk;
           const uint32_t sh = (c & ((1u << lga) - 1u)) * (uint32_t)ab;
@@ -685,7 +696,8 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
       if (cached) {
 #pragma unroll
         for (int k = 0; k < MKR; ++k)
-          if (ik[k]) add_all(kp[k], ik[k], as_list ? (int64_t)(tid + k * MTH) : int64_t(-1));
+          if (ik[k]) add_all(kp[k], ik[k], as_list ? (int64_t)(tid + k * MTH) : int64_t(-1), kBc ? bc[k] : nullptr);
+        have_bc = kBc;
       } else {
         // the next step's key loads go out before this step's keys are added
         constexpr int64_t kStep = 4 * MTH;
@@ -718,7 +730,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
           if (base + kStep < hi) fetch(base + kStep);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            if (inc4[u]) add_all(keys.resolve(kk[u]), inc4[u], -1);
+            if (inc4[u]) add_all(keys.resolve(kk[u]), inc4[u], -1, nullptr);
             mass += inc4[u];
           }
         }
@@ -863,6 +875,15 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
     // the 4-bit image overflowed (or was skipped): one sketch row at a time, u8 then u16
     if (level < 0) level = start > 1 || u8_failed ? 2 : 1;
     else level = -level - 1;  // done: mark so the row passes are skipped
+    if (kBc && cached && level >= 0 && !have_bc) {  // all d buckets of the cached keys, once
+#pragma unroll
+      for (int k = 0; k < MKR; ++k)
+        if (ik[k])
+          each_bucket<D>(hp, kp[k], [&](int d, uint32_t bk) {
+            bc[k][d >> 1] = (d & 1) ? (bc[k][d >> 1] | bk << 16) : bk;
+          });
+      have_bc = true;
+    }
     for (;;) {
       if (level < 0) break;  // an all-rows image held every counter
       const int bits = 4 << level;
@@ -882,8 +903,14 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         __syncthreads();
         uint64_t sq = 0;
         bool ovf = false;
-        auto add = [&](uint64_t kr, uint32_t inc) {
-          const uint32_t c = bucket(hp, d, kr);
+        auto add = [&](uint64_t kr, uint32_t inc, const uint32_t* bcache) {
+          uint32_t c;
+          if (kBc && bcache) {  // the cached pair of row d: a select chain (d is not a compile-time index here)
+            const uint32_t pr = d < 2 ? bcache[0] : (d < 4 || kBcW < 3) ? bcache[kBcW > 1 ? 1 : 0] : bcache[kBcW - 1];
+            c = (pr >> ((d & 1) << 4)) & 0xFFFFu;
+          } else {
+            c = bucket(hp, d, kr);
+          }
           const uint32_t sh = (c & ((1u << lg) - 1u)) * (uint32_t)bits;
           const uint32_t old = (atomicAdd(&lds[c >> lg], inc << sh) >> sh) & cap;
           const uint32_t nv = old + inc;
@@ -894,7 +921,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
         if (cached) {
 #pragma unroll
           for (int k = 0; k < MKR; ++k)
-            if (ik[k]) add(kp[k], ik[k]);
+            if (ik[k]) add(kp[k], ik[k], kBc && have_bc ? bc[k] : nullptr);
         } else {
 #if CMS_MID_ROW_PREFETCH
           // the next step's key loads go out before this step's keys are
@@ -939,7 +966,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              if (inc4[u]) add(kk[u], inc4[u]);
+              if (inc4[u]) add(kk[u], inc4[u], nullptr);
               if (mass_pending) mass += inc4[u];
             }
           }

@@ -78,22 +78,22 @@ struct PendingEvent {
 // slot at the arena's end (widen_rows relocates it), so in-place adds only
 // ever touch full slots.  Handles without forms keep every row in a full slot.
 //
-// Narrow FORMS: a fresh build stores a row whose counters are all
-// below 2^8 as u8 in the first dw bytes of its slot, and one whose counters
-// are all below 2^4 as packed nibbles (counter j in bits 4*(j&1) of byte j/2)
-// in the first dw/2 bytes, and one whose counters are all below 2^2 as 2-bit
-// counters (counter j in bits 2*(j&3) of byte j/4) in the first dw/4 bytes,
-// and one whose counters are all 0 or 1 as bits (counter j in bit j&7 of
-// byte j/8) in the first dw/8 bytes -- at config 3 most of the 1M owners, so the build
-// writes a fraction of the u16 bytes.  hidx[row] names the form (< 0) or the
-// hot slot (>= 0).  cbound[row] (u32) bounds a form row's counters; a writer
-// widens a form row to u16 in place (widen_rows) before its bound could pass
-// the form's capacity.  Forms exist only when dw % 32 == 0 (every slot and
-// every nibble row then starts 64-byte aligned).
+// Narrow FORMS: a fresh build stores a row whose counters are all below 2^8
+// as u8 (dw bytes at its offset), one whose counters are all below 2^4 as
+// packed nibbles (counter j in bits 4*(j&1) of byte j/2; dw/2 bytes), one
+// whose counters are all below 2^2 as 2-bit counters (counter j in bits
+// 2*(j&3) of byte j/4; dw/4 bytes), and one whose counters are all 0 or 1 as
+// bits (counter j in bit j&7 of byte j/8; dw/8 bytes) -- at config 3 most of
+// the 1M owners, so the build writes a fraction of the u16 bytes.  hidx[row]
+// names the form (< 0) or the hot slot (>= 0).  cbound[row] (u32) bounds a
+// form row's counters; a writer widens a form row (widen_rows: in place in a
+// whole slot, else into a new one) before its bound could pass the form's
+// capacity.  Forms exist only when dw % 32 == 0 (every row then starts
+// 64-byte aligned, every nibble row holds whole 16-B words).
 //
 // LIST rows (kFormList): the smallest owners of a fresh build with unit
-// increments are stored sparse -- slot[0] = m, the owner's key count, then
-// for each sketch row r the m buckets its keys hash to, slot[1 + r m + t]
+// increments are stored sparse -- row[0] = m, the owner's key count, then
+// for each sketch row r the m buckets its keys hash to, row[1 + r m + t]
 // (u16, unsorted, repeats allowed): counter (r, j) is the number of entries
 // of row r equal to j.  2 + 2 d m bytes instead of a dense row (config 3: an
 // owner of 100 keys takes 1 KB instead of the 10 KB of its 2-bit rows).  A
