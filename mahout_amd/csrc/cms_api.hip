@@ -437,7 +437,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   // (the byte-class and mid kernels store whole 16-B words of a 4-bit sketch
   // row: w % 32 == 0)
   h->forms_ok = !per_owner && !f64 && h->p.width % 32 == 0 && h->tune.forms;
-  // compact rows (cms_internal.h TableView) when the layout's 64-B units fit
+  // compact rows (cms_internal.h TableView) when the layout's 128-B units fit
   // the u32 scan; the arena then starts as the zero row alone
   h->compact = h->forms_ok && !h->tune.no_compact &&
                (double)h->n * (double)(slot_units(h->dw) / kRowAlign + 1) < 4.0e9;

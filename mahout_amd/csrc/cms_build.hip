@@ -1332,7 +1332,7 @@ __host__ __device__ __forceinline__ bool nib_list_row(int64_t m, int w, int d, b
 }
 
 // Compact layout of a fresh build (row_layout): each row's arena capacity in
-// 64-B units, by what its class's kernel can store -- a hot row nothing (its
+// 128-B units, by what its class's kernel can store -- a hot row nothing (its
 // counters are u32 slot rows), a byte-class row its list entries or its u8
 // image (k_build_nibbles' forms up to k_build_bytes' u8 rows), any other row
 // (the mid class, or every row without forms) a whole u16 slot (kRowFull).

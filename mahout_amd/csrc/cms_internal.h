@@ -69,7 +69,7 @@ struct PendingEvent {
 // bound can reach 2^16 (promote_rows), so a u16 counter never overflows.
 //
 // ROW STORAGE: the narrow rows live in one arena (t16) at per-row offsets
-// (off[row], u16 units, 64-B aligned; bit 0 = kRowFull: the row owns a whole
+// (off[row], u16 units, 128-B aligned; bit 0 = kRowFull: the row owns a whole
 // u16 slot of dw counters there).  Offset 0 is a shared row of zeros that
 // every row of an empty table points to.  A fresh build with forms lays the
 // rows out compactly (row_layout: each row gets what its form can need -- a
@@ -107,7 +107,7 @@ constexpr uint32_t form_cap(int32_t form) {
 }
 
 constexpr int64_t kRowFull = 1;  // off[row] bit 0: the row owns a whole u16 slot (in-place writes allowed)
-constexpr int64_t kRowAlign = 32;  // u16 units (64 B) per arena allocation unit
+constexpr int64_t kRowAlign = 64;  // u16 units (128 B: an L2 line, so no two rows share one) per arena allocation unit
 __host__ __device__ constexpr int64_t slot_units(int64_t dw) { return (dw + kRowAlign - 1) / kRowAlign * kRowAlign; }
 
 struct TableView {
@@ -514,7 +514,7 @@ int arena_reserve(cms_handle* h, int64_t need, bool keep);
 int init_row_offsets(cms_handle* h);
 // unmaps and frees the arena (cms_destroy)
 void arena_release(cms_handle* h);
-// Compact layout of a fresh build (cms_build.hip): caps[r] (64-B units) ->
+// Compact layout of a fresh build (cms_build.hip): caps[r] (128-B units) ->
 // off[] after the zero row; returns the arena units in use.  Synchronises
 // h->stream (the plan's stream) to size the arena.
 int row_layout(cms_handle* h, const uint32_t* d_caps, uint32_t* d_scratch);

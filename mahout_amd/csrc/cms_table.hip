@@ -588,7 +588,7 @@ int reset_rows_zero(cms_handle* h) {
   return reset_table_layout(h);
 }
 
-// off[r] from the rows' capacities (64-B units): the rows follow the zero
+// off[r] from the rows' capacities (128-B units): the rows follow the zero
 // row in row order; a row of capacity 0 (a hot row) points at the zero row
 __global__ void k_row_offsets(const uint32_t* caps, const uint32_t* ex, int64_t n, int64_t su, int64_t* off,
                               uint32_t* total) {
