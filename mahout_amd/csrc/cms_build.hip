@@ -581,6 +581,11 @@ constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
 #ifndef CMS_MID_ROW_PREFETCH
 #define CMS_MID_ROW_PREFETCH 0
 #endif
+// byte-class list owners take their LDS adds back after each sketch row
+// instead of zeroing the wave's 4-bit row before the next one
+#ifndef CMS_NIB_UNADD
+#define CMS_NIB_UNADD 0
+#endif
 // register-cached owners keep their keys' d buckets (u16 pairs) from one
 // all-rows hash, so the u8 / u16 row passes (an escalation from 4-bit, or an
 // owner starting at u8) do not hash again
@@ -1430,8 +1435,12 @@ __device__ __forceinline__ void nib_owner(
     const int nq = (w * bits) >> 7;   // uint4 per sketch row
     vmax = 0;
     ovf = false;
+    // a list row's counts leave nothing behind: its adds are taken back after
+    // each sketch row (CMS_NIB_UNADD), so only the first row zeroes the slot
+    const bool unadd = CMS_NIB_UNADD && as_list;
     for (int d = 0; d < hp.depth; ++d) {
-      for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
+      if (!unadd || d == 0)
+        for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
       uint32_t sq = 0;
 #pragma unroll
       for (int k = 0; k < kKeyRegs; ++k)
@@ -1447,7 +1456,15 @@ __device__ __forceinline__ void nib_owner(
           vmax = max(vmax, nv);
           if (as_list) lst[1 + (int64_t)d * m + lane + 64 * k] = (uint16_t)c;
         }
-      if (__ballot(ovf)) break;  // uniform: escalate
+      if (__ballot(ovf)) break;  // uniform: escalate (the slot is zeroed by the next owner's first row)
+      if (unadd) {  // no counter carried (checked above), so each subtraction only removes its own add
+#pragma unroll
+        for (int k = 0; k < kKeyRegs; ++k)
+          if (ik[k]) {  // (the bucket read back from the entry this lane just wrote: no registers held)
+            const uint32_t c = lst[1 + (int64_t)d * m + lane + 64 * k];
+            atomicSub(&slot[c >> lg], ik[k] << ((c & ((1u << lg) - 1u)) * (uint32_t)bits));
+          }
+      }
       sq = wave_sum_u32(sq);  // <= mass * 15
 #ifdef CMS_BUILD_NOWRITE  // bound analysis only: no table stores
       if (false)
