@@ -126,3 +126,47 @@ def test_compact_merge_forms_equal_oracle(oracle):
             ref = oracle.similarities_row(exp, q)
             ref[q] = oracle.cosine_cm(exp[q], exp[q])
             assert same(t.similarities(q, np.arange(n)), ref), q
+
+
+@pytest.mark.parametrize("vmm", [True, False])
+def test_compact_arena_regrows_and_shrinks(oracle, monkeypatch, vmm):
+    """One handle through a large fresh build, a reset and a small one (the
+    arena gives back what it no longer needs: unmapped chunks, or a smaller
+    hipMalloc with CMS_NO_VMM=1), incremental batches that move rows to slots
+    of their own (the arena grows), and a large build again -- each stage
+    bit-exact against the oracle's rebuild."""
+    from mahout_amd import SketchTable
+    monkeypatch.setenv("CMS_NO_VMM", "0" if vmm else "1")
+    n, d, w = 30000, 5, 4096
+    a, b = oracle.hash_params(11, d)
+    big_i, big_u = zipf_stream(1_000_000, n, 3_000_000, seed=31)
+    small_i, small_u = zipf_stream(1_000_000, 300, 400_000, seed=32)  # owners 0..299 only
+    rng = np.random.Generator(np.random.PCG64(33))
+    more_i = rng.integers(0, n, 100_000).astype(np.int64)
+    more_u = rng.integers(0, 1_000_000, more_i.size).astype(np.int64)
+    sel = np.array([0, 1, 2, 150, 299, 5000, n - 1])
+
+    def check(t, items, users):
+        m = np.isin(items, sel)
+        exp = oracle.build_table(sel.size, d, w, a, b, np.searchsorted(sel, items[m]), users[m], None)
+        got = t.read_counters_device()[sel].cpu().numpy().astype(np.float64)
+        assert same(got, exp)
+        return t.stats()["table_bytes"]
+
+    with SketchTable(n, depth=d, width=w, seed=11) as t:
+        t.ingest(big_i, big_u)
+        t.finalize()
+        tb_big = check(t, big_i, big_u)
+        t.reset()
+        t.ingest(small_i, small_u)
+        t.finalize()
+        tb_small = check(t, small_i, small_u)
+        assert tb_small < tb_big, (tb_small, tb_big)
+        t.ingest(more_i, more_u)  # touched rows without a slot of their own move to one
+        t.finalize()
+        tb_more = check(t, np.concatenate([small_i, more_i]), np.concatenate([small_u, more_u]))
+        assert tb_more > tb_small
+        t.reset()
+        t.ingest(big_i, big_u)
+        t.finalize()
+        check(t, big_i, big_u)
