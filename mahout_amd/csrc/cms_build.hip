@@ -581,6 +581,10 @@ constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
 #ifndef CMS_MID_ROW_PREFETCH
 #define CMS_MID_ROW_PREFETCH 0
 #endif
+// keys per thread in flight per step of an uncached owner's row pass
+#ifndef CMS_MID_ROW_KEYS
+#define CMS_MID_ROW_KEYS 4
+#endif
 // byte-class list owners take their LDS adds back after each sketch row
 // instead of zeroing the wave's 4-bit row before the next one
 #ifndef CMS_NIB_UNADD
@@ -603,6 +607,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
   constexpr int MTH = MT;                   // threads per owner (a workgroup)
   constexpr int MKR = kKeyRegs * 256 / MT;  // key registers per thread: 1024 keys cached per owner
   constexpr bool kBc = CMS_MID_BKT_CACHE && D > 0 && MKR <= 4;  // cached buckets (w <= 65536: u16)
+  constexpr int RK = CMS_MID_ROW_PREFETCH ? 4 : CMS_MID_ROW_KEYS;  // keys per thread per step of an uncached row pass
   constexpr int kBcW = kBc ? (D + 1) / 2 : 1;                   // u16 pairs per key
   extern __shared__ __align__(16) uint32_t lds[];  // one sketch row of up to w u16 counters, or the [d][w] 4-bit image
   __shared__ unsigned long long s_norm[CMS_MAX_DEPTH];
@@ -942,9 +947,9 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
           };
           fetch(lo);
 #endif
-          for (int64_t base = lo; base < hi; base += 4 * MTH) {
-            uint64_t kk[4];
-            uint32_t inc4[4];
+          for (int64_t base = lo; base < hi; base += RK * MTH) {
+            uint64_t kk[RK];
+            uint32_t inc4[RK];
 #if CMS_MID_ROW_PREFETCH
             uint64_t raw[4];
 #pragma unroll
@@ -952,7 +957,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
             if (base + kStep < hi) fetch(base + kStep);
 #endif
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < RK; ++u) {
               const int64_t i = base + tid + (int64_t)u * MTH;
 #if CMS_MID_ROW_PREFETCH
               kk[u] = i < hi ? keys.resolve(raw[u]) : 0;
@@ -970,7 +975,7 @@ __global__ __launch_bounds__(MT) __attribute__((amdgpu_waves_per_eu(4, 8))) void
               }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < RK; ++u) {
               if (inc4[u]) add(kk[u], inc4[u], nullptr);
               if (mass_pending) mass += inc4[u];
             }
