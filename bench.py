@@ -866,7 +866,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     total = int(args.stream_pairs)
     bsize = int(args.stream_batch)
     nbatch = (total + bsize - 1) // bsize
-    ingest_s, local, worst = 0.0, 0, 0.0
+    ingest_s, local, worst, worst_b = 0.0, 0, 0.0, -1
     for b in range(nbatch):
         it_, us = batch(555_000 + b, min(bsize, total - b * bsize))
         bar()
@@ -875,7 +875,8 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         bar()
         dt = max_over_ranks(time.perf_counter() - t0)
         ingest_s += dt
-        worst = max(worst, dt)
+        if dt > worst:
+            worst, worst_b = dt, b
         local += int(it_.numel())
         del it_, us
     t0 = time.perf_counter()
@@ -892,7 +893,8 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "ingest_s": ingest_s, "finalize_s": fin_s,
         "sustained_updates_per_s": total / ingest_s,
         "x_realtime": (total / ingest_s) / 10e6,  # the stream arrives at 10M pairs/s
-        "batch_latency_ms": ingest_s * 1e3 / nbatch, "batch_latency_max_ms": worst * 1e3,
+        "batch_latency_ms": ingest_s * 1e3 / nbatch, "batch_latency_max_ms": worst * 1e3, "slowest_batch": worst_b,
+        "widen_ms": t.timing("widen_rows")[0],
         "path": f"{kern} (batches of >= 32768 pairs into a live table are grouped by owner first and take "
                 "k_ingest_sorted: exact u32 global atomics, norm / row-max / mass deltas reduced per owner inside the "
                 "wave; smaller batches take k_ingest_atomic)",
