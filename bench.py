@@ -894,7 +894,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "sustained_updates_per_s": total / ingest_s,
         "x_realtime": (total / ingest_s) / 10e6,  # the stream arrives at 10M pairs/s
         "batch_latency_ms": ingest_s * 1e3 / nbatch, "batch_latency_max_ms": worst * 1e3, "slowest_batch": worst_b,
-        "widen_ms": t.timing("widen_rows")[0],
+        "widen_ms": t.timing("widen_rows")[0], "arena_map_ms": t.timing("arena_map"),
         "path": f"{kern} (batches of >= 32768 pairs into a live table are grouped by owner first and take "
                 "k_ingest_sorted: exact u32 global atomics, norm / row-max / mass deltas reduced per owner inside the "
                 "wave; smaller batches take k_ingest_atomic)",

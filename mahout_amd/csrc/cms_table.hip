@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 
 #include "cms_internal.h"
 
@@ -437,6 +438,7 @@ static int arena_map(cms_handle* h, size_t want) {
   prop.location.type = hipMemLocationTypeDevice;
   prop.location.id = h->device;
   const size_t g = h->arena_gran;
+  const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = std::min(h->arena_va_bytes - h->arena_mapped, (want - h->arena_mapped + g - 1) / g * g);
   if (h->arena_mapped + bytes < want) return set_error(CMS_E_OOM, "row arena: %.2f GB exceeds its reserved range", 1e-9 * want);
   hipMemGenericAllocationHandle_t mem;
@@ -461,6 +463,11 @@ static int arena_map(cms_handle* h, size_t want) {
   }
   h->arena_chunks.push_back({mem, bytes});
   h->arena_mapped += bytes;
+  if (h->timing) {  // host time of the mapping (cms_get_timing "arena_map")
+    auto& acc = h->timing_acc["arena_map"];
+    acc.total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    acc.launches += 1;
+  }
   return CMS_OK;
 }
 
