@@ -114,6 +114,7 @@ int cms_shape_from_delta_epsilon(double delta, double epsilon, int32_t* width, i
  * result, only the storage or kernel a result comes from:
  *   CMS_NO_FORMS=1        narrow rows stay u16 (no 1/2/4/8-bit row forms)
  *   CMS_NO_COMPACT=1      every narrow row keeps a whole u16 slot (no compact row layout)
+ *   CMS_EARLY_SLICES=1    the hot-routed split owners built beside pass 2 of the partition
  *   CMS_NO_VMM=1          the compact row arena as one hipMalloc grown by copying
  *                         (no reserved virtual range mapped in chunks)
  *   CMS_BIT_KEYS=<n>      byte-class owners of <= n keys try 1-bit rows first (64)

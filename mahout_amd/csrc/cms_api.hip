@@ -359,6 +359,7 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
     h->tune.forms = !flag("CMS_NO_FORMS");
     h->tune.no_compact = flag("CMS_NO_COMPACT");
     h->tune.no_vmm = flag("CMS_NO_VMM");
+    h->tune.early_slices = flag("CMS_EARLY_SLICES") ? 1 : 0;
     h->tune.hot_routing = !flag("CMS_NO_HOT_ROUTING");
     h->tune.fp4 = !flag("CMS_NO_FP4");
     h->tune.mls = !flag("CMS_NO_MLS");
@@ -404,6 +405,10 @@ static int create_impl(const cms_params* p, bool per_owner, cms_handle** out) {
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamDefault)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&h->side_stream2, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&h->side_stream3, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_p1, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_e1, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&h->ev_early, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_join3, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_spans, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&h->ev_plan, hipEventDisableTiming)) != hipSuccess ||
@@ -467,6 +472,9 @@ void cms_destroy(cms_handle* h) {
   if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
   if (h->side_stream2) (void)hipStreamSynchronize(h->side_stream2);
+  if (h->side_stream3) (void)hipStreamSynchronize(h->side_stream3);
+  for (hipEvent_t ev : {h->ev_p1, h->ev_e1, h->ev_early})
+    if (ev) (void)hipEventDestroy(ev);
   if (h->ev_join3) (void)hipEventDestroy(h->ev_join3);
   if (h->ev_spans) (void)hipEventDestroy(h->ev_spans);
   if (h->ev_plan) (void)hipEventDestroy(h->ev_plan);
@@ -494,6 +502,7 @@ void cms_destroy(cms_handle* h) {
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
   if (h->side_stream2) (void)hipStreamDestroy(h->side_stream2);
+  if (h->side_stream3) (void)hipStreamDestroy(h->side_stream3);
   delete h;
 }
 

@@ -60,12 +60,12 @@ __device__ __forceinline__ uint32_t nibbles8(uint32_t lo, uint32_t hi) {
 __global__ void k_build_plan(const int64_t* lo_, const int64_t* hi_, int64_t nrows, int64_t split, int64_t slice,
                              int first, int32_t* row_hot, HotInfo* hot, int2* extra_map,
                              uint32_t* counters /* [0]=hot rows [1]=mapped slices */, uint64_t* norm, uint32_t* rowmax,
-                             int depth) {
+                             int depth, const uint8_t* early) {
   const int lane = (int)__lane_id();
   for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nrows; base += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = base + threadIdx.x;
     const int64_t c = r < nrows ? hi_[r] - lo_[r] : 0;
-    const bool is_hot = c > split;
+    const bool is_hot = c > split && !(early && early[r]);  // (an early row is built already: k_early_plan)
     if (r < nrows && !is_hot) row_hot[r] = -1;
     int32_t ns = 0;
     uint32_t hidx = 0, e0 = 0;
@@ -525,7 +525,8 @@ __global__ __launch_bounds__(kBuildThreads) __attribute__((amdgpu_waves_per_eu(C
 constexpr int kClassChunk = 4096;
 __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const int64_t* hi_, int64_t nrows,
                                                        const int32_t* hidx, const uint64_t* bound, int32_t* slot_list,
-                                                       int32_t* mid_list, uint32_t* cnt /* [0] slot, [1] mid */) {
+                                                       int32_t* mid_list, uint32_t* cnt /* [0] slot, [1] mid */,
+                                                       const uint8_t* early) {
   __shared__ int32_t s_slot[kClassChunk], s_mid[kClassChunk];
   __shared__ uint32_t s_n[2], s_b[2];
   const int lane = (int)__lane_id();
@@ -536,7 +537,7 @@ __global__ __launch_bounds__(256) void k_build_classes(const int64_t* lo_, const
     __syncthreads();
     for (int64_t r = r0 + tid; r < r0 + kClassChunk; r += 256) {  // (whole waves: the ballots)
       bool is_slot = false, is_mid = false;
-      if (r < nrows) {
+      if (r < nrows && !(early && early[r])) {  // (an early row is built already)
         const int32_t sl = hidx[r];
         is_slot = sl >= 0;
         is_mid = !is_slot && !byte_class(sl, hi_[r] - lo_[r], bound[r]);
@@ -1890,6 +1891,46 @@ __global__ __launch_bounds__(256) void k_slice_reduce(const HotInfo* hot, const 
   }
 }
 
+// Early slices (Tunables::early_slices): the hot-routed owners of more than
+// `split` keys, whose keys pass 1 of the partition already placed, claim hot
+// slot base + t (t: their routing slot), their spans and slice map, with
+// their norms and maxima zeroed -- one thread per routing slot, the slice map
+// written by the row's own thread (a Zipf head owner: ~1000 slices).
+__global__ void k_early_plan(const unsigned long long* slotkey, const uint32_t* bs1, int P1, int nslots,
+                             int64_t split, int64_t slice, int64_t base, int32_t* hidx, uint8_t* early, int64_t* elo,
+                             int64_t* ehi, HotInfo* hot, int2* extra_map, uint32_t* counters, uint64_t* norm,
+                             uint32_t* rowmax, int depth) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nslots) return;
+  const uint32_t o1 = (uint32_t)slotkey[t];
+  if (o1 == 0) return;
+  const int64_t row = (int64_t)o1 - 1;
+  const int64_t lo = bs1[P1 + t], hi = bs1[P1 + t + 1];
+  if (hi - lo <= split) return;  // built with the other rows after pass 2
+  const int32_t ns = (int32_t)((hi - lo + slice - 1) / slice);
+  const unsigned long long old = atomicAdd(reinterpret_cast<unsigned long long*>(counters), ((unsigned long long)ns << 32) | 1ULL);
+  const uint32_t hx = (uint32_t)old, e0 = (uint32_t)(old >> 32);
+  hot[hx] = HotInfo{row, ns, (int32_t)e0};
+  for (int32_t sl = 0; sl < ns; ++sl) extra_map[e0 + sl] = make_int2((int)hx, sl);
+  early[row] = 1;
+  elo[row] = lo;
+  ehi[row] = hi;
+  hidx[row] = (int32_t)(base + t);
+  for (int d = 0; d < depth; ++d) norm[row * depth + d] = 0;
+  rowmax[row] = 0;
+}
+
+// ... and the slots of the early rows built by more than one slice (their
+// slices add into the slot) are zeroed; a single slice stores its row whole.
+__global__ __launch_bounds__(256) void k_early_zero(const HotInfo* hot, const uint32_t* counters, TableView tv) {
+  const uint32_t nh = counters[0];
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    if (hot[i].nslices <= 1) continue;
+    uint4* dst = reinterpret_cast<uint4*>(tv.hot + (int64_t)tv.hidx[hot[i].row] * tv.dw);
+    for (int64_t j = threadIdx.x; j < (tv.dw >> 2); j += 256) dst[j] = make_uint4(0, 0, 0, 0);
+  }
+}
+
 int row_bounds(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi, const float* d_val, const uint64_t* old_mass,
                int64_t slice, uint64_t* bound, uint8_t* force) {
   const int64_t n = h->n;
@@ -1942,6 +1983,73 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
   HotInfo* hot = reinterpret_cast<HotInfo*>(base + sz_rowhot);
   int2* extra_map = reinterpret_cast<int2*>(base + sz_rowhot + sz_hot);
   uint32_t* counters = h->d_flags + 4;  // [4..7]: hot rows, mapped slices (one u64 atomic), spare
+  // Early slices (Tunables::early_slices): the hot-routed owners of more than
+  // kSplit keys are final after pass 1 of the partition, so their rows are
+  // claimed and built on side_stream3 beside pass 2 (k_early_plan,
+  // k_early_zero, k_build_slices, k_hot_norms); the plan below skips them
+  // (early flags) and the build joins them at its end.
+  auto slices_kernel = [&]() {
+    static bool attr = [] {
+      for (const void* f : {(const void*)k_build_slices<0>, (const void*)k_build_slices<4>,
+                            (const void*)k_build_slices<5>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      return true;
+    }();
+    (void)attr;
+    return h->p.depth == 5 ? k_build_slices<5> : h->p.depth == 4 ? k_build_slices<4> : k_build_slices<0>;
+  };
+  const uint8_t* eflag = nullptr;
+  struct EarlyJoin {
+    cms_handle* h;
+    bool on = false;
+    void end() {
+      if (!on) return;
+      on = false;
+      (void)hipStreamWaitEvent(h->stream, h->ev_early, 0);
+    }
+    ~EarlyJoin() { end(); }
+  } early_join{h};
+  if (h->p1_event && !accumulate && fast_slices && whole_slices && h->forms_ok && (size_t)h->dw <= kFormLdsMax &&
+      !h->plan_side_active) {
+    h->p1_event = false;
+    const hipStream_t s3 = h->side_stream3;
+    const int nslots = h->p1_nslots;
+    const int64_t emax_e = npairs / kSliceKeys + nslots + 1;
+    const size_t sz_span = sizeof(int64_t) * (size_t)n;
+    const size_t sz_flag = ((size_t)n + 15) & ~size_t(15);
+    const size_t sz_ehot = (sizeof(HotInfo) * (size_t)nslots + 15) & ~size_t(15);
+    CMS_HIP(h->ws_early.ensure(2 * sz_span + sz_flag + sz_ehot + sizeof(int2) * (size_t)emax_e + 64));
+    char* eb = h->ws_early.as<char>();
+    int64_t* elo = reinterpret_cast<int64_t*>(eb);
+    int64_t* ehi = reinterpret_cast<int64_t*>(eb + sz_span);
+    uint8_t* ef = reinterpret_cast<uint8_t*>(eb + 2 * sz_span);
+    HotInfo* ehot = reinterpret_cast<HotInfo*>(eb + 2 * sz_span + sz_flag);
+    int2* emap = reinterpret_cast<int2*>(eb + 2 * sz_span + sz_flag + sz_ehot);
+    uint32_t* ecnt = h->d_flags + 12;  // [12..13]: early hot rows, mapped slices (one u64 atomic)
+    // the table layout restarts here (the plan's own reset is skipped)
+    CMS_HIP(hipStreamWaitEvent(s3, h->ev_p1, 0));
+    CMS_HIP(hipMemsetAsync(h->d_hidx, 0xff, sizeof(int32_t) * (size_t)n, s3));
+    h->hot_used = 0;
+    int64_t ebase = 0;
+    if ((rc0 = reserve_hot_slots(h, nslots, &ebase))) return rc0;
+    CMS_HIP(hipMemsetAsync(ef, 0, (size_t)n, s3));
+    CMS_HIP(hipMemsetAsync(ecnt, 0, 2 * sizeof(uint32_t), s3));
+    hipLaunchKernelGGL(k_early_plan, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s3, h->p1_slotkey,
+                       h->p1_bs1, h->p1_P1, nslots, kSplit, kSliceKeys, ebase, h->d_hidx, ef, elo, ehi, ehot, emap,
+                       ecnt, h->d_norm, h->d_rowmax, h->p.depth);
+    CMS_HIP(hipEventRecord(h->ev_e1, s3));  // rows claimed: the plan may read hidx and the flags
+    hipLaunchKernelGGL(k_early_zero, dim3((unsigned)std::min(nslots, 1024)), dim3(256), 0, s3, ehot, ecnt, h->tview());
+    hipLaunchKernelGGL(slices_kernel(), dim3((unsigned)emax_e), dim3(kSliceThreads), img_lds, s3, elo, ehi, keys,
+                       h->hp, kSliceKeys, ehot, emap, ecnt, h->tview(), h->d_row_mass, h->d_flags, (uint16_t*)nullptr,
+                       1, h->d_norm, h->d_rowmax);
+    hipLaunchKernelGGL(k_hot_norms, dim3((unsigned)std::min(nslots, 1024), (unsigned)h->p.depth), dim3(256), 0, s3,
+                       ehot, ecnt, h->hp, h->tview(), h->d_norm, h->d_rowmax, 1);
+    CMS_HIP(hipGetLastError());
+    CMS_HIP(hipEventRecord(h->ev_early, s3));
+    early_join.on = true;
+    eflag = ef;
+  }
+  h->p1_event = false;
   // A fresh unit-increment build right after a partition that marked its
   // spans (ingest_coo): the plan below needs only the spans, so it runs on
   // the side stream beside the partition's last scatter (h->stream swapped
@@ -1965,11 +2073,12 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     h->plan_side_active = true;  // nothing in the section may launch on h->side_stream (it is the main stream now)
     plan_side.on = true;
   }
+  if (eflag) CMS_HIP(hipStreamWaitEvent(h->stream, h->ev_e1, 0));  // the early rows' claims first
   CMS_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), h->stream));
   // table layout: rows that could reach 2^16, and split rows, get u32 slots
   {
     TimedScope ts(h, "build_plan");
-    if (!accumulate && (rc0 = reset_table_layout(h))) return rc0;
+    if (!accumulate && !eflag && (rc0 = reset_table_layout(h))) return rc0;
     DevBuf& bound = h->ws_bound;
     DevBuf& force = h->ws_force;
     CMS_HIP(bound.ensure(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1)));
@@ -2007,7 +2116,8 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     TimedScope ts(h, "build_plan");
     unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
     hipLaunchKernelGGL(k_build_plan, dim3(grid), dim3(256), 0, h->stream, d_lo, d_hi, n, kSplit, kSliceKeys,
-                       fast_slices ? 0 : 1, row_hot, hot, extra_map, counters, h->d_norm, h->d_rowmax, h->p.depth);
+                       fast_slices ? 0 : 1, row_hot, hot, extra_map, counters, h->d_norm, h->d_rowmax, h->p.depth,
+                       eflag);
     CMS_HIP(hipGetLastError());
   }
   // fresh builds may store byte forms: the whole [d][w] byte image in LDS
@@ -2057,14 +2167,10 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     // forks, so they overlap the byte and mid classes)
     auto launch_slices = [&]() -> int {
       if (!fast_slices) return CMS_OK;
-      static bool attr = [] {
-        for (const void* f : {(const void*)k_build_slices<0>, (const void*)k_build_slices<4>,
-                              (const void*)k_build_slices<5>})
-          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        return true;
-      }();
-      (void)attr;
-      auto kslices = h->p.depth == 5 ? k_build_slices<5> : h->p.depth == 4 ? k_build_slices<4> : k_build_slices<0>;
+#ifdef CMS_BUILD_SKIP_SLICES  // bound analysis only: the split owners' slices not built (wrong table)
+      return CMS_OK;
+#endif
+      auto kslices = slices_kernel();
       hipLaunchKernelGGL(kslices, dim3((unsigned)emax), dim3(kSliceThreads), img_lds, h->stream, d_lo, d_hi,
                          keys, h->hp, kSliceKeys, hot, extra_map, counters, h->tview(), h->d_row_mass, h->d_flags,
                          simg, whole_slices, h->d_norm, h->d_rowmax);
@@ -2096,7 +2202,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
       hipLaunchKernelGGL(k_build_classes,
                          dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kClassChunk - 1) / kClassChunk, 1024))),
                          dim3(256), 0, h->stream, d_lo, d_hi, n, h->d_hidx, h->ws_bound.as<uint64_t>(), slot_list,
-                         mid_list, lcnt);
+                         mid_list, lcnt, eflag);
       CMS_HIP(hipGetLastError());
       if (h->plan_side_active) return set_error(CMS_E_STATE, "internal: side stream used while swapped for the plan");
       hipStream_t side = h->side_stream ? h->side_stream : h->stream;
@@ -2220,6 +2326,7 @@ int ingest_spans_device(cms_handle* h, const int64_t* d_lo, const int64_t* d_hi,
     }
   }
   if (!hot_norms_done && (rc0 = launch_hot_norms())) return rc0;
+  early_join.end();  // the early rows' build joins the handle's stream
   h->empty = false;
   h->norms_valid = true;  // build_rows + hot_norms wrote the norm of every row
   return CMS_OK;

@@ -234,6 +234,7 @@ struct Tunables {
   int split_keys = 0;       // CMS_SPLIT_KEYS: rows with more keys get a u32 slot and k_build_slices (0: 8192, 16384 at w >= 8192)
   int mid_waves = 0;        // CMS_MID_WAVES=<k>: mid owners one wave each (k_build_mid_waves), k persistent 4-wave workgroups per CU; 0: k_build_mid
   int slice_reduce = 0;     // CMS_SLICE_REDUCE=1: split owners' slices leave u16 images summed by k_slice_reduce (no slot atomics)
+  int early_slices = 0;     // CMS_EARLY_SLICES=1: the hot-routed split owners are built beside pass 2 of the partition
   bool forms = true;       // CMS_NO_FORMS=1: every narrow row stays u16 (no 1/2/4/8-bit forms)
   bool no_compact = false; // CMS_NO_COMPACT=1: every narrow row keeps a whole u16 slot (no compact layout)
   bool no_vmm = false;     // CMS_NO_VMM=1: the compact arena as one hipMalloc grown by copying (no virtual range)
@@ -259,6 +260,15 @@ struct cms_handle {
   // the owner spans of a partition are ready (recorded before its last
   // scatter): the build plan may start on the side stream meanwhile
   hipEvent_t ev_spans = nullptr, ev_plan = nullptr;
+  // early slices (Tunables::early_slices): pass 1 of the partition has placed
+  // the hot-routed owners' keys (ev_p1); their build runs on side_stream3,
+  // ev_e1 marks their rows claimed (hidx, early flags), ev_early its end
+  hipStream_t side_stream3 = nullptr;
+  hipEvent_t ev_p1 = nullptr, ev_e1 = nullptr, ev_early = nullptr;
+  bool p1_event = false;
+  const unsigned long long* p1_slotkey = nullptr;  // hot slot t -> owner row + 1 (0: free)
+  const uint32_t* p1_bs1 = nullptr;                // pass-1 bin starts: hot slot t spans [bs1[P1 + t], bs1[P1 + t + 1])
+  int p1_P1 = 0, p1_nslots = 0;
   bool spans_event = false, plan_side_request = false;
   bool plan_side_active = false;  // h->stream and h->side_stream are swapped (the build plan's section)
   // Writers (ingest, finalize, reset, top-k passes, ...) hold mu exclusively;
@@ -298,6 +308,7 @@ struct cms_handle {
   cms::DevBuf ws_bound, ws_force, ws_plist;  // promotion scratch: u64 [n], u8 [n], i32 [n] + count
   cms::DevBuf ws_blist;                      // row build: slot-row and mid-class row lists + counts
   cms::DevBuf ws_layout;                     // row layout: capacities / scan (u32 [2n + ...]); widen: movers
+  cms::DevBuf ws_early;                      // early slices: spans i64 [2n], flags u8 [n], HotInfo / slice map
   int64_t hot_cap = 0, hot_used = 0;
   cms::TableView tview() const {
     return cms::TableView{d_t16, hot_tab.as<uint32_t>(), d_hidx, dw, p.width, d_off};
@@ -482,6 +493,9 @@ int local_norms(cms_handle* h);
 // round trip: that many slots are reserved and claimed on the device).
 int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force, bool copy_old, int64_t max_new = -1,
                  uint64_t whole_bound = 0);
+// count consecutive hot slots for the caller's rows (host bookkeeping; the
+// table grows first if needed): [*base, *base + count)
+int reserve_hot_slots(cms_handle* h, int64_t count, int64_t* base);
 // rows holding a u32 slot (synchronises the stream)
 int count_hot_rows(cms_handle* h, int64_t* out);
 // rows per storage form: [0] hot, [1] u16, [2] u8, [3] nibble (synchronises)

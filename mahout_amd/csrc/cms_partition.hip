@@ -908,6 +908,17 @@ static int partition_impl(cms_handle* h, const int64_t* d_row, const int64_t* d_
     hipLaunchKernelGGL(scat, dim3(NB), dim3(kPartThreads), tile_lds_bytes(P, d_val != nullptr, true, hot, (int)tile1),
                        h->stream, d_row, d_key, d_val, npairs, s2, P1, n, O1, NB, fine, key1, val1, slotkey,
                        ckey, cval);
+    // the hot-routed owners' keys are in place now (their pass-1 bins are
+    // their final spans): the build may start on them beside pass 2
+    h->p1_event = false;
+    if (hot && h->tune.early_slices && h->plan_side_request && h->side_stream3 && !d_val && !h->plan_side_active) {
+      CMS_HIP(hipEventRecord(h->ev_p1, h->stream));
+      h->p1_event = true;
+      h->p1_slotkey = slotkey;
+      h->p1_bs1 = bs1;
+      h->p1_P1 = P1;
+      h->p1_nslots = kHotBins;
+    }
     hipLaunchKernelGGL(k_p2_plan, dim3(1), dim3(1024), 0, h->stream, bs1, P1, CH2, binStart, blkStart);
     const int64_t g2h = std::min<int64_t>((nb2max + 7) & ~int64_t(7), (int64_t)h->num_cus * 8);
     hipLaunchKernelGGL(k_p2_hist, dim3((unsigned)g2h), dim3(256), sizeof(uint32_t) * P2, h->stream, fine,

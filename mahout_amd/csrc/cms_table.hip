@@ -59,6 +59,9 @@ __global__ __launch_bounds__(256) void k_promote_rows(const int32_t* list, int64
 
 static int grow_hot(cms_handle* h, int64_t need) {
   if (need <= h->hot_cap) return CMS_OK;
+  // (early slices may still be writing slots on their own stream: the copy
+  // below must see their rows, and the old table outlive them)
+  CMS_HIP(hipDeviceSynchronize());
   {  // grow: new slot table, live slots copied over
     // at least `need` (reserved-but-unclaimed slots can make it exceed n)
     const int64_t cap =
@@ -72,6 +75,13 @@ static int grow_hot(cms_handle* h, int64_t need) {
     h->hot_tab = std::move(nb);
     h->hot_cap = cap;
   }
+  return CMS_OK;
+}
+
+int reserve_hot_slots(cms_handle* h, int64_t count, int64_t* base) {
+  if (int rc = grow_hot(h, h->hot_used + count)) return rc;
+  *base = h->hot_used;
+  h->hot_used += count;
   return CMS_OK;
 }
 

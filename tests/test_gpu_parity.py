@@ -952,3 +952,42 @@ def test_lower_split_threshold_same_table(oracle, split, monkeypatch):
     remap[sel] = np.arange(sel.size)
     exp = oracle_table(oracle, sel.size, d, w, 23, remap[items[m]], users[m], None)
     assert same(got[(split, False)][0].numpy()[sel].astype(np.float64), exp)
+
+
+def test_early_slices_same_table(oracle, monkeypatch):
+    """CMS_EARLY_SLICES=1: the hot-routed owners of more than the split
+    threshold are built beside pass 2 of the partition (k_early_plan,
+    k_build_slices on a stream of their own) and the plan skips them: the
+    table, the forms, the norms (through the similarities) and the row
+    maxima equal the default build's, and the heaviest owners equal the
+    oracle."""
+    import torch
+    n, d, w = 4096, 5, 8192
+    rng = np.random.Generator(np.random.PCG64(41))
+    # owners 0..2: 1.3M / 300K / 70K keys (many, several, two slices), a Zipf tail
+    heavy = [np.zeros(1_300_000, np.int64), np.ones(300_000, np.int64), np.full(70_000, 2, np.int64)]
+    tail_items, tail_users = zipf_stream(3_000_000, n - 3, 2_000_000, seed=42)
+    items = np.concatenate(heavy + [tail_items + 3])
+    users = np.concatenate([rng.integers(0, 5_000_000, sum(h.size for h in heavy)), tail_users]).astype(np.int64)
+    perm = rng.permutation(items.size)
+    items, users = items[perm], users[perm]
+    got = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CMS_EARLY_SLICES", mode)
+        with SketchTable(n, depth=d, width=w, seed=13) as t:
+            for _ in range(2):  # twice: the second build reuses the handle's slots and scratch
+                t.reset()
+                t.ingest(items, users)
+                t.finalize()
+            got[mode] = (t.read_counters_device().cpu(), t.owner_forms()[0],
+                         np.stack([t.similarities(q, np.arange(n)) for q in (0, 1, 2, 3, 100)]),
+                         t.stats()["hot_rows"])
+            torch.cuda.synchronize()
+    assert torch.equal(got["0"][0], got["1"][0])
+    assert np.array_equal(got["0"][1], got["1"][1])
+    assert same(got["0"][2], got["1"][2])
+    assert got["1"][3] >= 3
+    sel = np.array([0, 1, 2, 3])
+    m = np.isin(items, sel)
+    exp = oracle_table(oracle, sel.size, d, w, 13, items[m], users[m], None)
+    assert same(got["1"][0].numpy()[sel].astype(np.float64), exp)
