@@ -36,6 +36,15 @@ METRIC = "sketch updates/sec + item-pair cosines/sec @1M items, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
+_T0 = time.time()
+
+
+def progress(msg):
+    """A progress line on stderr (the JSON line stays the last stdout line):
+    a long run keeps writing, so a watchdog can tell it from a hang."""
+    print(f"bench-progress: {time.time() - _T0:7.1f} s {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -735,7 +744,9 @@ def cosine_1m(args, t, local, device, rank, world, bar, max_over_ranks):
     # allocated and written once per table (the timed job is the steady state)
     t.reset_timing()
     first_t0 = time.perf_counter()
+    progress("config 4: first all-pairs job")
     t.top_k_all_device(k)
+    progress("config 4: steady job")
     first_job_s = time.perf_counter() - first_t0
     # GPU time of the first job's scopes (HIP events); the rest of its wall is
     # host work: the operand images' and candidate lists' first allocations
@@ -861,6 +872,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         return it_.contiguous(), us.contiguous()
 
     # ---- sustained ingest of the 1B-pair stream ----
+    progress("config 5: stream")
     t.set_timing(True)
     t.reset_timing()
     total = int(args.stream_pairs)
@@ -1150,6 +1162,7 @@ def config2_line(args, rank, world, local, device):
     if "extras" in out:
         # the reference's per-owner-shape mode at this scale (SURVEY 8(f) rank
         # 2), on the same stream, with the fixed-shape table released first
+        progress("config 2: per-owner shapes")
         out["extras"]["per_owner_shapes_cfg2"] = per_owner_scale(items, users, n, c2.n_users)
     del items, users
     torch.cuda.empty_cache()
@@ -1191,8 +1204,10 @@ def main():
         return float(v.item())
 
     # secondary lines first (their tables are freed before the 82 GB headline table)
+    progress("config 2 line")
     config2 = None if args.no_config2 else config2_line(args, rank, world, local, device)
     cfg1 = None
+    progress("config 1")
     if rank == 0 and world == 1 and not args.no_config1 and not args.no_extras:
         cfg1 = config1()
 
@@ -1206,6 +1221,7 @@ def main():
         return
 
     # ---- headline: config 3's shape ----
+    progress("headline ingest")
     n, d, w = args.n_items, args.depth, args.width
     table = SketchTable(n, depth=d, width=w, seed=42, device=local)
     if world > 1:
@@ -1261,6 +1277,7 @@ def main():
         mw = st["merge_words"]
         result["merge"] = {"allreduce_bytes_per_step": mw * 8, "u32_table_bytes": n * d * w * 4,
                            "payload_ratio": mw * 8 / (n * d * w * 4)}
+    progress("headline done; CPU baseline")
     if rank == 0 and not args.no_cpu_baseline:
         # bounded sample of the same workload: the owners [0, 65536) of rank 0's
         # shard (IDs are a seeded permutation of popularity ranks, so an ID
@@ -1283,6 +1300,7 @@ def main():
         cos_cpu = cosine_cpu_baseline(items, users, n, d, w)
     del items, users
     torch.cuda.empty_cache()
+    progress("config 4 / 5")
     if not args.no_cosine_1m:
         try:
             table.release_scratch()

@@ -1346,7 +1346,7 @@ __host__ __device__ __forceinline__ bool nib_list_row(int64_t m, int w, int d, b
 // 128-B units, by what its class's kernel can store -- a hot row nothing (its
 // counters are u32 slot rows), a byte-class row its list entries or its u8
 // image (k_build_nibbles' forms up to k_build_bytes' u8 rows), any other row
-// (the mid class, or every row without forms) a whole u16 slot (kRowFull).
+// (the mid class, or every row without forms) a whole u16 slot (kCapU16).
 __global__ void k_row_caps(const int64_t* lo_, const int64_t* hi_, int64_t n, const uint64_t* bound,
                            const int32_t* hidx, int forms, int weighted, int frac_bits, int d, int w, int bit_keys,
                            int crumb_keys, int list_keys, uint32_t* caps) {

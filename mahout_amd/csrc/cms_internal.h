@@ -69,14 +69,16 @@ struct PendingEvent {
 // bound can reach 2^16 (promote_rows), so a u16 counter never overflows.
 //
 // ROW STORAGE: the narrow rows live in one arena (t16) at per-row offsets
-// (off[row], u16 units, 128-B aligned; bit 0 = kRowFull: the row owns a whole
-// u16 slot of dw counters there).  Offset 0 is a shared row of zeros that
-// every row of an empty table points to.  A fresh build with forms lays the
-// rows out compactly (row_layout: each row gets what its form can need -- a
+// (off[row], u16 units, 128-B aligned; bits 0-2: kCap*, the widest form the
+// row's place holds).  Offset 0 is a shared row of zeros that every row of an
+// empty table points to.  A fresh build with forms lays the rows out
+// compactly (row_layout: each row gets what its class's kernel can store -- a
 // list row its entries, a byte-class row its u8 image, a mid row a whole
-// slot); any later writer first gives a row that is not kRowFull a whole
-// slot at the arena's end (widen_rows relocates it), so in-place adds only
-// ever touch full slots.  Handles without forms keep every row in a full slot.
+// slot); a writer widens a row in place when its place holds the new form,
+// else moves it to a whole u16 slot at the arena's end (widen_rows), and the
+// zero row always moves first -- so in-place adds only ever touch a row's
+// own place.  Handles without forms keep every row in a
+// whole u16 slot.
 //
 // Narrow FORMS: a fresh build stores a row whose counters are all below 2^8
 // as u8 (dw bytes at its offset), one whose counters are all below 2^4 as
@@ -106,18 +108,38 @@ constexpr uint32_t form_cap(int32_t form) {
        : form == kFormU8 ? 255u : 65535u;
 }
 
-constexpr int64_t kRowFull = 1;  // off[row] bit 0: the row owns a whole u16 slot (in-place writes allowed)
 constexpr int64_t kRowAlign = 64;  // u16 units (128 B: an L2 line, so no two rows share one) per arena allocation unit
 __host__ __device__ constexpr int64_t slot_units(int64_t dw) { return (dw + kRowAlign - 1) / kRowAlign * kRowAlign; }
+// off[row] bits 0-2 (the offset is a multiple of kRowAlign): the widest form
+// the row's place holds -- a row is written in place only in a form no wider.
+// kCapNone: a list row's place, or the shared zero row (offset 0).
+constexpr int64_t kCapMask = 7;
+enum : int { kCapNone = 0, kCapU1 = 1, kCapU2 = 2, kCapU4 = 3, kCapU8 = 4, kCapU16 = 5 };
+__host__ __device__ constexpr int form_class(int32_t f) {
+  return f == kFormU1 ? kCapU1 : f == kFormU2 ? kCapU2 : f == kFormU4 ? kCapU4 : f == kFormU8 ? kCapU8
+       : f == kFormU16 ? kCapU16 : kCapNone;
+}
+// u16 units a form's row takes in the arena (rounded to kRowAlign)
+__host__ __device__ constexpr int64_t class_units(int c, int64_t dw) {
+  return c == kCapU16 ? slot_units(dw)
+       : ((c == kCapU8 ? dw / 2 : c == kCapU4 ? dw / 4 : c == kCapU2 ? dw / 8 : c == kCapU1 ? dw / 16 : 0) +
+          kRowAlign - 1) / kRowAlign * kRowAlign;
+}
+// the widest form a place of `units` u16 holds
+__host__ __device__ constexpr int class_of_units(int64_t units, int64_t dw) {
+  return units >= class_units(kCapU16, dw) ? kCapU16 : units >= class_units(kCapU8, dw) ? kCapU8
+       : units >= class_units(kCapU4, dw) ? kCapU4 : units >= class_units(kCapU2, dw) ? kCapU2
+       : units >= class_units(kCapU1, dw) && dw >= 16 ? kCapU1 : kCapNone;
+}
 
 struct TableView {
-  uint16_t* t16;        // the narrow-row arena (row r at off[r] & ~kRowFull)
+  uint16_t* t16;        // the narrow-row arena (row r at off[r] & ~kCapMask)
   uint32_t* hot;        // [hot_cap][dw] u32 rows
   const int32_t* hidx;  // [n] slot of a hot row, or the narrow form (kForm*)
   int64_t dw;
   int32_t w;            // sketch row width (list rows)
-  const int64_t* off;   // [n] arena offset of each narrow row (u16 units) | kRowFull
-  __device__ __forceinline__ int64_t base(int64_t row) const { return off[row] & ~kRowFull; }
+  const int64_t* off;   // [n] arena offset of each narrow row (u16 units) | its place's form class (kCap*)
+  __device__ __forceinline__ int64_t base(int64_t row) const { return off[row] & ~kCapMask; }
   __device__ __forceinline__ uint16_t* row16(int64_t row) const { return t16 + base(row); }
   // list row: key count and the entries of sketch row r
   __device__ __forceinline__ uint32_t list_m(int64_t row) const { return t16[base(row)]; }
@@ -286,7 +308,7 @@ struct cms_handle {
   int64_t dw = 0;      // d*w counters per row
   uint16_t* d_t16 = nullptr;        // arena of the narrow rows (TableView; [0, slot_units(dw)) the zero row)
   int64_t t16_cap = 0, t16_used = 0;  // arena capacity and end of the allocated part (u16 units)
-  int64_t* d_off = nullptr;         // [n] arena offset of each narrow row | kRowFull
+  int64_t* d_off = nullptr;         // [n] arena offset of each narrow row | its place's form class (kCap*)
   // compact handles: the arena is a reserved virtual range whose physical
   // memory is mapped (and unmapped) in chunks at its end -- growing never
   // copies and the base never moves (arena_reserve); without the virtual

@@ -136,36 +136,59 @@ int promote_rows(cms_handle* h, const uint64_t* d_bound, const uint8_t* d_force,
 // has keys -- the build rewrites every such row through its u16 / u32 image
 // even when all its increments are 0 (no mass added).  A listed row's cbound
 // becomes its bound after the write, which picks the form it widens to.
-// A touched row without a full slot (a compact row, or the zero row) is
-// listed too, whatever its bound: it moves to a slot of its own (mv[i], the
-// mover's index among cnt[1] movers) -- in-place adds need a whole slot.
+__device__ __forceinline__ int form_bits(int32_t f) {  // counter bits of a form (0: a list row)
+  return f == kFormList ? 0 : f == kFormU1 ? 1 : f == kFormU2 ? 2 : f == kFormU4 ? 4 : f == kFormU8 ? 8 : 16;
+}
+
+// The form a listed row is rewritten in: the narrowest form wider than its
+// own whose capacity holds its new bound nb (u16 for an accumulate build) --
+// a 2-bit row that one more pair lifts to 4 becomes a 4-bit row.  The zero
+// row counts as a list row (it holds nothing of its own).
+__device__ __forceinline__ int32_t widen_target(int32_t f, uint32_t nb, int to_u16, int w) {
+  if (to_u16) return kFormU16;
+  if (f == kFormList && nb <= 1u && (w & 127) == 0) return kFormU1;
+  if (form_bits(f) < 2 && nb <= 3u && (w & 63) == 0) return kFormU2;
+  if (form_bits(f) < 4 && nb <= 15u) return kFormU4;
+  if (form_bits(f) < 8 && nb <= 255u) return kFormU8;
+  return kFormU16;
+}
+
+// A listed row is rewritten in place when its place holds the target form
+// (its kCap class), else it moves to a whole u16 slot at the arena's end
+// (mv[i]: its offset in kRowAlign units among the cnt[1] units the movers
+// take), where any later widening is in place -- places sized to the target
+// form instead left a row moving once per widening, and a 1B-pair stream
+// then held 151 GB against 102 GB (scripts/stream_compact_probe.py).  A
+// touched row on the zero row is always listed.
 __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int64_t* lo, const int64_t* hi,
                              const int32_t* hidx, const int64_t* off, uint32_t* cbound, int64_t n, int all_touched,
-                             int32_t* list, int32_t* mv, uint32_t* cnt) {
+                             int to_u16, int w, int64_t dw, int32_t* list, int32_t* mv, int8_t* tfa, uint32_t* cnt) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = hidx[r];
     if (f >= 0) continue;
-    const bool full = (off[r] & kRowFull) != 0;
-    if (f == kFormU16 && full) continue;
+    const int64_t o = off[r];
+    const int cc = (int)(o & kCapMask);
+    if (f == kFormU16 && cc == kCapU16) continue;  // a u16 row in a whole slot takes its adds in place
     bool need = true;
+    uint32_t nbv = cbound[r];
     if (bound) {
       const uint64_t b = bound[r], m = old_mass ? old_mass[r] : 0ULL;
       const bool has_keys = lo && hi[r] > lo[r];
       if (b <= m && !has_keys) continue;  // no update lands on this row
       const uint64_t nb = (uint64_t)cbound[r] + (b - m);
-      need = all_touched || nb > (uint64_t)form_cap(f) || !full;
-      cbound[r] = (uint32_t)min<uint64_t>(nb, 0xFFFFFFFFull);  // <= the capacity of the form it keeps or takes
+      need = all_touched || nb > (uint64_t)form_cap(f) || o == 0;
+      nbv = (uint32_t)min<uint64_t>(nb, 0xFFFFFFFFull);
+      cbound[r] = nbv;  // <= the capacity of the form it keeps or takes
     }
     if (need) {
+      const int32_t tf = widen_target(o == 0 ? kFormList : f, nbv, to_u16, w);
+      const int tc = form_class(tf);
       const uint32_t i = atomicAdd(cnt, 1u);
       list[i] = (int32_t)r;
-      mv[i] = full ? -1 : (int32_t)atomicAdd(cnt + 1, 1u);
+      tfa[i] = (int8_t)tf;
+      mv[i] = (o != 0 && cc >= tc) ? -1 : (int32_t)atomicAdd(cnt + 1, (uint32_t)(slot_units(dw) / kRowAlign));
     }
   }
-}
-
-__device__ __forceinline__ int form_bits(int32_t f) {  // counter bits of a form (0: a list row)
-  return f == kFormList ? 0 : f == kFormU1 ? 1 : f == kFormU2 ? 2 : f == kFormU4 ? 4 : f == kFormU8 ? 8 : 16;
 }
 
 // 16 counters v[0..16) packed at 32 / C bits into C-counter words at w32[j / C ...]
@@ -181,7 +204,8 @@ __device__ __forceinline__ void pack16(const uint32_t (&v)[16], uint32_t* w32, i
 }
 
 // One workgroup per listed row, rewritten (in place, or into a mover's new
-// slot at base + mv[i] * slot_units(dw)) in the narrowest form
+// slot at base + mv[i] * kRowAlign) in its target form tfa[i] (widen_target:
+// the narrowest form
 // wider than its own whose capacity holds its new bound (cbound), u16 for an
 // accumulate build (to_u16) -- a 2-bit row that one more pair lifts to 4
 // becomes a 4-bit row (half the bytes of u8, a quarter of u16).
@@ -192,9 +216,9 @@ __device__ __forceinline__ void pack16(const uint32_t (&v)[16], uint32_t* w32, i
 //  * list rows: every entry is read first (at most 32 per lane: d <= 32,
 //    m <= 256), then each sketch row is counted in LDS (u8 counters, four per
 //    word: a list row's counters are < 2^8) and leaves packed.
-__global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const int32_t* mv, const uint32_t* dcount,
-                                                    TableView tv, int64_t* off_w, int64_t base, int32_t* hidx,
-                                                    const uint32_t* cbound, int to_u16) {
+__global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const int32_t* mv, const int8_t* tfa,
+                                                    const uint32_t* dcount, TableView tv, int64_t* off_w, int64_t base,
+                                                    int32_t* hidx) {
   extern __shared__ uint32_t lc[];  // [w / 4] (list rows)
   const int64_t count = *dcount;
   const int64_t dw = tv.dw;
@@ -203,17 +227,10 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const i
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int64_t r = list[i];
     const int32_t f = hidx[r];
-    const uint32_t nb = cbound[r];
-    int32_t tf = kFormU16;
-    if (!to_u16) {
-      if (f == kFormList && nb <= 1u && (w & 127) == 0) tf = kFormU1;
-      else if (form_bits(f) < 2 && nb <= 3u && (w & 63) == 0) tf = kFormU2;
-      else if (form_bits(f) < 4 && nb <= 15u) tf = kFormU4;
-      else if (form_bits(f) < 8 && nb <= 255u) tf = kFormU8;
-    }
+    const int32_t tf = tfa[i];
     const int tb = form_bits(tf);
     const uint16_t* src = tv.row16(r);
-    const int64_t dst_off = mv[i] >= 0 ? base + (int64_t)mv[i] * slot_units(dw) : tv.base(r);
+    const int64_t dst_off = mv[i] >= 0 ? base + (int64_t)mv[i] * kRowAlign : tv.base(r);
     const uint8_t* p8 = reinterpret_cast<const uint8_t*>(src);
     uint32_t* w32 = reinterpret_cast<uint32_t*>(tv.t16 + dst_off);
     if (f == kFormList) {
@@ -286,7 +303,7 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const i
     }
     if (threadIdx.x == 0) {
       hidx[r] = tf;
-      if (mv[i] >= 0) off_w[r] = dst_off | kRowFull;
+      if (mv[i] >= 0) off_w[r] = dst_off | kCapU16;  // a mover's new place is a whole slot
     }
   }
 }
@@ -297,33 +314,34 @@ int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass,
   TimedScope ts(h, "widen_rows");
   const int64_t n = h->n;
   CMS_HIP(h->ws_plist.ensure(sizeof(int32_t) * (size_t)(n + 1)));
-  CMS_HIP(h->ws_layout.ensure(sizeof(int32_t) * (size_t)(n + 2)));
+  CMS_HIP(h->ws_layout.ensure(sizeof(int32_t) * (size_t)(n + 4) + (size_t)n));
   int32_t* list = h->ws_plist.as<int32_t>();
   int32_t* mv = h->ws_layout.as<int32_t>();
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(mv + n);  // [0] listed rows, [1] movers
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(mv + n);  // [0] listed rows, [1] the movers' kRowAlign units
+  int8_t* tfa = reinterpret_cast<int8_t*>(mv + n + 4);  // [n] target forms
   CMS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), h->stream));
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+  // u16 for an accumulate build or when no bound is known
+  const int to_u16 = (all_touched || !d_bound) ? 1 : 0;
   hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, d_lo, d_hi, h->d_hidx,
-                     h->d_off, h->d_cbound, n, all_touched ? 1 : 0, list, mv, cnt);
+                     h->d_off, h->d_cbound, n, all_touched ? 1 : 0, to_u16, h->p.width, h->dw, list, mv, tfa, cnt);
   CMS_HIP(hipGetLastError());
-  // movers get whole slots at the arena's end: their count sizes it (a
-  // handle without compact rows has none and skips the read-back)
+  // movers take whole slots at the arena's end: the units they need size it
+  // (a handle without compact rows has no movers and skips the read-back)
   int64_t base = h->t16_used;
   if (h->compact) {
     CMS_HIP(hipMemcpyAsync(h->h_pin + 8, cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
     CMS_HIP(hipStreamSynchronize(h->stream));
-    const int64_t movers = h->h_pin[8];
-    if (movers > 0) {
-      int rc = arena_reserve(h, h->t16_used + movers * slot_units(h->dw), true);
+    const int64_t units = (int64_t)h->h_pin[8] * kRowAlign;
+    if (units > 0) {
+      int rc = arena_reserve(h, h->t16_used + units, true);
       if (rc) return rc;
-      h->t16_used += movers * slot_units(h->dw);
+      h->t16_used += units;
     }
   }
-  // one workgroup per row, looping: the row count stays on the device; u16
-  // for an accumulate build or when no bound is known
+  // one workgroup per row, looping: the row count stays on the device
   hipLaunchKernelGGL(k_widen_rows, dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(256), (size_t)h->p.width,
-                     h->stream, list, mv, cnt, h->tview(), h->d_off, base, h->d_hidx, h->d_cbound,
-                     (all_touched || !d_bound) ? 1 : 0);
+                     h->stream, list, mv, tfa, cnt, h->tview(), h->d_off, base, h->d_hidx);
   CMS_HIP(hipGetLastError());
   return CMS_OK;
 }
@@ -438,7 +456,7 @@ int reset_table_layout(cms_handle* h) {
 
 __global__ void k_off_identity(int64_t* off, int64_t n, int64_t su) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
-    off[r] = (su + r * su) | kRowFull;
+    off[r] = (su + r * su) | kCapU16;
 }
 
 // Virtual arena: physical chunks mapped at the end of the reserved range.
@@ -607,12 +625,11 @@ int reset_rows_zero(cms_handle* h) {
 
 // off[r] from the rows' capacities (128-B units): the rows follow the zero
 // row in row order; a row of capacity 0 (a hot row) points at the zero row
-__global__ void k_row_offsets(const uint32_t* caps, const uint32_t* ex, int64_t n, int64_t su, int64_t* off,
+__global__ void k_row_offsets(const uint32_t* caps, const uint32_t* ex, int64_t n, int64_t su, int64_t dw, int64_t* off,
                               uint32_t* total) {
-  const int64_t full_units = su / kRowAlign;
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t c = caps[r];
-    off[r] = c ? (su + (int64_t)ex[r] * kRowAlign) | (c == full_units ? kRowFull : 0) : 0;
+    off[r] = c ? (su + (int64_t)ex[r] * kRowAlign) | class_of_units((int64_t)c * kRowAlign, dw) : 0;
     if (r == n - 1) *total = ex[r] + c;
   }
 }
@@ -626,7 +643,7 @@ int row_layout(cms_handle* h, const uint32_t* d_caps, uint32_t* d_scratch) {
   int rc = scan_exclusive_u32(h, d_caps, ex, n, bsum);
   if (rc) return rc;
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
-  hipLaunchKernelGGL(k_row_offsets, dim3(g), dim3(256), 0, h->stream, d_caps, ex, n, su, h->d_off, total);
+  hipLaunchKernelGGL(k_row_offsets, dim3(g), dim3(256), 0, h->stream, d_caps, ex, n, su, h->dw, h->d_off, total);
   CMS_HIP(hipGetLastError());
   CMS_HIP(hipMemcpyAsync(h->h_pin + 8, total, sizeof(uint32_t), hipMemcpyDeviceToHost, h->stream));
   CMS_HIP(hipStreamSynchronize(h->stream));
