@@ -879,6 +879,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
     bsize = int(args.stream_batch)
     nbatch = (total + bsize - 1) // bsize
     ingest_s, local, worst, worst_b = 0.0, 0, 0.0, -1
+    lat = []
     for b in range(nbatch):
         it_, us = batch(555_000 + b, min(bsize, total - b * bsize))
         bar()
@@ -887,6 +888,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         bar()
         dt = max_over_ranks(time.perf_counter() - t0)
         ingest_s += dt
+        lat.append(dt)
         if dt > worst:
             worst, worst_b = dt, b
         local += int(it_.numel())
@@ -907,6 +909,11 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
         "x_realtime": (total / ingest_s) / 10e6,  # the stream arrives at 10M pairs/s
         "batch_latency_ms": ingest_s * 1e3 / nbatch, "batch_latency_max_ms": worst * 1e3, "slowest_batch": worst_b,
         "widen_ms": t.timing("widen_rows")[0], "arena_map_ms": t.timing("arena_map"),
+        "arena_map_parts_ms": {k: t.timing("arena_map_" + k)[0] for k in ("create", "map", "access")},
+        # the first batches move the touched compact rows to slots of their
+        # own, mapping arena memory (host time in arena_map_ms, box-dependent);
+        # the rate over the later batches is the table's steady state
+        "steady_updates_per_s": (bsize * len(lat[10:]) / sum(lat[10:])) if len(lat) > 10 else None,
         "path": f"{kern} (batches of >= 32768 pairs into a live table are grouped by owner first and take "
                 "k_ingest_sorted: exact u32 global atomics, norm / row-max / mass deltas reduced per owner inside the "
                 "wave; smaller batches take k_ingest_atomic)",
@@ -999,6 +1006,7 @@ def streaming_refresh(t, args, n, k, rank, world, device, bar, max_over_ranks):
                     f"finalize + incremental top-{k} refresh of every item (cms_top_k_refresh)",
         "sustained": sustained,
         "sustained_updates_per_s": sustained["sustained_updates_per_s"],
+        "steady_updates_per_s": sustained["steady_updates_per_s"],
         "path": sustained["path"],
         "roofline": sustained["roofline"],
         "refresh_batches": nb, "pairs_per_batch_per_gpu": per_batch,
@@ -1410,6 +1418,7 @@ def summary(res):
         st = cos.get("config5_streaming") or {}
         if st:
             out.update({"cfg5_sustained_updates_per_s": _r(st.get("sustained_updates_per_s")),
+                        "cfg5_steady_updates_per_s": _r(st.get("steady_updates_per_s")),
                         "cfg5_refresh_latency_s": _r(st.get("refresh_latency_s")),
                         "cfg5_refresh_pair_rate_vs_whole_job": _r(st.get("refresh_pair_rate_vs_whole_job"), 3),
                         "cfg5_refresh_class_weighted_rate": _r(st.get("refresh_class_weighted_rate_vs_whole_job"), 3),

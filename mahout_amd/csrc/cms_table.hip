@@ -471,6 +471,7 @@ static int arena_map(cms_handle* h, size_t want) {
   if (h->arena_mapped + bytes < want) return set_error(CMS_E_OOM, "row arena: %.2f GB exceeds its reserved range", 1e-9 * want);
   hipMemGenericAllocationHandle_t mem;
   hipError_t e = hipMemCreate(&mem, bytes, &prop, 0);
+  const auto t1 = std::chrono::steady_clock::now();
   if (e != hipSuccess) {
     (void)hipGetLastError();
     return set_error(CMS_E_OOM, "row arena chunk of %.2f GB: %s", 1e-9 * bytes, hipGetErrorString(e));
@@ -482,7 +483,8 @@ static int arena_map(cms_handle* h, size_t want) {
   // (access is set over the whole mapped range from the reservation's start:
   // on this ROCm a sub-range starting inside it is refused once other
   // allocations exist -- scripts/vmm_probe.cpp)
-  if ((e = hipMemMap(at, bytes, 0, mem, 0)) != hipSuccess ||
+  std::chrono::steady_clock::time_point t2;
+  if ((e = hipMemMap(at, bytes, 0, mem, 0)) != hipSuccess || (t2 = std::chrono::steady_clock::now(), false) ||
       (e = hipMemSetAccess(h->arena_va, h->arena_mapped + bytes, &acc, 1)) != hipSuccess) {
     (void)hipMemUnmap(at, bytes);
     (void)hipMemRelease(mem);
@@ -491,10 +493,18 @@ static int arena_map(cms_handle* h, size_t want) {
   }
   h->arena_chunks.push_back({mem, bytes});
   h->arena_mapped += bytes;
-  if (h->timing) {  // host time of the mapping (cms_get_timing "arena_map")
-    auto& acc = h->timing_acc["arena_map"];
-    acc.total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    acc.launches += 1;
+  if (h->timing) {  // host time of the mapping (cms_get_timing "arena_map"; its create / map / access parts)
+    const auto t3 = std::chrono::steady_clock::now();
+    auto add = [h](const char* name, double ms) {
+      auto& a = h->timing_acc[name];
+      a.total_ms += ms;
+      a.launches += 1;
+    };
+    using ms = std::chrono::duration<double, std::milli>;
+    add("arena_map", ms(t3 - t0).count());
+    add("arena_map_create", ms(t1 - t0).count());
+    add("arena_map_map", ms(t2 - t1).count());
+    add("arena_map_access", ms(t3 - t2).count());
   }
   return CMS_OK;
 }
