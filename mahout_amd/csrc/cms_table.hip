@@ -144,6 +144,10 @@ __device__ __forceinline__ int form_bits(int32_t f) {  // counter bits of a form
 // own whose capacity holds its new bound nb (u16 for an accumulate build) --
 // a 2-bit row that one more pair lifts to 4 becomes a 4-bit row.  The zero
 // row counts as a list row (it holds nothing of its own).
+// the smallest place a moved row takes (kCap class; kCapU16: a whole slot)
+#ifndef CMS_MOVE_CLASS
+#define CMS_MOVE_CLASS 5
+#endif
 __device__ __forceinline__ int32_t widen_target(int32_t f, uint32_t nb, int to_u16, int w) {
   if (to_u16) return kFormU16;
   if (f == kFormList && nb <= 1u && (w & 127) == 0) return kFormU1;
@@ -186,7 +190,8 @@ __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, co
       const uint32_t i = atomicAdd(cnt, 1u);
       list[i] = (int32_t)r;
       tfa[i] = (int8_t)tf;
-      mv[i] = (o != 0 && cc >= tc) ? -1 : (int32_t)atomicAdd(cnt + 1, (uint32_t)(slot_units(dw) / kRowAlign));
+      const int mc = tc >= CMS_MOVE_CLASS ? kCapU16 : CMS_MOVE_CLASS;  // the class of a mover's new place
+      mv[i] = (o != 0 && cc >= tc) ? -1 : (int32_t)atomicAdd(cnt + 1, (uint32_t)(class_units(mc, dw) / kRowAlign));
     }
   }
 }
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(256) void k_widen_rows(const int32_t* list, const i
     }
     if (threadIdx.x == 0) {
       hidx[r] = tf;
-      if (mv[i] >= 0) off_w[r] = dst_off | kCapU16;  // a mover's new place is a whole slot
+      if (mv[i] >= 0) off_w[r] = dst_off | (form_class(tf) >= CMS_MOVE_CLASS ? kCapU16 : CMS_MOVE_CLASS);  // (k_widen_mark)
     }
   }
 }

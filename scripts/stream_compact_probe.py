@@ -43,4 +43,5 @@ slow = sorted(range(nb), key=lambda i: -lat[i])[:3]
 print(json.dumps({"batches": nb, "hold_gb": hold_gb, "slowest": [(i, round(lat[i], 2)) for i in slow], "total_ms": sum(lat), "mean_ms": sum(lat) / nb, "max_ms": max(lat),
                   "first5": [round(x, 2) for x in lat[:5]], "median_ms": sorted(lat)[nb // 2],
                   "scopes_ms": scopes, "table_bytes": st["table_bytes"],
+                  "forms": {k: st[k] for k in ("hot_rows", "u8_rows", "nibble_rows", "crumb_rows", "bit_rows", "list_rows")},
                   "used_gb_after_build": (mem0[1] - mem0[0]) / 1e9, "used_gb_after_stream": (mem1[1] - mem1[0]) / 1e9}))
