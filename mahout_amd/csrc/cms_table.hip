@@ -144,9 +144,17 @@ __device__ __forceinline__ int form_bits(int32_t f) {  // counter bits of a form
 // own whose capacity holds its new bound nb (u16 for an accumulate build) --
 // a 2-bit row that one more pair lifts to 4 becomes a 4-bit row.  The zero
 // row counts as a list row (it holds nothing of its own).
-// the smallest place a moved row takes (kCap class; kCapU16: a whole slot)
+// the smallest place a moved row takes (kCap class): a mover whose target
+// form fits a u8 row takes a u8 place, one past it a whole slot.  With the
+// rows' bounds from their tracked maxima most rows never pass u8: after the
+// 1B-pair config-5 stream 78.7 GB in use against 102 GB with whole slots
+// for every mover (scripts/stream_compact_probe.py)
 #ifndef CMS_MOVE_CLASS
-#define CMS_MOVE_CLASS 5
+#define CMS_MOVE_CLASS 4
+#endif
+// widening bounds from the tracked row maxima (0: the accumulated cbound alone)
+#ifndef CMS_WIDEN_ROWMAX
+#define CMS_WIDEN_ROWMAX 1
 #endif
 __device__ __forceinline__ int32_t widen_target(int32_t f, uint32_t nb, int to_u16, int w) {
   if (to_u16) return kFormU16;
@@ -158,15 +166,15 @@ __device__ __forceinline__ int32_t widen_target(int32_t f, uint32_t nb, int to_u
 }
 
 // A listed row is rewritten in place when its place holds the target form
-// (its kCap class), else it moves to a whole u16 slot at the arena's end
-// (mv[i]: its offset in kRowAlign units among the cnt[1] units the movers
-// take), where any later widening is in place -- places sized to the target
-// form instead left a row moving once per widening, and a 1B-pair stream
-// then held 151 GB against 102 GB (scripts/stream_compact_probe.py).  A
+// (its kCap class), else it moves to a place of class CMS_MOVE_CLASS (or a
+// whole slot) at the arena's end (mv[i]: its offset in kRowAlign units among
+// the cnt[1] units the movers take) -- places sized to each target form left
+// a row moving once per widening (a 1B-pair stream then held 151 GB).  A
 // touched row on the zero row is always listed.
 __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, const int64_t* lo, const int64_t* hi,
-                             const int32_t* hidx, const int64_t* off, uint32_t* cbound, int64_t n, int all_touched,
-                             int to_u16, int w, int64_t dw, int32_t* list, int32_t* mv, int8_t* tfa, uint32_t* cnt) {
+                             const int32_t* hidx, const int64_t* off, uint32_t* cbound, const uint32_t* rowmax,
+                             int64_t n, int all_touched, int to_u16, int w, int64_t dw, int32_t* list, int32_t* mv,
+                             int8_t* tfa, uint32_t* cnt) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = hidx[r];
     if (f >= 0) continue;
@@ -179,7 +187,10 @@ __global__ void k_widen_mark(const uint64_t* bound, const uint64_t* old_mass, co
       const uint64_t b = bound[r], m = old_mass ? old_mass[r] : 0ULL;
       const bool has_keys = lo && hi[r] > lo[r];
       if (b <= m && !has_keys) continue;  // no update lands on this row
-      const uint64_t nb = (uint64_t)cbound[r] + (b - m);
+      // the row's current largest counter (rowmax, exact while the norms
+      // are tracked) bounds it more tightly than the accumulated cbound
+      const uint64_t cur = rowmax ? min<uint64_t>(cbound[r], rowmax[r]) : (uint64_t)cbound[r];
+      const uint64_t nb = cur + (b - m);
       need = all_touched || nb > (uint64_t)form_cap(f) || o == 0;
       nbv = (uint32_t)min<uint64_t>(nb, 0xFFFFFFFFull);
       cbound[r] = nbv;  // <= the capacity of the form it keeps or takes
@@ -328,8 +339,11 @@ int widen_rows(cms_handle* h, const uint64_t* d_bound, const uint64_t* old_mass,
   const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
   // u16 for an accumulate build or when no bound is known
   const int to_u16 = (all_touched || !d_bound) ? 1 : 0;
+  // (the row maxima are current when the norms are: every writer tracks them then)
+  const uint32_t* rmax = h->norms_valid && CMS_WIDEN_ROWMAX ? h->d_rowmax : nullptr;
   hipLaunchKernelGGL(k_widen_mark, dim3(g), dim3(256), 0, h->stream, d_bound, old_mass, d_lo, d_hi, h->d_hidx,
-                     h->d_off, h->d_cbound, n, all_touched ? 1 : 0, to_u16, h->p.width, h->dw, list, mv, tfa, cnt);
+                     h->d_off, h->d_cbound, rmax, n, all_touched ? 1 : 0, to_u16, h->p.width, h->dw, list, mv, tfa,
+                     cnt);
   CMS_HIP(hipGetLastError());
   // movers take whole slots at the arena's end: the units they need size it
   // (a handle without compact rows has no movers and skips the read-back)
