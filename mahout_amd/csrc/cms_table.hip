@@ -565,8 +565,10 @@ int arena_reserve(cms_handle* h, int64_t need, bool keep) {
     if (want > h->arena_mapped) {
       const bool first = h->arena_mapped == 0;
       // a growing table (rows moving to slots) maps a quarter more than it needs
-      const size_t ask = keep ? std::min(h->arena_va_bytes, want + want / 4) : want;
-      if (int rc = arena_map(h, std::max(ask, want))) return rc;
+      const size_t ask = std::max(keep ? std::min(h->arena_va_bytes, want + want / 4) : want, want);
+      int rc = arena_map(h, ask);
+      if (rc && ask > want) rc = arena_map(h, want);  // (short of memory: without the headroom)
+      if (rc) return rc;
       if (first) CMS_HIP(hipMemsetAsync(h->arena_va, 0, sizeof(uint16_t) * (size_t)su, h->stream));  // the zero row
     }
     h->t16_cap = (int64_t)(h->arena_mapped / sizeof(uint16_t));
