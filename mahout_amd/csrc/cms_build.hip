@@ -586,6 +586,11 @@ constexpr int kMidListKeys = CMS_MID_LIST_KEYS;
 #ifndef CMS_MID_ROW_KEYS
 #define CMS_MID_ROW_KEYS 4
 #endif
+// byte-class list owners of <= 64 keys clear the words they added into after
+// each sketch row instead of zeroing the wave's whole 4-bit row
+#ifndef CMS_NIB_CLEAR1
+#define CMS_NIB_CLEAR1 0
+#endif
 // byte-class list owners take their LDS adds back after each sketch row
 // instead of zeroing the wave's 4-bit row before the next one
 #ifndef CMS_NIB_UNADD
@@ -1444,8 +1449,12 @@ __device__ __forceinline__ void nib_owner(
     // a list row's counts leave nothing behind: its adds are taken back after
     // each sketch row (CMS_NIB_UNADD), so only the first row zeroes the slot
     const bool unadd = CMS_NIB_UNADD && as_list;
+    // a list owner of <= 64 keys (one per lane) clears the words its adds
+    // touched instead of zeroing the whole 4-bit row before the next sketch row
+    const bool clear1 = CMS_NIB_CLEAR1 && as_list && m <= 64;
+    uint32_t c0 = 0;
     for (int d = 0; d < hp.depth; ++d) {
-      if (!unadd || d == 0)
+      if ((!unadd && !clear1) || d == 0)
         for (int j = lane; j < nq; j += 64) slot4[j] = make_uint4(0, 0, 0, 0);
       uint32_t sq = 0;
 #pragma unroll
@@ -1454,6 +1463,7 @@ __device__ __forceinline__ void nib_owner(
           const uint32_t c = (D > 0 && k == 0)
                                  ? (d == 0 ? b0 : d == 1 ? b1 : d == 2 ? b2 : d == 3 ? b3 : b4)
                                  : bucket(hp, d, kp[k]);
+          if (k == 0) c0 = c;
           const uint32_t sh = (c & ((1u << lg) - 1u)) * (uint32_t)bits;
           const uint32_t old = (atomicAdd(&slot[c >> lg], ik[k] << sh) >> sh) & cap;
           const uint32_t nv = old + ik[k];
@@ -1463,6 +1473,10 @@ __device__ __forceinline__ void nib_owner(
           if (as_list) lst[1 + (int64_t)d * m + lane + 64 * k] = (uint16_t)c;
         }
       if (__ballot(ovf)) break;  // uniform: escalate (the slot is zeroed by the next owner's first row)
+      // every nonzero nibble sits in a word some lane added into: those words
+      // back to zero (after all the row's adds: one wave's LDS operations
+      // execute in program order)
+      if (clear1 && ik[0]) slot[c0 >> lg] = 0u;
       if (unadd) {  // no counter carried (checked above), so each subtraction only removes its own add
 #pragma unroll
         for (int k = 0; k < kKeyRegs; ++k)
