@@ -319,6 +319,7 @@ struct cms_handle {
   };
   void* arena_va = nullptr;
   size_t arena_va_bytes = 0, arena_mapped = 0, arena_gran = 0;
+  int arena_small_layouts = 0;  // consecutive layouts that wanted under a quarter of the arena (arena_reserve)
   std::vector<ArenaChunk> arena_chunks;
   bool compact = false;             // forms_ok: fresh builds lay the rows out compactly (row_layout)
   bool f64 = false;                 // CMS_COUNTER_F64: fp64 counters in d_t64 (cms_f64.hip), no u16/u32 table

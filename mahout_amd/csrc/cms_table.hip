@@ -556,9 +556,21 @@ void arena_release(cms_handle* h) {
 int arena_reserve(cms_handle* h, int64_t need, bool keep) {
   const int64_t su = slot_units(h->dw);
   need = std::max(need, su);
+  // A re-laid-out table gives back what it no longer needs -- once three
+  // layouts in a row wanted under a quarter of the arena: a multi-rank step
+  // alternates a small local build with the larger merged layout, and
+  // unmapping and mapping that difference every step would cost more than
+  // it frees.
+  bool shrink = false;
+  if (!keep) {
+    const int64_t have = h->arena_va ? (int64_t)(h->arena_mapped / sizeof(uint16_t)) : h->t16_cap;
+    h->arena_small_layouts = have > 4 * need + (int64_t)(h->arena_gran / sizeof(uint16_t)) ? h->arena_small_layouts + 1 : 0;
+    shrink = h->arena_small_layouts >= 3;
+    if (shrink) h->arena_small_layouts = 0;
+  }
   if (h->arena_va) {
     const size_t want = sizeof(uint16_t) * (size_t)need;
-    if (!keep && h->arena_mapped > 4 * want + h->arena_gran) {  // a re-laid-out table gives back what it no longer needs
+    if (shrink) {
       CMS_HIP(hipDeviceSynchronize());
       arena_unmap_above(h, want);
     }
@@ -574,7 +586,7 @@ int arena_reserve(cms_handle* h, int64_t need, bool keep) {
     h->t16_cap = (int64_t)(h->arena_mapped / sizeof(uint16_t));
     return CMS_OK;
   }
-  if (!keep && h->t16_cap > 4 * need) {  // a re-laid-out table shrinks back (its rows are dead)
+  if (shrink) {  // (its rows are dead: a smaller arena)
     CMS_HIP(hipFree(h->d_t16));
     h->d_t16 = nullptr;
     h->t16_cap = 0;
