@@ -106,11 +106,12 @@ def test_compact_layout_equals_slots_through_every_writer(oracle, monkeypatch):
     assert same(stages[True][3][0][sel].cpu().numpy().astype(np.float64), exp)
 
 
-def test_compact_merge_forms_equal_oracle(oracle):
+def test_compact_merge_forms_equal_oracle(oracle, monkeypatch):
     """The one-rank packed merge of a compact table: rows re-laid out by their
     merged widths (u8 and 4-bit forms, the zero row for owners without keys)
     read back as the oracle's table, with the oracle's similarities."""
     from mahout_amd import SketchTable
+    monkeypatch.setenv("CMS_NO_COMPACT", "0")
     n, d, w = 3000, 4, 1024
     items, users = zipf_stream(500_000, n - 200, 600_000, seed=23)  # the last 200 owners stay empty
     a, b = oracle.hash_params(7, d)
@@ -138,6 +139,7 @@ def test_compact_arena_regrows_and_shrinks(oracle, monkeypatch, vmm):
     bit-exact against the oracle's rebuild."""
     from mahout_amd import SketchTable
     monkeypatch.setenv("CMS_NO_VMM", "0" if vmm else "1")
+    monkeypatch.setenv("CMS_NO_COMPACT", "0")
     n, d, w = 30000, 5, 4096
     a, b = oracle.hash_params(11, d)
     big_i, big_u = zipf_stream(1_000_000, n, 3_000_000, seed=31)
